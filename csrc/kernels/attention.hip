@@ -1,0 +1,364 @@
+// Paged attention for gfx950: decode (split-K / flash-decoding) and varlen
+// causal prefill (chunked-prefill capable: queries attend to the paged cache).
+//
+// KV cache layout (per layer): [num_blocks][Hkv][BS=16][D=128] bf16.
+//
+// Both kernels use the "swapped" product S^T = K . Q^T on v_mfma_f32_16x16x32_bf16:
+//   A = K tile (lane: K[tok l&15][d 8(l>>4)+j]  -> a plain 16-B row load),
+//   B = Q^T   (lane: Q[col l&15][d 8(l>>4)+j]   -> a plain 16-B row load),
+//   C = S^T   (lane: S[col l&15][tok 4(l>>4)+i]) -> every softmax statistic of a
+//               query column lives in ONE lane group: the row max/sum need only
+//               two xor-shuffles (16, 32) and the O rescale is lane-local.
+// Then O^T = V^T . P^T:
+//   B = P^T: built in-register from two S^T tiles with the k-order permuted to
+//            {4g..4g+3, 16+4g..16+4g+3} (g = l>>4),
+//   A = V^T: read from an LDS image of the V chunk with ds_read_b64_tr_b16, whose
+//            4-row x 16-col transposed gather delivers exactly that k-order.
+// The LDS image of V is XOR-swizzled on 8-B chunks (chunk ^= 4*(row&7)), which
+// makes the transposed reads conflict-free (cdna_hip_programming.md T10).
+#include "common.h"
+#include "launchers.h"
+
+namespace vgate {
+
+constexpr int D_ = 128;
+constexpr int BS_ = 16;
+constexpr int CHUNK = 32;
+constexpr float LOG2E = 1.4426950408889634f;
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+__device__ __forceinline__ int v_lds_off(int r, int c) {  // element offset, c % 4 == 0
+  return r * D_ + ((((c >> 2) ^ ((r & 7) << 2))) << 2);
+}
+
+// Stage a 32-token V chunk into the swizzled LDS image. `valid` = tokens < valid are real.
+// Instruction i: lane reads 16 B at element (4i + l>>4, 8(l&15)) -> 1 KiB coalesced.
+__device__ __forceinline__ void load_v_regs(uint4 (&vr)[8], const bf16_t* vb0, const bf16_t* vb1,
+                                            int lane) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = 4 * i + (lane >> 4);
+    const int c = 8 * (lane & 15);
+    const bf16_t* src = (r < 16 ? vb0 + r * D_ : vb1 + (r - 16) * D_) + c;
+    vr[i] = *reinterpret_cast<const uint4*>(src);
+  }
+}
+
+__device__ __forceinline__ void store_v_lds(bf16_t* lds, const uint4 (&vr)[8], int lane, int valid) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = 4 * i + (lane >> 4);
+    const int c = 8 * (lane & 15);
+    const uint4 v = r < valid ? vr[i] : make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint4*>(lds + v_lds_off(r, c)) = v;
+  }
+}
+
+// O^T[16mt + ..][col] += V^T(chunk) . P^T ; pb = P^T fragment (bf16x8)
+__device__ __forceinline__ void pv_update(f32x4 (&o)[8], const bf16_t* lds, const bf16x8& pb,
+                                          int lane) {
+  const int g = lane >> 4;
+  const int q = (lane >> 2) & 3;
+  const int p = lane & 3;
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) {
+    const int c = 16 * mt + 4 * p;
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+        (lds_bf16x4*)(lds + v_lds_off(4 * g + q, c)));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+        (lds_bf16x4*)(lds + v_lds_off(16 + 4 * g + q, c)));
+    bf16x8 a;
+    a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
+    a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
+    o[mt] = mfma16(a, pb, o[mt]);
+  }
+}
+
+__device__ __forceinline__ bf16x8 pack_p(const f32x4& s0, const f32x4& s1) {
+  bf16x8 b;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    b[i] = (__bf16)s0[i];
+    b[4 + i] = (__bf16)s1[i];
+  }
+  return b;
+}
+
+// S^T tile for 16 tokens starting at kbase (row-major [16][D] in cache)
+__device__ __forceinline__ f32x4 qk_tile(const bf16_t* kbase, const uint4 (&qf)[4], int lane) {
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const bf16_t* kp = kbase + (lane & 15) * D_ + 8 * (lane >> 4);
+  uint4 kf[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) kf[kk] = *reinterpret_cast<const uint4*>(kp + 32 * kk);
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) acc = mfma16(as_bf16x8(kf[kk]), as_bf16x8(qf[kk]), acc);
+  return acc;
+}
+
+// Online-softmax step over one 32-token chunk for the lane's query column.
+// tok_lo: absolute token index of chunk row 0; lim: tokens >= lim are masked for this column.
+__device__ __forceinline__ bf16x8 softmax_step(f32x4& s0, f32x4& s1, float& m, float& l,
+                                               f32x4 (&o)[8], int tok_lo, int lim, float cscale,
+                                               int lane) {
+  const int g = lane >> 4;
+  float cmax = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int t0 = tok_lo + 4 * g + i, t1 = tok_lo + 16 + 4 * g + i;
+    s0[i] = t0 < lim ? s0[i] * cscale : -INFINITY;
+    s1[i] = t1 < lim ? s1[i] * cscale : -INFINITY;
+    cmax = fmaxf(cmax, fmaxf(s0[i], s1[i]));
+  }
+  cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+  cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+  const float mn = fmaxf(m, cmax);
+  const bool dead = (mn == -INFINITY);
+  const float alpha = dead ? 1.f : exp2f(m - mn);
+  float ps = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    s0[i] = dead ? 0.f : exp2f(s0[i] - mn);
+    s1[i] = dead ? 0.f : exp2f(s1[i] - mn);
+    ps += s0[i] + s1[i];
+  }
+  l = l * alpha + ps;
+  m = mn;
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) o[mt] *= alpha;
+  return pack_p(s0, s1);
+}
+
+// ---------------------------------------------------------------- decode ----
+// grid (S, Hkv, P); block 256 = 4 waves; wave w takes chunks w, w+4, ... of the
+// partition. Query columns = the G = Hq/Hkv heads sharing this KV head.
+__global__ __launch_bounds__(256) void attn_decode_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int s = blockIdx.x, h = blockIdx.y, part = blockIdx.z;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int ctx = a.context_lens[s];
+  const int pstart = part * a.part_size;
+  if (ctx <= 0 || pstart >= ctx) return;
+  // with query_start, only single-query sequences are decode work (prefill tiles cover the rest)
+  if (a.query_start && a.query_start[s + 1] - a.query_start[s] != 1) return;
+  const int pend = min(ctx, pstart + a.part_size);
+  const int nparts = (ctx + a.part_size - 1) / a.part_size;
+  const int G = a.Hq / a.Hkv;
+  const int col = lane & 15;
+  const int qtok = a.query_start ? a.query_start[s + 1] - 1 : s;
+
+  uint4 qf[4];
+  {
+    const bool ok = col < G;
+    const bf16_t* qp = a.q + (size_t)qtok * a.q_stride + (size_t)(h * G + (ok ? col : 0)) * D_ +
+                       8 * (lane >> 4);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+      qf[kk] = ok ? *reinterpret_cast<const uint4*>(qp + 32 * kk) : make_uint4(0, 0, 0, 0);
+  }
+  const float cscale = a.scale * LOG2E;
+  float m = -INFINITY, l = 0.f;
+  f32x4 o[8];
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16_t* vl = reinterpret_cast<bf16_t*>(smem) + wid * (CHUNK * D_);
+  const int* bt = a.block_tables + (size_t)s * a.max_blocks;
+  const size_t head_off = (size_t)h * BS_ * D_;
+  const size_t blk_stride = (size_t)a.Hkv * BS_ * D_;
+  const int nch = (pend - pstart + CHUNK - 1) / CHUNK;
+
+  for (int c = wid; c < nch; c += 4) {
+    const int tb = pstart + c * CHUNK;
+    const int b0 = bt[tb / BS_];
+    const int b1 = (tb + BS_ < pend) ? bt[tb / BS_ + 1] : b0;
+    const bf16_t* kb0 = a.k_cache + (size_t)b0 * blk_stride + head_off;
+    const bf16_t* kb1 = a.k_cache + (size_t)b1 * blk_stride + head_off;
+    const bf16_t* vb0 = a.v_cache + (size_t)b0 * blk_stride + head_off;
+    const bf16_t* vb1 = a.v_cache + (size_t)b1 * blk_stride + head_off;
+    uint4 vr[8];
+    load_v_regs(vr, vb0, vb1, lane);
+    f32x4 s0 = qk_tile(kb0, qf, lane);
+    f32x4 s1 = qk_tile(kb1, qf, lane);
+    const bf16x8 pb = softmax_step(s0, s1, m, l, o, tb, pend, cscale, lane);
+    store_v_lds(vl, vr, lane, pend - tb);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pv_update(o, vl, pb, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+
+  // ---- merge the 4 waves: scratch reuses the V images ----
+  __syncthreads();
+  float* sm_m = reinterpret_cast<float*>(smem);    // [4][16]
+  float* sm_l = sm_m + 64;                         // [4][16]
+  float* sm_o = sm_l + 64;                         // [4][128][16]
+  if (lane < 16) {
+    sm_m[wid * 16 + lane] = m;
+    sm_l[wid * 16 + lane] = l;
+  }
+  {
+    const int g = lane >> 4;
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sm_o[(wid * D_ + 16 * mt + 4 * g + i) * 16 + col] = o[mt][i];
+  }
+  __syncthreads();
+  // thread -> (col, d-range): G*128 outputs, 256 threads
+  for (int idx = threadIdx.x; idx < G * (D_ / 4); idx += blockDim.x) {
+    const int cc = idx / (D_ / 4);
+    const int d0 = (idx % (D_ / 4)) * 4;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm_m[w * 16 + cc]);
+    float L = 0.f, acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float mw = sm_m[w * 16 + cc];
+      const float f = (mw == -INFINITY) ? 0.f : exp2f(mw - M);
+      L += sm_l[w * 16 + cc] * f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += sm_o[(w * D_ + d0 + j) * 16 + cc] * f;
+    }
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+    const int hq = h * G + cc;
+    if (nparts == 1) {
+      bf16_t* op = a.out + (size_t)qtok * a.out_stride + (size_t)hq * D_ + d0;
+      uint2 pk;
+      pk.x = pack_bf2(acc[0] * inv, acc[1] * inv);
+      pk.y = pack_bf2(acc[2] * inv, acc[3] * inv);
+      *reinterpret_cast<uint2*>(op) = pk;
+    } else {
+      float* po = a.part_o + (((size_t)s * a.Hq + hq) * a.num_parts + part) * D_ + d0;
+      *reinterpret_cast<float4*>(po) = make_float4(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
+      if (d0 == 0) {
+        float* pm = a.part_ml + (((size_t)s * a.Hq + hq) * a.num_parts + part) * 2;
+        pm[0] = M;
+        pm[1] = L;
+      }
+    }
+  }
+}
+
+// Combine split-K partitions: grid (S, Hq), block 128 (one thread per d).
+__global__ __launch_bounds__(128) void attn_decode_reduce_kernel(AttnArgs a) {
+  const int s = blockIdx.x, hq = blockIdx.y, d = threadIdx.x;
+  const int ctx = a.context_lens[s];
+  if (ctx <= 0) return;
+  if (a.query_start && a.query_start[s + 1] - a.query_start[s] != 1) return;
+  const int nparts = (ctx + a.part_size - 1) / a.part_size;
+  if (nparts <= 1) return;
+  const float* pm = a.part_ml + ((size_t)s * a.Hq + hq) * a.num_parts * 2;
+  const float* po = a.part_o + ((size_t)s * a.Hq + hq) * a.num_parts * D_;
+  float M = -INFINITY;
+  for (int p = 0; p < nparts; ++p) M = fmaxf(M, pm[2 * p]);
+  float L = 0.f, acc = 0.f;
+  for (int p = 0; p < nparts; ++p) {
+    const float w = pm[2 * p + 1] * exp2f(pm[2 * p] - M);
+    L += w;
+    acc += w * po[p * D_ + d];
+  }
+  const int qtok = a.query_start ? a.query_start[s + 1] - 1 : s;
+  a.out[(size_t)qtok * a.out_stride + (size_t)hq * D_ + d] = f2bf(L > 0.f ? acc / L : 0.f);
+}
+
+void launch_attn_decode(const AttnArgs& a, hipStream_t st) {
+  if (a.S <= 0) return;
+  dim3 grid(a.S, a.Hkv, a.num_parts);
+  // 4 per-wave V images (32 KiB) reused as merge scratch: m,l [2][4][16] + O [4][128][16] f32
+  constexpr size_t kVImg = 4 * CHUNK * D_ * 2;
+  constexpr size_t kMerge = (128 + 4 * D_ * 16) * 4;
+  const size_t lds = kVImg > kMerge ? kVImg : kMerge;
+  hipLaunchKernelGGL(attn_decode_kernel, grid, dim3(256), lds, st, a);
+  if (a.num_parts > 1) hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(a.S, a.Hq), dim3(128), 0, st, a);
+}
+
+// --------------------------------------------------------------- prefill ----
+// grid (num_tiles, Hkv); block = 64*G threads (one wave per query head of the
+// group); every wave walks the same KV chunks, V is staged once per block into
+// a double-buffered LDS image (one barrier per chunk). Query columns = 16
+// consecutive query tokens of the wave's head.
+__global__ __launch_bounds__(1024) void attn_prefill_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t vls[2][CHUNK * D_];
+  const int tile = blockIdx.x, h = blockIdx.y;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nthr = blockDim.x;
+  const int s = a.tile_seq[tile];
+  if (s < 0) return;  // padding tile of a graph bucket
+  const int q0 = a.tile_q0[tile];
+  const int qs = a.query_start[s];
+  const int qlen = a.query_start[s + 1] - qs;
+  const int ctx = a.context_lens[s];
+  const int G = a.Hq / a.Hkv;
+  const int hq = h * G + wid;
+  const int col = lane & 15;
+  const int qi = q0 + col;
+  const bool qok = qi < qlen;
+  const int qpos = ctx - qlen + qi;  // absolute position of this column's query
+  const int lim = qok ? qpos + 1 : 0;
+  const int kv_end = min(ctx, ctx - qlen + min(q0 + 16, qlen));
+
+  uint4 qf[4];
+  {
+    const bf16_t* qp = a.q + (size_t)(qs + (qok ? qi : 0)) * a.q_stride + (size_t)hq * D_ + 8 * (lane >> 4);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+      qf[kk] = qok ? *reinterpret_cast<const uint4*>(qp + 32 * kk) : make_uint4(0, 0, 0, 0);
+  }
+  const float cscale = a.scale * LOG2E;
+  float m = -INFINITY, l = 0.f;
+  f32x4 o[8];
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int* bt = a.block_tables + (size_t)s * a.max_blocks;
+  const size_t head_off = (size_t)h * BS_ * D_;
+  const size_t blk_stride = (size_t)a.Hkv * BS_ * D_;
+  const int nch = (kv_end + CHUNK - 1) / CHUNK;
+  for (int c = 0; c < nch; ++c) {
+    const int tb = c * CHUNK;
+    const int b0 = bt[tb / BS_];
+    const int b1 = (tb + BS_ < kv_end) ? bt[tb / BS_ + 1] : b0;
+    const bf16_t* vb0 = a.v_cache + (size_t)b0 * blk_stride + head_off;
+    const bf16_t* vb1 = a.v_cache + (size_t)b1 * blk_stride + head_off;
+    bf16_t* vl = vls[c & 1];
+    // cooperative V staging: 512 16-B vectors per chunk
+    for (int e = threadIdx.x; e < CHUNK * D_ / 8; e += nthr) {
+      const int r = e >> 4, cc = (e & 15) * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (tb + r < kv_end) v = *reinterpret_cast<const uint4*>((r < 16 ? vb0 + r * D_ : vb1 + (r - 16) * D_) + cc);
+      *reinterpret_cast<uint4*>(vl + v_lds_off(r, cc)) = v;
+    }
+    const bf16_t* kb0 = a.k_cache + (size_t)b0 * blk_stride + head_off;
+    const bf16_t* kb1 = a.k_cache + (size_t)b1 * blk_stride + head_off;
+    f32x4 s0 = qk_tile(kb0, qf, lane);
+    f32x4 s1 = qk_tile(kb1, qf, lane);
+    const bf16x8 pb = softmax_step(s0, s1, m, l, o, tb, min(lim, kv_end), cscale, lane);
+    __syncthreads();
+    pv_update(o, vl, pb, lane);
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (!qok) return;
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  bf16_t* op = a.out + (size_t)(qs + qi) * a.out_stride + (size_t)hq * D_;
+  const int g = lane >> 4;
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) {
+    uint2 pk;
+    pk.x = pack_bf2(o[mt][0] * inv, o[mt][1] * inv);
+    pk.y = pack_bf2(o[mt][2] * inv, o[mt][3] * inv);
+    *reinterpret_cast<uint2*>(op + 16 * mt + 4 * g) = pk;
+  }
+}
+
+void launch_attn_prefill(const AttnArgs& a, hipStream_t st) {
+  if (a.num_tiles <= 0) return;
+  const int G = a.Hq / a.Hkv;
+  hipLaunchKernelGGL(attn_prefill_kernel, dim3(a.num_tiles, a.Hkv), dim3(64 * G), 0, st, a);
+}
+
+}  // namespace vgate

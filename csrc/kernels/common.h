@@ -1,0 +1,110 @@
+// Shared device helpers for the vgate gfx950 (CDNA4 / MI355X) kernels.
+//
+// Conventions used by every kernel in this directory:
+//   * wave = 64 lanes; block sizes are multiples of 64.
+//   * bf16 is moved as raw 16-bit words (uint16_t / uint4 of 8 elements) and
+//     converted with bit operations; MFMA operands are `bf16x8` ext-vectors.
+//   * MFMA shape is v_mfma_f32_16x16x32_bf16. Operand lane maps (gfx950):
+//       A: lane l holds A[row l&15][k 8(l>>4)+j], j=0..7
+//       B: lane l holds B[k 8(l>>4)+j][col l&15]
+//       C: lane l holds C[row 4(l>>4)+i][col l&15], i=0..3
+//   * Every launcher takes an explicit hipStream_t so the whole forward pass is
+//     hipGraph-capturable (no allocation / sync inside launchers).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vgate {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t bf16_t;  // storage type
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+
+// round-to-nearest-even f32 -> bf16 (NaN stays NaN via the compiler's cvt path)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 r;
+  r.x = pack_bf2(f[0], f[1]); r.y = pack_bf2(f[2], f[3]);
+  r.z = pack_bf2(f[4], f[5]); r.w = pack_bf2(f[6], f[7]);
+  return r;
+}
+
+__device__ __forceinline__ bf16x8 as_bf16x8(const uint4& v) {
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_reduce_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_reduce_max(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024; `red` needs >= 16 floats of LDS.
+__device__ __forceinline__ float block_reduce_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  v = wave_reduce_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int i = 0; i < nw; ++i) r += red[i];
+  return r;
+}
+
+__device__ __forceinline__ float block_reduce_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  v = wave_reduce_max(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float r = -INFINITY;
+  for (int i = 0; i < nw; ++i) r = fmaxf(r, red[i]);
+  return r;
+}
+
+// Non-temporal 16-B load for once-read weight streams (decode GEMV regime).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt16(const uint4* p) {
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+
+}  // namespace vgate

@@ -1,0 +1,117 @@
+// Host-side launcher declarations for the vgate HIP kernels.
+// The kernels (*.hip) are compiled by hipcc without any torch headers; the
+// torch binding layer (csrc/runtime/bindings.cpp) only sees these plain structs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vgate {
+
+struct GemmArgs {
+  const uint16_t* x;  // [M, K] bf16, row stride lda
+  int lda;
+  int M;
+  const void* wp;     // fragment-packed weight [N/16][K/32][64][8] bf16
+  int N;
+  int K;
+  const uint16_t* bias;  // [N] bf16 or null
+  const uint16_t* res;   // residual [M, N] bf16 (stride ldr) or null; may alias out
+  int ldr;
+  void* out;          // bf16 [M, N] (or [M, N/2] for silu, f32 for EPI_F32)
+  int ldo;
+  int epi;            // 0 bf16, 1 f32, 2 silu*mul (gate/up tiles interleaved)
+  int waves;          // 0 = auto
+};
+void launch_gemm(const GemmArgs& g, hipStream_t st);
+
+struct AwqGemmArgs {
+  const uint16_t* x;
+  int lda;
+  int M;
+  const uint32_t* qw;      // packed int4, fragment-major [N/16][K/32][64] uint32 (8 nibbles)
+  const uint16_t* scales;  // [K/group][N] bf16
+  const uint16_t* zeros;   // [K/group][N] bf16 (already scale*zero)
+  int group;
+  int N;
+  int K;
+  const uint16_t* bias;
+  const uint16_t* res;
+  int ldr;
+  void* out;
+  int ldo;
+  int epi;
+};
+void launch_awq_gemm(const AwqGemmArgs& g, hipStream_t st);
+
+// y = rmsnorm(x) * w ; if res != null: res = x + res (in place) and the norm is of the sum.
+void launch_rmsnorm(const uint16_t* x, int ldx, uint16_t* res, int ldres, const uint16_t* w,
+                    uint16_t* y, int ldy, int M, int H, float eps, hipStream_t st);
+
+// Embedding gather with vocab-shard masking (TP): rows outside [vstart, vstart+vrows) -> 0.
+void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int T, int H,
+                      int vstart, int vrows, hipStream_t st);
+
+// NeoX RoPE on q,k inside the fused qkv buffer + paged KV-cache write.
+// qkv: [T, (Hq + 2*Hkv) * D]; cos_sin: [max_pos, D] f32 (cos | sin halves)
+// k_cache/v_cache: [num_blocks, Hkv, BS, D]; slot < 0 => skip write.
+void launch_rope_kv(uint16_t* qkv, const int32_t* positions, const int32_t* slots,
+                    const float* cos_sin, uint16_t* k_cache, uint16_t* v_cache, int T, int Hq,
+                    int Hkv, int D, int BS, hipStream_t st);
+
+struct AttnArgs {
+  const uint16_t* q;  // [T, Hq, D] with row stride q_stride (elements, per token)
+  int q_stride;
+  const uint16_t* k_cache;  // [num_blocks, Hkv, BS, D]
+  const uint16_t* v_cache;
+  const int32_t* block_tables;  // [S, max_blocks]
+  int max_blocks;
+  const int32_t* context_lens;  // [S] total kv length (incl. new tokens)
+  const int32_t* query_start;   // [S+1] cumulative query offsets (prefill); null => decode
+  uint16_t* out;                // [T, Hq, D]
+  int out_stride;
+  float* part_o;    // decode split-K workspace [S, Hq, P, D]
+  float* part_ml;   // [S, Hq, P, 2]
+  int S;
+  int Hq;
+  int Hkv;
+  int D;
+  int BS;
+  int num_parts;    // decode: partitions per sequence (grid z)
+  int part_size;    // tokens per partition (multiple of 32)
+  float scale;
+  // prefill tiling (host computed): tile -> (seq, q offset)
+  const int32_t* tile_seq;
+  const int32_t* tile_q0;
+  int num_tiles;
+};
+void launch_attn_decode(const AttnArgs& a, hipStream_t st);
+void launch_attn_prefill(const AttnArgs& a, hipStream_t st);
+
+struct SampleArgs {
+  const float* logits;  // [B, V] f32, row stride ldl
+  int ldl;
+  int B;
+  int V;
+  const float* temperature;  // [B]
+  const float* top_p;        // [B]
+  const int32_t* top_k;      // [B]
+  const uint64_t* seeds;     // [B]
+  const int64_t* offsets;    // [B] per-row philox offset (e.g. generated-token count)
+  int32_t* out;              // [B]
+  float* out_logprob;        // [B] or null
+};
+void launch_sample(const SampleArgs& s, hipStream_t st);
+
+// Custom one-shot all-reduce over IPC-mapped peer buffers (xGMI).
+struct AllReduceArgs {
+  void* const* peers;     // device array of world_size peer buffer pointers
+  uint32_t* const* flags; // device array of world_size peer flag pointers
+  int rank;
+  int world;
+  uint16_t* out;
+  int64_t numel;
+  uint32_t epoch;
+};
+void launch_allreduce_oneshot(const AllReduceArgs& a, hipStream_t st);
+
+}  // namespace vgate

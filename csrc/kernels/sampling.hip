@@ -1,0 +1,198 @@
+// Per-row token sampling over the full vocabulary (V ~ 128k-152k) on gfx950:
+// temperature -> top-k -> top-p -> categorical, or argmax when temperature == 0.
+//
+// Exact top-k/top-p WITHOUT sorting or histogram atomics (rejection sampling):
+//   1. one pass: running max m and Z = sum exp((x - m)/T)
+//   2. draw token j by inverse CDF over {i : x_i > pivot} (thread-major order:
+//      any fixed order is a valid CDF order, so every load stays coalesced)
+//   3. one pass: c = #{x_i > x_j}, q = sum_{x_i > x_j} e_i
+//      accept j iff c < top_k and q < top_p * Z (j is inside both prefix sets);
+//      otherwise every token <= x_j is outside the nucleus too: pivot = x_j,
+//      the remaining mass is exactly q, repeat.
+// Accepted samples are distributed exactly as the renormalised filtered
+// distribution. Typical cost: 3-5 L2-resident passes over the row.
+// RNG: Philox4x32-10 keyed by the per-row seed, countered by (offset, round).
+#include "common.h"
+#include "launchers.h"
+
+namespace vgate {
+
+__device__ __forceinline__ void philox_round(uint32_t (&c)[4], const uint32_t (&k)[2]) {
+  const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+  const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+  const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+  const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+  c[0] = hi1 ^ c[1] ^ k[0];
+  c[1] = lo1;
+  c[2] = hi0 ^ c[3] ^ k[1];
+  c[3] = lo0;
+}
+
+__device__ __forceinline__ float philox_uniform(uint64_t seed, uint64_t offset, uint32_t round) {
+  uint32_t c[4] = {(uint32_t)offset, (uint32_t)(offset >> 32), round, 0x9E3779B9u};
+  uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    philox_round(c, k);
+    k[0] += 0x9E3779B9u;
+    k[1] += 0xBB67AE85u;
+  }
+  return (float)(c[0] >> 8) * (1.0f / 16777216.0f);
+}
+
+constexpr int SAMPLE_THREADS = 1024;
+constexpr float LOG2E_S = 1.4426950408889634f;
+
+// Block-wide exclusive scan of one float per thread (1024 threads, 16 waves).
+__device__ __forceinline__ float block_excl_scan(float v, float* sw, float& total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  __syncthreads();
+  if (lane == 63) sw[wid] = inc;
+  __syncthreads();
+  float base = 0.f;
+  total = 0.f;
+  const int nw = blockDim.x >> 6;
+  for (int w = 0; w < nw; ++w) {
+    const float t = sw[w];
+    if (w < wid) base += t;
+    total += t;
+  }
+  return base + inc - v;
+}
+
+__global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
+  __shared__ float red[64];
+  __shared__ float sw[16];
+  __shared__ int sel;
+  const int row = blockIdx.x;
+  const int V = a.V;
+  const float* x = a.logits + (size_t)row * a.ldl;
+  const int tid = threadIdx.x;
+  const int nt = blockDim.x;
+  const float T = a.temperature ? a.temperature[row] : 0.f;
+
+  // ---- pass 1: max (+ argmax) ----
+  float mx = -INFINITY;
+  int amx = 0x7fffffff;
+  for (int i = tid; i < V; i += nt) {
+    const float v = x[i];
+    if (v > mx) { mx = v; amx = i; }
+  }
+  // block argmax (ties -> lowest index)
+  {
+    const int lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float om = __shfl_xor(mx, o, 64);
+      const int oi = __shfl_xor(amx, o, 64);
+      if (om > mx || (om == mx && oi < amx)) { mx = om; amx = oi; }
+    }
+    __shared__ int ridx[16];
+    if (lane == 0) { red[wid] = mx; ridx[wid] = amx; }
+    __syncthreads();
+    if (tid == 0) {
+      float bm = red[0];
+      int bi = ridx[0];
+      for (int w = 1; w < (nt >> 6); ++w)
+        if (red[w] > bm || (red[w] == bm && ridx[w] < bi)) { bm = red[w]; bi = ridx[w]; }
+      red[32] = bm;
+      sel = bi;
+    }
+    __syncthreads();
+    mx = red[32];
+    amx = sel;
+    __syncthreads();
+  }
+
+  const bool greedy = !(T > 1e-5f);
+  const float c = greedy ? LOG2E_S : LOG2E_S / T;
+  // Z = sum exp2((x - mx) * c)
+  float z = 0.f;
+  for (int i = tid; i < V; i += nt) z += exp2f((x[i] - mx) * c);
+  z = block_reduce_sum(z, red);
+
+  int chosen = amx;
+  if (!greedy) {
+    const int topk = a.top_k ? a.top_k[row] : -1;
+    const float topp = a.top_p ? a.top_p[row] : 1.f;
+    const bool use_k = topk > 0 && topk < V;
+    const bool use_p = topp < 1.f;
+    const float pmass = topp * z;
+    const uint64_t seed = a.seeds ? a.seeds[row] : 0ull;
+    const uint64_t off = a.offsets ? (uint64_t)a.offsets[row] : 0ull;
+    float pivot = -INFINITY;
+    float mass = z;
+    chosen = -1;
+    for (int round = 0; round < 64; ++round) {
+      const float u = philox_uniform(seed, off, (uint32_t)round);
+      // local sum over this thread's elements above the pivot
+      float ls = 0.f;
+      for (int i = tid; i < V; i += nt) {
+        const float v = x[i];
+        if (v > pivot) ls += exp2f((v - mx) * c);
+      }
+      float total;
+      const float excl = block_excl_scan(ls, sw, total);
+      const float target = u * total;
+      if (tid == 0) sel = -1;
+      __syncthreads();
+      // owner: excl <= target < excl + ls (last non-empty thread catches rounding)
+      const bool own = (ls > 0.f) && (target >= excl) && (target < excl + ls || excl + ls >= total);
+      if (own) {
+        float run = excl;
+        int pick = -1, last = -1;
+        for (int i = tid; i < V; i += nt) {
+          const float v = x[i];
+          if (v > pivot) {
+            last = i;
+            run += exp2f((v - mx) * c);
+            if (run > target) { pick = i; break; }
+          }
+        }
+        if (pick < 0) pick = last;
+        atomicMax(&sel, pick);  // ties between owners (rounding) resolve deterministically
+      }
+      __syncthreads();
+      const int j = sel;
+      __syncthreads();
+      if (j < 0) break;
+      if (!use_k && !use_p) { chosen = j; break; }
+      const float xj = x[j];
+      float cnt = 0.f, q = 0.f;
+      for (int i = tid; i < V; i += nt) {
+        const float v = x[i];
+        if (v > xj) { cnt += 1.f; q += exp2f((v - mx) * c); }
+      }
+      cnt = block_reduce_sum(cnt, red);
+      q = block_reduce_sum(q, red);
+      const bool ok_k = !use_k || cnt < (float)topk;
+      const bool ok_p = !use_p || q < pmass;
+      if (ok_k && ok_p) { chosen = j; break; }
+      pivot = xj;
+      mass = q;
+      (void)mass;
+    }
+    if (chosen < 0) chosen = amx;
+  }
+  if (tid == 0) {
+    a.out[row] = chosen;
+    if (a.out_logprob) {
+      // natural-log probability of the chosen token under the tempered distribution
+      const float lp = ((x[chosen] - mx) * c - log2f(z)) / LOG2E_S;
+      a.out_logprob[row] = lp;
+    }
+  }
+}
+
+void launch_sample(const SampleArgs& s, hipStream_t st) {
+  if (s.B <= 0) return;
+  hipLaunchKernelGGL(sample_kernel, dim3(s.B), dim3(SAMPLE_THREADS), 0, st, s);
+}
+
+}  // namespace vgate

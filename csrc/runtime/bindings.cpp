@@ -1,0 +1,251 @@
+// Torch / pybind11 binding layer for the vgate gfx950 kernels.
+//
+// This is the only translation unit that sees torch headers; kernels are plain
+// HIP objects (csrc/kernels/*.hip) reached through csrc/kernels/launchers.h.
+// Every op launches on torch's current HIP stream, so ops are hipGraph
+// capturable via torch.cuda.graph / vgate.runtime.graphs.
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
+
+#include "../kernels/launchers.h"
+#include "allocator.h"
+
+namespace {
+
+using torch::Tensor;
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_DT(t, d) do { TORCH_CHECK((t).scalar_type() == (d), #t " has wrong dtype ", (t).scalar_type()); } while (0)
+#define CHECK_LASTDIM(t) TORCH_CHECK((t).stride(-1) == 1, #t " must be contiguous in its last dim")
+
+// torch-ROCm exposes HIP devices as DeviceType::CUDA ("masquerading")
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+const uint16_t* bf16p(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+uint16_t* bf16p_mut(Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
+const uint16_t* opt_bf16(const c10::optional<Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  CHECK_DEV(*t);
+  CHECK_DT(*t, torch::kBFloat16);
+  return reinterpret_cast<const uint16_t*>(t->data_ptr());
+}
+
+// out = epi(x @ W^T); W is fragment-packed [N/16, K/32, 64, 8]
+void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K,
+          const c10::optional<Tensor>& bias, const c10::optional<Tensor>& res, Tensor& out,
+          int64_t epi, int64_t waves) {
+  CHECK_DEV(x); CHECK_DEV(wp); CHECK_DEV(out);
+  CHECK_DT(x, torch::kBFloat16);
+  CHECK_DT(wp, torch::kBFloat16);
+  CHECK_LASTDIM(x); CHECK_LASTDIM(out);
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2, "gemm: x/out must be 2-D");
+  TORCH_CHECK(K % 32 == 0 && N % 16 == 0, "gemm: K%32 / N%16");
+  TORCH_CHECK(x.size(1) >= K, "gemm: x has ", x.size(1), " cols < K=", K);
+  TORCH_CHECK(wp.numel() == N * K, "gemm: packed weight numel mismatch");
+  const int64_t M = x.size(0);
+  TORCH_CHECK(out.size(0) >= M, "gemm: out rows");
+  const int64_t ncols = (epi == 2) ? N / 2 : N;
+  TORCH_CHECK(out.size(1) >= ncols, "gemm: out cols");
+  if (epi == 2) TORCH_CHECK((N / 16) % 2 == 0, "silu gemm needs an even tile count");
+  if (epi == 1) CHECK_DT(out, torch::kFloat32); else CHECK_DT(out, torch::kBFloat16);
+  vgate::GemmArgs g;
+  g.x = bf16p(x); g.lda = (int)x.stride(0); g.M = (int)M;
+  g.wp = wp.data_ptr(); g.N = (int)N; g.K = (int)K;
+  g.bias = opt_bf16(bias);
+  g.res = opt_bf16(res);
+  g.ldr = res.has_value() && res->defined() ? (int)res->stride(0) : 0;
+  if (g.res) TORCH_CHECK(res->size(0) >= M && res->size(1) >= N, "gemm: residual shape");
+  g.out = out.data_ptr(); g.ldo = (int)out.stride(0);
+  g.epi = (int)epi; g.waves = (int)waves;
+  c10::DeviceGuard guard(x.device());
+  vgate::launch_gemm(g, cur_stream());
+}
+
+void awq_gemm(const Tensor& x, const Tensor& qw, const Tensor& scales, const Tensor& zeros,
+              int64_t group, int64_t N, int64_t K, const c10::optional<Tensor>& bias,
+              const c10::optional<Tensor>& res, Tensor& out, int64_t epi) {
+  CHECK_DEV(x); CHECK_DEV(qw); CHECK_DEV(scales); CHECK_DEV(zeros); CHECK_DEV(out);
+  CHECK_DT(x, torch::kBFloat16);
+  CHECK_DT(qw, torch::kInt32);
+  CHECK_DT(scales, torch::kBFloat16);
+  CHECK_DT(zeros, torch::kBFloat16);
+  TORCH_CHECK(K % group == 0 && group % 32 == 0, "awq: group must divide K and be a multiple of 32");
+  TORCH_CHECK(qw.numel() == N * K / 8, "awq: packed qweight numel");
+  TORCH_CHECK(scales.size(0) == K / group && scales.size(1) == N, "awq: scales shape");
+  const int64_t M = x.size(0);
+  if (epi == 1) CHECK_DT(out, torch::kFloat32); else CHECK_DT(out, torch::kBFloat16);
+  vgate::AwqGemmArgs g;
+  g.x = bf16p(x); g.lda = (int)x.stride(0); g.M = (int)M;
+  g.qw = reinterpret_cast<const uint32_t*>(qw.data_ptr());
+  g.scales = bf16p(scales); g.zeros = bf16p(zeros); g.group = (int)group;
+  g.N = (int)N; g.K = (int)K;
+  g.bias = opt_bf16(bias); g.res = opt_bf16(res);
+  g.ldr = g.res ? (int)res->stride(0) : 0;
+  g.out = out.data_ptr(); g.ldo = (int)out.stride(0); g.epi = (int)epi;
+  c10::DeviceGuard guard(x.device());
+  vgate::launch_awq_gemm(g, cur_stream());
+}
+
+// y = rmsnorm(x [+ res]) * w ; res (if given) is updated in place to x + res
+void rmsnorm(const Tensor& x, const c10::optional<Tensor>& res, const Tensor& w, Tensor& y,
+             double eps) {
+  CHECK_DEV(x); CHECK_DEV(w); CHECK_DEV(y);
+  CHECK_DT(x, torch::kBFloat16); CHECK_DT(w, torch::kBFloat16); CHECK_DT(y, torch::kBFloat16);
+  CHECK_LASTDIM(x); CHECK_LASTDIM(y);
+  const int64_t M = x.size(0), H = x.size(1);
+  TORCH_CHECK(H % 8 == 0 && H <= 16384, "rmsnorm: H");
+  uint16_t* rp = nullptr;
+  int ldr = 0;
+  if (res.has_value() && res->defined()) {
+    CHECK_DT(*res, torch::kBFloat16);
+    rp = reinterpret_cast<uint16_t*>(res->data_ptr());
+    ldr = (int)res->stride(0);
+  }
+  c10::DeviceGuard guard(x.device());
+  vgate::launch_rmsnorm(bf16p(x), (int)x.stride(0), rp, ldr, bf16p(w), bf16p_mut(y),
+                        (int)y.stride(0), (int)M, (int)H, (float)eps, cur_stream());
+}
+
+void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart) {
+  CHECK_DEV(ids); CHECK_DEV(table); CHECK_DEV(out);
+  CHECK_DT(ids, torch::kInt32); CHECK_DT(table, torch::kBFloat16); CHECK_DT(out, torch::kBFloat16);
+  TORCH_CHECK(table.is_contiguous() && out.is_contiguous(), "embedding: contiguous");
+  const int64_t T = ids.numel(), H = table.size(1);
+  TORCH_CHECK(H % 8 == 0 && out.numel() >= T * H, "embedding: shapes");
+  c10::DeviceGuard guard(ids.device());
+  vgate::launch_embedding(reinterpret_cast<const int32_t*>(ids.data_ptr()), bf16p(table),
+                          bf16p_mut(out), (int)T, (int)H, (int)vstart, (int)table.size(0),
+                          cur_stream());
+}
+
+void rope_kv(Tensor& qkv, const Tensor& positions, const c10::optional<Tensor>& slots,
+             const Tensor& cos_sin, Tensor& k_cache, Tensor& v_cache, int64_t Hq, int64_t Hkv,
+             int64_t D) {
+  CHECK_DEV(qkv); CHECK_DEV(positions); CHECK_DEV(cos_sin);
+  CHECK_DT(qkv, torch::kBFloat16); CHECK_DT(positions, torch::kInt32);
+  CHECK_DT(cos_sin, torch::kFloat32);
+  TORCH_CHECK(qkv.is_contiguous() && qkv.size(1) == (Hq + 2 * Hkv) * D, "rope_kv: qkv shape");
+  TORCH_CHECK(D % 8 == 0 && cos_sin.size(1) == D, "rope_kv: D / cos_sin");
+  const int32_t* sp = nullptr;
+  if (slots.has_value() && slots->defined()) {
+    CHECK_DT(*slots, torch::kInt32);
+    sp = reinterpret_cast<const int32_t*>(slots->data_ptr());
+  }
+  const int BS = (int)k_cache.size(2);
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == D, "rope_kv: cache shape");
+  c10::DeviceGuard guard(qkv.device());
+  vgate::launch_rope_kv(bf16p_mut(qkv), reinterpret_cast<const int32_t*>(positions.data_ptr()), sp,
+                        reinterpret_cast<const float*>(cos_sin.data_ptr()), bf16p_mut(k_cache),
+                        bf16p_mut(v_cache), (int)qkv.size(0), (int)Hq, (int)Hkv, (int)D, BS,
+                        cur_stream());
+}
+
+vgate::AttnArgs attn_common(const Tensor& q, int64_t q_stride, const Tensor& k_cache,
+                            const Tensor& v_cache, const Tensor& block_tables,
+                            const Tensor& context_lens, Tensor& out, int64_t Hq, int64_t Hkv,
+                            double scale) {
+  CHECK_DEV(q); CHECK_DEV(k_cache); CHECK_DEV(v_cache); CHECK_DEV(block_tables);
+  CHECK_DEV(context_lens); CHECK_DEV(out);
+  CHECK_DT(q, torch::kBFloat16); CHECK_DT(out, torch::kBFloat16);
+  CHECK_DT(block_tables, torch::kInt32); CHECK_DT(context_lens, torch::kInt32);
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 16 && k_cache.size(3) == 128,
+              "attention: cache must be [nblk, Hkv, 16, 128]");
+  TORCH_CHECK(Hq % Hkv == 0 && Hq / Hkv <= 16, "attention: GQA group must be <= 16");
+  TORCH_CHECK(block_tables.is_contiguous(), "attention: block_tables contiguous");
+  vgate::AttnArgs a{};
+  a.q = bf16p(q); a.q_stride = (int)q_stride;
+  a.k_cache = bf16p(k_cache); a.v_cache = bf16p(v_cache);
+  a.block_tables = reinterpret_cast<const int32_t*>(block_tables.data_ptr());
+  a.max_blocks = (int)block_tables.size(1);
+  a.context_lens = reinterpret_cast<const int32_t*>(context_lens.data_ptr());
+  a.out = bf16p_mut(out); a.out_stride = (int)(Hq * 128);
+  TORCH_CHECK(out.is_contiguous(), "attention: out contiguous");
+  a.S = (int)context_lens.numel();
+  a.Hq = (int)Hq; a.Hkv = (int)Hkv; a.D = 128; a.BS = 16;
+  a.scale = (float)scale;
+  return a;
+}
+
+void attn_decode(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const Tensor& v_cache,
+                 const Tensor& block_tables, const Tensor& context_lens,
+                 const c10::optional<Tensor>& query_start, Tensor& out, Tensor& part_o,
+                 Tensor& part_ml, int64_t Hq, int64_t Hkv, int64_t part_size, double scale) {
+  auto a = attn_common(q, q_stride, k_cache, v_cache, block_tables, context_lens, out, Hq, Hkv, scale);
+  CHECK_DT(part_o, torch::kFloat32); CHECK_DT(part_ml, torch::kFloat32);
+  TORCH_CHECK(part_size % 32 == 0, "attention: part_size % 32");
+  TORCH_CHECK(part_o.dim() == 4 && part_o.size(0) >= a.S && part_o.size(1) == Hq && part_o.size(3) == 128,
+              "attention: part_o must be [S, Hq, P, 128]");
+  a.num_parts = (int)part_o.size(2);
+  TORCH_CHECK((int64_t)a.num_parts * part_size >= block_tables.size(1) * 16,
+              "attention: partitions do not cover max context");
+  a.part_size = (int)part_size;
+  a.part_o = reinterpret_cast<float*>(part_o.data_ptr());
+  a.part_ml = reinterpret_cast<float*>(part_ml.data_ptr());
+  a.query_start = nullptr;
+  if (query_start.has_value() && query_start->defined()) {
+    CHECK_DT(*query_start, torch::kInt32);
+    a.query_start = reinterpret_cast<const int32_t*>(query_start->data_ptr());
+  }
+  c10::DeviceGuard guard(q.device());
+  vgate::launch_attn_decode(a, cur_stream());
+}
+
+void attn_prefill(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const Tensor& v_cache,
+                  const Tensor& block_tables, const Tensor& context_lens,
+                  const Tensor& query_start, const Tensor& tile_seq, const Tensor& tile_q0,
+                  Tensor& out, int64_t Hq, int64_t Hkv, double scale) {
+  auto a = attn_common(q, q_stride, k_cache, v_cache, block_tables, context_lens, out, Hq, Hkv, scale);
+  CHECK_DT(query_start, torch::kInt32); CHECK_DT(tile_seq, torch::kInt32); CHECK_DT(tile_q0, torch::kInt32);
+  a.query_start = reinterpret_cast<const int32_t*>(query_start.data_ptr());
+  a.tile_seq = reinterpret_cast<const int32_t*>(tile_seq.data_ptr());
+  a.tile_q0 = reinterpret_cast<const int32_t*>(tile_q0.data_ptr());
+  a.num_tiles = (int)tile_seq.numel();
+  c10::DeviceGuard guard(q.device());
+  vgate::launch_attn_prefill(a, cur_stream());
+}
+
+void sample(const Tensor& logits, const c10::optional<Tensor>& temperature,
+            const c10::optional<Tensor>& top_p, const c10::optional<Tensor>& top_k,
+            const c10::optional<Tensor>& seeds, const c10::optional<Tensor>& offsets, Tensor& out,
+            const c10::optional<Tensor>& out_logprob) {
+  CHECK_DEV(logits); CHECK_DEV(out);
+  CHECK_DT(logits, torch::kFloat32); CHECK_DT(out, torch::kInt32);
+  CHECK_LASTDIM(logits);
+  vgate::SampleArgs s{};
+  s.logits = reinterpret_cast<const float*>(logits.data_ptr());
+  s.ldl = (int)logits.stride(0);
+  s.B = (int)logits.size(0);
+  s.V = (int)logits.size(1);
+  auto fp = [](const c10::optional<Tensor>& t, c10::ScalarType dt) -> const void* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->scalar_type() == dt, "sample: dtype mismatch");
+    TORCH_CHECK(t->is_cuda(), "sample: GPU tensor expected");
+    return t->data_ptr();
+  };
+  s.temperature = static_cast<const float*>(fp(temperature, torch::kFloat32));
+  s.top_p = static_cast<const float*>(fp(top_p, torch::kFloat32));
+  s.top_k = static_cast<const int32_t*>(fp(top_k, torch::kInt32));
+  s.seeds = static_cast<const uint64_t*>(fp(seeds, torch::kInt64));
+  s.offsets = static_cast<const int64_t*>(fp(offsets, torch::kInt64));
+  s.out = reinterpret_cast<int32_t*>(out.data_ptr());
+  s.out_logprob = const_cast<float*>(static_cast<const float*>(fp(out_logprob, torch::kFloat32)));
+  c10::DeviceGuard guard(logits.device());
+  vgate::launch_sample(s, cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "vgate gfx950 (MI355X) HIP kernels and native runtime";
+  m.def("gemm", &gemm, "fragment-packed MFMA GEMM with fused epilogue");
+  m.def("awq_gemm", &awq_gemm, "AWQ W4A16 dequant-GEMM");
+  m.def("rmsnorm", &rmsnorm, "RMSNorm with optional fused residual add");
+  m.def("embedding", &embedding, "vocab-sharded embedding gather");
+  m.def("rope_kv", &rope_kv, "NeoX RoPE + paged KV-cache write");
+  m.def("attn_decode", &attn_decode, "paged split-K decode attention");
+  m.def("attn_prefill", &attn_prefill, "paged varlen causal prefill attention");
+  m.def("sample", &sample, "temperature/top-k/top-p sampling");
+  vgate::bind_runtime(m);
+}

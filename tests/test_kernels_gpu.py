@@ -1,0 +1,241 @@
+"""Numerics of every gfx950 HIP kernel against a plain PyTorch fp32 reference.
+
+Run on an MI355X: ``python -m pytest tests -m gpu``. Shapes include the real
+Qwen2.5-1.5B / Llama-3 projection sizes.
+"""
+import math
+
+import pytest
+import torch
+
+from vgate import ops
+from vgate.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-6)).item()
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _native():
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    ops.native()  # must load: no silent fallback
+    yield
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 2048, 1536), (8, 1536, 1536), (8, 1536, 8960), (17, 256, 512),
+                                   (33, 4096, 4096), (64, 6144, 4096), (100, 512, 1024), (300, 1024, 2048)])
+def test_gemm_plain(M, N, K):
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    lin = ops.Linear(w)
+    y = ops.linear(x, lin)
+    yr = ref.linear_ref(x, w)
+    assert _rel_err(y, yr) < 1e-2
+
+
+def test_gemm_bias_residual_f32():
+    torch.manual_seed(1)
+    M, N, K = 8, 2048, 1536
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device=DEV).bfloat16()
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    lin = ops.Linear(w, bias=b)
+    assert _rel_err(ops.linear(x, lin), ref.linear_ref(x, w, b)) < 1e-2
+    lin2 = ops.Linear(w)
+    assert _rel_err(ops.linear(x, lin2, residual=r), ref.linear_ref(x, w, None, r)) < 1e-2
+    y32 = ops.linear(x, lin2, out_f32=True)
+    assert y32.dtype == torch.float32
+    assert _rel_err(y32, ref.linear_ref(x, w, out_f32=True)) < 5e-3
+    # in-place residual (out aliases residual), as the model's o_proj/down_proj do
+    r2 = r.clone()
+    ops.linear(x, lin2, out=r2, residual=r2)
+    assert _rel_err(r2, ref.linear_ref(x, w, None, r)) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 8, 40])
+def test_gemm_silu(M):
+    torch.manual_seed(2)
+    I, K = 8960 // 4, 1536
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    wg = (torch.randn(I, K, device=DEV) / math.sqrt(K)).bfloat16()
+    wu = (torch.randn(I, K, device=DEV) / math.sqrt(K)).bfloat16()
+    lin = ops.Linear(torch.cat([wg, wu]), kind="silu")
+    y = ops.linear(x, lin)
+    assert y.shape == (M, I)
+    assert _rel_err(y, ref.silu_mul_linear_ref(x, wg, wu)) < 1e-2
+
+
+def test_gemm_asymmetric_identity():
+    # A = I with an asymmetric B catches transposed C writes (cdna_hip_programming.md §3)
+    K = 64
+    x = torch.eye(16, K, device=DEV).bfloat16()
+    w = torch.arange(32 * K, device=DEV, dtype=torch.float32).reshape(32, K).remainder(7).bfloat16()
+    y = ops.linear(x, ops.Linear(w))
+    assert torch.equal(y.float(), (x.float() @ w.float().t()))
+
+
+def test_awq_gemm():
+    torch.manual_seed(3)
+    M, N, K, g = 8, 512, 1024, 128
+    q = torch.randint(0, 16, (N, K), dtype=torch.int32)
+    scales = (torch.rand(K // g, N) * 0.02 + 0.005).bfloat16()
+    zeros = torch.randint(0, 16, (K // g, N)).float().bfloat16()
+    lin = ops.Linear(None, kind="awq", awq={"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV), "group": g})
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    wd = ref.awq_dequant_ref(q, scales, zeros, g).to(DEV)
+    assert _rel_err(ops.linear(x, lin), ref.linear_ref(x, wd)) < 2e-2
+
+
+@pytest.mark.parametrize("H", [1536, 4096, 8192])
+def test_rmsnorm(H):
+    torch.manual_seed(4)
+    x = torch.randn(13, H, device=DEV).bfloat16()
+    r = torch.randn(13, H, device=DEV).bfloat16()
+    w = torch.randn(H, device=DEV).bfloat16()
+    y = ops.rmsnorm(x, w, 1e-6)
+    yr, _ = ref.rmsnorm_ref(x, w, 1e-6)
+    assert _rel_err(y, yr) < 1e-2
+    r2 = r.clone()
+    y2 = ops.rmsnorm(x, w, 1e-6, residual=r2)
+    yr2, sr = ref.rmsnorm_ref(x, w, 1e-6, r)
+    assert torch.equal(r2, sr)
+    assert _rel_err(y2, yr2) < 1e-2
+
+
+def test_embedding_vocab_shard():
+    table = torch.randn(100, 64, device=DEV).bfloat16()
+    ids = torch.tensor([0, 5, 99, 100, 150, 42], device=DEV, dtype=torch.int32)
+    out = ops.embedding(ids, table, vstart=50)
+    assert torch.equal(out, ref.embedding_ref(ids, table, 50))
+
+
+def test_rope_kv():
+    torch.manual_seed(5)
+    Hq, Hkv, D, BS, T = 12, 2, 128, 16, 37
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV).bfloat16()
+    pos = torch.randint(0, 4000, (T,), device=DEV, dtype=torch.int32)
+    slots = torch.randperm(64 * BS, device=DEV)[:T].int()
+    slots[3] = -1
+    cs = ref.rope_cos_sin(4096, D, 1e6, device=DEV)
+    kc = torch.zeros(64, Hkv, BS, D, device=DEV).bfloat16()
+    vc = torch.zeros_like(kc)
+    a, kc2, vc2 = qkv.clone(), kc.clone(), vc.clone()
+    ops.rope_kv(a, pos, slots, cs, kc, vc, Hq, Hkv, D)
+    ref.rope_kv_ref(qkv, pos, slots, cs, kc2, vc2, Hq, Hkv, D)
+    assert _rel_err(a, qkv) < 1e-2
+    assert _rel_err(kc, kc2) < 1e-2
+    assert torch.equal(vc, vc2)
+
+
+def _make_cache(num_blocks, Hkv, D=128, BS=16, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    kc = torch.randn(num_blocks, Hkv, BS, D, generator=g).bfloat16().to(DEV)
+    vc = torch.randn(num_blocks, Hkv, BS, D, generator=g).bfloat16().to(DEV)
+    return kc, vc
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(12, 2), (32, 8), (8, 1), (64, 8)])
+@pytest.mark.parametrize("ctxs", [[1, 7, 33, 100], [513, 2048, 1500, 64], [5]])
+def test_attention_decode(Hq, Hkv, ctxs):
+    torch.manual_seed(6)
+    D, BS = 128, 16
+    S = len(ctxs)
+    maxb = 2048 // BS
+    nblk = S * maxb + 8
+    kc, vc = _make_cache(nblk, Hkv)
+    perm = torch.randperm(nblk - 1)[: S * maxb] + 1
+    bt = perm.reshape(S, maxb).int().to(DEV)
+    cl = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
+    q = torch.randn(S, Hq * D, device=DEV).bfloat16()
+    part = 512
+    P = (maxb * BS + part - 1) // part
+    po = torch.empty(S, Hq, P, D, device=DEV)
+    pml = torch.empty(S, Hq, P, 2, device=DEV)
+    out = torch.zeros(S, Hq * D, device=DEV).bfloat16()
+    scale = 1 / math.sqrt(D)
+    ops.attention_decode(q, Hq * D, kc, vc, bt, cl, out, po, pml, Hq, Hkv, part, scale)
+    r = ref.attention_ref(q.view(S, Hq, D), kc, vc, bt, cl, torch.arange(S + 1, dtype=torch.int32), Hq, Hkv, scale)
+    assert _rel_err(out.view(S, Hq, D), r) < 2e-2
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(12, 2), (32, 8), (16, 16)])
+def test_attention_prefill_chunked(Hq, Hkv):
+    torch.manual_seed(7)
+    D, BS = 128, 16
+    qlens = [1, 17, 64, 5, 130]
+    ctxs = [1, 17, 100, 300, 130]  # ctx > qlen => chunked prefill against earlier cache
+    S = len(qlens)
+    maxb = 32
+    nblk = S * maxb + 4
+    kc, vc = _make_cache(nblk, Hkv, seed=1)
+    bt = (torch.randperm(nblk)[: S * maxb]).reshape(S, maxb).int().to(DEV)
+    qs = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32, device=DEV)
+    T = int(qs[-1])
+    cl = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
+    stride = (Hq + 2 * Hkv) * D  # q lives inside a fused qkv row
+    qkv = torch.randn(T, stride, device=DEV).bfloat16()
+    ts, tq = ops.prefill_tiles(qlens)
+    ts = torch.tensor(ts, dtype=torch.int32, device=DEV)
+    tq = torch.tensor(tq, dtype=torch.int32, device=DEV)
+    out = torch.zeros(T, Hq * D, device=DEV).bfloat16()
+    scale = 1 / math.sqrt(D)
+    ops.attention_prefill(qkv, stride, kc, vc, bt, cl, qs, ts, tq, out, Hq, Hkv, scale)
+    q = qkv[:, : Hq * D].reshape(T, Hq, D)
+    r = ref.attention_ref(q, kc, vc, bt, cl, qs.cpu(), Hq, Hkv, scale)
+    assert _rel_err(out.view(T, Hq, D), r) < 2e-2
+
+
+def test_sample_greedy_and_topk1():
+    torch.manual_seed(8)
+    B, V = 6, 151936
+    logits = torch.randn(B, V, device=DEV) * 3
+    out = ops.sample(logits, temperature=torch.zeros(B, device=DEV))
+    assert torch.equal(out.long().cpu(), logits.argmax(-1).cpu())
+    t = torch.ones(B, device=DEV)
+    out2 = ops.sample(logits, temperature=t, top_k=torch.ones(B, dtype=torch.int32, device=DEV),
+                      seeds=torch.arange(B, device=DEV), offsets=torch.zeros(B, dtype=torch.int64, device=DEV))
+    assert torch.equal(out2.long().cpu(), logits.argmax(-1).cpu())
+
+
+def test_sample_distribution_topk_topp():
+    V = 1000
+    logits = torch.full((1, V), -10.0, device=DEV)
+    logits[0, :4] = torch.tensor([2.0, 1.5, 1.0, 0.2], device=DEV)
+    n = 3000
+    L = logits.expand(n, V).contiguous()
+    t = torch.ones(n, device=DEV)
+    seeds = torch.arange(n, device=DEV, dtype=torch.int64) * 7919 + 1
+    offs = torch.zeros(n, dtype=torch.int64, device=DEV)
+    # top_k = 2 -> only tokens 0/1 with ratio e^2 : e^1.5
+    out = ops.sample(L, t, top_k=torch.full((n,), 2, dtype=torch.int32, device=DEV), seeds=seeds, offsets=offs)
+    o = out.cpu()
+    assert set(o.tolist()) <= {0, 1}
+    p0 = (o == 0).float().mean().item()
+    exp0 = math.exp(2.0) / (math.exp(2.0) + math.exp(1.5))
+    assert abs(p0 - exp0) < 0.04
+    # top_p = 0.7 -> nucleus {0, 1} (p0=.47 < .7, p0+p1=.76 >= .7)
+    out = ops.sample(L, t, top_p=torch.full((n,), 0.7, device=DEV), seeds=seeds, offsets=offs)
+    assert set(out.cpu().tolist()) <= {0, 1}
+    # determinism
+    out_b = ops.sample(L, t, top_p=torch.full((n,), 0.7, device=DEV), seeds=seeds, offsets=offs)
+    assert torch.equal(out, out_b)
+    # plain multinomial hits the tail sometimes, never invalid ids
+    out = ops.sample(L, t, seeds=seeds, offsets=offs)
+    assert int(out.max()) < V and int(out.min()) >= 0
+
+
+def test_sample_logprob():
+    torch.manual_seed(9)
+    logits = torch.randn(4, 5000, device=DEV)
+    lp = torch.empty(4, device=DEV)
+    out = ops.sample(logits, temperature=torch.zeros(4, device=DEV), out_logprob=lp)
+    exp = torch.log_softmax(logits, -1).gather(1, out.long()[:, None]).squeeze(1)
+    assert torch.allclose(lp, exp, atol=1e-3)

@@ -1,0 +1,93 @@
+"""CPU checks of the op layer: weight packing layouts and the reference paths."""
+import math
+
+import torch
+
+from vgate import ops
+from vgate.ops import reference as ref
+
+
+def test_pack_roundtrip_and_fragment_layout():
+    N, K = 48, 96
+    w = torch.randn(N, K).bfloat16()
+    wp = ops.pack_weight(w)
+    assert torch.equal(ops.unpack_weight(wp, N, K), w)
+    flat = wp.reshape(-1, 8)
+    # tile (nt=1, kt=2), lane 37 -> row 16 + 37%16, cols 64 + 8*(37//16) ...
+    nt, kt, lane = 1, 2, 37
+    idx = (nt * (K // 32) + kt) * 64 + lane
+    assert torch.equal(flat[idx], w[16 * nt + lane % 16, 32 * kt + 8 * (lane // 16): 32 * kt + 8 * (lane // 16) + 8])
+
+
+def test_interleave_gate_up_roundtrip():
+    I, K = 64, 32
+    wg, wu = torch.randn(I, K).bfloat16(), torch.randn(I, K).bfloat16()
+    lin = ops.Linear(torch.cat([wg, wu]), kind="silu")
+    assert torch.equal(lin.dense_weight(), torch.cat([wg, wu]))
+    x = torch.randn(3, K).bfloat16()
+    assert torch.allclose(ops.linear(x, lin).float(), ref.silu_mul_linear_ref(x, wg, wu).float())
+
+
+def test_pack_awq_layout():
+    N, K = 32, 256
+    q = torch.randint(0, 16, (N, K), dtype=torch.int32)
+    p = ops.pack_awq(q).view(torch.int32).reshape(-1)
+    nt, kq, lane, u = 1, 1, 21, 2
+    word = int(p[((nt * (K // 128) + kq) * 64 + lane) * 4 + u]) & 0xFFFFFFFF
+    row = 16 * nt + (lane & 15)
+    k0 = 128 * kq + 32 * u + 8 * (lane >> 4)
+    vals = [(word >> (4 * j)) & 0xF for j in range(8)]
+    assert vals == q[row, k0:k0 + 8].tolist()
+
+
+def test_attention_ref_matches_dense():
+    torch.manual_seed(0)
+    Hq, Hkv, D, BS = 4, 2, 128, 16
+    ctx = 40
+    kc = torch.randn(8, Hkv, BS, D).bfloat16()
+    vc = torch.randn(8, Hkv, BS, D).bfloat16()
+    bt = torch.tensor([[5, 2, 7, 0]], dtype=torch.int32)
+    q = torch.randn(1, Hq, D).bfloat16()
+    out = ref.attention_ref(q, kc, vc, bt, torch.tensor([ctx]), torch.tensor([0, 1]), Hq, Hkv, 1 / math.sqrt(D))
+    K = torch.cat([kc[b] for b in [5, 2, 7]], dim=1)[:, :ctx].float()
+    V = torch.cat([vc[b] for b in [5, 2, 7]], dim=1)[:, :ctx].float()
+    for h in range(Hq):
+        kv = h // 2
+        p = torch.softmax(q[0, h].float() @ K[kv].t() / math.sqrt(D), -1)
+        assert torch.allclose(out[0, h].float(), (p @ V[kv]), atol=2e-2)
+
+
+def test_rope_table_llama3_scaling_shapes():
+    t = ref.rope_cos_sin(64, 128, 5e5, {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                         "high_freq_factor": 4.0, "original_max_position_embeddings": 8192})
+    assert t.shape == (64, 128)
+    assert torch.allclose(t[0, :64], torch.ones(64))
+
+
+def test_sample_ref_topk():
+    logits = torch.tensor([[0.0, 5.0, 1.0, 4.0]])
+    gens = [torch.Generator().manual_seed(0)]
+    outs = {int(ref.sample_ref(logits, torch.tensor([1.0]), None, torch.tensor([2]), gens)[0]) for _ in range(50)}
+    assert outs <= {1, 3}
+
+
+def test_native_allocator_if_built():
+    try:
+        C = ops.native()
+    except RuntimeError:
+        import pytest
+        pytest.skip("native extension not built")
+    a = C.BlockAllocator(8, 16, True)
+    b = a.allocate(3)
+    assert len(set(b)) == 3 and a.num_free() == 5
+    h = C.BlockAllocator.hash_block(0, [1, 2, 3])
+    a.register_hash(b[0], h)
+    a.free(b)
+    assert a.num_free() == 8
+    got = a.lookup(h)
+    assert got == b[0] and a.refcount(got) == 1 and a.num_free() == 7
+    a.free([got])
+    # evictable cached block is reused last
+    c = a.allocate(8)
+    assert len(set(c)) == 8
+    assert a.lookup(h) == -1

@@ -1,0 +1,225 @@
+"""Decoder-only transformer (Qwen2 / Llama families) on the vgate kernel set.
+
+One forward pass = one engine step over a flat token batch (any mix of decode
+tokens and prefill chunks), reading all step metadata from device buffers
+(:class:`vgate.runtime.step_meta.StepView`) so the identical code path is
+captured into a hipGraph per token-count bucket.
+
+Per layer (TP degree t, Megatron layout):
+    x    = rmsnorm(resid)                              K2
+    qkv  = x @ Wqkv^T + b           column-parallel    K3 (MFMA, fused bias)
+    rope(q, k); k, v -> paged cache                    K4
+    a    = paged attention(q)       heads sharded      K5 / K6
+    resid = resid + a @ Wo^T        row-parallel       K7 (+residual epilogue) -> C1 all-reduce
+    x    = rmsnorm(resid)                              K2
+    h    = silu(x Wg^T) * (x Wu^T)  column-parallel    K8 (fused SiLU*mul epilogue)
+    resid = resid + h @ Wd^T        row-parallel       K9 (+residual epilogue) -> C1
+The residual add of a row-parallel GEMM is applied by TP rank 0 only, so the
+all-reduce of the partial outputs yields resid + sum(partials) on every rank
+with no extra kernel.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from vgate import ops
+from vgate.models.config import ModelArch
+from vgate.parallel.comm import TPGroup
+
+
+@dataclass
+class LayerWeights:
+    in_norm: torch.Tensor
+    qkv: ops.Linear
+    o: ops.Linear
+    post_norm: torch.Tensor
+    gate_up: ops.Linear
+    down: ops.Linear
+
+
+class ShardSpec:
+    """Per-rank sizes for a TP degree."""
+
+    def __init__(self, arch: ModelArch, tp: TPGroup):
+        self.tp = tp
+        t, r = tp.size, tp.rank
+        if arch.num_heads % t:
+            raise ValueError(f"num_heads {arch.num_heads} not divisible by tp {t}")
+        self.hq = arch.num_heads // t
+        if arch.num_kv_heads >= t:
+            if arch.num_kv_heads % t:
+                raise ValueError("num_kv_heads not divisible by tp")
+            self.hkv = arch.num_kv_heads // t
+            self.kv_head0 = r * self.hkv
+        else:  # replicate KV heads across ranks (e.g. Qwen 2 KV heads at tp 4/8)
+            if t % arch.num_kv_heads:
+                raise ValueError("tp not a multiple of num_kv_heads")
+            self.hkv = 1
+            self.kv_head0 = r // (t // arch.num_kv_heads)
+        self.q_head0 = r * self.hq
+        if arch.intermediate_size % (16 * t):
+            raise ValueError("intermediate_size must split into 16-row tiles per rank")
+        self.inter = arch.intermediate_size // t
+        self.inter0 = r * self.inter
+        vpad = ((arch.vocab_size + 16 * t - 1) // (16 * t)) * 16 * t
+        self.vocab_padded = vpad
+        self.vocab = vpad // t
+        self.vocab0 = r * self.vocab
+
+
+class DecoderModel:
+    def __init__(self, arch: ModelArch, device: torch.device | str, tp: TPGroup | None = None,
+                 quantization: str | None = None, seed: int = 0, weights_path: str | None = None,
+                 max_model_len: int = 4096):
+        self.arch = arch
+        self.device = torch.device(device)
+        self.tp = tp or TPGroup()
+        self.shard = ShardSpec(arch, self.tp)
+        self.quant = (quantization or "").lower() or None
+        if self.device.type == "cuda" and arch.head_dim != 128:
+            raise ValueError("the gfx950 attention kernels require head_dim == 128")
+        self.max_model_len = max_model_len
+        self.scale = 1.0 / math.sqrt(arch.head_dim)
+        if weights_path:
+            from vgate.models.weights import load_checkpoint
+            load_checkpoint(self, weights_path)
+        else:
+            from vgate.models.weights import random_init
+            random_init(self, seed)
+        table_len = max(max_model_len, 16) + 1
+        self.cos_sin = ops.ref.rope_cos_sin(table_len, arch.head_dim, arch.rope_theta, arch.rope_scaling,
+                                            device=self.device)
+
+    # ------------------------------------------------------------------ sizes
+    @property
+    def num_kv_heads_local(self) -> int:
+        return self.shard.hkv
+
+    @property
+    def num_heads_local(self) -> int:
+        return self.shard.hq
+
+    def weight_bytes(self) -> int:
+        n = self.embed.numel() * 2 + self.final_norm.numel() * 2 + self.lm_head.nbytes()
+        for L in self.layers:
+            n += L.qkv.nbytes() + L.o.nbytes() + L.gate_up.nbytes() + L.down.nbytes() + 4 * L.in_norm.numel()
+        return n
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, sv, kv_caches, part_size: int) -> torch.Tensor:
+        """One step. ``sv`` is a StepView (token/seq metadata views, bucket sizes T and S).
+
+        Returns f32 logits [S, vocab] for the sample rows (one per sequence).
+        """
+        a = self.arch
+        sh = self.shard
+        tp = self.tp
+        T, S = sv.T, sv.S
+        D = a.head_dim
+        dev = self.device
+        gpu = dev.type == "cuda"
+        resid = ops.embedding(sv.ids, self.embed, vstart=sh.vocab0)
+        if tp.size > 1:
+            tp.all_reduce(resid)
+        x = torch.empty_like(resid)
+        attn = torch.empty(T, sh.hq * D, dtype=torch.bfloat16, device=dev)
+        qkv_w = (sh.hq + 2 * sh.hkv) * D
+        qkv = torch.empty(T, qkv_w, dtype=torch.bfloat16, device=dev)
+        mlp = torch.empty(T, sh.inter, dtype=torch.bfloat16, device=dev)
+        if gpu:
+            P = max(1, (self.max_model_len + part_size - 1) // part_size)
+            part_o = torch.empty(S, sh.hq, P, D, dtype=torch.float32, device=dev)
+            part_ml = torch.empty(S, sh.hq, P, 2, dtype=torch.float32, device=dev)
+        first = tp.is_first
+        for li, L in enumerate(self.layers):
+            kc, vc = kv_caches[li]
+            ops.rmsnorm(resid, L.in_norm, a.rms_eps, out=x)
+            ops.linear(x, L.qkv, out=qkv)
+            ops.rope_kv(qkv, sv.positions, sv.slots, self.cos_sin, kc, vc, sh.hq, sh.hkv, D)
+            if gpu:
+                ops.attention_decode(qkv, qkv_w, kc, vc, sv.block_tables, sv.context_lens, attn, part_o, part_ml,
+                                     sh.hq, sh.hkv, part_size, self.scale, query_start=sv.query_start)
+                ops.attention_prefill(qkv, qkv_w, kc, vc, sv.block_tables, sv.context_lens, sv.query_start,
+                                      sv.tile_seq, sv.tile_q0, attn, sh.hq, sh.hkv, self.scale)
+            else:
+                self._attention_cpu(qkv, attn, kc, vc, sv)
+            ops.linear(attn, L.o, out=resid, residual=resid if first else None)
+            if tp.size > 1:
+                tp.all_reduce(resid)
+            ops.rmsnorm(resid, L.post_norm, a.rms_eps, out=x)
+            ops.linear(x, L.gate_up, out=mlp)
+            ops.linear(mlp, L.down, out=resid, residual=resid if first else None)
+            if tp.size > 1:
+                tp.all_reduce(resid)
+        xs = resid.index_select(0, sv.sample_idx)
+        xn = ops.rmsnorm(xs, self.final_norm, a.rms_eps)
+        logits = ops.linear(xn, self.lm_head, out_f32=True)
+        if tp.size > 1:
+            logits = tp.all_gather_lastdim(logits)
+        return logits[:, : a.vocab_size]
+
+    def _attention_cpu(self, qkv, attn, kc, vc, sv):
+        sh = self.shard
+        D = self.arch.head_dim
+        n = int(sv.num_tokens)
+        nseq = int(sv.num_seqs)
+        if n == 0 or nseq == 0:
+            return
+        T = qkv.shape[0]
+        q = qkv[:, : sh.hq * D].reshape(T, sh.hq, D)
+        qs = sv.query_start[: nseq + 1]
+        o = ops.ref.attention_ref(q[:n], kc, vc, sv.block_tables[:nseq], sv.context_lens[:nseq], qs,
+                                  sh.hq, sh.hkv, self.scale)
+        attn[:n] = o.reshape(n, sh.hq * D)
+
+    # ------------------------------------------------------------- reference
+    @torch.no_grad()
+    def reference_logits(self, token_ids: list[int]) -> torch.Tensor:
+        """Dense fp32 forward of one sequence (no KV cache, no custom kernels) -> [len, vocab].
+
+        Used by tests as the oracle for the engine's kernel path (TP=1 only).
+        """
+        assert self.tp.size == 1
+        a = self.arch
+        D = a.head_dim
+        ids = torch.tensor(token_ids, device=self.device)
+        n = len(token_ids)
+        r = self.embed[ids].float()
+        cs = self.cos_sin[:n]
+        c, s = cs[:, None, : D // 2], cs[:, None, D // 2:]
+
+        def rope(t):
+            x1, x2 = t[..., : D // 2], t[..., D // 2:]
+            return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], -1)
+
+        def norm(t, w):
+            return t * torch.rsqrt(t.pow(2).mean(-1, keepdim=True) + a.rms_eps) * w.float()
+
+        mask = torch.full((n, n), float("-inf"), device=self.device).triu(1)
+        G = a.num_heads // a.num_kv_heads
+        for L in self.layers:
+            x = norm(r, L.in_norm)
+            wqkv = L.qkv.dense_weight().float()
+            qkv = x @ wqkv.t()
+            if L.qkv.bias is not None:
+                qkv = qkv + L.qkv.bias.float()
+            q = qkv[:, : a.q_size].view(n, a.num_heads, D)
+            k = qkv[:, a.q_size: a.q_size + a.kv_size].view(n, a.num_kv_heads, D)
+            v = qkv[:, a.q_size + a.kv_size:].view(n, a.num_kv_heads, D)
+            q, k = rope(q), rope(k)
+            k = k.repeat_interleave(G, 1)
+            v = v.repeat_interleave(G, 1)
+            sc = torch.einsum("qhd,khd->hqk", q, k) * self.scale + mask
+            o = torch.einsum("hqk,khd->qhd", torch.softmax(sc, -1), v).reshape(n, -1)
+            r = r + o @ L.o.dense_weight().float().t()
+            x = norm(r, L.post_norm)
+            gu = L.gate_up.dense_weight().float()
+            I = gu.shape[0] // 2
+            h = torch.nn.functional.silu(x @ gu[:I].t()) * (x @ gu[I:].t())
+            r = r + h @ L.down.dense_weight().float().t()
+        x = norm(r, self.final_norm)
+        w = self.embed if a.tie_embeddings else self.lm_head.dense_weight()
+        return (x @ w.float().t())[:, : a.vocab_size]

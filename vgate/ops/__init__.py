@@ -1,0 +1,283 @@
+"""vgate compute ops: gfx950 HIP kernels (``vgate._C``) with fp32 torch references.
+
+Dispatch rule: GPU tensors ALWAYS go to the native HIP kernels — if the
+extension is missing on a GPU machine the op raises (no silent eager fallback);
+CPU tensors use the reference implementations in :mod:`vgate.ops.reference`.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import torch
+
+from . import reference as ref
+
+_C = None
+_C_ERR: Exception | None = None
+
+
+def native():
+    """Return the compiled extension module, building it in-tree if needed."""
+    global _C, _C_ERR
+    if _C is not None:
+        return _C
+    try:
+        from vgate import _C as mod  # type: ignore
+        _C = mod
+    except ImportError as e:  # pragma: no cover - depends on build state
+        if os.environ.get("VGATE_AUTOBUILD", "1") == "1":
+            try:
+                import importlib
+                import sys
+                from pathlib import Path
+                sys.path.insert(0, str(Path(__file__).resolve().parents[2] / "csrc"))
+                import build as _build  # type: ignore
+                _build.build(verbose=False)
+                _C = importlib.import_module("vgate._C")
+                return _C
+            except Exception as e2:  # noqa: BLE001
+                _C_ERR = e2
+        else:
+            _C_ERR = e
+        raise RuntimeError(f"vgate native extension unavailable: {_C_ERR}") from _C_ERR
+    return _C
+
+
+def native_available() -> bool:
+    try:
+        native()
+        return True
+    except RuntimeError:
+        return False
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# ----------------------------------------------------------------------------- packing
+def pack_weight(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] -> fragment-major [N/16, K/32, 4, 16, 8] (see csrc/kernels/gemm.hip)."""
+    N, K = w.shape
+    assert N % 16 == 0 and K % 32 == 0, (N, K)
+    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+
+
+def unpack_weight(wp: torch.Tensor, N: int, K: int) -> torch.Tensor:
+    return wp.reshape(N // 16, K // 32, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(N, K)
+
+
+def interleave_gate_up(w_gate: torch.Tensor, w_up: torch.Tensor) -> torch.Tensor:
+    """Rows ordered [G0 U0 G1 U1 ...] in 16-row tiles for the fused SiLU*mul epilogue."""
+    I, K = w_gate.shape
+    assert I % 16 == 0
+    return torch.stack([w_gate.reshape(I // 16, 16, K), w_up.reshape(I // 16, 16, K)], 1).reshape(2 * I, K)
+
+
+def pack_awq(qint: torch.Tensor) -> torch.Tensor:
+    """int4 values [N, K] (0..15) -> int32 [N/16, K/128, 64, 4]; word u of lane l holds
+    W[16nt + (l&15)][128kq + 32u + 8(l>>4) + j] in nibble j."""
+    N, K = qint.shape
+    assert N % 16 == 0 and K % 128 == 0
+    q = qint.to(torch.int64).reshape(N // 16, 16, K // 128, 4, 4, 8)  # nt, r, kq, u, g, j
+    q = q.permute(0, 2, 4, 1, 3, 5)  # nt, kq, g, r, u, j  -> lane = g*16 + r
+    shifts = (torch.arange(8, dtype=torch.int64) * 4)
+    words = (q << shifts).sum(-1)  # [nt, kq, g, r, u]
+    words = words.reshape(N // 16, K // 128, 64, 4)
+    words = torch.where(words >= 2**31, words - 2**32, words)
+    return words.to(torch.int32).contiguous()
+
+
+class Linear:
+    """A linear layer's weights in kernel-ready form.
+
+    kind: "plain" | "silu" (rows are [gate; up], output is silu(gate) * up) | "awq".
+    On GPU the weight is stored fragment-packed only (no second copy); on CPU the
+    plain [N, K] matrix is kept for the reference path.
+    """
+
+    def __init__(self, w: torch.Tensor | None, bias: torch.Tensor | None = None, kind: str = "plain",
+                 awq: dict | None = None):
+        self.kind = kind
+        self.bias = bias
+        if kind == "awq":
+            assert awq is not None
+            self.N, self.K = awq["qint"].shape
+            self.group = awq["group"]
+            self.awq_epi_silu = awq.get("silu", False)
+            dev = awq["scales"].device
+            if dev.type == "cuda":
+                self.qw = pack_awq(awq["qint"].cpu()).to(dev)
+                self.scales = awq["scales"].to(torch.bfloat16).contiguous()
+                self.zeros = (awq["scales"].float() * awq["zeros"].float()).to(torch.bfloat16).contiguous()
+                self.w = None
+            else:
+                w_full = ref.awq_dequant_ref(awq["qint"], awq["scales"], awq["zeros"], self.group)
+                self.w = w_full
+            self.wp = None
+            return
+        self.N, self.K = w.shape
+        if kind == "silu":
+            I = self.N // 2
+            w = interleave_gate_up(w[:I], w[I:])
+        if w.is_cuda:
+            self.wp = pack_weight(w)
+            self.w = None
+        else:
+            self.wp = None
+            self.w = w
+
+    @property
+    def out_features(self) -> int:
+        if self.kind == "silu" or (self.kind == "awq" and self.awq_epi_silu):
+            return self.N // 2
+        return self.N
+
+    def dense_weight(self) -> torch.Tensor:
+        """[N, K] in the ORIGINAL row order (for references / checkpoint export)."""
+        if self.kind == "awq":
+            raise NotImplementedError
+        w = self.w if self.w is not None else unpack_weight(self.wp, self.N, self.K)
+        if self.kind == "silu":
+            I = self.N // 2
+            t = w.reshape(I // 16, 2, 16, self.K)
+            w = torch.cat([t[:, 0].reshape(I, self.K), t[:, 1].reshape(I, self.K)], 0)
+        return w
+
+    def nbytes(self) -> int:
+        if self.kind == "awq":
+            if self.w is not None:
+                return self.w.numel() * 2
+            return self.qw.numel() * 4 + self.scales.numel() * 4
+        t = self.wp if self.wp is not None else self.w
+        return t.numel() * t.element_size()
+
+
+def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
+           residual: torch.Tensor | None = None, out_f32: bool = False, waves: int = 0) -> torch.Tensor:
+    """out = epi(x @ W^T). x: [M, K] bf16 (row stride allowed)."""
+    M = x.shape[0]
+    silu = lin.kind == "silu" or (lin.kind == "awq" and lin.awq_epi_silu)
+    ncols = lin.N // 2 if silu else lin.N
+    if out is None:
+        out = torch.empty(M, ncols, dtype=torch.float32 if out_f32 else torch.bfloat16, device=x.device)
+    if not _gpu(x):
+        w = lin.w if lin.kind != "silu" else lin.dense_weight()
+        if silu:
+            I = lin.N // 2
+            if lin.kind == "silu":
+                wd = lin.dense_weight()
+            else:
+                wd = lin.w
+            out.copy_(ref.silu_mul_linear_ref(x, wd[:I], wd[I:]))
+        else:
+            out.copy_(ref.linear_ref(x, w, lin.bias, residual, out_f32))
+        return out
+    C = native()
+    epi = 2 if silu else (1 if out_f32 else 0)
+    if lin.kind == "awq":
+        C.awq_gemm(x, lin.qw, lin.scales, lin.zeros, lin.group, lin.N, lin.K, lin.bias, residual, out, epi)
+    else:
+        C.gemm(x, lin.wp, lin.N, lin.K, lin.bias, residual, out, epi, waves)
+    return out
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor | None = None,
+            out: torch.Tensor | None = None) -> torch.Tensor:
+    """y = RMSNorm(x [+ residual]) * w; when residual is given it is updated in place to x + residual."""
+    if out is None:
+        out = torch.empty_like(x)
+    if not _gpu(x):
+        y, s = ref.rmsnorm_ref(x, w, eps, residual)
+        if residual is not None:
+            residual.copy_(s)
+        out.copy_(y)
+        return out
+    native().rmsnorm(x, residual, w, out, eps)
+    return out
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None, vstart: int = 0):
+    if out is None:
+        out = torch.empty(ids.numel(), table.shape[1], dtype=table.dtype, device=table.device)
+    if not _gpu(table):
+        out.copy_(ref.embedding_ref(ids, table, vstart))
+        return out
+    native().embedding(ids, table, out, vstart)
+    return out
+
+
+def rope_kv(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq: int, Hkv: int, D: int) -> None:
+    if not _gpu(qkv):
+        ref.rope_kv_ref(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D)
+        return
+    native().rope_kv(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D)
+
+
+def attention_decode(q, q_stride, k_cache, v_cache, block_tables, context_lens, out, part_o, part_ml,
+                     Hq: int, Hkv: int, part_size: int, scale: float, query_start=None):
+    """One query token per sequence. q rows index = sequence (or query_start[s+1]-1)."""
+    if not _gpu(q):
+        S = context_lens.numel()
+        if query_start is None:
+            qs = torch.arange(S + 1, dtype=torch.int32)
+        else:
+            qs = query_start
+        # reference wants only the decode rows
+        rows = (qs[1:] - 1).long()
+        D = k_cache.shape[-1]
+        qq = q.view(q.shape[0], -1)[rows, : Hq * D].reshape(S, Hq, D)
+        o = ref.attention_ref(qq, k_cache, v_cache, block_tables, context_lens,
+                              torch.arange(S + 1, dtype=torch.int32), Hq, Hkv, scale)
+        out.view(out.shape[0], Hq, D)[rows] = o
+        return out
+    native().attn_decode(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start, out,
+                         part_o, part_ml, Hq, Hkv, part_size, scale)
+    return out
+
+
+def prefill_tiles(query_lens: list[int]) -> tuple[list[int], list[int]]:
+    seq, q0 = [], []
+    for s, ql in enumerate(query_lens):
+        for t in range(0, ql, 16):
+            seq.append(s)
+            q0.append(t)
+    return seq, q0
+
+
+def attention_prefill(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start,
+                      tile_seq, tile_q0, out, Hq: int, Hkv: int, scale: float):
+    if not _gpu(q):
+        D = k_cache.shape[-1]
+        T = q.shape[0]
+        qq = q.view(T, -1)[:, : Hq * D].reshape(T, Hq, D)
+        o = ref.attention_ref(qq, k_cache, v_cache, block_tables, context_lens, query_start, Hq, Hkv, scale)
+        out.view(T, Hq, D).copy_(o)
+        return out
+    native().attn_prefill(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start,
+                          tile_seq, tile_q0, out, Hq, Hkv, scale)
+    return out
+
+
+def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, offsets=None,
+           out=None, out_logprob=None, generators=None):
+    B = logits.shape[0]
+    if out is None:
+        out = torch.empty(B, dtype=torch.int32, device=logits.device)
+    if not _gpu(logits):
+        out.copy_(ref.sample_ref(logits, temperature, top_p, top_k, generators))
+        return out
+    native().sample(logits, temperature, top_p, top_k, seeds, offsets, out, out_logprob)
+    return out
+
+
+def softmax_scale(head_dim: int) -> float:
+    return 1.0 / math.sqrt(head_dim)
+
+
+__all__ = [
+    "native", "native_available", "pack_weight", "unpack_weight", "interleave_gate_up", "pack_awq",
+    "Linear", "linear", "rmsnorm", "embedding", "rope_kv", "attention_decode", "attention_prefill",
+    "prefill_tiles", "sample", "softmax_scale", "ref",
+]

@@ -1,0 +1,117 @@
+"""Tensor-parallel process group: one process per GPU, RCCL over xGMI.
+
+``torch.distributed`` with backend ``"nccl"`` IS RCCL on ROCm. The model calls
+only two collectives per transformer layer (after the row-parallel o_proj and
+down_proj) plus one all-reduce after the vocab-parallel embedding and one
+all-gather of the vocab-sharded logits — the Megatron layout of SURVEY.md §2.3.1.
+
+Small decode-sized all-reduces (<= ``custom_ar_max_bytes``) go to the custom
+one-shot xGMI kernel (:mod:`vgate.parallel.custom_allreduce`) when it is
+available (all ranks on one node with peer access); larger ones, and every
+collective under the gloo backend (CPU tests), go through torch.distributed.
+All collectives issue on the current stream, so they are hipGraph-capturable.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class TPGroup:
+    rank: int = 0
+    size: int = 1
+    group: object = None
+    backend: str = "none"
+    custom_ar: object = None
+
+    @property
+    def is_first(self) -> bool:
+        return self.rank == 0
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum over the TP group."""
+        if self.size == 1:
+            return t
+        if self.custom_ar is not None and self.custom_ar.should_use(t):
+            return self.custom_ar.all_reduce(t)
+        if self.backend == "gloo" and t.dtype in (torch.bfloat16, torch.float16):
+            f = t.float()
+            dist.all_reduce(f, group=self.group)
+            t.copy_(f)
+            return t
+        dist.all_reduce(t, group=self.group)
+        return t
+
+    def all_gather_lastdim(self, t: torch.Tensor) -> torch.Tensor:
+        """[..., n] per rank -> [..., n * size] concatenated in rank order."""
+        if self.size == 1:
+            return t
+        t = t.contiguous()
+        out = torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        if self.backend == "gloo":
+            parts = list(out.unbind(0))
+            dist.all_gather(parts, t, group=self.group)
+        else:
+            dist.all_gather_into_tensor(out, t, group=self.group)
+        return out.movedim(0, -2).reshape(*t.shape[:-1], self.size * t.shape[-1])
+
+    def broadcast_object(self, obj, src: int = 0):
+        if self.size == 1:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=src, group=self.group)
+        return lst[0]
+
+    def barrier(self):
+        if self.size > 1:
+            dist.barrier(group=self.group)
+
+
+_TP: TPGroup | None = None
+
+
+def init_tp(tp_size: int, backend: str | None = None) -> TPGroup:
+    """Initialise (or return) the TP group from torchrun-style env vars.
+
+    With tp_size == 1 no process group is created. With tp_size > 1 the caller
+    must have launched ``tp_size`` processes (torchrun) with RANK/WORLD_SIZE/
+    MASTER_ADDR/MASTER_PORT set; LOCAL_RANK selects the GPU.
+    """
+    global _TP
+    if _TP is not None and _TP.size == tp_size:
+        return _TP
+    if tp_size == 1:
+        _TP = TPGroup()
+        return _TP
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend=backend)
+    world = dist.get_world_size()
+    rank = dist.get_rank()
+    if world % tp_size:
+        raise ValueError(f"world size {world} not divisible by tp {tp_size}")
+    # contiguous TP groups: ranks [k*tp, (k+1)*tp)
+    grp = None
+    for k in range(world // tp_size):
+        ranks = list(range(k * tp_size, (k + 1) * tp_size))
+        g = dist.new_group(ranks, backend=backend) if world != tp_size else dist.group.WORLD
+        if rank in ranks:
+            grp = g
+    _TP = TPGroup(rank=rank % tp_size, size=tp_size, group=grp, backend=backend)
+    return _TP
+
+
+def get_tp() -> TPGroup:
+    return _TP if _TP is not None else TPGroup()
+
+
+def shard_range(n: int, rank: int, size: int) -> tuple[int, int]:
+    assert n % size == 0, f"{n} not divisible by tp={size}"
+    per = n // size
+    return rank * per, (rank + 1) * per
