@@ -82,7 +82,7 @@ def pack_awq(qint: torch.Tensor) -> torch.Tensor:
     assert N % 16 == 0 and K % 128 == 0
     q = qint.to(torch.int64).reshape(N // 16, 16, K // 128, 4, 4, 8)  # nt, r, kq, u, g, j
     q = q.permute(0, 2, 4, 1, 3, 5)  # nt, kq, g, r, u, j  -> lane = g*16 + r
-    shifts = (torch.arange(8, dtype=torch.int64) * 4)
+    shifts = (torch.arange(8, dtype=torch.int64, device=qint.device) * 4)
     words = (q << shifts).sum(-1)  # [nt, kq, g, r, u]
     words = words.reshape(N // 16, K // 128, 64, 4)
     words = torch.where(words >= 2**31, words - 2**32, words)
@@ -108,7 +108,7 @@ class Linear:
             self.awq_epi_silu = awq.get("silu", False)
             dev = awq["scales"].device
             if dev.type == "cuda":
-                self.qw = pack_awq(awq["qint"].cpu()).to(dev)
+                self.qw = pack_awq(awq["qint"].to(dev))
                 self.scales = awq["scales"].to(torch.bfloat16).contiguous()
                 self.zeros = (awq["scales"].float() * awq["zeros"].float()).to(torch.bfloat16).contiguous()
                 self.w = None

@@ -1,0 +1,412 @@
+"""The native LLM engine: one background thread driving schedule -> execute -> emit.
+
+Thread model: the HTTP event loop only enqueues requests (``add_request``) and
+receives results through per-request callbacks (the backend marshals them onto
+its asyncio loop); the engine thread owns the scheduler, KV manager and GPU.
+No executor thread is held per request — this removes the reference's
+thread-pool ceiling by construction.
+
+Tensor parallelism: TP rank 0 runs the scheduler; followers run
+:meth:`LLMEngine.follower_loop`, receiving each step's metadata buffer by an
+RCCL broadcast (device to device) and replaying the same hipGraph bucket, so all
+ranks stay in lock-step without any Python object traffic on the hot path.
+"""
+from __future__ import annotations
+
+import collections
+import logging
+import os
+import threading
+import time
+import zlib
+from dataclasses import dataclass, field
+
+import torch
+
+from vgate.models.config import resolve_arch
+from vgate.models.transformer import DecoderModel
+from vgate.parallel.comm import TPGroup, init_tp
+from vgate.runtime.kv_cache import BLOCK_SIZE, KVCacheManager, allocate_kv_tensors
+from vgate.runtime.model_runner import ModelRunner
+from vgate.runtime.sampling_params import SamplingParams
+from vgate.runtime.scheduler import Scheduler
+from vgate.runtime.sequence import Sequence, SeqStatus
+from vgate.runtime.tokenizer import IncrementalDecoder, load_tokenizer
+
+log = logging.getLogger("vgate.engine")
+
+
+@dataclass
+class EngineConfig:
+    model: str = "Qwen/Qwen2.5-1.5B-Instruct"
+    weights_path: str | None = None
+    tokenizer: str | None = None
+    quantization: str | None = None
+    dtype: str = "bfloat16"
+    device: str = "auto"
+    tensor_parallel_size: int = 1
+    max_model_len: int = 2048
+    max_num_seqs: int = 256
+    max_num_batched_tokens: int = 2048
+    gpu_memory_utilization: float = 0.7
+    num_kv_blocks: int | None = None
+    enforce_eager: bool = False
+    enable_prefix_caching: bool = True
+    seed: int = 0
+    block_size: int = BLOCK_SIZE
+    part_size: int = 512
+    graph_token_buckets: list[int] | None = None
+    warmup: bool = True
+    arch_overrides: dict | None = None
+
+    def resolve_device(self) -> torch.device:
+        if self.device != "auto":
+            d = torch.device(self.device)
+            if d.type == "cuda" and d.index is None:
+                d = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
+            return d
+        if torch.cuda.is_available():
+            local = int(os.environ.get("LOCAL_RANK", "0"))
+            return torch.device("cuda", local % max(1, torch.cuda.device_count()))
+        return torch.device("cpu")
+
+
+@dataclass
+class EngineStats:
+    steps: int = 0
+    tokens_generated: int = 0
+    prompt_tokens: int = 0
+    prefill_tokens: int = 0
+    decode_tokens: int = 0
+    step_time_s: float = 0.0
+    requests_finished: int = 0
+    last_step_ms: float = 0.0
+    batch_sizes: collections.Counter = field(default_factory=collections.Counter)
+
+
+class LLMEngine:
+    def __init__(self, cfg: EngineConfig, tp: TPGroup | None = None):
+        self.cfg = cfg
+        self.device = cfg.resolve_device()
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        self.tp = tp or (init_tp(cfg.tensor_parallel_size) if cfg.tensor_parallel_size > 1 else TPGroup())
+        weights = cfg.weights_path
+        if weights is None and os.path.isdir(os.path.expanduser(cfg.model)):
+            weights = os.path.expanduser(cfg.model)
+        self.arch = resolve_arch(cfg.model, cfg.arch_overrides)
+        t0 = time.perf_counter()
+        self.model = DecoderModel(self.arch, self.device, self.tp, cfg.quantization, cfg.seed, weights,
+                                  cfg.max_model_len)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+        self.load_seconds = time.perf_counter() - t0
+        self.num_blocks = self._size_kv()
+        self.kv_caches = allocate_kv_tensors(self.arch.num_layers, self.num_blocks, self.model.num_kv_heads_local,
+                                             self.arch.head_dim, self.device, block_size=cfg.block_size)
+        self.kvm = KVCacheManager(self.num_blocks, cfg.block_size, cfg.enable_prefix_caching)
+        self.scheduler = Scheduler(self.kvm, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len)
+        self.runner = ModelRunner(self.model, self.kv_caches, cfg.max_num_seqs, cfg.max_num_batched_tokens,
+                                  cfg.max_model_len, cfg.block_size, cfg.enforce_eager, cfg.part_size,
+                                  cfg.graph_token_buckets)
+        self.tokenizer = load_tokenizer(weights, cfg.tokenizer, self.arch)
+        self.stats = EngineStats()
+        self._inbox: collections.deque = collections.deque()
+        self._aborts: collections.deque = collections.deque()
+        self._cv = threading.Condition()
+        self._running = False
+        self._thread: threading.Thread | None = None
+        self._by_id: dict[str, Sequence] = {}
+        self._seq_counter = 0
+        self.healthy = True
+        self.last_error: str | None = None
+        self.last_step_wall = time.monotonic()
+        log.info("engine ready: model=%s params=%.2fB weights=%.2f GB load=%.1fs kv_blocks=%d (%.1fk tokens) device=%s tp=%d",
+                 self.arch.name, self.arch.num_params() / 1e9, self.model.weight_bytes() / 1e9, self.load_seconds,
+                 self.num_blocks, self.num_blocks * cfg.block_size / 1e3, self.device, self.tp.size)
+
+    # ------------------------------------------------------------------ sizing
+    def _size_kv(self) -> int:
+        cfg = self.cfg
+        per_block = 2 * self.arch.num_layers * self.model.num_kv_heads_local * cfg.block_size * self.arch.head_dim * 2
+        max_useful = cfg.max_num_seqs * ((cfg.max_model_len + cfg.block_size - 1) // cfg.block_size) * 2 + 64
+        if cfg.num_kv_blocks:
+            n = cfg.num_kv_blocks
+        elif self.device.type == "cuda":
+            free, total = torch.cuda.mem_get_info(self.device)
+            reserve = 4 * 2**30 + cfg.max_num_seqs * self.arch.vocab_size * 12
+            budget = cfg.gpu_memory_utilization * total - (total - free) - reserve
+            n = int(max(0, budget) // per_block)
+            n = min(n, max_useful)
+        else:
+            n = min(max_useful, 4096)
+        if self.tp.size > 1:  # identical pool on every rank
+            t = torch.tensor([n], device=self.device if self.tp.backend == "nccl" else "cpu")
+            import torch.distributed as dist
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.tp.group)
+            n = int(t.item())
+        if n < (1 if cfg.num_kv_blocks else 16):
+            raise RuntimeError(f"not enough memory for the KV cache ({n} blocks)")
+        return n
+
+    # --------------------------------------------------------------- lifecycle
+    def start(self) -> None:
+        if self._running:
+            return
+        if self.cfg.warmup and self.runner.use_graphs:
+            secs = self.runner.warmup([1, 2, 4, 8, 16], [1, 2, 4, 8])
+            log.info("pre-captured %d hipGraphs in %.2fs", len(self.runner.graphs), secs)
+        self._running = True
+        self._thread = threading.Thread(target=self._loop, name="vgate-engine", daemon=True)
+        self._thread.start()
+
+    def stop(self) -> None:
+        self._running = False
+        with self._cv:
+            self._cv.notify_all()
+        if self._thread is not None:
+            self._thread.join(timeout=30)
+            self._thread = None
+
+    # ------------------------------------------------------------------- input
+    def add_request(self, request_id: str, prompt: str | None = None, params: SamplingParams | None = None,
+                    callback=None, stream: bool = False, prompt_ids: list[int] | None = None) -> Sequence:
+        params = params or SamplingParams()
+        if prompt_ids is None:
+            prompt_ids = self.tokenizer.encode(prompt or "")
+        if not prompt_ids:
+            prompt_ids = [self.arch.bos_token_id]
+        if len(prompt_ids) >= self.cfg.max_model_len:
+            prompt_ids = prompt_ids[-(self.cfg.max_model_len - 1):]
+        seq = Sequence(request_id=request_id, prompt_ids=list(prompt_ids), params=params, callback=callback,
+                       stream=stream)
+        seq.seed = params.seed if params.seed is not None else \
+            (self.cfg.seed * 1000003 + zlib.crc32(request_id.encode())) & 0x7FFFFFFFFFFFFFFF
+        if stream:
+            seq.detok = IncrementalDecoder(self.tokenizer)
+        with self._cv:
+            self._inbox.append(seq)
+            self._cv.notify()
+        return seq
+
+    def abort(self, request_id: str) -> None:
+        with self._cv:
+            self._aborts.append(request_id)
+            self._cv.notify()
+
+    def has_unfinished(self) -> bool:
+        return bool(self._inbox) or self.scheduler.has_work()
+
+    # -------------------------------------------------------------------- loop
+    def _drain_inbox(self) -> None:
+        while self._inbox:
+            seq = self._inbox.popleft()
+            self._by_id[seq.request_id] = seq
+            self.scheduler.add(seq)
+        while self._aborts:
+            rid = self._aborts.popleft()
+            seq = self._by_id.get(rid)
+            if seq is not None and not seq.is_finished:
+                self.scheduler.remove(seq)
+                seq.aborted = True
+                self._finish(seq, "abort", notify_sched=False)
+
+    def _loop(self) -> None:
+        torch.set_grad_enabled(False)
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        while self._running:
+            with self._cv:
+                while self._running and not self._inbox and not self._aborts and not self.scheduler.has_work():
+                    self._cv.wait(timeout=0.5)
+                if not self._running:
+                    break
+                self._drain_inbox()
+            try:
+                self.step()
+            except Exception as e:  # noqa: BLE001 - engine faults fail every in-flight request
+                log.exception("engine step failed")
+                self.healthy = False
+                self.last_error = f"{type(e).__name__}: {e}"
+                for seq in list(self.scheduler.running) + list(self.scheduler.waiting):
+                    self.scheduler.remove(seq)
+                    self._finish(seq, "error", notify_sched=False, error=self.last_error)
+        if self.tp.size > 1 and self.tp.is_first:
+            self._broadcast_header(-1, 0, 0)
+
+    def run_until_idle(self, max_steps: int = 1_000_000) -> None:
+        """Synchronous driver (tests / offline use): process everything queued."""
+        self._drain_inbox()
+        n = 0
+        while self.scheduler.has_work() and n < max_steps:
+            self.step()
+            self._drain_inbox()
+            n += 1
+
+    # -------------------------------------------------------------------- step
+    def step(self) -> int:
+        batch = self.scheduler.schedule()
+        if batch.empty:
+            return 0
+        t0 = time.perf_counter()
+        if self.tp.size > 1:
+            toks, samples = self._execute_tp(batch)
+        else:
+            toks, samples = self.runner.execute(batch)
+        now = time.perf_counter()
+        st = self.stats
+        st.steps += 1
+        st.step_time_s += now - t0
+        st.last_step_ms = 1e3 * (now - t0)
+        st.prefill_tokens += batch.num_prefill_tokens
+        st.decode_tokens += batch.num_decode
+        st.batch_sizes[len(batch.items)] += 1
+        self.last_step_wall = time.monotonic()
+        eos = set(self.arch.eos_token_ids)
+        for (seq, n), tok, smp in zip(batch.items, toks, samples):
+            seq.num_computed += n
+            self.kvm.register_computed(seq)
+            if not smp or seq.is_finished:
+                continue
+            seq.output_ids.append(tok)
+            st.tokens_generated += 1
+            if seq.first_token_time is None:
+                seq.first_token_time = now
+            seq.last_token_time = now
+            sp = seq.params
+            nout = len(seq.output_ids)
+            reason = None
+            if not sp.ignore_eos and tok in eos and nout >= sp.min_tokens:
+                reason = "stop"
+            elif tok in sp.stop_token_ids and nout >= sp.min_tokens:
+                reason = "stop"
+            elif nout >= sp.max_tokens:
+                reason = "length"
+            elif seq.total_len >= self.cfg.max_model_len:
+                reason = "length"
+            delta = ""
+            if seq.stream and seq.detok is not None:
+                delta = seq.detok.push(tok) if reason != "stop" or tok not in eos else ""
+                seq.text += delta
+            if sp.stop and reason is None:
+                text = seq.text if seq.stream else self.tokenizer.decode(seq.output_ids)
+                for s in sp.stop:
+                    if s and s in text:
+                        reason = "stop"
+                        break
+            if seq.stream and seq.callback is not None and delta:
+                seq.callback("token", seq, delta)
+            if reason is not None:
+                self._finish(seq, reason)
+        return len(batch.items)
+
+    def _finish(self, seq: Sequence, reason: str, notify_sched: bool = True, error: str | None = None) -> None:
+        if notify_sched:
+            self.scheduler.finish(seq, reason)
+        else:
+            seq.status = SeqStatus.FINISHED
+            seq.finish_reason = reason
+        seq.finish_time = time.perf_counter()
+        self._by_id.pop(seq.request_id, None)
+        self.stats.requests_finished += 1
+        self.stats.prompt_tokens += len(seq.prompt_ids)
+        if seq.stream and seq.detok is not None:
+            tail = seq.detok.flush()
+            if tail:
+                seq.text += tail
+                if seq.callback is not None:
+                    seq.callback("token", seq, tail)
+        elif not seq.stream:
+            out = seq.output_ids
+            if reason == "stop" and out and out[-1] in self.arch.eos_token_ids:
+                out = out[:-1]
+            seq.text = self.tokenizer.decode(out)
+        if seq.callback is not None:
+            seq.callback("error" if error else "finish", seq, error)
+
+    # ----------------------------------------------------------- tensor parallel
+    def _broadcast_header(self, T: int, S: int, ns: int) -> None:
+        import torch.distributed as dist
+        hdr = torch.tensor([T, S, ns], dtype=torch.int64,
+                           device=self.device if self.tp.backend == "nccl" else "cpu")
+        dist.broadcast(hdr, src=self._tp_src(), group=self.tp.group)
+
+    def _tp_src(self) -> int:
+        import torch.distributed as dist
+        return dist.get_global_rank(self.tp.group, 0) if self.tp.group is not None else 0
+
+    def _execute_tp(self, batch):
+        """Rank-0 side: run the step locally after shipping its metadata to the followers."""
+        import torch.distributed as dist
+        r = self.runner
+        ns, nt = len(batch.items), batch.num_tokens
+        T = r._bucket(r.t_buckets, nt) if r.gpu else nt
+        S = r._bucket(r.s_buckets, ns) if r.gpu else ns
+        samples = r._fill(batch, T, S)
+        r.meta.upload(ns)
+        self._broadcast_header(T, S, ns)
+        n = r.meta.used_bytes(ns)
+        dist.broadcast(r.meta.dev[:n], src=self._tp_src(), group=self.tp.group)
+        toks = self._run_step(T, S, ns, nt)
+        return toks, samples
+
+    def _run_step(self, T, S, ns, nt):
+        r = self.runner
+        if r.use_graphs:
+            g = r.graphs.get((T, S))
+            if g is None:
+                g = r._capture(T, S)
+                r.graphs[(T, S)] = g
+            g.replay()
+        else:
+            view = r.meta.view(T, S)
+            view.num_tokens, view.num_seqs = nt, ns
+            if r.gpu:
+                r._forward_sample(view)
+            else:
+                logits = self.model.forward(view, self.kv_caches, r.part_size)
+                r.out_tokens[:S] = logits.argmax(-1).int()  # CPU TP path is greedy-only (tests)
+        if r.gpu:
+            r.out_host[:ns].copy_(r.out_tokens[:ns], non_blocking=True)
+            r.done.record()
+            r.done.synchronize()
+            return r.out_host[:ns].tolist()
+        return r.out_tokens[:ns].tolist()
+
+    def follower_loop(self) -> None:
+        """TP ranks > 0: execute whatever rank 0 schedules, until it broadcasts T < 0."""
+        import torch.distributed as dist
+        torch.set_grad_enabled(False)
+        r = self.runner
+        while True:
+            hdr = torch.zeros(3, dtype=torch.int64, device=self.device if self.tp.backend == "nccl" else "cpu")
+            dist.broadcast(hdr, src=self._tp_src(), group=self.tp.group)
+            T, S, ns = (int(v) for v in hdr.tolist())
+            if T < 0:
+                return
+            n = r.meta.used_bytes(ns)
+            buf = r.meta.dev[:n]
+            dist.broadcast(buf, src=self._tp_src(), group=self.tp.group)
+            if not r.gpu:
+                r.meta.host[:n].copy_(buf)
+            nt = int(r.meta.h["query_start"][ns]) if not r.gpu else 0
+            self._run_step(T, S, ns, nt)
+
+    def shutdown_followers(self) -> None:
+        if self.tp.size > 1 and self.tp.is_first:
+            self._broadcast_header(-1, 0, 0)
+
+    # ------------------------------------------------------------------- stats
+    def snapshot(self) -> dict:
+        st = self.stats
+        return {
+            "model": self.arch.name, "device": str(self.device), "tp": self.tp.size,
+            "running": len(self.scheduler.running), "waiting": len(self.scheduler.waiting),
+            "kv_blocks_total": self.num_blocks, "kv_blocks_free": self.kvm.num_free(),
+            "kv_usage": round(self.kvm.usage(), 4), "steps": st.steps, "tokens_generated": st.tokens_generated,
+            "prefill_tokens": st.prefill_tokens, "decode_tokens": st.decode_tokens,
+            "avg_step_ms": round(1e3 * st.step_time_s / max(1, st.steps), 3),
+            "graphs_captured": len(self.runner.graphs), "graph_hits": self.runner.graph_hits,
+            "preemptions": self.scheduler.num_preemptions, "prefix_cache_hits": int(getattr(self.kvm.alloc, "hits", 0)),
+            "healthy": self.healthy,
+        }

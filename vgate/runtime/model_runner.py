@@ -1,0 +1,229 @@
+"""Executes scheduled batches on the model: metadata build, hipGraph replay, sampling.
+
+Graph strategy (MI355X-first, no tracing compiler): every step — decode-only,
+prefill-only or mixed — is padded to a (token bucket T, sequence bucket S) and
+replayed from a hipGraph captured on first use (``torch.cuda.graph`` records the
+HIP stream: every kernel launch of the forward plus the sampler). All dynamic
+inputs live in :class:`StepMeta` device buffers, so a replay costs one H2D copy,
+one graph launch and one D2H copy of the sampled token ids. ``enforce_eager``
+(or a CPU device) runs the same code without capture.
+"""
+from __future__ import annotations
+
+import bisect
+import logging
+import time
+
+import numpy as np
+import torch
+
+from vgate import ops
+from vgate.runtime.scheduler import ScheduledBatch
+from vgate.runtime.step_meta import StepMeta
+
+log = logging.getLogger("vgate.engine")
+
+DEFAULT_T_BUCKETS = [1, 2, 4, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256, 384, 512, 768, 1024, 1536, 2048,
+                     3072, 4096, 6144, 8192, 12288, 16384]
+DEFAULT_S_BUCKETS = [1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024]
+
+
+class ModelRunner:
+    def __init__(self, model, kv_caches, max_num_seqs: int, max_num_batched_tokens: int, max_model_len: int,
+                 block_size: int = 16, enforce_eager: bool = False, part_size: int = 512,
+                 graph_token_buckets: list[int] | None = None):
+        self.model = model
+        self.kv = kv_caches
+        self.device = model.device
+        self.gpu = self.device.type == "cuda"
+        self.block_size = block_size
+        self.max_blocks = (max_model_len + block_size - 1) // block_size
+        self.part_size = part_size
+        tb = [b for b in (graph_token_buckets or DEFAULT_T_BUCKETS) if b < max_num_batched_tokens]
+        self.t_buckets = sorted(set(tb + [max_num_batched_tokens]))
+        sb = [b for b in DEFAULT_S_BUCKETS if b < max_num_seqs]
+        self.s_buckets = sorted(set(sb + [max_num_seqs]))
+        self.max_tokens = self.t_buckets[-1]
+        self.max_seqs = max_num_seqs
+        self.meta = StepMeta(self.max_tokens, self.max_seqs, self.max_blocks, self.device)
+        self.use_graphs = self.gpu and not enforce_eager
+        self.graphs: dict[tuple[int, int], tuple] = {}
+        self.pool = None
+        self.out_tokens = torch.zeros(self.max_seqs, dtype=torch.int32, device=self.device)
+        if self.gpu:
+            self.out_host = torch.zeros(self.max_seqs, dtype=torch.int32, pin_memory=True)
+            self.stream = torch.cuda.Stream(self.device)
+            self.done = torch.cuda.Event()
+        else:
+            self.out_host = self.out_tokens
+        self.graph_hits = 0
+        self.graph_misses = 0
+        self.capture_seconds = 0.0
+
+    # ----------------------------------------------------------------- buckets
+    def _bucket(self, buckets, n):
+        i = bisect.bisect_left(buckets, n)
+        if i == len(buckets):
+            raise ValueError(f"{n} exceeds the largest bucket {buckets[-1]}")
+        return buckets[i]
+
+    # ---------------------------------------------------------------- metadata
+    def _fill(self, batch: ScheduledBatch, T: int, S: int) -> list[bool]:
+        m = self.meta
+        h = m.h
+        bs = self.block_size
+        ids, pos, slots = h["ids"], h["positions"], h["slots"]
+        qs, cl, sidx = h["query_start"], h["context_lens"], h["sample_idx"]
+        temp, topp, topk, seeds, offs = h["temperature"], h["top_p"], h["top_k"], h["seeds"], h["offsets"]
+        tseq, tq0 = h["tile_seq"], h["tile_q0"]
+        bt = m.bt_host
+        t = 0
+        ntile = 0
+        samples = []
+        qs[0] = 0
+        for s, (seq, n) in enumerate(batch.items):
+            c0 = seq.num_computed
+            toks = seq.all_ids[c0: c0 + n]
+            ids[t: t + n] = toks
+            p = np.arange(c0, c0 + n, dtype=np.int32)
+            pos[t: t + n] = p
+            blocks = np.asarray(seq.blocks, dtype=np.int32)
+            slots[t: t + n] = blocks[p // bs] * bs + (p % bs)
+            nb = len(seq.blocks)
+            bt[s, :nb] = blocks
+            ctx = c0 + n
+            cl[s] = ctx
+            t += n
+            qs[s + 1] = t
+            sidx[s] = t - 1
+            if n > 1:
+                for q0 in range(0, n, 16):
+                    tseq[ntile] = s
+                    tq0[ntile] = q0
+                    ntile += 1
+            sp = seq.params
+            temp[s] = 0.0 if sp.greedy else sp.temperature
+            topp[s] = sp.top_p
+            topk[s] = sp.top_k
+            seeds[s] = seq.seed
+            offs[s] = len(seq.output_ids)
+            samples.append(ctx == seq.total_len)
+        ns = len(batch.items)
+        # padding (graph bucket)
+        ids[t:T] = 0
+        pos[t:T] = 0
+        slots[t:T] = -1
+        qs[ns + 1: S + 1] = t
+        cl[ns:S] = 0
+        sidx[ns:S] = 0
+        temp[ns:S] = 0.0
+        topp[ns:S] = 1.0
+        topk[ns:S] = -1
+        tile_cap = T // 16 + S
+        if ntile > tile_cap:
+            raise RuntimeError("prefill tile overflow")
+        tseq[ntile:tile_cap] = -1
+        self._n_tok, self._n_seq = t, ns
+        return samples
+
+    # ----------------------------------------------------------------- forward
+    def _forward_sample(self, view):
+        logits = self.model.forward(view, self.kv, self.part_size)
+        ops.sample(logits, view.temperature, view.top_p, view.top_k, view.seeds, view.offsets,
+                   out=self.out_tokens[: view.S])
+        return logits
+
+    def _capture(self, T: int, S: int):
+        t0 = time.perf_counter()
+        view = self.meta.view(T, S)
+        # warm-up (eager) on the capture stream, then capture
+        s = self.stream
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._forward_sample(view)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        if self.pool is None:
+            self.pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(g, pool=self.pool, stream=s):
+            self._forward_sample(view)
+        torch.cuda.synchronize()
+        self.capture_seconds += time.perf_counter() - t0
+        log.debug("captured hipGraph T=%d S=%d in %.1f ms", T, S, 1e3 * (time.perf_counter() - t0))
+        return g
+
+    @torch.inference_mode()
+    def execute(self, batch: ScheduledBatch) -> tuple[list[int], list[bool]]:
+        """Run one step; returns (sampled token per item, whether the item consumes it)."""
+        ns = len(batch.items)
+        nt = batch.num_tokens
+        if self.gpu:
+            T = self._bucket(self.t_buckets, nt)
+            S = self._bucket(self.s_buckets, ns)
+        else:
+            T, S = nt, ns
+        samples = self._fill(batch, T, S)
+        self.meta.upload(ns)
+        if self.gpu:
+            if self.use_graphs:
+                key = (T, S)
+                g = self.graphs.get(key)
+                if g is None:
+                    self.graph_misses += 1
+                    g = self._capture(T, S)
+                    self.graphs[key] = g
+                    # the capture's warm-up/capture runs consumed the same metadata: replay for real
+                else:
+                    self.graph_hits += 1
+                g.replay()
+            else:
+                view = self.meta.view(T, S)
+                view.num_tokens, view.num_seqs = nt, ns
+                self._forward_sample(view)
+            self.out_host[:ns].copy_(self.out_tokens[:ns], non_blocking=True)
+            self.done.record()
+            self.done.synchronize()
+            toks = self.out_host[:ns].tolist()
+        else:
+            view = self.meta.view(T, S)
+            view.num_tokens, view.num_seqs = nt, ns
+            self._cpu_sample(view, batch)
+            toks = self.out_tokens[:ns].tolist()
+        return toks, samples
+
+    def _cpu_sample(self, view, batch):
+        logits = self.model.forward(view, self.kv, self.part_size)
+        gens = []
+        for seq, _ in batch.items:
+            g = torch.Generator()
+            g.manual_seed((seq.seed * 1000003 + len(seq.output_ids)) & 0x7FFFFFFFFFFFFFFF)
+            gens.append(g)
+        self.out_tokens[: view.S] = ops.ref.sample_ref(logits, view.temperature, view.top_p, view.top_k, gens)
+
+    def warmup(self, token_buckets: list[int] | None = None, seq_buckets: list[int] | None = None) -> float:
+        """Pre-capture graphs for the given buckets (all-padding metadata)."""
+        if not self.use_graphs:
+            return 0.0
+        t0 = time.perf_counter()
+        for T in token_buckets or []:
+            for S in seq_buckets or [1]:
+                if S > T or (T, S) in self.graphs:
+                    continue
+                self._fill_padding(T, S)
+                self.meta.upload(0)
+                self.graphs[(T, S)] = self._capture(T, S)
+        return time.perf_counter() - t0
+
+    def _fill_padding(self, T, S):
+        h = self.meta.h
+        h["ids"][:T] = 0
+        h["positions"][:T] = 0
+        h["slots"][:T] = -1
+        h["query_start"][: S + 1] = 0
+        h["context_lens"][:S] = 0
+        h["sample_idx"][:S] = 0
+        h["temperature"][:S] = 0
+        h["top_p"][:S] = 1
+        h["top_k"][:S] = -1
+        h["tile_seq"][: T // 16 + S] = -1

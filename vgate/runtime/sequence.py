@@ -1,0 +1,62 @@
+"""Request state inside the native engine."""
+from __future__ import annotations
+
+import enum
+import itertools
+import time
+from dataclasses import dataclass, field
+from typing import Callable
+
+from vgate.runtime.sampling_params import SamplingParams
+
+_ids = itertools.count()
+
+
+class SeqStatus(enum.Enum):
+    WAITING = 0
+    RUNNING = 1
+    FINISHED = 2
+
+
+@dataclass
+class Sequence:
+    request_id: str
+    prompt_ids: list[int]
+    params: SamplingParams
+    callback: Callable | None = None
+    stream: bool = False
+    seq_id: int = field(default_factory=lambda: next(_ids))
+    arrival: float = field(default_factory=time.perf_counter)
+    output_ids: list[int] = field(default_factory=list)
+    status: SeqStatus = SeqStatus.WAITING
+    blocks: list[int] = field(default_factory=list)
+    num_computed: int = 0
+    num_cached_prefix: int = 0
+    num_preemptions: int = 0
+    first_token_time: float | None = None
+    last_token_time: float | None = None
+    finish_time: float | None = None
+    finish_reason: str | None = None
+    seed: int = 0
+    text: str = ""
+    detok: object = None
+    hashed_blocks: int = 0
+    block_hashes: list[int] = field(default_factory=list)
+    aborted: bool = False
+
+    @property
+    def all_ids(self) -> list[int]:
+        return self.prompt_ids + self.output_ids if self.output_ids else self.prompt_ids
+
+    @property
+    def total_len(self) -> int:
+        return len(self.prompt_ids) + len(self.output_ids)
+
+    @property
+    def remaining(self) -> int:
+        """Tokens whose KV is not yet computed (>= 1 while running)."""
+        return self.total_len - self.num_computed
+
+    @property
+    def is_finished(self) -> bool:
+        return self.status == SeqStatus.FINISHED
