@@ -1,0 +1,195 @@
+"""Headline benchmark: req/s + p50/p99 end-to-end latency of ``POST /v1/chat/completions``
+(Qwen2.5-1.5B-Instruct architecture, bf16, random-init weights, synthetic unique
+prompts) at fixed client concurrency — the reference's published metric
+(6.47 req/s, p50 1.19 s, p99 1.53 s at concurrency 8, max_tokens 64).
+
+Every rank is one GPU running a full V-Gate stack (gateway + native engine) as a
+DP serving replica behind a real uvicorn HTTP server on 127.0.0.1; a closed-loop
+client in the same process keeps ``--concurrency`` requests in flight against it
+through the full path (HTTP -> security -> cache/dedup/admission -> engine ->
+JSON). One "step" = ``--requests-per-step`` requests (40 = the reference run).
+``value`` is the whole-job aggregate (sum over ranks of requests / max wall time).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import sys
+import time
+
+os.environ.setdefault("VGATE_LOGGING__LEVEL", "WARNING")
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+BASELINE_REQ_S = 6.47
+METRIC = "req/s + p50/p99 end-to-end latency, Qwen2.5-1.5B /v1/chat/completions at fixed concurrency"
+
+WORDS = ("the quick brown fox jumps over a lazy dog while engineers measure latency throughput memory "
+         "bandwidth kernels scheduling batching caching tokens requests gateway worker cluster").split()
+
+
+def make_prompt(rank: int, i: int) -> str:
+    # unique, ~24-word prompts (the reference load test used unique prompts: no cache hits)
+    h = (rank * 1_000_003 + i * 7919) & 0xFFFFFFFF
+    words = [WORDS[(h >> (k % 24)) % len(WORDS) ^ 0] if k % 3 else WORDS[(h + k * 31) % len(WORDS)] for k in range(22)]
+    return f"Request {rank}-{i}: " + " ".join(words) + "?"
+
+
+def pct(xs, p):
+    xs = sorted(xs)
+    return xs[min(int(len(xs) * p / 100), len(xs) - 1)] if xs else 0.0
+
+
+async def run_load(port: int, n: int, concurrency: int, max_tokens: int, rank: int, start_idx: int):
+    import aiohttp
+    lat, fails, tokens = [], 0, 0
+    sem = asyncio.Semaphore(concurrency)
+    url = f"http://127.0.0.1:{port}/v1/chat/completions"
+    conn = aiohttp.TCPConnector(limit=concurrency * 2)
+    timeout = aiohttp.ClientTimeout(total=300)
+    async with aiohttp.ClientSession(connector=conn, timeout=timeout) as s:
+        async def one(i):
+            nonlocal fails, tokens
+            async with sem:
+                body = {"model": "Qwen/Qwen2.5-1.5B-Instruct",
+                        "messages": [{"role": "user", "content": make_prompt(rank, start_idx + i)}],
+                        "max_tokens": max_tokens}
+                t0 = time.perf_counter()
+                try:
+                    async with s.post(url, json=body) as r:
+                        data = await r.json()
+                        if r.status != 200:
+                            fails += 1
+                        else:
+                            tokens += data["usage"]["completion_tokens"]
+                except Exception:  # noqa: BLE001
+                    fails += 1
+                lat.append(time.perf_counter() - t0)
+
+        t0 = time.perf_counter()
+        await asyncio.gather(*(one(i) for i in range(n)))
+        wall = time.perf_counter() - t0
+    return lat, fails, tokens, wall
+
+
+async def serve_and_bench(args, rank: int, world: int, dist_ok: bool):
+    import torch
+    import uvicorn
+
+    from vgate.api.app import create_app
+    from vgate.config import VGateConfig
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cfg = VGateConfig(
+        role="gateway",
+        model={"model_id": args.model, "quantization": args.quantization, "engine_type": "native",
+               "random_init": True, "max_model_len": 2048, "max_num_seqs": 256,
+               "max_num_batched_tokens": 2048, "num_kv_blocks": args.kv_blocks, "enforce_eager": args.eager,
+               "device": f"cuda:{local}" if torch.cuda.is_available() else "cpu", "seed": 1234 + rank},
+        batch={"max_batch_size": args.concurrency},
+        cache={"enabled": True, "maxsize": 1000},
+        logging={"level": "WARNING", "json_format": True},
+    )
+    app = create_app(cfg)
+    port = args.port + local
+    server = uvicorn.Server(uvicorn.Config(app, host="127.0.0.1", port=port, log_level="warning",
+                                           access_log=False, lifespan="on"))
+    srv_task = asyncio.create_task(server.serve())
+    t_boot = time.perf_counter()
+    while not server.started:
+        if srv_task.done():
+            srv_task.result()
+            raise RuntimeError("server exited during startup")
+        await asyncio.sleep(0.1)
+    boot_s = time.perf_counter() - t_boot
+
+    def barrier():
+        if dist_ok:
+            import torch.distributed as dist
+            dist.barrier()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    per_step = args.requests_per_step
+    # warmup (also captures the hipGraph buckets this load uses)
+    if args.warmup > 0:
+        await run_load(port, per_step * args.warmup, args.concurrency, args.max_tokens, rank, 10_000_000)
+    barrier()
+    t0 = time.perf_counter()
+    lat, fails, tokens, _ = await run_load(port, per_step * args.steps, args.concurrency, args.max_tokens, rank, 0)
+    barrier()
+    wall = time.perf_counter() - t0
+    eng = app.state.vgate.engine
+    snap = eng.backend.stats() if hasattr(eng.backend, "stats") else {}
+    server.should_exit = True
+    await srv_task
+    return {"lat": lat, "fails": fails, "tokens": tokens, "wall": wall, "boot_s": boot_s,
+            "n": per_step * args.steps, "engine": snap}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--concurrency", type=int, default=8)
+    ap.add_argument("--requests-per-step", type=int, default=40)
+    ap.add_argument("--max-tokens", type=int, default=64)
+    ap.add_argument("--model", default="Qwen/Qwen2.5-1.5B-Instruct")
+    ap.add_argument("--quantization", default=None)
+    ap.add_argument("--kv-blocks", type=int, default=4096)
+    ap.add_argument("--eager", action="store_true")
+    ap.add_argument("--port", type=int, default=18100)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    dist_ok = False
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")  # coordination only: replicas share no tensors
+        dist_ok = True
+    res = asyncio.run(serve_and_bench(args, rank, world, dist_ok))
+    if dist_ok:
+        import torch.distributed as dist
+        allr = [None] * world
+        dist.all_gather_object(allr, res)
+    else:
+        allr = [res]
+    if rank == 0:
+        lat = [x for r in allr for x in r["lat"]]
+        total = sum(r["n"] for r in allr)
+        wall = max(r["wall"] for r in allr)
+        value = total / wall
+        toks = sum(r["tokens"] for r in allr)
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "req/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * wall / args.steps, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": round(value / BASELINE_REQ_S, 3), "dtype": "bf16",
+            "data": "synthetic unique prompts, random-init weights (Qwen2.5-1.5B architecture)",
+            "config": {"model": "Qwen2.5-1.5B-Instruct", "global_batch": args.concurrency * world,
+                       "seq_len": args.max_tokens, "parallelism": f"dp{world}",
+                       "concurrency_per_gpu": args.concurrency, "max_tokens": args.max_tokens,
+                       "requests_per_step_per_gpu": args.requests_per_step},
+            "p50_s": round(pct(lat, 50), 4), "p99_s": round(pct(lat, 99), 4),
+            "mean_s": round(sum(lat) / max(1, len(lat)), 4),
+            "generated_tokens_per_s": round(toks / wall, 1),
+            "failures": sum(r["fails"] for r in allr),
+            "engine_avg_step_ms": allr[0]["engine"].get("avg_step_ms"),
+            "boot_s": round(max(r["boot_s"] for r in allr), 1),
+        }
+        print(json.dumps(out), flush=True)
+    if dist_ok:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    main()

@@ -66,97 +66,127 @@ __device__ __forceinline__ float block_excl_scan(float v, float* sw, float& tota
   return base + inc - v;
 }
 
+// Row sweep helper: every thread visits float4 vectors v = tid + k*nt (k ascending),
+// U vectors in flight per iteration (latency hiding: a 1024-thread block on one CU
+// needs many bytes in flight to stream a 600 KB row at L2/HBM rate).
+#define ROW_SWEEP(BODY)                                                        \
+  for (int v0 = tid; v0 < V4; v0 += nt * 4) {                                  \
+    float4 q_[4];                                                              \
+    _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {                         \
+      const int vi_ = v0 + u_ * nt;                                            \
+      q_[u_] = vi_ < V4 ? x4[vi_] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY); \
+    }                                                                          \
+    _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {                         \
+      const int vi_ = v0 + u_ * nt;                                            \
+      const float e_[4] = {q_[u_].x, q_[u_].y, q_[u_].z, q_[u_].w};            \
+      _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) {                       \
+        const float v = e_[j_];                                                \
+        const int i = 4 * vi_ + j_;                                            \
+        (void)i;                                                               \
+        BODY                                                                   \
+      }                                                                        \
+    }                                                                          \
+  }
+
 __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
   __shared__ float red[64];
+  __shared__ int ridx[16];
   __shared__ float sw[16];
   __shared__ int sel;
   const int row = blockIdx.x;
-  const int V = a.V;
+  const int V4 = a.V >> 2;  // host guarantees V % 4 == 0 and 16-B aligned rows
   const float* x = a.logits + (size_t)row * a.ldl;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
   const int tid = threadIdx.x;
   const int nt = blockDim.x;
+  const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
   const float T = a.temperature ? a.temperature[row] : 0.f;
-
-  // ---- pass 1: max (+ argmax) ----
-  float mx = -INFINITY;
-  int amx = 0x7fffffff;
-  for (int i = tid; i < V; i += nt) {
-    const float v = x[i];
-    if (v > mx) { mx = v; amx = i; }
-  }
-  // block argmax (ties -> lowest index)
-  {
-    const int lane = tid & 63, wid = tid >> 6;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float om = __shfl_xor(mx, o, 64);
-      const int oi = __shfl_xor(amx, o, 64);
-      if (om > mx || (om == mx && oi < amx)) { mx = om; amx = oi; }
-    }
-    __shared__ int ridx[16];
-    if (lane == 0) { red[wid] = mx; ridx[wid] = amx; }
-    __syncthreads();
-    if (tid == 0) {
-      float bm = red[0];
-      int bi = ridx[0];
-      for (int w = 1; w < (nt >> 6); ++w)
-        if (red[w] > bm || (red[w] == bm && ridx[w] < bi)) { bm = red[w]; bi = ridx[w]; }
-      red[32] = bm;
-      sel = bi;
-    }
-    __syncthreads();
-    mx = red[32];
-    amx = sel;
-    __syncthreads();
-  }
-
   const bool greedy = !(T > 1e-5f);
   const float c = greedy ? LOG2E_S : LOG2E_S / T;
-  // Z = sum exp2((x - mx) * c)
-  float z = 0.f;
-  for (int i = tid; i < V; i += nt) z += exp2f((x[i] - mx) * c);
-  z = block_reduce_sum(z, red);
+
+  // ---- pass 1: online (max, argmax, Z) in one sweep ----
+  float mx = -INFINITY, z = 0.f;
+  int amx = 0x7fffffff;
+  ROW_SWEEP({
+    if (v > mx) {
+      z = (mx == -INFINITY ? 0.f : z * exp2f((mx - v) * c)) + 1.f;
+      mx = v;
+      amx = i;
+    } else if (v > -INFINITY) {
+      z += exp2f((v - mx) * c);
+    }
+  })
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const float oz = __shfl_xor(z, o, 64);
+    const int oi = __shfl_xor(amx, o, 64);
+    const float nm = fmaxf(mx, om);
+    const float zz = (mx == -INFINITY ? 0.f : z * exp2f((mx - nm) * c)) +
+                     (om == -INFINITY ? 0.f : oz * exp2f((om - nm) * c));
+    if (om > mx || (om == mx && oi < amx)) amx = oi;
+    mx = nm;
+    z = zz;
+  }
+  if (lane == 0) { red[wid] = mx; red[16 + wid] = z; ridx[wid] = amx; }
+  __syncthreads();
+  if (tid == 0) {
+    float bm = red[0], bz = red[16];
+    int bi = ridx[0];
+    for (int w = 1; w < nw; ++w) {
+      const float om = red[w], oz = red[16 + w];
+      const float nm = fmaxf(bm, om);
+      bz = (bm == -INFINITY ? 0.f : bz * exp2f((bm - nm) * c)) + (om == -INFINITY ? 0.f : oz * exp2f((om - nm) * c));
+      if (om > bm || (om == bm && ridx[w] < bi)) bi = ridx[w];
+      bm = nm;
+    }
+    red[32] = bm;
+    red[33] = bz;
+    sel = bi;
+  }
+  __syncthreads();
+  mx = red[32];
+  z = red[33];
+  amx = sel;
+  __syncthreads();
 
   int chosen = amx;
   if (!greedy) {
     const int topk = a.top_k ? a.top_k[row] : -1;
     const float topp = a.top_p ? a.top_p[row] : 1.f;
-    const bool use_k = topk > 0 && topk < V;
+    const bool use_k = topk > 0 && topk < a.V;
     const bool use_p = topp < 1.f;
     const float pmass = topp * z;
     const uint64_t seed = a.seeds ? a.seeds[row] : 0ull;
     const uint64_t off = a.offsets ? (uint64_t)a.offsets[row] : 0ull;
     float pivot = -INFINITY;
-    float mass = z;
     chosen = -1;
     for (int round = 0; round < 64; ++round) {
       const float u = philox_uniform(seed, off, (uint32_t)round);
-      // local sum over this thread's elements above the pivot
       float ls = 0.f;
-      for (int i = tid; i < V; i += nt) {
-        const float v = x[i];
-        if (v > pivot) ls += exp2f((v - mx) * c);
-      }
+      ROW_SWEEP({ if (v > pivot) ls += exp2f((v - mx) * c); })
       float total;
       const float excl = block_excl_scan(ls, sw, total);
       const float target = u * total;
       if (tid == 0) sel = -1;
       __syncthreads();
-      // owner: excl <= target < excl + ls (last non-empty thread catches rounding)
       const bool own = (ls > 0.f) && (target >= excl) && (target < excl + ls || excl + ls >= total);
       if (own) {
         float run = excl;
         int pick = -1, last = -1;
-        for (int i = tid; i < V; i += nt) {
-          const float v = x[i];
-          if (v > pivot) {
-            last = i;
-            run += exp2f((v - mx) * c);
-            if (run > target) { pick = i; break; }
+        for (int vi = tid; vi < V4 && pick < 0; vi += nt) {
+          const float4 q = x4[vi];
+          const float e[4] = {q.x, q.y, q.z, q.w};
+          for (int j = 0; j < 4; ++j) {
+            if (e[j] > pivot) {
+              last = 4 * vi + j;
+              run += exp2f((e[j] - mx) * c);
+              if (run > target) { pick = 4 * vi + j; break; }
+            }
           }
         }
         if (pick < 0) pick = last;
-        atomicMax(&sel, pick);  // ties between owners (rounding) resolve deterministically
+        atomicMax(&sel, pick);
       }
       __syncthreads();
       const int j = sel;
@@ -165,28 +195,19 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
       if (!use_k && !use_p) { chosen = j; break; }
       const float xj = x[j];
       float cnt = 0.f, q = 0.f;
-      for (int i = tid; i < V; i += nt) {
-        const float v = x[i];
-        if (v > xj) { cnt += 1.f; q += exp2f((v - mx) * c); }
-      }
+      ROW_SWEEP({ if (v > xj) { cnt += 1.f; q += exp2f((v - mx) * c); } })
       cnt = block_reduce_sum(cnt, red);
       q = block_reduce_sum(q, red);
       const bool ok_k = !use_k || cnt < (float)topk;
       const bool ok_p = !use_p || q < pmass;
       if (ok_k && ok_p) { chosen = j; break; }
       pivot = xj;
-      mass = q;
-      (void)mass;
     }
     if (chosen < 0) chosen = amx;
   }
   if (tid == 0) {
     a.out[row] = chosen;
-    if (a.out_logprob) {
-      // natural-log probability of the chosen token under the tempered distribution
-      const float lp = ((x[chosen] - mx) * c - log2f(z)) / LOG2E_S;
-      a.out_logprob[row] = lp;
-    }
+    if (a.out_logprob) a.out_logprob[row] = ((x[chosen] - mx) * c - log2f(z)) / LOG2E_S;
   }
 }
 

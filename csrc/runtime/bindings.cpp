@@ -218,6 +218,8 @@ void sample(const Tensor& logits, const c10::optional<Tensor>& temperature,
   s.ldl = (int)logits.stride(0);
   s.B = (int)logits.size(0);
   s.V = (int)logits.size(1);
+  TORCH_CHECK(s.V % 4 == 0 && s.ldl % 4 == 0 && (reinterpret_cast<uintptr_t>(logits.data_ptr()) % 16) == 0,
+              "sample: vocab and row stride must be multiples of 4 floats (16-B aligned rows)");
   auto fp = [](const c10::optional<Tensor>& t, c10::ScalarType dt) -> const void* {
     if (!t.has_value() || !t->defined()) return nullptr;
     TORCH_CHECK(t->scalar_type() == dt, "sample: dtype mismatch");

@@ -1,0 +1,450 @@
+"""FastAPI application: routes, lifespan, middleware (reference ``main.py``).
+
+``create_app(config, engine)`` builds an app (tests inject a config and/or a
+pre-built engine); ``main.py`` exposes ``app = create_app()`` for ``uvicorn main:app``.
+
+Routes (drop-in): ``GET /health``, ``POST /v1/chat/completions`` (JSON or SSE),
+``POST /v1/embeddings``, ``GET /metrics`` (Prometheus / OpenMetrics), ``GET /stats``,
+``POST /v1/benchmark``; worker role: ``POST /internal/generate`` (+ ``_stream``).
+New: ``GET /ready`` (503 until a healthy engine / >=1 healthy worker), ``GET /v1/models``.
+
+Every response carries ``X-Request-ID``. Client routes are 404 in the worker role.
+Streaming keeps the reference SSE framing (role chunk, content deltas, a final
+``{}`` delta with ``finish_reason``, ``data: [DONE]``; in-band error event then
+``[DONE]``; no ``[DONE]`` after a client disconnect) but now goes through the
+admission limit and works through remote workers; a disconnect aborts the
+generation in the engine.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import time
+import uuid
+from contextlib import asynccontextmanager
+from typing import Optional
+
+from fastapi import Depends, FastAPI, HTTPException, Request
+from fastapi.responses import JSONResponse, Response, StreamingResponse
+from prometheus_client import CONTENT_TYPE_LATEST, generate_latest
+from pydantic import BaseModel, Field
+
+from vgate import metrics as M
+from vgate.batcher import RequestBatcher
+from vgate.config import VGateConfig, get_config, set_config
+from vgate.engine import VGateEngine
+from vgate.logging_config import get_logger, setup_logging
+from vgate.security import SecurityMiddleware
+from vgate.tracing import get_current_trace_id, init_tracing, shutdown_tracing
+from vgate.worker_registry import NoHealthyWorkersError
+
+app_logger = get_logger("vgate.app")
+
+
+# ------------------------------------------------------------------ request models
+class ChatMessage(BaseModel):
+    role: str
+    content: str
+
+
+class ChatCompletionRequest(BaseModel):
+    model: str
+    messages: list[ChatMessage]
+    temperature: float = Field(0.7, ge=0.0)
+    top_p: float = Field(0.9, gt=0.0, le=1.0)
+    max_tokens: int = Field(256, ge=1)
+    stream: bool = False
+
+
+class EmbeddingRequest(BaseModel):
+    model: str
+    input: str
+
+
+class BenchmarkRequest(BaseModel):
+    prompts: list[str] = []
+    max_tokens: int = 128
+    rounds: int = 3
+
+
+def messages_to_prompt(messages: list[ChatMessage]) -> str:
+    """Reference flattening: ``"Role: content"`` lines then ``"\\nAssistant:"`` (cache keys stay stable)."""
+    return "\n".join(f"{m.role.capitalize()}: {m.content}" for m in messages) + "\nAssistant:"
+
+
+def _percentile(data, pct):
+    if not data:
+        return 0.0
+    s = sorted(data)
+    return s[min(int(len(s) * pct / 100), len(s) - 1)]
+
+
+# ---------------------------------------------------------------- observability
+class ObservabilityMiddleware:
+    """Outermost pure-ASGI middleware: request id, Prometheus HTTP metrics, completion log."""
+
+    SKIP_LOG = {"/metrics", "/health", "/ready"}
+
+    def __init__(self, app):
+        self.app = app
+
+    async def __call__(self, scope, receive, send):
+        if scope["type"] != "http":
+            await self.app(scope, receive, send)
+            return
+        trace_id = get_current_trace_id()
+        rid = trace_id or uuid.uuid4().hex[:8]
+        t0 = time.perf_counter()
+        endpoint = scope.get("path", "")
+        method = scope.get("method", "GET")
+        status = [500]
+        M.REQUEST_IN_PROGRESS.labels(endpoint=endpoint).inc()
+        rid_b = rid.encode()
+
+        async def send_wrapped(msg):
+            if msg["type"] == "http.response.start":
+                status[0] = msg["status"]
+                msg = dict(msg)
+                msg["headers"] = list(msg.get("headers", [])) + [(b"x-request-id", rid_b)]
+            await send(msg)
+
+        try:
+            await self.app(scope, receive, send_wrapped)
+        finally:
+            lat = time.perf_counter() - t0
+            ex = {"trace_id": trace_id} if trace_id else None
+            M.REQUEST_COUNT.labels(endpoint=endpoint, method=method, status=str(status[0])).inc(exemplar=ex)
+            M.REQUEST_LATENCY.labels(endpoint=endpoint, method=method).observe(lat, exemplar=ex)
+            M.REQUEST_IN_PROGRESS.labels(endpoint=endpoint).dec()
+            if endpoint not in self.SKIP_LOG:
+                app_logger.info("Request completed", extra={"extra_data": {
+                    "request_id": rid, "trace_id": trace_id, "method": method, "path": endpoint,
+                    "status": status[0], "latency_ms": round(lat * 1000, 2)}})
+
+
+class AppState:
+    def __init__(self, config: VGateConfig):
+        self.config = config
+        self.engine: Optional[VGateEngine] = None
+        self.batcher: Optional[RequestBatcher] = None
+        self.health_checker = None
+        self.engine_metrics_task: Optional[asyncio.Task] = None
+
+
+def _json(data, status: int = 200, headers: dict | None = None) -> Response:
+    return Response(content=json.dumps(data), status_code=status, media_type="application/json", headers=headers)
+
+
+def create_app(config: Optional[VGateConfig] = None, engine: Optional[VGateEngine] = None) -> FastAPI:
+    if config is None:
+        config = get_config()
+    else:
+        set_config(config)
+    setup_logging(config.logging.level, config.logging.json_format)
+    is_worker = config.role == "worker"
+    version = config.version
+    st = AppState(config)
+
+    @asynccontextmanager
+    async def lifespan(app: FastAPI):
+        init_tracing(config)
+        st.engine = engine if engine is not None else await asyncio.get_running_loop().run_in_executor(None, VGateEngine)
+        M.init_app_info(version=version, model=config.model.model_id)
+        if is_worker:
+            from vgate import worker_api
+            worker_api.set_engine(st.engine)
+            app_logger.info("V-Gate worker started", extra={"extra_data": {
+                "version": version, "model": config.model.model_id, "engine_type": config.model.engine_type}})
+            st.engine_metrics_task = asyncio.create_task(_engine_metrics_loop(st))
+            yield
+            st.engine_metrics_task.cancel()
+            st.engine.backend.shutdown()
+            shutdown_tracing()
+            app_logger.info("V-Gate worker stopped")
+            return
+        st.batcher = RequestBatcher(engine=st.engine)
+        if st.engine.is_remote:
+            from vgate.health_checker import WorkerHealthChecker
+            from vgate.worker_discovery import DnsWorkerDiscovery
+            disc = None
+            if config.worker.discovery.dns_name:
+                d = config.worker.discovery
+                disc = DnsWorkerDiscovery(dns_name=d.dns_name, port=d.port, scheme=d.scheme)
+            st.health_checker = WorkerHealthChecker(
+                registry=st.engine.backend.registry, interval_seconds=config.worker.health_check_interval_seconds,
+                timeout_seconds=config.worker.health_check_timeout_seconds, api_key=config.worker.api_key,
+                discovery=disc)
+            await st.health_checker.start()
+        await st.batcher.start()
+        st.engine_metrics_task = asyncio.create_task(_engine_metrics_loop(st))
+        app_logger.info("V-Gate started", extra={"extra_data": {
+            "version": version, "model": config.model.model_id, "engine_type": config.model.engine_type,
+            "inference": "remote" if st.engine.is_remote else "in-process",
+            "worker_endpoints": config.worker.endpoints,
+            "batch_config": {"max_batch_size": config.batch.max_batch_size,
+                             "max_wait_time_ms": config.batch.max_wait_time_ms},
+            "cache_config": {"enabled": config.cache.enabled, "maxsize": config.cache.maxsize},
+            "security_config": {"enabled": config.security.enabled,
+                                "api_keys_count": len(config.security.api_keys),
+                                "rate_limiting_enabled": config.security.rate_limiting.enabled}}})
+        yield
+        st.engine_metrics_task.cancel()
+        await st.batcher.stop()
+        if st.health_checker is not None:
+            await st.health_checker.stop()
+        if st.engine.is_remote:
+            await st.engine.backend.aclose()
+        elif engine is None:
+            st.engine.backend.shutdown()
+        shutdown_tracing()
+        app_logger.info("V-Gate stopped")
+
+    app = FastAPI(
+        title="V-Gate LLM Inference Worker" if is_worker else "V-Gate LLM Inference Gateway",
+        description="MI355X-native LLM serving gateway (OpenAI-shaped Chat Completions subset)",
+        version=version, lifespan=lifespan)
+    app.state.vgate = st
+    if is_worker:
+        from vgate import worker_api
+        app.include_router(worker_api.router)
+    app.add_middleware(SecurityMiddleware, config=config.security)
+    app.add_middleware(ObservabilityMiddleware)
+
+    def gateway_only() -> None:
+        if is_worker:
+            raise HTTPException(status_code=404, detail="Not available in worker role; call the gateway instead")
+
+    # -------------------------------------------------------------- routes
+    @app.get("/health", summary="Health Check")
+    async def health_check():
+        return {"status": "ok", "version": version, "role": config.role}
+
+    @app.get("/ready", summary="Readiness")
+    async def ready():
+        eng = st.engine
+        ok, detail = eng is not None, "starting"
+        if eng is not None:
+            if eng.is_remote:
+                ok = eng.backend.registry.has_healthy()
+                detail = "no healthy workers" if not ok else "ok"
+            else:
+                h = getattr(eng.backend, "healthy", None)
+                ok = h() if callable(h) else True
+                detail = "ok" if ok else "engine unhealthy"
+        return _json({"status": "ready" if ok else "unavailable", "detail": detail}, 200 if ok else 503)
+
+    @app.get("/v1/models", summary="List models", dependencies=[Depends(gateway_only)])
+    async def list_models():
+        return {"object": "list", "data": [{"id": config.model.model_id, "object": "model", "owned_by": "vgate"}]}
+
+    @app.post("/v1/chat/completions", summary="Create Chat Completion", dependencies=[Depends(gateway_only)])
+    async def create_chat_completion(request: ChatCompletionRequest):
+        backend = st.engine.backend
+        prompt = messages_to_prompt(request.messages)
+        if request.stream:
+            if not getattr(backend, "supports_streaming", True):
+                raise HTTPException(status_code=501, detail=(
+                    "Streaming is not supported by this backend. Send stream=false."))
+            return StreamingResponse(_stream_chat(st, prompt, request), media_type="text/event-stream")
+        try:
+            r = await st.batcher.submit(prompt, max_tokens=request.max_tokens, temperature=request.temperature,
+                                        top_p=request.top_p)
+        except NoHealthyWorkersError as e:
+            app_logger.error("No healthy workers", extra={"extra_data": {"error": str(e)}})
+            raise HTTPException(status_code=503, detail=str(e), headers={"Retry-After": "5"})
+        except Exception as e:  # noqa: BLE001
+            app_logger.error("Chat completion error", extra={"extra_data": {"error": str(e),
+                                                                             "error_type": type(e).__name__}})
+            raise HTTPException(status_code=500, detail=str(e))
+        pt = r.get("prompt_tokens", 0)
+        ct = r.get("total_tokens", 0)
+        return _json({
+            "id": "chatcmpl-" + uuid.uuid4().hex[:8], "object": "chat.completion", "created": int(time.time()),
+            "model": request.model,
+            "choices": [{"index": 0, "message": {"role": "assistant", "content": r["text"]},
+                         "finish_reason": r.get("finish_reason", "stop")}],
+            "usage": {"prompt_tokens": pt, "completion_tokens": ct, "total_tokens": ct + pt}})
+
+    @app.post("/v1/embeddings", summary="Create Embeddings", dependencies=[Depends(gateway_only)])
+    async def create_embeddings(request: EmbeddingRequest):
+        try:
+            loop = asyncio.get_running_loop()
+            r = await loop.run_in_executor(None, st.engine.embeddings, request.input)
+        except Exception as e:  # noqa: BLE001
+            app_logger.error("Embeddings error", extra={"extra_data": {"error": str(e)}})
+            raise HTTPException(status_code=500, detail=str(e))
+        return {"object": "list", "data": r["data"], "model": request.model, "usage": r["usage"]}
+
+    @app.get("/metrics", summary="Prometheus Metrics")
+    async def prometheus_metrics(request: Request):
+        if "application/openmetrics-text" in request.headers.get("accept", ""):
+            from prometheus_client.openmetrics.exposition import generate_latest as om_latest
+            return Response(content=om_latest(),
+                            media_type="application/openmetrics-text; version=1.0.0; charset=utf-8")
+        return Response(content=generate_latest(), media_type=CONTENT_TYPE_LATEST)
+
+    @app.get("/stats", summary="JSON Statistics", dependencies=[Depends(gateway_only)])
+    async def get_stats():
+        m = st.batcher.get_metrics()
+        out = {
+            "batcher": {k: m[k] for k in ("total_requests", "total_batches", "average_batch_size",
+                                          "pending_requests", "total_deduplicated", "avg_queue_time_s",
+                                          "avg_ttft_s", "avg_tpot_s")},
+            "cache": m["cache"],
+            "config": {
+                "batch": {"max_batch_size": config.batch.max_batch_size,
+                          "max_wait_time_ms": config.batch.max_wait_time_ms},
+                "cache": {"enabled": config.cache.enabled, "maxsize": config.cache.maxsize},
+                "logging": {"level": config.logging.level, "json_format": config.logging.json_format},
+                "security": {"enabled": config.security.enabled,
+                             "rate_limiting_enabled": config.security.rate_limiting.enabled,
+                             "exempt_paths": config.security.exempt_paths},
+            },
+            "version": version,
+        }
+        if st.engine.is_remote:
+            out["workers"] = st.engine.backend.registry.snapshot()
+        stats = getattr(st.engine.backend, "stats", None)
+        if callable(stats):
+            out["engine"] = stats()
+        return out
+
+    @app.post("/v1/benchmark", summary="Run Inline Benchmark", dependencies=[Depends(gateway_only)])
+    async def run_benchmark(request: BenchmarkRequest):
+        prompts = request.prompts or config.benchmark.prompts
+        before = st.batcher.get_metrics()
+        lats, toks, ttfts, tpots = [], [], [], []
+        for _ in range(request.rounds):
+            t0 = time.perf_counter()
+            res = await asyncio.gather(*(st.batcher.submit(p, max_tokens=request.max_tokens) for p in prompts))
+            lats.append(time.perf_counter() - t0)
+            toks.append(sum(r.get("total_tokens", 0) for r in res))
+            ttfts.extend(r["ttft"] for r in res if r.get("ttft", 0) > 0)
+            tpots.extend(r["tpot"] for r in res if r.get("tpot", 0) > 0)
+        after = st.batcher.get_metrics()
+        total_t = sum(lats)
+        total_tok = sum(toks)
+        sl = sorted(lats)
+        return {
+            "engine_type": config.model.engine_type, "rounds": request.rounds, "prompts_per_round": len(prompts),
+            "latency": {"mean_s": round(total_t / max(1, request.rounds), 4),
+                        "p50_s": round(sl[len(sl) // 2], 4) if sl else 0.0,
+                        "p95_s": round(sl[min(int(len(sl) * 0.95), len(sl) - 1)], 4) if sl else 0.0,
+                        "total_s": round(total_t, 4)},
+            "ttft": {"mean_s": round(sum(ttfts) / len(ttfts), 4) if ttfts else 0.0,
+                     "p50_s": round(_percentile(ttfts, 50), 4), "p95_s": round(_percentile(ttfts, 95), 4)},
+            "tpot": {"mean_s": round(sum(tpots) / len(tpots), 4) if tpots else 0.0,
+                     "p50_s": round(_percentile(tpots, 50), 4), "p95_s": round(_percentile(tpots, 95), 4)},
+            "batching": {"requests": after["total_requests"] - before["total_requests"],
+                         "batches": after["total_batches"] - before["total_batches"],
+                         "average_batch_size": after["average_batch_size"],
+                         "deduplicated": after["total_deduplicated"] - before["total_deduplicated"]},
+            "cache": {"hits": after["cache"]["hits"] - before["cache"]["hits"],
+                      "misses": after["cache"]["misses"] - before["cache"]["misses"],
+                      "hit_rate": after["cache"]["hit_rate"]},
+            "throughput": {"total_tokens": total_tok,
+                           "tokens_per_second": round(total_tok / total_t, 2) if total_t > 0 else 0.0},
+        }
+
+    return app
+
+
+async def _stream_chat(st: AppState, prompt: str, request: ChatCompletionRequest):
+    """SSE generator (framing and metrics of the reference; admission-controlled)."""
+    backend = st.engine.backend
+    cid = "chatcmpl-" + uuid.uuid4().hex[:8]
+    created = int(time.time())
+    t_start = time.monotonic()
+
+    def chunk(delta: dict, finish_reason=None) -> str:
+        return "data: " + json.dumps({"id": cid, "object": "chat.completion.chunk", "created": created,
+                                      "model": request.model,
+                                      "choices": [{"index": 0, "delta": delta, "finish_reason": finish_reason}]}) + "\n\n"
+
+    ttft_done = False
+    prev_n = 0
+    prev_t = t_start
+    dec_t = 0.0
+    dec_n = 0
+    final_n = 0
+    finish = "stop"
+    status = "cancelled"
+    sem = st.batcher._semaphore if st.batcher is not None else None
+    acquired = False
+    try:
+        yield chunk({"role": "assistant"})
+        if sem is not None:
+            await sem.acquire()
+            acquired = True
+        sp = backend.create_sampling_params(temperature=request.temperature, top_p=request.top_p,
+                                            max_tokens=request.max_tokens)
+        async for piece in backend.stream_generate(prompt, sp):
+            delta = piece.get("delta")
+            n = piece.get("num_tokens", prev_n)
+            final_n = n
+            if piece.get("finish_reason"):
+                finish = piece["finish_reason"]
+            now = time.monotonic()
+            if delta:
+                if not ttft_done:
+                    M.STREAM_TTFT.observe(now - t_start)
+                    ttft_done = True
+                else:
+                    inc = n - prev_n
+                    if inc > 0:
+                        dec_t += now - prev_t
+                        dec_n += inc
+                prev_n = n
+                prev_t = now
+                yield chunk({"content": delta})
+        yield chunk({}, finish_reason=finish)
+        status = "completed"
+        if dec_n > 0:
+            M.STREAM_TPOT.observe(dec_t / dec_n)
+        M.STREAM_DURATION.observe(time.monotonic() - t_start)
+    except (GeneratorExit, asyncio.CancelledError):
+        status = "cancelled"
+        raise
+    except Exception as e:  # noqa: BLE001
+        status = "error"
+        M.INFERENCE_ERRORS.labels(error_type=type(e).__name__).inc()
+        app_logger.error("Streaming chat completion error", extra={"extra_data": {
+            "completion_id": cid, "error": str(e), "error_type": type(e).__name__}})
+        yield "data: " + json.dumps({"error": {"message": str(e), "type": type(e).__name__}}) + "\n\n"
+    finally:
+        if acquired:
+            sem.release()
+        M.STREAM_REQUESTS.labels(status=status).inc()
+        if final_n > 0:
+            M.STREAM_TOKENS.inc(final_n)
+            M.TOKENS_GENERATED.inc(final_n)
+    if status != "cancelled":
+        yield "data: [DONE]\n\n"
+
+
+async def _engine_metrics_loop(st: AppState, period: float = 1.0):
+    """Mirror native-engine counters into Prometheus gauges/counters."""
+    last = {}
+    try:
+        while True:
+            await asyncio.sleep(period)
+            b = getattr(st.engine, "backend", None)
+            stats = getattr(b, "stats", None)
+            if not callable(stats):
+                continue
+            s = stats()
+            if not s:
+                continue
+            M.ENGINE_RUNNING.set(s.get("running", 0))
+            M.ENGINE_WAITING.set(s.get("waiting", 0))
+            M.ENGINE_KV_USAGE.set(s.get("kv_usage", 0.0))
+            for key, ctr in (("prefill_tokens", M.ENGINE_PREFILL_TOKENS), ("decode_tokens", M.ENGINE_DECODE_TOKENS),
+                             ("graph_hits", M.ENGINE_GRAPH_REPLAYS), ("preemptions", M.ENGINE_PREEMPTIONS),
+                             ("prefix_cache_hits", M.ENGINE_PREFIX_HITS)):
+                v = s.get(key, 0)
+                d = v - last.get(key, 0)
+                if d > 0:
+                    ctr.inc(d)
+                last[key] = v
+    except asyncio.CancelledError:
+        pass

@@ -1,0 +1,86 @@
+"""LRU result cache for completed generations (reference ``vgate/cache.py:28-108`` behavior).
+
+Key = first 16 hex chars of sha256 over the sorted-key JSON of
+``{prompt, temperature, top_p, max_tokens}`` — identical to the reference so
+keys stay stable across the swap. Differences (fixes of SURVEY.md §2.9): hits
+return a *copy* of the stored dict, so callers cannot mutate the cache.
+"""
+from __future__ import annotations
+
+import asyncio
+import copy
+import hashlib
+import json
+from collections import OrderedDict
+from typing import Any, Optional
+
+from vgate.config import get_config
+from vgate.logging_config import get_logger
+from vgate.metrics import CACHE_EVICTIONS, CACHE_HITS, CACHE_MISSES, CACHE_SIZE
+from vgate.tracing import get_tracer
+
+logger = get_logger("vgate.cache")
+tracer = get_tracer(__name__)
+
+
+class ResultCache:
+    def __init__(self, maxsize: Optional[int] = None, enabled: Optional[bool] = None):
+        cfg = get_config()
+        self.maxsize = maxsize if maxsize is not None else cfg.cache.maxsize
+        self.enabled = enabled if enabled is not None else cfg.cache.enabled
+        self._data: OrderedDict[str, dict] = OrderedDict()
+        self._lock = asyncio.Lock()
+        self.hits = 0
+        self.misses = 0
+        self.evictions = 0
+
+    @staticmethod
+    def make_key(prompt: str, temperature: float, top_p: float, max_tokens: int) -> str:
+        blob = json.dumps({"prompt": prompt, "temperature": temperature, "top_p": top_p,
+                           "max_tokens": max_tokens}, sort_keys=True)
+        return hashlib.sha256(blob.encode("utf-8")).hexdigest()[:16]
+
+    async def get(self, key: str) -> Optional[dict[str, Any]]:
+        if not self.enabled:
+            return None
+        with tracer.start_as_current_span("cache.get") as span:
+            async with self._lock:
+                val = self._data.get(key)
+                if val is None:
+                    self.misses += 1
+                    CACHE_MISSES.inc()
+                    span.set_attribute("hit", False)
+                    return None
+                self._data.move_to_end(key)
+                self.hits += 1
+                CACHE_HITS.inc()
+                span.set_attribute("hit", True)
+                return copy.deepcopy(val)
+
+    async def put(self, key: str, value: dict[str, Any]) -> None:
+        if not self.enabled or self.maxsize <= 0:
+            return
+        with tracer.start_as_current_span("cache.put"):
+            async with self._lock:
+                if key in self._data:
+                    self._data.move_to_end(key)
+                self._data[key] = copy.deepcopy(value)
+                while len(self._data) > self.maxsize:
+                    old, _ = self._data.popitem(last=False)
+                    self.evictions += 1
+                    CACHE_EVICTIONS.inc()
+                    logger.debug("Cache eviction", extra={"extra_data": {"cache_key": old[:8]}})
+                CACHE_SIZE.set(len(self._data))
+
+    async def clear(self) -> None:
+        async with self._lock:
+            self._data.clear()
+            CACHE_SIZE.set(0)
+
+    def __len__(self) -> int:
+        return len(self._data)
+
+    def get_stats(self) -> dict[str, Any]:
+        total = self.hits + self.misses
+        return {"size": len(self._data), "maxsize": self.maxsize, "hits": self.hits, "misses": self.misses,
+                "evictions": self.evictions, "hit_rate": round(self.hits / total, 4) if total else 0.0}
