@@ -1,0 +1,107 @@
+"""GPU micro-benchmarks (run on the MI355X box):
+
+  1. per-kernel floor: N trivial launches captured in one hipGraph, replayed;
+  2. decode GEMM sweep: every Qwen2.5-1.5B projection at M=8 over (waves, split-K),
+     each timed as 20 launches inside a hipGraph (no host overhead), reporting
+     us/launch and effective weight bandwidth.
+
+    python benchmarks/micro_gpu.py [--quick]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+import torch  # noqa: E402
+
+from vgate import ops  # noqa: E402
+
+
+def graph_time(fn, reps=20, iters=30):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        for _ in range(reps):
+            fn()
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = 1e9
+    for _ in range(5):
+        e0.record()
+        for _ in range(iters):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1) * 1e3 / (iters * reps))
+    return best  # us per launch
+
+
+def floor():
+    x = torch.randn(1, 128, device="cuda").bfloat16()
+    w = torch.ones(128, device="cuda").bfloat16()
+    y = torch.empty_like(x)
+    C = ops.native()
+    return {"trivial_kernel_us": round(graph_time(lambda: C.rmsnorm(x, None, w, y, 1e-6), reps=100), 3)}
+
+
+SHAPES = [  # name, N, K, layout, out_f32
+    ("qkv", 2048, 1536, "plain", False),
+    ("o_proj", 1536, 1536, "plain", False),
+    ("gate_up", 17920, 1536, "silu", False),
+    ("down", 1536, 8960, "plain", False),
+    ("lm_head", 151936, 1536, "plain", True),
+]
+
+
+def sweep(M=8, quick=False):
+    out = []
+    for name, N, K, layout, f32 in SHAPES:
+        x = torch.randn(M, K, device="cuda").bfloat16()
+        w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).bfloat16()
+        lin = ops.Linear(w, layout=layout)
+        res = torch.randn(M, N, device="cuda").bfloat16() if name in ("o_proj", "down") else None
+        y = torch.empty(M, lin.out_features, device="cuda", dtype=torch.float32 if f32 else torch.bfloat16)
+        nbytes = N * K * 2
+        rows = []
+        waves = [1, 2, 4, 8, 16] if not quick else [4, 8, 16]
+        splits = [1, 2, 4, 8] if name not in ("gate_up", "lm_head") else [1, 2]
+        for wv in waves:
+            for sk in splits:
+                try:
+                    t = graph_time(lambda: ops.linear(x, lin, out=y, residual=res, out_f32=f32, waves=wv, splitk=sk))
+                except Exception as e:  # noqa: BLE001
+                    rows.append({"waves": wv, "splitk": sk, "error": str(e)[:80]})
+                    continue
+                rows.append({"waves": wv, "splitk": sk, "us": round(t, 2), "TBps": round(nbytes / t / 1e6, 2)})
+        auto = graph_time(lambda: ops.linear(x, lin, out=y, residual=res, out_f32=f32))
+        best = min((r for r in rows if "us" in r), key=lambda r: r["us"])
+        out.append({"shape": name, "N": N, "K": K, "M": M, "auto_us": round(auto, 2),
+                    "auto_TBps": round(nbytes / auto / 1e6, 2), "best": best, "all": rows})
+        print(json.dumps(out[-1]), flush=True)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--M", type=int, default=8)
+    a = ap.parse_args()
+    print(json.dumps(floor()), flush=True)
+    sweep(a.M, a.quick)
+
+
+if __name__ == "__main__":
+    main()

@@ -131,16 +131,14 @@ __device__ __forceinline__ bf16x8 softmax_step(f32x4& s0, f32x4& s1, float& m, f
 }
 
 // ---------------------------------------------------------------- decode ----
-// grid (S, Hkv, P); block 256 = 4 waves; wave w takes chunks w, w+4, ... of the
-// partition. Query columns = the G = Hq/Hkv heads sharing this KV head.
-__global__ __launch_bounds__(256) void attn_decode_kernel(AttnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int s = blockIdx.x, h = blockIdx.y, part = blockIdx.z;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+// One block per (sequence, KV head, partition); its nw waves take chunks w, w+nw, ...
+// Query columns = the G = Hq/Hkv heads sharing this KV head. Only sequences with a
+// single new query token are decode work (prefill tiles cover the rest).
+__device__ __forceinline__ void decode_body(const AttnArgs& a, int s, int h, int part, char* smem) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int ctx = a.context_lens[s];
   const int pstart = part * a.part_size;
   if (ctx <= 0 || pstart >= ctx) return;
-  // with query_start, only single-query sequences are decode work (prefill tiles cover the rest)
   if (a.query_start && a.query_start[s + 1] - a.query_start[s] != 1) return;
   const int pend = min(ctx, pstart + a.part_size);
   const int nparts = (ctx + a.part_size - 1) / a.part_size;
@@ -151,8 +149,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnArgs a) {
   uint4 qf[4];
   {
     const bool ok = col < G;
-    const bf16_t* qp = a.q + (size_t)qtok * a.q_stride + (size_t)(h * G + (ok ? col : 0)) * D_ +
-                       8 * (lane >> 4);
+    const bf16_t* qp = a.q + (size_t)qtok * a.q_stride + (size_t)(h * G + (ok ? col : 0)) * D_ + 8 * (lane >> 4);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)
       qf[kk] = ok ? *reinterpret_cast<const uint4*>(qp + 32 * kk) : make_uint4(0, 0, 0, 0);
@@ -169,7 +166,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnArgs a) {
   const size_t blk_stride = (size_t)a.Hkv * BS_ * D_;
   const int nch = (pend - pstart + CHUNK - 1) / CHUNK;
 
-  for (int c = wid; c < nch; c += 4) {
+  for (int c = wid; c < nch; c += nw) {
     const int tb = pstart + c * CHUNK;
     const int b0 = bt[tb / BS_];
     const int b1 = (tb + BS_ < pend) ? bt[tb / BS_ + 1] : b0;
@@ -190,11 +187,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnArgs a) {
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
 
-  // ---- merge the 4 waves: scratch reuses the V images ----
+  // ---- merge the nw waves: scratch reuses the V images ----
   __syncthreads();
-  float* sm_m = reinterpret_cast<float*>(smem);    // [4][16]
-  float* sm_l = sm_m + 64;                         // [4][16]
-  float* sm_o = sm_l + 64;                         // [4][128][16]
+  float* sm_m = reinterpret_cast<float*>(smem);   // [nw][16]
+  float* sm_l = sm_m + 16 * nw;                   // [nw][16]
+  float* sm_o = sm_l + 16 * nw;                   // [nw][128][16]
   if (lane < 16) {
     sm_m[wid * 16 + lane] = m;
     sm_l[wid * 16 + lane] = l;
@@ -207,16 +204,13 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnArgs a) {
       for (int i = 0; i < 4; ++i) sm_o[(wid * D_ + 16 * mt + 4 * g + i) * 16 + col] = o[mt][i];
   }
   __syncthreads();
-  // thread -> (col, d-range): G*128 outputs, 256 threads
   for (int idx = threadIdx.x; idx < G * (D_ / 4); idx += blockDim.x) {
     const int cc = idx / (D_ / 4);
     const int d0 = (idx % (D_ / 4)) * 4;
     float M = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm_m[w * 16 + cc]);
+    for (int w = 0; w < nw; ++w) M = fmaxf(M, sm_m[w * 16 + cc]);
     float L = 0.f, acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < nw; ++w) {
       const float mw = sm_m[w * 16 + cc];
       const float f = (mw == -INFINITY) ? 0.f : exp2f(mw - M);
       L += sm_l[w * 16 + cc] * f;
@@ -265,39 +259,26 @@ __global__ __launch_bounds__(128) void attn_decode_reduce_kernel(AttnArgs a) {
   a.out[(size_t)qtok * a.out_stride + (size_t)hq * D_ + d] = f2bf(L > 0.f ? acc / L : 0.f);
 }
 
-void launch_attn_decode(const AttnArgs& a, hipStream_t st) {
-  if (a.S <= 0) return;
-  dim3 grid(a.S, a.Hkv, a.num_parts);
-  // 4 per-wave V images (32 KiB) reused as merge scratch: m,l [2][4][16] + O [4][128][16] f32
-  constexpr size_t kVImg = 4 * CHUNK * D_ * 2;
-  constexpr size_t kMerge = (128 + 4 * D_ * 16) * 4;
-  const size_t lds = kVImg > kMerge ? kVImg : kMerge;
-  hipLaunchKernelGGL(attn_decode_kernel, grid, dim3(256), lds, st, a);
-  if (a.num_parts > 1) hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(a.S, a.Hq), dim3(128), 0, st, a);
-}
-
 // --------------------------------------------------------------- prefill ----
-// grid (num_tiles, Hkv); block = 64*G threads (one wave per query head of the
-// group); every wave walks the same KV chunks, V is staged once per block into
-// a double-buffered LDS image (one barrier per chunk). Query columns = 16
-// consecutive query tokens of the wave's head.
-__global__ __launch_bounds__(1024) void attn_prefill_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16_t vls[2][CHUNK * D_];
-  const int tile = blockIdx.x, h = blockIdx.y;
+// One block per (16-query tile, KV head); wave w < G owns query head h*G + w and
+// its 16 query columns; every wave walks the same KV chunks, V is staged once per
+// block into a double-buffered LDS image (one barrier per chunk).
+__device__ __forceinline__ void prefill_body(const AttnArgs& a, int tile, int h, char* smem) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nthr = blockDim.x;
   const int s = a.tile_seq[tile];
-  if (s < 0) return;  // padding tile of a graph bucket
+  if (s < 0) return;  // padding tile of a graph bucket (uniform over the block)
   const int q0 = a.tile_q0[tile];
   const int qs = a.query_start[s];
   const int qlen = a.query_start[s + 1] - qs;
   const int ctx = a.context_lens[s];
   const int G = a.Hq / a.Hkv;
-  const int hq = h * G + wid;
+  const bool wave_ok = wid < G;
+  const int hq = h * G + (wave_ok ? wid : 0);
   const int col = lane & 15;
   const int qi = q0 + col;
-  const bool qok = qi < qlen;
-  const int qpos = ctx - qlen + qi;  // absolute position of this column's query
+  const bool qok = wave_ok && qi < qlen;
+  const int qpos = ctx - qlen + qi;
   const int lim = qok ? qpos + 1 : 0;
   const int kv_end = min(ctx, ctx - qlen + min(q0 + 16, qlen));
 
@@ -314,6 +295,7 @@ __global__ __launch_bounds__(1024) void attn_prefill_kernel(AttnArgs a) {
 #pragma unroll
   for (int mt = 0; mt < 8; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  bf16_t* vls = reinterpret_cast<bf16_t*>(smem);
   const int* bt = a.block_tables + (size_t)s * a.max_blocks;
   const size_t head_off = (size_t)h * BS_ * D_;
   const size_t blk_stride = (size_t)a.Hkv * BS_ * D_;
@@ -324,8 +306,7 @@ __global__ __launch_bounds__(1024) void attn_prefill_kernel(AttnArgs a) {
     const int b1 = (tb + BS_ < kv_end) ? bt[tb / BS_ + 1] : b0;
     const bf16_t* vb0 = a.v_cache + (size_t)b0 * blk_stride + head_off;
     const bf16_t* vb1 = a.v_cache + (size_t)b1 * blk_stride + head_off;
-    bf16_t* vl = vls[c & 1];
-    // cooperative V staging: 512 16-B vectors per chunk
+    bf16_t* vl = vls + (c & 1) * (CHUNK * D_);
     for (int e = threadIdx.x; e < CHUNK * D_ / 8; e += nthr) {
       const int r = e >> 4, cc = (e & 15) * 8;
       uint4 v = make_uint4(0, 0, 0, 0);
@@ -355,10 +336,52 @@ __global__ __launch_bounds__(1024) void attn_prefill_kernel(AttnArgs a) {
   }
 }
 
-void launch_attn_prefill(const AttnArgs& a, hipStream_t st) {
-  if (a.num_tiles <= 0) return;
+// ------------------------------------------------------------- unified launch ----
+// grid.x = [decode blocks for sequences 0..dec_seqs) ++ [prefill tiles], grid.y = KV
+// heads, grid.z = decode partitions. One launch serves a decode-only, prefill-only or
+// mixed (chunked-prefill) step; blocks without work exit immediately.
+__global__ __launch_bounds__(1024) void attn_kernel(AttnArgs a, int dec_seqs) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int bx = blockIdx.x;
+  if (bx < dec_seqs) {
+    decode_body(a, bx, blockIdx.y, blockIdx.z, smem);
+  } else if (blockIdx.z == 0) {
+    prefill_body(a, bx - dec_seqs, blockIdx.y, smem);
+  }
+}
+
+static int attn_waves(const AttnArgs& a) {
   const int G = a.Hq / a.Hkv;
-  hipLaunchKernelGGL(attn_prefill_kernel, dim3(a.num_tiles, a.Hkv), dim3(64 * G), 0, st, a);
+  return G > 4 ? G : 4;
+}
+
+static size_t attn_lds(int nw) {
+  const size_t vimg = (size_t)nw * CHUNK * D_ * 2;          // decode: one V image per wave
+  const size_t merge = (size_t)(2 * 16 * nw + nw * D_ * 16) * 4;  // decode merge scratch
+  const size_t pre = 2 * CHUNK * D_ * 2;                     // prefill double buffer
+  size_t m = vimg > merge ? vimg : merge;
+  return m > pre ? m : pre;
+}
+
+void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
+  const int tiles = a.num_tiles > 0 ? a.num_tiles : 0;
+  const int nx = dec_seqs + tiles;
+  if (nx <= 0) return;
+  const int nw = attn_waves(a);
+  const int nz = dec_seqs > 0 ? a.num_parts : 1;
+  hipLaunchKernelGGL(attn_kernel, dim3(nx, a.Hkv, nz), dim3(64 * nw), attn_lds(nw), st, a, dec_seqs);
+  if (dec_seqs > 0 && a.num_parts > 1)
+    hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(dec_seqs, a.Hq), dim3(128), 0, st, a);
+}
+
+void launch_attn_decode(const AttnArgs& a, hipStream_t st) {
+  AttnArgs b = a;
+  b.num_tiles = 0;
+  launch_attention(b, a.S, st);
+}
+
+void launch_attn_prefill(const AttnArgs& a, hipStream_t st) {
+  launch_attention(a, 0, st);
 }
 
 }  // namespace vgate

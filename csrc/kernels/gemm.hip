@@ -1,6 +1,7 @@
-// Weight-streaming MFMA GEMMs for the decode / small-M regime on gfx950.
+// Weight-streaming MFMA GEMMs for the decode / small-M regime on gfx950, with the
+// transformer's neighbouring ops fused in so a decoder layer is 4 GEMM launches.
 //
-//   out[m][n] = epilogue( sum_k x[m][k] * W[n][k] )
+//   out[m][n] = epilogue( sum_k prologue(x)[m][k] * W[n][k] )
 //
 // Weights are pre-packed ONCE at load time into "fragment-major" order so that
 // one wave-instruction of 16 B/lane reads 1 KiB of contiguous HBM that is
@@ -8,46 +9,268 @@
 //
 //   Wp[nt][kt][lane][j] = W[16*nt + (lane & 15)][32*kt + 8*(lane >> 4) + j]
 //
-// (nt = 16-row n-tile, kt = 32-wide k-tile). No LDS staging of weights: in the
-// M <= 64 regime each weight byte is used by one wave only, so the bytes go
-// straight to VGPRs with non-temporal loads (cdna_hip_programming.md §5 'GEMV /
-// M <= 16 decode weights' row). Activation (x) fragments are L2-resident.
+// No LDS staging of weights: in the M <= 64 regime each weight byte is used by one
+// wave only, so the bytes go straight to VGPRs with non-temporal loads
+// (cdna_hip_programming.md §5 'GEMV / M <= 16 decode weights').
 //
-// Decomposition: one workgroup owns NTB n-tiles for a 16*MB row chunk of x and
-// ALL of K; its W waves split K into contiguous ranges (each wave streams one
-// contiguous weight region) and the partial accumulators are reduced through
-// LDS. The epilogue (bias, residual add, SiLU*mul, f32 logits) is fused, so no
-// split-K workspace or second launch exists.
+// Decomposition: grid = (n-tile groups, m-chunks of 16*MB rows, SPLITK k-slices).
+// Inside a block, W waves split the block's k-slice into contiguous ranges and
+// their accumulators are reduced through LDS. With SPLITK > 1 every block writes
+// an fp32 partial slab and the LAST-ARRIVING block of the tile (agent-scope
+// release -> ticket atomic -> agent-scope acquire, §5 'In-launch split-K
+// reduction') sums the slabs and runs the epilogue — no second launch, and the
+// small-N projections (o_proj / down_proj: 96 tiles) still fill all 256 CUs.
 //
-// Orientation: D = Wfrag(A) x xfrag(B) -> lane holds D[n = 4(l>>4)+i][m = l&15],
-// i.e. 4 consecutive output columns of one row -> 8-byte stores.
+// Fusions:
+//   NORM prologue : x := bf16(bf16(x * rsqrt(mean(x^2) + eps)) * w) computed on the
+//                   fly from the residual stream (RMSNorm never runs as a kernel);
+//   row_idx       : rows gathered by index (LM head reads only sampled rows);
+//   epilogues     : +bias, +residual (in place), SiLU(gate)*up (tile pairs),
+//                   f32 logits, and QKV: bias + NeoX RoPE + paged KV-cache write
+//                   (tile pairs (j, j+4) of one head hold rotation partners d, d+64).
 //
-// AWQ W4A16 variant: int4 weights packed in the same fragment order, 4 k-tiles
-// per 16-B lane load ([nt][kt/4][lane][4] uint32, nibble j = element j), with
-// group-wise (scale, scale*zero) applied in registers before the bf16 MFMA.
+// Orientation: D = Wfrag(A) x xfrag(B) -> lane holds D[n = 4(l>>4)+i][m = l&15]:
+// 4 consecutive output columns of one row -> 8-byte stores.
+//
+// AWQ W4A16 variant: int4 weights in the same fragment order, 4 k-tiles per 16-B
+// lane load ([nt][kt/4][lane][4] uint32, nibble j = element j), group-wise
+// (scale, scale*zero) applied in registers before the bf16 MFMA.
 #include "common.h"
 #include "launchers.h"
 
 namespace vgate {
 
-enum GemmEpi : int { EPI_BF16 = 0, EPI_F32 = 1, EPI_SILU = 2 };
+enum GemmEpi : int { EPI_BF16 = 0, EPI_F32 = 1, EPI_SILU = 2, EPI_QKV = 3 };
 
-// Cross-wave LDS reduction of acc[MB][NTB] + fused epilogue + store.
+struct GemmParams {
+  const bf16_t* x; int lda; int M; const int32_t* row_idx;
+  const uint4* wp; int N; int K;
+  const bf16_t* norm_w; float eps;
+  const bf16_t* bias; const bf16_t* res; int ldr;
+  void* out; int ldo;
+  int splitk; float* slabs; uint32_t* counters;
+  const int32_t* positions; const int32_t* slots; const float* cos_sin;
+  bf16_t* k_cache; bf16_t* v_cache; int hq; int hkv; int bs;
+  const bf16_t* scales; const bf16_t* zeros; int group;
+  const float* ssq_in; float* ssq_out; int ssq_parts;
+};
+
+__device__ __forceinline__ int row_of(const GemmParams& p, int m) {
+  m = m < p.M ? m : p.M - 1;  // clamp: duplicated rows are computed but never stored
+  return p.row_idx ? p.row_idx[m] : m;
+}
+
+// LDS carve (one dynamic array; Guideline 17): [reduce | inv_rms[64] | flag]
+template <int MB, int NTB>
+__host__ __device__ constexpr int red_bytes(int nw) { return nw > 1 ? nw * MB * NTB * 64 * 16 : 0; }
+
+// ---- NORM prologue: inv_rms of the block's rows, stored in LDS ----
+// Fast path (ssq_in): the kernel that produced x left deterministic per-row partial
+// sums of squares (ssq_parts floats per row) in its epilogue, so one short L2 read per
+// row replaces re-reading the whole row. A fixed group of TPR lanes owns each row and
+// reduces with xor-shuffles, so the summation order is fixed (bit-reproducible).
+// Fallback: sum x^2 over the full row (TP ranks, whose residual is all-reduced later).
+template <int MB>
+__device__ __forceinline__ void norm_prologue(const GemmParams& p, float* inv, int m_base) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (p.ssq_in) {
+    const int tpr = (int)blockDim.x / (16 * MB);  // power of two, <= 64
+    const int r = threadIdx.x / tpr, sub = threadIdx.x % tpr;
+    const float* src = p.ssq_in + (size_t)row_of(p, m_base + r) * p.ssq_parts;
+    float ss = 0.f;
+    for (int i = sub; i < p.ssq_parts; i += tpr) ss += src[i];
+    for (int o = tpr >> 1; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+    if (sub == 0) inv[r] = rsqrtf(ss / (float)p.K + p.eps);
+    __syncthreads();
+    return;
+  }
+  const int nvec = p.K >> 3;
+  for (int r = wid; r < 16 * MB; r += nw) {
+    const int m = m_base + r;
+    const uint4* xr = reinterpret_cast<const uint4*>(p.x + (size_t)row_of(p, m) * p.lda);
+    float ss = 0.f;
+    for (int c = lane; c < nvec; c += 64) {
+      float f[8];
+      unpack8(xr[c], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
+    }
+    ss = wave_reduce_sum(ss);
+    if (lane == 0) inv[r] = rsqrtf(ss / (float)p.K + p.eps);
+  }
+  __syncthreads();
+}
+
+// normalise one A fragment (8 elements of row m at column k0) in registers
+__device__ __forceinline__ uint4 norm_frag(uint4 a, float inv, const bf16_t* w, int k0) {
+  const uint4 wv = *reinterpret_cast<const uint4*>(w + k0);
+  float f[8], g[8];
+  unpack8(a, f);
+  unpack8(wv, g);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = bf2f(f2bf(f[j] * inv)) * g[j];
+  return pack8(f);
+}
+
+// ---- epilogue for one (row m, 4 columns) group; v[j] are the NTB reduced tiles ----
+template <int NTB, int EPI>
+__device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[NTB], int m, int nt0, int nsub) {
+  if constexpr (EPI == EPI_SILU) {
+    const int n = (nt0 >> 1) * 16 + nsub;
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = silu(v[0][i]) * v[NTB - 1][i];
+    uint2 pk;
+    pk.x = pack_bf2(o[0], o[1]);
+    pk.y = pack_bf2(o[2], o[3]);
+    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + n) = pk;
+  } else if constexpr (EPI == EPI_QKV) {
+    // tiles (nt0, nt0+1) = original tiles (8h + t, 8h + t + 4) of head h: columns d and d + 64
+    const int head = nt0 >> 3;
+    const int d = ((nt0 >> 1) & 3) * 16 + nsub;  // rotation index 0..63
+    float x1[4], x2[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float a = v[0][i], b = v[NTB - 1][i];
+      if (p.bias) {
+        a += bf2f(p.bias[head * 128 + d + i]);
+        b += bf2f(p.bias[head * 128 + 64 + d + i]);
+      }
+      x1[i] = bf2f(f2bf(a));  // qkv is bf16 in the reference: round before rotating
+      x2[i] = bf2f(f2bf(b));
+    }
+    if (head < p.hq + p.hkv) {  // q or k: NeoX rotation
+      const float* cs = p.cos_sin + (size_t)p.positions[m] * 128;
+      const float4 c = *reinterpret_cast<const float4*>(cs + d);
+      const float4 s = *reinterpret_cast<const float4*>(cs + 64 + d);
+      const float cc[4] = {c.x, c.y, c.z, c.w}, sn[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float a = x1[i], b = x2[i];
+        x1[i] = a * cc[i] - b * sn[i];
+        x2[i] = b * cc[i] + a * sn[i];
+      }
+    }
+    uint2 p1, p2;
+    p1.x = pack_bf2(x1[0], x1[1]); p1.y = pack_bf2(x1[2], x1[3]);
+    p2.x = pack_bf2(x2[0], x2[1]); p2.y = pack_bf2(x2[2], x2[3]);
+    if (head < p.hq) {
+      bf16_t* q = reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + head * 128 + d;
+      *reinterpret_cast<uint2*>(q) = p1;
+      *reinterpret_cast<uint2*>(q + 64) = p2;
+    } else {
+      const int slot = p.slots[m];
+      if (slot >= 0) {
+        const bool is_k = head < p.hq + p.hkv;
+        const int kh = is_k ? head - p.hq : head - p.hq - p.hkv;
+        bf16_t* dst = (is_k ? p.k_cache : p.v_cache) +
+                      (((size_t)(slot / p.bs) * p.hkv + kh) * p.bs + (slot % p.bs)) * 128 + d;
+        *reinterpret_cast<uint2*>(dst) = p1;
+        *reinterpret_cast<uint2*>(dst + 64) = p2;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NTB; ++j) {
+      const int n = (nt0 + j) * 16 + nsub;
+      float o[4] = {v[j][0], v[j][1], v[j][2], v[j][3]};
+      if (p.bias) {
+        const uint2 b = *reinterpret_cast<const uint2*>(p.bias + n);
+        o[0] += __uint_as_float(b.x << 16); o[1] += __uint_as_float(b.x & 0xffff0000u);
+        o[2] += __uint_as_float(b.y << 16); o[3] += __uint_as_float(b.y & 0xffff0000u);
+      }
+      if constexpr (EPI == EPI_F32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.out) + (size_t)m * p.ldo + n) =
+            make_float4(o[0], o[1], o[2], o[3]);
+      } else {
+        if (p.res) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] = bf2f(f2bf(o[i]));  // torch: (x@W).bf16() + res
+          const uint2 r = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldr + n);
+          o[0] += __uint_as_float(r.x << 16); o[1] += __uint_as_float(r.x & 0xffff0000u);
+          o[2] += __uint_as_float(r.y << 16); o[3] += __uint_as_float(r.y & 0xffff0000u);
+        }
+        uint2 pk;
+        pk.x = pack_bf2(o[0], o[1]);
+        pk.y = pack_bf2(o[2], o[3]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + n) = pk;
+        if (p.ssq_out) {  // partial sum of squares of the stored (bf16) values, for the next norm
+          const float a0 = __uint_as_float(pk.x << 16), a1 = __uint_as_float(pk.x & 0xffff0000u);
+          const float a2 = __uint_as_float(pk.y << 16), a3 = __uint_as_float(pk.y & 0xffff0000u);
+          p.ssq_out[(size_t)m * p.ssq_parts + (n >> 2)] = a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+        }
+      }
+    }
+  }
+}
+
+// ---- cross-wave reduction, optional in-launch split-K combine, epilogue ----
 template <int MB, int NTB, int EPI>
-__device__ __forceinline__ void gemm_finish(f32x4 (&acc)[MB][NTB], float* red, int M, int m_base,
-                                            int nt0, const bf16_t* __restrict__ bias,
-                                            const bf16_t* res, int ldr, void* out, int ldo) {
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int nw = blockDim.x >> 6;
-  constexpr int SLOTS = MB * NTB * 64;  // f32x4 slots per wave
-  f32x4* red4 = reinterpret_cast<f32x4*>(red);
+__device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB][NTB], char* smem, int m_base,
+                                            int nt0) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  constexpr int SLOTS = MB * NTB * 64;  // f32x4 slots per block tile
+  f32x4* red4 = reinterpret_cast<f32x4*>(smem);
+  int* flag = reinterpret_cast<int*>(smem + red_bytes<MB, NTB>(nw) + 256);
   if (nw > 1) {
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
       for (int j = 0; j < NTB; ++j) red4[wid * SLOTS + (mb * NTB + j) * 64 + lane] = acc[mb][j];
     __syncthreads();
+  }
+  const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+  if (p.splitk > 1) {
+    // 1) this slice's partial tile -> fp32 slab [tile][slice][SLOTS]
+    f32x4* slab = reinterpret_cast<f32x4*>(p.slabs) + ((size_t)tile * p.splitk + blockIdx.z) * SLOTS;
+    for (int s = threadIdx.x; s < SLOTS; s += blockDim.x) {
+      f32x4 t;
+      if (nw > 1) {
+        t = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int w = 0; w < nw; ++w) t += red4[w * SLOTS + s];
+      } else {
+        const int mb = s / (NTB * 64), j = (s / 64) % NTB;
+        t = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int a = 0; a < MB; ++a)
+#pragma unroll
+          for (int b = 0; b < NTB; ++b)
+            if (a == mb && b == j) t = acc[a][b];
+      }
+      slab[s] = t;
+    }
+    // 2) publish: every wave drains its stores, one agent-scope release, one ticket
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t old = __hip_atomic_fetch_add(p.counters + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (old == (uint32_t)(p.splitk - 1));
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(p.counters + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    // 3) the last arriver sums every slice's slab (plain loads behind the acquire)
+    const f32x4* all = reinterpret_cast<const f32x4*>(p.slabs) + (size_t)tile * p.splitk * SLOTS;
+    for (int s = threadIdx.x; s < MB * 64; s += blockDim.x) {
+      const int mb = s >> 6, l = s & 63;
+      const int m = m_base + mb * 16 + (l & 15);
+      f32x4 v[NTB];
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) {
+        f32x4 t = {0.f, 0.f, 0.f, 0.f};
+        for (int z = 0; z < p.splitk; ++z) t += all[(size_t)z * SLOTS + (mb * NTB + j) * 64 + l];
+        v[j] = t;
+      }
+      if (m < p.M) epilogue<NTB, EPI>(p, v, m, nt0, 4 * (l >> 4));
+    }
+    return;
   }
   for (int s = threadIdx.x; s < MB * 64; s += blockDim.x) {
     const int mb = s >> 6, l = s & 63;
@@ -61,95 +284,46 @@ __device__ __forceinline__ void gemm_finish(f32x4 (&acc)[MB][NTB], float* red, i
         v[j] = t;
       }
     } else {
-      // single-wave block (thread == lane): select this m-block's registers statically
 #pragma unroll
       for (int mm = 0; mm < MB; ++mm)
         if (mm == mb)
 #pragma unroll
           for (int j = 0; j < NTB; ++j) v[j] = acc[mm][j];
     }
-    if (m >= M) continue;
-    const int nsub = 4 * (l >> 4);
-    if constexpr (EPI == EPI_SILU) {
-      static_assert(NTB == 2, "silu epilogue pairs a gate tile with an up tile");
-      const int n = (nt0 >> 1) * 16 + nsub;  // output column (N/2 wide)
-      float o[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) o[i] = silu(v[0][i]) * v[1][i];
-      bf16_t* op = reinterpret_cast<bf16_t*>(out) + (size_t)m * ldo + n;
-      uint2 pk;
-      pk.x = pack_bf2(o[0], o[1]);
-      pk.y = pack_bf2(o[2], o[3]);
-      *reinterpret_cast<uint2*>(op) = pk;
-    } else {
-#pragma unroll
-      for (int j = 0; j < NTB; ++j) {
-        const int n = (nt0 + j) * 16 + nsub;
-        float o[4] = {v[j][0], v[j][1], v[j][2], v[j][3]};
-        if (bias) {
-          const uint2 b = *reinterpret_cast<const uint2*>(bias + n);
-          o[0] += __uint_as_float(b.x << 16); o[1] += __uint_as_float(b.x & 0xffff0000u);
-          o[2] += __uint_as_float(b.y << 16); o[3] += __uint_as_float(b.y & 0xffff0000u);
-        }
-        if constexpr (EPI == EPI_F32) {
-          float* op = reinterpret_cast<float*>(out) + (size_t)m * ldo + n;
-          *reinterpret_cast<float4*>(op) = make_float4(o[0], o[1], o[2], o[3]);
-        } else {
-          if (res) {
-            // round the GEMM result to bf16 first (matches torch: (x@W).bf16() + res)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) o[i] = bf2f(f2bf(o[i]));
-            const uint2 r = *reinterpret_cast<const uint2*>(res + (size_t)m * ldr + n);
-            o[0] += __uint_as_float(r.x << 16); o[1] += __uint_as_float(r.x & 0xffff0000u);
-            o[2] += __uint_as_float(r.y << 16); o[3] += __uint_as_float(r.y & 0xffff0000u);
-          }
-          bf16_t* op = reinterpret_cast<bf16_t*>(out) + (size_t)m * ldo + n;
-          uint2 pk;
-          pk.x = pack_bf2(o[0], o[1]);
-          pk.y = pack_bf2(o[2], o[3]);
-          *reinterpret_cast<uint2*>(op) = pk;
-        }
-      }
-    }
+    if (m < p.M) epilogue<NTB, EPI>(p, v, m, nt0, 4 * (l >> 4));
   }
 }
 
-template <int MB>
-__device__ __forceinline__ void x_rows(const bf16_t* (&xrow)[MB], const bf16_t* x, int lda, int M,
-                                       int m_base, int lane) {
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb) {
-    int m = m_base + mb * 16 + (lane & 15);
-    m = m < M ? m : M - 1;  // clamp: duplicated rows are computed but never stored
-    xrow[mb] = x + (size_t)m * lda + 8 * (lane >> 4);
-  }
-}
-
-template <int MB, int NTB, int U, int EPI>
-__global__ __launch_bounds__(1024) void gemm_skinny_kernel(
-    const bf16_t* __restrict__ x, int lda, int M, const uint4* __restrict__ Wp, int N, int K,
-    const bf16_t* __restrict__ bias, const bf16_t* res, int ldr, void* out, int ldo) {
-  extern __shared__ __attribute__((aligned(16))) float red[];
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int nw = blockDim.x >> 6;
-  const int KT = K >> 5;
+template <int MB, int NTB, int U, int EPI, bool NORM>
+__global__ __launch_bounds__(1024) void gemm_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int KT = p.K >> 5;
   const int nt0 = blockIdx.x * NTB;
   const int m_base = blockIdx.y * 16 * MB;
-  const int kbeg = (KT * wid) / nw;
-  const int kend = (KT * (wid + 1)) / nw;
+  // this block's k-slice, then this wave's contiguous range inside it
+  const int s0 = (KT * blockIdx.z) / p.splitk, s1 = (KT * (blockIdx.z + 1)) / p.splitk;
+  const int kbeg = s0 + ((s1 - s0) * wid) / nw;
+  const int kend = s0 + ((s1 - s0) * (wid + 1)) / nw;
+  float* inv = reinterpret_cast<float*>(smem + red_bytes<MB, NTB>(nw));
+  if constexpr (NORM) norm_prologue<MB>(p, inv, m_base);
 
   f32x4 acc[MB][NTB];
 #pragma unroll
   for (int a = 0; a < MB; ++a)
 #pragma unroll
     for (int b = 0; b < NTB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-
   const uint4* wbase[NTB];
 #pragma unroll
-  for (int j = 0; j < NTB; ++j) wbase[j] = Wp + ((size_t)(nt0 + j) * KT) * 64 + lane;
+  for (int j = 0; j < NTB; ++j) wbase[j] = p.wp + ((size_t)(nt0 + j) * KT) * 64 + lane;
   const bf16_t* xrow[MB];
-  x_rows<MB>(xrow, x, lda, M, m_base, lane);
+  float rinv[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    xrow[mb] = p.x + (size_t)row_of(p, m_base + mb * 16 + (lane & 15)) * p.lda + 8 * (lane >> 4);
+    rinv[mb] = NORM ? inv[mb * 16 + (lane & 15)] : 1.f;
+  }
+  const bf16_t* nw_ptr = p.norm_w + 8 * (lane >> 4);
 
   int kt = kbeg;
   for (; kt + U <= kend; kt += U) {
@@ -162,32 +336,38 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb)
-        a[u][mb] = *reinterpret_cast<const uint4*>(xrow[mb] + (kt + u) * 32);
+      for (int mb = 0; mb < MB; ++mb) a[u][mb] = *reinterpret_cast<const uint4*>(xrow[mb] + (kt + u) * 32);
+    if constexpr (NORM) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) a[u][mb] = norm_frag(a[u][mb], rinv[mb], nw_ptr, (kt + u) * 32);
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int j = 0; j < NTB; ++j)
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb)
-          acc[mb][j] = mfma16(as_bf16x8(b[u][j]), as_bf16x8(a[u][mb]), acc[mb][j]);
+        for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(as_bf16x8(b[u][j]), as_bf16x8(a[u][mb]), acc[mb][j]);
   }
   for (; kt < kend; ++kt) {
     uint4 b[NTB], a[MB];
 #pragma unroll
     for (int j = 0; j < NTB; ++j) b[j] = ld_nt16(wbase[j] + (size_t)kt * 64);
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) a[mb] = *reinterpret_cast<const uint4*>(xrow[mb] + kt * 32);
+    for (int mb = 0; mb < MB; ++mb) {
+      a[mb] = *reinterpret_cast<const uint4*>(xrow[mb] + kt * 32);
+      if constexpr (NORM) a[mb] = norm_frag(a[mb], rinv[mb], nw_ptr, kt * 32);
+    }
 #pragma unroll
     for (int j = 0; j < NTB; ++j)
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(as_bf16x8(b[j]), as_bf16x8(a[mb]), acc[mb][j]);
   }
-  gemm_finish<MB, NTB, EPI>(acc, red, M, m_base, nt0, bias, res, ldr, out, ldo);
+  gemm_finish<MB, NTB, EPI>(p, acc, smem, m_base, nt0);
 }
 
 // ---- AWQ W4A16 ----
-// dequant 8 nibbles of one 32-bit word: w = q * s - sz  (sz = s * zero)
 __device__ __forceinline__ bf16x8 dq8(uint32_t q, float s, float sz) {
   bf16x8 r;
 #pragma unroll
@@ -195,37 +375,43 @@ __device__ __forceinline__ bf16x8 dq8(uint32_t q, float s, float sz) {
   return r;
 }
 
-template <int MB, int NTB, int EPI>
-__global__ __launch_bounds__(1024) void awq_gemm_kernel(
-    const bf16_t* __restrict__ x, int lda, int M, const uint4* __restrict__ qw,
-    const bf16_t* __restrict__ scales, const bf16_t* __restrict__ zeros, int group, int N, int K,
-    const bf16_t* __restrict__ bias, const bf16_t* res, int ldr, void* out, int ldo) {
-  extern __shared__ __attribute__((aligned(16))) float red[];
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int nw = blockDim.x >> 6;
-  const int KQ = K >> 7;  // 128-wide k quads (4 k-tiles per 16-B lane load)
+template <int MB, int NTB, int EPI, bool NORM>
+__global__ __launch_bounds__(1024) void awq_gemm_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int KQ = p.K >> 7;
   const int nt0 = blockIdx.x * NTB;
   const int m_base = blockIdx.y * 16 * MB;
-  const int qbeg = (KQ * wid) / nw;
-  const int qend = (KQ * (wid + 1)) / nw;
+  const int s0 = (KQ * blockIdx.z) / p.splitk, s1 = (KQ * (blockIdx.z + 1)) / p.splitk;
+  const int qbeg = s0 + ((s1 - s0) * wid) / nw;
+  const int qend = s0 + ((s1 - s0) * (wid + 1)) / nw;
+  float* inv = reinterpret_cast<float*>(smem + red_bytes<MB, NTB>(nw));
+  if constexpr (NORM) norm_prologue<MB>(p, inv, m_base);
   f32x4 acc[MB][NTB];
 #pragma unroll
   for (int a = 0; a < MB; ++a)
 #pragma unroll
     for (int b = 0; b < NTB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   const bf16_t* xrow[MB];
-  x_rows<MB>(xrow, x, lda, M, m_base, lane);
+  float rinv[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    xrow[mb] = p.x + (size_t)row_of(p, m_base + mb * 16 + (lane & 15)) * p.lda + 8 * (lane >> 4);
+    rinv[mb] = NORM ? inv[mb * 16 + (lane & 15)] : 1.f;
+  }
+  const bf16_t* nw_ptr = p.norm_w + 8 * (lane >> 4);
   for (int kq = qbeg; kq < qend; ++kq) {
     uint4 w[NTB];
 #pragma unroll
-    for (int j = 0; j < NTB; ++j) w[j] = ld_nt16(qw + ((size_t)(nt0 + j) * KQ + kq) * 64 + lane);
+    for (int j = 0; j < NTB; ++j) w[j] = ld_nt16(p.wp + ((size_t)(nt0 + j) * KQ + kq) * 64 + lane);
     uint4 a[4][MB];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb)
+      for (int mb = 0; mb < MB; ++mb) {
         a[u][mb] = *reinterpret_cast<const uint4*>(xrow[mb] + (kq * 4 + u) * 32);
+        if constexpr (NORM) a[u][mb] = norm_frag(a[u][mb], rinv[mb], nw_ptr, (kq * 4 + u) * 32);
+      }
 #pragma unroll
     for (int j = 0; j < NTB; ++j) {
       const int n = (nt0 + j) * 16 + (lane & 15);
@@ -233,84 +419,113 @@ __global__ __launch_bounds__(1024) void awq_gemm_kernel(
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int k = (kq * 4 + u) * 32 + 8 * (lane >> 4);
-        const int gi = k / group;
-        const float s = bf2f(scales[(size_t)gi * N + n]);
-        const float sz = bf2f(zeros[(size_t)gi * N + n]);
+        const int gi = k / p.group;
+        const float s = bf2f(p.scales[(size_t)gi * p.N + n]);
+        const float sz = bf2f(p.zeros[(size_t)gi * p.N + n]);
         const bf16x8 wf = dq8(wq[u], s, sz);
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(wf, as_bf16x8(a[u][mb]), acc[mb][j]);
       }
     }
   }
-  gemm_finish<MB, NTB, EPI>(acc, red, M, m_base, nt0, bias, res, ldr, out, ldo);
+  gemm_finish<MB, NTB, EPI>(p, acc, smem, m_base, nt0);
 }
 
-static int pick_waves(int total_blocks, int ksteps, int mb, int ntb, int forced) {
-  if (forced > 0) return forced;
-  int w = 1;
-  while (w < 16 && total_blocks * w < 4096) w <<= 1;
-  while (w > 1 && ksteps / w < 4) w >>= 1;
-  while (w > 1 && w * mb * ntb > 64) w >>= 1;
-  return w;
+// ------------------------------------------------------------------ host side
+struct Plan { int waves, splitk; };
+
+// Decomposition from the MI355X sweep (benchmarks/micro_gpu.py, M=8, in-graph timing;
+// profiles/r1_gemm_sweep.log): 8 waves per block without split-K is best for the
+// small projections (qkv 3.5 us, o_proj 3.6 us — at the ~1.8 us launch floor plus one
+// HBM round trip); 4 waves for the >= 512-block GEMMs (gate_up 4.7 TB/s, LM head
+// 6.7 TB/s); split-K (release/acquire + slab round trip) only pays for few tiles x very
+// long K (down_proj: 96 tiles x 280 k-steps, 16 waves x 2 slices).
+static Plan plan(int nblk, int mchunks, int ksteps, int MB, int NTB, int force_w, int force_s) {
+  const int blocks = nblk * mchunks;
+  int w = blocks >= 512 ? 4 : 8;
+  int s = 1;
+  if (blocks < 256 && ksteps >= 192) {
+    w = 16;
+    s = 2;
+  }
+  while (w > 1 && ksteps / (w * s) < 2) w >>= 1;
+  while (w > 1 && w * MB * NTB > 64) w >>= 1;
+  if (force_s > 0) s = force_s;
+  if (force_w > 0) w = force_w;
+  return {w, s};
 }
 
-template <int MB, int NTB, int EPI>
-static void launch_mb(const GemmArgs& g, hipStream_t st) {
-  const int KT = g.K / 32;
-  const int nblk = g.N / 16 / NTB;
+template <int MB, int NTB, int EPI, bool NORM, bool AWQ>
+static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
+  const int ntiles = g.N / 16;
+  const int nblk = ntiles / NTB;
   const int mchunks = (g.M + 16 * MB - 1) / (16 * MB);
-  const int w = pick_waves(nblk * mchunks, KT, MB, NTB, g.waves);
-  const size_t lds = (w > 1) ? (size_t)w * MB * NTB * 64 * 16 : 0;
-  hipLaunchKernelGGL((gemm_skinny_kernel<MB, NTB, 4, EPI>), dim3(nblk, mchunks), dim3(64 * w), lds, st,
-                     g.x, g.lda, g.M, reinterpret_cast<const uint4*>(g.wp), g.N, g.K, g.bias, g.res,
-                     g.ldr, g.out, g.ldo);
+  const int ksteps = AWQ ? g.K / 128 : g.K / 32;
+  Plan pl = plan(nblk, mchunks, ksteps, MB, NTB, g.waves, g.splitk);
+  const size_t need_slab = (size_t)nblk * mchunks * pl.splitk * MB * NTB * 64 * 16;
+  if (pl.splitk > 1 && (g.slabs == nullptr || need_slab > g.slab_bytes || nblk * mchunks > g.max_counters))
+    pl.splitk = 1;  // workspace too small: fall back to one slice (still correct)
+  p.splitk = pl.splitk;
+  const size_t lds = red_bytes<MB, NTB>(pl.waves) + 256 + 16;
+  dim3 grid(nblk, mchunks, pl.splitk), block(64 * pl.waves);
+  if constexpr (AWQ)
+    hipLaunchKernelGGL((awq_gemm_kernel<MB, NTB, EPI, NORM>), grid, block, lds, st, p);
+  else
+    hipLaunchKernelGGL((gemm_kernel<MB, NTB, 4, EPI, NORM>), grid, block, lds, st, p);
 }
 
-template <int NTB, int EPI>
-static void launch_ntb(const GemmArgs& g, hipStream_t st) {
-  if (g.M <= 16) launch_mb<1, NTB, EPI>(g, st);
-  else if (g.M <= 32) launch_mb<2, NTB, EPI>(g, st);
-  else launch_mb<4, NTB, EPI>(g, st);
+template <int NTB, int EPI, bool NORM, bool AWQ>
+static void launch_m(GemmParams p, const GemmArgs& g, hipStream_t st) {
+  if (g.M <= 16) launch_one<1, NTB, EPI, NORM, AWQ>(p, g, st);
+  else if (g.M <= 32) launch_one<2, NTB, EPI, NORM, AWQ>(p, g, st);
+  else launch_one<4, NTB, EPI, NORM, AWQ>(p, g, st);
+}
+
+template <bool AWQ>
+static void launch_dispatch(GemmParams p, const GemmArgs& g, hipStream_t st) {
+  const bool norm = g.norm_w != nullptr;
+  const int ntiles = g.N / 16;
+  const bool pair = ntiles % 2 == 0 && ntiles >= 1024;
+#define VG_NORM(NTB_, EPI_)                                                     \
+  do {                                                                          \
+    if (norm) launch_m<NTB_, EPI_, true, AWQ>(p, g, st);                        \
+    else launch_m<NTB_, EPI_, false, AWQ>(p, g, st);                            \
+  } while (0)
+  switch (g.epi) {
+    case EPI_SILU: VG_NORM(2, EPI_SILU); break;
+    case EPI_QKV: VG_NORM(2, EPI_QKV); break;
+    case EPI_F32:
+      if (pair) VG_NORM(2, EPI_F32); else VG_NORM(1, EPI_F32);
+      break;
+    default:
+      if (pair) VG_NORM(2, EPI_BF16); else VG_NORM(1, EPI_BF16);
+  }
+#undef VG_NORM
+}
+
+static GemmParams to_params(const GemmArgs& g) {
+  GemmParams p{};
+  p.x = g.x; p.lda = g.lda; p.M = g.M; p.row_idx = g.row_idx;
+  p.wp = reinterpret_cast<const uint4*>(g.wp); p.N = g.N; p.K = g.K;
+  p.norm_w = g.norm_w; p.eps = g.eps;
+  p.bias = g.bias; p.res = g.res; p.ldr = g.ldr;
+  p.out = g.out; p.ldo = g.ldo;
+  p.slabs = g.slabs; p.counters = g.counters;
+  p.positions = g.positions; p.slots = g.slots; p.cos_sin = g.cos_sin;
+  p.k_cache = g.k_cache; p.v_cache = g.v_cache; p.hq = g.hq; p.hkv = g.hkv; p.bs = g.bs;
+  p.scales = g.scales; p.zeros = g.zeros; p.group = g.group;
+  p.ssq_in = g.ssq_in; p.ssq_out = g.ssq_out; p.ssq_parts = g.ssq_parts;
+  return p;
 }
 
 void launch_gemm(const GemmArgs& g, hipStream_t st) {
   if (g.M <= 0) return;
-  const int ntiles = g.N / 16;
-  if (g.epi == EPI_SILU) {
-    launch_ntb<2, EPI_SILU>(g, st);
-  } else if (g.epi == EPI_F32) {
-    if (ntiles % 2 == 0 && ntiles >= 1024) launch_ntb<2, EPI_F32>(g, st);
-    else launch_ntb<1, EPI_F32>(g, st);
-  } else {
-    if (ntiles % 2 == 0 && ntiles >= 1024) launch_ntb<2, EPI_BF16>(g, st);
-    else launch_ntb<1, EPI_BF16>(g, st);
-  }
+  launch_dispatch<false>(to_params(g), g, st);
 }
 
-template <int MB, int NTB, int EPI>
-static void awq_launch_mb(const AwqGemmArgs& g, hipStream_t st) {
-  const int KQ = g.K / 128;
-  const int nblk = g.N / 16 / NTB;
-  const int mchunks = (g.M + 16 * MB - 1) / (16 * MB);
-  const int w = pick_waves(nblk * mchunks, KQ * 2, MB, NTB, 0);
-  const size_t lds = (w > 1) ? (size_t)w * MB * NTB * 64 * 16 : 0;
-  hipLaunchKernelGGL((awq_gemm_kernel<MB, NTB, EPI>), dim3(nblk, mchunks), dim3(64 * w), lds, st, g.x,
-                     g.lda, g.M, reinterpret_cast<const uint4*>(g.qw), g.scales, g.zeros, g.group,
-                     g.N, g.K, g.bias, g.res, g.ldr, g.out, g.ldo);
-}
-
-template <int NTB, int EPI>
-static void awq_launch_ntb(const AwqGemmArgs& g, hipStream_t st) {
-  if (g.M <= 16) awq_launch_mb<1, NTB, EPI>(g, st);
-  else if (g.M <= 32) awq_launch_mb<2, NTB, EPI>(g, st);
-  else awq_launch_mb<4, NTB, EPI>(g, st);
-}
-
-void launch_awq_gemm(const AwqGemmArgs& g, hipStream_t st) {
+void launch_awq_gemm(const GemmArgs& g, hipStream_t st) {
   if (g.M <= 0) return;
-  if (g.epi == EPI_SILU) awq_launch_ntb<2, EPI_SILU>(g, st);
-  else if (g.epi == EPI_F32) awq_launch_ntb<1, EPI_F32>(g, st);
-  else awq_launch_ntb<1, EPI_BF16>(g, st);
+  launch_dispatch<true>(to_params(g), g, st);
 }
 
 }  // namespace vgate

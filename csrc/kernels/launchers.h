@@ -8,40 +8,47 @@
 namespace vgate {
 
 struct GemmArgs {
-  const uint16_t* x;  // [M, K] bf16, row stride lda
+  const uint16_t* x;  // [M, K] bf16, row stride lda (rows gathered through row_idx if set)
   int lda;
   int M;
-  const void* wp;     // fragment-packed weight [N/16][K/32][64][8] bf16
+  const int32_t* row_idx;  // optional [M] row gather (LM head over sampled rows)
+  const void* wp;     // fragment-packed weight (bf16 [N/16][K/32][64][8] or AWQ int4 [N/16][K/128][64][4])
   int N;
   int K;
+  const uint16_t* norm_w;  // optional fused RMSNorm prologue weight [K]
+  float eps;
   const uint16_t* bias;  // [N] bf16 or null
   const uint16_t* res;   // residual [M, N] bf16 (stride ldr) or null; may alias out
   int ldr;
-  void* out;          // bf16 [M, N] (or [M, N/2] for silu, f32 for EPI_F32)
+  void* out;          // bf16 [M, N] (silu: [M, N/2]; f32 for EPI_F32; qkv: q [M, hq*128])
   int ldo;
-  int epi;            // 0 bf16, 1 f32, 2 silu*mul (gate/up tiles interleaved)
-  int waves;          // 0 = auto
+  int epi;            // 0 bf16, 1 f32, 2 silu*mul (gate/up tiles interleaved), 3 qkv+rope+kv-write
+  int waves;          // 0 = heuristic
+  int splitk;         // 0 = heuristic
+  float* slabs;       // split-K fp32 partial slabs (workspace) or null
+  size_t slab_bytes;
+  uint32_t* counters; // split-K arrival tickets, zero-initialised, self-resetting
+  int max_counters;
+  // EPI_QKV
+  const int32_t* positions;
+  const int32_t* slots;
+  const float* cos_sin;  // [max_pos, 128] f32
+  uint16_t* k_cache;
+  uint16_t* v_cache;
+  int hq;
+  int hkv;
+  int bs;
+  // AWQ
+  const uint16_t* scales;  // [K/group][N] bf16
+  const uint16_t* zeros;   // [K/group][N] bf16 (= scale * zero)
+  int group;
+  // residual-stream sum-of-squares hand-off for the fused RMSNorm prologue
+  const float* ssq_in;  // [M][ssq_parts] partials written by the producer of x (or null)
+  float* ssq_out;       // this GEMM's residual epilogue writes [M][N/4] partials (or null)
+  int ssq_parts;        // partials per row (= hidden / 4)
 };
 void launch_gemm(const GemmArgs& g, hipStream_t st);
-
-struct AwqGemmArgs {
-  const uint16_t* x;
-  int lda;
-  int M;
-  const uint32_t* qw;      // packed int4, fragment-major [N/16][K/32][64] uint32 (8 nibbles)
-  const uint16_t* scales;  // [K/group][N] bf16
-  const uint16_t* zeros;   // [K/group][N] bf16 (already scale*zero)
-  int group;
-  int N;
-  int K;
-  const uint16_t* bias;
-  const uint16_t* res;
-  int ldr;
-  void* out;
-  int ldo;
-  int epi;
-};
-void launch_awq_gemm(const AwqGemmArgs& g, hipStream_t st);
+void launch_awq_gemm(const GemmArgs& g, hipStream_t st);
 
 // y = rmsnorm(x) * w ; if res != null: res = x + res (in place) and the norm is of the sum.
 void launch_rmsnorm(const uint16_t* x, int ldx, uint16_t* res, int ldres, const uint16_t* w,
@@ -49,7 +56,7 @@ void launch_rmsnorm(const uint16_t* x, int ldx, uint16_t* res, int ldres, const 
 
 // Embedding gather with vocab-shard masking (TP): rows outside [vstart, vstart+vrows) -> 0.
 void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int T, int H,
-                      int vstart, int vrows, hipStream_t st);
+                      int vstart, int vrows, hipStream_t st, float* ssq_out = nullptr);
 
 // NeoX RoPE on q,k inside the fused qkv buffer + paged KV-cache write.
 // qkv: [T, (Hq + 2*Hkv) * D]; cos_sin: [max_pos, D] f32 (cos | sin halves)
@@ -86,6 +93,9 @@ struct AttnArgs {
 };
 void launch_attn_decode(const AttnArgs& a, hipStream_t st);
 void launch_attn_prefill(const AttnArgs& a, hipStream_t st);
+// One launch for a mixed step: decode blocks for sequences [0, dec_seqs) (only those
+// with a single query token do work) + prefill tiles (tile_seq < 0 = padding).
+void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st);
 
 struct SampleArgs {
   const float* logits;  // [B, V] f32, row stride ldl

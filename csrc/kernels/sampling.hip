@@ -70,17 +70,19 @@ __device__ __forceinline__ float block_excl_scan(float v, float* sw, float& tota
 // U vectors in flight per iteration (latency hiding: a 1024-thread block on one CU
 // needs many bytes in flight to stream a 600 KB row at L2/HBM rate).
 #define ROW_SWEEP(BODY)                                                        \
-  for (int v0 = tid; v0 < V4; v0 += nt * 4) {                                  \
-    float4 q_[4];                                                              \
-    _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {                         \
+  for (int v0 = tid; v0 < V4; v0 += nt * 8) {                                  \
+    float4 q_[8];                                                              \
+    /* clamped, unconditional loads: no per-element branch/vmcnt(0) (guide §5 trap c) */ \
+    _Pragma("unroll") for (int u_ = 0; u_ < 8; ++u_) {                         \
       const int vi_ = v0 + u_ * nt;                                            \
-      q_[u_] = vi_ < V4 ? x4[vi_] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY); \
+      q_[u_] = x4[vi_ < V4 ? vi_ : V4 - 1];                                    \
     }                                                                          \
-    _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) {                         \
+    _Pragma("unroll") for (int u_ = 0; u_ < 8; ++u_) {                         \
       const int vi_ = v0 + u_ * nt;                                            \
+      const bool ok_ = vi_ < V4;                                               \
       const float e_[4] = {q_[u_].x, q_[u_].y, q_[u_].z, q_[u_].w};            \
       _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) {                       \
-        const float v = e_[j_];                                                \
+        const float v = ok_ ? e_[j_] : -INFINITY;                              \
         const int i = 4 * vi_ + j_;                                            \
         (void)i;                                                               \
         BODY                                                                   \

@@ -32,60 +32,101 @@ const uint16_t* opt_bf16(const c10::optional<Tensor>& t) {
   return reinterpret_cast<const uint16_t*>(t->data_ptr());
 }
 
-// out = epi(x @ W^T); W is fragment-packed [N/16, K/32, 64, 8]
-void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K,
-          const c10::optional<Tensor>& bias, const c10::optional<Tensor>& res, Tensor& out,
-          int64_t epi, int64_t waves) {
+template <typename T>
+T* opt_ptr(const c10::optional<Tensor>& t, c10::ScalarType dt, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t->scalar_type() == dt, name, " has wrong dtype ", t->scalar_type());
+  return reinterpret_cast<T*>(t->data_ptr());
+}
+
+// out = epilogue(prologue(x) @ W^T); W fragment-packed [N/16, K/32, 64, 8] bf16, or AWQ
+// int4 [N/16, K/128, 64, 4] int32 with scales/zeros. ws = int32 workspace: [0, 65536)
+// split-K tickets (zeroed once, self-resetting), the rest fp32 slabs.
+void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, int64_t epi,
+          const c10::optional<Tensor>& bias, const c10::optional<Tensor>& res,
+          const c10::optional<Tensor>& norm_w, double eps, const c10::optional<Tensor>& row_idx,
+          const c10::optional<Tensor>& ws, int64_t waves, int64_t splitk,
+          const c10::optional<Tensor>& positions, const c10::optional<Tensor>& slots,
+          const c10::optional<Tensor>& cos_sin, const c10::optional<Tensor>& k_cache,
+          const c10::optional<Tensor>& v_cache, int64_t hq, int64_t hkv,
+          const c10::optional<Tensor>& awq_scales, const c10::optional<Tensor>& awq_zeros, int64_t group,
+          const c10::optional<Tensor>& ssq_in, const c10::optional<Tensor>& ssq_out) {
   CHECK_DEV(x); CHECK_DEV(wp); CHECK_DEV(out);
   CHECK_DT(x, torch::kBFloat16);
-  CHECK_DT(wp, torch::kBFloat16);
   CHECK_LASTDIM(x); CHECK_LASTDIM(out);
   TORCH_CHECK(x.dim() == 2 && out.dim() == 2, "gemm: x/out must be 2-D");
   TORCH_CHECK(K % 32 == 0 && N % 16 == 0, "gemm: K%32 / N%16");
   TORCH_CHECK(x.size(1) >= K, "gemm: x has ", x.size(1), " cols < K=", K);
-  TORCH_CHECK(wp.numel() == N * K, "gemm: packed weight numel mismatch");
-  const int64_t M = x.size(0);
-  TORCH_CHECK(out.size(0) >= M, "gemm: out rows");
+  const bool awq = awq_scales.has_value() && awq_scales->defined();
+  if (awq) {
+    CHECK_DT(wp, torch::kInt32);
+    TORCH_CHECK(K % 128 == 0 && K % group == 0 && group % 32 == 0, "awq: K/group");
+    TORCH_CHECK(wp.numel() == N * K / 8, "awq: packed qweight numel");
+    TORCH_CHECK(awq_scales->size(0) == K / group && awq_scales->size(1) == N, "awq: scales shape");
+  } else {
+    CHECK_DT(wp, torch::kBFloat16);
+    TORCH_CHECK(wp.numel() == N * K, "gemm: packed weight numel mismatch");
+  }
+  int64_t M = x.size(0);
+  const int32_t* ridx = opt_ptr<const int32_t>(row_idx, torch::kInt32, "row_idx");
+  if (ridx) M = row_idx->numel();
   const int64_t ncols = (epi == 2) ? N / 2 : N;
-  TORCH_CHECK(out.size(1) >= ncols, "gemm: out cols");
-  if (epi == 2) TORCH_CHECK((N / 16) % 2 == 0, "silu gemm needs an even tile count");
   if (epi == 1) CHECK_DT(out, torch::kFloat32); else CHECK_DT(out, torch::kBFloat16);
-  vgate::GemmArgs g;
-  g.x = bf16p(x); g.lda = (int)x.stride(0); g.M = (int)M;
+  if (epi == 2 || epi == 3) TORCH_CHECK((N / 16) % 2 == 0, "paired-tile epilogue needs an even tile count");
+  if (epi == 3) {
+    TORCH_CHECK(N == (hq + 2 * hkv) * 128, "qkv epilogue: N must be (hq + 2 hkv) * 128");
+    TORCH_CHECK(out.size(1) >= hq * 128, "qkv epilogue: q out cols");
+    TORCH_CHECK(positions.has_value() && slots.has_value() && cos_sin.has_value() && k_cache.has_value() &&
+                v_cache.has_value(), "qkv epilogue needs positions/slots/cos_sin/k_cache/v_cache");
+    TORCH_CHECK(k_cache->dim() == 4 && k_cache->size(1) == hkv && k_cache->size(3) == 128, "qkv: cache shape");
+    TORCH_CHECK(cos_sin->size(1) == 128, "qkv: cos_sin must be [max_pos, 128]");
+  } else {
+    TORCH_CHECK(out.size(1) >= ncols, "gemm: out cols");
+  }
+  TORCH_CHECK(out.size(0) >= M, "gemm: out rows");
+  vgate::GemmArgs g{};
+  g.x = bf16p(x); g.lda = (int)x.stride(0); g.M = (int)M; g.row_idx = ridx;
   g.wp = wp.data_ptr(); g.N = (int)N; g.K = (int)K;
+  g.norm_w = opt_bf16(norm_w); g.eps = (float)eps;
+  if (g.norm_w) TORCH_CHECK(norm_w->numel() == K, "norm_w must have K elements");
   g.bias = opt_bf16(bias);
   g.res = opt_bf16(res);
-  g.ldr = res.has_value() && res->defined() ? (int)res->stride(0) : 0;
+  g.ldr = g.res ? (int)res->stride(0) : 0;
   if (g.res) TORCH_CHECK(res->size(0) >= M && res->size(1) >= N, "gemm: residual shape");
   g.out = out.data_ptr(); g.ldo = (int)out.stride(0);
-  g.epi = (int)epi; g.waves = (int)waves;
+  g.epi = (int)epi; g.waves = (int)waves; g.splitk = (int)splitk;
+  if (ws.has_value() && ws->defined()) {
+    CHECK_DEV(*ws); CHECK_DT(*ws, torch::kInt32);
+    TORCH_CHECK(ws->numel() > 65536 * 2, "gemm: workspace too small");
+    g.counters = reinterpret_cast<uint32_t*>(ws->data_ptr());
+    g.max_counters = 65536;
+    g.slabs = reinterpret_cast<float*>(reinterpret_cast<int32_t*>(ws->data_ptr()) + 65536);
+    g.slab_bytes = (size_t)(ws->numel() - 65536) * 4;
+  }
+  g.positions = opt_ptr<const int32_t>(positions, torch::kInt32, "positions");
+  g.slots = opt_ptr<const int32_t>(slots, torch::kInt32, "slots");
+  g.cos_sin = opt_ptr<const float>(cos_sin, torch::kFloat32, "cos_sin");
+  g.k_cache = opt_ptr<uint16_t>(k_cache, torch::kBFloat16, "k_cache");
+  g.v_cache = opt_ptr<uint16_t>(v_cache, torch::kBFloat16, "v_cache");
+  g.hq = (int)hq; g.hkv = (int)hkv; g.bs = k_cache.has_value() && k_cache->defined() ? (int)k_cache->size(2) : 16;
+  g.scales = opt_bf16(awq_scales); g.zeros = opt_bf16(awq_zeros); g.group = (int)group;
+  g.ssq_in = opt_ptr<const float>(ssq_in, torch::kFloat32, "ssq_in");
+  g.ssq_out = opt_ptr<float>(ssq_out, torch::kFloat32, "ssq_out");
+  if (g.ssq_in) {
+    TORCH_CHECK(g.norm_w, "ssq_in requires norm_w");
+    TORCH_CHECK(ssq_in->dim() == 2 && ssq_in->size(1) == K / 4 && ssq_in->is_contiguous(), "ssq_in must be [rows, K/4]");
+    g.ssq_parts = (int)(K / 4);
+  }
+  if (g.ssq_out) {
+    TORCH_CHECK(epi == 0 && g.res, "ssq_out is produced by the residual (bf16) epilogue");
+    TORCH_CHECK(ssq_out->dim() == 2 && ssq_out->size(1) == N / 4 && ssq_out->size(0) >= M && ssq_out->is_contiguous(),
+                "ssq_out must be [M, N/4]");
+    g.ssq_parts = (int)(N / 4);
+  }
   c10::DeviceGuard guard(x.device());
-  vgate::launch_gemm(g, cur_stream());
-}
-
-void awq_gemm(const Tensor& x, const Tensor& qw, const Tensor& scales, const Tensor& zeros,
-              int64_t group, int64_t N, int64_t K, const c10::optional<Tensor>& bias,
-              const c10::optional<Tensor>& res, Tensor& out, int64_t epi) {
-  CHECK_DEV(x); CHECK_DEV(qw); CHECK_DEV(scales); CHECK_DEV(zeros); CHECK_DEV(out);
-  CHECK_DT(x, torch::kBFloat16);
-  CHECK_DT(qw, torch::kInt32);
-  CHECK_DT(scales, torch::kBFloat16);
-  CHECK_DT(zeros, torch::kBFloat16);
-  TORCH_CHECK(K % group == 0 && group % 32 == 0, "awq: group must divide K and be a multiple of 32");
-  TORCH_CHECK(qw.numel() == N * K / 8, "awq: packed qweight numel");
-  TORCH_CHECK(scales.size(0) == K / group && scales.size(1) == N, "awq: scales shape");
-  const int64_t M = x.size(0);
-  if (epi == 1) CHECK_DT(out, torch::kFloat32); else CHECK_DT(out, torch::kBFloat16);
-  vgate::AwqGemmArgs g;
-  g.x = bf16p(x); g.lda = (int)x.stride(0); g.M = (int)M;
-  g.qw = reinterpret_cast<const uint32_t*>(qw.data_ptr());
-  g.scales = bf16p(scales); g.zeros = bf16p(zeros); g.group = (int)group;
-  g.N = (int)N; g.K = (int)K;
-  g.bias = opt_bf16(bias); g.res = opt_bf16(res);
-  g.ldr = g.res ? (int)res->stride(0) : 0;
-  g.out = out.data_ptr(); g.ldo = (int)out.stride(0); g.epi = (int)epi;
-  c10::DeviceGuard guard(x.device());
-  vgate::launch_awq_gemm(g, cur_stream());
+  if (awq) vgate::launch_awq_gemm(g, cur_stream());
+  else vgate::launch_gemm(g, cur_stream());
 }
 
 // y = rmsnorm(x [+ res]) * w ; res (if given) is updated in place to x + res
@@ -108,7 +149,8 @@ void rmsnorm(const Tensor& x, const c10::optional<Tensor>& res, const Tensor& w,
                         (int)y.stride(0), (int)M, (int)H, (float)eps, cur_stream());
 }
 
-void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart) {
+void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart,
+               const c10::optional<Tensor>& ssq_out) {
   CHECK_DEV(ids); CHECK_DEV(table); CHECK_DEV(out);
   CHECK_DT(ids, torch::kInt32); CHECK_DT(table, torch::kBFloat16); CHECK_DT(out, torch::kBFloat16);
   TORCH_CHECK(table.is_contiguous() && out.is_contiguous(), "embedding: contiguous");
@@ -117,7 +159,7 @@ void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vsta
   c10::DeviceGuard guard(ids.device());
   vgate::launch_embedding(reinterpret_cast<const int32_t*>(ids.data_ptr()), bf16p(table),
                           bf16p_mut(out), (int)T, (int)H, (int)vstart, (int)table.size(0),
-                          cur_stream());
+                          cur_stream(), opt_ptr<float>(ssq_out, torch::kFloat32, "ssq_out"));
 }
 
 void rope_kv(Tensor& qkv, const Tensor& positions, const c10::optional<Tensor>& slots,
@@ -206,6 +248,31 @@ void attn_prefill(const Tensor& q, int64_t q_stride, const Tensor& k_cache, cons
   vgate::launch_attn_prefill(a, cur_stream());
 }
 
+void attention(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const Tensor& v_cache,
+               const Tensor& block_tables, const Tensor& context_lens, const Tensor& query_start,
+               const Tensor& tile_seq, const Tensor& tile_q0, Tensor& out, Tensor& part_o, Tensor& part_ml,
+               int64_t Hq, int64_t Hkv, int64_t part_size, double scale, int64_t out_stride) {
+  auto a = attn_common(q, q_stride, k_cache, v_cache, block_tables, context_lens, out, Hq, Hkv, scale);
+  if (out_stride > 0) a.out_stride = (int)out_stride;
+  CHECK_DT(query_start, torch::kInt32); CHECK_DT(tile_seq, torch::kInt32); CHECK_DT(tile_q0, torch::kInt32);
+  CHECK_DT(part_o, torch::kFloat32); CHECK_DT(part_ml, torch::kFloat32);
+  TORCH_CHECK(part_size % 32 == 0, "attention: part_size % 32");
+  TORCH_CHECK(query_start.numel() >= a.S + 1, "attention: query_start needs S+1 entries");
+  a.query_start = reinterpret_cast<const int32_t*>(query_start.data_ptr());
+  a.tile_seq = reinterpret_cast<const int32_t*>(tile_seq.data_ptr());
+  a.tile_q0 = reinterpret_cast<const int32_t*>(tile_q0.data_ptr());
+  a.num_tiles = (int)tile_seq.numel();
+  a.num_parts = (int)part_o.size(2);
+  a.part_size = (int)part_size;
+  TORCH_CHECK((int64_t)a.num_parts * part_size >= block_tables.size(1) * 16,
+              "attention: partitions do not cover max context");
+  TORCH_CHECK(part_o.size(0) >= a.S && part_o.size(1) == Hq, "attention: part_o shape");
+  a.part_o = reinterpret_cast<float*>(part_o.data_ptr());
+  a.part_ml = reinterpret_cast<float*>(part_ml.data_ptr());
+  c10::DeviceGuard guard(q.device());
+  vgate::launch_attention(a, a.S, cur_stream());
+}
+
 void sample(const Tensor& logits, const c10::optional<Tensor>& temperature,
             const c10::optional<Tensor>& top_p, const c10::optional<Tensor>& top_k,
             const c10::optional<Tensor>& seeds, const c10::optional<Tensor>& offsets, Tensor& out,
@@ -241,10 +308,20 @@ void sample(const Tensor& logits, const c10::optional<Tensor>& temperature,
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "vgate gfx950 (MI355X) HIP kernels and native runtime";
-  m.def("gemm", &gemm, "fragment-packed MFMA GEMM with fused epilogue");
-  m.def("awq_gemm", &awq_gemm, "AWQ W4A16 dequant-GEMM");
+  namespace py = pybind11;
+  m.def("gemm", &gemm, "fragment-packed MFMA GEMM (+RMSNorm prologue, split-K, fused epilogues; bf16 or AWQ int4)",
+        py::arg("x"), py::arg("wp"), py::arg("N"), py::arg("K"), py::arg("out"), py::arg("epi") = 0,
+        py::arg("bias") = py::none(), py::arg("res") = py::none(), py::arg("norm_w") = py::none(),
+        py::arg("eps") = 1e-6, py::arg("row_idx") = py::none(), py::arg("ws") = py::none(),
+        py::arg("waves") = 0, py::arg("splitk") = 0, py::arg("positions") = py::none(),
+        py::arg("slots") = py::none(), py::arg("cos_sin") = py::none(), py::arg("k_cache") = py::none(),
+        py::arg("v_cache") = py::none(), py::arg("hq") = 0, py::arg("hkv") = 0,
+        py::arg("awq_scales") = py::none(), py::arg("awq_zeros") = py::none(), py::arg("group") = 128,
+        py::arg("ssq_in") = py::none(), py::arg("ssq_out") = py::none());
+  m.def("attention", &attention, "unified paged attention: decode (split-K) + varlen prefill tiles, one launch");
   m.def("rmsnorm", &rmsnorm, "RMSNorm with optional fused residual add");
-  m.def("embedding", &embedding, "vocab-sharded embedding gather");
+  m.def("embedding", &embedding, "vocab-sharded embedding gather (+row sum of squares)", py::arg("ids"),
+        py::arg("table"), py::arg("out"), py::arg("vstart") = 0, py::arg("ssq_out") = py::none());
   m.def("rope_kv", &rope_kv, "NeoX RoPE + paged KV-cache write");
   m.def("attn_decode", &attn_decode, "paged split-K decode attention");
   m.def("attn_prefill", &attn_prefill, "paged varlen causal prefill attention");

@@ -239,3 +239,136 @@ def test_sample_logprob():
     out = ops.sample(logits, temperature=torch.zeros(4, device=DEV), out_logprob=lp)
     exp = torch.log_softmax(logits, -1).gather(1, out.long()[:, None]).squeeze(1)
     assert torch.allclose(lp, exp, atol=1e-3)
+
+
+# ---------------------------------------------------------------- fused GEMM v2
+@pytest.mark.parametrize("M,N,K", [(8, 1536, 1536), (8, 1536, 8960), (40, 2048, 1536), (200, 512, 1024)])
+@pytest.mark.parametrize("splitk", [1, 4])
+def test_gemm_splitk_residual_inplace(M, N, K, splitk):
+    torch.manual_seed(10)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    exp = ref.linear_ref(x, w, None, r)
+    lin = ops.Linear(w)
+    for _ in range(3):  # repeated launches: split-K tickets must self-reset
+        r2 = r.clone()
+        ops.linear(x, lin, out=r2, residual=r2, splitk=splitk)
+        assert _rel_err(r2, exp) < 1e-2
+
+
+def test_gemm_norm_prologue_and_row_gather():
+    torch.manual_seed(11)
+    T, H, N = 37, 1536, 4096
+    x = torch.randn(T, H, device=DEV).bfloat16()
+    nw = (torch.rand(H, device=DEV) + 0.5).bfloat16()
+    w = (torch.randn(N, H, device=DEV) / math.sqrt(H)).bfloat16()
+    idx = torch.tensor([36, 0, 17, 5], dtype=torch.int32, device=DEV)
+    y = ops.linear(x, ops.Linear(w), out_f32=True, norm=(nw, 1e-6), row_idx=idx)
+    xn, _ = ref.rmsnorm_ref(x[idx.long()], nw, 1e-6)
+    assert _rel_err(y, ref.linear_ref(xn, w, out_f32=True)) < 1e-2
+    # silu + norm
+    wg = (torch.randn(512, H, device=DEV) / math.sqrt(H)).bfloat16()
+    wu = (torch.randn(512, H, device=DEV) / math.sqrt(H)).bfloat16()
+    y2 = ops.linear(x, ops.Linear(torch.cat([wg, wu]), kind="silu"), norm=(nw, 1e-6))
+    xn2, _ = ref.rmsnorm_ref(x, nw, 1e-6)
+    assert _rel_err(y2, ref.silu_mul_linear_ref(xn2, wg, wu)) < 1e-2
+
+
+@pytest.mark.parametrize("hq,hkv", [(12, 2), (8, 1)])
+def test_gemm_qkv_rope_kv_epilogue(hq, hkv):
+    torch.manual_seed(12)
+    T, H, D, BS = 21, 1536, 128, 16
+    N = (hq + 2 * hkv) * D
+    x = torch.randn(T, H, device=DEV).bfloat16()
+    nw = (torch.rand(H, device=DEV) + 0.5).bfloat16()
+    w = (torch.randn(N, H, device=DEV) / math.sqrt(H)).bfloat16()
+    b = (torch.randn(N, device=DEV) * 0.1).bfloat16()
+    pos = torch.randint(0, 1000, (T,), dtype=torch.int32, device=DEV)
+    slots = torch.randperm(32 * BS, device=DEV)[:T].int()
+    slots[4] = -1
+    cs = ref.rope_cos_sin(1024, D, 1e6, device=DEV)
+    kc = torch.zeros(32, hkv, BS, D, device=DEV).bfloat16()
+    vc = torch.zeros_like(kc)
+    lin = ops.Linear(w, bias=b, layout="qkv")
+    q = ops.linear(x, lin, norm=(nw, 1e-6), qkv=dict(positions=pos, slots=slots, cos_sin=cs, k_cache=kc,
+                                                      v_cache=vc, hq=hq, hkv=hkv))
+    # reference: norm -> linear(+bias) -> rope + kv write
+    xn, _ = ref.rmsnorm_ref(x, nw, 1e-6)
+    qkv = ref.linear_ref(xn, w, b)
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    ref.rope_kv_ref(qkv, pos, slots, cs, kc2, vc2, hq, hkv, D)
+    assert _rel_err(q, qkv[:, : hq * D]) < 1e-2
+    assert _rel_err(kc, kc2) < 1e-2 and _rel_err(vc, vc2) < 1e-2
+    assert torch.equal(lin.dense_weight(), w)
+
+
+def test_awq_norm_splitk():
+    torch.manual_seed(13)
+    M, N, K, g = 8, 1536, 1536, 128
+    q = torch.randint(0, 16, (N, K), dtype=torch.int32)
+    scales = (torch.rand(K // g, N) * 0.02 + 0.005).bfloat16()
+    zeros = torch.randint(0, 16, (K // g, N)).float().bfloat16()
+    lin = ops.Linear(None, awq={"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV), "group": g})
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    nw = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+    wd = ref.awq_dequant_ref(q, scales, zeros, g).to(DEV)
+    xn, _ = ref.rmsnorm_ref(x, nw, 1e-6)
+    for sk in (1, 4):
+        y = ops.linear(x, lin, norm=(nw, 1e-6), splitk=sk)
+        assert _rel_err(y, ref.linear_ref(xn, wd)) < 2e-2
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(12, 2), (32, 8), (64, 8)])
+def test_unified_attention_mixed_batch(Hq, Hkv):
+    """decode rows (qlen 1, incl. split-K partitions) + prefill chunks in one launch."""
+    torch.manual_seed(14)
+    D, BS = 128, 16
+    qlens = [1, 1, 37, 1, 16, 3]
+    ctxs = [700, 5, 100, 1500, 16, 40]
+    S = len(qlens)
+    maxb = 128
+    nblk = S * maxb + 4
+    kc, vc = _make_cache(nblk, Hkv, seed=3)
+    bt = (torch.randperm(nblk)[: S * maxb]).reshape(S, maxb).int().to(DEV)
+    qs = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32, device=DEV)
+    T = int(qs[-1])
+    cl = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
+    q = torch.randn(T, Hq * D, device=DEV).bfloat16()
+    ts, tq = ops.prefill_tiles([ql if ql > 1 else 0 for ql in qlens])
+    ts = torch.tensor(ts + [-1, -1], dtype=torch.int32, device=DEV)  # + padding tiles
+    tq = torch.tensor(tq + [0, 0], dtype=torch.int32, device=DEV)
+    scale = 1 / math.sqrt(D)
+    for part in (512, 2048):
+        P = (maxb * BS + part - 1) // part
+        po = torch.empty(S, Hq, P, D, device=DEV)
+        pml = torch.empty(S, Hq, P, 2, device=DEV)
+        out = torch.zeros(T, Hq * D, device=DEV).bfloat16()
+        ops.attention(q, Hq * D, kc, vc, bt, cl, qs, ts, tq, out, po, pml, Hq, Hkv, part, scale)
+        r = ref.attention_ref(q.view(T, Hq, D), kc, vc, bt, cl, qs.cpu(), Hq, Hkv, scale)
+        assert _rel_err(out.view(T, Hq, D), r) < 2e-2
+
+
+def test_ssq_handoff_norm_matches_full_row_norm():
+    """residual epilogue ssq partials -> next GEMM's norm prologue == full-row RMSNorm."""
+    torch.manual_seed(15)
+    T, H, N = 11, 1536, 2048
+    C = ops.native()
+    ids = torch.randint(0, 1000, (T,), dtype=torch.int32, device=DEV)
+    table = torch.randn(1000, H, device=DEV).bfloat16()
+    ssq = torch.empty(T, H // 4, device=DEV)
+    resid = ops.embedding(ids, table, ssq_out=ssq)
+    nw = (torch.rand(H, device=DEV) + 0.5).bfloat16()
+    w = (torch.randn(N, H, device=DEV) / math.sqrt(H)).bfloat16()
+    y_fast = ops.linear(resid, ops.Linear(w), norm=(nw, 1e-6), ssq_in=ssq)
+    y_full = ops.linear(resid, ops.Linear(w), norm=(nw, 1e-6))
+    assert _rel_err(y_fast, y_full) < 2e-3
+    # residual epilogue producer
+    x = torch.randn(T, 1536, device=DEV).bfloat16()
+    wo = (torch.randn(H, 1536, device=DEV) / math.sqrt(1536)).bfloat16()
+    ops.linear(x, ops.Linear(wo), out=resid, residual=resid, ssq_out=ssq)
+    exp = resid.float().pow(2).sum(-1)
+    assert torch.allclose(ssq.sum(-1), exp, rtol=1e-3)
+    y_fast = ops.linear(resid, ops.Linear(w), norm=(nw, 1e-6), ssq_in=ssq)
+    y_full = ops.linear(resid, ops.Linear(w), norm=(nw, 1e-6))
+    assert _rel_err(y_fast, y_full) < 2e-3

@@ -278,8 +278,9 @@ def create_app(config: Optional[VGateConfig] = None, engine: Optional[VGateEngin
     @app.get("/metrics", summary="Prometheus Metrics")
     async def prometheus_metrics(request: Request):
         if "application/openmetrics-text" in request.headers.get("accept", ""):
+            from prometheus_client import REGISTRY
             from prometheus_client.openmetrics.exposition import generate_latest as om_latest
-            return Response(content=om_latest(),
+            return Response(content=om_latest(REGISTRY),
                             media_type="application/openmetrics-text; version=1.0.0; charset=utf-8")
         return Response(content=generate_latest(), media_type=CONTENT_TYPE_LATEST)
 

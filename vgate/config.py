@@ -100,7 +100,7 @@ class ModelConfig(_Section):
     max_num_batched_tokens: int = 2048
     enable_prefix_caching: bool = True
     hip_graph_token_buckets: Optional[list[int]] = None
-    attention_partition_size: int = 512
+    attention_partition_size: int = 0  # 0 = auto
 
     @field_validator("engine_type")
     @classmethod

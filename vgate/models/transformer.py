@@ -113,39 +113,76 @@ class DecoderModel:
         """One step. ``sv`` is a StepView (token/seq metadata views, bucket sizes T and S).
 
         Returns f32 logits [S, vocab] for the sample rows (one per sequence).
+        GPU: 4 fused GEMM launches + 1 attention launch per layer (RMSNorm, RoPE, KV
+        write, bias, SiLU*mul and residual adds all live inside them).
         """
+        if self.device.type != "cuda":
+            return self._forward_reference(sv, kv_caches, part_size)
         a = self.arch
         sh = self.shard
         tp = self.tp
         T, S = sv.T, sv.S
         D = a.head_dim
         dev = self.device
-        gpu = dev.type == "cuda"
+        # Residual-stream sum-of-squares hand-off (TP=1): each producer of `resid` (embedding,
+        # o_proj / down_proj residual epilogues) writes per-row partials the next fused
+        # RMSNorm prologue reduces — no kernel ever re-reads a full row just for its norm.
+        # Under TP the residual is completed by an all-reduce after the GEMM, so the
+        # consumer normalises from the full row instead.
+        ssq = torch.empty(T, a.hidden_size // 4, dtype=torch.float32, device=dev) if tp.size == 1 else None
+        resid = ops.embedding(sv.ids, self.embed, vstart=sh.vocab0, ssq_out=ssq)
+        if tp.size > 1:
+            tp.all_reduce(resid)
+        q = torch.empty(T, sh.hq * D, dtype=torch.bfloat16, device=dev)
+        attn = torch.empty(T, sh.hq * D, dtype=torch.bfloat16, device=dev)
+        mlp = torch.empty(T, sh.inter, dtype=torch.bfloat16, device=dev)
+        P = max(1, (self.max_model_len + part_size - 1) // part_size)
+        part_o = torch.empty(S, sh.hq, P, D, dtype=torch.float32, device=dev)
+        part_ml = torch.empty(S, sh.hq, P, 2, dtype=torch.float32, device=dev)
+        first = tp.is_first
+        eps = a.rms_eps
+        for li, L in enumerate(self.layers):
+            kc, vc = kv_caches[li]
+            ops.linear(resid, L.qkv, out=q, norm=(L.in_norm, eps), ssq_in=ssq,
+                       qkv=dict(positions=sv.positions, slots=sv.slots, cos_sin=self.cos_sin, k_cache=kc,
+                                v_cache=vc, hq=sh.hq, hkv=sh.hkv))
+            ops.attention(q, sh.hq * D, kc, vc, sv.block_tables, sv.context_lens, sv.query_start, sv.tile_seq,
+                          sv.tile_q0, attn, part_o, part_ml, sh.hq, sh.hkv, part_size, self.scale)
+            ops.linear(attn, L.o, out=resid, residual=resid if first else None, ssq_out=ssq)
+            if tp.size > 1:
+                tp.all_reduce(resid)
+            ops.linear(resid, L.gate_up, out=mlp, norm=(L.post_norm, eps), ssq_in=ssq)
+            ops.linear(mlp, L.down, out=resid, residual=resid if first else None, ssq_out=ssq)
+            if tp.size > 1:
+                tp.all_reduce(resid)
+        logits = ops.linear(resid, self.lm_head, out_f32=True, norm=(self.final_norm, eps), row_idx=sv.sample_idx,
+                            ssq_in=ssq)
+        if tp.size > 1:
+            logits = tp.all_gather_lastdim(logits)
+        return logits[:, : a.vocab_size]
+
+    def _forward_reference(self, sv, kv_caches, part_size: int) -> torch.Tensor:
+        """Same math with the fp32 reference ops, one op at a time (CPU path)."""
+        a = self.arch
+        sh = self.shard
+        tp = self.tp
+        T = sv.T
+        D = a.head_dim
+        dev = self.device
         resid = ops.embedding(sv.ids, self.embed, vstart=sh.vocab0)
         if tp.size > 1:
             tp.all_reduce(resid)
         x = torch.empty_like(resid)
         attn = torch.empty(T, sh.hq * D, dtype=torch.bfloat16, device=dev)
-        qkv_w = (sh.hq + 2 * sh.hkv) * D
-        qkv = torch.empty(T, qkv_w, dtype=torch.bfloat16, device=dev)
+        qkv = torch.empty(T, (sh.hq + 2 * sh.hkv) * D, dtype=torch.bfloat16, device=dev)
         mlp = torch.empty(T, sh.inter, dtype=torch.bfloat16, device=dev)
-        if gpu:
-            P = max(1, (self.max_model_len + part_size - 1) // part_size)
-            part_o = torch.empty(S, sh.hq, P, D, dtype=torch.float32, device=dev)
-            part_ml = torch.empty(S, sh.hq, P, 2, dtype=torch.float32, device=dev)
         first = tp.is_first
         for li, L in enumerate(self.layers):
             kc, vc = kv_caches[li]
             ops.rmsnorm(resid, L.in_norm, a.rms_eps, out=x)
             ops.linear(x, L.qkv, out=qkv)
             ops.rope_kv(qkv, sv.positions, sv.slots, self.cos_sin, kc, vc, sh.hq, sh.hkv, D)
-            if gpu:
-                ops.attention_decode(qkv, qkv_w, kc, vc, sv.block_tables, sv.context_lens, attn, part_o, part_ml,
-                                     sh.hq, sh.hkv, part_size, self.scale, query_start=sv.query_start)
-                ops.attention_prefill(qkv, qkv_w, kc, vc, sv.block_tables, sv.context_lens, sv.query_start,
-                                      sv.tile_seq, sv.tile_q0, attn, sh.hq, sh.hkv, self.scale)
-            else:
-                self._attention_cpu(qkv, attn, kc, vc, sv)
+            self._attention_cpu(qkv, attn, kc, vc, sv)
             ops.linear(attn, L.o, out=resid, residual=resid if first else None)
             if tp.size > 1:
                 tp.all_reduce(resid)
@@ -154,7 +191,7 @@ class DecoderModel:
             ops.linear(mlp, L.down, out=resid, residual=resid if first else None)
             if tp.size > 1:
                 tp.all_reduce(resid)
-        xs = resid.index_select(0, sv.sample_idx)
+        xs = resid.index_select(0, sv.sample_idx.long())
         xn = ops.rmsnorm(xs, self.final_norm, a.rms_eps)
         logits = ops.linear(xn, self.lm_head, out_f32=True)
         if tp.size > 1:

@@ -31,13 +31,13 @@ def _randn(shape, std, g, device):
     return (torch.randn(shape, generator=g, device=device, dtype=torch.float32) * std).to(torch.bfloat16)
 
 
-def _rand_awq(N, K, group, g, device, silu=False):
+def _rand_awq(N, K, group, g, device, silu=False, layout="plain"):
     q = torch.randint(0, 16, (N, K), generator=g, device=device, dtype=torch.int32)
     target = 1.0 / math.sqrt(K)
     scales = torch.full((K // group, N), target / 4.61, device=device).to(torch.bfloat16)
     zeros = torch.full((K // group, N), 8.0, device=device).to(torch.bfloat16)
-    return ops.Linear(None, kind="awq", awq={"qint": q, "scales": scales, "zeros": zeros, "group": group,
-                                             "silu": silu})
+    return ops.Linear(None, awq={"qint": q, "scales": scales, "zeros": zeros, "group": group,
+                                 "layout": "silu" if silu else layout})
 
 
 def random_init(model, seed: int = 0) -> None:
@@ -55,20 +55,20 @@ def random_init(model, seed: int = 0) -> None:
     for _ in range(a.num_layers):
         qkv_b = _randn((q_out,), 0.02, g, dev) if a.qkv_bias else None
         if awq and H % 128 == 0 and (sh.hq * D) % 128 == 0 and sh.inter % 128 == 0:
-            qkv = _rand_awq(q_out, H, group, g, dev)
+            qkv = _rand_awq(q_out, H, group, g, dev, layout="qkv")
             qkv.bias = qkv_b
             o = _rand_awq(H, sh.hq * D, group, g, dev)
             gu = _rand_awq(2 * sh.inter, H, group, g, dev, silu=True)
             down = _rand_awq(H, sh.inter, group, g, dev)
         else:
-            qkv = ops.Linear(_randn((q_out, H), 1 / math.sqrt(H), g, dev), bias=qkv_b)
+            qkv = ops.Linear(_randn((q_out, H), 1 / math.sqrt(H), g, dev), bias=qkv_b, layout="qkv")
             o = ops.Linear(_randn((H, sh.hq * D), 1 / math.sqrt(sh.hq * D * sh.tp.size), g, dev))
             gu = ops.Linear(_randn((2 * sh.inter, H), 1 / math.sqrt(H), g, dev), kind="silu")
             down = ops.Linear(_randn((H, sh.inter), 1 / math.sqrt(sh.inter * sh.tp.size), g, dev))
         layers.append(LayerWeights(
             in_norm=torch.ones(H, dtype=torch.bfloat16, device=dev), qkv=qkv, o=o,
             post_norm=torch.ones(H, dtype=torch.bfloat16, device=dev), gate_up=gu, down=down))
-        if awq and qkv.kind == "awq" and dev.type == "cuda":
+        if awq and dev.type == "cuda":
             torch.cuda.empty_cache()
     model.layers = layers
     model.final_norm = torch.ones(H, dtype=torch.bfloat16, device=dev)
@@ -161,10 +161,10 @@ def load_checkpoint(model, path: str) -> None:
         sc = idx.get(prefix + ".scales").to(torch.bfloat16)[k0 // group:k1 // group]
         return qw.t().contiguous(), sc.contiguous(), qz.to(torch.bfloat16).contiguous()
 
-    def make_awq(t, silu=False):
+    def make_awq(t, silu=False, layout="plain"):
         q, s, z = t
-        return ops.Linear(None, kind="awq", awq={"qint": q, "scales": s.to(dev), "zeros": z.to(dev),
-                                                 "group": group, "silu": silu})
+        return ops.Linear(None, awq={"qint": q, "scales": s.to(dev), "zeros": z.to(dev), "group": group,
+                                     "layout": "silu" if silu else layout})
 
     qa, qb = sh.q_head0 * D, (sh.q_head0 + sh.hq) * D
     ka, kb = a.q_size + sh.kv_head0 * D, a.q_size + (sh.kv_head0 + sh.hkv) * D
@@ -183,7 +183,7 @@ def load_checkpoint(model, path: str) -> None:
             k = awq_rows(att + ".k_proj", [(ka - a.q_size, kb - a.q_size)])
             v = awq_rows(att + ".v_proj", [(va - a.q_size - a.kv_size, vb - a.q_size - a.kv_size)])
             qkv = make_awq((torch.cat([q[0], k[0], v[0]]), torch.cat([q[1], k[1], v[1]], 1),
-                            torch.cat([q[2], k[2], v[2]], 1)))
+                            torch.cat([q[2], k[2], v[2]], 1)), layout="qkv")
             qkv.bias = bias
             o = make_awq(awq_cols(att + ".o_proj", qa, qb))
             g_ = awq_rows(mlp + ".gate_proj", [(sh.inter0, sh.inter0 + sh.inter)])
@@ -195,7 +195,7 @@ def load_checkpoint(model, path: str) -> None:
             wq = dense(att + ".q_proj.weight")[qa:qb]
             wk = dense(att + ".k_proj.weight")[ka - a.q_size: kb - a.q_size]
             wv = dense(att + ".v_proj.weight")[va - a.q_size - a.kv_size: vb - a.q_size - a.kv_size]
-            qkv = ops.Linear(torch.cat([wq, wk, wv]).to(dev), bias=bias)
+            qkv = ops.Linear(torch.cat([wq, wk, wv]).to(dev), bias=bias, layout="qkv")
             o = ops.Linear(dense(att + ".o_proj.weight")[:, qa:qb].contiguous().to(dev))
             wg = dense(mlp + ".gate_proj.weight")[sh.inter0: sh.inter0 + sh.inter]
             wu = dense(mlp + ".up_proj.weight")[sh.inter0: sh.inter0 + sh.inter]

@@ -89,40 +89,68 @@ def pack_awq(qint: torch.Tensor) -> torch.Tensor:
     return words.to(torch.int32).contiguous()
 
 
+def row_permutation(N: int, layout: str) -> torch.Tensor | None:
+    """Row order of the packed weight for a fused epilogue (None = identity).
+
+    silu: [G0 U0 G1 U1 ...] 16-row tiles (gate rows then up rows in the dense matrix);
+    qkv : per 128-wide head, tiles [t0 t4 t1 t5 t2 t6 t3 t7] so each block's tile pair
+          holds the NeoX rotation partners d and d + 64.
+    """
+    if layout == "silu":
+        I = N // 2
+        t = torch.arange(2 * I).reshape(2, I // 16, 16).transpose(0, 1)
+        return t.reshape(-1)
+    if layout == "qkv":
+        assert N % 128 == 0
+        order = torch.tensor([0, 4, 1, 5, 2, 6, 3, 7])
+        heads = N // 128
+        t = torch.arange(N).reshape(heads, 8, 16)[:, order]
+        return t.reshape(-1)
+    return None
+
+
 class Linear:
     """A linear layer's weights in kernel-ready form.
 
-    kind: "plain" | "silu" (rows are [gate; up], output is silu(gate) * up) | "awq".
-    On GPU the weight is stored fragment-packed only (no second copy); on CPU the
-    plain [N, K] matrix is kept for the reference path.
+    layout: "plain" | "silu" (rows [gate; up] -> out = silu(gate) * up)
+            | "qkv" (rows [q; k; v], heads of 128: fused bias + RoPE + KV-cache write).
+    Dense bf16 weights or AWQ int4 (``awq={"qint", "scales", "zeros", "group"}``).
+    On GPU only the fragment-packed copy is kept; on CPU the dense matrix (reference path).
     """
 
     def __init__(self, w: torch.Tensor | None, bias: torch.Tensor | None = None, kind: str = "plain",
-                 awq: dict | None = None):
-        self.kind = kind
+                 awq: dict | None = None, layout: str | None = None):
+        if kind in ("silu", "qkv"):
+            layout, kind = kind, "dense"
+        self.layout = layout or (awq.get("layout", "plain") if awq else "plain")
+        if awq is not None and awq.get("silu"):
+            self.layout = "silu"
+        self.kind = "awq" if awq is not None else "dense"
         self.bias = bias
-        if kind == "awq":
-            assert awq is not None
-            self.N, self.K = awq["qint"].shape
+        if self.kind == "awq":
+            q = awq["qint"]
+            self.N, self.K = q.shape
             self.group = awq["group"]
-            self.awq_epi_silu = awq.get("silu", False)
             dev = awq["scales"].device
+            perm = row_permutation(self.N, self.layout)
+            scales, zeros = awq["scales"], awq["zeros"]
             if dev.type == "cuda":
-                self.qw = pack_awq(awq["qint"].to(dev))
-                self.scales = awq["scales"].to(torch.bfloat16).contiguous()
-                self.zeros = (awq["scales"].float() * awq["zeros"].float()).to(torch.bfloat16).contiguous()
+                q = q.to(dev)
+                if perm is not None:
+                    pd = perm.to(dev)
+                    q, scales, zeros = q[pd], scales[:, pd], zeros[:, pd]
+                self.wp = pack_awq(q)
+                self.scales = scales.to(torch.bfloat16).contiguous()
+                self.zeros = (scales.float() * zeros.float()).to(torch.bfloat16).contiguous()
                 self.w = None
             else:
-                w_full = ref.awq_dequant_ref(awq["qint"], awq["scales"], awq["zeros"], self.group)
-                self.w = w_full
-            self.wp = None
+                self.w = ref.awq_dequant_ref(q, scales, zeros, self.group)
+                self.wp = None
             return
         self.N, self.K = w.shape
-        if kind == "silu":
-            I = self.N // 2
-            w = interleave_gate_up(w[:I], w[I:])
         if w.is_cuda:
-            self.wp = pack_weight(w)
+            perm = row_permutation(self.N, self.layout)
+            self.wp = pack_weight(w[perm.to(w.device)] if perm is not None else w)
             self.w = None
         else:
             self.wp = None
@@ -130,56 +158,101 @@ class Linear:
 
     @property
     def out_features(self) -> int:
-        if self.kind == "silu" or (self.kind == "awq" and self.awq_epi_silu):
-            return self.N // 2
-        return self.N
+        return self.N // 2 if self.layout == "silu" else self.N
 
     def dense_weight(self) -> torch.Tensor:
-        """[N, K] in the ORIGINAL row order (for references / checkpoint export)."""
+        """[N, K] in the ORIGINAL row order (references / checkpoint export)."""
+        if self.w is not None:
+            return self.w
         if self.kind == "awq":
-            raise NotImplementedError
-        w = self.w if self.w is not None else unpack_weight(self.wp, self.N, self.K)
-        if self.kind == "silu":
-            I = self.N // 2
-            t = w.reshape(I // 16, 2, 16, self.K)
-            w = torch.cat([t[:, 0].reshape(I, self.K), t[:, 1].reshape(I, self.K)], 0)
+            raise NotImplementedError("AWQ weights are kept packed on the GPU")
+        w = unpack_weight(self.wp, self.N, self.K)
+        perm = row_permutation(self.N, self.layout)
+        if perm is not None:
+            out = torch.empty_like(w)
+            out[perm.to(w.device)] = w
+            w = out
         return w
 
     def nbytes(self) -> int:
-        if self.kind == "awq":
-            if self.w is not None:
-                return self.w.numel() * 2
-            return self.qw.numel() * 4 + self.scales.numel() * 4
+        if self.kind == "awq" and self.w is None:
+            return self.wp.numel() * 4 + self.scales.numel() * 4
         t = self.wp if self.wp is not None else self.w
         return t.numel() * t.element_size()
 
 
+_WS: dict = {}
+
+
+def workspace(device) -> torch.Tensor:
+    """Per-device GEMM workspace: 64k split-K tickets (zeroed once) + 32 MiB fp32 slabs."""
+    key = str(device)
+    ws = _WS.get(key)
+    if ws is None:
+        ws = torch.zeros(65536 + 8 * 2**20, dtype=torch.int32, device=device)
+        _WS[key] = ws
+    return ws
+
+
 def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
-           residual: torch.Tensor | None = None, out_f32: bool = False, waves: int = 0) -> torch.Tensor:
-    """out = epi(x @ W^T). x: [M, K] bf16 (row stride allowed)."""
-    M = x.shape[0]
-    silu = lin.kind == "silu" or (lin.kind == "awq" and lin.awq_epi_silu)
-    ncols = lin.N // 2 if silu else lin.N
+           residual: torch.Tensor | None = None, out_f32: bool = False, waves: int = 0, splitk: int = 0,
+           norm: tuple | None = None, row_idx: torch.Tensor | None = None, qkv: dict | None = None,
+           ssq_in: torch.Tensor | None = None, ssq_out: torch.Tensor | None = None) -> torch.Tensor:
+    """out = epilogue(prologue(x) @ W^T).
+
+    norm=(w, eps): fused RMSNorm of x rows; row_idx: gather rows of x first;
+    qkv=dict(positions, slots, cos_sin, k_cache, v_cache, hq, hkv): fused bias + RoPE +
+    KV write, returns q [M, hq*128] (layout "qkv" only).
+    """
+    M = row_idx.numel() if row_idx is not None else x.shape[0]
+    silu = lin.layout == "silu"
+    if qkv is not None:
+        ncols = qkv["hq"] * 128
+    else:
+        ncols = lin.N // 2 if silu else lin.N
     if out is None:
         out = torch.empty(M, ncols, dtype=torch.float32 if out_f32 else torch.bfloat16, device=x.device)
     if not _gpu(x):
-        w = lin.w if lin.kind != "silu" else lin.dense_weight()
+        xx = x[row_idx.long()] if row_idx is not None else x
+        if norm is not None:
+            xx, _ = ref.rmsnorm_ref(xx, norm[0], norm[1])
+        wd = lin.dense_weight()
         if silu:
             I = lin.N // 2
-            if lin.kind == "silu":
-                wd = lin.dense_weight()
-            else:
-                wd = lin.w
-            out.copy_(ref.silu_mul_linear_ref(x, wd[:I], wd[I:]))
+            out.copy_(ref.silu_mul_linear_ref(xx, wd[:I], wd[I:]))
+        elif qkv is not None:
+            y = ref.linear_ref(xx, wd, lin.bias)
+            ref.rope_kv_ref(y, qkv["positions"], qkv["slots"], qkv["cos_sin"], qkv["k_cache"], qkv["v_cache"],
+                            qkv["hq"], qkv["hkv"], 128)
+            out.copy_(y[:, :ncols])
         else:
-            out.copy_(ref.linear_ref(x, w, lin.bias, residual, out_f32))
+            out.copy_(ref.linear_ref(xx, wd, lin.bias, residual, out_f32))
         return out
     C = native()
-    epi = 2 if silu else (1 if out_f32 else 0)
+    epi = 3 if qkv is not None else (2 if silu else (1 if out_f32 else 0))
+    kw = dict(bias=lin.bias, res=residual, ws=workspace(x.device), waves=waves, splitk=splitk)
+    if norm is not None:
+        kw.update(norm_w=norm[0], eps=float(norm[1]))
+    if row_idx is not None:
+        kw["row_idx"] = row_idx
+    if qkv is not None:
+        kw.update(positions=qkv["positions"], slots=qkv["slots"], cos_sin=qkv["cos_sin"],
+                  k_cache=qkv["k_cache"], v_cache=qkv["v_cache"], hq=qkv["hq"], hkv=qkv["hkv"])
     if lin.kind == "awq":
-        C.awq_gemm(x, lin.qw, lin.scales, lin.zeros, lin.group, lin.N, lin.K, lin.bias, residual, out, epi)
-    else:
-        C.gemm(x, lin.wp, lin.N, lin.K, lin.bias, residual, out, epi, waves)
+        kw.update(awq_scales=lin.scales, awq_zeros=lin.zeros, group=lin.group)
+    if ssq_in is not None:
+        kw["ssq_in"] = ssq_in
+    if ssq_out is not None:
+        kw["ssq_out"] = ssq_out
+    C.gemm(x, lin.wp, lin.N, lin.K, out, epi, **kw)
+    return out
+
+
+def attention(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start, tile_seq, tile_q0, out,
+              part_o, part_ml, Hq: int, Hkv: int, part_size: int, scale: float):
+    """Unified paged attention for a mixed step (decode rows + prefill tiles, one launch)."""
+    native().attention(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start, tile_seq, tile_q0,
+                       out, part_o, part_ml, Hq, Hkv, part_size, scale, 0)
     return out
 
 
@@ -198,13 +271,15 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor
     return out
 
 
-def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None, vstart: int = 0):
+def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None, vstart: int = 0,
+              ssq_out: torch.Tensor | None = None):
+    """Row gather; optionally also emits per-row sum-of-squares partials ([T, H/4], total in col 0)."""
     if out is None:
         out = torch.empty(ids.numel(), table.shape[1], dtype=table.dtype, device=table.device)
     if not _gpu(table):
         out.copy_(ref.embedding_ref(ids, table, vstart))
         return out
-    native().embedding(ids, table, out, vstart)
+    native().embedding(ids, table, out, vstart, ssq_out)
     return out
 
 
@@ -278,6 +353,6 @@ def softmax_scale(head_dim: int) -> float:
 
 __all__ = [
     "native", "native_available", "pack_weight", "unpack_weight", "interleave_gate_up", "pack_awq",
-    "Linear", "linear", "rmsnorm", "embedding", "rope_kv", "attention_decode", "attention_prefill",
+    "Linear", "linear", "attention", "workspace", "row_permutation", "rmsnorm", "embedding", "rope_kv", "attention_decode", "attention_prefill",
     "prefill_tiles", "sample", "softmax_scale", "ref",
 ]

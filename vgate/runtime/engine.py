@@ -54,7 +54,7 @@ class EngineConfig:
     enable_prefix_caching: bool = True
     seed: int = 0
     block_size: int = BLOCK_SIZE
-    part_size: int = 512
+    part_size: int = 0  # 0 = auto: one decode partition up to 2048 tokens, 512-token split-K beyond
     graph_token_buckets: list[int] | None = None
     warmup: bool = True
     arch_overrides: dict | None = None
@@ -106,8 +106,10 @@ class LLMEngine:
                                              self.arch.head_dim, self.device, block_size=cfg.block_size)
         self.kvm = KVCacheManager(self.num_blocks, cfg.block_size, cfg.enable_prefix_caching)
         self.scheduler = Scheduler(self.kvm, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len)
+        part = cfg.part_size or (cfg.max_model_len if cfg.max_model_len <= 2048 else 512)
+        part = max(32, (part + 31) // 32 * 32)
         self.runner = ModelRunner(self.model, self.kv_caches, cfg.max_num_seqs, cfg.max_num_batched_tokens,
-                                  cfg.max_model_len, cfg.block_size, cfg.enforce_eager, cfg.part_size,
+                                  cfg.max_model_len, cfg.block_size, cfg.enforce_eager, part,
                                   cfg.graph_token_buckets)
         self.tokenizer = load_tokenizer(weights, cfg.tokenizer, self.arch)
         self.stats = EngineStats()
