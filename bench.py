@@ -181,6 +181,8 @@ def main():
             "generated_tokens_per_s": round(toks / wall, 1),
             "failures": sum(r["fails"] for r in allr),
             "engine_avg_step_ms": allr[0]["engine"].get("avg_step_ms"),
+            "engine_avg_cycle_ms": allr[0]["engine"].get("avg_cycle_ms"),
+            "engine_avg_gpu_ms": allr[0]["engine"].get("avg_gpu_ms"),
             "boot_s": round(max(r["boot_s"] for r in allr), 1),
         }
         print(json.dumps(out), flush=True)

@@ -74,6 +74,7 @@ def main():
     snap = eng.snapshot()
     eng.stop()
     r.update({"avg_step_ms": snap["avg_step_ms"], "graphs": snap["graphs_captured"],
+              "avg_cycle_ms": snap["avg_cycle_ms"], "avg_gpu_ms": snap["avg_gpu_ms"], "avg_host_ms": snap["avg_host_ms"],
               "weights_gb": eng.model.weight_bytes() / 1e9})
     # pure decode step timing at a fixed batch
     print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}))

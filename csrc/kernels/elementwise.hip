@@ -77,40 +77,22 @@ void launch_rmsnorm(const uint16_t* x, int ldx, uint16_t* res, int ldres, const 
     hipLaunchKernelGGL(rmsnorm_kernel<8>, grid, block, 0, st, x, ldx, res, ldres, w, y, ldy, H, eps);
 }
 
-// Also emits the row's sum of squares (ssq[t][0], zeros in [1, H/4)) for the first
-// layer's fused RMSNorm prologue (same hand-off format as the GEMM residual epilogue).
 __global__ __launch_bounds__(256) void embedding_kernel(const int32_t* __restrict__ ids,
                                                          const bf16_t* __restrict__ table,
                                                          bf16_t* __restrict__ out, int H,
-                                                         int vstart, int vrows, float* ssq) {
-  __shared__ float red[16];
+                                                         int vstart, int vrows) {
   const int t = blockIdx.x;
   const int id = ids[t] - vstart;
   const bool ok = id >= 0 && id < vrows;
   const uint4* src = reinterpret_cast<const uint4*>(table + (size_t)(ok ? id : 0) * H);
   uint4* dst = reinterpret_cast<uint4*>(out + (size_t)t * H);
-  float ss = 0.f;
-  for (int c = threadIdx.x; c < (H >> 3); c += blockDim.x) {
-    const uint4 v = ok ? src[c] : make_uint4(0, 0, 0, 0);
-    dst[c] = v;
-    if (ssq) {
-      float f[8];
-      unpack8(v, f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
-    }
-  }
-  if (ssq) {
-    ss = block_reduce_sum(ss, red);
-    float* row = ssq + (size_t)t * (H >> 2);
-    for (int i = threadIdx.x; i < (H >> 2); i += blockDim.x) row[i] = (i == 0) ? ss : 0.f;
-  }
+  for (int c = threadIdx.x; c < (H >> 3); c += blockDim.x) dst[c] = ok ? src[c] : make_uint4(0, 0, 0, 0);
 }
 
 void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int T, int H,
-                      int vstart, int vrows, hipStream_t st, float* ssq_out) {
+                      int vstart, int vrows, hipStream_t st) {
   if (T <= 0) return;
-  hipLaunchKernelGGL(embedding_kernel, dim3(T), dim3(256), 0, st, ids, table, out, H, vstart, vrows, ssq_out);
+  hipLaunchKernelGGL(embedding_kernel, dim3(T), dim3(256), 0, st, ids, table, out, H, vstart, vrows);
 }
 
 // One workgroup per token. Work items:

@@ -22,8 +22,11 @@
 // small-N projections (o_proj / down_proj: 96 tiles) still fill all 256 CUs.
 //
 // Fusions:
-//   NORM prologue : x := bf16(bf16(x * rsqrt(mean(x^2) + eps)) * w) computed on the
-//                   fly from the residual stream (RMSNorm never runs as a kernel);
+//   NORM          : RMSNorm folded into the GEMM with a DEFERRED row scale:
+//                   out = rsqrt(mean(x^2) + eps) * (bf16(x * w) @ W^T). The sum of squares
+//                   is accumulated from the same x fragments the MFMA loop already loads
+//                   (no prologue pass, no serial latency before the weight stream) and
+//                   applied per row in the epilogue (RMSNorm never runs as a kernel);
 //   row_idx       : rows gathered by index (LM head reads only sampled rows);
 //   epilogues     : +bias, +residual (in place), SiLU(gate)*up (tile pairs),
 //                   f32 logits, and QKV: bias + NeoX RoPE + paged KV-cache write
@@ -52,7 +55,6 @@ struct GemmParams {
   const int32_t* positions; const int32_t* slots; const float* cos_sin;
   bf16_t* k_cache; bf16_t* v_cache; int hq; int hkv; int bs;
   const bf16_t* scales; const bf16_t* zeros; int group;
-  const float* ssq_in; float* ssq_out; int ssq_parts;
 };
 
 __device__ __forceinline__ int row_of(const GemmParams& p, int m) {
@@ -60,55 +62,24 @@ __device__ __forceinline__ int row_of(const GemmParams& p, int m) {
   return p.row_idx ? p.row_idx[m] : m;
 }
 
-// LDS carve (one dynamic array; Guideline 17): [reduce | inv_rms[64] | flag]
+// LDS carve (one dynamic array; Guideline 17): [reduce | ssq[nw][16*MB] | flag]
 template <int MB, int NTB>
 __host__ __device__ constexpr int red_bytes(int nw) { return nw > 1 ? nw * MB * NTB * 64 * 16 : 0; }
-
-// ---- NORM prologue: inv_rms of the block's rows, stored in LDS ----
-// Fast path (ssq_in): the kernel that produced x left deterministic per-row partial
-// sums of squares (ssq_parts floats per row) in its epilogue, so one short L2 read per
-// row replaces re-reading the whole row. A fixed group of TPR lanes owns each row and
-// reduces with xor-shuffles, so the summation order is fixed (bit-reproducible).
-// Fallback: sum x^2 over the full row (TP ranks, whose residual is all-reduced later).
 template <int MB>
-__device__ __forceinline__ void norm_prologue(const GemmParams& p, float* inv, int m_base) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  if (p.ssq_in) {
-    const int tpr = (int)blockDim.x / (16 * MB);  // power of two, <= 64
-    const int r = threadIdx.x / tpr, sub = threadIdx.x % tpr;
-    const float* src = p.ssq_in + (size_t)row_of(p, m_base + r) * p.ssq_parts;
-    float ss = 0.f;
-    for (int i = sub; i < p.ssq_parts; i += tpr) ss += src[i];
-    for (int o = tpr >> 1; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
-    if (sub == 0) inv[r] = rsqrtf(ss / (float)p.K + p.eps);
-    __syncthreads();
-    return;
-  }
-  const int nvec = p.K >> 3;
-  for (int r = wid; r < 16 * MB; r += nw) {
-    const int m = m_base + r;
-    const uint4* xr = reinterpret_cast<const uint4*>(p.x + (size_t)row_of(p, m) * p.lda);
-    float ss = 0.f;
-    for (int c = lane; c < nvec; c += 64) {
-      float f[8];
-      unpack8(xr[c], f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
-    }
-    ss = wave_reduce_sum(ss);
-    if (lane == 0) inv[r] = rsqrtf(ss / (float)p.K + p.eps);
-  }
-  __syncthreads();
-}
+__host__ __device__ constexpr int ssq_bytes(int nw) { return nw * MB * 16 * 4; }
 
-// normalise one A fragment (8 elements of row m at column k0) in registers
-__device__ __forceinline__ uint4 norm_frag(uint4 a, float inv, const bf16_t* w, int k0) {
+// NORM: one A fragment (8 elements of row m at column k0): accumulate x^2 for the
+// deferred row scale and return bf16(x * w) for the MFMA.
+__device__ __forceinline__ uint4 norm_frag(uint4 a, const bf16_t* w, int k0, float& ss) {
   const uint4 wv = *reinterpret_cast<const uint4*>(w + k0);
   float f[8], g[8];
   unpack8(a, f);
   unpack8(wv, g);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = bf2f(f2bf(f[j] * inv)) * g[j];
+  for (int j = 0; j < 8; ++j) {
+    ss += f[j] * f[j];
+    f[j] *= g[j];
+  }
   return pack8(f);
 }
 
@@ -194,24 +165,41 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[N
         pk.x = pack_bf2(o[0], o[1]);
         pk.y = pack_bf2(o[2], o[3]);
         *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + n) = pk;
-        if (p.ssq_out) {  // partial sum of squares of the stored (bf16) values, for the next norm
-          const float a0 = __uint_as_float(pk.x << 16), a1 = __uint_as_float(pk.x & 0xffff0000u);
-          const float a2 = __uint_as_float(pk.y << 16), a3 = __uint_as_float(pk.y & 0xffff0000u);
-          p.ssq_out[(size_t)m * p.ssq_parts + (n >> 2)] = a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
-        }
       }
     }
   }
 }
 
 // ---- cross-wave reduction, optional in-launch split-K combine, epilogue ----
-template <int MB, int NTB, int EPI>
-__device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB][NTB], char* smem, int m_base,
-                                            int nt0) {
+// Row scale of the deferred RMSNorm: the waves' partial sums of squares (LDS, fixed
+// summation order -> bit-reproducible) -> rsqrt(mean + eps).
+template <int MB>
+__device__ __forceinline__ float row_scale(const GemmParams& p, const float* ssqw, int r) {
+  const int nw = blockDim.x >> 6;
+  float ss = 0.f;
+  for (int w = 0; w < nw; ++w) ss += ssqw[w * 16 * MB + r];
+  return rsqrtf(ss / (float)p.K + p.eps);
+}
+
+template <int MB, int NTB, int EPI, bool NORM>
+__device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB][NTB], const float (&ssr)[MB],
+                                            char* smem, int m_base, int nt0) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   constexpr int SLOTS = MB * NTB * 64;  // f32x4 slots per block tile
   f32x4* red4 = reinterpret_cast<f32x4*>(smem);
-  int* flag = reinterpret_cast<int*>(smem + red_bytes<MB, NTB>(nw) + 256);
+  float* ssqw = reinterpret_cast<float*>(smem + red_bytes<MB, NTB>(nw));
+  int* flag = reinterpret_cast<int*>(smem + red_bytes<MB, NTB>(nw) + ssq_bytes<MB>(nw));
+  if constexpr (NORM) {
+    // lanes l, l^16, l^32, l^48 hold the same row: fold them, publish one value per row
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      float v = ssr[mb];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (lane < 16) ssqw[wid * 16 * MB + mb * 16 + lane] = v;
+    }
+    if (nw == 1) __syncthreads();
+  }
   if (nw > 1) {
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
@@ -220,7 +208,7 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
     __syncthreads();
   }
   const int tile = blockIdx.y * gridDim.x + blockIdx.x;
-  if (p.splitk > 1) {
+  if (!NORM && p.splitk > 1) {  // host never splits K under NORM (the row scale needs all of K)
     // 1) this slice's partial tile -> fp32 slab [tile][slice][SLOTS]
     f32x4* slab = reinterpret_cast<f32x4*>(p.slabs) + ((size_t)tile * p.splitk + blockIdx.z) * SLOTS;
     for (int s = threadIdx.x; s < SLOTS; s += blockDim.x) {
@@ -290,6 +278,11 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
 #pragma unroll
           for (int j = 0; j < NTB; ++j) v[j] = acc[mm][j];
     }
+    if constexpr (NORM) {
+      const float sc = row_scale<MB>(p, ssqw, mb * 16 + (l & 15));
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) v[j] *= sc;
+    }
     if (m < p.M) epilogue<NTB, EPI>(p, v, m, nt0, 4 * (l >> 4));
   }
 }
@@ -305,9 +298,6 @@ __global__ __launch_bounds__(1024) void gemm_kernel(GemmParams p) {
   const int s0 = (KT * blockIdx.z) / p.splitk, s1 = (KT * (blockIdx.z + 1)) / p.splitk;
   const int kbeg = s0 + ((s1 - s0) * wid) / nw;
   const int kend = s0 + ((s1 - s0) * (wid + 1)) / nw;
-  float* inv = reinterpret_cast<float*>(smem + red_bytes<MB, NTB>(nw));
-  if constexpr (NORM) norm_prologue<MB>(p, inv, m_base);
-
   f32x4 acc[MB][NTB];
 #pragma unroll
   for (int a = 0; a < MB; ++a)
@@ -317,11 +307,11 @@ __global__ __launch_bounds__(1024) void gemm_kernel(GemmParams p) {
 #pragma unroll
   for (int j = 0; j < NTB; ++j) wbase[j] = p.wp + ((size_t)(nt0 + j) * KT) * 64 + lane;
   const bf16_t* xrow[MB];
-  float rinv[MB];
+  float ssr[MB];
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
     xrow[mb] = p.x + (size_t)row_of(p, m_base + mb * 16 + (lane & 15)) * p.lda + 8 * (lane >> 4);
-    rinv[mb] = NORM ? inv[mb * 16 + (lane & 15)] : 1.f;
+    ssr[mb] = 0.f;
   }
   const bf16_t* nw_ptr = p.norm_w + 8 * (lane >> 4);
 
@@ -341,7 +331,7 @@ __global__ __launch_bounds__(1024) void gemm_kernel(GemmParams p) {
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb) a[u][mb] = norm_frag(a[u][mb], rinv[mb], nw_ptr, (kt + u) * 32);
+        for (int mb = 0; mb < MB; ++mb) a[u][mb] = norm_frag(a[u][mb], nw_ptr, (kt + u) * 32, ssr[mb]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -357,14 +347,14 @@ __global__ __launch_bounds__(1024) void gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
       a[mb] = *reinterpret_cast<const uint4*>(xrow[mb] + kt * 32);
-      if constexpr (NORM) a[mb] = norm_frag(a[mb], rinv[mb], nw_ptr, kt * 32);
+      if constexpr (NORM) a[mb] = norm_frag(a[mb], nw_ptr, kt * 32, ssr[mb]);
     }
 #pragma unroll
     for (int j = 0; j < NTB; ++j)
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(as_bf16x8(b[j]), as_bf16x8(a[mb]), acc[mb][j]);
   }
-  gemm_finish<MB, NTB, EPI>(p, acc, smem, m_base, nt0);
+  gemm_finish<MB, NTB, EPI, NORM>(p, acc, ssr, smem, m_base, nt0);
 }
 
 // ---- AWQ W4A16 ----
@@ -385,19 +375,17 @@ __global__ __launch_bounds__(1024) void awq_gemm_kernel(GemmParams p) {
   const int s0 = (KQ * blockIdx.z) / p.splitk, s1 = (KQ * (blockIdx.z + 1)) / p.splitk;
   const int qbeg = s0 + ((s1 - s0) * wid) / nw;
   const int qend = s0 + ((s1 - s0) * (wid + 1)) / nw;
-  float* inv = reinterpret_cast<float*>(smem + red_bytes<MB, NTB>(nw));
-  if constexpr (NORM) norm_prologue<MB>(p, inv, m_base);
   f32x4 acc[MB][NTB];
 #pragma unroll
   for (int a = 0; a < MB; ++a)
 #pragma unroll
     for (int b = 0; b < NTB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   const bf16_t* xrow[MB];
-  float rinv[MB];
+  float ssr[MB];
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
     xrow[mb] = p.x + (size_t)row_of(p, m_base + mb * 16 + (lane & 15)) * p.lda + 8 * (lane >> 4);
-    rinv[mb] = NORM ? inv[mb * 16 + (lane & 15)] : 1.f;
+    ssr[mb] = 0.f;
   }
   const bf16_t* nw_ptr = p.norm_w + 8 * (lane >> 4);
   for (int kq = qbeg; kq < qend; ++kq) {
@@ -410,7 +398,7 @@ __global__ __launch_bounds__(1024) void awq_gemm_kernel(GemmParams p) {
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb) {
         a[u][mb] = *reinterpret_cast<const uint4*>(xrow[mb] + (kq * 4 + u) * 32);
-        if constexpr (NORM) a[u][mb] = norm_frag(a[u][mb], rinv[mb], nw_ptr, (kq * 4 + u) * 32);
+        if constexpr (NORM) a[u][mb] = norm_frag(a[u][mb], nw_ptr, (kq * 4 + u) * 32, ssr[mb]);
       }
 #pragma unroll
     for (int j = 0; j < NTB; ++j) {
@@ -428,7 +416,7 @@ __global__ __launch_bounds__(1024) void awq_gemm_kernel(GemmParams p) {
       }
     }
   }
-  gemm_finish<MB, NTB, EPI>(p, acc, smem, m_base, nt0);
+  gemm_finish<MB, NTB, EPI, NORM>(p, acc, ssr, smem, m_base, nt0);
 }
 
 // ------------------------------------------------------------------ host side
@@ -462,11 +450,12 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
   const int mchunks = (g.M + 16 * MB - 1) / (16 * MB);
   const int ksteps = AWQ ? g.K / 128 : g.K / 32;
   Plan pl = plan(nblk, mchunks, ksteps, MB, NTB, g.waves, g.splitk);
+  if (NORM) pl.splitk = 1;  // the deferred row scale needs the whole K range in one block
   const size_t need_slab = (size_t)nblk * mchunks * pl.splitk * MB * NTB * 64 * 16;
   if (pl.splitk > 1 && (g.slabs == nullptr || need_slab > g.slab_bytes || nblk * mchunks > g.max_counters))
     pl.splitk = 1;  // workspace too small: fall back to one slice (still correct)
   p.splitk = pl.splitk;
-  const size_t lds = red_bytes<MB, NTB>(pl.waves) + 256 + 16;
+  const size_t lds = red_bytes<MB, NTB>(pl.waves) + ssq_bytes<MB>(pl.waves) + 16;
   dim3 grid(nblk, mchunks, pl.splitk), block(64 * pl.waves);
   if constexpr (AWQ)
     hipLaunchKernelGGL((awq_gemm_kernel<MB, NTB, EPI, NORM>), grid, block, lds, st, p);
@@ -514,7 +503,6 @@ static GemmParams to_params(const GemmArgs& g) {
   p.positions = g.positions; p.slots = g.slots; p.cos_sin = g.cos_sin;
   p.k_cache = g.k_cache; p.v_cache = g.v_cache; p.hq = g.hq; p.hkv = g.hkv; p.bs = g.bs;
   p.scales = g.scales; p.zeros = g.zeros; p.group = g.group;
-  p.ssq_in = g.ssq_in; p.ssq_out = g.ssq_out; p.ssq_parts = g.ssq_parts;
   return p;
 }
 

@@ -42,10 +42,6 @@ struct GemmArgs {
   const uint16_t* scales;  // [K/group][N] bf16
   const uint16_t* zeros;   // [K/group][N] bf16 (= scale * zero)
   int group;
-  // residual-stream sum-of-squares hand-off for the fused RMSNorm prologue
-  const float* ssq_in;  // [M][ssq_parts] partials written by the producer of x (or null)
-  float* ssq_out;       // this GEMM's residual epilogue writes [M][N/4] partials (or null)
-  int ssq_parts;        // partials per row (= hidden / 4)
 };
 void launch_gemm(const GemmArgs& g, hipStream_t st);
 void launch_awq_gemm(const GemmArgs& g, hipStream_t st);
@@ -56,7 +52,7 @@ void launch_rmsnorm(const uint16_t* x, int ldx, uint16_t* res, int ldres, const 
 
 // Embedding gather with vocab-shard masking (TP): rows outside [vstart, vstart+vrows) -> 0.
 void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int T, int H,
-                      int vstart, int vrows, hipStream_t st, float* ssq_out = nullptr);
+                      int vstart, int vrows, hipStream_t st);
 
 // NeoX RoPE on q,k inside the fused qkv buffer + paged KV-cache write.
 // qkv: [T, (Hq + 2*Hkv) * D]; cos_sin: [max_pos, D] f32 (cos | sin halves)

@@ -50,8 +50,7 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
           const c10::optional<Tensor>& positions, const c10::optional<Tensor>& slots,
           const c10::optional<Tensor>& cos_sin, const c10::optional<Tensor>& k_cache,
           const c10::optional<Tensor>& v_cache, int64_t hq, int64_t hkv,
-          const c10::optional<Tensor>& awq_scales, const c10::optional<Tensor>& awq_zeros, int64_t group,
-          const c10::optional<Tensor>& ssq_in, const c10::optional<Tensor>& ssq_out) {
+          const c10::optional<Tensor>& awq_scales, const c10::optional<Tensor>& awq_zeros, int64_t group) {
   CHECK_DEV(x); CHECK_DEV(wp); CHECK_DEV(out);
   CHECK_DT(x, torch::kBFloat16);
   CHECK_LASTDIM(x); CHECK_LASTDIM(out);
@@ -111,19 +110,6 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
   g.v_cache = opt_ptr<uint16_t>(v_cache, torch::kBFloat16, "v_cache");
   g.hq = (int)hq; g.hkv = (int)hkv; g.bs = k_cache.has_value() && k_cache->defined() ? (int)k_cache->size(2) : 16;
   g.scales = opt_bf16(awq_scales); g.zeros = opt_bf16(awq_zeros); g.group = (int)group;
-  g.ssq_in = opt_ptr<const float>(ssq_in, torch::kFloat32, "ssq_in");
-  g.ssq_out = opt_ptr<float>(ssq_out, torch::kFloat32, "ssq_out");
-  if (g.ssq_in) {
-    TORCH_CHECK(g.norm_w, "ssq_in requires norm_w");
-    TORCH_CHECK(ssq_in->dim() == 2 && ssq_in->size(1) == K / 4 && ssq_in->is_contiguous(), "ssq_in must be [rows, K/4]");
-    g.ssq_parts = (int)(K / 4);
-  }
-  if (g.ssq_out) {
-    TORCH_CHECK(epi == 0 && g.res, "ssq_out is produced by the residual (bf16) epilogue");
-    TORCH_CHECK(ssq_out->dim() == 2 && ssq_out->size(1) == N / 4 && ssq_out->size(0) >= M && ssq_out->is_contiguous(),
-                "ssq_out must be [M, N/4]");
-    g.ssq_parts = (int)(N / 4);
-  }
   c10::DeviceGuard guard(x.device());
   if (awq) vgate::launch_awq_gemm(g, cur_stream());
   else vgate::launch_gemm(g, cur_stream());
@@ -149,8 +135,7 @@ void rmsnorm(const Tensor& x, const c10::optional<Tensor>& res, const Tensor& w,
                         (int)y.stride(0), (int)M, (int)H, (float)eps, cur_stream());
 }
 
-void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart,
-               const c10::optional<Tensor>& ssq_out) {
+void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart) {
   CHECK_DEV(ids); CHECK_DEV(table); CHECK_DEV(out);
   CHECK_DT(ids, torch::kInt32); CHECK_DT(table, torch::kBFloat16); CHECK_DT(out, torch::kBFloat16);
   TORCH_CHECK(table.is_contiguous() && out.is_contiguous(), "embedding: contiguous");
@@ -159,7 +144,7 @@ void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vsta
   c10::DeviceGuard guard(ids.device());
   vgate::launch_embedding(reinterpret_cast<const int32_t*>(ids.data_ptr()), bf16p(table),
                           bf16p_mut(out), (int)T, (int)H, (int)vstart, (int)table.size(0),
-                          cur_stream(), opt_ptr<float>(ssq_out, torch::kFloat32, "ssq_out"));
+                          cur_stream());
 }
 
 void rope_kv(Tensor& qkv, const Tensor& positions, const c10::optional<Tensor>& slots,
@@ -316,12 +301,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("waves") = 0, py::arg("splitk") = 0, py::arg("positions") = py::none(),
         py::arg("slots") = py::none(), py::arg("cos_sin") = py::none(), py::arg("k_cache") = py::none(),
         py::arg("v_cache") = py::none(), py::arg("hq") = 0, py::arg("hkv") = 0,
-        py::arg("awq_scales") = py::none(), py::arg("awq_zeros") = py::none(), py::arg("group") = 128,
-        py::arg("ssq_in") = py::none(), py::arg("ssq_out") = py::none());
+        py::arg("awq_scales") = py::none(), py::arg("awq_zeros") = py::none(), py::arg("group") = 128);
   m.def("attention", &attention, "unified paged attention: decode (split-K) + varlen prefill tiles, one launch");
   m.def("rmsnorm", &rmsnorm, "RMSNorm with optional fused residual add");
   m.def("embedding", &embedding, "vocab-sharded embedding gather (+row sum of squares)", py::arg("ids"),
-        py::arg("table"), py::arg("out"), py::arg("vstart") = 0, py::arg("ssq_out") = py::none());
+        py::arg("table"), py::arg("out"), py::arg("vstart") = 0);
   m.def("rope_kv", &rope_kv, "NeoX RoPE + paged KV-cache write");
   m.def("attn_decode", &attn_decode, "paged split-K decode attention");
   m.def("attn_prefill", &attn_prefill, "paged varlen causal prefill attention");

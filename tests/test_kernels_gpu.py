@@ -349,26 +349,20 @@ def test_unified_attention_mixed_batch(Hq, Hkv):
         assert _rel_err(out.view(T, Hq, D), r) < 2e-2
 
 
-def test_ssq_handoff_norm_matches_full_row_norm():
-    """residual epilogue ssq partials -> next GEMM's norm prologue == full-row RMSNorm."""
-    torch.manual_seed(15)
-    T, H, N = 11, 1536, 2048
-    C = ops.native()
-    ids = torch.randint(0, 1000, (T,), dtype=torch.int32, device=DEV)
-    table = torch.randn(1000, H, device=DEV).bfloat16()
-    ssq = torch.empty(T, H // 4, device=DEV)
-    resid = ops.embedding(ids, table, ssq_out=ssq)
+@pytest.mark.parametrize("T", [5, 40])
+@pytest.mark.parametrize("waves", [1, 4, 16])
+def test_deferred_norm_all_wave_counts(T, waves):
+    """Fused RMSNorm (deferred row scale, per-wave ssq partials) == rmsnorm_ref -> linear_ref,
+    for every wave decomposition, and bit-reproducible run to run."""
+    torch.manual_seed(15 + T + waves)
+    H, N = 1536, 2048
+    x = (torch.randn(T, H, device=DEV) * 3).bfloat16()
     nw = (torch.rand(H, device=DEV) + 0.5).bfloat16()
     w = (torch.randn(N, H, device=DEV) / math.sqrt(H)).bfloat16()
-    y_fast = ops.linear(resid, ops.Linear(w), norm=(nw, 1e-6), ssq_in=ssq)
-    y_full = ops.linear(resid, ops.Linear(w), norm=(nw, 1e-6))
-    assert _rel_err(y_fast, y_full) < 2e-3
-    # residual epilogue producer
-    x = torch.randn(T, 1536, device=DEV).bfloat16()
-    wo = (torch.randn(H, 1536, device=DEV) / math.sqrt(1536)).bfloat16()
-    ops.linear(x, ops.Linear(wo), out=resid, residual=resid, ssq_out=ssq)
-    exp = resid.float().pow(2).sum(-1)
-    assert torch.allclose(ssq.sum(-1), exp, rtol=1e-3)
-    y_fast = ops.linear(resid, ops.Linear(w), norm=(nw, 1e-6), ssq_in=ssq)
-    y_full = ops.linear(resid, ops.Linear(w), norm=(nw, 1e-6))
-    assert _rel_err(y_fast, y_full) < 2e-3
+    lin = ops.Linear(w)
+    y = ops.linear(x, lin, norm=(nw, 1e-6), waves=waves)
+    y2 = ops.linear(x, lin, norm=(nw, 1e-6), waves=waves)
+    xn, _ = ref.rmsnorm_ref(x.cpu(), nw.cpu(), 1e-6)
+    r = ref.linear_ref(xn, w.cpu())
+    assert _rel_err(y.float().cpu(), r.float()) < 1e-2
+    assert torch.equal(y, y2)

@@ -124,13 +124,9 @@ class DecoderModel:
         T, S = sv.T, sv.S
         D = a.head_dim
         dev = self.device
-        # Residual-stream sum-of-squares hand-off (TP=1): each producer of `resid` (embedding,
-        # o_proj / down_proj residual epilogues) writes per-row partials the next fused
-        # RMSNorm prologue reduces — no kernel ever re-reads a full row just for its norm.
-        # Under TP the residual is completed by an all-reduce after the GEMM, so the
-        # consumer normalises from the full row instead.
-        ssq = torch.empty(T, a.hidden_size // 4, dtype=torch.float32, device=dev) if tp.size == 1 else None
-        resid = ops.embedding(sv.ids, self.embed, vstart=sh.vocab0, ssq_out=ssq)
+        # RMSNorms are folded into the consuming GEMMs (deferred row scale), so a layer is
+        # qkv GEMM -> attention -> o GEMM (+residual) -> gate_up GEMM -> down GEMM (+residual).
+        resid = ops.embedding(sv.ids, self.embed, vstart=sh.vocab0)
         if tp.size > 1:
             tp.all_reduce(resid)
         q = torch.empty(T, sh.hq * D, dtype=torch.bfloat16, device=dev)
@@ -143,20 +139,19 @@ class DecoderModel:
         eps = a.rms_eps
         for li, L in enumerate(self.layers):
             kc, vc = kv_caches[li]
-            ops.linear(resid, L.qkv, out=q, norm=(L.in_norm, eps), ssq_in=ssq,
+            ops.linear(resid, L.qkv, out=q, norm=(L.in_norm, eps),
                        qkv=dict(positions=sv.positions, slots=sv.slots, cos_sin=self.cos_sin, k_cache=kc,
                                 v_cache=vc, hq=sh.hq, hkv=sh.hkv))
             ops.attention(q, sh.hq * D, kc, vc, sv.block_tables, sv.context_lens, sv.query_start, sv.tile_seq,
                           sv.tile_q0, attn, part_o, part_ml, sh.hq, sh.hkv, part_size, self.scale)
-            ops.linear(attn, L.o, out=resid, residual=resid if first else None, ssq_out=ssq)
+            ops.linear(attn, L.o, out=resid, residual=resid if first else None)
             if tp.size > 1:
                 tp.all_reduce(resid)
-            ops.linear(resid, L.gate_up, out=mlp, norm=(L.post_norm, eps), ssq_in=ssq)
-            ops.linear(mlp, L.down, out=resid, residual=resid if first else None, ssq_out=ssq)
+            ops.linear(resid, L.gate_up, out=mlp, norm=(L.post_norm, eps))
+            ops.linear(mlp, L.down, out=resid, residual=resid if first else None)
             if tp.size > 1:
                 tp.all_reduce(resid)
-        logits = ops.linear(resid, self.lm_head, out_f32=True, norm=(self.final_norm, eps), row_idx=sv.sample_idx,
-                            ssq_in=ssq)
+        logits = ops.linear(resid, self.lm_head, out_f32=True, norm=(self.final_norm, eps), row_idx=sv.sample_idx)
         if tp.size > 1:
             logits = tp.all_gather_lastdim(logits)
         return logits[:, : a.vocab_size]

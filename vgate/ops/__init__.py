@@ -196,11 +196,10 @@ def workspace(device) -> torch.Tensor:
 
 def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
            residual: torch.Tensor | None = None, out_f32: bool = False, waves: int = 0, splitk: int = 0,
-           norm: tuple | None = None, row_idx: torch.Tensor | None = None, qkv: dict | None = None,
-           ssq_in: torch.Tensor | None = None, ssq_out: torch.Tensor | None = None) -> torch.Tensor:
+           norm: tuple | None = None, row_idx: torch.Tensor | None = None, qkv: dict | None = None) -> torch.Tensor:
     """out = epilogue(prologue(x) @ W^T).
 
-    norm=(w, eps): fused RMSNorm of x rows; row_idx: gather rows of x first;
+    norm=(w, eps): fused RMSNorm of x rows (deferred row scale, see gemm.hip); row_idx: gather rows of x first;
     qkv=dict(positions, slots, cos_sin, k_cache, v_cache, hq, hkv): fused bias + RoPE +
     KV write, returns q [M, hq*128] (layout "qkv" only).
     """
@@ -240,10 +239,6 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
                   k_cache=qkv["k_cache"], v_cache=qkv["v_cache"], hq=qkv["hq"], hkv=qkv["hkv"])
     if lin.kind == "awq":
         kw.update(awq_scales=lin.scales, awq_zeros=lin.zeros, group=lin.group)
-    if ssq_in is not None:
-        kw["ssq_in"] = ssq_in
-    if ssq_out is not None:
-        kw["ssq_out"] = ssq_out
     C.gemm(x, lin.wp, lin.N, lin.K, out, epi, **kw)
     return out
 
@@ -271,15 +266,14 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor
     return out
 
 
-def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None, vstart: int = 0,
-              ssq_out: torch.Tensor | None = None):
-    """Row gather; optionally also emits per-row sum-of-squares partials ([T, H/4], total in col 0)."""
+def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None, vstart: int = 0):
+    """Row gather with vocab-shard masking (rows outside this TP rank's shard are zero)."""
     if out is None:
         out = torch.empty(ids.numel(), table.shape[1], dtype=table.dtype, device=table.device)
     if not _gpu(table):
         out.copy_(ref.embedding_ref(ids, table, vstart))
         return out
-    native().embedding(ids, table, out, vstart, ssq_out)
+    native().embedding(ids, table, out, vstart)
     return out
 
 

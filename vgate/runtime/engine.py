@@ -79,6 +79,7 @@ class EngineStats:
     prefill_tokens: int = 0
     decode_tokens: int = 0
     step_time_s: float = 0.0
+    cycle_time_s: float = 0.0  # schedule + execute + output processing
     requests_finished: int = 0
     last_step_ms: float = 0.0
     batch_sizes: collections.Counter = field(default_factory=collections.Counter)
@@ -247,6 +248,7 @@ class LLMEngine:
 
     # -------------------------------------------------------------------- step
     def step(self) -> int:
+        tc = time.perf_counter()
         batch = self.scheduler.schedule()
         if batch.empty:
             return 0
@@ -300,6 +302,7 @@ class LLMEngine:
                 seq.callback("token", seq, delta)
             if reason is not None:
                 self._finish(seq, reason)
+        st.cycle_time_s += time.perf_counter() - tc
         return len(batch.items)
 
     def _finish(self, seq: Sequence, reason: str, notify_sched: bool = True, error: str | None = None) -> None:
@@ -408,6 +411,9 @@ class LLMEngine:
             "kv_usage": round(self.kvm.usage(), 4), "steps": st.steps, "tokens_generated": st.tokens_generated,
             "prefill_tokens": st.prefill_tokens, "decode_tokens": st.decode_tokens,
             "avg_step_ms": round(1e3 * st.step_time_s / max(1, st.steps), 3),
+            "avg_cycle_ms": round(1e3 * st.cycle_time_s / max(1, st.steps), 3),
+            "avg_gpu_ms": round(self.runner.gpu_ms / max(1, self.runner.gpu_steps), 3),
+            "avg_host_ms": round(self.runner.host_ms / max(1, st.steps), 3),
             "graphs_captured": len(self.runner.graphs), "graph_hits": self.runner.graph_hits,
             "preemptions": self.scheduler.num_preemptions, "prefix_cache_hits": int(getattr(self.kvm.alloc, "hits", 0)),
             "healthy": self.healthy,

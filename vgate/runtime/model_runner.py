@@ -53,12 +53,16 @@ class ModelRunner:
         if self.gpu:
             self.out_host = torch.zeros(self.max_seqs, dtype=torch.int32, pin_memory=True)
             self.stream = torch.cuda.Stream(self.device)
-            self.done = torch.cuda.Event()
+            self.started = torch.cuda.Event(enable_timing=True)
+            self.done = torch.cuda.Event(enable_timing=True)
         else:
             self.out_host = self.out_tokens
         self.graph_hits = 0
         self.graph_misses = 0
         self.capture_seconds = 0.0
+        self.gpu_ms = 0.0  # device time of replayed steps (upload -> sampled ids on host)
+        self.host_ms = 0.0  # host time of execute() outside the device wait
+        self.gpu_steps = 0
 
     # ----------------------------------------------------------------- buckets
     def _bucket(self, buckets, n):
@@ -163,7 +167,10 @@ class ModelRunner:
             S = self._bucket(self.s_buckets, ns)
         else:
             T, S = nt, ns
+        t_host = time.perf_counter()
         samples = self._fill(batch, T, S)
+        if self.gpu:
+            self.started.record()
         self.meta.upload(ns)
         if self.gpu:
             if self.use_graphs:
@@ -183,7 +190,12 @@ class ModelRunner:
                 self._forward_sample(view)
             self.out_host[:ns].copy_(self.out_tokens[:ns], non_blocking=True)
             self.done.record()
+            t_wait = time.perf_counter()
             self.done.synchronize()
+            t_end = time.perf_counter()
+            self.host_ms += 1e3 * ((t_wait - t_host) + (time.perf_counter() - t_end))
+            self.gpu_ms += self.started.elapsed_time(self.done)
+            self.gpu_steps += 1
             toks = self.out_host[:ns].tolist()
         else:
             view = self.meta.view(T, S)

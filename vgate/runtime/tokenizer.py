@@ -3,14 +3,24 @@
 * :class:`HFTokenizer` wraps the ``tokenizers`` library when a ``tokenizer.json``
   is available next to a checkpoint.
 * :class:`SyntheticTokenizer` is the default for random-init models (no vocab
-  files exist on this machine): UTF-8 bytes map to ids ``[OFFSET, OFFSET+256)``
-  so any prompt round-trips exactly; ids outside that range (which a random
-  model emits freely) decode to short deterministic pseudo-words so generated
-  text has realistic length/shape for streaming and benchmarks.
+  files exist on this machine). It pre-tokenises like a byte-level BPE (words
+  with their leading space, digit groups, punctuation runs; long words split
+  into <= 6-byte pieces) and maps each multi-byte piece to a stable hashed id
+  (crc32, identical in every process) in ``[OFFSET+256, vocab)``, single bytes
+  to ``[OFFSET, OFFSET+256)``. Token counts therefore track a real BPE (~1.3
+  tokens per English word) instead of one token per byte, so prompt/prefill
+  load in benchmarks is realistic. Round-trips are exact (the piece of every
+  id this process encoded is remembered; a hash collision falls back to the
+  piece's bytes); ids never encoded here (a random model emits them freely)
+  decode to short deterministic pseudo-words.
 """
 from __future__ import annotations
 
+import re
+import zlib
 from pathlib import Path
+
+_PRETOK = re.compile(rb" ?[A-Za-z]+| ?[0-9]{1,3}| ?[^\sA-Za-z0-9]+|\s+")
 
 _SYLL = ["ka", "lo", "mi", "ne", "ru", "ta", "vo", "zi", "pe", "sa", "do", "fu", "gi", "ha", "ju", "be"]
 
@@ -23,16 +33,37 @@ class SyntheticTokenizer:
         self.bos_token_id = bos_token_id
         self.eos_token_ids = tuple(eos_token_ids)
         self._special = {bos_token_id, *self.eos_token_ids}
+        self._lo = self.OFFSET + 256
+        self._table: dict[int, bytes] = {}
+
+    def _pieces(self, data: bytes):
+        for m in _PRETOK.finditer(data):
+            p = m.group()
+            for i in range(0, len(p), 6):
+                yield p[i: i + 6]
 
     def encode(self, text: str, add_bos: bool = False) -> list[int]:
-        ids = [self.OFFSET + b for b in text.encode("utf-8")]
-        return ([self.bos_token_id] + ids) if add_bos else ids
+        ids = [self.bos_token_id] if add_bos else []
+        span = self.vocab_size - self._lo
+        for p in self._pieces(text.encode("utf-8")):
+            if len(p) > 1 and span > 0:
+                t = self._lo + zlib.crc32(p) % span
+                if t not in self._special:
+                    prev = self._table.setdefault(t, p)
+                    if prev == p:
+                        ids.append(t)
+                        continue
+            ids.extend(self.OFFSET + b for b in p)
+        return ids
 
     def _piece(self, t: int) -> bytes:
         if t in self._special:
             return b""
-        if self.OFFSET <= t < self.OFFSET + 256:
+        if self.OFFSET <= t < self._lo:
             return bytes([t - self.OFFSET])
+        known = self._table.get(t)
+        if known is not None:
+            return known
         h = (t * 2654435761) & 0xFFFFFFFF
         w = _SYLL[h & 15] + _SYLL[(h >> 4) & 15]
         if (h >> 8) & 1:
