@@ -3,7 +3,10 @@
   1. per-kernel floor: N trivial launches captured in one hipGraph, replayed;
   2. decode GEMM sweep: every Qwen2.5-1.5B projection at M=8 over (waves, split-K),
      each timed as 20 launches inside a hipGraph (no host overhead), reporting
-     us/launch and effective weight bandwidth.
+     us/launch and effective weight bandwidth. The launches cycle through enough
+     weight copies (> 512 MB) that every launch streams its weights from HBM, as in
+     the real forward (the 256 MB MALL would otherwise serve a repeated matrix);
+  3. decode attention (unified kernel) and the sampler at the bench shape.
 
     python benchmarks/micro_gpu.py [--quick]
 """
@@ -71,27 +74,73 @@ def sweep(M=8, quick=False):
     for name, N, K, layout, f32 in SHAPES:
         x = torch.randn(M, K, device="cuda").bfloat16()
         w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).bfloat16()
-        lin = ops.Linear(w, layout=layout)
+        ncopy = max(1, math.ceil(512e6 / (N * K * 2)))
+        lins = [ops.Linear(w, layout=layout) for _ in range(ncopy)]
+        lin = lins[0]
+        cyc = {"i": 0}
+
+        def nxt():
+            cyc["i"] = (cyc["i"] + 1) % ncopy
+            return lins[cyc["i"]]
         res = torch.randn(M, N, device="cuda").bfloat16() if name in ("o_proj", "down") else None
         y = torch.empty(M, lin.out_features, device="cuda", dtype=torch.float32 if f32 else torch.bfloat16)
         nbytes = N * K * 2
         rows = []
-        waves = [1, 2, 4, 8, 16] if not quick else [4, 8, 16]
+        waves = [1, 2, 4, 8, 16] if not quick else [4, 8]
         splits = [1, 2, 4, 8] if name not in ("gate_up", "lm_head") else [1, 2]
         for wv in waves:
             for sk in splits:
                 try:
-                    t = graph_time(lambda: ops.linear(x, lin, out=y, residual=res, out_f32=f32, waves=wv, splitk=sk))
+                    t = graph_time(lambda: ops.linear(x, nxt(), out=y, residual=res, out_f32=f32, waves=wv, splitk=sk))
                 except Exception as e:  # noqa: BLE001
                     rows.append({"waves": wv, "splitk": sk, "error": str(e)[:80]})
                     continue
                 rows.append({"waves": wv, "splitk": sk, "us": round(t, 2), "TBps": round(nbytes / t / 1e6, 2)})
-        auto = graph_time(lambda: ops.linear(x, lin, out=y, residual=res, out_f32=f32))
+        auto = graph_time(lambda: ops.linear(x, nxt(), out=y, residual=res, out_f32=f32))
         best = min((r for r in rows if "us" in r), key=lambda r: r["us"])
         out.append({"shape": name, "N": N, "K": K, "M": M, "auto_us": round(auto, 2),
                     "auto_TBps": round(nbytes / auto / 1e6, 2), "best": best, "all": rows})
         print(json.dumps(out[-1]), flush=True)
     return out
+
+
+def attention_bench(S=8, ctx=64, Hq=12, Hkv=2, D=128, part=2048, max_len=2048):
+    """Decode attention (S sequences, 1 query token each) through the unified kernel."""
+    bs, nblk = 16, 4096
+    kc = torch.randn(nblk, Hkv, bs, D, device="cuda").bfloat16()
+    vc = torch.randn(nblk, Hkv, bs, D, device="cuda").bfloat16()
+    mb = (ctx + bs - 1) // bs
+    bt = torch.randperm(nblk, device="cuda")[: S * mb].view(S, mb).int().contiguous()
+    cl = torch.full((S,), ctx, dtype=torch.int32, device="cuda")
+    qs = torch.arange(S + 1, dtype=torch.int32, device="cuda")
+    q = torch.randn(S, Hq * D, device="cuda").bfloat16()
+    out = torch.empty(S, Hq * D, device="cuda").bfloat16()
+    ts = torch.full((S,), -1, dtype=torch.int32, device="cuda")
+    tq = torch.zeros(S, dtype=torch.int32, device="cuda")
+    P = (max_len + part - 1) // part
+    po = torch.empty(S, Hq, P, D, device="cuda")
+    pml = torch.empty(S, Hq, P, 2, device="cuda")
+    bt = torch.cat([bt, torch.zeros(S, max_len // bs - mb, dtype=torch.int32, device="cuda")], 1).contiguous()
+    t = graph_time(lambda: ops.attention(q, Hq * D, kc, vc, bt, cl, qs, ts, tq, out, po, pml, Hq, Hkv, part,
+                                         1 / math.sqrt(D)))
+    return {"attention_decode": {"S": S, "ctx": ctx, "part": part, "Hq": Hq, "Hkv": Hkv, "us": round(t, 2)}}
+
+
+def sampler_bench(B=8, V=151936):
+    logits = torch.randn(B, V, device="cuda") * 2
+    temp = torch.full((B,), 0.7, device="cuda")
+    topp = torch.full((B,), 0.9, device="cuda")
+    topk = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+    seeds = torch.arange(B, dtype=torch.int64, device="cuda")
+    offs = torch.zeros(B, dtype=torch.int64, device="cuda")
+    out = torch.empty(B, dtype=torch.int32, device="cuda")
+    res = {}
+    for name, tp in (("top_p0.9", topp), ("plain", torch.ones_like(topp))):
+        t = graph_time(lambda: ops.sample(logits, temp, tp, topk, seeds, offs, out=out))
+        res[name] = round(t, 2)
+    t = graph_time(lambda: ops.sample(logits, torch.zeros_like(temp), topp, topk, seeds, offs, out=out))
+    res["greedy"] = round(t, 2)
+    return {"sampler_us": res, "B": B, "V": V}
 
 
 def main():
@@ -100,6 +149,10 @@ def main():
     ap.add_argument("--M", type=int, default=8)
     a = ap.parse_args()
     print(json.dumps(floor()), flush=True)
+    for ctx in (64, 512, 2048):
+        for part in (256, 512, 2048):
+            print(json.dumps(attention_bench(ctx=ctx, part=part)), flush=True)
+    print(json.dumps(sampler_bench()), flush=True)
     sweep(a.M, a.quick)
 
 

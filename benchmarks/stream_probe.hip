@@ -1,0 +1,133 @@
+// HBM streaming probe for gfx950: how many CUs / waves / loads-in-flight does it take to
+// stream a once-read weight matrix at full bandwidth? (Calibrates the decode GEMM
+// decomposition in csrc/kernels/gemm.hip.)
+//
+//   hipcc --offload-arch=gfx950 -O3 -o build/stream_probe benchmarks/stream_probe.hip
+//   build/stream_probe            -> one JSON line per configuration
+//
+// Each block streams a contiguous slice (1 KiB per wave-instruction, like the packed
+// weight fragments), accumulating an XOR so the loads cannot be elided. A buffer set
+// of > 1 GB is cycled so every launch reads from HBM (not the 256 MB MALL).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// X: also issue one L2-resident 16-B "activation" load per weight load (as the decode
+// GEMM's B operand does), to price the extra vector-memory requests.
+template <int U, bool NT, bool X = false>
+__global__ __launch_bounds__(1024) void stream_kernel(const uint4* __restrict__ src, size_t per_block16,
+                                                      unsigned* sink, const uint4* __restrict__ xs = nullptr) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint4* base = src + (size_t)blockIdx.x * per_block16;
+  // wave w takes a contiguous range of 64-lane "fragments" (1 KiB each)
+  const size_t nfrag = per_block16 / 64;
+  const size_t f0 = nfrag * wid / nw, f1 = nfrag * (wid + 1) / nw;
+  unsigned acc = 0;
+  size_t f = f0;
+  for (; f + U <= f1; f += U) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint4* p = base + (f + u) * 64 + lane;
+      if (NT) {
+        u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+        v[u] = make_uint4(t.x, t.y, t.z, t.w);
+      } else {
+        v[u] = *p;
+      }
+    }
+    if (X) {
+      uint4 xv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) xv[u] = xs[((f + u) * 64 + lane) & 8191];
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc += xv[u].x ^ xv[u].w;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  for (; f < f1; ++f) {
+    const uint4 v = base[f * 64 + lane];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;  // practically never: keeps the loads live
+}
+
+template <int U, bool NT, bool X = false>
+static float run(const std::vector<uint4*>& bufs, size_t bytes, int blocks, int waves, unsigned* sink,
+                 const uint4* xs = nullptr) {
+  const size_t per_block16 = bytes / 16 / blocks / 64 * 64;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int reps = 40;
+  for (int i = 0; i < 4; ++i)
+    hipLaunchKernelGGL((stream_kernel<U, NT, X>), dim3(blocks), dim3(64 * waves), 0, 0, bufs[i % bufs.size()], per_block16, sink, xs);
+  CK(hipEventRecord(e0));
+  for (int i = 0; i < reps; ++i)
+    hipLaunchKernelGGL((stream_kernel<U, NT, X>), dim3(blocks), dim3(64 * waves), 0, 0, bufs[i % bufs.size()], per_block16, sink, xs);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms * 1e3f / reps;  // us per launch (includes launch overhead)
+}
+
+int main() {
+  const size_t sizes[] = {4718592, 27525120, 55050240};  // o_proj, down_proj, gate_up bytes (Qwen2.5-1.5B)
+  std::vector<uint4*> bufs;
+  const size_t maxb = 55050240;
+  for (int i = 0; i < 24; ++i) {  // 1.3 GB > MALL
+    uint4* p;
+    CK(hipMalloc(&p, maxb));
+    CK(hipMemset(p, i + 1, maxb));
+    bufs.push_back(p);
+  }
+  unsigned* sink;
+  CK(hipMalloc(&sink, 64));
+  uint4* xs;
+  CK(hipMalloc(&xs, 8192 * 16));
+  CK(hipMemset(xs, 3, 8192 * 16));
+  for (int blocks : {96, 192, 256}) {
+    for (int waves : {8, 16}) {
+      const size_t bytes = 27525120;
+      const float a = run<8, true>(bufs, bytes, blocks, waves, sink);
+      const float b = run<8, true, true>(bufs, bytes, blocks, waves, sink, xs);
+      printf("{\"xprobe\": 1, \"bytes\": %zu, \"blocks\": %d, \"waves\": %d, \"us_w\": %.2f, \"us_w_plus_x\": %.2f}\n",
+             bytes, blocks, waves, a, b);
+      fflush(stdout);
+    }
+  }
+  const int blocks_list[] = {64, 96, 192, 256, 512, 1024};
+  const int waves_list[] = {4, 8, 16};
+  if (getenv("PROBE_X_ONLY")) return 0;
+  for (size_t bytes : sizes) {
+    for (int blocks : blocks_list) {
+      for (int waves : waves_list) {
+        const float t4 = run<4, true>(bufs, bytes, blocks, waves, sink);
+        const float t8 = run<8, true>(bufs, bytes, blocks, waves, sink);
+        const float t16 = run<16, true>(bufs, bytes, blocks, waves, sink);
+        const float t8n = run<8, false>(bufs, bytes, blocks, waves, sink);
+        printf("{\"bytes\": %zu, \"blocks\": %d, \"waves\": %d, \"us_U4nt\": %.2f, \"us_U8nt\": %.2f, "
+               "\"us_U16nt\": %.2f, \"us_U8\": %.2f, \"best_TBps\": %.2f}\n",
+               bytes, blocks, waves, t4, t8, t16, t8n,
+               bytes / 1e6 / std::min(std::min(t4, t8), std::min(t16, t8n)));
+        fflush(stdout);
+      }
+    }
+  }
+  return 0;
+}

@@ -130,21 +130,42 @@ __device__ __forceinline__ bf16x8 softmax_step(f32x4& s0, f32x4& s1, float& m, f
   return pack_p(s0, s1);
 }
 
+// LDS: max(decode V images, decode merge scratch, prefill double buffer) | ticket flag
+__host__ __device__ constexpr int attn_flag_off(int nw) {
+  const int vimg = nw * CHUNK * D_ * 2;
+  const int merge = (2 * 16 * nw + nw * D_ * 16) * 4;
+  const int pre = 2 * CHUNK * D_ * 2;
+  const int m = vimg > merge ? vimg : merge;
+  return m > pre ? m : pre;
+}
+
 // ---------------------------------------------------------------- decode ----
 // One block per (sequence, KV head, partition); its nw waves take chunks w, w+nw, ...
 // Query columns = the G = Hq/Hkv heads sharing this KV head. Only sequences with a
 // single new query token are decode work (prefill tiles cover the rest).
 __device__ __forceinline__ void decode_body(const AttnArgs& a, int s, int h, int part, char* smem) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int ctx = a.context_lens[s];
   const int pstart = part * a.part_size;
+  const int* bt = a.block_tables + (size_t)s * a.max_blocks;
+  // Issue every independent load of the dependency chain up front: context length,
+  // query offsets and this wave's first two block-table entries (the row is always
+  // in bounds) are in flight together, so K/V addresses are ready one round trip in.
+  const int ctx = a.context_lens[s];
+  const int qbeg = a.query_start ? a.query_start[s] : s;
+  const int qend = a.query_start ? a.query_start[s + 1] : s + 1;
+  const int bi0 = min((pstart + wid * CHUNK) / BS_, a.max_blocks - 1);
+  const int bt_first0 = bt[bi0];
+  const int bt_first1 = bt[min(bi0 + 1, a.max_blocks - 1)];
   if (ctx <= 0 || pstart >= ctx) return;
-  if (a.query_start && a.query_start[s + 1] - a.query_start[s] != 1) return;
+  if (qend - qbeg != 1) return;
   const int pend = min(ctx, pstart + a.part_size);
   const int nparts = (ctx + a.part_size - 1) / a.part_size;
   const int G = a.Hq / a.Hkv;
   const int col = lane & 15;
-  const int qtok = a.query_start ? a.query_start[s + 1] - 1 : s;
+  const int qtok = qbeg;
+  const int nch = (pend - pstart + CHUNK - 1) / CHUNK;
+  const bool ticketed = nparts > 1 && a.tickets != nullptr;
+  if (nch <= 1 && wid > 0 && !ticketed) return;  // single chunk: wave 0 alone, no merge
 
   uint4 qf[4];
   {
@@ -161,15 +182,14 @@ __device__ __forceinline__ void decode_body(const AttnArgs& a, int s, int h, int
   for (int mt = 0; mt < 8; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   bf16_t* vl = reinterpret_cast<bf16_t*>(smem) + wid * (CHUNK * D_);
-  const int* bt = a.block_tables + (size_t)s * a.max_blocks;
   const size_t head_off = (size_t)h * BS_ * D_;
   const size_t blk_stride = (size_t)a.Hkv * BS_ * D_;
-  const int nch = (pend - pstart + CHUNK - 1) / CHUNK;
 
   for (int c = wid; c < nch; c += nw) {
     const int tb = pstart + c * CHUNK;
-    const int b0 = bt[tb / BS_];
-    const int b1 = (tb + BS_ < pend) ? bt[tb / BS_ + 1] : b0;
+    const bool first = c == wid;
+    const int b0 = first ? bt_first0 : bt[tb / BS_];
+    const int b1 = (tb + BS_ < pend) ? (first ? bt_first1 : bt[tb / BS_ + 1]) : b0;
     const bf16_t* kb0 = a.k_cache + (size_t)b0 * blk_stride + head_off;
     const bf16_t* kb1 = a.k_cache + (size_t)b1 * blk_stride + head_off;
     const bf16_t* vb0 = a.v_cache + (size_t)b0 * blk_stride + head_off;
@@ -187,53 +207,122 @@ __device__ __forceinline__ void decode_body(const AttnArgs& a, int s, int h, int
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
 
-  // ---- merge the nw waves: scratch reuses the V images ----
-  __syncthreads();
-  float* sm_m = reinterpret_cast<float*>(smem);   // [nw][16]
-  float* sm_l = sm_m + 16 * nw;                   // [nw][16]
-  float* sm_o = sm_l + 16 * nw;                   // [nw][128][16]
-  if (lane < 16) {
-    sm_m[wid * 16 + lane] = m;
-    sm_l[wid * 16 + lane] = l;
-  }
-  {
-    const int g = lane >> 4;
+  if (nch <= 1) {  // wave 0 holds the whole result: normalise and store from registers
+    if (wid == 0 && col < G) {
+      const int hq = h * G + col;
+      const int g = lane >> 4;
+      const float inv = l > 0.f ? 1.f / l : 0.f;
+      if (nparts == 1) {
+        bf16_t* op = a.out + (size_t)qtok * a.out_stride + (size_t)hq * D_;
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt)
+        for (int mt = 0; mt < 8; ++mt) {
+          uint2 pk;
+          pk.x = pack_bf2(o[mt][0] * inv, o[mt][1] * inv);
+          pk.y = pack_bf2(o[mt][2] * inv, o[mt][3] * inv);
+          *reinterpret_cast<uint2*>(op + 16 * mt + 4 * g) = pk;
+        }
+      } else {
+        float* po = a.part_o + (((size_t)s * a.Hq + hq) * a.num_parts + part) * D_;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sm_o[(wid * D_ + 16 * mt + 4 * g + i) * 16 + col] = o[mt][i];
-  }
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < G * (D_ / 4); idx += blockDim.x) {
-    const int cc = idx / (D_ / 4);
-    const int d0 = (idx % (D_ / 4)) * 4;
-    float M = -INFINITY;
-    for (int w = 0; w < nw; ++w) M = fmaxf(M, sm_m[w * 16 + cc]);
-    float L = 0.f, acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int w = 0; w < nw; ++w) {
-      const float mw = sm_m[w * 16 + cc];
-      const float f = (mw == -INFINITY) ? 0.f : exp2f(mw - M);
-      L += sm_l[w * 16 + cc] * f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] += sm_o[(w * D_ + d0 + j) * 16 + cc] * f;
-    }
-    const float inv = L > 0.f ? 1.f / L : 0.f;
-    const int hq = h * G + cc;
-    if (nparts == 1) {
-      bf16_t* op = a.out + (size_t)qtok * a.out_stride + (size_t)hq * D_ + d0;
-      uint2 pk;
-      pk.x = pack_bf2(acc[0] * inv, acc[1] * inv);
-      pk.y = pack_bf2(acc[2] * inv, acc[3] * inv);
-      *reinterpret_cast<uint2*>(op) = pk;
-    } else {
-      float* po = a.part_o + (((size_t)s * a.Hq + hq) * a.num_parts + part) * D_ + d0;
-      *reinterpret_cast<float4*>(po) = make_float4(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
-      if (d0 == 0) {
-        float* pm = a.part_ml + (((size_t)s * a.Hq + hq) * a.num_parts + part) * 2;
-        pm[0] = M;
-        pm[1] = L;
+        for (int mt = 0; mt < 8; ++mt)
+          *reinterpret_cast<float4*>(po + 16 * mt + 4 * g) =
+              make_float4(o[mt][0] * inv, o[mt][1] * inv, o[mt][2] * inv, o[mt][3] * inv);
+        if (g == 0) {
+          float* pm = a.part_ml + (((size_t)s * a.Hq + hq) * a.num_parts + part) * 2;
+          pm[0] = m;
+          pm[1] = l;
+        }
       }
     }
+  } else {
+    // ---- merge the nw waves: scratch reuses the V images ----
+    __syncthreads();
+    float* sm_m = reinterpret_cast<float*>(smem);   // [nw][16]
+    float* sm_l = sm_m + 16 * nw;                   // [nw][16]
+    float* sm_o = sm_l + 16 * nw;                   // [nw][128][16]
+    if (lane < 16) {
+      sm_m[wid * 16 + lane] = m;
+      sm_l[wid * 16 + lane] = l;
+    }
+    {
+      const int g = lane >> 4;
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sm_o[(wid * D_ + 16 * mt + 4 * g + i) * 16 + col] = o[mt][i];
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < G * (D_ / 4); idx += blockDim.x) {
+      const int cc = idx / (D_ / 4);
+      const int d0 = (idx % (D_ / 4)) * 4;
+      float M = -INFINITY;
+      for (int w = 0; w < nw; ++w) M = fmaxf(M, sm_m[w * 16 + cc]);
+      float L = 0.f, acc[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int w = 0; w < nw; ++w) {
+        const float mw = sm_m[w * 16 + cc];
+        const float f = (mw == -INFINITY) ? 0.f : exp2f(mw - M);
+        L += sm_l[w * 16 + cc] * f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] += sm_o[(w * D_ + d0 + j) * 16 + cc] * f;
+      }
+      const float inv = L > 0.f ? 1.f / L : 0.f;
+      const int hq = h * G + cc;
+      if (nparts == 1) {
+        bf16_t* op = a.out + (size_t)qtok * a.out_stride + (size_t)hq * D_ + d0;
+        uint2 pk;
+        pk.x = pack_bf2(acc[0] * inv, acc[1] * inv);
+        pk.y = pack_bf2(acc[2] * inv, acc[3] * inv);
+        *reinterpret_cast<uint2*>(op) = pk;
+      } else {
+        float* po = a.part_o + (((size_t)s * a.Hq + hq) * a.num_parts + part) * D_ + d0;
+        *reinterpret_cast<float4*>(po) = make_float4(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
+        if (d0 == 0) {
+          float* pm = a.part_ml + (((size_t)s * a.Hq + hq) * a.num_parts + part) * 2;
+          pm[0] = M;
+          pm[1] = L;
+        }
+      }
+    }
+  }
+  if (!ticketed) return;
+
+  // ---- partitions of (s, h): the last-arriving block merges them (in-launch) ----
+  int* flag = reinterpret_cast<int*>(smem + attn_flag_off(nw));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t* t = a.tickets + (size_t)s * a.Hkv + h;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const uint32_t old = __hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (uint32_t)(nparts - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  for (int idx = threadIdx.x; idx < G * (D_ / 4); idx += blockDim.x) {
+    const int hq = h * G + idx / (D_ / 4);
+    const int d0 = (idx % (D_ / 4)) * 4;
+    const float* pm = a.part_ml + ((size_t)s * a.Hq + hq) * a.num_parts * 2;
+    const float* po = a.part_o + ((size_t)s * a.Hq + hq) * a.num_parts * D_ + d0;
+    float M = -INFINITY;
+    for (int p = 0; p < nparts; ++p) M = fmaxf(M, pm[2 * p]);
+    float L = 0.f, acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < nparts; ++p) {
+      const float w = pm[2 * p + 1] * exp2f(pm[2 * p] - M);
+      const float4 v = *reinterpret_cast<const float4*>(po + (size_t)p * D_);
+      L += w;
+      acc[0] += w * v.x; acc[1] += w * v.y; acc[2] += w * v.z; acc[3] += w * v.w;
+    }
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+    bf16_t* op = a.out + (size_t)qtok * a.out_stride + (size_t)hq * D_ + d0;
+    uint2 pk;
+    pk.x = pack_bf2(acc[0] * inv, acc[1] * inv);
+    pk.y = pack_bf2(acc[2] * inv, acc[3] * inv);
+    *reinterpret_cast<uint2*>(op) = pk;
   }
 }
 
@@ -355,13 +444,7 @@ static int attn_waves(const AttnArgs& a) {
   return G > 4 ? G : 4;
 }
 
-static size_t attn_lds(int nw) {
-  const size_t vimg = (size_t)nw * CHUNK * D_ * 2;          // decode: one V image per wave
-  const size_t merge = (size_t)(2 * 16 * nw + nw * D_ * 16) * 4;  // decode merge scratch
-  const size_t pre = 2 * CHUNK * D_ * 2;                     // prefill double buffer
-  size_t m = vimg > merge ? vimg : merge;
-  return m > pre ? m : pre;
-}
+static size_t attn_lds(int nw) { return attn_flag_off(nw) + 16; }
 
 void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
   const int tiles = a.num_tiles > 0 ? a.num_tiles : 0;
@@ -370,7 +453,7 @@ void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
   const int nw = attn_waves(a);
   const int nz = dec_seqs > 0 ? a.num_parts : 1;
   hipLaunchKernelGGL(attn_kernel, dim3(nx, a.Hkv, nz), dim3(64 * nw), attn_lds(nw), st, a, dec_seqs);
-  if (dec_seqs > 0 && a.num_parts > 1)
+  if (dec_seqs > 0 && a.num_parts > 1 && a.tickets == nullptr)
     hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(dec_seqs, a.Hq), dim3(128), 0, st, a);
 }
 

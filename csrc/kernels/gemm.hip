@@ -48,7 +48,7 @@ enum GemmEpi : int { EPI_BF16 = 0, EPI_F32 = 1, EPI_SILU = 2, EPI_QKV = 3 };
 struct GemmParams {
   const bf16_t* x; int lda; int M; const int32_t* row_idx;
   const uint4* wp; int N; int K;
-  const bf16_t* norm_w; float eps;
+  const bf16_t* norm_w; float eps;  // norm_w null under NORM = gamma folded into W (row scale only)
   const bf16_t* bias; const bf16_t* res; int ldr;
   void* out; int ldo;
   int splitk; float* slabs; uint32_t* counters;
@@ -69,18 +69,25 @@ template <int MB>
 __host__ __device__ constexpr int ssq_bytes(int nw) { return nw * MB * 16 * 4; }
 
 // NORM: one A fragment (8 elements of row m at column k0): accumulate x^2 for the
-// deferred row scale and return bf16(x * w) for the MFMA.
+// deferred row scale and return bf16(x * w) for the MFMA. With gamma folded into the
+// packed weight at load time (w == null) the fragment passes through unchanged and no
+// gamma bytes are fetched (they would double the per-k-step vector-memory requests).
+template <int MODE>  // 1: gamma in registers, 2: gamma folded into W (row scale only)
 __device__ __forceinline__ uint4 norm_frag(uint4 a, const bf16_t* w, int k0, float& ss) {
-  const uint4 wv = *reinterpret_cast<const uint4*>(w + k0);
-  float f[8], g[8];
+  float f[8];
   unpack8(a, f);
-  unpack8(wv, g);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    ss += f[j] * f[j];
-    f[j] *= g[j];
+  for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
+  if constexpr (MODE == 2) {
+    return a;
+  } else {
+    const uint4 wv = *reinterpret_cast<const uint4*>(w + k0);
+    float g[8];
+    unpack8(wv, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] *= g[j];
+    return pack8(f);
   }
-  return pack8(f);
 }
 
 // ---- epilogue for one (row m, 4 columns) group; v[j] are the NTB reduced tiles ----
@@ -181,7 +188,7 @@ __device__ __forceinline__ float row_scale(const GemmParams& p, const float* ssq
   return rsqrtf(ss / (float)p.K + p.eps);
 }
 
-template <int MB, int NTB, int EPI, bool NORM>
+template <int MB, int NTB, int EPI, int NORM>
 __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB][NTB], const float (&ssr)[MB],
                                             char* smem, int m_base, int nt0) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -287,8 +294,36 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
   }
 }
 
-template <int MB, int NTB, int U, int EPI, bool NORM>
-__global__ __launch_bounds__(1024) void gemm_kernel(GemmParams p) {
+// Rotate a 16-B fragment across lanes within each 16-lane DPP row: lane r <- lane (r + S) % 16.
+template <int S>
+__device__ __forceinline__ uint4 row_ror(uint4 v) {
+  if constexpr (S == 0) {
+    return v;
+  } else {
+    constexpr int ctrl = 0x120 + ((16 - S) & 15);  // DPP row_ror:n moves lane i - n -> lane i
+    uint4 r;
+    r.x = __builtin_amdgcn_mov_dpp((int)v.x, ctrl, 0xf, 0xf, false);
+    r.y = __builtin_amdgcn_mov_dpp((int)v.y, ctrl, 0xf, 0xf, false);
+    r.z = __builtin_amdgcn_mov_dpp((int)v.z, ctrl, 0xf, 0xf, false);
+    r.w = __builtin_amdgcn_mov_dpp((int)v.w, ctrl, 0xf, 0xf, false);
+    return r;
+  }
+}
+
+// PIPE (decode, MB == 1): ping-pong pipelined stream, <= 8 waves per block so each wave
+// may hold 256 VGPRs (two U-deep register groups in flight). Otherwise (prefill tiles):
+// one group at a time, up to 16 waves per block at 128 VGPRs.
+//
+// XP (activation packing, decode only): with M <= 16/XP real rows, ONE 16-B activation
+// load per lane covers XP k-steps (lane r of a 16-lane row loads row r % R of k-step
+// r / R, R = 16/XP) and the XP B-fragments are rebuilt with DPP row rotations. Every
+// vector-memory instruction a CU issues for activations is one it cannot issue for the
+// weight stream (measured: benchmarks/stream_probe.hip, +75% time at 96 blocks), so the
+// activation side must be as thin as the batch allows.
+template <int MB, int NTB, int U, int EPI, int NORM, bool PIPE, int XP>
+__global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
+  static_assert(XP == 1 || (MB == 1 && PIPE && U % XP == 0), "activation packing is a decode-kernel mode");
+  constexpr int R = 16 / XP;  // real rows per packed load
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int KT = p.K >> 5;
@@ -296,8 +331,13 @@ __global__ __launch_bounds__(1024) void gemm_kernel(GemmParams p) {
   const int m_base = blockIdx.y * 16 * MB;
   // this block's k-slice, then this wave's contiguous range inside it
   const int s0 = (KT * blockIdx.z) / p.splitk, s1 = (KT * (blockIdx.z + 1)) / p.splitk;
-  const int kbeg = s0 + ((s1 - s0) * wid) / nw;
-  const int kend = s0 + ((s1 - s0) * (wid + 1)) / nw;
+  int kbeg = s0 + ((s1 - s0) * wid) / nw;
+  int kend = s0 + ((s1 - s0) * (wid + 1)) / nw;
+  if constexpr (XP > 1) {  // waves take whole packs of XP k-steps (K % (32 * XP) == 0 on host)
+    const int np0 = s0 / XP, np1 = s1 / XP;
+    kbeg = XP * (np0 + ((np1 - np0) * wid) / nw);
+    kend = XP * (np0 + ((np1 - np0) * (wid + 1)) / nw);
+  }
   f32x4 acc[MB][NTB];
 #pragma unroll
   for (int a = 0; a < MB; ++a)
@@ -306,32 +346,58 @@ __global__ __launch_bounds__(1024) void gemm_kernel(GemmParams p) {
   const uint4* wbase[NTB];
 #pragma unroll
   for (int j = 0; j < NTB; ++j) wbase[j] = p.wp + ((size_t)(nt0 + j) * KT) * 64 + lane;
+  // Rows >= M (the 16-row MFMA tile is padded for decode batches < 16) are zero and never
+  // loaded. Under XP packing lane r loads row r % R at k-step offset r / R.
   const bf16_t* xrow[MB];
+  bool xok[MB];
   float ssr[MB];
+  const int r16 = lane & 15;
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
-    xrow[mb] = p.x + (size_t)row_of(p, m_base + mb * 16 + (lane & 15)) * p.lda + 8 * (lane >> 4);
+    const int m = m_base + mb * 16 + (XP > 1 ? r16 % R : r16);
+    xok[mb] = m < p.M;
+    xrow[mb] = p.x + (size_t)row_of(p, m) * p.lda + 8 * (lane >> 4) + (XP > 1 ? (r16 / R) * 32 : 0);
     ssr[mb] = 0.f;
   }
-  const bf16_t* nw_ptr = p.norm_w + 8 * (lane >> 4);
+  const bf16_t* nw_ptr = p.norm_w ? p.norm_w + 8 * (lane >> 4) : nullptr;
 
-  int kt = kbeg;
-  for (; kt + U <= kend; kt += U) {
-    uint4 b[U][NTB];
-    uint4 a[U][MB];
+  // Software-pipelined weight stream (ping-pong register groups of U k-steps): group
+  // g+1's weights AND activations are issued before group g is consumed, so the wait
+  // for g is a partial vmcnt that leaves g+1 in flight (issue order = wait order).
+  auto load_grp = [&](uint4 (&b)[U][NTB], uint4 (&a)[U][MB], int k0) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int j = 0; j < NTB; ++j) b[u][j] = ld_nt16(wbase[j] + (size_t)(kt + u) * 64);
+      for (int j = 0; j < NTB; ++j) b[u][j] = ld_nt16(wbase[j] + (size_t)(k0 + u) * 64);
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; u += XP)  // packed: slot u holds the raw load for k-steps u..u+XP-1
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb) a[u][mb] = *reinterpret_cast<const uint4*>(xrow[mb] + (kt + u) * 32);
+      for (int mb = 0; mb < MB; ++mb)
+        a[u][mb] = xok[mb] ? *reinterpret_cast<const uint4*>(xrow[mb] + (k0 + u) * 32) : make_uint4(0, 0, 0, 0);
+  };
+  auto unpack_grp = [&](uint4 (&a)[U][MB]) {
+    if constexpr (XP > 1) {
+      const bool lo = r16 < R;
+#pragma unroll
+      for (int u = 0; u < U; u += XP) {
+        const uint4 v = a[u][0];
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        a[u][0] = lo ? v : z;
+        a[u + 1][0] = lo ? row_ror<R>(v) : z;
+        if constexpr (XP == 4) {
+          a[u + 2][0] = lo ? row_ror<2 * R>(v) : z;
+          a[u + 3][0] = lo ? row_ror<3 * R>(v) : z;
+        }
+      }
+    }
+  };
+  auto mma_grp = [&](const uint4 (&b)[U][NTB], uint4 (&a)[U][MB], int k0) {
+    unpack_grp(a);
     if constexpr (NORM) {
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb) a[u][mb] = norm_frag(a[u][mb], nw_ptr, (kt + u) * 32, ssr[mb]);
+        for (int mb = 0; mb < MB; ++mb) a[u][mb] = norm_frag<NORM>(a[u][mb], nw_ptr, (k0 + u) * 32, ssr[mb]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -339,20 +405,62 @@ __global__ __launch_bounds__(1024) void gemm_kernel(GemmParams p) {
       for (int j = 0; j < NTB; ++j)
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(as_bf16x8(b[u][j]), as_bf16x8(a[u][mb]), acc[mb][j]);
+  };
+  int kt = kbeg;
+  const int ngrp = (kend - kbeg) / U;
+  if constexpr (!PIPE) {
+    for (int g = 0; g < ngrp; ++g, kt += U) {
+      uint4 b[U][NTB], a[U][MB];
+      load_grp(b, a, kt);
+      mma_grp(b, a, kt);
+    }
+  } else if (ngrp > 0) {
+    uint4 b0[U][NTB], a0[U][MB], b1[U][NTB], a1[U][MB];
+    load_grp(b0, a0, kt);
+    int g = 0;
+    for (; g + 2 <= ngrp; g += 2) {
+      load_grp(b1, a1, kt + U);
+      mma_grp(b0, a0, kt);
+      if (g + 2 < ngrp) load_grp(b0, a0, kt + 2 * U);
+      mma_grp(b1, a1, kt + U);
+      kt += 2 * U;
+    }
+    if (g < ngrp) {
+      mma_grp(b0, a0, kt);
+      kt += U;
+    }
   }
-  for (; kt < kend; ++kt) {
-    uint4 b[NTB], a[MB];
+  // tail: whole packs of XP k-steps
+  for (; kt < kend; kt += XP) {
+    uint4 b[XP][NTB], a[XP][MB];
 #pragma unroll
-    for (int j = 0; j < NTB; ++j) b[j] = ld_nt16(wbase[j] + (size_t)kt * 64);
+    for (int u = 0; u < XP; ++u)
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
-      a[mb] = *reinterpret_cast<const uint4*>(xrow[mb] + kt * 32);
-      if constexpr (NORM) a[mb] = norm_frag(a[mb], nw_ptr, kt * 32, ssr[mb]);
+      for (int j = 0; j < NTB; ++j) b[u][j] = ld_nt16(wbase[j] + (size_t)(kt + u) * 64);
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+      a[0][mb] = xok[mb] ? *reinterpret_cast<const uint4*>(xrow[mb] + kt * 32) : make_uint4(0, 0, 0, 0);
+    if constexpr (XP > 1) {
+      const bool lo = r16 < R;
+      const uint4 v = a[0][0], z = make_uint4(0, 0, 0, 0);
+      a[0][0] = lo ? v : z;
+      a[1][0] = lo ? row_ror<R>(v) : z;
+      if constexpr (XP == 4) {
+        a[2][0] = lo ? row_ror<2 * R>(v) : z;
+        a[3][0] = lo ? row_ror<3 * R>(v) : z;
+      }
     }
 #pragma unroll
-    for (int j = 0; j < NTB; ++j)
+    for (int u = 0; u < XP; ++u) {
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(as_bf16x8(b[j]), as_bf16x8(a[mb]), acc[mb][j]);
+      for (int mb = 0; mb < MB; ++mb) {
+        if constexpr (NORM) a[u][mb] = norm_frag<NORM>(a[u][mb], nw_ptr, (kt + u) * 32, ssr[mb]);
+      }
+#pragma unroll
+      for (int j = 0; j < NTB; ++j)
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(as_bf16x8(b[u][j]), as_bf16x8(a[u][mb]), acc[mb][j]);
+    }
   }
   gemm_finish<MB, NTB, EPI, NORM>(p, acc, ssr, smem, m_base, nt0);
 }
@@ -365,7 +473,7 @@ __device__ __forceinline__ bf16x8 dq8(uint32_t q, float s, float sz) {
   return r;
 }
 
-template <int MB, int NTB, int EPI, bool NORM>
+template <int MB, int NTB, int EPI, int NORM>
 __global__ __launch_bounds__(1024) void awq_gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -380,14 +488,19 @@ __global__ __launch_bounds__(1024) void awq_gemm_kernel(GemmParams p) {
   for (int a = 0; a < MB; ++a)
 #pragma unroll
     for (int b = 0; b < NTB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // Rows >= M (the 16-row MFMA tile is padded for decode batches < 16) are zero and never
+  // loaded: on a 96-block GEMM every activation byte is a weight byte the CU cannot stream.
   const bf16_t* xrow[MB];
+  bool xok[MB];
   float ssr[MB];
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
-    xrow[mb] = p.x + (size_t)row_of(p, m_base + mb * 16 + (lane & 15)) * p.lda + 8 * (lane >> 4);
+    const int m = m_base + mb * 16 + (lane & 15);
+    xok[mb] = m < p.M;
+    xrow[mb] = p.x + (size_t)row_of(p, m) * p.lda + 8 * (lane >> 4);
     ssr[mb] = 0.f;
   }
-  const bf16_t* nw_ptr = p.norm_w + 8 * (lane >> 4);
+  const bf16_t* nw_ptr = p.norm_w ? p.norm_w + 8 * (lane >> 4) : nullptr;
   for (int kq = qbeg; kq < qend; ++kq) {
     uint4 w[NTB];
 #pragma unroll
@@ -397,8 +510,8 @@ __global__ __launch_bounds__(1024) void awq_gemm_kernel(GemmParams p) {
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb) {
-        a[u][mb] = *reinterpret_cast<const uint4*>(xrow[mb] + (kq * 4 + u) * 32);
-        if constexpr (NORM) a[u][mb] = norm_frag(a[u][mb], nw_ptr, (kq * 4 + u) * 32, ssr[mb]);
+        a[u][mb] = xok[mb] ? *reinterpret_cast<const uint4*>(xrow[mb] + (kq * 4 + u) * 32) : make_uint4(0, 0, 0, 0);
+        if constexpr (NORM) a[u][mb] = norm_frag<NORM>(a[u][mb], nw_ptr, (kq * 4 + u) * 32, ssr[mb]);
       }
 #pragma unroll
     for (int j = 0; j < NTB; ++j) {
@@ -440,10 +553,11 @@ static Plan plan(int nblk, int mchunks, int ksteps, int MB, int NTB, int force_w
   while (w > 1 && w * MB * NTB > 64) w >>= 1;
   if (force_s > 0) s = force_s;
   if (force_w > 0) w = force_w;
+  if (MB == 1 && w > 8) w = 8;  // pipelined decode kernel: __launch_bounds__(512)
   return {w, s};
 }
 
-template <int MB, int NTB, int EPI, bool NORM, bool AWQ>
+template <int MB, int NTB, int EPI, int NORM, bool AWQ>
 static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
   const int ntiles = g.N / 16;
   const int nblk = ntiles / NTB;
@@ -459,11 +573,21 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
   dim3 grid(nblk, mchunks, pl.splitk), block(64 * pl.waves);
   if constexpr (AWQ)
     hipLaunchKernelGGL((awq_gemm_kernel<MB, NTB, EPI, NORM>), grid, block, lds, st, p);
-  else
-    hipLaunchKernelGGL((gemm_kernel<MB, NTB, 4, EPI, NORM>), grid, block, lds, st, p);
+  else if constexpr (MB == 1) {
+    constexpr int U = NTB == 1 ? 8 : 4;
+    const int KT = g.K / 32;
+    if (g.M <= 4 && KT % 4 == 0)
+      hipLaunchKernelGGL((gemm_kernel<MB, NTB, U, EPI, NORM, true, 4>), grid, block, lds, st, p);
+    else if (g.M <= 8 && KT % 2 == 0)
+      hipLaunchKernelGGL((gemm_kernel<MB, NTB, U, EPI, NORM, true, 2>), grid, block, lds, st, p);
+    else
+      hipLaunchKernelGGL((gemm_kernel<MB, NTB, U, EPI, NORM, true, 1>), grid, block, lds, st, p);
+  } else {
+    hipLaunchKernelGGL((gemm_kernel<MB, NTB, MB == 4 ? 2 : 4, EPI, NORM, false, 1>), grid, block, lds, st, p);
+  }
 }
 
-template <int NTB, int EPI, bool NORM, bool AWQ>
+template <int NTB, int EPI, int NORM, bool AWQ>
 static void launch_m(GemmParams p, const GemmArgs& g, hipStream_t st) {
   if (g.M <= 16) launch_one<1, NTB, EPI, NORM, AWQ>(p, g, st);
   else if (g.M <= 32) launch_one<2, NTB, EPI, NORM, AWQ>(p, g, st);
@@ -472,13 +596,14 @@ static void launch_m(GemmParams p, const GemmArgs& g, hipStream_t st) {
 
 template <bool AWQ>
 static void launch_dispatch(GemmParams p, const GemmArgs& g, hipStream_t st) {
-  const bool norm = g.norm_w != nullptr;
+  const int norm = g.norm_w != nullptr ? 1 : (g.rownorm ? 2 : 0);
   const int ntiles = g.N / 16;
   const bool pair = ntiles % 2 == 0 && ntiles >= 1024;
 #define VG_NORM(NTB_, EPI_)                                                     \
   do {                                                                          \
-    if (norm) launch_m<NTB_, EPI_, true, AWQ>(p, g, st);                        \
-    else launch_m<NTB_, EPI_, false, AWQ>(p, g, st);                            \
+    if (norm == 1) launch_m<NTB_, EPI_, 1, AWQ>(p, g, st);                      \
+    else if (norm == 2 && !AWQ) launch_m<NTB_, EPI_, 2, AWQ>(p, g, st);         \
+    else launch_m<NTB_, EPI_, 0, AWQ>(p, g, st);                                \
   } while (0)
   switch (g.epi) {
     case EPI_SILU: VG_NORM(2, EPI_SILU); break;

@@ -15,8 +15,9 @@ struct GemmArgs {
   const void* wp;     // fragment-packed weight (bf16 [N/16][K/32][64][8] or AWQ int4 [N/16][K/128][64][4])
   int N;
   int K;
-  const uint16_t* norm_w;  // optional fused RMSNorm prologue weight [K]
+  const uint16_t* norm_w;  // optional fused RMSNorm weight [K] (null + rownorm: gamma pre-folded into W)
   float eps;
+  int rownorm;             // 1: apply the RMSNorm row scale (gamma folded into the packed weight)
   const uint16_t* bias;  // [N] bf16 or null
   const uint16_t* res;   // residual [M, N] bf16 (stride ldr) or null; may alias out
   int ldr;
@@ -86,6 +87,10 @@ struct AttnArgs {
   const int32_t* tile_seq;
   const int32_t* tile_q0;
   int num_tiles;
+  // decode partitions merged in-launch by the last-arriving partition block of each
+  // (sequence, KV head): zero-initialised, self-resetting [S * Hkv] tickets (null ->
+  // separate reduce launch)
+  uint32_t* tickets;
 };
 void launch_attn_decode(const AttnArgs& a, hipStream_t st);
 void launch_attn_prefill(const AttnArgs& a, hipStream_t st);
@@ -105,8 +110,12 @@ struct SampleArgs {
   const int64_t* offsets;    // [B] per-row philox offset (e.g. generated-token count)
   int32_t* out;              // [B]
   float* out_logprob;        // [B] or null
+  // segmented (multi-block per row) mode; null -> one block per row
+  float* parts;              // [B * nseg][8] partials (B * nseg <= 256)
+  uint32_t* sync;            // [2 * B] zero-initialised, self-resetting row counters
 };
 void launch_sample(const SampleArgs& s, hipStream_t st);
+int sample_segments(int B, int V);
 
 // Custom one-shot all-reduce over IPC-mapped peer buffers (xGMI).
 struct AllReduceArgs {

@@ -1,17 +1,27 @@
 // Per-row token sampling over the full vocabulary (V ~ 128k-152k) on gfx950:
 // temperature -> top-k -> top-p -> categorical, or argmax when temperature == 0.
 //
-// Exact top-k/top-p WITHOUT sorting or histogram atomics (rejection sampling):
-//   1. one pass: running max m and Z = sum exp((x - m)/T)
-//   2. draw token j by inverse CDF over {i : x_i > pivot} (thread-major order:
-//      any fixed order is a valid CDF order, so every load stays coalesced)
-//   3. one pass: c = #{x_i > x_j}, q = sum_{x_i > x_j} e_i
-//      accept j iff c < top_k and q < top_p * Z (j is inside both prefix sets);
-//      otherwise every token <= x_j is outside the nucleus too: pivot = x_j,
-//      the remaining mass is exactly q, repeat.
-// Accepted samples are distributed exactly as the renormalised filtered
-// distribution. Typical cost: 3-5 L2-resident passes over the row.
-// RNG: Philox4x32-10 keyed by the per-row seed, countered by (offset, round).
+// Parallel layout: each row is split into NSEG segments, one 256-thread block per
+// (segment, row), so a batch-8 step spreads its 8 x 600 KB of logits over 256 CUs
+// instead of 8. The blocks of a row meet at a per-row arrival counter after each
+// pass (agent-scope release -> ticket -> acquire; NSEG is chosen on the host so that
+// B * NSEG <= 256 blocks, all co-resident, and every spin has a give-up bound).
+// With NSEG == 1 (large batches) a row is one block and the "meeting" is a barrier.
+//
+// Exact sampling, no sort, no histogram atomics:
+//   pass 0: per segment (max, Z = sum e^{(x-max)/T}, argmax) and the Gumbel-max draw
+//           argmax_i (x_i / T + G_i) — an exact sample of the tempered distribution.
+//   Without top-k/top-p the Gumbel winner is the answer (one pass).
+//   With them, rejection on the pivot: candidate j is accepted iff
+//     #{x_i > x_j} < top_k  and  sum_{x_i > x_j} e_i < top_p * Z
+//   (j is inside both prefix sets). Every pass computes those two counts for the
+//   current candidate AND, speculatively, the next candidate = Gumbel-max restricted
+//   to {x_i > x_j} with fresh noise (if j is rejected, every token <= x_j is outside
+//   the nucleus too). So each rejection round costs one parallel pass; accepted
+//   samples are distributed exactly as the renormalised filtered distribution.
+// RNG: Philox4x32-10 keyed by the per-row seed, counter (float4 index, offset, round),
+// so results are reproducible for a given (seed, offset) and independent of NSEG.
+// Merges read the segments' partials in a fixed order: bit-reproducible.
 #include "common.h"
 #include "launchers.h"
 
@@ -28,8 +38,10 @@ __device__ __forceinline__ void philox_round(uint32_t (&c)[4], const uint32_t (&
   c[3] = lo0;
 }
 
-__device__ __forceinline__ float philox_uniform(uint64_t seed, uint64_t offset, uint32_t round) {
-  uint32_t c[4] = {(uint32_t)offset, (uint32_t)(offset >> 32), round, 0x9E3779B9u};
+// Four uniforms in (0, 1) for counter (i4, offset, round).
+__device__ __forceinline__ void philox4(uint64_t seed, uint64_t offset, uint32_t i4, uint32_t round,
+                                        float (&u)[4]) {
+  uint32_t c[4] = {i4, (uint32_t)offset, round, (uint32_t)(offset >> 32) ^ 0x9E3779B9u};
   uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
@@ -37,185 +49,241 @@ __device__ __forceinline__ float philox_uniform(uint64_t seed, uint64_t offset, 
     k[0] += 0x9E3779B9u;
     k[1] += 0xBB67AE85u;
   }
-  return (float)(c[0] >> 8) * (1.0f / 16777216.0f);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) u[j] = ((float)(c[j] >> 9) + 0.5f) * (1.0f / 8388608.0f);  // (0,1): 1-2^-24 max is exact
 }
 
-constexpr int SAMPLE_THREADS = 1024;
+constexpr int SAMPLE_THREADS = 256;
+constexpr int SAMPLE_MAX_BLOCKS = 256;  // B * NSEG bound (co-residency of a row's blocks)
 constexpr float LOG2E_S = 1.4426950408889634f;
 
-// Block-wide exclusive scan of one float per thread (1024 threads, 16 waves).
-__device__ __forceinline__ float block_excl_scan(float v, float* sw, float& total) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  float inc = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float t = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += t;
-  }
-  __syncthreads();
-  if (lane == 63) sw[wid] = inc;
-  __syncthreads();
-  float base = 0.f;
-  total = 0.f;
-  const int nw = blockDim.x >> 6;
-  for (int w = 0; w < nw; ++w) {
-    const float t = sw[w];
-    if (w < wid) base += t;
-    total += t;
-  }
-  return base + inc - v;
+// Per-(row, segment) partial, 8 words.
+struct SamplePart {
+  float mx, z;      // segment max and sum e^{(x - mx) c}
+  int amx;          // segment argmax (lowest index on ties)
+  float gk;         // best Gumbel key
+  int gi;           // its index (-1 = none)
+  float cnt, q;     // acceptance statistics for the current candidate
+  int pad;
+};
+
+struct Acc {  // POD (lives in LDS too); start from acc_init()
+  float mx, z;
+  int amx;
+  float gk;
+  int gi;
+  float cnt, q;
+};
+
+__device__ __forceinline__ Acc acc_init() { return Acc{-INFINITY, 0.f, 0x7fffffff, -INFINITY, -1, 0.f, 0.f}; }
+
+__device__ __forceinline__ void merge_mz(float& mx, float& z, int& amx, float om, float oz, int oi, float c) {
+  const float nm = fmaxf(mx, om);
+  const float zz = (mx == -INFINITY ? 0.f : z * exp2f((mx - nm) * c)) + (om == -INFINITY ? 0.f : oz * exp2f((om - nm) * c));
+  if (om > mx || (om == mx && oi < amx)) amx = oi;
+  mx = nm;
+  z = zz;
 }
 
-// Row sweep helper: every thread visits float4 vectors v = tid + k*nt (k ascending),
-// U vectors in flight per iteration (latency hiding: a 1024-thread block on one CU
-// needs many bytes in flight to stream a 600 KB row at L2/HBM rate).
-#define ROW_SWEEP(BODY)                                                        \
-  for (int v0 = tid; v0 < V4; v0 += nt * 8) {                                  \
-    float4 q_[8];                                                              \
-    /* clamped, unconditional loads: no per-element branch/vmcnt(0) (guide §5 trap c) */ \
-    _Pragma("unroll") for (int u_ = 0; u_ < 8; ++u_) {                         \
-      const int vi_ = v0 + u_ * nt;                                            \
-      q_[u_] = x4[vi_ < V4 ? vi_ : V4 - 1];                                    \
-    }                                                                          \
-    _Pragma("unroll") for (int u_ = 0; u_ < 8; ++u_) {                         \
-      const int vi_ = v0 + u_ * nt;                                            \
-      const bool ok_ = vi_ < V4;                                               \
-      const float e_[4] = {q_[u_].x, q_[u_].y, q_[u_].z, q_[u_].w};            \
-      _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) {                       \
-        const float v = ok_ ? e_[j_] : -INFINITY;                              \
-        const int i = 4 * vi_ + j_;                                            \
-        (void)i;                                                               \
-        BODY                                                                   \
-      }                                                                        \
-    }                                                                          \
+__device__ __forceinline__ void merge_g(float& gk, int& gi, float ok, int oi) {
+  if (oi >= 0 && (ok > gk || (ok == gk && (gi < 0 || oi < gi)))) {
+    gk = ok;
+    gi = oi;
   }
+}
 
-__global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
-  __shared__ float red[64];
-  __shared__ int ridx[16];
-  __shared__ float sw[16];
-  __shared__ int sel;
-  const int row = blockIdx.x;
-  const int V4 = a.V >> 2;  // host guarantees V % 4 == 0 and 16-B aligned rows
-  const float* x = a.logits + (size_t)row * a.ldl;
-  const float4* x4 = reinterpret_cast<const float4*>(x);
-  const int tid = threadIdx.x;
-  const int nt = blockDim.x;
-  const int lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
-  const float T = a.temperature ? a.temperature[row] : 0.f;
-  const bool greedy = !(T > 1e-5f);
-  const float c = greedy ? LOG2E_S : LOG2E_S / T;
-
-  // ---- pass 1: online (max, argmax, Z) in one sweep ----
-  float mx = -INFINITY, z = 0.f;
-  int amx = 0x7fffffff;
-  ROW_SWEEP({
-    if (v > mx) {
-      z = (mx == -INFINITY ? 0.f : z * exp2f((mx - v) * c)) + 1.f;
-      mx = v;
-      amx = i;
-    } else if (v > -INFINITY) {
-      z += exp2f((v - mx) * c);
-    }
-  })
+// Block-wide reduction of an Acc into LDS slot `out` (thread 0 holds the result).
+__device__ __forceinline__ void block_reduce_acc(Acc& a, float c, Acc* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();  // `red` may still be read by thread 0 from a previous reduction
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const float om = __shfl_xor(mx, o, 64);
-    const float oz = __shfl_xor(z, o, 64);
-    const int oi = __shfl_xor(amx, o, 64);
-    const float nm = fmaxf(mx, om);
-    const float zz = (mx == -INFINITY ? 0.f : z * exp2f((mx - nm) * c)) +
-                     (om == -INFINITY ? 0.f : oz * exp2f((om - nm) * c));
-    if (om > mx || (om == mx && oi < amx)) amx = oi;
-    mx = nm;
-    z = zz;
+    merge_mz(a.mx, a.z, a.amx, __shfl_xor(a.mx, o, 64), __shfl_xor(a.z, o, 64), __shfl_xor(a.amx, o, 64), c);
+    merge_g(a.gk, a.gi, __shfl_xor(a.gk, o, 64), __shfl_xor(a.gi, o, 64));
+    a.cnt += __shfl_xor(a.cnt, o, 64);
+    a.q += __shfl_xor(a.q, o, 64);
   }
-  if (lane == 0) { red[wid] = mx; red[16 + wid] = z; ridx[wid] = amx; }
+  if (lane == 0) red[wid] = a;
   __syncthreads();
-  if (tid == 0) {
-    float bm = red[0], bz = red[16];
-    int bi = ridx[0];
+  if (threadIdx.x == 0) {
+    Acc r = red[0];
     for (int w = 1; w < nw; ++w) {
-      const float om = red[w], oz = red[16 + w];
-      const float nm = fmaxf(bm, om);
-      bz = (bm == -INFINITY ? 0.f : bz * exp2f((bm - nm) * c)) + (om == -INFINITY ? 0.f : oz * exp2f((om - nm) * c));
-      if (om > bm || (om == bm && ridx[w] < bi)) bi = ridx[w];
-      bm = nm;
+      merge_mz(r.mx, r.z, r.amx, red[w].mx, red[w].z, red[w].amx, c);
+      merge_g(r.gk, r.gi, red[w].gk, red[w].gi);
+      r.cnt += red[w].cnt;
+      r.q += red[w].q;
     }
-    red[32] = bm;
-    red[33] = bz;
-    sel = bi;
+    a = r;
+  }
+}
+
+// Per-row meeting point of the NSEG blocks after pass `gen` (1-based).
+// Returns false if the wait gave up (caller falls back to the argmax).
+__device__ __forceinline__ bool row_meet(uint32_t* ctr, uint32_t target, int* ok_flag) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int ok = 1;
+    uint32_t spins = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 22)) { ok = 0; break; }  // ~seconds: never hang the GPU
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    *ok_flag = ok;
   }
   __syncthreads();
-  mx = red[32];
-  z = red[33];
-  amx = sel;
-  __syncthreads();
+  return *ok_flag != 0;
+}
 
-  int chosen = amx;
-  if (!greedy) {
-    const int topk = a.top_k ? a.top_k[row] : -1;
-    const float topp = a.top_p ? a.top_p[row] : 1.f;
-    const bool use_k = topk > 0 && topk < a.V;
-    const bool use_p = topp < 1.f;
-    const float pmass = topp * z;
-    const uint64_t seed = a.seeds ? a.seeds[row] : 0ull;
-    const uint64_t off = a.offsets ? (uint64_t)a.offsets[row] : 0ull;
-    float pivot = -INFINITY;
-    chosen = -1;
-    for (int round = 0; round < 64; ++round) {
-      const float u = philox_uniform(seed, off, (uint32_t)round);
-      float ls = 0.f;
-      ROW_SWEEP({ if (v > pivot) ls += exp2f((v - mx) * c); })
-      float total;
-      const float excl = block_excl_scan(ls, sw, total);
-      const float target = u * total;
-      if (tid == 0) sel = -1;
-      __syncthreads();
-      const bool own = (ls > 0.f) && (target >= excl) && (target < excl + ls || excl + ls >= total);
-      if (own) {
-        float run = excl;
-        int pick = -1, last = -1;
-        for (int vi = tid; vi < V4 && pick < 0; vi += nt) {
-          const float4 q = x4[vi];
-          const float e[4] = {q.x, q.y, q.z, q.w};
-          for (int j = 0; j < 4; ++j) {
-            if (e[j] > pivot) {
-              last = 4 * vi + j;
-              run += exp2f((e[j] - mx) * c);
-              if (run > target) { pick = 4 * vi + j; break; }
+__global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
+  __shared__ Acc red[SAMPLE_THREADS / 64];
+  __shared__ Acc merged;
+  __shared__ int ok_flag;
+  const int seg = blockIdx.x, nseg = gridDim.x;
+  const int row = blockIdx.y;
+  const int V4 = a.V >> 2;  // host guarantees V % 4 == 0 and 16-B aligned rows
+  const int v_lo = (int)(((long long)V4 * seg) / nseg), v_hi = (int)(((long long)V4 * (seg + 1)) / nseg);
+  const float* x = a.logits + (size_t)row * a.ldl;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const float T = a.temperature ? a.temperature[row] : 0.f;
+  const bool greedy = !(T > 1e-5f);
+  const float c = greedy ? LOG2E_S : LOG2E_S / T;  // log2-domain scale
+  const float cn = greedy ? 1.f : 1.f / T;         // natural-domain scale (Gumbel keys)
+  const uint64_t seed = a.seeds ? a.seeds[row] : 0ull;
+  const uint64_t off = a.offsets ? (uint64_t)a.offsets[row] : 0ull;
+  const int topk = a.top_k ? a.top_k[row] : -1;
+  const float topp = a.top_p ? a.top_p[row] : 1.f;
+  const bool use_k = topk > 0 && topk < a.V;
+  const bool use_p = topp < 1.f;
+  SamplePart* parts = reinterpret_cast<SamplePart*>(a.parts) + (size_t)row * nseg;
+  uint32_t* ctr = a.sync ? a.sync + row : nullptr;
+
+  // One sweep of this block's segment (8 float4 loads in flight per thread).
+  // mode 0: max/Z/argmax + Gumbel; mode 1: acceptance stats for xj + Gumbel restricted to x > xj.
+  auto sweep = [&](int mode, float xj, uint32_t round, Acc& acc) {
+    for (int v0 = v_lo + tid; v0 < v_hi; v0 += nt * 8) {
+      float4 q[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int vi = v0 + u * nt;
+        q[u] = x4[vi < v_hi ? vi : v_hi - 1];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int vi = v0 + u * nt;
+        if (vi >= v_hi) break;
+        const float e[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+        float uu[4] = {0.5f, 0.5f, 0.5f, 0.5f};
+        if (!greedy) philox4(seed, off, (uint32_t)vi, round, uu);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float v = e[j];
+          const int i = 4 * vi + j;
+          if (mode == 0) {
+            if (v > acc.mx) {
+              acc.z = (acc.mx == -INFINITY ? 0.f : acc.z * exp2f((acc.mx - v) * c)) + 1.f;
+              acc.mx = v;
+              acc.amx = i;
+            } else if (v > -INFINITY) {
+              acc.z += exp2f((v - acc.mx) * c);
             }
+          } else if (v > xj) {
+            acc.cnt += 1.f;
+            acc.q += exp2f((v - merged.mx) * c);
+          }
+          if (!greedy && (mode == 0 || v > xj) && v > -INFINITY) {
+            // accurate logs: a fast log rounding -log(u) to 0 near u = 1 would make an infinite key
+            const float g = v * cn - logf(fmaxf(-logf(uu[j]), 1e-30f));
+            if (g > acc.gk) { acc.gk = g; acc.gi = i; }
           }
         }
-        if (pick < 0) pick = last;
-        atomicMax(&sel, pick);
       }
-      __syncthreads();
-      const int j = sel;
-      __syncthreads();
-      if (j < 0) break;
-      if (!use_k && !use_p) { chosen = j; break; }
-      const float xj = x[j];
-      float cnt = 0.f, q = 0.f;
-      ROW_SWEEP({ if (v > xj) { cnt += 1.f; q += exp2f((v - mx) * c); } })
-      cnt = block_reduce_sum(cnt, red);
-      q = block_reduce_sum(q, red);
-      const bool ok_k = !use_k || cnt < (float)topk;
-      const bool ok_p = !use_p || q < pmass;
-      if (ok_k && ok_p) { chosen = j; break; }
-      pivot = xj;
     }
-    if (chosen < 0) chosen = amx;
+  };
+
+  // publish this block's partial and merge all segments of the row (fixed order)
+  auto exchange = [&](Acc& acc, uint32_t gen) -> bool {
+    block_reduce_acc(acc, c, red);
+    bool ok = true;
+    if (nseg > 1) {
+      if (tid == 0) {
+        SamplePart p{acc.mx, acc.z, acc.amx, acc.gk, acc.gi, acc.cnt, acc.q, 0};
+        parts[seg] = p;
+      }
+      ok = row_meet(ctr, gen * (uint32_t)nseg, &ok_flag);
+      if (ok) {  // all partials loaded at once (one per thread), then a fixed-shape tree
+        Acc r = acc_init();
+        if (tid < nseg) {
+          const SamplePart p = parts[tid];
+          r = Acc{p.mx, p.z, p.amx, p.gk, p.gi, p.cnt, p.q};
+        }
+        block_reduce_acc(r, c, red);
+        if (tid == 0) acc = r;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) merged = acc;
+    __syncthreads();
+    return ok;
+  };
+
+  Acc acc = acc_init();
+  sweep(0, 0.f, 0u, acc);
+  bool ok = exchange(acc, 1);
+  const float mx = merged.mx, z = merged.z;
+  int chosen = merged.amx;
+  uint32_t gen = 1;
+  if (ok && !greedy) {
+    int j = merged.gi;
+    if (use_k || use_p) {
+      const float pmass = topp * z;
+      for (uint32_t round = 1; round <= 64 && j >= 0; ++round) {
+        const float xj = x[j];
+        Acc st = acc_init();
+        sweep(1, xj, round, st);
+        ++gen;
+        ok = exchange(st, gen);
+        if (!ok) { j = -1; break; }
+        const bool ok_k = !use_k || merged.cnt < (float)topk;
+        const bool ok_p = !use_p || merged.q < pmass;
+        if (ok_k && ok_p) break;
+        j = merged.gi;  // next candidate, drawn from {x > x_j}
+      }
+    }
+    if (j >= 0) chosen = j;
   }
-  if (tid == 0) {
+  if (seg == 0 && tid == 0) {
     a.out[row] = chosen;
     if (a.out_logprob) a.out_logprob[row] = ((x[chosen] - mx) * c - log2f(z)) / LOG2E_S;
   }
+  // self-reset for the next launch: the last block of the row to leave zeroes the counters
+  if (nseg > 1 && tid == 0) {
+    uint32_t* done = a.sync + a.B;
+    const uint32_t d = __hip_atomic_fetch_add(done + row, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == (uint32_t)nseg - 1) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done + row, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+int sample_segments(int B, int V) {
+  const int V4 = V >> 2;
+  int nseg = SAMPLE_MAX_BLOCKS / (B > 0 ? B : 1);
+  if (nseg > SAMPLE_THREADS) nseg = SAMPLE_THREADS;  // the merge loads one partial per thread
+  const int cap = V4 / 1024;  // >= 4096 logits per segment
+  if (nseg > cap) nseg = cap;
+  return nseg < 1 ? 1 : nseg;
 }
 
 void launch_sample(const SampleArgs& s, hipStream_t st) {
   if (s.B <= 0) return;
-  hipLaunchKernelGGL(sample_kernel, dim3(s.B), dim3(SAMPLE_THREADS), 0, st, s);
+  int nseg = sample_segments(s.B, s.V);
+  if (s.parts == nullptr || s.sync == nullptr) nseg = 1;
+  hipLaunchKernelGGL(sample_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, s);
 }
 
 }  // namespace vgate

@@ -50,7 +50,8 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
           const c10::optional<Tensor>& positions, const c10::optional<Tensor>& slots,
           const c10::optional<Tensor>& cos_sin, const c10::optional<Tensor>& k_cache,
           const c10::optional<Tensor>& v_cache, int64_t hq, int64_t hkv,
-          const c10::optional<Tensor>& awq_scales, const c10::optional<Tensor>& awq_zeros, int64_t group) {
+          const c10::optional<Tensor>& awq_scales, const c10::optional<Tensor>& awq_zeros, int64_t group,
+          bool rownorm) {
   CHECK_DEV(x); CHECK_DEV(wp); CHECK_DEV(out);
   CHECK_DT(x, torch::kBFloat16);
   CHECK_LASTDIM(x); CHECK_LASTDIM(out);
@@ -87,7 +88,7 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
   vgate::GemmArgs g{};
   g.x = bf16p(x); g.lda = (int)x.stride(0); g.M = (int)M; g.row_idx = ridx;
   g.wp = wp.data_ptr(); g.N = (int)N; g.K = (int)K;
-  g.norm_w = opt_bf16(norm_w); g.eps = (float)eps;
+  g.norm_w = opt_bf16(norm_w); g.eps = (float)eps; g.rownorm = rownorm ? 1 : 0;
   if (g.norm_w) TORCH_CHECK(norm_w->numel() == K, "norm_w must have K elements");
   g.bias = opt_bf16(bias);
   g.res = opt_bf16(res);
@@ -236,7 +237,8 @@ void attn_prefill(const Tensor& q, int64_t q_stride, const Tensor& k_cache, cons
 void attention(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const Tensor& v_cache,
                const Tensor& block_tables, const Tensor& context_lens, const Tensor& query_start,
                const Tensor& tile_seq, const Tensor& tile_q0, Tensor& out, Tensor& part_o, Tensor& part_ml,
-               int64_t Hq, int64_t Hkv, int64_t part_size, double scale, int64_t out_stride) {
+               int64_t Hq, int64_t Hkv, int64_t part_size, double scale, int64_t out_stride,
+               const c10::optional<Tensor>& tickets) {
   auto a = attn_common(q, q_stride, k_cache, v_cache, block_tables, context_lens, out, Hq, Hkv, scale);
   if (out_stride > 0) a.out_stride = (int)out_stride;
   CHECK_DT(query_start, torch::kInt32); CHECK_DT(tile_seq, torch::kInt32); CHECK_DT(tile_q0, torch::kInt32);
@@ -254,6 +256,11 @@ void attention(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const T
   TORCH_CHECK(part_o.size(0) >= a.S && part_o.size(1) == Hq, "attention: part_o shape");
   a.part_o = reinterpret_cast<float*>(part_o.data_ptr());
   a.part_ml = reinterpret_cast<float*>(part_ml.data_ptr());
+  if (tickets.has_value() && tickets->defined()) {
+    CHECK_DEV(*tickets); CHECK_DT(*tickets, torch::kInt32);
+    TORCH_CHECK(tickets->numel() >= (int64_t)a.S * Hkv, "attention: tickets need S*Hkv zeroed int32");
+    a.tickets = reinterpret_cast<uint32_t*>(tickets->data_ptr());
+  }
   c10::DeviceGuard guard(q.device());
   vgate::launch_attention(a, a.S, cur_stream());
 }
@@ -261,7 +268,7 @@ void attention(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const T
 void sample(const Tensor& logits, const c10::optional<Tensor>& temperature,
             const c10::optional<Tensor>& top_p, const c10::optional<Tensor>& top_k,
             const c10::optional<Tensor>& seeds, const c10::optional<Tensor>& offsets, Tensor& out,
-            const c10::optional<Tensor>& out_logprob) {
+            const c10::optional<Tensor>& out_logprob, const c10::optional<Tensor>& ws) {
   CHECK_DEV(logits); CHECK_DEV(out);
   CHECK_DT(logits, torch::kFloat32); CHECK_DT(out, torch::kInt32);
   CHECK_LASTDIM(logits);
@@ -285,6 +292,14 @@ void sample(const Tensor& logits, const c10::optional<Tensor>& temperature,
   s.offsets = static_cast<const int64_t*>(fp(offsets, torch::kInt64));
   s.out = reinterpret_cast<int32_t*>(out.data_ptr());
   s.out_logprob = const_cast<float*>(static_cast<const float*>(fp(out_logprob, torch::kFloat32)));
+  if (ws.has_value() && ws->defined()) {
+    // [0, 512): row counters (2 per row, B <= 256 in segmented mode); [512, 2560): partials
+    TORCH_CHECK(ws->scalar_type() == torch::kInt32 && ws->is_cuda() && ws->numel() >= 2560, "sample: ws must be int32[>=2560]");
+    if (vgate::sample_segments(s.B, s.V) > 1) {
+      s.sync = reinterpret_cast<uint32_t*>(ws->data_ptr());
+      s.parts = reinterpret_cast<float*>(ws->data_ptr()) + 512;
+    }
+  }
   c10::DeviceGuard guard(logits.device());
   vgate::launch_sample(s, cur_stream());
 }
@@ -301,14 +316,21 @@ PYBIND11_MODULE(_C, m) {
         py::arg("waves") = 0, py::arg("splitk") = 0, py::arg("positions") = py::none(),
         py::arg("slots") = py::none(), py::arg("cos_sin") = py::none(), py::arg("k_cache") = py::none(),
         py::arg("v_cache") = py::none(), py::arg("hq") = 0, py::arg("hkv") = 0,
-        py::arg("awq_scales") = py::none(), py::arg("awq_zeros") = py::none(), py::arg("group") = 128);
-  m.def("attention", &attention, "unified paged attention: decode (split-K) + varlen prefill tiles, one launch");
+        py::arg("awq_scales") = py::none(), py::arg("awq_zeros") = py::none(), py::arg("group") = 128,
+        py::arg("rownorm") = false);
+  m.def("attention", &attention, "unified paged attention: decode (partitions merged in-launch) + varlen prefill tiles",
+        py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
+        py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),
+        py::arg("part_o"), py::arg("part_ml"), py::arg("Hq"), py::arg("Hkv"), py::arg("part_size"), py::arg("scale"),
+        py::arg("out_stride") = 0, py::arg("tickets") = py::none());
+  m.def("embedding", &embedding, "vocab-sharded embedding gather", py::arg("ids"), py::arg("table"), py::arg("out"),
+        py::arg("vstart") = 0);
   m.def("rmsnorm", &rmsnorm, "RMSNorm with optional fused residual add");
-  m.def("embedding", &embedding, "vocab-sharded embedding gather (+row sum of squares)", py::arg("ids"),
-        py::arg("table"), py::arg("out"), py::arg("vstart") = 0);
   m.def("rope_kv", &rope_kv, "NeoX RoPE + paged KV-cache write");
   m.def("attn_decode", &attn_decode, "paged split-K decode attention");
   m.def("attn_prefill", &attn_prefill, "paged varlen causal prefill attention");
-  m.def("sample", &sample, "temperature/top-k/top-p sampling");
+  m.def("sample", &sample, "temperature/top-k/top-p sampling (segmented Gumbel-max + exact rejection)",
+        py::arg("logits"), py::arg("temperature"), py::arg("top_p"), py::arg("top_k"), py::arg("seeds"),
+        py::arg("offsets"), py::arg("out"), py::arg("out_logprob") = py::none(), py::arg("ws") = py::none());
   vgate::bind_runtime(m);
 }

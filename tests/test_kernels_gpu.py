@@ -232,6 +232,45 @@ def test_sample_distribution_topk_topp():
     assert int(out.max()) < V and int(out.min()) >= 0
 
 
+def test_sample_segmented_matches_single_block_and_distribution():
+    """Small batches split each row over many blocks (per-row meeting counters); the
+    Gumbel noise is indexed by token, so the draw is identical to one block per row."""
+    torch.manual_seed(21)
+    V = 151936
+    base = torch.full((V,), -30.0, device=DEV)
+    hot = torch.tensor([5, 77_000, 151_935, 40_000, 123_456], device=DEV)
+    base[hot] = torch.tensor([2.0, 1.6, 1.2, 0.8, 0.0], device=DEV)
+    B = 4
+    L = base.expand(B, V).contiguous()
+    seeds = torch.tensor([3, 5, 7, 11], device=DEV, dtype=torch.int64)
+    t = torch.full((B,), 1.0, device=DEV)
+    for kw in ({}, {"top_p": torch.full((B,), 0.8, device=DEV)}, {"top_k": torch.full((B,), 3, dtype=torch.int32, device=DEV)}):
+        counts = torch.zeros(V, dtype=torch.long)
+        for off in range(150):
+            offs = torch.full((B,), off, dtype=torch.int64, device=DEV)
+            seg = ops.sample(L, t, seeds=seeds, offsets=offs, **kw)
+            # the same rows inside a 300-row batch run one block per row
+            big = 300
+            Lb = base.expand(big, V).contiguous()
+            kwb = {k: v.repeat(big // B) for k, v in kw.items()}
+            one = ops.sample(Lb, t.repeat(big // B), seeds=seeds.repeat(big // B),
+                             offsets=offs.repeat(big // B), **kwb)[:B]
+            assert torch.equal(seg, one), (kw, off)
+            counts += torch.bincount(seg.long().cpu(), minlength=V)
+        n = counts.sum().item()
+        p = torch.softmax(base.cpu(), -1)
+        if "top_p" in kw:
+            allowed = hot[:3].cpu()   # .40 + .27 < .8 <= .40 + .27 + .18
+        elif "top_k" in kw:
+            allowed = hot[:3].cpu()
+        else:
+            allowed = hot.cpu()
+        assert counts[allowed].sum().item() == n
+        q = p[allowed] / p[allowed].sum()
+        emp = counts[allowed].double() / n
+        assert (emp - q.double()).abs().max().item() < 0.07, (kw, emp, q)
+
+
 def test_sample_logprob():
     torch.manual_seed(9)
     logits = torch.randn(4, 5000, device=DEV)
@@ -339,13 +378,13 @@ def test_unified_attention_mixed_batch(Hq, Hkv):
     ts = torch.tensor(ts + [-1, -1], dtype=torch.int32, device=DEV)  # + padding tiles
     tq = torch.tensor(tq + [0, 0], dtype=torch.int32, device=DEV)
     scale = 1 / math.sqrt(D)
-    for part in (512, 2048):
+    r = ref.attention_ref(q.view(T, Hq, D), kc, vc, bt, cl, qs.cpu(), Hq, Hkv, scale)
+    for part in (256, 512, 2048, 256):  # repeated: in-launch partition tickets must self-reset
         P = (maxb * BS + part - 1) // part
         po = torch.empty(S, Hq, P, D, device=DEV)
         pml = torch.empty(S, Hq, P, 2, device=DEV)
         out = torch.zeros(T, Hq * D, device=DEV).bfloat16()
         ops.attention(q, Hq * D, kc, vc, bt, cl, qs, ts, tq, out, po, pml, Hq, Hkv, part, scale)
-        r = ref.attention_ref(q.view(T, Hq, D), kc, vc, bt, cl, qs.cpu(), Hq, Hkv, scale)
         assert _rel_err(out.view(T, Hq, D), r) < 2e-2
 
 
@@ -366,3 +405,53 @@ def test_deferred_norm_all_wave_counts(T, waves):
     r = ref.linear_ref(xn, w.cpu())
     assert _rel_err(y.float().cpu(), r.float()) < 1e-2
     assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("T", [3, 8, 40])
+def test_gemm_folded_norm(T):
+    """RMSNorm gamma folded into the packed weight (row scale only in the kernel) == gamma path."""
+    torch.manual_seed(30 + T)
+    H, N = 1536, 4096
+    x = (torch.randn(T, H, device=DEV) * 2).bfloat16()
+    g = (torch.rand(H, device=DEV) + 0.5).bfloat16()
+    w = (torch.randn(N, H, device=DEV) / math.sqrt(H)).bfloat16()
+    xn, _ = ref.rmsnorm_ref(x.cpu(), g.cpu(), 1e-6)
+    r = ref.linear_ref(xn, w.cpu())
+    plain = ops.Linear(w)
+    folded = ops.Linear(w)
+    assert folded.fold_norm(g)
+    y1 = ops.linear(x, plain, norm=(g, 1e-6))
+    y2 = ops.linear(x, folded, norm=(g, 1e-6))
+    assert _rel_err(y1.float().cpu(), r.float()) < 1e-2
+    assert _rel_err(y2.float().cpu(), r.float()) < 1e-2
+    # silu layout too (the fold is along K, the row permutation along N)
+    wg = torch.cat([w[:1024], w[1024:2048]])
+    f2 = ops.Linear(wg, kind="silu")
+    f2.fold_norm(g)
+    y3 = ops.linear(x, f2, norm=(g, 1e-6))
+    assert _rel_err(y3.float().cpu(), ref.silu_mul_linear_ref(xn, w[:1024].cpu(), w[1024:2048].cpu()).float()) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4, 5, 7, 8, 9, 16])
+def test_gemm_small_batch_activation_packing(M):
+    """Decode batches <= 4 / <= 8 pack 4 / 2 k-steps of activations per load (DPP unpack)."""
+    torch.manual_seed(40 + M)
+    K = 1536
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    g = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+    for N, kind in ((1536, "plain"), (1024, "silu")):
+        w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+        lin = ops.Linear(w, kind=kind) if kind == "silu" else ops.Linear(w)
+        wc = w.cpu()
+        r_res = torch.randn(M, N // (2 if kind == "silu" else 1), device=DEV).bfloat16()
+        for waves in (1, 4, 8):
+            for sk in ((1, 2) if kind == "plain" else (1,)):
+                if kind == "silu":
+                    y = ops.linear(x, lin, norm=(g, 1e-6), waves=waves)
+                    xn, _ = ref.rmsnorm_ref(x.cpu(), g.cpu(), 1e-6)
+                    r = ref.silu_mul_linear_ref(xn, wc[: N // 2], wc[N // 2:])
+                else:
+                    out = r_res.clone()
+                    y = ops.linear(x, lin, out=out, residual=out, waves=waves, splitk=sk)
+                    r = ref.linear_ref(x.cpu(), wc, None, r_res.cpu())
+                assert _rel_err(y.float().cpu(), r.float()) < 1e-2, (N, kind, waves, sk)

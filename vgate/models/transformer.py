@@ -21,6 +21,7 @@ with no extra kernel.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -89,9 +90,20 @@ class DecoderModel:
         else:
             from vgate.models.weights import random_init
             random_init(self, seed)
+        if self.device.type == "cuda" and os.environ.get("VGATE_FOLD_NORM", "1") != "0":
+            self.fold_norms()
         table_len = max(max_model_len, 16) + 1
         self.cos_sin = ops.ref.rope_cos_sin(table_len, arch.head_dim, arch.rope_theta, arch.rope_scaling,
                                             device=self.device)
+
+    def fold_norms(self) -> int:
+        """Fold every RMSNorm weight into the packed matrix of the GEMM that consumes it
+        (qkv <- input_layernorm, gate_up <- post_attention_layernorm, LM head <- final norm);
+        the fused GEMMs then apply only the deferred per-row scale. Dense bf16 only."""
+        n = 0
+        for L in self.layers:
+            n += L.qkv.fold_norm(L.in_norm) + L.gate_up.fold_norm(L.post_norm)
+        return n + self.lm_head.fold_norm(self.final_norm)
 
     # ------------------------------------------------------------------ sizes
     @property

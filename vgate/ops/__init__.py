@@ -127,6 +127,7 @@ class Linear:
             self.layout = "silu"
         self.kind = "awq" if awq is not None else "dense"
         self.bias = bias
+        self.norm_gamma = None  # RMSNorm weight folded into the packed copy (see fold_norm)
         if self.kind == "awq":
             q = awq["qint"]
             self.N, self.K = q.shape
@@ -156,6 +157,19 @@ class Linear:
             self.wp = None
             self.w = w
 
+    def fold_norm(self, gamma: torch.Tensor) -> bool:
+        """Fold the preceding RMSNorm's weight into the packed matrix: W'[n,k] = W[n,k]*g[k].
+
+        The fused GEMM then applies only the per-row scale rsqrt(mean(x^2)+eps) (deferred, in
+        the epilogue) and streams no gamma bytes. GPU bf16 weights only; returns whether folded.
+        """
+        if self.kind != "dense" or self.wp is None or self.norm_gamma is not None:
+            return False
+        g = gamma.to(self.wp.device, torch.float32).reshape(1, self.K // 32, 4, 1, 8)
+        self.wp.copy_((self.wp.float() * g).to(torch.bfloat16))
+        self.norm_gamma = gamma.detach().clone()
+        return True
+
     @property
     def out_features(self) -> int:
         return self.N // 2 if self.layout == "silu" else self.N
@@ -167,6 +181,8 @@ class Linear:
         if self.kind == "awq":
             raise NotImplementedError("AWQ weights are kept packed on the GPU")
         w = unpack_weight(self.wp, self.N, self.K)
+        if self.norm_gamma is not None:  # un-fold (approximate: W' was rounded to bf16)
+            w = (w.float() / self.norm_gamma.to(w.device, torch.float32)[None]).to(torch.bfloat16)
         perm = row_permutation(self.N, self.layout)
         if perm is not None:
             out = torch.empty_like(w)
@@ -231,7 +247,10 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
     epi = 3 if qkv is not None else (2 if silu else (1 if out_f32 else 0))
     kw = dict(bias=lin.bias, res=residual, ws=workspace(x.device), waves=waves, splitk=splitk)
     if norm is not None:
-        kw.update(norm_w=norm[0], eps=float(norm[1]))
+        if lin.norm_gamma is not None:  # gamma lives in the weights: row scale only
+            kw.update(rownorm=True, eps=float(norm[1]))
+        else:
+            kw.update(norm_w=norm[0], eps=float(norm[1]))
     if row_idx is not None:
         kw["row_idx"] = row_idx
     if qkv is not None:
@@ -244,11 +263,28 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
 
 
 def attention(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start, tile_seq, tile_q0, out,
-              part_o, part_ml, Hq: int, Hkv: int, part_size: int, scale: float):
-    """Unified paged attention for a mixed step (decode rows + prefill tiles, one launch)."""
+              part_o, part_ml, Hq: int, Hkv: int, part_size: int, scale: float, tickets=None):
+    """Unified paged attention for a mixed step (decode rows + prefill tiles, one launch).
+    Decode partitions of one (sequence, KV head) are merged in-launch by the last arriving
+    block (``tickets``: zeroed int32 [>= S*Hkv], defaults to a per-device buffer)."""
+    if tickets is None:
+        tickets = attn_tickets(q.device)
     native().attention(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start, tile_seq, tile_q0,
-                       out, part_o, part_ml, Hq, Hkv, part_size, scale, 0)
+                       out, part_o, part_ml, Hq, Hkv, part_size, scale, 0, tickets)
     return out
+
+
+_TICKETS: dict = {}
+
+
+def attn_tickets(device) -> torch.Tensor:
+    """Self-resetting decode-partition tickets (allocated once per device, before any capture)."""
+    key = str(device)
+    t = _TICKETS.get(key)
+    if t is None:
+        t = torch.zeros(1 << 16, dtype=torch.int32, device=device)
+        _TICKETS[key] = t
+    return t
 
 
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor | None = None,
@@ -337,8 +373,21 @@ def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, offsets
     if not _gpu(logits):
         out.copy_(ref.sample_ref(logits, temperature, top_p, top_k, generators))
         return out
-    native().sample(logits, temperature, top_p, top_k, seeds, offsets, out, out_logprob)
+    native().sample(logits, temperature, top_p, top_k, seeds, offsets, out, out_logprob, sample_workspace(logits.device))
     return out
+
+
+_SWS: dict = {}
+
+
+def sample_workspace(device) -> torch.Tensor:
+    """Zeroed row counters + partials of the segmented sampler (self-resetting, per device)."""
+    key = str(device)
+    ws = _SWS.get(key)
+    if ws is None:
+        ws = torch.zeros(4096, dtype=torch.int32, device=device)
+        _SWS[key] = ws
+    return ws
 
 
 def softmax_scale(head_dim: int) -> float:
