@@ -126,6 +126,22 @@ def attention_bench(S=8, ctx=64, Hq=12, Hkv=2, D=128, part=2048, max_len=2048):
     return {"attention_decode": {"S": S, "ctx": ctx, "part": part, "Hq": Hq, "Hkv": Hkv, "us": round(t, 2)}}
 
 
+def sampler_sweep(V=151936):
+    out = {}
+    for B in (1, 8, 32, 256):
+        logits = torch.randn(B, V, device="cuda") * 2
+        z = torch.zeros(B, device="cuda")
+        t = torch.full((B,), 0.7, device="cuda")
+        p = torch.full((B,), 0.9, device="cuda")
+        k = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+        sd = torch.arange(B, dtype=torch.int64, device="cuda")
+        of = torch.zeros(B, dtype=torch.int64, device="cuda")
+        o = torch.empty(B, dtype=torch.int32, device="cuda")
+        out[f"B{B}_greedy"] = round(graph_time(lambda: ops.sample(logits, z, p, k, sd, of, out=o)), 2)
+        out[f"B{B}_top_p"] = round(graph_time(lambda: ops.sample(logits, t, p, k, sd, of, out=o)), 2)
+    return {"sampler_sweep_us": out}
+
+
 def sampler_bench(B=8, V=151936):
     logits = torch.randn(B, V, device="cuda") * 2
     temp = torch.full((B,), 0.7, device="cuda")
@@ -153,6 +169,7 @@ def main():
         for part in (256, 512, 2048):
             print(json.dumps(attention_bench(ctx=ctx, part=part)), flush=True)
     print(json.dumps(sampler_bench()), flush=True)
+    print(json.dumps(sampler_sweep()), flush=True)
     sweep(a.M, a.quick)
 
 

@@ -222,15 +222,15 @@ __device__ __forceinline__ void decode_body(const AttnArgs& a, int s, int h, int
           *reinterpret_cast<uint2*>(op + 16 * mt + 4 * g) = pk;
         }
       } else {
+        // partials travel by device-coherent sc1 stores (read by another block in-launch)
         float* po = a.part_o + (((size_t)s * a.Hq + hq) * a.num_parts + part) * D_;
 #pragma unroll
         for (int mt = 0; mt < 8; ++mt)
-          *reinterpret_cast<float4*>(po + 16 * mt + 4 * g) =
-              make_float4(o[mt][0] * inv, o[mt][1] * inv, o[mt][2] * inv, o[mt][3] * inv);
+          st_sc1_f4(po + 16 * mt + 4 * g, o[mt][0] * inv, o[mt][1] * inv, o[mt][2] * inv, o[mt][3] * inv);
         if (g == 0) {
           float* pm = a.part_ml + (((size_t)s * a.Hq + hq) * a.num_parts + part) * 2;
-          pm[0] = m;
-          pm[1] = l;
+          st_sc1(pm, m);
+          st_sc1(pm + 1, l);
         }
       }
     }
@@ -275,11 +275,11 @@ __device__ __forceinline__ void decode_body(const AttnArgs& a, int s, int h, int
         *reinterpret_cast<uint2*>(op) = pk;
       } else {
         float* po = a.part_o + (((size_t)s * a.Hq + hq) * a.num_parts + part) * D_ + d0;
-        *reinterpret_cast<float4*>(po) = make_float4(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
+        st_sc1_f4(po, acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
         if (d0 == 0) {
           float* pm = a.part_ml + (((size_t)s * a.Hq + hq) * a.num_parts + part) * 2;
-          pm[0] = M;
-          pm[1] = L;
+          st_sc1(pm, M);
+          st_sc1(pm + 1, L);
         }
       }
     }
@@ -290,15 +290,11 @@ __device__ __forceinline__ void decode_body(const AttnArgs& a, int s, int h, int
   int* flag = reinterpret_cast<int*>(smem + attn_flag_off(nw));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0) {  // sc1 partials drained above: one ticket, no cache-wide fence
     uint32_t* t = a.tickets + (size_t)s * a.Hkv + h;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const uint32_t old = __hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old == (uint32_t)(nparts - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      __hip_atomic_store(t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (last) __hip_atomic_store(t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *flag = last;
   }
   __syncthreads();
@@ -309,13 +305,13 @@ __device__ __forceinline__ void decode_body(const AttnArgs& a, int s, int h, int
     const float* pm = a.part_ml + ((size_t)s * a.Hq + hq) * a.num_parts * 2;
     const float* po = a.part_o + ((size_t)s * a.Hq + hq) * a.num_parts * D_ + d0;
     float M = -INFINITY;
-    for (int p = 0; p < nparts; ++p) M = fmaxf(M, pm[2 * p]);
+    for (int p = 0; p < nparts; ++p) M = fmaxf(M, ld_sc1(pm + 2 * p));
     float L = 0.f, acc[4] = {0.f, 0.f, 0.f, 0.f};
     for (int p = 0; p < nparts; ++p) {
-      const float w = pm[2 * p + 1] * exp2f(pm[2 * p] - M);
-      const float4 v = *reinterpret_cast<const float4*>(po + (size_t)p * D_);
+      const float w = ld_sc1(pm + 2 * p + 1) * exp2f(ld_sc1(pm + 2 * p) - M);
+      const f32x4 v = ld_sc1_f4(po + (size_t)p * D_);
       L += w;
-      acc[0] += w * v.x; acc[1] += w * v.y; acc[2] += w * v.z; acc[3] += w * v.w;
+      acc[0] += w * v[0]; acc[1] += w * v[1]; acc[2] += w * v[2]; acc[3] += w * v[3];
     }
     const float inv = L > 0.f ? 1.f / L : 0.f;
     bf16_t* op = a.out + (size_t)qtok * a.out_stride + (size_t)hq * D_ + d0;

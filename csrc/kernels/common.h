@@ -107,4 +107,26 @@ __device__ __forceinline__ uint4 ld_nt16(const uint4* p) {
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
+// ---- in-launch cross-workgroup hand-off (cross-XCD safe, no cache-wide fences) ----
+// The per-XCD L2s are not coherent, and an agent-scope release/acquire fence compiles to
+// buffer_wbl2 / buffer_inv of the WHOLE L2 (write back every dirty line, drop every clean
+// one: the weights and activations the next kernels want). Instead, hand-off data travels
+// with device-coherent (sc1) stores and loads only: producer sc1 stores -> s_waitcnt
+// vmcnt(0) -> relaxed agent-scope atomic (ticket / counter); consumer observes the atomic
+// -> sc1 loads (MI355X_MICROARCH.md, inter-workgroup visibility).
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1_f4(float* p, float a, float b, float c, float d) {
+  st_sc1(p, a); st_sc1(p + 1, b); st_sc1(p + 2, c); st_sc1(p + 3, d);
+}
+__device__ __forceinline__ f32x4 ld_sc1_f4(const float* p) {
+  return f32x4{ld_sc1(p), ld_sc1(p + 1), ld_sc1(p + 2), ld_sc1(p + 3)};
+}
+// all of this thread's stores have reached the device-coherent level
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 }  // namespace vgate

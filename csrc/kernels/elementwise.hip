@@ -77,12 +77,17 @@ void launch_rmsnorm(const uint16_t* x, int ldx, uint16_t* res, int ldres, const 
     hipLaunchKernelGGL(rmsnorm_kernel<8>, grid, block, 0, st, x, ldx, res, ldres, w, y, ldy, H, eps);
 }
 
+// ids[t] < 0 refers to a token sampled by the PREVIOUS step that the host has not seen
+// yet (asynchronous scheduling): id = prev[-ids[t] - 1], read on the device.
 __global__ __launch_bounds__(256) void embedding_kernel(const int32_t* __restrict__ ids,
+                                                         const int32_t* __restrict__ prev,
                                                          const bf16_t* __restrict__ table,
                                                          bf16_t* __restrict__ out, int H,
                                                          int vstart, int vrows) {
   const int t = blockIdx.x;
-  const int id = ids[t] - vstart;
+  int tok = ids[t];
+  if (tok < 0 && prev != nullptr) tok = prev[-tok - 1];
+  const int id = tok - vstart;
   const bool ok = id >= 0 && id < vrows;
   const uint4* src = reinterpret_cast<const uint4*>(table + (size_t)(ok ? id : 0) * H);
   uint4* dst = reinterpret_cast<uint4*>(out + (size_t)t * H);
@@ -90,9 +95,9 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int32_t* __restric
 }
 
 void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int T, int H,
-                      int vstart, int vrows, hipStream_t st) {
+                      int vstart, int vrows, hipStream_t st, const int32_t* prev) {
   if (T <= 0) return;
-  hipLaunchKernelGGL(embedding_kernel, dim3(T), dim3(256), 0, st, ids, table, out, H, vstart, vrows);
+  hipLaunchKernelGGL(embedding_kernel, dim3(T), dim3(256), 0, st, ids, prev, table, out, H, vstart, vrows);
 }
 
 // One workgroup per token. Work items:

@@ -16,9 +16,9 @@
 // Decomposition: grid = (n-tile groups, m-chunks of 16*MB rows, SPLITK k-slices).
 // Inside a block, W waves split the block's k-slice into contiguous ranges and
 // their accumulators are reduced through LDS. With SPLITK > 1 every block writes
-// an fp32 partial slab and the LAST-ARRIVING block of the tile (agent-scope
-// release -> ticket atomic -> agent-scope acquire, §5 'In-launch split-K
-// reduction') sums the slabs and runs the epilogue — no second launch, and the
+// an fp32 partial slab and the LAST-ARRIVING block of the tile (sc1 slab stores ->
+// drain -> ticket atomic; sc1 slab loads: no L2-wide release/acquire fences, see
+// common.h) sums the slabs and runs the epilogue — no second launch, and the
 // small-N projections (o_proj / down_proj: 96 tiles) still fill all 256 CUs.
 //
 // Fusions:
@@ -232,27 +232,21 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
           for (int b = 0; b < NTB; ++b)
             if (a == mb && b == j) t = acc[a][b];
       }
-      slab[s] = t;
+      st_sc1_f4(reinterpret_cast<float*>(slab + s), t[0], t[1], t[2], t[3]);
     }
-    // 2) publish: every wave drains its stores, one agent-scope release, one ticket
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // 2) publish: every wave drains its sc1 stores, then one ticket (no cache-wide fence)
+    drain_stores();
     __syncthreads();
     if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const uint32_t old = __hip_atomic_fetch_add(p.counters + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = (old == (uint32_t)(p.splitk - 1));
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(p.counters + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      if (last) __hip_atomic_store(p.counters + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *flag = last;
     }
     __syncthreads();
     if (!*flag) return;
-    // 3) the last arriver sums every slice's slab (plain loads behind the acquire)
-    const f32x4* all = reinterpret_cast<const f32x4*>(p.slabs) + (size_t)tile * p.splitk * SLOTS;
+    // 3) the last arriver sums every slice's slab (device-coherent sc1 loads)
+    const float* all = p.slabs + (size_t)tile * p.splitk * SLOTS * 4;
     for (int s = threadIdx.x; s < MB * 64; s += blockDim.x) {
       const int mb = s >> 6, l = s & 63;
       const int m = m_base + mb * 16 + (l & 15);
@@ -260,7 +254,7 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
 #pragma unroll
       for (int j = 0; j < NTB; ++j) {
         f32x4 t = {0.f, 0.f, 0.f, 0.f};
-        for (int z = 0; z < p.splitk; ++z) t += all[(size_t)z * SLOTS + (mb * NTB + j) * 64 + l];
+        for (int z = 0; z < p.splitk; ++z) t += ld_sc1_f4(all + ((size_t)z * SLOTS + (mb * NTB + j) * 64 + l) * 4);
         v[j] = t;
       }
       if (m < p.M) epilogue<NTB, EPI>(p, v, m, nt0, 4 * (l >> 4));
@@ -309,6 +303,9 @@ __device__ __forceinline__ uint4 row_ror(uint4 v) {
     return r;
   }
 }
+
+// keep v on lanes where m == ~0u, zero elsewhere (component-wise: no struct select)
+__device__ __forceinline__ uint4 and_mask(uint4 v, uint32_t m) { return make_uint4(v.x & m, v.y & m, v.z & m, v.w & m); }
 
 // PIPE (decode, MB == 1): ping-pong pipelined stream, <= 8 waves per block so each wave
 // may hold 256 VGPRs (two U-deep register groups in flight). Otherwise (prefill tiles):
@@ -377,16 +374,18 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
   };
   auto unpack_grp = [&](uint4 (&a)[U][MB]) {
     if constexpr (XP > 1) {
-      const bool lo = r16 < R;
+      const uint32_t lom = r16 < R ? ~0u : 0u;
 #pragma unroll
       for (int u = 0; u < U; u += XP) {
+        // the DPP reads lanes r >= R: evaluate it with every lane active, select after
         const uint4 v = a[u][0];
-        const uint4 z = make_uint4(0, 0, 0, 0);
-        a[u][0] = lo ? v : z;
-        a[u + 1][0] = lo ? row_ror<R>(v) : z;
+        const uint4 v1 = row_ror<R>(v);
+        a[u][0] = and_mask(v, lom);
+        a[u + 1][0] = and_mask(v1, lom);
         if constexpr (XP == 4) {
-          a[u + 2][0] = lo ? row_ror<2 * R>(v) : z;
-          a[u + 3][0] = lo ? row_ror<3 * R>(v) : z;
+          const uint4 v2 = row_ror<2 * R>(v), v3 = row_ror<3 * R>(v);
+          a[u + 2][0] = and_mask(v2, lom);
+          a[u + 3][0] = and_mask(v3, lom);
         }
       }
     }
@@ -441,13 +440,15 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
     for (int mb = 0; mb < MB; ++mb)
       a[0][mb] = xok[mb] ? *reinterpret_cast<const uint4*>(xrow[mb] + kt * 32) : make_uint4(0, 0, 0, 0);
     if constexpr (XP > 1) {
-      const bool lo = r16 < R;
-      const uint4 v = a[0][0], z = make_uint4(0, 0, 0, 0);
-      a[0][0] = lo ? v : z;
-      a[1][0] = lo ? row_ror<R>(v) : z;
+      const uint32_t lom = r16 < R ? ~0u : 0u;
+      const uint4 v = a[0][0];
+      const uint4 v1 = row_ror<R>(v);
+      a[0][0] = and_mask(v, lom);
+      a[1][0] = and_mask(v1, lom);
       if constexpr (XP == 4) {
-        a[2][0] = lo ? row_ror<2 * R>(v) : z;
-        a[3][0] = lo ? row_ror<3 * R>(v) : z;
+        const uint4 v2 = row_ror<2 * R>(v), v3 = row_ror<3 * R>(v);
+        a[2][0] = and_mask(v2, lom);
+        a[3][0] = and_mask(v3, lom);
       }
     }
 #pragma unroll

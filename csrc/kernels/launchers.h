@@ -53,7 +53,7 @@ void launch_rmsnorm(const uint16_t* x, int ldx, uint16_t* res, int ldres, const 
 
 // Embedding gather with vocab-shard masking (TP): rows outside [vstart, vstart+vrows) -> 0.
 void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int T, int H,
-                      int vstart, int vrows, hipStream_t st);
+                      int vstart, int vrows, hipStream_t st, const int32_t* prev = nullptr);
 
 // NeoX RoPE on q,k inside the fused qkv buffer + paged KV-cache write.
 // qkv: [T, (Hq + 2*Hkv) * D]; cos_sin: [max_pos, D] f32 (cos | sin halves)

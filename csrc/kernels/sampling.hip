@@ -4,7 +4,7 @@
 // Parallel layout: each row is split into NSEG segments, one 256-thread block per
 // (segment, row), so a batch-8 step spreads its 8 x 600 KB of logits over 256 CUs
 // instead of 8. The blocks of a row meet at a per-row arrival counter after each
-// pass (agent-scope release -> ticket -> acquire; NSEG is chosen on the host so that
+// pass (sc1 partial stores -> drain -> counter; sc1 loads; NSEG is chosen on the host so that
 // B * NSEG <= 256 blocks, all co-resident, and every spin has a give-up bound).
 // With NSEG == 1 (large batches) a row is one block and the "meeting" is a barrier.
 //
@@ -22,6 +22,8 @@
 // RNG: Philox4x32-10 keyed by the per-row seed, counter (float4 index, offset, round),
 // so results are reproducible for a given (seed, offset) and independent of NSEG.
 // Merges read the segments' partials in a fixed order: bit-reproducible.
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -120,9 +122,9 @@ __device__ __forceinline__ void block_reduce_acc(Acc& a, float c, Acc* red) {
 // Per-row meeting point of the NSEG blocks after pass `gen` (1-based).
 // Returns false if the wait gave up (caller falls back to the argmax).
 __device__ __forceinline__ bool row_meet(uint32_t* ctr, uint32_t target, int* ok_flag) {
+  drain_stores();  // this block's sc1 partial stores are device-visible before it arrives
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int ok = 1;
     uint32_t spins = 0;
@@ -130,7 +132,6 @@ __device__ __forceinline__ bool row_meet(uint32_t* ctr, uint32_t target, int* ok
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1u << 22)) { ok = 0; break; }  // ~seconds: never hang the GPU
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     *ok_flag = ok;
   }
   __syncthreads();
@@ -209,16 +210,19 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
     block_reduce_acc(acc, c, red);
     bool ok = true;
     if (nseg > 1) {
-      if (tid == 0) {
-        SamplePart p{acc.mx, acc.z, acc.amx, acc.gk, acc.gi, acc.cnt, acc.q, 0};
-        parts[seg] = p;
+      if (tid == 0) {  // device-coherent (sc1) stores: read by the row's other blocks in-launch
+        float* w = reinterpret_cast<float*>(parts + seg);
+        st_sc1(w + 0, acc.mx); st_sc1(w + 1, acc.z); st_sc1(w + 2, __int_as_float(acc.amx));
+        st_sc1(w + 3, acc.gk); st_sc1(w + 4, __int_as_float(acc.gi)); st_sc1(w + 5, acc.cnt);
+        st_sc1(w + 6, acc.q);
       }
       ok = row_meet(ctr, gen * (uint32_t)nseg, &ok_flag);
       if (ok) {  // all partials loaded at once (one per thread), then a fixed-shape tree
         Acc r = acc_init();
         if (tid < nseg) {
-          const SamplePart p = parts[tid];
-          r = Acc{p.mx, p.z, p.amx, p.gk, p.gi, p.cnt, p.q};
+          const float* w = reinterpret_cast<const float*>(parts + tid);
+          r = Acc{ld_sc1(w + 0), ld_sc1(w + 1), __float_as_int(ld_sc1(w + 2)), ld_sc1(w + 3),
+                  __float_as_int(ld_sc1(w + 4)), ld_sc1(w + 5), ld_sc1(w + 6)};
         }
         block_reduce_acc(r, c, red);
         if (tid == 0) acc = r;
@@ -262,7 +266,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
   // self-reset for the next launch: the last block of the row to leave zeroes the counters
   if (nseg > 1 && tid == 0) {
     uint32_t* done = a.sync + a.B;
-    const uint32_t d = __hip_atomic_fetch_add(done + row, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t d = __hip_atomic_fetch_add(done + row, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (d == (uint32_t)nseg - 1) {
       __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(done + row, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -272,7 +276,12 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
 
 int sample_segments(int B, int V) {
   const int V4 = V >> 2;
+  static const int force = [] {
+    const char* e = getenv("VGATE_SAMPLE_NSEG");  // experiments only (bounded below)
+    return e ? atoi(e) : 0;
+  }();
   int nseg = SAMPLE_MAX_BLOCKS / (B > 0 ? B : 1);
+  if (force > 0 && force < nseg) nseg = force;
   if (nseg > SAMPLE_THREADS) nseg = SAMPLE_THREADS;  // the merge loads one partial per thread
   const int cap = V4 / 1024;  // >= 4096 logits per segment
   if (nseg > cap) nseg = cap;

@@ -136,7 +136,8 @@ void rmsnorm(const Tensor& x, const c10::optional<Tensor>& res, const Tensor& w,
                         (int)y.stride(0), (int)M, (int)H, (float)eps, cur_stream());
 }
 
-void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart) {
+void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart,
+               const c10::optional<Tensor>& prev) {
   CHECK_DEV(ids); CHECK_DEV(table); CHECK_DEV(out);
   CHECK_DT(ids, torch::kInt32); CHECK_DT(table, torch::kBFloat16); CHECK_DT(out, torch::kBFloat16);
   TORCH_CHECK(table.is_contiguous() && out.is_contiguous(), "embedding: contiguous");
@@ -145,7 +146,7 @@ void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vsta
   c10::DeviceGuard guard(ids.device());
   vgate::launch_embedding(reinterpret_cast<const int32_t*>(ids.data_ptr()), bf16p(table),
                           bf16p_mut(out), (int)T, (int)H, (int)vstart, (int)table.size(0),
-                          cur_stream());
+                          cur_stream(), opt_ptr<const int32_t>(prev, torch::kInt32, "prev"));
 }
 
 void rope_kv(Tensor& qkv, const Tensor& positions, const c10::optional<Tensor>& slots,
@@ -323,8 +324,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),
         py::arg("part_o"), py::arg("part_ml"), py::arg("Hq"), py::arg("Hkv"), py::arg("part_size"), py::arg("scale"),
         py::arg("out_stride") = 0, py::arg("tickets") = py::none());
-  m.def("embedding", &embedding, "vocab-sharded embedding gather", py::arg("ids"), py::arg("table"), py::arg("out"),
-        py::arg("vstart") = 0);
+  m.def("embedding", &embedding, "vocab-sharded embedding gather (negative ids: previous step's samples)",
+        py::arg("ids"), py::arg("table"), py::arg("out"), py::arg("vstart") = 0, py::arg("prev") = py::none());
   m.def("rmsnorm", &rmsnorm, "RMSNorm with optional fused residual add");
   m.def("rope_kv", &rope_kv, "NeoX RoPE + paged KV-cache write");
   m.def("attn_decode", &attn_decode, "paged split-K decode attention");

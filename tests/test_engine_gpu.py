@@ -68,3 +68,27 @@ def test_qwen_1p5b_shapes_run():
     out = _run(eng, [(f"r{i}", list(range(10, 40 + i)), sp) for i in range(8)])
     assert all(len(s.output_ids) == 16 for s in out.values())
     assert all(0 <= t < 151936 for s in out.values() for t in s.output_ids)
+
+
+def test_async_scheduling_matches_sync():
+    """Asynchronous scheduling (step t+1 queued before step t is post-processed, pending
+    tokens resolved on the device) produces exactly the synchronous engine's tokens —
+    sampled (seeded), greedy with EOS-driven early stops, and max_tokens cut-offs."""
+    def run(async_sched):
+        eng = _engine(async_scheduling=async_sched)
+        assert eng.async_sched == async_sched
+        reqs = []
+        for i, (k, v) in enumerate(PROMPTS.items()):
+            if i % 3 == 0:
+                sp = SamplingParams(temperature=0.9, top_p=0.9, top_k=40, max_tokens=9 + i, ignore_eos=True)
+            elif i % 3 == 1:
+                sp = SamplingParams(temperature=0.0, max_tokens=14, ignore_eos=True)
+            else:  # stop on an id the greedy model emits early (taken from a first sync run)
+                sp = SamplingParams(temperature=0.7, max_tokens=20, stop_token_ids=[7, 11, 13, 200, 300])
+            reqs.append((k, v, sp))
+        out = _run(eng, reqs)
+        assert eng.kvm.num_free() == eng.num_blocks
+        return {k: (s.output_ids, s.finish_reason) for k, s in out.items()}
+
+    a, b = run(False), run(True)
+    assert a == b

@@ -138,7 +138,7 @@ class DecoderModel:
         dev = self.device
         # RMSNorms are folded into the consuming GEMMs (deferred row scale), so a layer is
         # qkv GEMM -> attention -> o GEMM (+residual) -> gate_up GEMM -> down GEMM (+residual).
-        resid = ops.embedding(sv.ids, self.embed, vstart=sh.vocab0)
+        resid = ops.embedding(sv.ids, self.embed, vstart=sh.vocab0, prev=sv.prev_tokens)
         if tp.size > 1:
             tp.all_reduce(resid)
         q = torch.empty(T, sh.hq * D, dtype=torch.bfloat16, device=dev)

@@ -302,14 +302,18 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor
     return out
 
 
-def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None, vstart: int = 0):
-    """Row gather with vocab-shard masking (rows outside this TP rank's shard are zero)."""
+def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None, vstart: int = 0,
+              prev: torch.Tensor | None = None):
+    """Row gather with vocab-shard masking (rows outside this TP rank's shard are zero).
+    ids < 0 name a token the previous step sampled on the device: id = prev[-id - 1]."""
     if out is None:
         out = torch.empty(ids.numel(), table.shape[1], dtype=table.dtype, device=table.device)
     if not _gpu(table):
+        if prev is not None and bool((ids < 0).any()):
+            ids = torch.where(ids < 0, prev.to(ids.device)[(-ids - 1).clamp(min=0).long()], ids)
         out.copy_(ref.embedding_ref(ids, table, vstart))
         return out
-    native().embedding(ids, table, out, vstart)
+    native().embedding(ids, table, out, vstart, prev)
     return out
 
 

@@ -30,7 +30,7 @@ from vgate.runtime.kv_cache import BLOCK_SIZE, KVCacheManager, allocate_kv_tenso
 from vgate.runtime.model_runner import ModelRunner
 from vgate.runtime.sampling_params import SamplingParams
 from vgate.runtime.scheduler import Scheduler
-from vgate.runtime.sequence import Sequence, SeqStatus
+from vgate.runtime.sequence import PENDING, Sequence, SeqStatus
 from vgate.runtime.tokenizer import IncrementalDecoder, load_tokenizer
 
 log = logging.getLogger("vgate.engine")
@@ -54,7 +54,8 @@ class EngineConfig:
     enable_prefix_caching: bool = True
     seed: int = 0
     block_size: int = BLOCK_SIZE
-    part_size: int = 0  # 0 = auto: one decode partition up to 2048 tokens, 512-token split-K beyond
+    part_size: int = 0  # 0 = auto: 256-token decode partitions (merged in-launch)
+    async_scheduling: bool = True  # GPU, TP=1: queue step t+1 before post-processing step t
     graph_token_buckets: list[int] | None = None
     warmup: bool = True
     arch_overrides: dict | None = None
@@ -107,7 +108,7 @@ class LLMEngine:
                                              self.arch.head_dim, self.device, block_size=cfg.block_size)
         self.kvm = KVCacheManager(self.num_blocks, cfg.block_size, cfg.enable_prefix_caching)
         self.scheduler = Scheduler(self.kvm, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len)
-        part = cfg.part_size or (cfg.max_model_len if cfg.max_model_len <= 2048 else 512)
+        part = cfg.part_size or 256
         part = max(32, (part + 31) // 32 * 32)
         self.runner = ModelRunner(self.model, self.kv_caches, cfg.max_num_seqs, cfg.max_num_batched_tokens,
                                   cfg.max_model_len, cfg.block_size, cfg.enforce_eager, part,
@@ -122,6 +123,8 @@ class LLMEngine:
         self._by_id: dict[str, Sequence] = {}
         self._seq_counter = 0
         self.healthy = True
+        self.async_sched = bool(cfg.async_scheduling and self.device.type == "cuda" and self.tp.size == 1)
+        self._inflight = None  # (batch, handle) of the launched, not yet post-processed step
         self.last_error: str | None = None
         self.last_step_wall = time.monotonic()
         log.info("engine ready: model=%s params=%.2fB weights=%.2f GB load=%.1fs kv_blocks=%d (%.1fk tokens) device=%s tp=%d",
@@ -198,7 +201,7 @@ class LLMEngine:
             self._cv.notify()
 
     def has_unfinished(self) -> bool:
-        return bool(self._inbox) or self.scheduler.has_work()
+        return bool(self._inbox) or self.scheduler.has_work() or self._inflight is not None
 
     # -------------------------------------------------------------------- loop
     def _drain_inbox(self) -> None:
@@ -220,7 +223,8 @@ class LLMEngine:
             torch.cuda.set_device(self.device)
         while self._running:
             with self._cv:
-                while self._running and not self._inbox and not self._aborts and not self.scheduler.has_work():
+                while (self._running and not self._inbox and not self._aborts and not self.scheduler.has_work()
+                       and self._inflight is None):
                     self._cv.wait(timeout=0.5)
                 if not self._running:
                     break
@@ -229,6 +233,7 @@ class LLMEngine:
                 self.step()
             except Exception as e:  # noqa: BLE001 - engine faults fail every in-flight request
                 log.exception("engine step failed")
+                self._inflight = None
                 self.healthy = False
                 self.last_error = f"{type(e).__name__}: {e}"
                 for seq in list(self.scheduler.running) + list(self.scheduler.waiting):
@@ -241,13 +246,21 @@ class LLMEngine:
         """Synchronous driver (tests / offline use): process everything queued."""
         self._drain_inbox()
         n = 0
-        while self.scheduler.has_work() and n < max_steps:
+        while (self.scheduler.has_work() or self._inflight is not None) and n < max_steps:
             self.step()
             self._drain_inbox()
             n += 1
+        if self.async_sched:
+            self._drain_inflight()
 
     # -------------------------------------------------------------------- step
     def step(self) -> int:
+        """One engine iteration. Synchronous mode: schedule -> execute -> post-process.
+        Asynchronous mode (GPU, TP=1): schedule -> launch step t+1 -> post-process step t
+        while t+1 runs (tokens of the in-flight step are PENDING placeholders that the
+        device resolves from the previous sampler output)."""
+        if self.async_sched:
+            return self._step_async()
         tc = time.perf_counter()
         batch = self.scheduler.schedule()
         if batch.empty:
@@ -257,10 +270,51 @@ class LLMEngine:
             toks, samples = self._execute_tp(batch)
         else:
             toks, samples = self.runner.execute(batch)
+        for seq, n in batch.items:
+            seq.num_computed += n
+        self._process(batch, toks, samples, t0, tc, resolve=False)
+        return len(batch.items)
+
+    def _step_async(self) -> int:
+        tc = time.perf_counter()
+        batch = self.scheduler.schedule(no_preempt=self._inflight is not None)
+        if batch.kv_pressure:  # preemption needs every placeholder resolved first
+            self._drain_inflight()
+            batch = self.scheduler.schedule()
+        if batch.empty:
+            self._drain_inflight()
+            return 0
+        pend = {seq.seq_id: seq.pending_slot for seq, _ in batch.items if seq.pending}
+        h = self.runner.launch(batch, pend)
+        for i, ((seq, n), smp) in enumerate(zip(batch.items, h.samples)):
+            seq.num_computed += n
+            if smp:
+                seq.output_ids.append(PENDING)
+                seq.pending.append(len(seq.output_ids) - 1)
+                seq.pending_slot = i
+        prev, self._inflight = self._inflight, (batch, h, tc)
+        if prev is not None:
+            self._complete(prev)
+        return len(batch.items)
+
+    def _drain_inflight(self) -> None:
+        if self._inflight is not None:
+            prev, self._inflight = self._inflight, None
+            self._complete(prev)
+
+    def _complete(self, entry) -> None:
+        batch, h, tc = entry
+        toks = self.runner.collect(h)
+        self._process(batch, toks, h.samples, h.t_launch, tc, resolve=True)
+
+    def _process(self, batch, toks, samples, t0: float, tc: float, resolve: bool) -> None:
+        """Post-process one executed step: append (or resolve) sampled tokens, stop checks,
+        streaming deltas, prefix-cache registration, finished requests."""
         now = time.perf_counter()
         st = self.stats
         st.steps += 1
         st.step_time_s += now - t0
+        st.cycle_time_s += now - tc
         st.last_step_ms = 1e3 * (now - t0)
         st.prefill_tokens += batch.num_prefill_tokens
         st.decode_tokens += batch.num_decode
@@ -268,17 +322,27 @@ class LLMEngine:
         self.last_step_wall = time.monotonic()
         eos = set(self.arch.eos_token_ids)
         for (seq, n), tok, smp in zip(batch.items, toks, samples):
-            seq.num_computed += n
-            self.kvm.register_computed(seq)
-            if not smp or seq.is_finished:
+            if not smp:
+                if not seq.is_finished:
+                    self.kvm.register_computed(seq)
                 continue
-            seq.output_ids.append(tok)
+            if resolve:
+                idx = seq.pending.popleft() if seq.pending else None
+                if seq.is_finished or idx is None:
+                    continue  # finished (stop / abort) while this step was in flight: dropped
+                seq.output_ids[idx] = tok
+                nout = idx + 1
+            else:
+                if seq.is_finished:
+                    continue
+                seq.output_ids.append(tok)
+                nout = len(seq.output_ids)
+            self.kvm.register_computed(seq)
             st.tokens_generated += 1
             if seq.first_token_time is None:
                 seq.first_token_time = now
             seq.last_token_time = now
             sp = seq.params
-            nout = len(seq.output_ids)
             reason = None
             if not sp.ignore_eos and tok in eos and nout >= sp.min_tokens:
                 reason = "stop"
@@ -286,24 +350,25 @@ class LLMEngine:
                 reason = "stop"
             elif nout >= sp.max_tokens:
                 reason = "length"
-            elif seq.total_len >= self.cfg.max_model_len:
+            elif len(seq.prompt_ids) + nout >= self.cfg.max_model_len:
                 reason = "length"
             delta = ""
             if seq.stream and seq.detok is not None:
                 delta = seq.detok.push(tok) if reason != "stop" or tok not in eos else ""
                 seq.text += delta
             if sp.stop and reason is None:
-                text = seq.text if seq.stream else self.tokenizer.decode(seq.output_ids)
-                for s in sp.stop:
-                    if s and s in text:
+                text = seq.text if seq.stream else self.tokenizer.decode(seq.output_ids[:nout])
+                for stop_s in sp.stop:
+                    if stop_s and stop_s in text:
                         reason = "stop"
                         break
             if seq.stream and seq.callback is not None and delta:
                 seq.callback("token", seq, delta)
             if reason is not None:
+                if resolve:  # later in-flight samples of this sequence are discarded
+                    del seq.output_ids[nout:]
+                    seq.pending.clear()
                 self._finish(seq, reason)
-        st.cycle_time_s += time.perf_counter() - tc
-        return len(batch.items)
 
     def _finish(self, seq: Sequence, reason: str, notify_sched: bool = True, error: str | None = None) -> None:
         if notify_sched:
@@ -312,6 +377,9 @@ class LLMEngine:
             seq.status = SeqStatus.FINISHED
             seq.finish_reason = reason
         seq.finish_time = time.perf_counter()
+        if seq.pending:  # abort / error with samples still in flight: drop the placeholders
+            seq.output_ids = [t for t in seq.output_ids if t != PENDING]
+            seq.pending.clear()
         self._by_id.pop(seq.request_id, None)
         self.stats.requests_finished += 1
         self.stats.prompt_tokens += len(seq.prompt_ids)
@@ -347,6 +415,7 @@ class LLMEngine:
         ns, nt = len(batch.items), batch.num_tokens
         T = r._bucket(r.t_buckets, nt) if r.gpu else nt
         S = r._bucket(r.s_buckets, ns) if r.gpu else ns
+        r.meta.select(0)
         samples = r._fill(batch, T, S)
         r.meta.upload(ns)
         self._broadcast_header(T, S, ns)
@@ -372,10 +441,10 @@ class LLMEngine:
                 logits = self.model.forward(view, self.kv_caches, r.part_size)
                 r.out_tokens[:S] = logits.argmax(-1).int()  # CPU TP path is greedy-only (tests)
         if r.gpu:
-            r.out_host[:ns].copy_(r.out_tokens[:ns], non_blocking=True)
-            r.done.record()
-            r.done.synchronize()
-            return r.out_host[:ns].tolist()
+            r.out_hosts[0][:ns].copy_(r.out_tokens[:ns], non_blocking=True)
+            r.dones[0].record()
+            r.dones[0].synchronize()
+            return r.out_hosts[0][:ns].tolist()
         return r.out_tokens[:ns].tolist()
 
     def follower_loop(self) -> None:

@@ -7,12 +7,20 @@ HIP stream: every kernel launch of the forward plus the sampler). All dynamic
 inputs live in :class:`StepMeta` device buffers, so a replay costs one H2D copy,
 one graph launch and one D2H copy of the sampled token ids. ``enforce_eager``
 (or a CPU device) runs the same code without capture.
+
+Asynchronous scheduling: :meth:`launch` enqueues a step and returns at once;
+:meth:`collect` waits for its sampled ids. A decode token the host has not seen
+yet is passed as ``-(slot + 1)`` and resolved on the device from the previous
+step's sampler output (``out_tokens``), so step t+1 is queued behind step t while
+the host post-processes t: the GPU never idles between steps. Host metadata and
+host-side sample buffers are double-buffered for that overlap.
 """
 from __future__ import annotations
 
 import bisect
 import logging
 import time
+from dataclasses import dataclass
 
 import numpy as np
 import torch
@@ -26,6 +34,15 @@ log = logging.getLogger("vgate.engine")
 DEFAULT_T_BUCKETS = [1, 2, 4, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256, 384, 512, 768, 1024, 1536, 2048,
                      3072, 4096, 6144, 8192, 12288, 16384]
 DEFAULT_S_BUCKETS = [1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024]
+
+
+@dataclass
+class StepHandle:
+    k: int                 # double-buffer index
+    ns: int                # batch items
+    samples: list[bool]    # item consumes its sampled token
+    toks: list[int] | None  # already known (CPU path)
+    t_launch: float
 
 
 class ModelRunner:
@@ -50,13 +67,17 @@ class ModelRunner:
         self.graphs: dict[tuple[int, int], tuple] = {}
         self.pool = None
         self.out_tokens = torch.zeros(self.max_seqs, dtype=torch.int32, device=self.device)
+        self.meta.prev_tokens = self.out_tokens if self.gpu else None
+        self._k = 0  # double-buffer index of the next launch
         if self.gpu:
-            self.out_host = torch.zeros(self.max_seqs, dtype=torch.int32, pin_memory=True)
+            self.out_hosts = [torch.zeros(self.max_seqs, dtype=torch.int32, pin_memory=True) for _ in range(2)]
             self.stream = torch.cuda.Stream(self.device)
-            self.started = torch.cuda.Event(enable_timing=True)
-            self.done = torch.cuda.Event(enable_timing=True)
+            self.started = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            self.dones = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            self.meta_copied = [torch.cuda.Event() for _ in range(2)]
+            self._meta_pending = [False, False]
         else:
-            self.out_host = self.out_tokens
+            self.out_hosts = [self.out_tokens]
         self.graph_hits = 0
         self.graph_misses = 0
         self.capture_seconds = 0.0
@@ -72,7 +93,7 @@ class ModelRunner:
         return buckets[i]
 
     # ---------------------------------------------------------------- metadata
-    def _fill(self, batch: ScheduledBatch, T: int, S: int) -> list[bool]:
+    def _fill(self, batch: ScheduledBatch, T: int, S: int, pending_slots: dict | None = None) -> list[bool]:
         m = self.meta
         h = m.h
         bs = self.block_size
@@ -89,6 +110,8 @@ class ModelRunner:
             c0 = seq.num_computed
             toks = seq.all_ids[c0: c0 + n]
             ids[t: t + n] = toks
+            if pending_slots and toks[-1] < 0:  # unresolved sample of the previous step
+                ids[t + n - 1] = -(pending_slots[seq.seq_id] + 1)
             p = np.arange(c0, c0 + n, dtype=np.int32)
             pos[t: t + n] = p
             blocks = np.asarray(seq.blocks, dtype=np.int32)
@@ -159,50 +182,73 @@ class ModelRunner:
 
     @torch.inference_mode()
     def execute(self, batch: ScheduledBatch) -> tuple[list[int], list[bool]]:
-        """Run one step; returns (sampled token per item, whether the item consumes it)."""
+        """Run one step synchronously; returns (sampled token per item, whether consumed)."""
+        h = self.launch(batch)
+        return self.collect(h), h.samples
+
+    @torch.inference_mode()
+    def launch(self, batch: ScheduledBatch, pending_slots: dict | None = None) -> "StepHandle":
+        """Enqueue one step (GPU: returns before it runs). ``pending_slots`` maps a
+        sequence id to the previous step's sample slot of its unresolved last token."""
+        if not self.gpu:
+            toks, samples = self._execute_cpu(batch)
+            return StepHandle(0, len(batch.items), samples, toks, time.perf_counter())
         ns = len(batch.items)
         nt = batch.num_tokens
-        if self.gpu:
-            T = self._bucket(self.t_buckets, nt)
-            S = self._bucket(self.s_buckets, ns)
-        else:
-            T, S = nt, ns
+        T = self._bucket(self.t_buckets, nt)
+        S = self._bucket(self.s_buckets, ns)
         t_host = time.perf_counter()
-        samples = self._fill(batch, T, S)
-        if self.gpu:
-            self.started.record()
+        k = self._k
+        self._k ^= 1
+        if self._meta_pending[k]:  # host buffer k still feeding an H2D copy two steps back
+            self.meta_copied[k].synchronize()
+        self.meta.select(k)
+        samples = self._fill(batch, T, S, pending_slots)
+        self.started[k].record()
         self.meta.upload(ns)
-        if self.gpu:
-            if self.use_graphs:
-                key = (T, S)
-                g = self.graphs.get(key)
-                if g is None:
-                    self.graph_misses += 1
-                    g = self._capture(T, S)
-                    self.graphs[key] = g
-                    # the capture's warm-up/capture runs consumed the same metadata: replay for real
-                else:
-                    self.graph_hits += 1
-                g.replay()
+        self.meta_copied[k].record()
+        self._meta_pending[k] = True
+        if self.use_graphs:
+            key = (T, S)
+            g = self.graphs.get(key)
+            if g is None:
+                self.graph_misses += 1
+                # the capture's eager warm-up samples into out_tokens, which this step may
+                # still have to read (ids < 0): keep the previous step's samples aside
+                saved = self.out_tokens.clone()
+                g = self._capture(T, S)
+                self.out_tokens.copy_(saved)
+                self.graphs[key] = g
             else:
-                view = self.meta.view(T, S)
-                view.num_tokens, view.num_seqs = nt, ns
-                self._forward_sample(view)
-            self.out_host[:ns].copy_(self.out_tokens[:ns], non_blocking=True)
-            self.done.record()
-            t_wait = time.perf_counter()
-            self.done.synchronize()
-            t_end = time.perf_counter()
-            self.host_ms += 1e3 * ((t_wait - t_host) + (time.perf_counter() - t_end))
-            self.gpu_ms += self.started.elapsed_time(self.done)
-            self.gpu_steps += 1
-            toks = self.out_host[:ns].tolist()
+                self.graph_hits += 1
+            g.replay()
         else:
             view = self.meta.view(T, S)
             view.num_tokens, view.num_seqs = nt, ns
-            self._cpu_sample(view, batch)
-            toks = self.out_tokens[:ns].tolist()
-        return toks, samples
+            self._forward_sample(view)
+        self.out_hosts[k][:ns].copy_(self.out_tokens[:ns], non_blocking=True)
+        self.dones[k].record()
+        self.host_ms += 1e3 * (time.perf_counter() - t_host)
+        return StepHandle(k, ns, samples, None, t_host)
+
+    def collect(self, h: "StepHandle") -> list[int]:
+        """Wait for a launched step and return its sampled ids (one per batch item)."""
+        if h.toks is not None:
+            return h.toks
+        self.dones[h.k].synchronize()
+        self.gpu_ms += self.started[h.k].elapsed_time(self.dones[h.k])
+        self.gpu_steps += 1
+        return self.out_hosts[h.k][: h.ns].tolist()
+
+    def _execute_cpu(self, batch):
+        ns, nt = len(batch.items), batch.num_tokens
+        self.meta.select(0)
+        samples = self._fill(batch, nt, ns)
+        self.meta.upload(ns)
+        view = self.meta.view(nt, ns)
+        view.num_tokens, view.num_seqs = nt, ns
+        self._cpu_sample(view, batch)
+        return self.out_tokens[:ns].tolist(), samples
 
     def _cpu_sample(self, view, batch):
         logits = self.model.forward(view, self.kv, self.part_size)

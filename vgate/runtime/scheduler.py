@@ -29,6 +29,7 @@ class ScheduledBatch:
     num_prefill_tokens: int
     num_decode: int
     preempted: list[Sequence]
+    kv_pressure: bool = False  # no_preempt mode stopped early for lack of KV blocks
 
     @property
     def empty(self) -> bool:
@@ -71,7 +72,9 @@ class Scheduler:
         self.waiting.appendleft(victim)
         out.append(victim)
 
-    def schedule(self) -> ScheduledBatch:
+    def schedule(self, no_preempt: bool = False) -> ScheduledBatch:
+        """Build the next step. ``no_preempt`` (a step is in flight): stop instead of
+        preempting when the KV pool runs out (the caller drains and reschedules)."""
         budget = self.max_tokens
         items: list[tuple[Sequence, int]] = []
         preempted: list[Sequence] = []
@@ -81,7 +84,13 @@ class Scheduler:
         i = 0
         while i < len(self.running) and budget > 0:
             seq = self.running[i]
+            if seq.pending and (len(seq.output_ids) >= seq.params.max_tokens
+                                or seq.total_len >= self.max_model_len):
+                i += 1  # its last token is in flight and will end it: nothing to compute
+                continue
             n = min(seq.remaining, budget)
+            if no_preempt and not self.kv.ensure(seq, n):
+                return ScheduledBatch(items, sum(k for _, k in items), n_prefill, n_decode, preempted, True)
             while not self.kv.ensure(seq, n):
                 victim = self.running[-1]
                 self._preempt(victim, preempted)

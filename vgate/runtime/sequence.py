@@ -1,6 +1,7 @@
 """Request state inside the native engine."""
 from __future__ import annotations
 
+import collections
 import enum
 import itertools
 import time
@@ -10,6 +11,9 @@ from typing import Callable
 from vgate.runtime.sampling_params import SamplingParams
 
 _ids = itertools.count()
+
+
+PENDING = -1  # placeholder for a token sampled by an in-flight step
 
 
 class SeqStatus(enum.Enum):
@@ -43,6 +47,10 @@ class Sequence:
     hashed_blocks: int = 0
     block_hashes: list[int] = field(default_factory=list)
     aborted: bool = False
+    # asynchronous scheduling: output_ids indices still holding PENDING (sampled on the
+    # device, not yet seen by the host) and the sample slot of the newest one
+    pending: collections.deque = field(default_factory=collections.deque)
+    pending_slot: int = -1
 
     @property
     def all_ids(self) -> list[int]:
@@ -51,6 +59,10 @@ class Sequence:
     @property
     def total_len(self) -> int:
         return len(self.prompt_ids) + len(self.output_ids)
+
+    @property
+    def num_outputs_resolved(self) -> int:
+        return len(self.output_ids) - len(self.pending)
 
     @property
     def remaining(self) -> int:

@@ -36,6 +36,7 @@ class StepView:
     top_k: torch.Tensor
     seeds: torch.Tensor
     offsets: torch.Tensor
+    prev_tokens: torch.Tensor | None = None  # previous step's sampled ids (ids < 0 refer into it)
     num_tokens: int = 0
     num_seqs: int = 0
 
@@ -63,17 +64,29 @@ class StepMeta:
             off += np.dtype(dt).itemsize * n
         self.nbytes = _align(off, 16)
         use_pin = pinned and self.device.type == "cuda"
-        self.host = torch.zeros(self.nbytes, dtype=torch.uint8, pin_memory=use_pin)
+        # two pinned host buffers: with asynchronous scheduling the next step is written
+        # while the previous step's H2D copy may still be queued behind a running graph
+        nhost = 2 if self.device.type == "cuda" else 1
+        self.hosts = [torch.zeros(self.nbytes, dtype=torch.uint8, pin_memory=use_pin) for _ in range(nhost)]
         self.dev = torch.zeros(self.nbytes, dtype=torch.uint8, device=self.device) if self.device.type == "cuda" \
-            else self.host
-        hnp = self.host.numpy()
-        self.h = {}
-        self.d = {}
+            else self.hosts[0]
         tdt = {np.int64: torch.int64, np.float32: torch.float32, np.int32: torch.int32}
-        for name, (o, dt, n) in self.layout.items():
-            self.h[name] = hnp[o: o + np.dtype(dt).itemsize * n].view(dt)
-            self.d[name] = self.dev[o: o + np.dtype(dt).itemsize * n].view(tdt[dt])
-        self.bt_host = self.h["block_tables"].reshape(self.S, max_blocks)
+        self._h = []
+        for host in self.hosts:
+            hnp = host.numpy()
+            self._h.append({name: hnp[o: o + np.dtype(dt).itemsize * n].view(dt)
+                            for name, (o, dt, n) in self.layout.items()})
+        self.d = {name: self.dev[o: o + np.dtype(dt).itemsize * n].view(tdt[dt])
+                  for name, (o, dt, n) in self.layout.items()}
+        self.prev_tokens = None
+        self.select(0)
+
+    def select(self, k: int) -> None:
+        """Make host buffer k the one _fill writes and upload() copies from."""
+        self.k = k
+        self.host = self.hosts[k]
+        self.h = self._h[k]
+        self.bt_host = self.h["block_tables"].reshape(self.S, self.max_blocks)
 
     def reset(self) -> None:
         self.h["tile_seq"][:] = -1
@@ -97,4 +110,4 @@ class StepMeta:
             tile_seq=d["tile_seq"][: T // 16 + S], tile_q0=d["tile_q0"][: T // 16 + S],
             sample_idx=d["sample_idx"][:S], block_tables=d["block_tables"].view(self.S, self.max_blocks)[:S],
             temperature=d["temperature"][:S], top_p=d["top_p"][:S], top_k=d["top_k"][:S],
-            seeds=d["seeds"][:S], offsets=d["offsets"][:S])
+            seeds=d["seeds"][:S], offsets=d["offsets"][:S], prev_tokens=self.prev_tokens)
