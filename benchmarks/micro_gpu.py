@@ -163,11 +163,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--M", type=int, default=8)
+    ap.add_argument("--only", default=None, choices=[None, "attn", "sampler", "gemm"])
     a = ap.parse_args()
     print(json.dumps(floor()), flush=True)
+    if a.only == "gemm":
+        sweep(a.M, a.quick)
+        return
     for ctx in (64, 512, 2048):
-        for part in (256, 512, 2048):
+        for part in (64, 128, 256, 512):
             print(json.dumps(attention_bench(ctx=ctx, part=part)), flush=True)
+    if a.only == "attn":
+        return
     print(json.dumps(sampler_bench()), flush=True)
     print(json.dumps(sampler_sweep()), flush=True)
     sweep(a.M, a.quick)

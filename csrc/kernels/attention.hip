@@ -111,16 +111,19 @@ __device__ __forceinline__ bf16x8 softmax_step(f32x4& s0, f32x4& s1, float& m, f
     s1[i] = t1 < lim ? s1[i] * cscale : -INFINITY;
     cmax = fmaxf(cmax, fmaxf(s0[i], s1[i]));
   }
-  cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
-  cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+  cmax = fmaxf(cmax, xor16(cmax));
+  cmax = fmaxf(cmax, xor32(cmax));
   const float mn = fmaxf(m, cmax);
-  const bool dead = (mn == -INFINITY);
-  const float alpha = dead ? 1.f : exp2f(m - mn);
+  // a fully masked column keeps m = -inf: exponentiate against 0 instead, so masked
+  // scores give exp2(-inf) = 0 and alpha only multiplies zeros (no per-element selects).
+  // Raw v_exp_f32: the arguments are <= 0 and underflow to 0 is the wanted result.
+  const float mref = mn == -INFINITY ? 0.f : mn;
+  const float alpha = __builtin_amdgcn_exp2f(m - mref);
   float ps = 0.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    s0[i] = dead ? 0.f : exp2f(s0[i] - mn);
-    s1[i] = dead ? 0.f : exp2f(s1[i] - mn);
+    s0[i] = __builtin_amdgcn_exp2f(s0[i] - mref);
+    s1[i] = __builtin_amdgcn_exp2f(s1[i] - mref);
     ps += s0[i] + s1[i];
   }
   l = l * alpha + ps;
@@ -130,180 +133,171 @@ __device__ __forceinline__ bf16x8 softmax_step(f32x4& s0, f32x4& s1, float& m, f
   return pack_p(s0, s1);
 }
 
-// LDS: max(decode V images, decode merge scratch, prefill double buffer) | ticket flag
-__host__ __device__ constexpr int attn_flag_off(int nw) {
-  const int vimg = nw * CHUNK * D_ * 2;
-  const int merge = (2 * 16 * nw + nw * D_ * 16) * 4;
-  const int pre = 2 * CHUNK * D_ * 2;
-  const int m = vimg > merge ? vimg : merge;
-  return m > pre ? m : pre;
+// LDS: max(one V image per decode wave, prefill double buffer)
+__host__ __device__ constexpr int attn_lds_bytes(int nw) {
+  return nw * CHUNK * D_ * 2 > 2 * CHUNK * D_ * 2 ? nw * CHUNK * D_ * 2 : 2 * CHUNK * D_ * 2;
 }
 
 // ---------------------------------------------------------------- decode ----
-// One block per (sequence, KV head, partition); its nw waves take chunks w, w+nw, ...
-// Query columns = the G = Hq/Hkv heads sharing this KV head. Only sequences with a
-// single new query token are decode work (prefill tiles cover the rest).
-__device__ __forceinline__ void decode_body(const AttnArgs& a, int s, int h, int part, char* smem) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+// ONE WAVE per (sequence, KV head, partition): the wave walks its partition's 32-token
+// chunks itself, so no cross-wave merge (measured 3 us of LDS traffic + barriers per
+// launch for the split-across-waves form) and no block barrier anywhere on this path
+// (waves exit independently). The next chunk's K fragments are prefetched while the
+// current chunk computes; V is loaded at the top of its chunk and lands while QK^T and
+// the softmax run. Query columns = the G = Hq/Hkv heads sharing the KV head. Partitions
+// of one (sequence, head) are merged by the last-arriving wave (sc1 hand-off + ticket).
+// Only sequences with a single new query token are decode work.
+#define ATTN_STAMP(i)                                                                          \
+  do {                                                                                         \
+    if (a.dbg_ts != nullptr && lane == 0 && s == 0 && h == 0 && part == 0)                     \
+      a.dbg_ts[i] = __builtin_amdgcn_s_memtime();                                              \
+  } while (0)
+
+__device__ __forceinline__ void load_k_regs(uint4 (&kf)[8], const bf16_t* kb0, const bf16_t* kb1, int lane) {
+  const bf16_t* k0 = kb0 + (lane & 15) * D_ + 8 * (lane >> 4);
+  const bf16_t* k1 = kb1 + (lane & 15) * D_ + 8 * (lane >> 4);
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) kf[kk] = *reinterpret_cast<const uint4*>(k0 + 32 * kk);
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) kf[4 + kk] = *reinterpret_cast<const uint4*>(k1 + 32 * kk);
+}
+
+__device__ __forceinline__ void decode_wave(const AttnArgs& a, int s, int h, int part, bf16_t* vl, int* lds_flag) {
+  const int lane = threadIdx.x & 63;
+  ATTN_STAMP(0);
+  if (a.dbg_ts != nullptr && lane == 0 && s == 0 && h == 0 && part == 0) a.dbg_ts[6] = __builtin_amdgcn_s_memrealtime();
   const int pstart = part * a.part_size;
   const int* bt = a.block_tables + (size_t)s * a.max_blocks;
-  // Issue every independent load of the dependency chain up front: context length,
-  // query offsets and this wave's first two block-table entries (the row is always
-  // in bounds) are in flight together, so K/V addresses are ready one round trip in.
+  // every independent load of the dependency chain up front
   const int ctx = a.context_lens[s];
   const int qbeg = a.query_start ? a.query_start[s] : s;
   const int qend = a.query_start ? a.query_start[s + 1] : s + 1;
-  const int bi0 = min((pstart + wid * CHUNK) / BS_, a.max_blocks - 1);
-  const int bt_first0 = bt[bi0];
-  const int bt_first1 = bt[min(bi0 + 1, a.max_blocks - 1)];
-  if (ctx <= 0 || pstart >= ctx) return;
-  if (qend - qbeg != 1) return;
-  const int pend = min(ctx, pstart + a.part_size);
-  const int nparts = (ctx + a.part_size - 1) / a.part_size;
+  // the partition's block-table entries, one per lane (part_size <= 1024 tokens): chunk
+  // addresses come from v_readlane, never from a per-chunk global load (whose wait would
+  // also drain the prefetched K/V and re-serialise the chunk loop)
+  const int btv = bt[min(pstart / BS_ + lane, a.max_blocks - 1)];
   const int G = a.Hq / a.Hkv;
   const int col = lane & 15;
-  const int qtok = qbeg;
-  const int nch = (pend - pstart + CHUNK - 1) / CHUNK;
-  const bool ticketed = nparts > 1 && a.tickets != nullptr;
-  if (nch <= 1 && wid > 0 && !ticketed) return;  // single chunk: wave 0 alone, no merge
-
+  const bool cok = col < G;
   uint4 qf[4];
   {
-    const bool ok = col < G;
-    const bf16_t* qp = a.q + (size_t)qtok * a.q_stride + (size_t)(h * G + (ok ? col : 0)) * D_ + 8 * (lane >> 4);
+    const bf16_t* qp = a.q + (size_t)qbeg * a.q_stride + (size_t)(h * G + (cok ? col : 0)) * D_ + 8 * (lane >> 4);
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-      qf[kk] = ok ? *reinterpret_cast<const uint4*>(qp + 32 * kk) : make_uint4(0, 0, 0, 0);
+    for (int kk = 0; kk < 4; ++kk) qf[kk] = cok ? *reinterpret_cast<const uint4*>(qp + 32 * kk) : make_uint4(0, 0, 0, 0);
   }
+  if (ctx <= 0 || pstart >= ctx || qend - qbeg != 1) return;
+  ATTN_STAMP(1);
+  const int pend = min(ctx, pstart + a.part_size);
+  const int nparts = (ctx + a.part_size - 1) / a.part_size;
+  const int nch = (pend - pstart + CHUNK - 1) / CHUNK;
+  const size_t head_off = (size_t)h * BS_ * D_;
+  const size_t blk_stride = (size_t)a.Hkv * BS_ * D_;
   const float cscale = a.scale * LOG2E;
   float m = -INFINITY, l = 0.f;
   f32x4 o[8];
 #pragma unroll
   for (int mt = 0; mt < 8; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  bf16_t* vl = reinterpret_cast<bf16_t*>(smem) + wid * (CHUNK * D_);
-  const size_t head_off = (size_t)h * BS_ * D_;
-  const size_t blk_stride = (size_t)a.Hkv * BS_ * D_;
-
-  for (int c = wid; c < nch; c += nw) {
+  // chunk c covers tokens [tb, tb + 32) = cache blocks (b0, b1). Two register sets
+  // ping-pong: chunk c+1's K/V loads are issued before chunk c is consumed, and nothing
+  // copies between the sets, so the wait for chunk c is a partial vmcnt that leaves
+  // chunk c+1 in flight (a copy would force vmcnt(0) and re-serialise every chunk).
+  auto issue = [&](uint4 (&kf)[8], uint4 (&vr)[8], int c) {
     const int tb = pstart + c * CHUNK;
-    const bool first = c == wid;
-    const int b0 = first ? bt_first0 : bt[tb / BS_];
-    const int b1 = (tb + BS_ < pend) ? (first ? bt_first1 : bt[tb / BS_ + 1]) : b0;
-    const bf16_t* kb0 = a.k_cache + (size_t)b0 * blk_stride + head_off;
-    const bf16_t* kb1 = a.k_cache + (size_t)b1 * blk_stride + head_off;
-    const bf16_t* vb0 = a.v_cache + (size_t)b0 * blk_stride + head_off;
-    const bf16_t* vb1 = a.v_cache + (size_t)b1 * blk_stride + head_off;
-    uint4 vr[8];
-    load_v_regs(vr, vb0, vb1, lane);
-    f32x4 s0 = qk_tile(kb0, qf, lane);
-    f32x4 s1 = qk_tile(kb1, qf, lane);
+    const int n0 = __builtin_amdgcn_readlane(btv, 2 * c);
+    const int n1 = (tb + BS_ < pend) ? __builtin_amdgcn_readlane(btv, 2 * c + 1) : n0;
+    load_k_regs(kf, a.k_cache + (size_t)n0 * blk_stride + head_off, a.k_cache + (size_t)n1 * blk_stride + head_off, lane);
+    load_v_regs(vr, a.v_cache + (size_t)n0 * blk_stride + head_off, a.v_cache + (size_t)n1 * blk_stride + head_off, lane);
+  };
+  // profiling: chunk-1 sub-phase stamps (each after forcing its results), dbg mode only
+  const bool prof = a.dbg_ts != nullptr && s == 0 && h == 0 && part == 0;
+  auto pstamp = [&](int i, float dep) {
+    if (prof) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\tv_mov_b32 %0, %0" : "+v"(dep)::"memory");
+      if (lane == 0) a.dbg_ts[i] = __builtin_amdgcn_s_memtime();
+    }
+  };
+  auto consume = [&](const uint4 (&kf)[8], const uint4 (&vr)[8], int c) {
+    const int tb = pstart + c * CHUNK;
+    if (c == 1) pstamp(8, __uint_as_float(kf[7].x ^ vr[7].x));
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) s0 = mfma16(as_bf16x8(kf[kk]), as_bf16x8(qf[kk]), s0);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) s1 = mfma16(as_bf16x8(kf[4 + kk]), as_bf16x8(qf[kk]), s1);
+    if (c == 1) pstamp(9, s0[0] + s1[3]);
     const bf16x8 pb = softmax_step(s0, s1, m, l, o, tb, pend, cscale, lane);
-    store_v_lds(vl, vr, lane, pend - tb);
+    if (c == 1) pstamp(10, (float)pb[0] + o[7][3]);
+    // rows past the context hold finite cache contents (the pool is zero-initialised)
+    // and meet p = 0: stored unmasked
+    store_v_lds(vl, vr, lane, CHUNK);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (c == 1) pstamp(11, 0.f);
     pv_update(o, vl, pb, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (c == 1) pstamp(12, o[0][0] + o[7][3]);
+  };
+  // Loads are issued UNCONDITIONALLY (a chunk index past the end re-reads the last chunk):
+  // with straight-line issue the compiler can count outstanding loads across the loop
+  // back-edge and emit partial vmcnt waits; a conditional issue makes it drain to 0.
+  uint4 ka[8], va[8], kb[8], vb[8];
+  issue(ka, va, 0);
+  for (int c = 0; c < nch; c += 2) {
+    issue(kb, vb, min(c + 1, nch - 1));
+    consume(ka, va, c);
+    issue(ka, va, min(c + 2, nch - 1));
+    if (c + 1 < nch) consume(kb, vb, c + 1);
   }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-
-  if (nch <= 1) {  // wave 0 holds the whole result: normalise and store from registers
-    if (wid == 0 && col < G) {
-      const int hq = h * G + col;
-      const int g = lane >> 4;
-      const float inv = l > 0.f ? 1.f / l : 0.f;
-      if (nparts == 1) {
-        bf16_t* op = a.out + (size_t)qtok * a.out_stride + (size_t)hq * D_;
+  l += xor16(l);
+  l += xor32(l);
+  ATTN_STAMP(2);
+  const int g = lane >> 4;
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  const int hq = h * G + col;
+  if (nparts == 1) {
+    if (cok) {
+      bf16_t* op = a.out + (size_t)qbeg * a.out_stride + (size_t)hq * D_;
 #pragma unroll
-        for (int mt = 0; mt < 8; ++mt) {
-          uint2 pk;
-          pk.x = pack_bf2(o[mt][0] * inv, o[mt][1] * inv);
-          pk.y = pack_bf2(o[mt][2] * inv, o[mt][3] * inv);
-          *reinterpret_cast<uint2*>(op + 16 * mt + 4 * g) = pk;
-        }
-      } else {
-        // partials travel by device-coherent sc1 stores (read by another block in-launch)
-        float* po = a.part_o + (((size_t)s * a.Hq + hq) * a.num_parts + part) * D_;
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt)
-          st_sc1_f4(po + 16 * mt + 4 * g, o[mt][0] * inv, o[mt][1] * inv, o[mt][2] * inv, o[mt][3] * inv);
-        if (g == 0) {
-          float* pm = a.part_ml + (((size_t)s * a.Hq + hq) * a.num_parts + part) * 2;
-          st_sc1(pm, m);
-          st_sc1(pm + 1, l);
-        }
-      }
-    }
-  } else {
-    // ---- merge the nw waves: scratch reuses the V images ----
-    __syncthreads();
-    float* sm_m = reinterpret_cast<float*>(smem);   // [nw][16]
-    float* sm_l = sm_m + 16 * nw;                   // [nw][16]
-    float* sm_o = sm_l + 16 * nw;                   // [nw][128][16]
-    if (lane < 16) {
-      sm_m[wid * 16 + lane] = m;
-      sm_l[wid * 16 + lane] = l;
-    }
-    {
-      const int g = lane >> 4;
-#pragma unroll
-      for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sm_o[(wid * D_ + 16 * mt + 4 * g + i) * 16 + col] = o[mt][i];
-    }
-    __syncthreads();
-    for (int idx = threadIdx.x; idx < G * (D_ / 4); idx += blockDim.x) {
-      const int cc = idx / (D_ / 4);
-      const int d0 = (idx % (D_ / 4)) * 4;
-      float M = -INFINITY;
-      for (int w = 0; w < nw; ++w) M = fmaxf(M, sm_m[w * 16 + cc]);
-      float L = 0.f, acc[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int w = 0; w < nw; ++w) {
-        const float mw = sm_m[w * 16 + cc];
-        const float f = (mw == -INFINITY) ? 0.f : exp2f(mw - M);
-        L += sm_l[w * 16 + cc] * f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] += sm_o[(w * D_ + d0 + j) * 16 + cc] * f;
-      }
-      const float inv = L > 0.f ? 1.f / L : 0.f;
-      const int hq = h * G + cc;
-      if (nparts == 1) {
-        bf16_t* op = a.out + (size_t)qtok * a.out_stride + (size_t)hq * D_ + d0;
+      for (int mt = 0; mt < 8; ++mt) {
         uint2 pk;
-        pk.x = pack_bf2(acc[0] * inv, acc[1] * inv);
-        pk.y = pack_bf2(acc[2] * inv, acc[3] * inv);
-        *reinterpret_cast<uint2*>(op) = pk;
-      } else {
-        float* po = a.part_o + (((size_t)s * a.Hq + hq) * a.num_parts + part) * D_ + d0;
-        st_sc1_f4(po, acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
-        if (d0 == 0) {
-          float* pm = a.part_ml + (((size_t)s * a.Hq + hq) * a.num_parts + part) * 2;
-          st_sc1(pm, M);
-          st_sc1(pm + 1, L);
-        }
+        pk.x = pack_bf2(o[mt][0] * inv, o[mt][1] * inv);
+        pk.y = pack_bf2(o[mt][2] * inv, o[mt][3] * inv);
+        *reinterpret_cast<uint2*>(op + 16 * mt + 4 * g) = pk;
       }
     }
+    ATTN_STAMP(3);
+    if (a.dbg_ts != nullptr && lane == 0 && s == 0 && h == 0 && part == 0) a.dbg_ts[7] = __builtin_amdgcn_s_memrealtime();
+    return;
   }
-  if (!ticketed) return;
-
-  // ---- partitions of (s, h): the last-arriving block merges them (in-launch) ----
-  int* flag = reinterpret_cast<int*>(smem + attn_flag_off(nw));
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {  // sc1 partials drained above: one ticket, no cache-wide fence
+  // partial (normalised o, running max m, sum l) by device-coherent stores
+  if (cok) {
+    float* po = a.part_o + (((size_t)s * a.Hq + hq) * a.num_parts + part) * D_;
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt)
+      st_sc1_f4(po + 16 * mt + 4 * g, o[mt][0] * inv, o[mt][1] * inv, o[mt][2] * inv, o[mt][3] * inv);
+    if (g == 0) {
+      float* pm = a.part_ml + (((size_t)s * a.Hq + hq) * a.num_parts + part) * 2;
+      st_sc1(pm, m);
+      st_sc1(pm + 1, l);
+    }
+  }
+  if (a.tickets == nullptr) return;  // separate reduce launch
+  drain_stores();
+  int last = 0;
+  if (lane == 0) {
     uint32_t* t = a.tickets + (size_t)s * a.Hkv + h;
     const uint32_t old = __hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == (uint32_t)(nparts - 1);
+    last = old == (uint32_t)(nparts - 1);
     if (last) __hip_atomic_store(t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = last;
   }
-  __syncthreads();
-  if (!*flag) return;
-  for (int idx = threadIdx.x; idx < G * (D_ / 4); idx += blockDim.x) {
-    const int hq = h * G + idx / (D_ / 4);
+  last = __shfl(last, 0, 64);
+  if (!last) return;
+  // last arriver: merge the nparts partials of the G heads (64 lanes x G*32 float4 outputs)
+  for (int idx = lane; idx < G * (D_ / 4); idx += 64) {
+    const int hh = h * G + idx / (D_ / 4);
     const int d0 = (idx % (D_ / 4)) * 4;
-    const float* pm = a.part_ml + ((size_t)s * a.Hq + hq) * a.num_parts * 2;
-    const float* po = a.part_o + ((size_t)s * a.Hq + hq) * a.num_parts * D_ + d0;
+    const float* pm = a.part_ml + ((size_t)s * a.Hq + hh) * a.num_parts * 2;
+    const float* po = a.part_o + ((size_t)s * a.Hq + hh) * a.num_parts * D_ + d0;
     float M = -INFINITY;
     for (int p = 0; p < nparts; ++p) M = fmaxf(M, ld_sc1(pm + 2 * p));
     float L = 0.f, acc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -313,11 +307,11 @@ __device__ __forceinline__ void decode_body(const AttnArgs& a, int s, int h, int
       L += w;
       acc[0] += w * v[0]; acc[1] += w * v[1]; acc[2] += w * v[2]; acc[3] += w * v[3];
     }
-    const float inv = L > 0.f ? 1.f / L : 0.f;
-    bf16_t* op = a.out + (size_t)qtok * a.out_stride + (size_t)hq * D_ + d0;
+    const float iv = L > 0.f ? 1.f / L : 0.f;
+    bf16_t* op = a.out + (size_t)qbeg * a.out_stride + (size_t)hh * D_ + d0;
     uint2 pk;
-    pk.x = pack_bf2(acc[0] * inv, acc[1] * inv);
-    pk.y = pack_bf2(acc[2] * inv, acc[3] * inv);
+    pk.x = pack_bf2(acc[0] * iv, acc[1] * iv);
+    pk.y = pack_bf2(acc[2] * iv, acc[3] * iv);
     *reinterpret_cast<uint2*>(op) = pk;
   }
 }
@@ -385,10 +379,13 @@ __device__ __forceinline__ void prefill_body(const AttnArgs& a, int tile, int h,
   const size_t head_off = (size_t)h * BS_ * D_;
   const size_t blk_stride = (size_t)a.Hkv * BS_ * D_;
   const int nch = (kv_end + CHUNK - 1) / CHUNK;
+  const int lane64 = threadIdx.x & 63;
+  int btv = 0;  // a 64-entry window of the block table, one entry per lane (see decode_wave)
   for (int c = 0; c < nch; ++c) {
     const int tb = c * CHUNK;
-    const int b0 = bt[tb / BS_];
-    const int b1 = (tb + BS_ < kv_end) ? bt[tb / BS_ + 1] : b0;
+    if ((c & 31) == 0) btv = bt[min(2 * c + lane64, a.max_blocks - 1)];
+    const int b0 = __builtin_amdgcn_readlane(btv, (2 * c) & 63);
+    const int b1 = (tb + BS_ < kv_end) ? __builtin_amdgcn_readlane(btv, (2 * c + 1) & 63) : b0;
     const bf16_t* vb0 = a.v_cache + (size_t)b0 * blk_stride + head_off;
     const bf16_t* vb1 = a.v_cache + (size_t)b1 * blk_stride + head_off;
     bf16_t* vl = vls + (c & 1) * (CHUNK * D_);
@@ -422,16 +419,23 @@ __device__ __forceinline__ void prefill_body(const AttnArgs& a, int tile, int h,
 }
 
 // ------------------------------------------------------------- unified launch ----
-// grid.x = [decode blocks for sequences 0..dec_seqs) ++ [prefill tiles], grid.y = KV
-// heads, grid.z = decode partitions. One launch serves a decode-only, prefill-only or
-// mixed (chunked-prefill) step; blocks without work exit immediately.
-__global__ __launch_bounds__(1024) void attn_kernel(AttnArgs a, int dec_seqs) {
+// grid.x = [decode blocks: nw waves each, wave = unit (partition-major: unit = p*S + s)]
+//          ++ [prefill tiles], grid.y = KV heads. One launch serves a decode-only,
+// prefill-only or mixed (chunked-prefill) step; waves / blocks without work exit.
+// MAXT: 512 threads (G <= 8 query heads per KV head) leaves 256 VGPRs per wave for the
+// prefetched K + in-flight V + O accumulators; 1024 only for G > 8.
+template <int MAXT>
+__global__ __launch_bounds__(MAXT) void attn_kernel(AttnArgs a, int dec_seqs, int dec_blocks) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int bx = blockIdx.x;
-  if (bx < dec_seqs) {
-    decode_body(a, bx, blockIdx.y, blockIdx.z, smem);
-  } else if (blockIdx.z == 0) {
-    prefill_body(a, bx - dec_seqs, blockIdx.y, smem);
+  if (bx < dec_blocks) {
+    const int wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int unit = bx * nw + wid;
+    if (unit >= dec_seqs * a.num_parts) return;
+    decode_wave(a, unit % dec_seqs, blockIdx.y, unit / dec_seqs,
+                reinterpret_cast<bf16_t*>(smem) + wid * (CHUNK * D_), nullptr);
+  } else {
+    prefill_body(a, bx - dec_blocks, blockIdx.y, smem);
   }
 }
 
@@ -440,15 +444,17 @@ static int attn_waves(const AttnArgs& a) {
   return G > 4 ? G : 4;
 }
 
-static size_t attn_lds(int nw) { return attn_flag_off(nw) + 16; }
-
 void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
   const int tiles = a.num_tiles > 0 ? a.num_tiles : 0;
-  const int nx = dec_seqs + tiles;
-  if (nx <= 0) return;
   const int nw = attn_waves(a);
-  const int nz = dec_seqs > 0 ? a.num_parts : 1;
-  hipLaunchKernelGGL(attn_kernel, dim3(nx, a.Hkv, nz), dim3(64 * nw), attn_lds(nw), st, a, dec_seqs);
+  const int units = dec_seqs > 0 ? dec_seqs * a.num_parts : 0;
+  const int dec_blocks = (units + nw - 1) / nw;
+  const int nx = dec_blocks + tiles;
+  if (nx <= 0) return;
+  if (nw <= 8)
+    hipLaunchKernelGGL(attn_kernel<512>, dim3(nx, a.Hkv, 1), dim3(64 * nw), attn_lds_bytes(nw), st, a, dec_seqs, dec_blocks);
+  else
+    hipLaunchKernelGGL(attn_kernel<1024>, dim3(nx, a.Hkv, 1), dim3(64 * nw), attn_lds_bytes(nw), st, a, dec_seqs, dec_blocks);
   if (dec_seqs > 0 && a.num_parts > 1 && a.tickets == nullptr)
     hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(dec_seqs, a.Hq), dim3(128), 0, st, a);
 }

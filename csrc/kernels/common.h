@@ -107,6 +107,19 @@ __device__ __forceinline__ uint4 ld_nt16(const uint4* p) {
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
+// ---- cross-row lane exchange on the VALU (gfx950 v_permlane16/32_swap), no LDS pipe ----
+// xor32(v): lane l gets lane l^32's value; xor16(v): lane l gets lane l^16's value.
+// (__shfl_xor lowers to ds_bpermute: an LDS round trip on the critical path of a
+// softmax reduction.)
+__device__ __forceinline__ float xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float xor16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float((threadIdx.x & 16) ? r[0] : r[1]);
+}
+
 // ---- in-launch cross-workgroup hand-off (cross-XCD safe, no cache-wide fences) ----
 // The per-XCD L2s are not coherent, and an agent-scope release/acquire fence compiles to
 // buffer_wbl2 / buffer_inv of the WHOLE L2 (write back every dirty line, drop every clean

@@ -91,6 +91,8 @@ struct AttnArgs {
   // (sequence, KV head): zero-initialised, self-resetting [S * Hkv] tickets (null ->
   // separate reduce launch)
   uint32_t* tickets;
+  // profiling only: phase timestamps (s_memtime) of block (0,0,0) wave 0, or null
+  unsigned long long* dbg_ts;
 };
 void launch_attn_decode(const AttnArgs& a, hipStream_t st);
 void launch_attn_prefill(const AttnArgs& a, hipStream_t st);

@@ -203,7 +203,7 @@ void attn_decode(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const
                  Tensor& part_ml, int64_t Hq, int64_t Hkv, int64_t part_size, double scale) {
   auto a = attn_common(q, q_stride, k_cache, v_cache, block_tables, context_lens, out, Hq, Hkv, scale);
   CHECK_DT(part_o, torch::kFloat32); CHECK_DT(part_ml, torch::kFloat32);
-  TORCH_CHECK(part_size % 32 == 0, "attention: part_size % 32");
+  TORCH_CHECK(part_size % 32 == 0 && part_size <= 1024, "attention: part_size must be a multiple of 32, <= 1024");
   TORCH_CHECK(part_o.dim() == 4 && part_o.size(0) >= a.S && part_o.size(1) == Hq && part_o.size(3) == 128,
               "attention: part_o must be [S, Hq, P, 128]");
   a.num_parts = (int)part_o.size(2);
@@ -239,12 +239,12 @@ void attention(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const T
                const Tensor& block_tables, const Tensor& context_lens, const Tensor& query_start,
                const Tensor& tile_seq, const Tensor& tile_q0, Tensor& out, Tensor& part_o, Tensor& part_ml,
                int64_t Hq, int64_t Hkv, int64_t part_size, double scale, int64_t out_stride,
-               const c10::optional<Tensor>& tickets) {
+               const c10::optional<Tensor>& tickets, const c10::optional<Tensor>& dbg_ts) {
   auto a = attn_common(q, q_stride, k_cache, v_cache, block_tables, context_lens, out, Hq, Hkv, scale);
   if (out_stride > 0) a.out_stride = (int)out_stride;
   CHECK_DT(query_start, torch::kInt32); CHECK_DT(tile_seq, torch::kInt32); CHECK_DT(tile_q0, torch::kInt32);
   CHECK_DT(part_o, torch::kFloat32); CHECK_DT(part_ml, torch::kFloat32);
-  TORCH_CHECK(part_size % 32 == 0, "attention: part_size % 32");
+  TORCH_CHECK(part_size % 32 == 0 && part_size <= 1024, "attention: part_size must be a multiple of 32, <= 1024");
   TORCH_CHECK(query_start.numel() >= a.S + 1, "attention: query_start needs S+1 entries");
   a.query_start = reinterpret_cast<const int32_t*>(query_start.data_ptr());
   a.tile_seq = reinterpret_cast<const int32_t*>(tile_seq.data_ptr());
@@ -261,6 +261,11 @@ void attention(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const T
     CHECK_DEV(*tickets); CHECK_DT(*tickets, torch::kInt32);
     TORCH_CHECK(tickets->numel() >= (int64_t)a.S * Hkv, "attention: tickets need S*Hkv zeroed int32");
     a.tickets = reinterpret_cast<uint32_t*>(tickets->data_ptr());
+  }
+  if (dbg_ts.has_value() && dbg_ts->defined()) {
+    CHECK_DEV(*dbg_ts); CHECK_DT(*dbg_ts, torch::kInt64);
+    TORCH_CHECK(dbg_ts->numel() >= 16, "attention: dbg_ts needs 16 int64");
+    a.dbg_ts = reinterpret_cast<unsigned long long*>(dbg_ts->data_ptr());
   }
   c10::DeviceGuard guard(q.device());
   vgate::launch_attention(a, a.S, cur_stream());
@@ -323,7 +328,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),
         py::arg("part_o"), py::arg("part_ml"), py::arg("Hq"), py::arg("Hkv"), py::arg("part_size"), py::arg("scale"),
-        py::arg("out_stride") = 0, py::arg("tickets") = py::none());
+        py::arg("out_stride") = 0, py::arg("tickets") = py::none(), py::arg("dbg_ts") = py::none());
   m.def("embedding", &embedding, "vocab-sharded embedding gather (negative ids: previous step's samples)",
         py::arg("ids"), py::arg("table"), py::arg("out"), py::arg("vstart") = 0, py::arg("prev") = py::none());
   m.def("rmsnorm", &rmsnorm, "RMSNorm with optional fused residual add");
