@@ -162,6 +162,7 @@ def main():
     else:
         allr = [res]
     if rank == 0:
+        model_name = args.model.split("/")[-1]
         lat = [x for r in allr for x in r["lat"]]
         total = sum(r["n"] for r in allr)
         wall = max(r["wall"] for r in allr)
@@ -171,8 +172,8 @@ def main():
             "metric": METRIC, "value": round(value, 3), "unit": "req/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * wall / args.steps, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": round(value / BASELINE_REQ_S, 3), "dtype": "bf16",
-            "data": "synthetic unique prompts, random-init weights (Qwen2.5-1.5B architecture)",
-            "config": {"model": "Qwen2.5-1.5B-Instruct", "global_batch": args.concurrency * world,
+            "data": f"synthetic unique prompts, random-init weights ({model_name} architecture)",
+            "config": {"model": model_name, "global_batch": args.concurrency * world,
                        "seq_len": args.max_tokens, "parallelism": f"dp{world}",
                        "concurrency_per_gpu": args.concurrency, "max_tokens": args.max_tokens,
                        "requests_per_step_per_gpu": args.requests_per_step},

@@ -55,6 +55,7 @@ struct GemmParams {
   const int32_t* positions; const int32_t* slots; const float* cos_sin;
   bf16_t* k_cache; bf16_t* v_cache; int hq; int hkv; int bs;
   const bf16_t* scales; const bf16_t* zeros; int group;
+  unsigned long long* dbg_ts;  // per-block [start, end] realtime stamps (profiling), or null
 };
 
 __device__ __forceinline__ int row_of(const GemmParams& p, int m) {
@@ -323,6 +324,8 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
   constexpr int R = 16 / XP;  // real rows per packed load
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const size_t bid = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  if (p.dbg_ts != nullptr && threadIdx.x == 0) p.dbg_ts[2 * bid] = __builtin_amdgcn_s_memrealtime();
   const int KT = p.K >> 5;
   const int nt0 = blockIdx.x * NTB;
   const int m_base = blockIdx.y * 16 * MB;
@@ -464,6 +467,7 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
     }
   }
   gemm_finish<MB, NTB, EPI, NORM>(p, acc, ssr, smem, m_base, nt0);
+  if (p.dbg_ts != nullptr && threadIdx.x == 0) p.dbg_ts[2 * bid + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ---- AWQ W4A16 ----
@@ -629,6 +633,7 @@ static GemmParams to_params(const GemmArgs& g) {
   p.positions = g.positions; p.slots = g.slots; p.cos_sin = g.cos_sin;
   p.k_cache = g.k_cache; p.v_cache = g.v_cache; p.hq = g.hq; p.hkv = g.hkv; p.bs = g.bs;
   p.scales = g.scales; p.zeros = g.zeros; p.group = g.group;
+  p.dbg_ts = g.dbg_ts;
   return p;
 }
 

@@ -43,6 +43,8 @@ struct GemmArgs {
   const uint16_t* scales;  // [K/group][N] bf16
   const uint16_t* zeros;   // [K/group][N] bf16 (= scale * zero)
   int group;
+  // profiling only: per-block [start, end] s_memrealtime stamps (2 x blocks u64), or null
+  unsigned long long* dbg_ts;
 };
 void launch_gemm(const GemmArgs& g, hipStream_t st);
 void launch_awq_gemm(const GemmArgs& g, hipStream_t st);

@@ -51,7 +51,7 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
           const c10::optional<Tensor>& cos_sin, const c10::optional<Tensor>& k_cache,
           const c10::optional<Tensor>& v_cache, int64_t hq, int64_t hkv,
           const c10::optional<Tensor>& awq_scales, const c10::optional<Tensor>& awq_zeros, int64_t group,
-          bool rownorm) {
+          bool rownorm, const c10::optional<Tensor>& dbg_ts) {
   CHECK_DEV(x); CHECK_DEV(wp); CHECK_DEV(out);
   CHECK_DT(x, torch::kBFloat16);
   CHECK_LASTDIM(x); CHECK_LASTDIM(out);
@@ -89,6 +89,7 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
   g.x = bf16p(x); g.lda = (int)x.stride(0); g.M = (int)M; g.row_idx = ridx;
   g.wp = wp.data_ptr(); g.N = (int)N; g.K = (int)K;
   g.norm_w = opt_bf16(norm_w); g.eps = (float)eps; g.rownorm = rownorm ? 1 : 0;
+  g.dbg_ts = reinterpret_cast<unsigned long long*>(opt_ptr<int64_t>(dbg_ts, torch::kInt64, "dbg_ts"));
   if (g.norm_w) TORCH_CHECK(norm_w->numel() == K, "norm_w must have K elements");
   g.bias = opt_bf16(bias);
   g.res = opt_bf16(res);
@@ -323,7 +324,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("slots") = py::none(), py::arg("cos_sin") = py::none(), py::arg("k_cache") = py::none(),
         py::arg("v_cache") = py::none(), py::arg("hq") = 0, py::arg("hkv") = 0,
         py::arg("awq_scales") = py::none(), py::arg("awq_zeros") = py::none(), py::arg("group") = 128,
-        py::arg("rownorm") = false);
+        py::arg("rownorm") = false, py::arg("dbg_ts") = py::none());
   m.def("attention", &attention, "unified paged attention: decode (partitions merged in-launch) + varlen prefill tiles",
         py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),
