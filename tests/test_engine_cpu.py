@@ -139,3 +139,28 @@ def test_threaded_engine_start_stop():
         assert len(res["seq"].output_ids) == 3
     finally:
         eng.stop()
+
+
+def test_embeddings_match_dense_reference():
+    """engine.embed: L2-normalised mean of the final-RMSNorm hidden states (prefill through
+    scratch KV blocks, released afterwards) == the dense fp32 oracle."""
+    import torch
+    eng = _engine() if "_engine" in globals() else None
+    if eng is None:
+        from vgate.runtime.engine import EngineConfig, LLMEngine
+        eng = LLMEngine(EngineConfig(model="tiny", device="cpu", max_model_len=256, max_num_seqs=8,
+                                     max_num_batched_tokens=128, num_kv_blocks=64, warmup=False))
+    free0 = eng.kvm.num_free()
+    ids = [5, 17, 99, 42, 7, 300, 11]
+    vec, n = eng.embed(prompt_ids=ids)
+    assert n == len(ids) and len(vec) == eng.arch.hidden_size
+    v = torch.tensor(vec)
+    assert abs(v.norm().item() - 1.0) < 1e-4
+    ref = eng.model.reference_logits(ids, return_hidden=True).float().mean(0)
+    ref = ref / ref.norm()
+    assert torch.nn.functional.cosine_similarity(v, ref, dim=0).item() > 0.999
+    assert eng.kvm.num_free() == free0
+    v2, _ = eng.embed(prompt_ids=ids)
+    assert v2 == vec
+    v3, _ = eng.embed("a different sentence")
+    assert torch.nn.functional.cosine_similarity(v, torch.tensor(v3), dim=0).item() < 0.999

@@ -92,3 +92,41 @@ def test_async_scheduling_matches_sync():
 
     a, b = run(False), run(True)
     assert a == b
+
+
+def test_embeddings_gpu_match_reference():
+    eng = _engine()
+    ids = PROMPTS["q3"]
+    vec, n = eng.embed(prompt_ids=ids)
+    v = torch.tensor(vec)
+    ref = eng.model.reference_logits(ids, return_hidden=True).float().mean(0).cpu()
+    ref = ref / ref.norm()
+    assert n == len(ids) and abs(v.norm().item() - 1) < 1e-3
+    assert torch.nn.functional.cosine_similarity(v, ref, dim=0).item() > 0.995
+
+
+def test_llama_family_graph_eager_reference():
+    """Llama-3 layout (no qkv bias, theta 5e5, Hkv=1) through the same fused kernels."""
+    sp = SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True)
+    g_eng = _engine(model="tiny-llama")
+    g = _run(g_eng, [(k, v, sp) for k, v in PROMPTS.items()])
+    e_eng = _engine(model="tiny-llama", enforce_eager=True)
+    e = _run(e_eng, [(k, v, sp) for k, v in PROMPTS.items()])
+    for k in PROMPTS:
+        assert g[k].output_ids == e[k].output_ids, k
+    for k, v in list(PROMPTS.items())[:2]:
+        ids = v + g[k].output_ids
+        logits = e_eng.model.reference_logits(ids[:-1])[len(v) - 1:]
+        for t, tok in enumerate(g[k].output_ids):
+            row = logits[t]
+            assert row[tok] >= row.max() - 0.05 * row.std(), (k, t)
+
+
+def test_awq_engine_generates():
+    """W4A16 (AWQ int4, group 128) engine path: packed int4 weights + in-register dequant GEMMs."""
+    eng = _engine(quantization="awq")
+    sp = SamplingParams(temperature=0.7, top_p=0.9, max_tokens=12, ignore_eos=True)
+    out = _run(eng, [(k, v, sp) for k, v in list(PROMPTS.items())[:4]])
+    assert all(len(s.output_ids) == 12 for s in out.values())
+    assert all(0 <= t < eng.arch.vocab_size for s in out.values() for t in s.output_ids)
+    assert eng.model.weight_bytes() < _engine().model.weight_bytes()

@@ -121,15 +121,16 @@ class DecoderModel:
         return n
 
     # ---------------------------------------------------------------- forward
-    def forward(self, sv, kv_caches, part_size: int) -> torch.Tensor:
+    def forward(self, sv, kv_caches, part_size: int, return_hidden: bool = False) -> torch.Tensor:
         """One step. ``sv`` is a StepView (token/seq metadata views, bucket sizes T and S).
 
-        Returns f32 logits [S, vocab] for the sample rows (one per sequence).
+        Returns f32 logits [S, vocab] for the sample rows (one per sequence), or with
+        ``return_hidden`` the residual stream [T, H] after the last layer (embeddings).
         GPU: 4 fused GEMM launches + 1 attention launch per layer (RMSNorm, RoPE, KV
         write, bias, SiLU*mul and residual adds all live inside them).
         """
         if self.device.type != "cuda":
-            return self._forward_reference(sv, kv_caches, part_size)
+            return self._forward_reference(sv, kv_caches, part_size, return_hidden)
         a = self.arch
         sh = self.shard
         tp = self.tp
@@ -163,12 +164,14 @@ class DecoderModel:
             ops.linear(mlp, L.down, out=resid, residual=resid if first else None)
             if tp.size > 1:
                 tp.all_reduce(resid)
+        if return_hidden:
+            return resid
         logits = ops.linear(resid, self.lm_head, out_f32=True, norm=(self.final_norm, eps), row_idx=sv.sample_idx)
         if tp.size > 1:
             logits = tp.all_gather_lastdim(logits)
         return logits[:, : a.vocab_size]
 
-    def _forward_reference(self, sv, kv_caches, part_size: int) -> torch.Tensor:
+    def _forward_reference(self, sv, kv_caches, part_size: int, return_hidden: bool = False) -> torch.Tensor:
         """Same math with the fp32 reference ops, one op at a time (CPU path)."""
         a = self.arch
         sh = self.shard
@@ -198,6 +201,8 @@ class DecoderModel:
             ops.linear(mlp, L.down, out=resid, residual=resid if first else None)
             if tp.size > 1:
                 tp.all_reduce(resid)
+        if return_hidden:
+            return resid
         xs = resid.index_select(0, sv.sample_idx.long())
         xn = ops.rmsnorm(xs, self.final_norm, a.rms_eps)
         logits = ops.linear(xn, self.lm_head, out_f32=True)
@@ -221,8 +226,9 @@ class DecoderModel:
 
     # ------------------------------------------------------------- reference
     @torch.no_grad()
-    def reference_logits(self, token_ids: list[int]) -> torch.Tensor:
-        """Dense fp32 forward of one sequence (no KV cache, no custom kernels) -> [len, vocab].
+    def reference_logits(self, token_ids: list[int], return_hidden: bool = False) -> torch.Tensor:
+        """Dense fp32 forward of one sequence (no KV cache, no custom kernels) -> [len, vocab]
+        (or, with ``return_hidden``, the final-RMSNorm hidden states [len, H]).
 
         Used by tests as the oracle for the engine's kernel path (TP=1 only).
         """
@@ -265,5 +271,7 @@ class DecoderModel:
             h = torch.nn.functional.silu(x @ gu[:I].t()) * (x @ gu[I:].t())
             r = r + h @ L.down.dense_weight().float().t()
         x = norm(r, self.final_norm)
+        if return_hidden:
+            return x
         w = self.embed if a.tie_embeddings else self.lm_head.dense_weight()
         return (x @ w.float().t())[:, : a.vocab_size]

@@ -125,6 +125,7 @@ class LLMEngine:
         self.healthy = True
         self.async_sched = bool(cfg.async_scheduling and self.device.type == "cuda" and self.tp.size == 1)
         self._inflight = None  # (batch, handle) of the launched, not yet post-processed step
+        self._calls: collections.deque = collections.deque()  # (fn, future) run on the engine thread
         self.last_error: str | None = None
         self.last_step_wall = time.monotonic()
         log.info("engine ready: model=%s params=%.2fB weights=%.2f GB load=%.1fs kv_blocks=%d (%.1fk tokens) device=%s tp=%d",
@@ -224,11 +225,13 @@ class LLMEngine:
         while self._running:
             with self._cv:
                 while (self._running and not self._inbox and not self._aborts and not self.scheduler.has_work()
-                       and self._inflight is None):
+                       and self._inflight is None and not self._calls):
                     self._cv.wait(timeout=0.5)
                 if not self._running:
                     break
                 self._drain_inbox()
+            if self._calls:
+                self._run_calls()
             try:
                 self.step()
             except Exception as e:  # noqa: BLE001 - engine faults fail every in-flight request
@@ -241,6 +244,55 @@ class LLMEngine:
                     self._finish(seq, "error", notify_sched=False, error=self.last_error)
         if self.tp.size > 1 and self.tp.is_first:
             self._broadcast_header(-1, 0, 0)
+
+    # ------------------------------------------------------------- side calls
+    def _run_calls(self) -> None:
+        """Work that needs the device between steps (embeddings): drain the in-flight step
+        first, since it shares the step-metadata buffers."""
+        self._drain_inflight()
+        while self._calls:
+            fn, fut = self._calls.popleft()
+            try:
+                fut.set_result(fn())
+            except Exception as e:  # noqa: BLE001
+                fut.set_exception(e)
+
+    def call(self, fn, timeout: float = 300.0):
+        """Run ``fn`` on the engine thread (or inline when no loop is running)."""
+        import concurrent.futures
+        if not self._running or threading.current_thread() is self._thread:
+            self._drain_inflight()
+            return fn()
+        fut: concurrent.futures.Future = concurrent.futures.Future()
+        with self._cv:
+            self._calls.append((fn, fut))
+            self._cv.notify()
+        return fut.result(timeout=timeout)
+
+    def embed(self, text: str | None = None, prompt_ids: list[int] | None = None) -> tuple[list[float], int]:
+        """Sentence embedding: L2-normalised mean over tokens of the final-RMSNorm hidden
+        states (prefill only, through scratch KV blocks that are released afterwards).
+        Returns (vector [hidden_size], prompt token count)."""
+        ids = prompt_ids if prompt_ids is not None else self.tokenizer.encode(text or "")
+        ids = (ids or [self.arch.bos_token_id])[: min(self.cfg.max_model_len - 1, self.cfg.max_num_batched_tokens)]
+
+        def run():
+            from vgate.runtime.scheduler import ScheduledBatch
+            seq = Sequence(request_id="__embed__", prompt_ids=list(ids), params=SamplingParams(max_tokens=1))
+            if not self.kvm.ensure(seq, len(ids)):
+                raise RuntimeError("no free KV blocks for the embedding request")
+            try:
+                batch = ScheduledBatch([(seq, len(ids))], len(ids), len(ids), 0, [])
+                hid = self.runner.hidden_states(batch).float()
+                var = hid.pow(2).mean(-1, keepdim=True)
+                xn = hid * torch.rsqrt(var + self.arch.rms_eps) * self.model.final_norm.float()
+                v = xn.mean(0)
+                v = v / v.norm().clamp_min(1e-12)
+                return v.cpu().tolist()
+            finally:
+                self.kvm.free(seq)
+
+        return self.call(run), len(ids)
 
     def run_until_idle(self, max_steps: int = 1_000_000) -> None:
         """Synchronous driver (tests / offline use): process everything queued."""

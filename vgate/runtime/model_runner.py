@@ -240,6 +240,23 @@ class ModelRunner:
         self.gpu_steps += 1
         return self.out_hosts[h.k][: h.ns].tolist()
 
+    @torch.inference_mode()
+    def hidden_states(self, batch: ScheduledBatch) -> torch.Tensor:
+        """Eager prefill of ``batch`` returning the last layer's residual stream [T, H]
+        (embeddings). The caller guarantees no step is in flight (shared metadata buffers)."""
+        ns, nt = len(batch.items), batch.num_tokens
+        if self.gpu:
+            self.meta.select(self._k)
+        else:
+            self.meta.select(0)
+        self._fill(batch, nt, ns)
+        self.meta.upload(ns)
+        view = self.meta.view(nt, ns)
+        view.num_tokens, view.num_seqs = nt, ns
+        view.prev_tokens = None
+        h = self.model.forward(view, self.kv, self.part_size, return_hidden=True)
+        return h[:nt]
+
     def _execute_cpu(self, batch):
         ns, nt = len(batch.items), batch.num_tokens
         self.meta.select(0)
