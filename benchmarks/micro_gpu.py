@@ -159,13 +159,38 @@ def sampler_bench(B=8, V=151936):
     return {"sampler_us": res, "B": B, "V": V}
 
 
+def prefill_sweep():
+    """M > 16: N-split tile kernel (forced, waves=-1) vs the K-split decode kernel family
+    (forced with waves=4), weights cycled through > 512 MB as in sweep()."""
+    for name, N, K, layout, f32 in SHAPES[:4]:
+        w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).bfloat16()
+        ncopy = max(1, math.ceil(512e6 / (N * K * 2)))
+        lins = [ops.Linear(w, layout=layout) for _ in range(ncopy)]
+        cyc = {"i": 0}
+
+        def nxt():
+            cyc["i"] = (cyc["i"] + 1) % ncopy
+            return lins[cyc["i"]]
+        row = {"shape": name}
+        for M in (24, 64, 192, 384, 1024):
+            x = torch.randn(M, K, device="cuda").bfloat16()
+            y = torch.empty(M, lins[0].out_features, device="cuda", dtype=torch.bfloat16)
+            t_tile = graph_time(lambda: ops.linear(x, nxt(), out=y, waves=-1), reps=10, iters=10)
+            t_old = graph_time(lambda: ops.linear(x, nxt(), out=y, waves=4), reps=10, iters=10)
+            row[f"M{M}"] = {"tile_us": round(t_tile, 1), "ksplit_us": round(t_old, 1)}
+        print(json.dumps(row), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--M", type=int, default=8)
-    ap.add_argument("--only", default=None, choices=[None, "attn", "sampler", "gemm"])
+    ap.add_argument("--only", default=None, choices=[None, "attn", "sampler", "gemm", "prefill"])
     a = ap.parse_args()
     print(json.dumps(floor()), flush=True)
+    if a.only == "prefill":
+        prefill_sweep()
+        return
     if a.only == "gemm":
         sweep(a.M, a.quick)
         return

@@ -105,6 +105,13 @@ __device__ __forceinline__ uint4 ld_nt16(const uint4* p) {
   return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
+// plain 16-B load as a value (a uint4 struct assignment from global memory can lower to a
+// memcpy through scratch that SROA does not undo)
+__device__ __forceinline__ uint4 ld16(const void* p) {
+  const u32x4 v = *reinterpret_cast<const u32x4*>(p);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
 // ---- cross-row lane exchange on the VALU (gfx950 v_permlane16/32_swap), no LDS pipe ----
@@ -141,5 +148,12 @@ __device__ __forceinline__ f32x4 ld_sc1_f4(const float* p) {
 }
 // all of this thread's stores have reached the device-coherent level
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Workgroup barrier for LDS hand-offs that leaves global loads in flight: __syncthreads()
+// is a release/acquire fence, which on gfx9 waits vmcnt(0) and so drains every outstanding
+// weight prefetch; this waits only for this wave's LDS traffic (lgkmcnt) and then barriers.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 
 }  // namespace vgate

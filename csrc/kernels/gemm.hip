@@ -537,6 +537,143 @@ __global__ __launch_bounds__(1024) void awq_gemm_kernel(GemmParams p) {
   gemm_finish<MB, NTB, EPI, NORM>(p, acc, ssr, smem, m_base, nt0);
 }
 
+// ---- prefill / medium-M tile GEMM (M > 16, bf16 weights) ----
+// The decode kernels split K across the waves of a block, which is right when x is a
+// few rows; once M grows, every wave would re-load x for its own k-range (the activation
+// requests then outnumber the weight requests). Here the waves of a block split N
+// instead and SHARE one LDS copy of x: block tile = 64 rows x (4 waves x NTW x 16) cols,
+// x staged through a double-buffered LDS ring of KS k-steps (fragment-major, so each
+// lane's B operand is one conflict-free ds_read_b128), weights stream straight to
+// registers (each weight fragment is used by exactly one wave, for 4 m-tiles), software-
+// pipelined one k-step ahead. For M > 64 the grid tiles M (the 256 MB MALL absorbs the
+// repeated weight reads of a prompt-sized M).
+constexpr int TG_WAVES = 4;   // waves per block
+constexpr int TG_MB = 4;      // 16-row m-tiles per block (64 rows)
+constexpr int TG_KS = 8;      // k-steps per LDS stage
+constexpr int TG_STAGE_BYTES = TG_KS * TG_MB * 64 * 16;  // 32 KiB
+
+template <int NTW, int EPI, int NORM>
+__global__ __launch_bounds__(256) void gemm_tile_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint4* xs = reinterpret_cast<uint4*>(smem);  // [2][KS][MB][64] fragments
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int KT = p.K >> 5;
+  // 1-D grid, XCD-aware: consecutive hardware block ids round-robin over the 8 XCDs (own L2
+  // each), so give every XCD one contiguous range of logical tiles, m-chunk fastest — the
+  // m-chunks that share a weight slab then run together on one XCD and read it from HBM once
+  const int mchunks = (p.M + 16 * TG_MB - 1) / (16 * TG_MB);
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int nt0 = ((wgid / mchunks) * TG_WAVES + wid) * NTW;
+  const int m_base = (wgid % mchunks) * 16 * TG_MB;
+  const uint4* wbase[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) wbase[j] = p.wp + ((size_t)(nt0 + j) * KT) * 64 + lane;
+  const bf16_t* nw_ptr = p.norm_w ? p.norm_w + 8 * (lane >> 4) : nullptr;
+  f32x4 acc[TG_MB][NTW];
+#pragma unroll
+  for (int a = 0; a < TG_MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NTW; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ssr[TG_MB];
+#pragma unroll
+  for (int mb = 0; mb < TG_MB; ++mb) ssr[mb] = 0.f;
+
+  // cooperative stage load: 256 threads x 16 B; fragment (kt, mb, l) <- x[row][col..+8]
+  constexpr int STAGE_FRAGS = TG_KS * TG_MB * 64;  // 16-B pieces per stage (2048)
+  // thread t always stages the same x row (fragment f = i*256 + t: lane t&63, m-tile t>>6,
+  // k-step i), so its row pointer is resolved once. Loads are clamped and unconditional (a
+  // guarded load makes the compiler wait vmcnt(0) on it): rows past M repeat row M-1
+  // (masked in the epilogue), k-steps past K are skipped by compute()
+  static_assert(STAGE_FRAGS / 256 == TG_KS && TG_MB == TG_WAVES, "stage mapping");
+  const bf16_t* xrow = p.x + (size_t)row_of(p, min(m_base + wid * 16 + (lane & 15), p.M - 1)) * p.lda +
+                       8 * (lane >> 4);
+  auto load_stage = [&](uint4 (&r)[STAGE_FRAGS / 256], int kt0) {
+#pragma unroll
+    for (int i = 0; i < STAGE_FRAGS / 256; ++i)
+      r[i] = ld16(xrow + min(kt0 + i, KT - 1) * 32);
+  };
+  auto store_stage = [&](const uint4 (&r)[STAGE_FRAGS / 256], int buf) {
+#pragma unroll
+    for (int i = 0; i < STAGE_FRAGS / 256; ++i) xs[buf * STAGE_FRAGS + i * 256 + threadIdx.x] = r[i];
+  };
+  const int nstage = (KT + TG_KS - 1) / TG_KS;
+  // weights: one register group of TG_KS k-steps per x stage, ping-pong (group s+1 is in
+  // flight while stage s computes); issue is unconditional (clamped k index) so the
+  // compiler can keep partial vmcnt waits across the loop
+  auto issue_w = [&](uint4 (&w)[TG_KS][NTW], int st) {
+#pragma unroll
+    for (int u = 0; u < TG_KS; ++u) {
+      const int kt = min(st * TG_KS + u, KT - 1);
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) w[u][j] = ld_nt16(wbase[j] + (size_t)kt * 64);
+    }
+  };
+  auto compute = [&](const uint4 (&w)[TG_KS][NTW], int st) {
+    const int buf = st & 1;
+    const int kt0 = st * TG_KS;
+#pragma unroll
+    for (int ks = 0; ks < TG_KS; ++ks) {
+      if (kt0 + ks < KT) {
+        uint4 xa[TG_MB];
+#pragma unroll
+        for (int mb = 0; mb < TG_MB; ++mb) {
+          xa[mb] = xs[buf * STAGE_FRAGS + (ks * TG_MB + mb) * 64 + lane];
+          if constexpr (NORM) xa[mb] = norm_frag<NORM>(xa[mb], nw_ptr, (kt0 + ks) * 32, ssr[mb]);
+        }
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+#pragma unroll
+          for (int mb = 0; mb < TG_MB; ++mb) acc[mb][j] = mfma16(as_bf16x8(w[ks][j]), as_bf16x8(xa[mb]), acc[mb][j]);
+      }
+    }
+  };
+  {
+    uint4 r[STAGE_FRAGS / 256];
+    load_stage(r, 0);
+    store_stage(r, 0);
+  }
+  uint4 wa[TG_KS][NTW], wb[TG_KS][NTW];
+  issue_w(wa, 0);
+  lds_barrier();
+  for (int st = 0; st < nstage; st += 2) {
+    {
+      uint4 r[STAGE_FRAGS / 256];
+      load_stage(r, (st + 1) * TG_KS);  // x stage st+1 (zeros past K)
+      issue_w(wb, st + 1);
+      compute(wa, st);
+      store_stage(r, (st + 1) & 1);
+      lds_barrier();
+    }
+    if (st + 1 >= nstage) break;
+    {
+      uint4 r[STAGE_FRAGS / 256];
+      load_stage(r, (st + 2) * TG_KS);
+      issue_w(wa, st + 2);
+      compute(wb, st + 1);
+      store_stage(r, st & 1);
+      lds_barrier();
+    }
+  }
+  // epilogue straight from registers: this wave owns rows m_base.. x its NTW tiles
+#pragma unroll
+  for (int mb = 0; mb < TG_MB; ++mb) {
+    const int m = m_base + mb * 16 + (lane & 15);
+    f32x4 v[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) v[j] = acc[mb][j];
+    if constexpr (NORM) {
+      float ss = ssr[mb];
+      ss += xor16(ss);
+      ss += xor32(ss);
+      const float sc = rsqrtf(ss / (float)p.K + p.eps);
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) v[j] *= sc;
+    }
+    if (m < p.M) epilogue<NTW, EPI>(p, v, m, nt0, 4 * (lane >> 4));
+  }
+}
+
 // ------------------------------------------------------------------ host side
 struct Plan { int waves, splitk; };
 
@@ -594,6 +731,24 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
 
 template <int NTB, int EPI, int NORM, bool AWQ>
 static void launch_m(GemmParams p, const GemmArgs& g, hipStream_t st) {
+  if constexpr (!AWQ) {
+    // M > 16: N-split tile kernel with a shared LDS copy of x (see gemm_tile_kernel);
+    // paired epilogues (silu / qkv) keep their tile pairs inside one wave (NTW = 2)
+    const int ntiles = g.N / 16;
+    constexpr int NTW = NTB;
+    const int tblocks = ntiles % (TG_WAVES * NTW) == 0
+                            ? ntiles / (TG_WAVES * NTW) * ((g.M + 16 * TG_MB - 1) / (16 * TG_MB)) : 0;
+    // measured crossover (benchmarks/micro_gpu.py --only prefill, profiles/r1_prefill_gemm.log):
+    // the tile kernel wins once its grid covers half the chip (wide N: gate_up, LM head) or
+    // M >= 128 for any shape; below that, narrow N (qkv / o / down) keeps the K-split
+    // kernels, which spread one matrix over more CUs. waves = -1 forces it (tests, sweeps)
+    const bool tile_wins = tblocks >= 128 || g.M >= 128;
+    if (g.M > 16 && g.splitk <= 0 && tblocks > 0 && (g.waves < 0 || (g.waves == 0 && tile_wins))) {
+      dim3 grid(tblocks), block(64 * TG_WAVES);
+      hipLaunchKernelGGL((gemm_tile_kernel<NTW, EPI, NORM>), grid, block, 2 * TG_STAGE_BYTES, st, p);
+      return;
+    }
+  }
   if (g.M <= 16) launch_one<1, NTB, EPI, NORM, AWQ>(p, g, st);
   else if (g.M <= 32) launch_one<2, NTB, EPI, NORM, AWQ>(p, g, st);
   else launch_one<4, NTB, EPI, NORM, AWQ>(p, g, st);

@@ -455,3 +455,32 @@ def test_gemm_small_batch_activation_packing(M):
                     y = ops.linear(x, lin, out=out, residual=out, waves=waves, splitk=sk)
                     r = ref.linear_ref(x.cpu(), wc, None, r_res.cpu())
                 assert _rel_err(y.float().cpu(), r.float()) < 1e-2, (N, kind, waves, sk)
+
+
+@pytest.mark.parametrize("M", [17, 40, 64, 100, 384])
+def test_gemm_tile_kernel_prefill_shapes(M):
+    """M > 16 with waves=-1 forces the N-split tile kernel (shared LDS copy of x): residual, folded-norm
+    SiLU, f32 + row gather and the QKV epilogue against the fp32 references."""
+    torch.manual_seed(50 + M)
+    K1, N1 = 2240, 1536
+    x = torch.randn(M, K1, device=DEV).bfloat16()
+    w = (torch.randn(N1, K1, device=DEV) / math.sqrt(K1)).bfloat16()
+    r = torch.randn(M, N1, device=DEV).bfloat16()
+    out = r.clone()
+    ops.linear(x, ops.Linear(w), out=out, residual=out, waves=-1)
+    assert _rel_err(out.float().cpu(), ref.linear_ref(x.cpu(), w.cpu(), None, r.cpu()).float()) < 1e-2
+    # folded-norm SiLU (gate_up shape class)
+    H, I = 1536, 1024
+    xh = (torch.randn(M, H, device=DEV) * 2).bfloat16()
+    g = (torch.rand(H, device=DEV) + 0.5).bfloat16()
+    wg = (torch.randn(2 * I, H, device=DEV) / math.sqrt(H)).bfloat16()
+    lin = ops.Linear(wg, kind="silu")
+    lin.fold_norm(g)
+    y = ops.linear(xh, lin, norm=(g, 1e-6), waves=-1)
+    xn, _ = ref.rmsnorm_ref(xh.cpu(), g.cpu(), 1e-6)
+    assert _rel_err(y.float().cpu(), ref.silu_mul_linear_ref(xn, wg[:I].cpu(), wg[I:].cpu()).float()) < 1e-2
+    # f32 logits over a gathered row subset (LM head with > 16 sequences)
+    idx = torch.randperm(M, device=DEV)[: max(17, M // 2)].int()
+    wl = (torch.randn(4096, H, device=DEV) / math.sqrt(H)).bfloat16()
+    lf = ops.linear(xh, ops.Linear(wl), out_f32=True, row_idx=idx, waves=-1)
+    assert _rel_err(lf.cpu(), ref.linear_ref(xh[idx.long()].cpu(), wl.cpu(), out_f32=True)) < 1e-2
