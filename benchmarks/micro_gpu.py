@@ -181,15 +181,71 @@ def prefill_sweep():
         print(json.dumps(row), flush=True)
 
 
+def engine_sweep(M=8, quick=False):
+    """The decode GEMMs exactly as the engine issues them for Qwen2.5-1.5B (folded norm +
+    QKV epilogue on qkv, residual on o/down, folded norm + SiLU on gate_up, folded norm +
+    f32 on the LM head), swept over (waves, splitk); weights cycled through > 512 MB."""
+    from vgate.ops import reference as ref
+    H, I, hq, hkv, D, V = 1536, 8960, 12, 2, 128, 151936
+    eps = 1e-6
+    g = (torch.rand(H, device="cuda") + 0.5).bfloat16()
+    pos = torch.arange(M, dtype=torch.int32, device="cuda") + 40
+    slots = torch.arange(M, dtype=torch.int32, device="cuda") * 16 + 5
+    cs = ref.rope_cos_sin(4096, D, 1e6, device="cuda")
+    kc = torch.zeros(256, hkv, 16, D, device="cuda").bfloat16()
+    vc = torch.zeros_like(kc)
+    shapes = [("qkv", (hq + 2 * hkv) * D, H, "qkv"), ("o_proj", H, hq * D, "plain"),
+              ("gate_up", 2 * I, H, "silu"), ("down", H, I, "plain"), ("lm_head", V, H, "plain")]
+    for name, N, K, layout in shapes:
+        w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).bfloat16()
+        b = (torch.randn(N, device="cuda") * 0.1).bfloat16() if name == "qkv" else None
+        ncopy = max(1, math.ceil(512e6 / (N * K * 2)))
+        lins = []
+        for _ in range(ncopy):
+            lin = ops.Linear(w, bias=b, layout=layout)
+            if name in ("qkv", "gate_up", "lm_head"):
+                lin.fold_norm(g)
+            lins.append(lin)
+        cyc = {"i": 0}
+
+        def nxt():
+            cyc["i"] = (cyc["i"] + 1) % ncopy
+            return lins[cyc["i"]]
+        x = torch.randn(M, K, device="cuda").bfloat16()
+        f32 = name == "lm_head"
+        y = torch.empty(M, lins[0].out_features if name != "qkv" else hq * D, device="cuda",
+                        dtype=torch.float32 if f32 else torch.bfloat16)
+        res = torch.randn(M, N, device="cuda").bfloat16() if name in ("o_proj", "down") else None
+        kw = dict(out=y, residual=res, out_f32=f32)
+        if name in ("qkv", "gate_up", "lm_head"):
+            kw["norm"] = (g, eps)
+        if name == "qkv":
+            kw["qkv"] = dict(positions=pos, slots=slots, cos_sin=cs, k_cache=kc, v_cache=vc, hq=hq, hkv=hkv)
+        rows = []
+        waves = [2, 4, 8] if quick else [1, 2, 4, 8, 16]
+        splits = [1, 2] if name in ("gate_up", "lm_head") else [1, 2, 3, 4, 6, 8]
+        for wv in waves:
+            for sk in splits:
+                t = graph_time(lambda: ops.linear(x, nxt(), waves=wv, splitk=sk, **kw))
+                rows.append({"waves": wv, "splitk": sk, "us": round(t, 2), "TBps": round(N * K * 2 / t / 1e6, 2)})
+        auto = graph_time(lambda: ops.linear(x, nxt(), **kw))
+        best = min(rows, key=lambda r: r["us"])
+        print(json.dumps({"shape": name, "M": M, "auto_us": round(auto, 2), "auto_TBps": round(N * K * 2 / auto / 1e6, 2),
+                          "best": best, "all": rows}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--M", type=int, default=8)
-    ap.add_argument("--only", default=None, choices=[None, "attn", "sampler", "gemm", "prefill"])
+    ap.add_argument("--only", default=None, choices=[None, "attn", "sampler", "gemm", "prefill", "engine"])
     a = ap.parse_args()
     print(json.dumps(floor()), flush=True)
     if a.only == "prefill":
         prefill_sweep()
+        return
+    if a.only == "engine":
+        engine_sweep(a.M, a.quick)
         return
     if a.only == "gemm":
         sweep(a.M, a.quick)

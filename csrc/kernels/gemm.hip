@@ -216,9 +216,19 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
     __syncthreads();
   }
   const int tile = blockIdx.y * gridDim.x + blockIdx.x;
-  if (!NORM && p.splitk > 1) {  // host never splits K under NORM (the row scale needs all of K)
-    // 1) this slice's partial tile -> fp32 slab [tile][slice][SLOTS]
+  if (p.splitk > 1) {
+    // 1) this slice's partial tile -> fp32 slab [tile][slice][SLOTS]; under NORM also the
+    //    slice's per-row partial sum of squares -> [tile][slice][16*MB] after all slabs
+    //    (the row scale is applied to the summed tile: y = rsqrt(sum ss / K + eps) * sum acc)
     f32x4* slab = reinterpret_cast<f32x4*>(p.slabs) + ((size_t)tile * p.splitk + blockIdx.z) * SLOTS;
+    float* ssq_all = p.slabs + (size_t)gridDim.x * gridDim.y * p.splitk * SLOTS * 4;
+    if constexpr (NORM) {
+      if (threadIdx.x < 16 * MB) {
+        float ss = 0.f;
+        for (int w = 0; w < nw; ++w) ss += ssqw[w * 16 * MB + threadIdx.x];
+        st_sc1(ssq_all + ((size_t)tile * p.splitk + blockIdx.z) * 16 * MB + threadIdx.x, ss);
+      }
+    }
     for (int s = threadIdx.x; s < SLOTS; s += blockDim.x) {
       f32x4 t;
       if (nw > 1) {
@@ -257,6 +267,14 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
         f32x4 t = {0.f, 0.f, 0.f, 0.f};
         for (int z = 0; z < p.splitk; ++z) t += ld_sc1_f4(all + ((size_t)z * SLOTS + (mb * NTB + j) * 64 + l) * 4);
         v[j] = t;
+      }
+      if constexpr (NORM) {
+        float ss = 0.f;  // fixed slice order: bit-reproducible
+        for (int z = 0; z < p.splitk; ++z)
+          ss += ld_sc1(ssq_all + ((size_t)tile * p.splitk + z) * 16 * MB + mb * 16 + (l & 15));
+        const float sc = rsqrtf(ss / (float)p.K + p.eps);
+#pragma unroll
+        for (int j = 0; j < NTB; ++j) v[j] *= sc;
       }
       if (m < p.M) epilogue<NTB, EPI>(p, v, m, nt0, 4 * (l >> 4));
     }
@@ -706,8 +724,7 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
   const int mchunks = (g.M + 16 * MB - 1) / (16 * MB);
   const int ksteps = AWQ ? g.K / 128 : g.K / 32;
   Plan pl = plan(nblk, mchunks, ksteps, MB, NTB, g.waves, g.splitk);
-  if (NORM) pl.splitk = 1;  // the deferred row scale needs the whole K range in one block
-  const size_t need_slab = (size_t)nblk * mchunks * pl.splitk * MB * NTB * 64 * 16;
+  const size_t need_slab = (size_t)nblk * mchunks * pl.splitk * (MB * NTB * 64 * 16 + (NORM ? 16 * MB * 4 : 0));
   if (pl.splitk > 1 && (g.slabs == nullptr || need_slab > g.slab_bytes || nblk * mchunks > g.max_counters))
     pl.splitk = 1;  // workspace too small: fall back to one slice (still correct)
   p.splitk = pl.splitk;

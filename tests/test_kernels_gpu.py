@@ -432,6 +432,49 @@ def test_gemm_folded_norm(T):
     assert _rel_err(y3.float().cpu(), ref.silu_mul_linear_ref(xn, w[:1024].cpu(), w[1024:2048].cpu()).float()) < 1e-2
 
 
+@pytest.mark.parametrize("T,splitk,waves", [(8, 2, 4), (8, 4, 2), (3, 3, 8), (16, 4, 4)])
+def test_gemm_norm_splitk(T, splitk, waves):
+    """Deferred RMSNorm under in-launch split-K: each slice publishes its partial sum of
+    squares next to its slab, the last arriver scales the summed tile (gamma in registers,
+    folded gamma, SiLU and the QKV epilogue)."""
+    torch.manual_seed(60 + T + splitk)
+    H, N = 1536, 1024
+    x = (torch.randn(T, H, device=DEV) * 2).bfloat16()
+    g = (torch.rand(H, device=DEV) + 0.5).bfloat16()
+    w = (torch.randn(N, H, device=DEV) / math.sqrt(H)).bfloat16()
+    xn, _ = ref.rmsnorm_ref(x.cpu(), g.cpu(), 1e-6)
+    r = ref.linear_ref(xn, w.cpu())
+    kw = dict(waves=waves, splitk=splitk)
+    y1 = ops.linear(x, ops.Linear(w), norm=(g, 1e-6), **kw)
+    folded = ops.Linear(w)
+    folded.fold_norm(g)
+    y2 = ops.linear(x, folded, norm=(g, 1e-6), **kw)
+    assert _rel_err(y1.float().cpu(), r.float()) < 1e-2
+    assert _rel_err(y2.float().cpu(), r.float()) < 1e-2
+    f3 = ops.Linear(w, kind="silu")
+    f3.fold_norm(g)
+    y3 = ops.linear(x, f3, norm=(g, 1e-6), **kw)
+    assert _rel_err(y3.float().cpu(), ref.silu_mul_linear_ref(xn, w[:512].cpu(), w[512:].cpu()).float()) < 1e-2
+    # QKV epilogue (Qwen2.5-1.5B heads) with the folded norm, as the engine runs it
+    hq, hkv, D, BS = 12, 2, 128, 16
+    wq = (torch.randn((hq + 2 * hkv) * D, H, device=DEV) / math.sqrt(H)).bfloat16()
+    b = (torch.randn(wq.shape[0], device=DEV) * 0.1).bfloat16()
+    pos = torch.randint(0, 1000, (T,), dtype=torch.int32, device=DEV)
+    slots = torch.randperm(32 * BS, device=DEV)[:T].int()
+    cs = ref.rope_cos_sin(1024, D, 1e6, device=DEV)
+    kc = torch.zeros(32, hkv, BS, D, device=DEV).bfloat16()
+    vc = torch.zeros_like(kc)
+    lq = ops.Linear(wq, bias=b, layout="qkv")
+    lq.fold_norm(g)
+    q = ops.linear(x, lq, norm=(g, 1e-6), qkv=dict(positions=pos, slots=slots, cos_sin=cs, k_cache=kc, v_cache=vc,
+                                                     hq=hq, hkv=hkv), **kw)
+    qkv = ref.linear_ref(xn.to(DEV), wq, b)
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    ref.rope_kv_ref(qkv, pos, slots, cs, kc2, vc2, hq, hkv, D)
+    assert _rel_err(q, qkv[:, : hq * D]) < 1e-2
+    assert _rel_err(kc, kc2) < 1e-2 and _rel_err(vc, vc2) < 1e-2
+
+
 @pytest.mark.parametrize("M", [1, 2, 3, 4, 5, 7, 8, 9, 16])
 def test_gemm_small_batch_activation_packing(M):
     """Decode batches <= 4 / <= 8 pack 4 / 2 k-steps of activations per load (DPP unpack)."""
