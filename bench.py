@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import contextlib
 import json
 import os
 import sys
@@ -98,6 +99,9 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool):
     port = args.port + local
     server = uvicorn.Server(uvicorn.Config(app, host="127.0.0.1", port=port, log_level="warning",
                                            access_log=False, lifespan="on"))
+    # the in-process server is stopped by this script, never by a signal: leave the process's
+    # handlers alone (a profiler's native SIGINT/SIGTERM handler is not restorable from Python)
+    server.capture_signals = contextlib.nullcontext
     srv_task = asyncio.create_task(server.serve())
     t_boot = time.perf_counter()
     while not server.started:

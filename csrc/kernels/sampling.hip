@@ -164,7 +164,9 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
 
   // One sweep of this block's segment (8 float4 loads in flight per thread).
   // mode 0: max/Z/argmax + Gumbel; mode 1: acceptance stats for xj + Gumbel restricted to x > xj.
-  auto sweep = [&](int mode, float xj, uint32_t round, Acc& acc) {
+  // `rmx` is the ROW max of pass 0 (the reference of Z): it must not be read from `merged`,
+  // which holds the previous round's acceptance partial (mx = -inf) from round 2 on.
+  auto sweep = [&](int mode, float xj, float rmx, uint32_t round, Acc& acc) {
     for (int v0 = v_lo + tid; v0 < v_hi; v0 += nt * 8) {
       float4 q[8];
 #pragma unroll
@@ -193,7 +195,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
             }
           } else if (v > xj) {
             acc.cnt += 1.f;
-            acc.q += exp2f((v - merged.mx) * c);
+            acc.q += exp2f((v - rmx) * c);
           }
           if (!greedy && (mode == 0 || v > xj) && v > -INFINITY) {
             // accurate logs: a fast log rounding -log(u) to 0 near u = 1 would make an infinite key
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
   };
 
   Acc acc = acc_init();
-  sweep(0, 0.f, 0u, acc);
+  sweep(0, 0.f, 0.f, 0u, acc);
   bool ok = exchange(acc, 1);
   const float mx = merged.mx, z = merged.z;
   int chosen = merged.amx;
@@ -247,7 +249,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
       for (uint32_t round = 1; round <= 64 && j >= 0; ++round) {
         const float xj = x[j];
         Acc st = acc_init();
-        sweep(1, xj, round, st);
+        sweep(1, xj, mx, round, st);
         ++gen;
         ok = exchange(st, gen);
         if (!ok) { j = -1; break; }

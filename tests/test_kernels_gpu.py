@@ -271,6 +271,46 @@ def test_sample_segmented_matches_single_block_and_distribution():
         assert (emp - q.double()).abs().max().item() < 0.07, (kw, emp, q)
 
 
+def _nucleus_probs(row: torch.Tensor, temp: float, top_p: float) -> torch.Tensor:
+    """Exact target of top-p sampling: token j is inside iff the tempered mass strictly
+    above x_j is < top_p (the token crossing top_p is included); renormalised."""
+    p = torch.softmax(row.double() / temp, -1)
+    above = torch.stack([p[row > v].sum() for v in row])
+    keep = above < top_p
+    q = torch.where(keep, p, torch.zeros_like(p))
+    return q / q.sum()
+
+
+@pytest.mark.parametrize("B", [8, 512])
+def test_sample_top_p_frequent_rejection(B):
+    """A flat head with a small nucleus: the first Gumbel candidate is rejected ~70% of the
+    time, so later rejection rounds decide the draw. Their acceptance statistics must be
+    measured against the ROW max of pass 0 (regression: a later round read the previous
+    round's partial and degenerated into the argmax)."""
+    V = 4096
+    hot = torch.tensor([1.0, 0.9, 0.8, 0.7, 0.6, 0.5, 0.4, 0.3, 0.2, 0.1])
+    row = torch.full((V,), -40.0)
+    idx = torch.arange(0, 10) * 397 + 11
+    row[idx] = hot
+    q = _nucleus_probs(row, 1.0, 0.3)
+    allowed = (q > 0).nonzero().flatten()
+    assert 2 <= len(allowed) <= 4
+    L = row.to(DEV).expand(B, V).contiguous()
+    t = torch.ones(B, device=DEV)
+    tp = torch.full((B,), 0.3, device=DEV)
+    counts = torch.zeros(V, dtype=torch.long)
+    reps = max(1, 6000 // B)
+    for off in range(reps):
+        seeds = torch.arange(B, device=DEV, dtype=torch.int64) * 104729 + 17
+        offs = torch.full((B,), off, dtype=torch.int64, device=DEV)
+        out = ops.sample(L, t, top_p=tp, seeds=seeds, offsets=offs)
+        counts += torch.bincount(out.long().cpu(), minlength=V)
+    n = counts.sum().item()
+    assert counts[allowed].sum().item() == n, "sampled outside the nucleus"
+    emp = counts.double() / n
+    assert (emp[allowed] - q[allowed]).abs().max().item() < 0.03, (emp[allowed], q[allowed])
+
+
 def test_sample_logprob():
     torch.manual_seed(9)
     logits = torch.randn(4, 5000, device=DEV)
