@@ -133,23 +133,25 @@ __device__ __forceinline__ bf16x8 softmax_step(f32x4& s0, f32x4& s1, float& m, f
   return pack_p(s0, s1);
 }
 
-// LDS: max(one V image per decode wave, prefill double buffer)
+// LDS: max(decode: one V image (then o partial) per wave + (m, l) + flag, prefill double buffer)
 __host__ __device__ constexpr int attn_lds_bytes(int nw) {
-  return nw * CHUNK * D_ * 2 > 2 * CHUNK * D_ * 2 ? nw * CHUNK * D_ * 2 : 2 * CHUNK * D_ * 2;
+  return nw * CHUNK * D_ * 2 + nw * 32 * 4 + 16 > 2 * CHUNK * D_ * 2 ? nw * CHUNK * D_ * 2 + nw * 32 * 4 + 16
+                                                                     : 2 * CHUNK * D_ * 2;
 }
 
 // ---------------------------------------------------------------- decode ----
-// ONE WAVE per (sequence, KV head, partition): the wave walks its partition's 32-token
-// chunks itself, so no cross-wave merge (measured 3 us of LDS traffic + barriers per
-// launch for the split-across-waves form) and no block barrier anywhere on this path
-// (waves exit independently). The next chunk's K fragments are prefetched while the
-// current chunk computes; V is loaded at the top of its chunk and lands while QK^T and
-// the softmax run. Query columns = the G = Hq/Hkv heads sharing the KV head. Partitions
-// of one (sequence, head) are merged by the last-arriving wave (sc1 hand-off + ticket).
+// ONE WORKGROUP per (sequence, KV head, partition); its nw waves take the partition's
+// 32-token chunks round-robin (chunk c -> wave c % nw), so a short context has every chunk's
+// K/V loads in flight at once (one HBM round trip instead of one per chunk: a single wave is
+// latency-bound at ~16 KB per round trip, MI355X_MICROARCH.md handoff-payload). Each wave
+// keeps its own online-softmax state; the waves' (m, l, o) are merged through LDS (the o
+// partials reuse each wave's V image). Query columns = the G = Hq/Hkv heads sharing the KV
+// head. Partitions of one (sequence, head) — contexts longer than part_size — are merged
+// by the last-arriving block (sc1 hand-off + ticket, no second launch).
 // Only sequences with a single new query token are decode work.
 #define ATTN_STAMP(i)                                                                          \
   do {                                                                                         \
-    if (a.dbg_ts != nullptr && lane == 0 && s == 0 && h == 0 && part == 0)                     \
+    if (a.dbg_ts != nullptr && threadIdx.x == 0 && s == 0 && h == 0 && part == 0)              \
       a.dbg_ts[i] = __builtin_amdgcn_s_memtime();                                              \
   } while (0)
 
@@ -162,19 +164,21 @@ __device__ __forceinline__ void load_k_regs(uint4 (&kf)[8], const bf16_t* kb0, c
   for (int kk = 0; kk < 4; ++kk) kf[4 + kk] = *reinterpret_cast<const uint4*>(k1 + 32 * kk);
 }
 
-__device__ __forceinline__ void decode_wave(const AttnArgs& a, int s, int h, int part, bf16_t* vl, int* lds_flag) {
-  const int lane = threadIdx.x & 63;
+// LDS of a decode block: [nw][CHUNK * D_] bf16 V images (then the waves' fp32 o partials,
+// 16 cols x 128 d = the same 8 KiB) | [nw][16][2] (m, l) | flag
+__host__ __device__ constexpr int dec_ml_off(int nw) { return nw * CHUNK * D_ * 2; }
+
+__device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, int part, char* smem) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   ATTN_STAMP(0);
-  if (a.dbg_ts != nullptr && lane == 0 && s == 0 && h == 0 && part == 0) a.dbg_ts[6] = __builtin_amdgcn_s_memrealtime();
   const int pstart = part * a.part_size;
   const int* bt = a.block_tables + (size_t)s * a.max_blocks;
-  // every independent load of the dependency chain up front
+  // every independent load of the dependency chain up front: context length, query
+  // bounds, the partition's block-table window (one entry per lane: chunk addresses come
+  // from v_readlane, never from a per-chunk global load) and the query fragments
   const int ctx = a.context_lens[s];
   const int qbeg = a.query_start ? a.query_start[s] : s;
   const int qend = a.query_start ? a.query_start[s + 1] : s + 1;
-  // the partition's block-table entries, one per lane (part_size <= 1024 tokens): chunk
-  // addresses come from v_readlane, never from a per-chunk global load (whose wait would
-  // also drain the prefetched K/V and re-serialise the chunk loop)
   const int btv = bt[min(pstart / BS_ + lane, a.max_blocks - 1)];
   const int G = a.Hq / a.Hkv;
   const int col = lane & 15;
@@ -185,139 +189,165 @@ __device__ __forceinline__ void decode_wave(const AttnArgs& a, int s, int h, int
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) qf[kk] = cok ? *reinterpret_cast<const uint4*>(qp + 32 * kk) : make_uint4(0, 0, 0, 0);
   }
-  if (ctx <= 0 || pstart >= ctx || qend - qbeg != 1) return;
+  if (ctx <= 0 || pstart >= ctx || qend - qbeg != 1) return;  // block-uniform
   ATTN_STAMP(1);
   const int pend = min(ctx, pstart + a.part_size);
   const int nparts = (ctx + a.part_size - 1) / a.part_size;
   const int nch = (pend - pstart + CHUNK - 1) / CHUNK;
+  const int myn = nch > wid ? (nch - wid + nw - 1) / nw : 0;  // chunks wid, wid + nw, ...
   const size_t head_off = (size_t)h * BS_ * D_;
   const size_t blk_stride = (size_t)a.Hkv * BS_ * D_;
   const float cscale = a.scale * LOG2E;
+  bf16_t* vl = reinterpret_cast<bf16_t*>(smem) + wid * (CHUNK * D_);
   float m = -INFINITY, l = 0.f;
   f32x4 o[8];
 #pragma unroll
   for (int mt = 0; mt < 8; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // chunk c covers tokens [tb, tb + 32) = cache blocks (b0, b1). Two register sets
-  // ping-pong: chunk c+1's K/V loads are issued before chunk c is consumed, and nothing
-  // copies between the sets, so the wait for chunk c is a partial vmcnt that leaves
-  // chunk c+1 in flight (a copy would force vmcnt(0) and re-serialise every chunk).
-  auto issue = [&](uint4 (&kf)[8], uint4 (&vr)[8], int c) {
+  // j-th chunk of this wave covers tokens [tb, tb + 32) = cache blocks (b0, b1). Two
+  // register sets ping-pong: chunk j+1's K/V loads are issued before chunk j is consumed.
+  auto issue = [&](uint4 (&kf)[8], uint4 (&vr)[8], int j) {
+    const int c = wid + j * nw;
     const int tb = pstart + c * CHUNK;
     const int n0 = __builtin_amdgcn_readlane(btv, 2 * c);
     const int n1 = (tb + BS_ < pend) ? __builtin_amdgcn_readlane(btv, 2 * c + 1) : n0;
     load_k_regs(kf, a.k_cache + (size_t)n0 * blk_stride + head_off, a.k_cache + (size_t)n1 * blk_stride + head_off, lane);
     load_v_regs(vr, a.v_cache + (size_t)n0 * blk_stride + head_off, a.v_cache + (size_t)n1 * blk_stride + head_off, lane);
   };
-  // profiling: chunk-1 sub-phase stamps (each after forcing its results), dbg mode only
-  const bool prof = a.dbg_ts != nullptr && s == 0 && h == 0 && part == 0;
-  auto pstamp = [&](int i, float dep) {
-    if (prof) {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\tv_mov_b32 %0, %0" : "+v"(dep)::"memory");
-      if (lane == 0) a.dbg_ts[i] = __builtin_amdgcn_s_memtime();
-    }
-  };
-  auto consume = [&](const uint4 (&kf)[8], const uint4 (&vr)[8], int c) {
-    const int tb = pstart + c * CHUNK;
-    if (c == 1) pstamp(8, __uint_as_float(kf[7].x ^ vr[7].x));
+  auto consume = [&](const uint4 (&kf)[8], const uint4 (&vr)[8], int j) {
+    const int tb = pstart + (wid + j * nw) * CHUNK;
     f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) s0 = mfma16(as_bf16x8(kf[kk]), as_bf16x8(qf[kk]), s0);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) s1 = mfma16(as_bf16x8(kf[4 + kk]), as_bf16x8(qf[kk]), s1);
-    if (c == 1) pstamp(9, s0[0] + s1[3]);
     const bf16x8 pb = softmax_step(s0, s1, m, l, o, tb, pend, cscale, lane);
-    if (c == 1) pstamp(10, (float)pb[0] + o[7][3]);
     // rows past the context hold finite cache contents (the pool is zero-initialised)
     // and meet p = 0: stored unmasked
     store_v_lds(vl, vr, lane, CHUNK);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (c == 1) pstamp(11, 0.f);
     pv_update(o, vl, pb, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (c == 1) pstamp(12, o[0][0] + o[7][3]);
   };
-  // Loads are issued UNCONDITIONALLY (a chunk index past the end re-reads the last chunk):
-  // with straight-line issue the compiler can count outstanding loads across the loop
-  // back-edge and emit partial vmcnt waits; a conditional issue makes it drain to 0.
-  uint4 ka[8], va[8], kb[8], vb[8];
-  issue(ka, va, 0);
-  for (int c = 0; c < nch; c += 2) {
-    issue(kb, vb, min(c + 1, nch - 1));
-    consume(ka, va, c);
-    issue(ka, va, min(c + 2, nch - 1));
-    if (c + 1 < nch) consume(kb, vb, c + 1);
+  if (myn > 0) {
+    // Loads are issued UNCONDITIONALLY (an index past the end re-reads the last chunk):
+    // straight-line issue lets the compiler keep partial vmcnt waits across the back-edge.
+    uint4 ka[8], va[8], kb[8], vb[8];
+    issue(ka, va, 0);
+    for (int j = 0; j < myn; j += 2) {
+      issue(kb, vb, min(j + 1, myn - 1));
+      consume(ka, va, j);
+      issue(ka, va, min(j + 2, myn - 1));
+      if (j + 1 < myn) consume(kb, vb, j + 1);
+    }
+    l += xor16(l);
+    l += xor32(l);
   }
-  l += xor16(l);
-  l += xor32(l);
   ATTN_STAMP(2);
-  const int g = lane >> 4;
-  const float inv = l > 0.f ? 1.f / l : 0.f;
-  const int hq = h * G + col;
-  if (nparts == 1) {
-    if (cok) {
-      bf16_t* op = a.out + (size_t)qbeg * a.out_stride + (size_t)hq * D_;
+  // ---- merge the waves through LDS: o partial [w][col][d] fp32 over the wave's V image
+  float* opart = reinterpret_cast<float*>(smem);
+  float* mlp = reinterpret_cast<float*>(smem + dec_ml_off(nw));
+  int* flag = reinterpret_cast<int*>(mlp + nw * 32);
+  {
+    float* ow = opart + wid * (16 * D_);
+    const int g = lane >> 4;
 #pragma unroll
-      for (int mt = 0; mt < 8; ++mt) {
-        uint2 pk;
-        pk.x = pack_bf2(o[mt][0] * inv, o[mt][1] * inv);
-        pk.y = pack_bf2(o[mt][2] * inv, o[mt][3] * inv);
-        *reinterpret_cast<uint2*>(op + 16 * mt + 4 * g) = pk;
+    for (int mt = 0; mt < 8; ++mt) *reinterpret_cast<f32x4*>(ow + col * D_ + 16 * mt + 4 * g) = o[mt];
+    if (lane < 16) {
+      mlp[(wid * 16 + lane) * 2] = m;
+      mlp[(wid * 16 + lane) * 2 + 1] = l;
+    }
+  }
+  __syncthreads();
+  // one thread per (query column, 8 d): rescale and sum the waves' partials
+  const int items = G * 16;
+  float M = -INFINITY, L = 0.f;
+  float acc[8];
+  const int it = threadIdx.x;
+  const int icol = it >> 4, d0 = (it & 15) * 8;
+  if (it < items) {
+    for (int w = 0; w < nw; ++w) M = fmaxf(M, mlp[(w * 16 + icol) * 2]);
+    const float Mref = M == -INFINITY ? 0.f : M;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int w = 0; w < nw; ++w) {
+      const float wl = mlp[(w * 16 + icol) * 2 + 1];
+      if (!(wl > 0.f)) continue;
+      const float e = __builtin_amdgcn_exp2f(mlp[(w * 16 + icol) * 2] - Mref);
+      L += wl * e;
+      const float* src = opart + w * (16 * D_) + icol * D_ + d0;
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(src), v1 = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[j] += e * v0[j];
+        acc[4 + j] += e * v1[j];
       }
     }
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  const int hq = h * G + icol;
+  if (nparts == 1) {
+    if (it < items) {
+      uint4 pk;
+      pk.x = pack_bf2(acc[0] * inv, acc[1] * inv);
+      pk.y = pack_bf2(acc[2] * inv, acc[3] * inv);
+      pk.z = pack_bf2(acc[4] * inv, acc[5] * inv);
+      pk.w = pack_bf2(acc[6] * inv, acc[7] * inv);
+      *reinterpret_cast<uint4*>(a.out + (size_t)qbeg * a.out_stride + (size_t)hq * D_ + d0) = pk;
+    }
     ATTN_STAMP(3);
-    if (a.dbg_ts != nullptr && lane == 0 && s == 0 && h == 0 && part == 0) a.dbg_ts[7] = __builtin_amdgcn_s_memrealtime();
     return;
   }
-  // partial (normalised o, running max m, sum l) by device-coherent stores
-  if (cok) {
-    float* po = a.part_o + (((size_t)s * a.Hq + hq) * a.num_parts + part) * D_;
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt)
-      st_sc1_f4(po + 16 * mt + 4 * g, o[mt][0] * inv, o[mt][1] * inv, o[mt][2] * inv, o[mt][3] * inv);
-    if (g == 0) {
+  // partial (normalised o, running max M, sum L) by device-coherent stores
+  if (it < items) {
+    float* po = a.part_o + (((size_t)s * a.Hq + hq) * a.num_parts + part) * D_ + d0;
+    st_sc1_f4(po, acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
+    st_sc1_f4(po + 4, acc[4] * inv, acc[5] * inv, acc[6] * inv, acc[7] * inv);
+    if ((it & 15) == 0) {
       float* pm = a.part_ml + (((size_t)s * a.Hq + hq) * a.num_parts + part) * 2;
-      st_sc1(pm, m);
-      st_sc1(pm + 1, l);
+      st_sc1(pm, M);
+      st_sc1(pm + 1, L);
     }
   }
   if (a.tickets == nullptr) return;  // separate reduce launch
   drain_stores();
-  int last = 0;
-  if (lane == 0) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
     uint32_t* t = a.tickets + (size_t)s * a.Hkv + h;
     const uint32_t old = __hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = old == (uint32_t)(nparts - 1);
+    const int last = old == (uint32_t)(nparts - 1);
     if (last) __hip_atomic_store(t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
   }
-  last = __shfl(last, 0, 64);
-  if (!last) return;
-  // last arriver: merge the nparts partials of the G heads (64 lanes x G*32 float4 outputs)
-  for (int idx = lane; idx < G * (D_ / 4); idx += 64) {
+  __syncthreads();
+  if (!*flag) return;
+  // last arriver: merge the nparts partials of the G heads (one thread per (head, 4 d))
+  for (int idx = threadIdx.x; idx < G * (D_ / 4); idx += blockDim.x) {
     const int hh = h * G + idx / (D_ / 4);
-    const int d0 = (idx % (D_ / 4)) * 4;
+    const int dd = (idx % (D_ / 4)) * 4;
     const float* pm = a.part_ml + ((size_t)s * a.Hq + hh) * a.num_parts * 2;
-    const float* po = a.part_o + ((size_t)s * a.Hq + hh) * a.num_parts * D_ + d0;
-    float M = -INFINITY;
-    for (int p = 0; p < nparts; ++p) M = fmaxf(M, ld_sc1(pm + 2 * p));
-    float L = 0.f, acc[4] = {0.f, 0.f, 0.f, 0.f};
+    const float* po = a.part_o + ((size_t)s * a.Hq + hh) * a.num_parts * D_ + dd;
+    float MM = -INFINITY;
+    for (int p = 0; p < nparts; ++p) MM = fmaxf(MM, ld_sc1(pm + 2 * p));
+    float LL = 0.f, r[4] = {0.f, 0.f, 0.f, 0.f};
     for (int p = 0; p < nparts; ++p) {
-      const float w = ld_sc1(pm + 2 * p + 1) * exp2f(ld_sc1(pm + 2 * p) - M);
+      const float w = ld_sc1(pm + 2 * p + 1) * exp2f(ld_sc1(pm + 2 * p) - MM);
       const f32x4 v = ld_sc1_f4(po + (size_t)p * D_);
-      L += w;
-      acc[0] += w * v[0]; acc[1] += w * v[1]; acc[2] += w * v[2]; acc[3] += w * v[3];
+      LL += w;
+      r[0] += w * v[0]; r[1] += w * v[1]; r[2] += w * v[2]; r[3] += w * v[3];
     }
-    const float iv = L > 0.f ? 1.f / L : 0.f;
-    bf16_t* op = a.out + (size_t)qbeg * a.out_stride + (size_t)hh * D_ + d0;
+    const float iv = LL > 0.f ? 1.f / LL : 0.f;
+    bf16_t* op = a.out + (size_t)qbeg * a.out_stride + (size_t)hh * D_ + dd;
     uint2 pk;
-    pk.x = pack_bf2(acc[0] * iv, acc[1] * iv);
-    pk.y = pack_bf2(acc[2] * iv, acc[3] * iv);
+    pk.x = pack_bf2(r[0] * iv, r[1] * iv);
+    pk.y = pack_bf2(r[2] * iv, r[3] * iv);
     *reinterpret_cast<uint2*>(op) = pk;
   }
 }
 
 // Combine split-K partitions: grid (S, Hq), block 128 (one thread per d).
 __global__ __launch_bounds__(128) void attn_decode_reduce_kernel(AttnArgs a) {
+  TLScope tl_scope(a.tl);
   const int s = blockIdx.x, hq = blockIdx.y, d = threadIdx.x;
   const int ctx = a.context_lens[s];
   if (ctx <= 0) return;
@@ -419,7 +449,7 @@ __device__ __forceinline__ void prefill_body(const AttnArgs& a, int tile, int h,
 }
 
 // ------------------------------------------------------------- unified launch ----
-// grid.x = [decode blocks: nw waves each, wave = unit (partition-major: unit = p*S + s)]
+// grid.x = [decode blocks: one per (sequence, partition), partition-major: bx = p*S + s]
 //          ++ [prefill tiles], grid.y = KV heads. One launch serves a decode-only,
 // prefill-only or mixed (chunked-prefill) step; waves / blocks without work exit.
 // MAXT: 512 threads (G <= 8 query heads per KV head) leaves 256 VGPRs per wave for the
@@ -427,13 +457,10 @@ __device__ __forceinline__ void prefill_body(const AttnArgs& a, int tile, int h,
 template <int MAXT>
 __global__ __launch_bounds__(MAXT) void attn_kernel(AttnArgs a, int dec_seqs, int dec_blocks) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  TLScope tl_scope(a.tl);
   const int bx = blockIdx.x;
   if (bx < dec_blocks) {
-    const int wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const int unit = bx * nw + wid;
-    if (unit >= dec_seqs * a.num_parts) return;
-    decode_wave(a, unit % dec_seqs, blockIdx.y, unit / dec_seqs,
-                reinterpret_cast<bf16_t*>(smem) + wid * (CHUNK * D_), nullptr);
+    decode_block(a, bx % dec_seqs, blockIdx.y, bx / dec_seqs, smem);  // block = (sequence, partition)
   } else {
     prefill_body(a, bx - dec_blocks, blockIdx.y, smem);
   }
@@ -447,16 +474,19 @@ static int attn_waves(const AttnArgs& a) {
 void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
   const int tiles = a.num_tiles > 0 ? a.num_tiles : 0;
   const int nw = attn_waves(a);
-  const int units = dec_seqs > 0 ? dec_seqs * a.num_parts : 0;
-  const int dec_blocks = (units + nw - 1) / nw;
+  const int dec_blocks = dec_seqs > 0 ? dec_seqs * a.num_parts : 0;
   const int nx = dec_blocks + tiles;
   if (nx <= 0) return;
+  AttnArgs b = a;
+  b.tl = tl_take("attention", nx * a.Hkv);
   if (nw <= 8)
-    hipLaunchKernelGGL(attn_kernel<512>, dim3(nx, a.Hkv, 1), dim3(64 * nw), attn_lds_bytes(nw), st, a, dec_seqs, dec_blocks);
+    hipLaunchKernelGGL(attn_kernel<512>, dim3(nx, a.Hkv, 1), dim3(64 * nw), attn_lds_bytes(nw), st, b, dec_seqs, dec_blocks);
   else
-    hipLaunchKernelGGL(attn_kernel<1024>, dim3(nx, a.Hkv, 1), dim3(64 * nw), attn_lds_bytes(nw), st, a, dec_seqs, dec_blocks);
-  if (dec_seqs > 0 && a.num_parts > 1 && a.tickets == nullptr)
-    hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(dec_seqs, a.Hq), dim3(128), 0, st, a);
+    hipLaunchKernelGGL(attn_kernel<1024>, dim3(nx, a.Hkv, 1), dim3(64 * nw), attn_lds_bytes(nw), st, b, dec_seqs, dec_blocks);
+  if (dec_seqs > 0 && a.num_parts > 1 && a.tickets == nullptr) {
+    b.tl = tl_take("attn_reduce", dec_seqs * a.Hq);
+    hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(dec_seqs, a.Hq), dim3(128), 0, st, b);
+  }
 }
 
 void launch_attn_decode(const AttnArgs& a, hipStream_t st) {

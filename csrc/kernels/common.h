@@ -157,3 +157,26 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 }  // namespace vgate
+
+// ---- launch timeline (profiling, benchmarks/timeline.py) ----
+// A kernel that receives a non-null `tl` stamps its block's [start, end] with the 100 MHz
+// s_memrealtime clock at tl[2 * bid] / tl[2 * bid + 1]: start by thread 0 on entry, end as
+// the max over the block's waves on every exit path (destructor). The host carves `tl` out
+// of one device buffer per launch (tl_take), so a captured hipGraph keeps its slots and
+// every replay rewrites them: inter-kernel gaps = next kernel's first start - last end.
+struct TLScope {
+  unsigned long long* p;
+  __device__ __forceinline__ explicit TLScope(unsigned long long* tl) {
+    p = nullptr;
+    if (tl != nullptr) {
+      const size_t bid = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+      p = tl + 2 * bid;
+      if (threadIdx.x == 0) p[0] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  __device__ __forceinline__ ~TLScope() {
+    if (p != nullptr && (threadIdx.x & 63) == 0)
+      __hip_atomic_fetch_max(p + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  }
+};

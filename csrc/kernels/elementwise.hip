@@ -83,7 +83,8 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int32_t* __restric
                                                          const int32_t* __restrict__ prev,
                                                          const bf16_t* __restrict__ table,
                                                          bf16_t* __restrict__ out, int H,
-                                                         int vstart, int vrows) {
+                                                         int vstart, int vrows, unsigned long long* tl) {
+  TLScope tl_scope(tl);
   const int t = blockIdx.x;
   int tok = ids[t];
   if (tok < 0 && prev != nullptr) tok = prev[-tok - 1];
@@ -97,7 +98,8 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int32_t* __restric
 void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int T, int H,
                       int vstart, int vrows, hipStream_t st, const int32_t* prev) {
   if (T <= 0) return;
-  hipLaunchKernelGGL(embedding_kernel, dim3(T), dim3(256), 0, st, ids, prev, table, out, H, vstart, vrows);
+  hipLaunchKernelGGL(embedding_kernel, dim3(T), dim3(256), 0, st, ids, prev, table, out, H, vstart, vrows,
+                     tl_take("embedding", T));
 }
 
 // One workgroup per token. Work items:
@@ -170,6 +172,32 @@ void launch_rope_kv(uint16_t* qkv, const int32_t* positions, const int32_t* slot
   if (T <= 0) return;
   hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(256), 0, st, qkv, positions, slots, cos_sin,
                      k_cache, v_cache, Hq, Hkv, D, BS);
+}
+
+// Read-only sweep of a byte range with the DEFAULT cache policy (not nt): the lines land in
+// the memory-side Infinity Cache (MALL, 256 MB) so a later non-temporal weight stream of the
+// same bytes hits there instead of HBM. Used on latency-bound phases (attention, small GEMMs)
+// whose HBM is otherwise idle. Nothing is written (the sink test is never true).
+__global__ __launch_bounds__(256) void prefetch_kernel(const uint4* __restrict__ p, size_t n16, uint32_t* sink,
+                                                        unsigned long long* tl) {
+  TLScope tl_scope(tl);
+  uint32_t acc = 0;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const uint4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
+    acc ^= a.x ^ b.y ^ c.z ^ d.w;
+  }
+  for (; i < n16; i += stride) acc ^= p[i].x;
+  if (acc == 0x9E3779B9u && sink != nullptr) *sink = acc;
+}
+
+void launch_prefetch(const void* p, size_t bytes, int blocks, hipStream_t st) {
+  const size_t n16 = bytes / 16;
+  if (n16 == 0) return;
+  if (blocks <= 0) blocks = 256;
+  hipLaunchKernelGGL(prefetch_kernel, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const uint4*>(p), n16,
+                     nullptr, tl_take("prefetch", blocks));
 }
 
 }  // namespace vgate

@@ -342,8 +342,7 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
   constexpr int R = 16 / XP;  // real rows per packed load
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const size_t bid = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-  if (p.dbg_ts != nullptr && threadIdx.x == 0) p.dbg_ts[2 * bid] = __builtin_amdgcn_s_memrealtime();
+  TLScope tl_scope(p.dbg_ts);
   const int KT = p.K >> 5;
   const int nt0 = blockIdx.x * NTB;
   const int m_base = blockIdx.y * 16 * MB;
@@ -485,7 +484,6 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
     }
   }
   gemm_finish<MB, NTB, EPI, NORM>(p, acc, ssr, smem, m_base, nt0);
-  if (p.dbg_ts != nullptr && threadIdx.x == 0) p.dbg_ts[2 * bid + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ---- AWQ W4A16 ----
@@ -499,6 +497,7 @@ __device__ __forceinline__ bf16x8 dq8(uint32_t q, float s, float sz) {
 template <int MB, int NTB, int EPI, int NORM>
 __global__ __launch_bounds__(1024) void awq_gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  TLScope tl_scope(p.dbg_ts);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int KQ = p.K >> 7;
   const int nt0 = blockIdx.x * NTB;
@@ -573,6 +572,7 @@ constexpr int TG_STAGE_BYTES = TG_KS * TG_MB * 64 * 16;  // 32 KiB
 template <int NTW, int EPI, int NORM>
 __global__ __launch_bounds__(256) void gemm_tile_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  TLScope tl_scope(p.dbg_ts);
   uint4* xs = reinterpret_cast<uint4*>(smem);  // [2][KS][MB][64] fragments
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int KT = p.K >> 5;
@@ -730,6 +730,9 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
   p.splitk = pl.splitk;
   const size_t lds = red_bytes<MB, NTB>(pl.waves) + ssq_bytes<MB>(pl.waves) + 16;
   dim3 grid(nblk, mchunks, pl.splitk), block(64 * pl.waves);
+  if (p.dbg_ts == nullptr)
+    p.dbg_ts = tl_take(AWQ ? "awq_gemm" : (EPI == EPI_QKV ? "gemm_qkv" : EPI == EPI_SILU ? "gemm_gate_up"
+                                            : EPI == EPI_F32 ? "gemm_f32" : "gemm"), nblk * mchunks * pl.splitk);
   if constexpr (AWQ)
     hipLaunchKernelGGL((awq_gemm_kernel<MB, NTB, EPI, NORM>), grid, block, lds, st, p);
   else if constexpr (MB == 1) {
@@ -762,6 +765,7 @@ static void launch_m(GemmParams p, const GemmArgs& g, hipStream_t st) {
     const bool tile_wins = tblocks >= 128 || g.M >= 128;
     if (g.M > 16 && g.splitk <= 0 && tblocks > 0 && (g.waves < 0 || (g.waves == 0 && tile_wins))) {
       dim3 grid(tblocks), block(64 * TG_WAVES);
+      if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("gemm_tile", tblocks);
       hipLaunchKernelGGL((gemm_tile_kernel<NTW, EPI, NORM>), grid, block, 2 * TG_STAGE_BYTES, st, p);
       return;
     }

@@ -47,6 +47,17 @@ struct GemmArgs {
   unsigned long long* dbg_ts;
 };
 void launch_gemm(const GemmArgs& g, hipStream_t st);
+
+// ---- launch timeline (profiling; csrc/runtime/timeline.cpp, benchmarks/timeline.py) ----
+// While a timeline is active every launcher takes 2 x blocks u64 stamps for its kernel
+// (TLScope in common.h) and records (name, offset, blocks); null when inactive or full.
+unsigned long long* tl_take(const char* name, int nblocks);
+void tl_start(unsigned long long* base, int64_t capacity);
+int64_t tl_stop();
+int tl_count();
+const char* tl_name(int i);
+int64_t tl_offset(int i);
+int tl_blocks(int i);
 void launch_awq_gemm(const GemmArgs& g, hipStream_t st);
 
 // y = rmsnorm(x) * w ; if res != null: res = x + res (in place) and the norm is of the sum.
@@ -56,6 +67,9 @@ void launch_rmsnorm(const uint16_t* x, int ldx, uint16_t* res, int ldres, const 
 // Embedding gather with vocab-shard masking (TP): rows outside [vstart, vstart+vrows) -> 0.
 void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int T, int H,
                       int vstart, int vrows, hipStream_t st, const int32_t* prev = nullptr);
+
+// Default-policy read sweep of [p, p + bytes) over `blocks` workgroups (MALL warm-up).
+void launch_prefetch(const void* p, size_t bytes, int blocks, hipStream_t st);
 
 // NeoX RoPE on q,k inside the fused qkv buffer + paged KV-cache write.
 // qkv: [T, (Hq + 2*Hkv) * D]; cos_sin: [max_pos, D] f32 (cos | sin halves)
@@ -95,6 +109,7 @@ struct AttnArgs {
   uint32_t* tickets;
   // profiling only: phase timestamps (s_memtime) of block (0,0,0) wave 0, or null
   unsigned long long* dbg_ts;
+  unsigned long long* tl;  // launch timeline slot (set by the launcher), or null
 };
 void launch_attn_decode(const AttnArgs& a, hipStream_t st);
 void launch_attn_prefill(const AttnArgs& a, hipStream_t st);
@@ -117,6 +132,7 @@ struct SampleArgs {
   // segmented (multi-block per row) mode; null -> one block per row
   float* parts;              // [B * nseg][8] partials (B * nseg <= 256)
   uint32_t* sync;            // [2 * B] zero-initialised, self-resetting row counters
+  unsigned long long* tl;    // launch timeline slot (set by the launcher), or null
 };
 void launch_sample(const SampleArgs& s, hipStream_t st);
 int sample_segments(int B, int V);

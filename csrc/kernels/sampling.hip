@@ -139,6 +139,7 @@ __device__ __forceinline__ bool row_meet(uint32_t* ctr, uint32_t target, int* ok
 }
 
 __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
+  TLScope tl_scope(a.tl);
   __shared__ Acc red[SAMPLE_THREADS / 64];
   __shared__ Acc merged;
   __shared__ int ok_flag;
@@ -294,7 +295,9 @@ void launch_sample(const SampleArgs& s, hipStream_t st) {
   if (s.B <= 0) return;
   int nseg = sample_segments(s.B, s.V);
   if (s.parts == nullptr || s.sync == nullptr) nseg = 1;
-  hipLaunchKernelGGL(sample_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, s);
+  SampleArgs a = s;
+  a.tl = tl_take("sample", nseg * s.B);
+  hipLaunchKernelGGL(sample_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, a);
 }
 
 }  // namespace vgate

@@ -311,6 +311,27 @@ void sample(const Tensor& logits, const c10::optional<Tensor>& temperature,
   vgate::launch_sample(s, cur_stream());
 }
 
+// Warm the memory-side cache with a tensor's bytes (default-policy read sweep, nothing written).
+void prefetch(const Tensor& t, int64_t blocks) {
+  CHECK_DEV(t);
+  TORCH_CHECK(t.is_contiguous(), "prefetch: contiguous tensor");
+  c10::DeviceGuard guard(t.device());
+  vgate::launch_prefetch(t.data_ptr(), (size_t)t.numel() * t.element_size(), (int)blocks, cur_stream());
+}
+
+// Launch timeline (profiling): every launch while active takes 2 x blocks u64 stamps of buf.
+void timeline_start(Tensor& buf) {
+  CHECK_DEV(buf); CHECK_DT(buf, torch::kInt64);
+  TORCH_CHECK(buf.is_contiguous(), "timeline buffer must be contiguous");
+  vgate::tl_start(reinterpret_cast<unsigned long long*>(buf.data_ptr()), buf.numel());
+}
+
+std::vector<std::tuple<std::string, int64_t, int64_t>> timeline_entries() {
+  std::vector<std::tuple<std::string, int64_t, int64_t>> r;
+  for (int i = 0; i < vgate::tl_count(); ++i) r.emplace_back(vgate::tl_name(i), vgate::tl_offset(i), vgate::tl_blocks(i));
+  return r;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -339,5 +360,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("sample", &sample, "temperature/top-k/top-p sampling (segmented Gumbel-max + exact rejection)",
         py::arg("logits"), py::arg("temperature"), py::arg("top_p"), py::arg("top_k"), py::arg("seeds"),
         py::arg("offsets"), py::arg("out"), py::arg("out_logprob") = py::none(), py::arg("ws") = py::none());
+  m.def("prefetch", &prefetch, "read a tensor once with the default cache policy (MALL warm-up)",
+        py::arg("t"), py::arg("blocks") = 256);
+  m.def("timeline_start", &timeline_start, "start a launch timeline in an int64 device buffer (zero it first)");
+  m.def("timeline_stop", &vgate::tl_stop, "stop handing out timeline slots; returns the slots used");
+  m.def("timeline_entries", &timeline_entries, "(kernel, offset, blocks) per launch since timeline_start");
   vgate::bind_runtime(m);
 }

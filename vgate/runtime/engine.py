@@ -54,7 +54,7 @@ class EngineConfig:
     enable_prefix_caching: bool = True
     seed: int = 0
     block_size: int = BLOCK_SIZE
-    part_size: int = 0  # 0 = auto: 128-token decode partitions (one wave each, merged in-launch)
+    part_size: int = 0  # 0 = auto: 512-token decode partitions (one workgroup each, merged in-launch)
     async_scheduling: bool = True  # GPU, TP=1: queue step t+1 before post-processing step t
     graph_token_buckets: list[int] | None = None
     warmup: bool = True
@@ -108,7 +108,7 @@ class LLMEngine:
                                              self.arch.head_dim, self.device, block_size=cfg.block_size)
         self.kvm = KVCacheManager(self.num_blocks, cfg.block_size, cfg.enable_prefix_caching)
         self.scheduler = Scheduler(self.kvm, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len)
-        part = cfg.part_size or 128
+        part = cfg.part_size or 512
         part = min(1024, max(32, (part + 31) // 32 * 32))
         self.runner = ModelRunner(self.model, self.kv_caches, cfg.max_num_seqs, cfg.max_num_batched_tokens,
                                   cfg.max_model_len, cfg.block_size, cfg.enforce_eager, part,
