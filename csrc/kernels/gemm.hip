@@ -91,9 +91,62 @@ __device__ __forceinline__ uint4 norm_frag(uint4 a, const bf16_t* w, int k0, flo
   }
 }
 
-// ---- epilogue for one (row m, 4 columns) group; v[j] are the NTB reduced tiles ----
+// ---- epilogue operands that do not depend on the GEMM result ----
+// The decode kernel loads them at launch (phase A: row / bias / residual words, phase B:
+// the RoPE cos/sin row of the position, issued once the first weight group is in flight),
+// so the epilogue after the reduction is pure ALU + stores instead of a dependent
+// positions -> cos_sin load chain behind the whole GEMM (benchmarks/qkv_probe.py).
+// (plain scalar members: an array member keeps the whole struct in scratch)
+template <int NTB>
+struct EpiPre {
+  uint2 r0, r1;  // EPI_BF16: residual words of tile 0 / 1 (4 bf16 each)
+  uint2 b0, b1;  // EPI_BF16 / EPI_F32: bias words of tile 0 / 1; EPI_QKV: bias of d.. / 64+d..
+  float4 cs, sn;
+  int pos, slot;
+};
+
 template <int NTB, int EPI>
-__device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[NTB], int m, int nt0, int nsub) {
+__device__ __forceinline__ void epi_pre_a(const GemmParams& p, EpiPre<NTB>& e, int m, int nt0, int nsub) {
+  m = m < p.M ? m : p.M - 1;
+  if constexpr (EPI == EPI_QKV) {
+    const int head = nt0 >> 3;
+    const int d = ((nt0 >> 1) & 3) * 16 + nsub;
+    e.pos = p.positions[m];
+    e.slot = p.slots[m];
+    e.b0 = p.bias ? *reinterpret_cast<const uint2*>(p.bias + head * 128 + d) : make_uint2(0, 0);
+    e.b1 = p.bias ? *reinterpret_cast<const uint2*>(p.bias + head * 128 + 64 + d) : make_uint2(0, 0);
+  } else if constexpr (EPI == EPI_BF16 || EPI == EPI_F32) {
+#pragma unroll
+    for (int j = 0; j < NTB; ++j) {
+      const int n = (nt0 + j) * 16 + nsub;
+      const uint2 b = p.bias ? *reinterpret_cast<const uint2*>(p.bias + n) : make_uint2(0, 0);
+      uint2 r = make_uint2(0, 0);
+      if constexpr (EPI == EPI_BF16) r = p.res ? *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldr + n) : r;
+      if (j == 0) { e.b0 = b; e.r0 = r; } else { e.b1 = b; e.r1 = r; }
+    }
+  }
+}
+
+template <int NTB, int EPI>
+__device__ __forceinline__ void epi_pre_b(const GemmParams& p, EpiPre<NTB>& e, int nt0, int nsub) {
+  if constexpr (EPI == EPI_QKV) {
+    const int d = ((nt0 >> 1) & 3) * 16 + nsub;
+    const float* cs = p.cos_sin + (size_t)e.pos * 128;
+    e.cs = *reinterpret_cast<const float4*>(cs + d);
+    e.sn = *reinterpret_cast<const float4*>(cs + 64 + d);
+  }
+}
+
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// ---- epilogue for one (row m, 4 columns) group; v[j] are the NTB reduced tiles ----
+// `e` = operands prefetched at launch (decode kernel) when `have`, else loaded here.
+// `have` is a compile-time choice: a runtime select between a prefetched register value
+// and a load becomes a select of ADDRESSES that puts the prefetch struct in scratch.
+template <int NTB, int EPI, bool have>
+__device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[NTB], int m, int nt0, int nsub,
+                                         const EpiPre<NTB> e) {
   if constexpr (EPI == EPI_SILU) {
     const int n = (nt0 >> 1) * 16 + nsub;
     float o[4];
@@ -107,27 +160,34 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[N
     // tiles (nt0, nt0+1) = original tiles (8h + t, 8h + t + 4) of head h: columns d and d + 64
     const int head = nt0 >> 3;
     const int d = ((nt0 >> 1) & 3) * 16 + nsub;  // rotation index 0..63
+    uint2 w1, w2;
+    float4 cs, sn;
+    int slot;
+    if constexpr (have) {
+      w1 = e.b0; w2 = e.b1; cs = e.cs; sn = e.sn; slot = e.slot;
+    } else {
+      w1 = p.bias ? *reinterpret_cast<const uint2*>(p.bias + head * 128 + d) : make_uint2(0, 0);
+      w2 = p.bias ? *reinterpret_cast<const uint2*>(p.bias + head * 128 + 64 + d) : make_uint2(0, 0);
+      const float* cp = p.cos_sin + (size_t)p.positions[m] * 128;
+      cs = *reinterpret_cast<const float4*>(cp + d);
+      sn = *reinterpret_cast<const float4*>(cp + 64 + d);
+      slot = p.slots[m];
+    }
+    const float b1[4] = {bf_lo(w1.x), bf_hi(w1.x), bf_lo(w1.y), bf_hi(w1.y)};
+    const float b2[4] = {bf_lo(w2.x), bf_hi(w2.x), bf_lo(w2.y), bf_hi(w2.y)};
     float x1[4], x2[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      float a = v[0][i], b = v[NTB - 1][i];
-      if (p.bias) {
-        a += bf2f(p.bias[head * 128 + d + i]);
-        b += bf2f(p.bias[head * 128 + 64 + d + i]);
-      }
-      x1[i] = bf2f(f2bf(a));  // qkv is bf16 in the reference: round before rotating
-      x2[i] = bf2f(f2bf(b));
+      x1[i] = bf2f(f2bf(v[0][i] + b1[i]));  // qkv is bf16 in the reference: round before rotating
+      x2[i] = bf2f(f2bf(v[NTB - 1][i] + b2[i]));
     }
     if (head < p.hq + p.hkv) {  // q or k: NeoX rotation
-      const float* cs = p.cos_sin + (size_t)p.positions[m] * 128;
-      const float4 c = *reinterpret_cast<const float4*>(cs + d);
-      const float4 s = *reinterpret_cast<const float4*>(cs + 64 + d);
-      const float cc[4] = {c.x, c.y, c.z, c.w}, sn[4] = {s.x, s.y, s.z, s.w};
+      const float cc[4] = {cs.x, cs.y, cs.z, cs.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float a = x1[i], b = x2[i];
-        x1[i] = a * cc[i] - b * sn[i];
-        x2[i] = b * cc[i] + a * sn[i];
+        x1[i] = a * cc[i] - b * ss[i];
+        x2[i] = b * cc[i] + a * ss[i];
       }
     }
     uint2 p1, p2;
@@ -138,7 +198,6 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[N
       *reinterpret_cast<uint2*>(q) = p1;
       *reinterpret_cast<uint2*>(q + 64) = p2;
     } else {
-      const int slot = p.slots[m];
       if (slot >= 0) {
         const bool is_k = head < p.hq + p.hkv;
         const int kh = is_k ? head - p.hq : head - p.hq - p.hkv;
@@ -154,9 +213,11 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[N
       const int n = (nt0 + j) * 16 + nsub;
       float o[4] = {v[j][0], v[j][1], v[j][2], v[j][3]};
       if (p.bias) {
-        const uint2 b = *reinterpret_cast<const uint2*>(p.bias + n);
-        o[0] += __uint_as_float(b.x << 16); o[1] += __uint_as_float(b.x & 0xffff0000u);
-        o[2] += __uint_as_float(b.y << 16); o[3] += __uint_as_float(b.y & 0xffff0000u);
+        uint2 b;
+        if constexpr (have) b = j == 0 ? e.b0 : e.b1;
+        else b = *reinterpret_cast<const uint2*>(p.bias + n);
+        o[0] += bf_lo(b.x); o[1] += bf_hi(b.x);
+        o[2] += bf_lo(b.y); o[3] += bf_hi(b.y);
       }
       if constexpr (EPI == EPI_F32) {
         *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.out) + (size_t)m * p.ldo + n) =
@@ -165,9 +226,11 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[N
         if (p.res) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) o[i] = bf2f(f2bf(o[i]));  // torch: (x@W).bf16() + res
-          const uint2 r = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldr + n);
-          o[0] += __uint_as_float(r.x << 16); o[1] += __uint_as_float(r.x & 0xffff0000u);
-          o[2] += __uint_as_float(r.y << 16); o[3] += __uint_as_float(r.y & 0xffff0000u);
+          uint2 r;
+          if constexpr (have) r = j == 0 ? e.r0 : e.r1;
+          else r = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldr + n);
+          o[0] += bf_lo(r.x); o[1] += bf_hi(r.x);
+          o[2] += bf_lo(r.y); o[3] += bf_hi(r.y);
         }
         uint2 pk;
         pk.x = pack_bf2(o[0], o[1]);
@@ -189,9 +252,12 @@ __device__ __forceinline__ float row_scale(const GemmParams& p, const float* ssq
   return rsqrtf(ss / (float)p.K + p.eps);
 }
 
-template <int MB, int NTB, int EPI, int NORM>
+// PRE: the epilogue thread of item s = threadIdx.x (MB == 1 decode: wave 0, one item each)
+// prefetched its operands at launch (EpiPre)
+template <int MB, int NTB, int EPI, int NORM, bool PRE>
 __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB][NTB], const float (&ssr)[MB],
-                                            char* smem, int m_base, int nt0) {
+                                            char* smem, int m_base, int nt0, const EpiPre<NTB> pre) {
+  static_assert(!PRE || MB == 1, "prefetched epilogue operands are a decode-kernel mode");
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   constexpr int SLOTS = MB * NTB * 64;  // f32x4 slots per block tile
   f32x4* red4 = reinterpret_cast<f32x4*>(smem);
@@ -276,7 +342,7 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
 #pragma unroll
         for (int j = 0; j < NTB; ++j) v[j] *= sc;
       }
-      if (m < p.M) epilogue<NTB, EPI>(p, v, m, nt0, 4 * (l >> 4));
+      if (m < p.M) epilogue<NTB, EPI, PRE>(p, v, m, nt0, 4 * (l >> 4), pre);
     }
     return;
   }
@@ -303,7 +369,7 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
 #pragma unroll
       for (int j = 0; j < NTB; ++j) v[j] *= sc;
     }
-    if (m < p.M) epilogue<NTB, EPI>(p, v, m, nt0, 4 * (l >> 4));
+    if (m < p.M) epilogue<NTB, EPI, PRE>(p, v, m, nt0, 4 * (l >> 4), pre);
   }
 }
 
@@ -382,15 +448,17 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
   // g+1's weights AND activations are issued before group g is consumed, so the wait
   // for g is a partial vmcnt that leaves g+1 in flight (issue order = wait order).
   auto load_grp = [&](uint4 (&b)[U][NTB], uint4 (&a)[U][MB], int k0) {
+    // a partial last group re-reads the last k-step / pack (clamped, so the issue stays
+    // unconditional); mma_grp zeroes those steps' activations
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int j = 0; j < NTB; ++j) b[u][j] = ld_nt16(wbase[j] + (size_t)(k0 + u) * 64);
+      for (int j = 0; j < NTB; ++j) b[u][j] = ld_nt16(wbase[j] + (size_t)min(k0 + u, kend - 1) * 64);
 #pragma unroll
     for (int u = 0; u < U; u += XP)  // packed: slot u holds the raw load for k-steps u..u+XP-1
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb)
-        a[u][mb] = xok[mb] ? *reinterpret_cast<const uint4*>(xrow[mb] + (k0 + u) * 32) : make_uint4(0, 0, 0, 0);
+        a[u][mb] = xok[mb] ? *reinterpret_cast<const uint4*>(xrow[mb] + min(k0 + u, kend - XP) * 32) : make_uint4(0, 0, 0, 0);
   };
   auto unpack_grp = [&](uint4 (&a)[U][MB]) {
     if constexpr (XP > 1) {
@@ -412,11 +480,16 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
   };
   auto mma_grp = [&](const uint4 (&b)[U][NTB], uint4 (&a)[U][MB], int k0) {
     unpack_grp(a);
+#pragma unroll
+    for (int u = 0; u < U; ++u)  // steps past this wave's range (partial last group) add 0
+      if (k0 + u >= kend)
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) a[u][mb] = make_uint4(0, 0, 0, 0);
     if constexpr (NORM) {
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb) a[u][mb] = norm_frag<NORM>(a[u][mb], nw_ptr, (k0 + u) * 32, ssr[mb]);
+        for (int mb = 0; mb < MB; ++mb) a[u][mb] = norm_frag<NORM>(a[u][mb], nw_ptr, min(k0 + u, kend - 1) * 32, ssr[mb]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -425,8 +498,15 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(as_bf16x8(b[u][j]), as_bf16x8(a[u][mb]), acc[mb][j]);
   };
+  // epilogue operands of this thread's (row, 4 columns) item (decode: wave 0 runs the epilogue)
+  EpiPre<NTB> pre;
+  const bool epi_thr = MB == 1 && threadIdx.x < 64;
+  if (epi_thr) epi_pre_a<NTB, EPI>(p, pre, m_base + r16, nt0, 4 * (lane >> 4));
+  bool pre_b = false;
+  // Whole groups of U k-steps, the last one possibly partial: no serial tail, so a wave
+  // with ngrp <= 2 waits on ONE round trip (e.g. the QKV projection: 6 steps per wave)
   int kt = kbeg;
-  const int ngrp = (kend - kbeg) / U;
+  const int ngrp = (kend - kbeg + U - 1) / U;
   if constexpr (!PIPE) {
     for (int g = 0; g < ngrp; ++g, kt += U) {
       uint4 b[U][NTB], a[U][MB];
@@ -436,6 +516,8 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
   } else if (ngrp > 0) {
     uint4 b0[U][NTB], a0[U][MB], b1[U][NTB], a1[U][MB];
     load_grp(b0, a0, kt);
+    if (epi_thr) epi_pre_b<NTB, EPI>(p, pre, nt0, 4 * (lane >> 4));  // dependent on phase A only
+    pre_b = true;
     int g = 0;
     for (; g + 2 <= ngrp; g += 2) {
       load_grp(b1, a1, kt + U);
@@ -444,46 +526,10 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
       mma_grp(b1, a1, kt + U);
       kt += 2 * U;
     }
-    if (g < ngrp) {
-      mma_grp(b0, a0, kt);
-      kt += U;
-    }
+    if (g < ngrp) mma_grp(b0, a0, kt);
   }
-  // tail: whole packs of XP k-steps
-  for (; kt < kend; kt += XP) {
-    uint4 b[XP][NTB], a[XP][MB];
-#pragma unroll
-    for (int u = 0; u < XP; ++u)
-#pragma unroll
-      for (int j = 0; j < NTB; ++j) b[u][j] = ld_nt16(wbase[j] + (size_t)(kt + u) * 64);
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb)
-      a[0][mb] = xok[mb] ? *reinterpret_cast<const uint4*>(xrow[mb] + kt * 32) : make_uint4(0, 0, 0, 0);
-    if constexpr (XP > 1) {
-      const uint32_t lom = r16 < R ? ~0u : 0u;
-      const uint4 v = a[0][0];
-      const uint4 v1 = row_ror<R>(v);
-      a[0][0] = and_mask(v, lom);
-      a[1][0] = and_mask(v1, lom);
-      if constexpr (XP == 4) {
-        const uint4 v2 = row_ror<2 * R>(v), v3 = row_ror<3 * R>(v);
-        a[2][0] = and_mask(v2, lom);
-        a[3][0] = and_mask(v3, lom);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < XP; ++u) {
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) {
-        if constexpr (NORM) a[u][mb] = norm_frag<NORM>(a[u][mb], nw_ptr, (kt + u) * 32, ssr[mb]);
-      }
-#pragma unroll
-      for (int j = 0; j < NTB; ++j)
-#pragma unroll
-        for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(as_bf16x8(b[u][j]), as_bf16x8(a[u][mb]), acc[mb][j]);
-    }
-  }
-  gemm_finish<MB, NTB, EPI, NORM>(p, acc, ssr, smem, m_base, nt0);
+  if (epi_thr && !pre_b) epi_pre_b<NTB, EPI>(p, pre, nt0, 4 * (lane >> 4));
+  gemm_finish<MB, NTB, EPI, NORM, MB == 1>(p, acc, ssr, smem, m_base, nt0, pre);
 }
 
 // ---- AWQ W4A16 ----
@@ -551,7 +597,7 @@ __global__ __launch_bounds__(1024) void awq_gemm_kernel(GemmParams p) {
       }
     }
   }
-  gemm_finish<MB, NTB, EPI, NORM>(p, acc, ssr, smem, m_base, nt0);
+  gemm_finish<MB, NTB, EPI, NORM, false>(p, acc, ssr, smem, m_base, nt0, EpiPre<NTB>{});
 }
 
 // ---- prefill / medium-M tile GEMM (M > 16, bf16 weights) ----
@@ -688,7 +734,7 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(GemmParams p) {
 #pragma unroll
       for (int j = 0; j < NTW; ++j) v[j] *= sc;
     }
-    if (m < p.M) epilogue<NTW, EPI>(p, v, m, nt0, 4 * (lane >> 4));
+    if (m < p.M) epilogue<NTW, EPI, false>(p, v, m, nt0, 4 * (lane >> 4), EpiPre<NTW>{});
   }
 }
 
@@ -790,10 +836,18 @@ static void launch_dispatch(GemmParams p, const GemmArgs& g, hipStream_t st) {
     case EPI_SILU: VG_NORM(2, EPI_SILU); break;
     case EPI_QKV: VG_NORM(2, EPI_QKV); break;
     case EPI_F32:
-      if (pair) VG_NORM(2, EPI_F32); else VG_NORM(1, EPI_F32);
+      if constexpr (!AWQ) {
+        if (g.ntb == 4 && ntiles % 4 == 0 && g.M <= 16) { VG_NORM(4, EPI_F32); break; }
+      }
+      if (g.ntb == 2 || (g.ntb == 0 && pair)) VG_NORM(2, EPI_F32);
+      else VG_NORM(1, EPI_F32);
       break;
     default:
-      if (pair) VG_NORM(2, EPI_BF16); else VG_NORM(1, EPI_BF16);
+      if constexpr (!AWQ) {
+        if (g.ntb == 4 && ntiles % 4 == 0 && g.M <= 16) { VG_NORM(4, EPI_BF16); break; }
+      }
+      if (g.ntb == 2 || (g.ntb == 0 && pair)) VG_NORM(2, EPI_BF16);
+      else VG_NORM(1, EPI_BF16);
   }
 #undef VG_NORM
 }

@@ -26,6 +26,7 @@ struct GemmArgs {
   int epi;            // 0 bf16, 1 f32, 2 silu*mul (gate/up tiles interleaved), 3 qkv+rope+kv-write
   int waves;          // 0 = heuristic
   int splitk;         // 0 = heuristic
+  int ntb;            // 16-column tiles per block for plain / f32 epilogues (0 = heuristic; 1, 2, 4)
   float* slabs;       // split-K fp32 partial slabs (workspace) or null
   size_t slab_bytes;
   uint32_t* counters; // split-K arrival tickets, zero-initialised, self-resetting

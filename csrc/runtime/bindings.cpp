@@ -51,7 +51,7 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
           const c10::optional<Tensor>& cos_sin, const c10::optional<Tensor>& k_cache,
           const c10::optional<Tensor>& v_cache, int64_t hq, int64_t hkv,
           const c10::optional<Tensor>& awq_scales, const c10::optional<Tensor>& awq_zeros, int64_t group,
-          bool rownorm, const c10::optional<Tensor>& dbg_ts) {
+          bool rownorm, const c10::optional<Tensor>& dbg_ts, int64_t ntb) {
   CHECK_DEV(x); CHECK_DEV(wp); CHECK_DEV(out);
   CHECK_DT(x, torch::kBFloat16);
   CHECK_LASTDIM(x); CHECK_LASTDIM(out);
@@ -96,7 +96,7 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
   g.ldr = g.res ? (int)res->stride(0) : 0;
   if (g.res) TORCH_CHECK(res->size(0) >= M && res->size(1) >= N, "gemm: residual shape");
   g.out = out.data_ptr(); g.ldo = (int)out.stride(0);
-  g.epi = (int)epi; g.waves = (int)waves; g.splitk = (int)splitk;
+  g.epi = (int)epi; g.waves = (int)waves; g.splitk = (int)splitk; g.ntb = (int)ntb;
   if (ws.has_value() && ws->defined()) {
     CHECK_DEV(*ws); CHECK_DT(*ws, torch::kInt32);
     TORCH_CHECK(ws->numel() > 65536 * 2, "gemm: workspace too small");
@@ -345,7 +345,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("slots") = py::none(), py::arg("cos_sin") = py::none(), py::arg("k_cache") = py::none(),
         py::arg("v_cache") = py::none(), py::arg("hq") = 0, py::arg("hkv") = 0,
         py::arg("awq_scales") = py::none(), py::arg("awq_zeros") = py::none(), py::arg("group") = 128,
-        py::arg("rownorm") = false, py::arg("dbg_ts") = py::none());
+        py::arg("rownorm") = false, py::arg("dbg_ts") = py::none(), py::arg("ntb") = 0);
   m.def("attention", &attention, "unified paged attention: decode (partitions merged in-launch) + varlen prefill tiles",
         py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),
