@@ -27,7 +27,8 @@ os.environ.setdefault("VGATE_LOGGING__LEVEL", "WARNING")
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 BASELINE_REQ_S = 6.47
-METRIC = "req/s + p50/p99 end-to-end latency, Qwen2.5-1.5B /v1/chat/completions at fixed concurrency"
+BENCH_KEY = "vgate-bench-key"
+METRIC = "req/s + p50/p99 end-to-end latency, {model} /v1/chat/completions at fixed concurrency"
 
 WORDS = ("the quick brown fox jumps over a lazy dog while engineers measure latency throughput memory "
          "bandwidth kernels scheduling batching caching tokens requests gateway worker cluster").split()
@@ -45,18 +46,20 @@ def pct(xs, p):
     return xs[min(int(len(xs) * p / 100), len(xs) - 1)] if xs else 0.0
 
 
-async def run_load(port: int, n: int, concurrency: int, max_tokens: int, rank: int, start_idx: int):
+async def run_load(port: int, n: int, concurrency: int, max_tokens: int, rank: int, start_idx: int,
+                   model: str = "Qwen/Qwen2.5-1.5B-Instruct", api_key: str | None = None):
     import aiohttp
     lat, fails, tokens = [], 0, 0
     sem = asyncio.Semaphore(concurrency)
     url = f"http://127.0.0.1:{port}/v1/chat/completions"
     conn = aiohttp.TCPConnector(limit=concurrency * 2)
     timeout = aiohttp.ClientTimeout(total=300)
-    async with aiohttp.ClientSession(connector=conn, timeout=timeout) as s:
+    headers = {"Authorization": f"Bearer {api_key}"} if api_key else None
+    async with aiohttp.ClientSession(connector=conn, timeout=timeout, headers=headers) as s:
         async def one(i):
             nonlocal fails, tokens
             async with sem:
-                body = {"model": "Qwen/Qwen2.5-1.5B-Instruct",
+                body = {"model": model,
                         "messages": [{"role": "user", "content": make_prompt(rank, start_idx + i)}],
                         "max_tokens": max_tokens}
                 t0 = time.perf_counter()
@@ -94,6 +97,11 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool):
         batch={"max_batch_size": args.concurrency},
         cache={"enabled": True, "maxsize": 1000},
         logging={"level": "WARNING", "json_format": True},
+        # --security: bearer auth + the sliding-window rate limiter on the hot path (BASELINE
+        # config 5: high-QPS rate limiter on); the key's limit is far above the offered load
+        security={"enabled": bool(args.security),
+                  "api_keys": [{"key": BENCH_KEY, "name": "bench", "rate_limit": 10_000_000}],
+                  "rate_limiting": {"enabled": True, "window_seconds": 60}},
     )
     app = create_app(cfg)
     port = args.port + local
@@ -119,12 +127,15 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool):
             torch.cuda.synchronize()
 
     per_step = args.requests_per_step
+    key = BENCH_KEY if args.security else None
     # warmup (also captures the hipGraph buckets this load uses)
     if args.warmup > 0:
-        await run_load(port, per_step * args.warmup, args.concurrency, args.max_tokens, rank, 10_000_000)
+        await run_load(port, per_step * args.warmup, args.concurrency, args.max_tokens, rank, 10_000_000,
+                       args.model, key)
     barrier()
     t0 = time.perf_counter()
-    lat, fails, tokens, _ = await run_load(port, per_step * args.steps, args.concurrency, args.max_tokens, rank, 0)
+    lat, fails, tokens, _ = await run_load(port, per_step * args.steps, args.concurrency, args.max_tokens, rank, 0,
+                                           args.model, key)
     barrier()
     wall = time.perf_counter() - t0
     eng = app.state.vgate.engine
@@ -148,6 +159,7 @@ def main():
     ap.add_argument("--kv-blocks", type=int, default=4096)
     ap.add_argument("--eager", action="store_true")
     ap.add_argument("--port", type=int, default=18100)
+    ap.add_argument("--security", action="store_true", help="bearer auth + rate limiter on the request path")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -173,11 +185,12 @@ def main():
         value = total / wall
         toks = sum(r["tokens"] for r in allr)
         out = {
-            "metric": METRIC, "value": round(value, 3), "unit": "req/s", "n_gpus": world, "steps": args.steps,
+            "metric": METRIC.format(model="Qwen2.5-1.5B" if model_name == "Qwen2.5-1.5B-Instruct" else model_name), "value": round(value, 3), "unit": "req/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * wall / args.steps, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": round(value / BASELINE_REQ_S, 3), "dtype": "bf16",
             "data": f"synthetic unique prompts, random-init weights ({model_name} architecture)",
-            "config": {"model": model_name, "global_batch": args.concurrency * world,
+            "config": {"model": model_name, "quantization": args.quantization or "none",
+                       "security_rate_limiter": bool(args.security), "global_batch": args.concurrency * world,
                        "seq_len": args.max_tokens, "parallelism": f"dp{world}",
                        "concurrency_per_gpu": args.concurrency, "max_tokens": args.max_tokens,
                        "requests_per_step_per_gpu": args.requests_per_step},
