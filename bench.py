@@ -20,6 +20,7 @@ import asyncio
 import contextlib
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -80,7 +81,7 @@ async def run_load(port: int, n: int, concurrency: int, max_tokens: int, rank: i
     return lat, fails, tokens, wall
 
 
-async def serve_and_bench(args, rank: int, world: int, dist_ok: bool):
+async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=None):
     import torch
     import uvicorn
 
@@ -128,14 +129,29 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool):
 
     per_step = args.requests_per_step
     key = BENCH_KEY if args.security else None
+
+    async def load(n, start_idx):
+        if client is None:  # default: the load loop shares this process's event loop / GIL
+            return await run_load(port, n, args.concurrency, args.max_tokens, rank, start_idx, args.model, key)
+        # the load generator is its own process (as the reference's bench_load.py against a
+        # running server): one command line in, one result line out; the server keeps serving
+        # on this event loop while the reply is awaited off-loop
+        cmd = {"port": port, "n": n, "concurrency": args.concurrency, "max_tokens": args.max_tokens,
+               "rank": rank, "start_idx": start_idx, "model": args.model, "api_key": key}
+        client.stdin.write(json.dumps(cmd) + "\n")
+        client.stdin.flush()
+        line = await asyncio.get_running_loop().run_in_executor(None, client.stdout.readline)
+        if not line:
+            raise RuntimeError("load client exited")
+        r = json.loads(line)
+        return r["lat"], r["fails"], r["tokens"], r["wall"]
+
     # warmup (also captures the hipGraph buckets this load uses)
     if args.warmup > 0:
-        await run_load(port, per_step * args.warmup, args.concurrency, args.max_tokens, rank, 10_000_000,
-                       args.model, key)
+        await load(per_step * args.warmup, 10_000_000)
     barrier()
     t0 = time.perf_counter()
-    lat, fails, tokens, _ = await run_load(port, per_step * args.steps, args.concurrency, args.max_tokens, rank, 0,
-                                           args.model, key)
+    lat, fails, tokens, _ = await load(per_step * args.steps, 0)
     barrier()
     wall = time.perf_counter() - t0
     eng = app.state.vgate.engine
@@ -144,6 +160,16 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool):
     await srv_task
     return {"lat": lat, "fails": fails, "tokens": tokens, "wall": wall, "boot_s": boot_s,
             "n": per_step * args.steps, "engine": snap}
+
+
+def client_loop():
+    """--client-proc: one JSON load command per stdin line -> one JSON result per stdout line."""
+    for line in sys.stdin:
+        c = json.loads(line)
+        lat, fails, tokens, wall = asyncio.run(run_load(c["port"], c["n"], c["concurrency"], c["max_tokens"],
+                                                        c["rank"], c["start_idx"], c["model"], c["api_key"]))
+        sys.stdout.write(json.dumps({"lat": lat, "fails": fails, "tokens": tokens, "wall": wall}) + "\n")
+        sys.stdout.flush()
 
 
 def main():
@@ -160,8 +186,20 @@ def main():
     ap.add_argument("--eager", action="store_true")
     ap.add_argument("--port", type=int, default=18100)
     ap.add_argument("--security", action="store_true", help="bearer auth + rate limiter on the request path")
+    ap.add_argument("--client-process", action="store_true",
+                    help="run the load loop in a separate client process (default: in the server process; "
+                         "measured slower on the 1-GPU box: 68 vs 81 req/s, profiles/r1_bench_client_modes.log)")
+    ap.add_argument("--client-proc", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.client_proc:
+        client_loop()
+        return
 
+    # start the load-client process before anything here touches the GPU
+    client = None
+    if args.client_process:
+        client = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--client-proc"],
+                                  stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     dist_ok = False
@@ -170,7 +208,12 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo")  # coordination only: replicas share no tensors
         dist_ok = True
-    res = asyncio.run(serve_and_bench(args, rank, world, dist_ok))
+    try:
+        res = asyncio.run(serve_and_bench(args, rank, world, dist_ok, client))
+    finally:
+        if client is not None:
+            client.stdin.close()
+            client.wait(timeout=30)
     if dist_ok:
         import torch.distributed as dist
         allr = [None] * world
@@ -190,7 +233,8 @@ def main():
             "scaling": "weak", "vs_baseline": round(value / BASELINE_REQ_S, 3), "dtype": "bf16",
             "data": f"synthetic unique prompts, random-init weights ({model_name} architecture)",
             "config": {"model": model_name, "quantization": args.quantization or "none",
-                       "security_rate_limiter": bool(args.security), "global_batch": args.concurrency * world,
+                       "security_rate_limiter": bool(args.security),
+                       "load_client": "separate process" if args.client_process else "in-process", "global_batch": args.concurrency * world,
                        "seq_len": args.max_tokens, "parallelism": f"dp{world}",
                        "concurrency_per_gpu": args.concurrency, "max_tokens": args.max_tokens,
                        "requests_per_step_per_gpu": args.requests_per_step},

@@ -34,11 +34,13 @@ def main():
     ap.add_argument("--ctx", type=int, default=40, help="prompt tokens per sequence")
     ap.add_argument("--kv-blocks", type=int, default=0, help="KV pool size in blocks (0 = engine sizing)")
     ap.add_argument("--max-seqs", type=int, default=64)
+    ap.add_argument("--quantization", default=None)
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     C = ops.native()
     eng = LLMEngine(EngineConfig(model=a.model, device="cuda:0", max_model_len=2048, max_num_seqs=a.max_seqs,
-                                 max_num_batched_tokens=2048, num_kv_blocks=a.kv_blocks or None, warmup=False))
+                                 max_num_batched_tokens=2048, num_kv_blocks=a.kv_blocks or None, warmup=False,
+                                 quantization=a.quantization))
     for i in range(a.batch):
         ids = [100 + (i * 131 + j * 17) % 5000 for j in range(a.ctx)]
         eng.add_request(f"r{i}", prompt_ids=ids,

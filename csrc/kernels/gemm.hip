@@ -533,11 +533,23 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
 }
 
 // ---- AWQ W4A16 ----
+// nibble order of ops.pack_awq: value j at bit (16 if j odd) + 4 (j >> 1)
 __device__ __forceinline__ bf16x8 dq8(uint32_t q, float s, float sz) {
   bf16x8 r;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (__bf16)((float)((q >> (4 * j)) & 0xF) * s - sz);
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)((float)((q >> ((j & 1) * 16 + 4 * (j >> 1))) & 0xF) * s - sz);
   return r;
+}
+
+// the 8 raw values as bf16 (128 + v): the group scale is applied after the MFMA
+// (sum_k x (128 + v) s - (128 s + s z) sum_k x = sum_k x (v - z) s)
+__device__ __forceinline__ bf16x8 raw8(uint32_t q) {
+  uint4 r;
+  r.x = (q & 0x000F000Fu) | 0x43004300u;
+  r.y = ((q >> 4) & 0x000F000Fu) | 0x43004300u;
+  r.z = ((q >> 8) & 0x000F000Fu) | 0x43004300u;
+  r.w = ((q >> 12) & 0x000F000Fu) | 0x43004300u;
+  return as_bf16x8(r);
 }
 
 template <int MB, int NTB, int EPI, int NORM>
@@ -598,6 +610,205 @@ __global__ __launch_bounds__(1024) void awq_gemm_kernel(GemmParams p) {
     }
   }
   gemm_finish<MB, NTB, EPI, NORM, false>(p, acc, ssr, smem, m_base, nt0, EpiPre<NTB>{});
+}
+
+// ---- AWQ W4A16 decode (M <= 16): waves split N and share ONE LDS copy of the activations ----
+// With int4 weights a 16-B lane load carries 4 k-steps of one 16-column tile, while the
+// matching activation fragments are 4 x 16 B: a K-split kernel (waves split K, every wave
+// its own x range) moves 2-4x more activation than weight bytes through the vector-memory
+// pipe. Here a block = 4 waves x NTW tiles, the activation slice of the block's K-slice is
+// staged once into LDS in MFMA B-fragment order (ds_read_b128 per k-step, off the vector
+// memory pipe; RMSNorm gamma applied while staging, the row sum of squares over the FULL row
+// so a split-K slice needs no ssq hand-off) and each wave streams only int4 weights + group
+// scales, software-pipelined G k-quads ahead (ping-pong register groups, partial last group
+// clamped). Split-K slices meet at a per-column-group ticket (sc1 slabs, last arriver sums).
+constexpr int AD_WAVES = 4;
+constexpr int AD_G = 2;  // k-quads (128 k) per register group
+
+template <int NTW, int EPI, int NORM>
+__global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  TLScope tl_scope(p.dbg_ts);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int KQ = p.K >> 7;
+  const int nt0 = (blockIdx.x * AD_WAVES + wid) * NTW;  // this wave's first 16-column tile
+  const int q0 = (KQ * blockIdx.z) / p.splitk, q1 = (KQ * (blockIdx.z + 1)) / p.splitk;
+  const int nq = q1 - q0, nst = nq * 4;  // k-quads / k-steps of the slice
+  uint4* xs = reinterpret_cast<uint4*>(smem);                             // [nst][64] B fragments
+  float* xsum = reinterpret_cast<float*>(smem + (size_t)nst * 64 * 16);  // [nq][16] per-group row sums
+  float* ssq = xsum + nq * 16;                                            // [4 waves][16] slice sums of squares
+  int* flag = reinterpret_cast<int*>(ssq + 4 * 16);
+  const int m = lane & 15, nsub = 4 * (lane >> 4);
+  // 1) activation slice -> registers (issued FIRST, so waiting for it leaves the weights that
+  //    follow in flight), then the first weight groups, then the LDS image of the slice.
+  //    Thread t stages fragment f = i * 256 + t: lane t & 63, k-step 4i + (t >> 6).
+  constexpr int XMAX = 16;  // k-steps per thread (slices of <= 16 k-quads, checked on the host)
+  uint4 xr[XMAX];
+  const int xrow_m = lane & 15;
+  const bf16_t* xrow = p.x + (size_t)row_of(p, min(xrow_m, p.M - 1)) * p.lda + 8 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < XMAX; ++i) {
+    const int t = 4 * i + wid;  // k-step of the slice
+    xr[i] = (t < nst && xrow_m < p.M) ? ld16(xrow + (q0 * 4 + t) * 32) : make_uint4(0, 0, 0, 0);
+  }
+  // 2) weight stream: this wave's NTW tiles over the block's k-quads. Per k-quad and tile:
+  //    P = sum over the quad's 4 MFMAs of raw8(w) . x, then acc += s (x) P - (128 s + s z) X
+  //    with s, s z of the lane's 4 output columns and X the row's activation sum (one group
+  //    per k-quad: group % 128 == 0, checked on the host)
+  f32x4 acc[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto load_grp = [&](uint4 (&w)[AD_G][NTW], uint2 (&sv)[AD_G][NTW], uint2 (&zv)[AD_G][NTW], int kq0) {
+#pragma unroll
+    for (int g = 0; g < AD_G; ++g) {
+      const int kq = min(kq0 + g, q1 - 1);
+      const size_t gi = (size_t)((kq * 128) / p.group) * p.N;
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        w[g][j] = ld_nt16(p.wp + ((size_t)(nt0 + j) * KQ + kq) * 64 + lane);
+        sv[g][j] = *reinterpret_cast<const uint2*>(p.scales + gi + (nt0 + j) * 16 + nsub);
+        zv[g][j] = *reinterpret_cast<const uint2*>(p.zeros + gi + (nt0 + j) * 16 + nsub);
+      }
+    }
+  };
+  auto mma_grp = [&](const uint4 (&w)[AD_G][NTW], const uint2 (&sv)[AD_G][NTW], const uint2 (&zv)[AD_G][NTW],
+                     int kq0) {
+#pragma unroll
+    for (int g = 0; g < AD_G; ++g) {
+      const int kq = kq0 + g;
+      if (kq >= q1) break;  // wave-uniform
+      const int t0 = (kq - q0) * 4;
+      f32x4 pr[NTW];
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) pr[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bf16x8 xb = as_bf16x8(xs[(t0 + u) * 64 + lane]);
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          const uint32_t q = u == 0 ? w[g][j].x : u == 1 ? w[g][j].y : u == 2 ? w[g][j].z : w[g][j].w;
+          pr[j] = mfma16(raw8(q), xb, pr[j]);
+        }
+      }
+      const float X = xsum[(kq - q0) * 16 + m];
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        const float s4[4] = {bf_lo(sv[g][j].x), bf_hi(sv[g][j].x), bf_lo(sv[g][j].y), bf_hi(sv[g][j].y)};
+        const float z4[4] = {bf_lo(zv[g][j].x), bf_hi(zv[g][j].x), bf_lo(zv[g][j].y), bf_hi(zv[g][j].y)};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[j][i] = fmaf(s4[i], pr[j][i], fmaf(-fmaf(128.f, s4[i], z4[i]), X, acc[j][i]));
+      }
+    }
+  };
+  const int ngrp = (nq + AD_G - 1) / AD_G;
+  {
+    uint4 wa[AD_G][NTW], wb[AD_G][NTW];
+    uint2 sa[AD_G][NTW], sb[AD_G][NTW], za[AD_G][NTW], zb[AD_G][NTW];
+    int kq = q0;
+    if (ngrp > 0) load_grp(wa, sa, za, kq);
+    // the activation image (x * gamma under NORM == 1) and this wave's slice sum of squares
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < XMAX; ++i) {
+      const int t = 4 * i + wid;
+      if (t < nst) {
+        uint4 v = xr[i];
+        if constexpr (NORM != 0) {
+          float a[8];
+          unpack8(v, a);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss += a[j] * a[j];
+          if constexpr (NORM == 1) {
+            float g8[8];
+            unpack8(ld16(p.norm_w + (q0 * 4 + t) * 32 + 8 * (lane >> 4)), g8);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[j] *= g8[j];
+            v = pack8(a);
+          }
+        }
+        xs[t * 64 + lane] = v;
+      }
+    }
+    if constexpr (NORM != 0) {
+      ss += xor16(ss);
+      ss += xor32(ss);
+      if (lane < 16) ssq[wid * 16 + lane] = ss;
+    }
+    lds_barrier();  // LDS image visible; the weight loads stay in flight
+    // per (k-quad, row) sum of the staged (bf16) activations, fixed order
+    for (int idx = threadIdx.x; idx < nq * 16; idx += blockDim.x) {
+      const int ql = idx >> 4, r = idx & 15;
+      float sacc = 0.f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          float a[8];
+          unpack8(xs[(ql * 4 + u) * 64 + g4 * 16 + r], a);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) sacc += a[j];
+        }
+      xsum[idx] = sacc;
+    }
+    lds_barrier();
+    int g = 0;
+    for (; g + 2 <= ngrp; g += 2) {
+      load_grp(wb, sb, zb, kq + AD_G);
+      mma_grp(wa, sa, za, kq);
+      if (g + 2 < ngrp) load_grp(wa, sa, za, kq + 2 * AD_G);
+      mma_grp(wb, sb, zb, kq + AD_G);
+      kq += 2 * AD_G;
+    }
+    if (g < ngrp) mma_grp(wa, sa, za, kq);
+  }
+  // 3) finish: lane holds D[n = 4(l>>4) + i][m = l & 15] of each tile
+  float ss_slice = 0.f;  // this slice's row sum of squares (fixed wave order)
+  if constexpr (NORM != 0) {
+#pragma unroll
+    for (int w = 0; w < AD_WAVES; ++w) ss_slice += ssq[w * 16 + m];
+  }
+  auto finish = [&](f32x4 (&v)[NTW], float ss_row) {
+    if constexpr (NORM != 0) {
+      const float rs = rsqrtf(ss_row / (float)p.K + p.eps);
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) v[j] *= rs;
+    }
+    if (m < p.M) epilogue<NTW, EPI, false>(p, v, m, nt0, nsub, EpiPre<NTW>{});
+  };
+  if (p.splitk == 1) {
+    finish(acc, ss_slice);
+    return;
+  }
+  const int grp = blockIdx.x;  // column group: AD_WAVES * NTW tiles
+  constexpr int SLOTS = AD_WAVES * NTW * 64;
+  constexpr int SLAB = SLOTS * 4 + 16;  // floats per (group, slice): tiles + per-row ssq
+  float* slab = p.slabs + ((size_t)grp * p.splitk + blockIdx.z) * SLAB;
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+    st_sc1_f4(slab + ((wid * NTW + j) * 64 + lane) * 4, acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+  if (NORM != 0 && wid == 0 && lane < 16) st_sc1(slab + SLOTS * 4 + lane, ss_slice);
+  drain_stores();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(p.counters + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (uint32_t)(p.splitk - 1);
+    if (last) __hip_atomic_store(p.counters + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  const float* all = p.slabs + (size_t)grp * p.splitk * SLAB;
+  f32x4 v[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    f32x4 t = {0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < p.splitk; ++z) t += ld_sc1_f4(all + (size_t)z * SLAB + ((wid * NTW + j) * 64 + lane) * 4);
+    v[j] = t;
+  }
+  float ss_row = 0.f;
+  if constexpr (NORM != 0)
+    for (int z = 0; z < p.splitk; ++z) ss_row += ld_sc1(all + (size_t)z * SLAB + SLOTS * 4 + m);
+  finish(v, ss_row);
 }
 
 // ---- prefill / medium-M tile GEMM (M > 16, bf16 weights) ----
@@ -795,8 +1006,41 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
   }
 }
 
+// AWQ decode (M <= 16): column groups of AD_WAVES x NTW tiles, K split so the grid covers the
+// chip (>= 256 blocks where K allows >= 2 k-quads per slice)
+template <int NTB, int EPI, int NORM>
+static bool launch_awq_dec(GemmParams p, const GemmArgs& g, hipStream_t st) {
+  const int ntiles = g.N / 16;
+  if (g.M > 16 || ntiles % (AD_WAVES * NTB) != 0 || g.waves > 0 || g.group % 128 != 0) return false;
+  // measured (benchmarks/awq_sweep.py, profiles/r1_awq_sweep.log, Qwen2.5-1.5B shapes, M = 8):
+  // the LDS-staged kernel wins for long K (down: 11.4 vs 18 us) and wide N (gate_up at one
+  // slice: 10.5 vs 12.1 us); for narrow N x short K (qkv, o_proj) its staging prologue costs
+  // more than the activation traffic it saves and the K-split kernel keeps them (4.8 vs 7.0 us)
+  const bool wide = g.N >= 8192, deep = g.K >= 4096;
+  if (g.splitk <= 0 && !wide && !deep) return false;
+  const int groups = ntiles / (AD_WAVES * NTB);
+  const int KQ = g.K / 128;
+  int sk = g.splitk > 0 ? g.splitk : (wide && !deep) ? 1 : (256 + groups - 1) / groups;
+  if (g.splitk <= 0 && sk > 8) sk = 8;  // more slices only add hand-off traffic (sweep)
+  sk = sk > KQ / 2 ? KQ / 2 : sk;
+  sk = sk < 1 ? 1 : sk;
+  if ((KQ + sk - 1) / sk > 16) sk = (KQ + 15) / 16;  // staging holds <= 16 k-quads per slice
+  const size_t need_slab = (size_t)groups * sk * (AD_WAVES * NTB * 64 * 16 + 64);
+  if (sk > 1 && (g.slabs == nullptr || need_slab > g.slab_bytes || groups > g.max_counters)) sk = 1;
+  p.splitk = sk;
+  const int qmax = (KQ + sk - 1) / sk;
+  const size_t lds = (size_t)qmax * 4 * 64 * 16 + (size_t)qmax * 16 * 4 + 4 * 16 * 4 + 16;
+  if (lds > 150 * 1024) return false;
+  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_dec", groups * sk);
+  hipLaunchKernelGGL((awq_dec_kernel<NTB, EPI, NORM>), dim3(groups, 1, sk), dim3(64 * AD_WAVES), lds, st, p);
+  return true;
+}
+
 template <int NTB, int EPI, int NORM, bool AWQ>
 static void launch_m(GemmParams p, const GemmArgs& g, hipStream_t st) {
+  if constexpr (AWQ) {
+    if (launch_awq_dec<NTB, EPI, NORM>(p, g, st)) return;
+  }
   if constexpr (!AWQ) {
     // M > 16: N-split tile kernel with a shared LDS copy of x (see gemm_tile_kernel);
     // paired epilogues (silu / qkv) keep their tile pairs inside one wave (NTW = 2)

@@ -398,6 +398,32 @@ def test_awq_norm_splitk():
         assert _rel_err(y, ref.linear_ref(xn, wd)) < 2e-2
 
 
+@pytest.mark.parametrize("M", [1, 5, 16, 24])
+@pytest.mark.parametrize("g", [64, 128])
+@pytest.mark.parametrize("sk", [0, 3])
+def test_awq_decode_kernel_shapes(M, g, sk):
+    """AWQ decode kernel (waves split N over an LDS copy of x, M <= 16) == dequantised
+    reference for plain + residual, silu pairs and group 64 / 128; M = 24 takes the
+    K-split kernel. Also == the K-split kernel (waves forced) on the same inputs."""
+    torch.manual_seed(40 + M + g + sk)
+    N, K = 1024, 2048
+    q = torch.randint(0, 16, (N, K), dtype=torch.int32)
+    scales = (torch.rand(K // g, N) * 0.02 + 0.005).bfloat16()
+    zeros = torch.randint(0, 16, (K // g, N)).float().bfloat16()
+    wd = ref.awq_dequant_ref(q, scales, zeros, g).to(DEV)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    res = torch.randn(M, N, device=DEV).bfloat16()
+    lin = ops.Linear(None, awq={"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV), "group": g})
+    y = ops.linear(x, lin, residual=res, splitk=sk)
+    assert _rel_err(y, ref.linear_ref(x, wd, None, res)) < 2e-2
+    y_ks = ops.linear(x, lin, residual=res, waves=4)
+    assert _rel_err(y, y_ks) < 1e-2
+    silu = ops.Linear(None, awq={"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV), "group": g,
+                                 "silu": True})
+    ys = ops.linear(x, silu, splitk=sk)
+    assert _rel_err(ys, ref.silu_mul_linear_ref(x, wd[: N // 2], wd[N // 2:])) < 2e-2
+
+
 @pytest.mark.parametrize("Hq,Hkv", [(12, 2), (32, 8), (64, 8)])
 def test_unified_attention_mixed_batch(Hq, Hkv):
     """decode rows (qlen 1, incl. split-K partitions) + prefill chunks in one launch."""

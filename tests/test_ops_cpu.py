@@ -36,8 +36,14 @@ def test_pack_awq_layout():
     word = int(p[((nt * (K // 128) + kq) * 64 + lane) * 4 + u]) & 0xFFFFFFFF
     row = 16 * nt + (lane & 15)
     k0 = 128 * kq + 32 * u + 8 * (lane >> 4)
-    vals = [(word >> (4 * j)) & 0xF for j in range(8)]
+    # value j at bit (16 if j odd) + 4 (j >> 1): (word >> 4d) & 0x000F000F holds values 2d, 2d+1
+    vals = [(word >> ((j & 1) * 16 + 4 * (j >> 1))) & 0xF for j in range(8)]
     assert vals == q[row, k0:k0 + 8].tolist()
+    for d in range(4):
+        pair = ((word >> (4 * d)) & 0x000F000F) | 0x43004300
+        lo = torch.tensor([pair & 0xFFFF], dtype=torch.int32).to(torch.int16).view(torch.bfloat16)
+        hi = torch.tensor([(pair >> 16) & 0xFFFF], dtype=torch.int32).to(torch.int16).view(torch.bfloat16)
+        assert lo.item() == 128 + vals[2 * d] and hi.item() == 128 + vals[2 * d + 1]
 
 
 def test_attention_ref_matches_dense():

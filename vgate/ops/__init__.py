@@ -76,13 +76,17 @@ def interleave_gate_up(w_gate: torch.Tensor, w_up: torch.Tensor) -> torch.Tensor
 
 
 def pack_awq(qint: torch.Tensor) -> torch.Tensor:
-    """int4 values [N, K] (0..15) -> int32 [N/16, K/128, 64, 4]; word u of lane l holds
-    W[16nt + (l&15)][128kq + 32u + 8(l>>4) + j] in nibble j."""
+    """int4 values [N, K] (0..15) -> int32 [N/16, K/128, 64, 4]; word u of lane l holds the 8
+    values W[16nt + (l&15)][128kq + 32u + 8(l>>4) + j], j = 0..7, with the EVEN j in the low
+    half-word and the odd j in the high one: value j at bit (16 if j odd) + 4 (j >> 1).
+    Then (word >> 4d) & 0x000F000F | 0x43004300 is the bf16 pair (128 + v_2d, 128 + v_2d+1):
+    two VALU ops per MFMA operand dword (gemm.hip, AWQ decode kernel)."""
     N, K = qint.shape
     assert N % 16 == 0 and K % 128 == 0
     q = qint.to(torch.int64).reshape(N // 16, 16, K // 128, 4, 4, 8)  # nt, r, kq, u, g, j
     q = q.permute(0, 2, 4, 1, 3, 5)  # nt, kq, g, r, u, j  -> lane = g*16 + r
-    shifts = (torch.arange(8, dtype=torch.int64, device=qint.device) * 4)
+    j = torch.arange(8, dtype=torch.int64, device=qint.device)
+    shifts = (j & 1) * 16 + (j >> 1) * 4
     words = (q << shifts).sum(-1)  # [nt, kq, g, r, u]
     words = words.reshape(N // 16, K // 128, 64, 4)
     words = torch.where(words >= 2**31, words - 2**32, words)
