@@ -149,6 +149,11 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
     # warmup (also captures the hipGraph buckets this load uses)
     if args.warmup > 0:
         await load(per_step * args.warmup, 10_000_000)
+    # buckets first seen during warmup ran eagerly; the engine captures them once idle
+    core = getattr(app.state.vgate.engine.backend, "engine", None)
+    t_cap = time.perf_counter()
+    while core is not None and core.runner.pending_captures and time.perf_counter() - t_cap < 120:
+        await asyncio.sleep(0.05)
     barrier()
     t0 = time.perf_counter()
     lat, fails, tokens, _ = await load(per_step * args.steps, 0)

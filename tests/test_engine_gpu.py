@@ -8,11 +8,15 @@ from vgate.runtime.sampling_params import SamplingParams
 pytestmark = pytest.mark.gpu
 
 
-def _engine(**kw):
+def _engine(defer_capture=False, **kw):
+    """defer_capture=False: capture each bucket on first use (every step replays a graph);
+    the serving default (True) runs first-seen buckets eagerly and captures them at idle."""
     cfg = dict(model="tiny", device="cuda", max_model_len=512, max_num_seqs=16, max_num_batched_tokens=256,
                num_kv_blocks=256, warmup=False, seed=0)
     cfg.update(kw)
-    return LLMEngine(EngineConfig(**cfg))
+    eng = LLMEngine(EngineConfig(**cfg))
+    eng.runner.defer_capture = defer_capture
+    return eng
 
 
 def _run(eng, reqs):
@@ -60,6 +64,22 @@ def test_sampling_path_and_no_kv_leak():
     assert all(len(s.output_ids) == 20 for s in out.values())
     assert eng.kvm.num_free() == eng.num_blocks
     assert len(eng.runner.graphs) > 0 and eng.runner.graph_hits > 0
+
+
+def test_deferred_capture_eager_then_graph():
+    """Serving default: a bucket first seen under load runs eagerly (no capture stall), is
+    captured once the engine idles, and later steps of that bucket replay the graph — with
+    the same tokens (greedy) as the capture-on-first-use engine."""
+    sp = SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True)
+    ref = _run(_engine(), [(k, v, sp) for k, v in PROMPTS.items()])
+    eng = _engine(defer_capture=True)
+    first = _run(eng, [(k, v, sp) for k, v in PROMPTS.items()])
+    assert eng.runner.graph_misses > 0 and not eng.runner.pending_captures and len(eng.runner.graphs) > 0
+    hits0 = eng.runner.graph_hits
+    again = _run(eng, [(k + "b", v, sp) for k, v in PROMPTS.items()])
+    assert eng.runner.graph_hits > hits0
+    for k in PROMPTS:
+        assert first[k].output_ids == ref[k].output_ids == again[k + "b"].output_ids, k
 
 
 def test_qwen_1p5b_shapes_run():

@@ -123,6 +123,9 @@ class LLMEngine:
         self._by_id: dict[str, Sequence] = {}
         self._seq_counter = 0
         self.healthy = True
+        # TP: every rank must capture at the same step (a capture's eager warm-up runs the
+        # collectives), so buckets are captured on first use there, not deferred to idle time
+        self.runner.defer_capture = self.tp.size == 1
         self.async_sched = bool(cfg.async_scheduling and self.device.type == "cuda" and self.tp.size == 1)
         self._inflight = None  # (batch, handle) of the launched, not yet post-processed step
         self._calls: collections.deque = collections.deque()  # (fn, future) run on the engine thread
@@ -218,14 +221,19 @@ class LLMEngine:
                 seq.aborted = True
                 self._finish(seq, "abort", notify_sched=False)
 
+    def _idle(self) -> bool:
+        return (not self._inbox and not self._aborts and not self.scheduler.has_work() and self._inflight is None
+                and not self._calls)
+
     def _loop(self) -> None:
         torch.set_grad_enabled(False)
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
         while self._running:
+            if self.runner.pending_captures and self._idle():
+                self.runner.capture_pending()  # buckets first seen under load (ran eagerly)
             with self._cv:
-                while (self._running and not self._inbox and not self._aborts and not self.scheduler.has_work()
-                       and self._inflight is None and not self._calls):
+                while self._running and self._idle():
                     self._cv.wait(timeout=0.5)
                 if not self._running:
                     break
@@ -304,6 +312,7 @@ class LLMEngine:
             n += 1
         if self.async_sched:
             self._drain_inflight()
+        self.runner.capture_pending()
 
     # -------------------------------------------------------------------- step
     def step(self) -> int:
@@ -536,6 +545,7 @@ class LLMEngine:
             "avg_gpu_ms": round(self.runner.gpu_ms / max(1, self.runner.gpu_steps), 3),
             "avg_host_ms": round(self.runner.host_ms / max(1, st.steps), 3),
             "graphs_captured": len(self.runner.graphs), "graph_hits": self.runner.graph_hits,
+            "graph_misses_eager": self.runner.graph_misses,
             "preemptions": self.scheduler.num_preemptions, "prefix_cache_hits": int(getattr(self.kvm.alloc, "hits", 0)),
             "healthy": self.healthy,
         }

@@ -80,6 +80,8 @@ class ModelRunner:
             self.out_hosts = [self.out_tokens]
         self.graph_hits = 0
         self.graph_misses = 0
+        self.defer_capture = True  # miss -> eager step now, capture at the next idle point
+        self.pending_captures: dict[tuple[int, int], int] = {}
         self.capture_seconds = 0.0
         self.gpu_ms = 0.0  # device time of replayed steps (upload -> sampled ids on host)
         self.host_ms = 0.0  # host time of execute() outside the device wait
@@ -208,21 +210,24 @@ class ModelRunner:
         self.meta.upload(ns)
         self.meta_copied[k].record()
         self._meta_pending[k] = True
-        if self.use_graphs:
-            key = (T, S)
-            g = self.graphs.get(key)
-            if g is None:
-                self.graph_misses += 1
-                # the capture's eager warm-up samples into out_tokens, which this step may
-                # still have to read (ids < 0): keep the previous step's samples aside
-                saved = self.out_tokens.clone()
-                g = self._capture(T, S)
-                self.out_tokens.copy_(saved)
-                self.graphs[key] = g
-            else:
-                self.graph_hits += 1
+        g = self.graphs.get((T, S)) if self.use_graphs else None
+        if g is None and self.use_graphs and not self.defer_capture:
+            # the capture's eager warm-up samples into out_tokens, which this step may
+            # still have to read (ids < 0): keep the previous step's samples aside
+            saved = self.out_tokens.clone()
+            g = self.graphs[(T, S)] = self._capture(T, S)
+            self.out_tokens.copy_(saved)
+        if g is not None:
+            self.graph_hits += 1
             g.replay()
         else:
+            if self.use_graphs:
+                # first sight of this bucket under load: run it eagerly (a few ms of launch
+                # overhead) and capture it when the engine is next idle (capture_pending) —
+                # a capture (eager warm-up + record, ~0.1-0.5 s) would stall every in-flight
+                # request behind this step
+                self.graph_misses += 1
+                self.pending_captures[(T, S)] = self.pending_captures.get((T, S), 0) + 1
             view = self.meta.view(T, S)
             view.num_tokens, view.num_seqs = nt, ns
             self._forward_sample(view)
@@ -289,6 +294,25 @@ class ModelRunner:
                 self.meta.upload(0)
                 self.graphs[(T, S)] = self._capture(T, S)
         return time.perf_counter() - t0
+
+    def capture_pending(self, max_graphs: int = 64) -> int:
+        """Capture the buckets that ran eagerly since the last call (most frequent first).
+        Call only with no step in flight: captures reuse the step-metadata buffers."""
+        if not self.use_graphs or not self.pending_captures:
+            return 0
+        keys = sorted(self.pending_captures, key=lambda k: -self.pending_captures[k])[:max_graphs]
+        t0 = time.perf_counter()
+        n = 0
+        for T, S in keys:
+            if (T, S) in self.graphs:
+                continue
+            self._fill_padding(T, S)
+            self.meta.upload(0)
+            self.graphs[(T, S)] = self._capture(T, S)
+            n += 1
+        self.pending_captures.clear()  # cleared last: non-empty means "capture still to come"
+        log.info("captured %d deferred hipGraph bucket(s) in %.2fs", n, time.perf_counter() - t0)
+        return n
 
     def _fill_padding(self, T, S):
         h = self.meta.h
