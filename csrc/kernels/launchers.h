@@ -49,6 +49,13 @@ struct GemmArgs {
 };
 void launch_gemm(const GemmArgs& g, hipStream_t st);
 
+// ---- custom one-shot all-reduce over xGMI peer memory (allreduce.hip) ----
+// bases[p]: rank p's IPC-mapped allocation = [AR_SIGNAL_BYTES signal area][2 x max_bytes data];
+// bf16 in/out (may alias), nbytes % 16 == 0, nbytes <= max_bytes
+constexpr int64_t AR_SIGNAL_BYTES = 65536;
+void launch_custom_allreduce(const void* in, void* out, int64_t nbytes, char* const* bases, int rank, int world,
+                             int64_t max_bytes, hipStream_t st);
+
 // ---- launch timeline (profiling; csrc/runtime/timeline.cpp, benchmarks/timeline.py) ----
 // While a timeline is active every launcher takes 2 x blocks u64 stamps for its kernel
 // (TLScope in common.h) and records (name, offset, blocks); null when inactive or full.

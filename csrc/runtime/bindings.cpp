@@ -4,6 +4,8 @@
 // HIP objects (csrc/kernels/*.hip) reached through csrc/kernels/launchers.h.
 // Every op launches on torch's current HIP stream, so ops are hipGraph
 // capturable via torch.cuda.graph / vgate.runtime.graphs.
+#include <cstring>
+
 #include <torch/extension.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
@@ -332,6 +334,63 @@ std::vector<std::tuple<std::string, int64_t, int64_t>> timeline_entries() {
   return r;
 }
 
+// ---- custom all-reduce: IPC-shared uncached buffers (vgate/parallel/custom_allreduce.py) ----
+#define HIP_OK(x) do { hipError_t e_ = (x); TORCH_CHECK(e_ == hipSuccess, #x ": ", hipGetErrorString(e_)); } while (0)
+
+int64_t ar_alloc(int64_t bytes) {
+  void* p = nullptr;
+  HIP_OK(hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached));
+  HIP_OK(hipMemset(p, 0, (size_t)bytes));
+  HIP_OK(hipDeviceSynchronize());
+  return reinterpret_cast<int64_t>(p);
+}
+
+void ar_free(int64_t ptr) { HIP_OK(hipFree(reinterpret_cast<void*>(ptr))); }
+
+Tensor ar_ipc_handle(int64_t ptr) {
+  hipIpcMemHandle_t h;
+  HIP_OK(hipIpcGetMemHandle(&h, reinterpret_cast<void*>(ptr)));
+  Tensor t = torch::empty({(int64_t)sizeof(h)}, torch::kUInt8);
+  std::memcpy(t.data_ptr(), &h, sizeof(h));
+  return t;
+}
+
+int64_t ar_open(const Tensor& handle) {
+  TORCH_CHECK(handle.numel() == (int64_t)sizeof(hipIpcMemHandle_t) && !handle.is_cuda(), "ar_open: 64-byte CPU handle");
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle.contiguous().data_ptr(), sizeof(h));
+  void* p = nullptr;
+  HIP_OK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+  return reinterpret_cast<int64_t>(p);
+}
+
+void ar_close(int64_t ptr) { HIP_OK(hipIpcCloseMemHandle(reinterpret_cast<void*>(ptr))); }
+
+// error word of the own signal area (a wait timed out); clears it
+int64_t ar_error(int64_t own_base) {
+  uint32_t v = 0, z = 0;
+  const size_t off = 64 * 8 * 4 + 64 * 4;  // ArSignal::error
+  HIP_OK(hipMemcpy(&v, reinterpret_cast<char*>(own_base) + off, 4, hipMemcpyDeviceToHost));
+  if (v) HIP_OK(hipMemcpy(reinterpret_cast<char*>(own_base) + off, &z, 4, hipMemcpyHostToDevice));
+  return v;
+}
+
+void custom_allreduce(const Tensor& inp, Tensor& out, const std::vector<int64_t>& bases, int64_t rank,
+                      int64_t max_bytes) {
+  CHECK_DEV(inp); CHECK_DEV(out);
+  CHECK_DT(inp, torch::kBFloat16); CHECK_DT(out, torch::kBFloat16);
+  TORCH_CHECK(inp.is_contiguous() && out.is_contiguous() && inp.numel() == out.numel(), "custom_allreduce: contiguous, same size");
+  const int64_t nbytes = inp.numel() * 2;
+  TORCH_CHECK(nbytes % 16 == 0 && nbytes <= max_bytes, "custom_allreduce: bytes ", nbytes, " (need %16, <= ", max_bytes, ")");
+  const int world = (int)bases.size();
+  TORCH_CHECK(world >= 1 && world <= 8 && rank >= 0 && rank < world, "custom_allreduce: world 1..8");
+  std::vector<char*> b(world);
+  for (int i = 0; i < world; ++i) b[i] = reinterpret_cast<char*>(bases[i]);
+  c10::DeviceGuard guard(inp.device());
+  vgate::launch_custom_allreduce(inp.data_ptr(), out.data_ptr(), nbytes, b.data(), (int)rank, world, max_bytes,
+                                 cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -362,6 +421,14 @@ PYBIND11_MODULE(_C, m) {
         py::arg("offsets"), py::arg("out"), py::arg("out_logprob") = py::none(), py::arg("ws") = py::none());
   m.def("prefetch", &prefetch, "read a tensor once with the default cache policy (MALL warm-up)",
         py::arg("t"), py::arg("blocks") = 256);
+  m.def("ar_alloc", &ar_alloc, "uncached device allocation for the custom all-reduce (zeroed)");
+  m.def("ar_free", &ar_free);
+  m.def("ar_ipc_handle", &ar_ipc_handle, "hipIpcMemHandle of an ar_alloc pointer (64 bytes, CPU uint8)");
+  m.def("ar_open", &ar_open, "map a peer's ar_alloc buffer (hipIpcOpenMemHandle)");
+  m.def("ar_close", &ar_close);
+  m.def("ar_error", &ar_error, "read-and-clear the wait-timeout word of the own signal area");
+  m.def("custom_allreduce", &custom_allreduce, "one-shot bf16 all-reduce over IPC-mapped peer buffers",
+        py::arg("inp"), py::arg("out"), py::arg("bases"), py::arg("rank"), py::arg("max_bytes"));
   m.def("timeline_start", &timeline_start, "start a launch timeline in an int64 device buffer (zero it first)");
   m.def("timeline_stop", &vgate::tl_stop, "stop handing out timeline slots; returns the slots used");
   m.def("timeline_entries", &timeline_entries, "(kernel, offset, blocks) per launch since timeline_start");

@@ -85,3 +85,26 @@ def test_tp2_matches_tp1(tmp_path):
     assert not errs, errs[0]
     tp_out = next(r[1] for r in results if r[1] is not None)
     assert tp_out == ref
+
+
+def test_tp_group_routes_small_allreduce_to_custom_ar():
+    """TPGroup.all_reduce: a tensor the custom all-reduce accepts goes to it (one-shot xGMI
+    kernel, tests/test_custom_allreduce_gpu.py), anything else to torch.distributed."""
+    import torch
+
+    from vgate.parallel.comm import TPGroup
+
+    class FakeAR:
+        def __init__(self):
+            self.seen = []
+
+        def should_use(self, t):
+            return t.numel() <= 16
+
+        def all_reduce(self, t):
+            self.seen.append(t.numel())
+            return t.mul_(2)
+
+    g = TPGroup(rank=0, size=2, group=None, backend="nccl", custom_ar=FakeAR())
+    t = torch.ones(8)
+    assert g.all_reduce(t) is t and t.tolist() == [2.0] * 8 and g.custom_ar.seen == [8]

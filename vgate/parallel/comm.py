@@ -5,7 +5,7 @@ only two collectives per transformer layer (after the row-parallel o_proj and
 down_proj) plus one all-reduce after the vocab-parallel embedding and one
 all-gather of the vocab-sharded logits — the Megatron layout of SURVEY.md §2.3.1.
 
-Small decode-sized all-reduces (<= ``custom_ar_max_bytes``) go to the custom
+Small decode-sized all-reduces (<= ``VGATE_CUSTOM_AR_MAX_BYTES``, 4 MiB) go to the custom
 one-shot xGMI kernel (:mod:`vgate.parallel.custom_allreduce`) when it is
 available (all ranks on one node with peer access); larger ones, and every
 collective under the gloo backend (CPU tests), go through torch.distributed.
@@ -104,6 +104,12 @@ def init_tp(tp_size: int, backend: str | None = None) -> TPGroup:
         if rank in ranks:
             grp = g
     _TP = TPGroup(rank=rank % tp_size, size=tp_size, group=grp, backend=backend)
+    if backend == "nccl" and os.environ.get("VGATE_CUSTOM_AR", "1") != "0":
+        from vgate.parallel.custom_allreduce import maybe_create
+
+        dev = torch.device("cuda", torch.cuda.current_device())
+        _TP.custom_ar = maybe_create(grp, _TP.rank, tp_size, dev,
+                                     max_bytes=int(os.environ.get("VGATE_CUSTOM_AR_MAX_BYTES", str(4 << 20))))
     return _TP
 
 

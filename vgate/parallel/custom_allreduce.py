@@ -1,0 +1,120 @@
+"""Custom one-shot all-reduce over xGMI peer memory for decode-sized TP collectives.
+
+Each rank owns one uncached device allocation (``ar_alloc``: a signal area plus two
+``max_bytes`` data buffers); the ranks exchange ``hipIpcMemHandle``s once over the
+process group and map every peer's buffer (``ar_open``). A call launches ONE kernel
+(``csrc/kernels/allreduce.hip``): each block copies its slice of the input into the own
+buffer, flags its arrival in every peer's signal area, waits for the peers' flags, and
+sums that slice over all ranks straight out of the peers' memory — every xGMI link is
+used at once and there is a single synchronisation, where a ring pays 2(n-1) dependent
+hops. Large messages (prefill) stay on RCCL (:class:`vgate.parallel.comm.TPGroup`).
+
+Launches take fixed addresses and keep their epoch counters on the device, so the
+all-reduce is captured into the decode hipGraphs like every other kernel.
+
+Reference parity: the reference has no GPU collectives at all; this
+is the MI355X-native data plane the TP engine needs.
+"""
+from __future__ import annotations
+
+import logging
+
+import torch
+import torch.distributed as dist
+
+log = logging.getLogger("vgate.parallel")
+
+SIGNAL_BYTES = 65536  # csrc/kernels/launchers.h AR_SIGNAL_BYTES
+MAX_RANKS = 8
+
+
+class CustomAllReduce:
+    """One per TP group and device. ``should_use(t)`` says whether ``t`` qualifies (bf16,
+    contiguous, 16-byte multiple, <= max_bytes); ``all_reduce(t)`` reduces in place."""
+
+    def __init__(self, group, rank: int, world: int, device: torch.device, max_bytes: int = 8 << 20):
+        from vgate import ops
+
+        if not 2 <= world <= MAX_RANKS:
+            raise ValueError(f"custom all-reduce supports 2..{MAX_RANKS} ranks, got {world}")
+        self.C = ops.native()
+        self.rank, self.world, self.device = rank, world, device
+        self.max_bytes = int(max_bytes)
+        self.own, self.bases, self._opened = None, [], []
+        mine = None
+        try:
+            with torch.cuda.device(device):
+                self.own = self.C.ar_alloc(SIGNAL_BYTES + 2 * self.max_bytes)
+                mine = bytes(self.C.ar_ipc_handle(self.own).numpy().tobytes())
+        except Exception as e:  # noqa: BLE001 - reported through the gather, so no rank waits
+            log.warning("custom all-reduce allocation failed: %s: %s", type(e).__name__, e)
+        handles = [None] * world
+        dist.all_gather_object(handles, mine, group=group)
+        if any(h is None for h in handles):
+            self.close()
+            raise RuntimeError("custom all-reduce setup failed: a rank could not allocate / export its buffer")
+        err = None
+        try:
+            with torch.cuda.device(device):
+                for p, h in enumerate(handles):
+                    if p == rank:
+                        self.bases.append(self.own)
+                    else:
+                        ptr = self.C.ar_open(torch.frombuffer(bytearray(h), dtype=torch.uint8))
+                        self._opened.append(ptr)
+                        self.bases.append(ptr)
+        except Exception as e:  # noqa: BLE001 - agreed on below, so no rank waits for a failed one
+            err = f"{type(e).__name__}: {e}"
+        errs = [None] * world
+        dist.all_gather_object(errs, err, group=group)  # also: every rank mapped every buffer
+        if any(errs):
+            self.close()
+            raise RuntimeError(f"custom all-reduce setup failed: {[e for e in errs if e]}")
+        self.calls = 0
+
+    def should_use(self, t: torch.Tensor) -> bool:
+        nbytes = t.numel() * t.element_size()
+        return (t.dtype == torch.bfloat16 and t.is_contiguous() and t.device == self.device and nbytes % 16 == 0
+                and 0 < nbytes <= self.max_bytes)
+
+    def all_reduce(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        out = t if out is None else out
+        self.C.custom_allreduce(t, out, self.bases, self.rank, self.max_bytes)
+        self.calls += 1
+        return out
+
+    def check(self) -> None:
+        """Raise if a wait timed out since the last check (a peer never arrived)."""
+        if self.C.ar_error(self.own):
+            raise RuntimeError("custom all-reduce: a peer did not arrive within the spin limit")
+
+    def close(self) -> None:
+        if self.own is None:
+            return
+        torch.cuda.synchronize(self.device)
+        for ptr in self._opened:
+            self.C.ar_close(ptr)
+        self.C.ar_free(self.own)
+        self.own, self._opened = None, []
+
+
+def maybe_create(group, rank: int, world: int, device: torch.device, max_bytes: int = 8 << 20):
+    """The custom all-reduce when every rank of ``group`` is a GPU of this node with peer
+    access, else None (callers fall back to RCCL)."""
+    if world < 2 or world > MAX_RANKS or device.type != "cuda":
+        return None
+    ok = True
+    n = torch.cuda.device_count()
+    for d in range(n):
+        if d != device.index and not torch.cuda.can_device_access_peer(device.index, d):
+            ok = False
+    flags = [None] * world
+    dist.all_gather_object(flags, ok, group=group)
+    if not all(flags):
+        log.info("custom all-reduce disabled: no peer access between all ranks")
+        return None
+    try:
+        return CustomAllReduce(group, rank, world, device, max_bytes)
+    except Exception as e:  # noqa: BLE001 - fall back to RCCL, loudly
+        log.warning("custom all-reduce unavailable (%s: %s); using RCCL for every all-reduce", type(e).__name__, e)
+        return None
