@@ -44,10 +44,12 @@ def _generate(eng):
     return done
 
 
-def _worker(rank, world, port, path, q):
+def _worker(rank, world, port, path, q, overlap_min=None):
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                           MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if overlap_min is not None:  # row-chunked row-parallel GEMMs + per-chunk all-reduce
+            os.environ.update(VGATE_TP_OVERLAP_MIN_TOKENS=str(overlap_min), VGATE_TP_OVERLAP_CHUNKS="3")
         torch.set_num_threads(1)
         eng = LLMEngine(_cfg(path, world))
         assert eng.tp.size == world and eng.tp.rank == rank
@@ -64,7 +66,8 @@ def _worker(rank, world, port, path, q):
 
 
 @pytest.mark.timeout(300)
-def test_tp2_matches_tp1(tmp_path):
+@pytest.mark.parametrize("overlap_min", [None, 16])
+def test_tp2_matches_tp1(tmp_path, overlap_min):
     ref_eng = LLMEngine(EngineConfig(model="tiny", device="cpu", max_model_len=256, max_num_seqs=8,
                                      max_num_batched_tokens=64, num_kv_blocks=128, warmup=False, seed=0))
     path = str(tmp_path / "ckpt")
@@ -75,7 +78,7 @@ def test_tp2_matches_tp1(tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, path, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, path, q, overlap_min)) for r in range(2)]
     for p in procs:
         p.start()
     results = [q.get(timeout=240) for _ in procs]

@@ -95,6 +95,12 @@ class DecoderModel:
         table_len = max(max_model_len, 16) + 1
         self.cos_sin = ops.ref.rope_cos_sin(table_len, arch.head_dim, arch.rope_theta, arch.rope_scaling,
                                             device=self.device)
+        # TP comm/compute overlap for long steps (prefill): row-parallel GEMMs run in row
+        # chunks and chunk i's all-reduce runs on a side stream while chunk i+1's GEMM runs
+        self.tp_overlap_chunks = int(os.environ.get("VGATE_TP_OVERLAP_CHUNKS", "4"))
+        self.tp_overlap_min_tokens = int(os.environ.get("VGATE_TP_OVERLAP_MIN_TOKENS", "256"))
+        self.comm_stream = (torch.cuda.Stream(self.device)
+                            if self.device.type == "cuda" and self.tp.size > 1 else None)
 
     def fold_norms(self) -> int:
         """Fold every RMSNorm weight into the packed matrix of the GEMM that consumes it
@@ -121,6 +127,41 @@ class DecoderModel:
         return n
 
     # ---------------------------------------------------------------- forward
+    def _row_parallel(self, x: torch.Tensor, lin, resid: torch.Tensor, first: bool) -> None:
+        """resid = all_reduce(x @ W^T [+ resid on TP rank 0]) for a row-parallel linear
+        (o_proj / down_proj). With TP and >= tp_overlap_min_tokens rows the GEMM runs in
+        row chunks (multiples of 16) and each chunk's all-reduce is issued on the comm
+        stream as soon as that chunk is written, so RCCL (or the custom xGMI kernel) moves
+        chunk i while the MFMA GEMM computes chunk i+1; the main stream joins the comm
+        stream before the next layer reads ``resid``. Fork/join through events, so the
+        pattern is captured into the prefill hipGraphs as well."""
+        tp = self.tp
+        T = x.shape[0]
+        nch = self.tp_overlap_chunks if tp.size > 1 and T >= self.tp_overlap_min_tokens else 1
+        if nch <= 1:
+            ops.linear(x, lin, out=resid, residual=resid if first else None)
+            if tp.size > 1:
+                tp.all_reduce(resid)
+            return
+        bounds = sorted({min(T, 16 * ((T * i // nch + 15) // 16)) for i in range(nch)} | {T})
+        if bounds[0] != 0:
+            bounds.insert(0, 0)
+        side = self.comm_stream if resid.is_cuda else None
+        main = torch.cuda.current_stream(resid.device) if side is not None else None
+        for a, b in zip(bounds[:-1], bounds[1:]):
+            r = resid[a:b]
+            ops.linear(x[a:b], lin, out=r, residual=r if first else None)
+            if side is None:
+                tp.all_reduce(r)
+                continue
+            ev = torch.cuda.Event()
+            ev.record(main)
+            with torch.cuda.stream(side):
+                side.wait_event(ev)
+                tp.all_reduce(r)
+        if side is not None:
+            main.wait_stream(side)
+
     def forward(self, sv, kv_caches, part_size: int, return_hidden: bool = False) -> torch.Tensor:
         """One step. ``sv`` is a StepView (token/seq metadata views, bucket sizes T and S).
 
@@ -157,13 +198,9 @@ class DecoderModel:
                                 v_cache=vc, hq=sh.hq, hkv=sh.hkv))
             ops.attention(q, sh.hq * D, kc, vc, sv.block_tables, sv.context_lens, sv.query_start, sv.tile_seq,
                           sv.tile_q0, attn, part_o, part_ml, sh.hq, sh.hkv, part_size, self.scale)
-            ops.linear(attn, L.o, out=resid, residual=resid if first else None)
-            if tp.size > 1:
-                tp.all_reduce(resid)
+            self._row_parallel(attn, L.o, resid, first)
             ops.linear(resid, L.gate_up, out=mlp, norm=(L.post_norm, eps))
-            ops.linear(mlp, L.down, out=resid, residual=resid if first else None)
-            if tp.size > 1:
-                tp.all_reduce(resid)
+            self._row_parallel(mlp, L.down, resid, first)
         if return_hidden:
             return resid
         logits = ops.linear(resid, self.lm_head, out_f32=True, norm=(self.final_norm, eps), row_idx=sv.sample_idx)
@@ -193,14 +230,10 @@ class DecoderModel:
             ops.linear(x, L.qkv, out=qkv)
             ops.rope_kv(qkv, sv.positions, sv.slots, self.cos_sin, kc, vc, sh.hq, sh.hkv, D)
             self._attention_cpu(qkv, attn, kc, vc, sv)
-            ops.linear(attn, L.o, out=resid, residual=resid if first else None)
-            if tp.size > 1:
-                tp.all_reduce(resid)
+            self._row_parallel(attn, L.o, resid, first)
             ops.rmsnorm(resid, L.post_norm, a.rms_eps, out=x)
             ops.linear(x, L.gate_up, out=mlp)
-            ops.linear(mlp, L.down, out=resid, residual=resid if first else None)
-            if tp.size > 1:
-                tp.all_reduce(resid)
+            self._row_parallel(mlp, L.down, resid, first)
         if return_hidden:
             return resid
         xs = resid.index_select(0, sv.sample_idx.long())
