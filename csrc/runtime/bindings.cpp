@@ -12,6 +12,7 @@
 
 #include "../kernels/launchers.h"
 #include "allocator.h"
+#include "lru_cache.h"
 
 namespace {
 
@@ -433,4 +434,28 @@ PYBIND11_MODULE(_C, m) {
   m.def("timeline_stop", &vgate::tl_stop, "stop handing out timeline slots; returns the slots used");
   m.def("timeline_entries", &timeline_entries, "(kernel, offset, blocks) per launch since timeline_start");
   vgate::bind_runtime(m);
+  py::class_<vgate::ShardedLRU>(m, "ShardedLRU", "sharded LRU of bytes values (result cache backend 'native')")
+      .def(py::init<int64_t, int64_t>(), py::arg("capacity"), py::arg("shards") = 16)
+      .def("get", [](vgate::ShardedLRU& c, const std::string& k) -> py::object {
+             std::optional<std::string> v;
+             {
+               py::gil_scoped_release nogil;
+               v = c.get(k);
+             }
+             if (!v) return py::none();
+             return py::bytes(*v);
+           })
+      .def("put", [](vgate::ShardedLRU& c, const std::string& k, py::bytes v) {
+             std::string val = v;  // copied under the GIL
+             py::gil_scoped_release nogil;
+             return c.put(k, std::move(val));
+           })
+      .def("erase", &vgate::ShardedLRU::erase, py::call_guard<py::gil_scoped_release>())
+      .def("clear", &vgate::ShardedLRU::clear, py::call_guard<py::gil_scoped_release>())
+      .def("__len__", &vgate::ShardedLRU::size)
+      .def_property_readonly("capacity", &vgate::ShardedLRU::capacity)
+      .def_property_readonly("num_shards", &vgate::ShardedLRU::num_shards)
+      .def_property_readonly("hits", &vgate::ShardedLRU::hits)
+      .def_property_readonly("misses", &vgate::ShardedLRU::misses)
+      .def_property_readonly("evictions", &vgate::ShardedLRU::evictions);
 }

@@ -24,10 +24,20 @@ tracer = get_tracer(__name__)
 
 
 class ResultCache:
-    def __init__(self, maxsize: Optional[int] = None, enabled: Optional[bool] = None):
+    def __init__(self, maxsize: Optional[int] = None, enabled: Optional[bool] = None,
+                 backend: Optional[str] = None):
         cfg = get_config()
         self.maxsize = maxsize if maxsize is not None else cfg.cache.maxsize
         self.enabled = enabled if enabled is not None else cfg.cache.enabled
+        self.backend = (backend or getattr(cfg.cache, "backend", "python")).lower()
+        self._native = None
+        if self.backend == "native":
+            # C++ sharded LRU (csrc/runtime/lru_cache.h): values stored as JSON bytes, so a
+            # hit is a fresh object by construction (no deepcopy)
+            from vgate import ops
+            self._native = ops.native().ShardedLRU(max(0, self.maxsize), int(getattr(cfg.cache, "shards", 16)))
+        elif self.backend != "python":
+            raise ValueError(f"cache.backend must be python or native, got {self.backend!r}")
         self._data: OrderedDict[str, dict] = OrderedDict()
         self._lock = asyncio.Lock()
         self.hits = 0
@@ -44,6 +54,17 @@ class ResultCache:
         if not self.enabled:
             return None
         with tracer.start_as_current_span("cache.get") as span:
+            if self._native is not None:
+                raw = self._native.get(key)
+                hit = raw is not None
+                span.set_attribute("hit", hit)
+                if not hit:
+                    self.misses += 1
+                    CACHE_MISSES.inc()
+                    return None
+                self.hits += 1
+                CACHE_HITS.inc()
+                return json.loads(raw)
             async with self._lock:
                 val = self._data.get(key)
                 if val is None:
@@ -61,6 +82,13 @@ class ResultCache:
         if not self.enabled or self.maxsize <= 0:
             return
         with tracer.start_as_current_span("cache.put"):
+            if self._native is not None:
+                ev = self._native.put(key, json.dumps(value, separators=(",", ":")).encode())
+                if ev:
+                    self.evictions += ev
+                    CACHE_EVICTIONS.inc(ev)
+                CACHE_SIZE.set(len(self._native))
+                return
             async with self._lock:
                 if key in self._data:
                     self._data.move_to_end(key)
@@ -73,14 +101,16 @@ class ResultCache:
                 CACHE_SIZE.set(len(self._data))
 
     async def clear(self) -> None:
+        if self._native is not None:
+            self._native.clear()
         async with self._lock:
             self._data.clear()
             CACHE_SIZE.set(0)
 
     def __len__(self) -> int:
-        return len(self._data)
+        return len(self._native) if self._native is not None else len(self._data)
 
     def get_stats(self) -> dict[str, Any]:
         total = self.hits + self.misses
-        return {"size": len(self._data), "maxsize": self.maxsize, "hits": self.hits, "misses": self.misses,
+        return {"size": len(self), "maxsize": self.maxsize, "hits": self.hits, "misses": self.misses,
                 "evictions": self.evictions, "hit_rate": round(self.hits / total, 4) if total else 0.0}

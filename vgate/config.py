@@ -136,6 +136,10 @@ class BatchConfig(_Section):
 class CacheConfig(_Section):
     enabled: bool = True
     maxsize: int = 1000
+    # "python": OrderedDict LRU (reference semantics); "native": C++ sharded LRU of JSON bytes
+    # (vgate._C.ShardedLRU, per-shard locks, GIL released) — LRU order is per shard
+    backend: str = "python"
+    shards: int = 16
 
 
 class InferenceConfig(_Section):
