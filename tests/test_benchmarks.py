@@ -79,3 +79,30 @@ def test_load_generator_streaming(server):
     assert r["throughput"]["content_chunks"] > 0
     assert r["throughput"]["total_tokens"] > 0  # from the server's vgate_stream_tokens_total
     assert r["latency"]["ttft_p50_s"] > 0
+
+
+@pytest.mark.timeout(300)
+def test_scenario_cli_and_aggregate(tmp_path):
+    """run_scenario_cli (one scenario, fresh dry-run server process) -> JSON, twice, then
+    aggregate_results -> one report (reference _run_scenario_cli.py / _aggregate_results.py)."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    out = tmp_path / "sc"
+    for name in ("baseline", "cache_impact"):
+        r = subprocess.run([sys.executable, str(root / "benchmarks/run_scenario_cli.py"), name, "--engine", "dry-run",
+                            "--requests", "8", "--concurrency", "4", "--max-tokens", "4", "--port", "18770",
+                            "--dry-latency-ms", "2", "--out-dir", str(out)],
+                           capture_output=True, text=True, timeout=240, cwd=str(root))
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert json.loads(r.stdout.strip().splitlines()[-1])["scenario"] == name
+    r = subprocess.run([sys.executable, str(root / "benchmarks/aggregate_results.py"), str(out)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    rep = json.loads((out / "report.json").read_text())
+    assert list(rep) == ["baseline", "cache_impact"]
+    assert rep["baseline"]["throughput"]["requests_per_second"] > 0
+    assert "| baseline |" in (out / "report.md").read_text()
