@@ -251,8 +251,11 @@ __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, in
   {
     float* ow = opart + wid * (16 * D_);
     const int g = lane >> 4;
+    // 16-B chunk k of query column c lives at chunk k ^ c of its row: the 16 columns of one
+    // store (same k) land in 16 different bank groups (unswizzled, every column's row starts
+    // on the same bank: a 16-way conflict, profiles/r1_pmc_sq.txt)
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt) *reinterpret_cast<f32x4*>(ow + col * D_ + 16 * mt + 4 * g) = o[mt];
+    for (int mt = 0; mt < 8; ++mt) *reinterpret_cast<f32x4*>(ow + col * D_ + 4 * ((4 * mt + g) ^ col)) = o[mt];
     if (lane < 16) {
       mlp[(wid * 16 + lane) * 2] = m;
       mlp[(wid * 16 + lane) * 2 + 1] = l;
@@ -275,8 +278,9 @@ __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, in
       if (!(wl > 0.f)) continue;
       const float e = __builtin_amdgcn_exp2f(mlp[(w * 16 + icol) * 2] - Mref);
       L += wl * e;
-      const float* src = opart + w * (16 * D_) + icol * D_ + d0;
-      const f32x4 v0 = *reinterpret_cast<const f32x4*>(src), v1 = *reinterpret_cast<const f32x4*>(src + 4);
+      const float* row = opart + w * (16 * D_) + icol * D_;
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(row + 4 * ((d0 >> 2) ^ icol));
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(row + 4 * (((d0 >> 2) + 1) ^ icol));
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         acc[j] += e * v0[j];
