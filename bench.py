@@ -195,7 +195,12 @@ def main():
                     help="run the load loop in a separate client process (default: in the server process; "
                          "measured slower on the 1-GPU box: 68 vs 81 req/s, profiles/r1_bench_client_modes.log)")
     ap.add_argument("--client-proc", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--switch-interval-us", type=float,
+                    default=float(os.environ.get("VGATE_SWITCH_INTERVAL_US", "0")),
+                    help="sys.setswitchinterval for the server process (0 = Python default 5 ms)")
     args = ap.parse_args()
+    if args.switch_interval_us > 0:
+        sys.setswitchinterval(args.switch_interval_us * 1e-6)
     if args.client_proc:
         client_loop()
         return

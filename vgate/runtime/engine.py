@@ -32,6 +32,7 @@ from vgate.runtime.sampling_params import SamplingParams
 from vgate.runtime.scheduler import Scheduler
 from vgate.runtime.sequence import PENDING, Sequence, SeqStatus
 from vgate.runtime.tokenizer import IncrementalDecoder, load_tokenizer
+from vgate.utils.profiling import range_
 
 log = logging.getLogger("vgate.engine")
 
@@ -126,6 +127,7 @@ class LLMEngine:
         # TP: every rank must capture at the same step (a capture's eager warm-up runs the
         # collectives), so buckets are captured on first use there, not deferred to idle time
         self.runner.defer_capture = self.tp.size == 1
+        self.capture_idle_s = 0.05
         self.async_sched = bool(cfg.async_scheduling and self.device.type == "cuda" and self.tp.size == 1)
         self._inflight = None  # (batch, handle) of the launched, not yet post-processed step
         self._calls: collections.deque = collections.deque()  # (fn, future) run on the engine thread
@@ -231,10 +233,23 @@ class LLMEngine:
             torch.cuda.set_device(self.device)
         while self._running:
             if self.runner.pending_captures and self._idle():
-                self.runner.capture_pending()  # buckets first seen under load (ran eagerly)
+                # buckets first seen under load ran eagerly; capture them once the engine has
+                # stayed idle for a moment (not in the microseconds between two requests of a
+                # running load), one bucket at a time, re-checking for new work in between
+                with self._cv:
+                    self._cv.wait_for(lambda: not self._running or not self._idle(), timeout=self.capture_idle_s)
+                if self._running and self._idle():
+                    try:
+                        self.runner.capture_pending(max_graphs=1)
+                    except Exception:  # noqa: BLE001 - those buckets keep running eagerly
+                        log.exception("deferred hipGraph capture failed")
+                        self.runner.defer_capture_failed = True
+                        self.runner.pending_captures.clear()
             with self._cv:
-                while self._running and self._idle():
+                while self._running and self._idle() and not self.runner.pending_captures:
                     self._cv.wait(timeout=0.5)
+                if self._idle():
+                    continue  # idle with captures pending: back to the capture check
                 if not self._running:
                     break
                 self._drain_inbox()
@@ -338,15 +353,17 @@ class LLMEngine:
 
     def _step_async(self) -> int:
         tc = time.perf_counter()
-        batch = self.scheduler.schedule(no_preempt=self._inflight is not None)
-        if batch.kv_pressure:  # preemption needs every placeholder resolved first
-            self._drain_inflight()
-            batch = self.scheduler.schedule()
+        with range_("vgate.schedule"):
+            batch = self.scheduler.schedule(no_preempt=self._inflight is not None)
+            if batch.kv_pressure:  # preemption needs every placeholder resolved first
+                self._drain_inflight()
+                batch = self.scheduler.schedule()
         if batch.empty:
             self._drain_inflight()
             return 0
         pend = {seq.seq_id: seq.pending_slot for seq, _ in batch.items if seq.pending}
-        h = self.runner.launch(batch, pend)
+        with range_("vgate.launch"):
+            h = self.runner.launch(batch, pend)
         for i, ((seq, n), smp) in enumerate(zip(batch.items, h.samples)):
             seq.num_computed += n
             if smp:
@@ -365,8 +382,10 @@ class LLMEngine:
 
     def _complete(self, entry) -> None:
         batch, h, tc = entry
-        toks = self.runner.collect(h)
-        self._process(batch, toks, h.samples, h.t_launch, tc, resolve=True)
+        with range_("vgate.collect"):
+            toks = self.runner.collect(h)
+        with range_("vgate.process"):
+            self._process(batch, toks, h.samples, h.t_launch, tc, resolve=True)
 
     def _process(self, batch, toks, samples, t0: float, tc: float, resolve: bool) -> None:
         """Post-process one executed step: append (or resolve) sampled tokens, stop checks,

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import bisect
 import logging
+import os
 import time
 from dataclasses import dataclass
 
@@ -28,12 +29,28 @@ import torch
 from vgate import ops
 from vgate.runtime.scheduler import ScheduledBatch
 from vgate.runtime.step_meta import StepMeta
+from vgate.utils.profiling import range_
 
 log = logging.getLogger("vgate.engine")
 
 DEFAULT_T_BUCKETS = [1, 2, 4, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256, 384, 512, 768, 1024, 1536, 2048,
                      3072, 4096, 6144, 8192, 12288, 16384]
 DEFAULT_S_BUCKETS = [1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024]
+
+
+class _GraphRing:
+    """Identical captures of one bucket; each replay() launches the next one in turn."""
+
+    __slots__ = ("execs", "i")
+
+    def __init__(self, execs):
+        self.execs = execs
+        self.i = 0
+
+    def replay(self) -> None:
+        g = self.execs[self.i]
+        self.i = (self.i + 1) % len(self.execs)
+        g.replay()
 
 
 @dataclass
@@ -81,7 +98,13 @@ class ModelRunner:
         self.graph_hits = 0
         self.graph_misses = 0
         self.defer_capture = True  # miss -> eager step now, capture at the next idle point
+        # execs per bucket, replayed round-robin. In isolation back-to-back launches of ONE
+        # hipGraphExec leave ~0.1 ms between them and alternating two identical execs ~0.015 ms
+        # (benchmarks/graph_relaunch_probe.py), but the engine's step loop (event records +
+        # a D2H copy between replays) shows no difference (88.9 req/s either way): default 1
+        self.graph_copies = max(1, int(os.environ.get("VGATE_GRAPH_COPIES", "1")))
         self.pending_captures: dict[tuple[int, int], int] = {}
+        self.defer_capture_failed = False  # a deferred capture raised: stop queueing more
         self.capture_seconds = 0.0
         self.gpu_ms = 0.0  # device time of replayed steps (upload -> sampled ids on host)
         self.host_ms = 0.0  # host time of execute() outside the device wait
@@ -163,6 +186,10 @@ class ModelRunner:
         return logits
 
     def _capture(self, T: int, S: int):
+        with range_(f"vgate.capture T={T} S={S}"):
+            return self._capture_impl(T, S)
+
+    def _capture_impl(self, T: int, S: int):
         t0 = time.perf_counter()
         view = self.meta.view(T, S)
         # warm-up (eager) on the capture stream, then capture
@@ -172,15 +199,18 @@ class ModelRunner:
             self._forward_sample(view)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
-        with torch.cuda.graph(g, pool=self.pool, stream=s):
-            self._forward_sample(view)
+        execs = []
+        for _ in range(self.graph_copies):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.pool, stream=s):
+                self._forward_sample(view)
+            execs.append(g)
         torch.cuda.synchronize()
         self.capture_seconds += time.perf_counter() - t0
         log.debug("captured hipGraph T=%d S=%d in %.1f ms", T, S, 1e3 * (time.perf_counter() - t0))
-        return g
+        return execs[0] if len(execs) == 1 else _GraphRing(execs)
 
     @torch.inference_mode()
     def execute(self, batch: ScheduledBatch) -> tuple[list[int], list[bool]]:
@@ -221,7 +251,7 @@ class ModelRunner:
             self.graph_hits += 1
             g.replay()
         else:
-            if self.use_graphs:
+            if self.use_graphs and not self.defer_capture_failed:
                 # first sight of this bucket under load: run it eagerly (a few ms of launch
                 # overhead) and capture it when the engine is next idle (capture_pending) —
                 # a capture (eager warm-up + record, ~0.1-0.5 s) would stall every in-flight
@@ -304,13 +334,12 @@ class ModelRunner:
         t0 = time.perf_counter()
         n = 0
         for T, S in keys:
-            if (T, S) in self.graphs:
-                continue
-            self._fill_padding(T, S)
-            self.meta.upload(0)
-            self.graphs[(T, S)] = self._capture(T, S)
-            n += 1
-        self.pending_captures.clear()  # cleared last: non-empty means "capture still to come"
+            if (T, S) not in self.graphs:
+                self._fill_padding(T, S)
+                self.meta.upload(0)
+                self.graphs[(T, S)] = self._capture(T, S)
+                n += 1
+            del self.pending_captures[(T, S)]  # removed last: present means "capture still to come"
         log.info("captured %d deferred hipGraph bucket(s) in %.2fs", n, time.perf_counter() - t0)
         return n
 
