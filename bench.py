@@ -94,7 +94,10 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
         model={"model_id": args.model, "quantization": args.quantization, "engine_type": "native",
                "random_init": True, "max_model_len": 2048, "max_num_seqs": 256,
                "max_num_batched_tokens": 2048, "num_kv_blocks": args.kv_blocks, "enforce_eager": args.eager,
-               "device": f"cuda:{local}" if torch.cuda.is_available() else "cpu", "seed": 1234 + rank},
+               # device_count() does not initialise HIP: with --engine-process the parent must
+               # not touch the GPU before it spawns the engine core
+               "device": f"cuda:{local}" if torch.cuda.device_count() > 0 else "cpu", "seed": 1234 + rank,
+               "engine_process": bool(args.engine_process)},
         batch={"max_batch_size": args.concurrency},
         cache={"enabled": True, "maxsize": 1000},
         logging={"level": "WARNING", "json_format": True},
@@ -150,9 +153,11 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
     if args.warmup > 0:
         await load(per_step * args.warmup, 10_000_000)
     # buckets first seen during warmup ran eagerly; the engine captures them once idle
-    core = getattr(app.state.vgate.engine.backend, "engine", None)
+    backend = app.state.vgate.engine.backend
+    stats = getattr(backend, "stats", None)
     t_cap = time.perf_counter()
-    while core is not None and core.runner.pending_captures and time.perf_counter() - t_cap < 120:
+    await asyncio.sleep(0.3)  # the engine core's stats snapshot is pushed every 0.25 s
+    while callable(stats) and stats().get("pending_captures", 0) and time.perf_counter() - t_cap < 120:
         await asyncio.sleep(0.05)
     barrier()
     t0 = time.perf_counter()
@@ -191,6 +196,8 @@ def main():
     ap.add_argument("--eager", action="store_true")
     ap.add_argument("--port", type=int, default=18100)
     ap.add_argument("--security", action="store_true", help="bearer auth + rate limiter on the request path")
+    ap.add_argument("--engine-process", action="store_true",
+                    help="run the engine core in its own process (model.engine_process)")
     ap.add_argument("--client-process", action="store_true",
                     help="run the load loop in a separate client process (default: in the server process; "
                          "measured slower on the 1-GPU box: 68 vs 81 req/s, profiles/r1_bench_client_modes.log)")
@@ -244,7 +251,8 @@ def main():
             "data": f"synthetic unique prompts, random-init weights ({model_name} architecture)",
             "config": {"model": model_name, "quantization": args.quantization or "none",
                        "security_rate_limiter": bool(args.security),
-                       "load_client": "separate process" if args.client_process else "in-process", "global_batch": args.concurrency * world,
+                       "load_client": "separate process" if args.client_process else "in-process",
+                       "engine_core": "separate process" if args.engine_process else "in-process", "global_batch": args.concurrency * world,
                        "seq_len": args.max_tokens, "parallelism": f"dp{world}",
                        "concurrency_per_gpu": args.concurrency, "max_tokens": args.max_tokens,
                        "requests_per_step_per_gpu": args.requests_per_step},

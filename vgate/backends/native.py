@@ -55,6 +55,10 @@ class NativeBackend:
     def load_model(self, model_config: ModelConfig) -> None:
         from vgate.runtime.engine import LLMEngine
         cfg = engine_config_from(model_config)
+        if getattr(model_config, "engine_process", False) and cfg.tensor_parallel_size == 1:
+            from vgate.runtime.engine_process import EngineProcessClient
+            self.engine = EngineProcessClient(cfg)
+            return
         self.engine = LLMEngine(cfg)
         if self.engine.tp.size > 1 and not self.engine.tp.is_first:
             # TP followers never serve HTTP: they execute rank 0's steps until shutdown

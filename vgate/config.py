@@ -91,6 +91,8 @@ class ModelConfig(_Section):
     dtype: str = "bfloat16"
     device: str = "auto"
     random_init: bool = True
+    # run the engine core in its own process (no GIL shared with the HTTP event loop); TP=1 only
+    engine_process: bool = False
     weights_path: Optional[str] = None
     tokenizer: Optional[str] = None
     seed: int = 0

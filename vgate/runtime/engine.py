@@ -565,6 +565,7 @@ class LLMEngine:
             "avg_host_ms": round(self.runner.host_ms / max(1, st.steps), 3),
             "graphs_captured": len(self.runner.graphs), "graph_hits": self.runner.graph_hits,
             "graph_misses_eager": self.runner.graph_misses,
+            "pending_captures": len(self.runner.pending_captures),
             "preemptions": self.scheduler.num_preemptions, "prefix_cache_hits": int(getattr(self.kvm.alloc, "hits", 0)),
             "healthy": self.healthy,
         }
