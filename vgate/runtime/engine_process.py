@@ -1,11 +1,9 @@
 """The engine core in its own process (``model.engine_process: true``).
 
 In-process, the engine thread shares one GIL with the HTTP event loop (uvicorn/h11
-parsing, pydantic validation, batcher, cache, metrics): every time the engine thread
-returns from a device call it may wait for the loop to yield the interpreter, and those
-waits sit between a step's metadata upload and its graph launch — measured as +0.12 ms
-per decode step (1.52 vs 1.40 ms, bench.py vs benchmarks/bench_engine.py). Here the
-:class:`vgate.runtime.engine.LLMEngine` runs in a child process (spawned before the
+parsing, pydantic validation, batcher, cache, metrics) and a fault in the engine takes the
+API server with it. Here the :class:`vgate.runtime.engine.LLMEngine` runs in a child
+process (spawned before the
 parent touches the GPU) and the API process talks to it over one duplex pipe:
 
   parent -> child   ("add", rid, prompt, prompt_ids, params, stream) | ("abort", rid)
@@ -19,7 +17,9 @@ use (add_request with callbacks, abort, embed, snapshot, healthy, stop), so
 :class:`SeqView` carrying the fields the backend reads. This mirrors the reference's
 vLLM deployment, whose EngineCore also runs in a separate process
 (reference benchmarks/run_report.py:89-93). TP > 1 keeps the in-process engine (rank 0
-drives its followers directly).
+drives its followers directly). Measured on the MI355X headline bench: equal throughput
+to the in-process engine (profiles/r1_engine_process_vs_inprocess.log) — the GIL is not
+the bottleneck at this load — so it is opt-in, for isolation.
 """
 from __future__ import annotations
 
