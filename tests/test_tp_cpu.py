@@ -111,3 +111,43 @@ def test_tp_group_routes_small_allreduce_to_custom_ar():
     g = TPGroup(rank=0, size=2, group=None, backend="nccl", custom_ar=FakeAR())
     t = torch.ones(8)
     assert g.all_reduce(t) is t and t.tolist() == [2.0] * 8 and g.custom_ar.seen == [8]
+
+
+def _failing_worker(rank, world, port, path, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), VGATE_TP_TIMEOUT_S="20")
+    torch.set_num_threads(1)
+    eng = LLMEngine(_cfg(path, world))
+    if rank == 1:
+        def boom(*a, **k):
+            raise RuntimeError("injected follower fault")
+        eng._run_step = boom
+        eng.follower_loop()  # exits the process with status 1
+        q.put(("returned", None))
+        return
+    try:
+        _generate(eng)
+        q.put(("rank0", "no error"))
+    except Exception as e:  # noqa: BLE001 - expected: the peer is gone
+        q.put(("rank0", type(e).__name__))
+
+
+@pytest.mark.timeout(300)
+def test_tp_follower_fault_tears_down_group(tmp_path):
+    """a TP group is one failure domain — a follower fault exits that rank
+    (status 1) and rank 0's next collective fails instead of hanging."""
+    ref_eng = LLMEngine(EngineConfig(model="tiny", device="cpu", max_model_len=256, max_num_seqs=8,
+                                     max_num_batched_tokens=64, num_kv_blocks=128, warmup=False, seed=0))
+    path = str(tmp_path / "ckpt")
+    save_checkpoint(ref_eng.model, path)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_failing_worker, args=(r, 2, port, path, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    procs[1].join(timeout=200)
+    assert procs[1].exitcode == 1
+    kind, val = q.get(timeout=200)
+    assert kind == "rank0" and val != "no error", (kind, val)
+    procs[0].join(timeout=60)

@@ -90,8 +90,12 @@ def init_tp(tp_size: int, backend: str | None = None) -> TPGroup:
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if not dist.is_initialized():
+        from datetime import timedelta
+
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend=backend)
+        # a hung collective (dead peer) fails after VGATE_TP_TIMEOUT_S instead of torch's 10 min
+        dist.init_process_group(backend=backend,
+                                timeout=timedelta(seconds=float(os.environ.get("VGATE_TP_TIMEOUT_S", "120"))))
     world = dist.get_world_size()
     rank = dist.get_rank()
     if world % tp_size:

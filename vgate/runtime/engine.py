@@ -532,6 +532,17 @@ class LLMEngine:
         import torch.distributed as dist
         torch.set_grad_enabled(False)
         r = self.runner
+        try:
+            self._follow(r, dist)
+        except BaseException:  # noqa: BLE001 - a TP group is one failure domain
+            # rank 0 would otherwise wait in its next collective until the process-group
+            # timeout: exit now, so the launcher (torchrun) tears the whole group down and the
+            # gateway's health checks take this worker out of rotation
+            log.exception("TP follower rank %d failed; exiting so the TP group is torn down", self.tp.rank)
+            logging.shutdown()
+            os._exit(1)
+
+    def _follow(self, r, dist) -> None:
         while True:
             hdr = torch.zeros(3, dtype=torch.int64, device=self.device if self.tp.backend == "nccl" else "cpu")
             dist.broadcast(hdr, src=self._tp_src(), group=self.tp.group)
