@@ -629,6 +629,14 @@ template <int NTW, int EPI, int NORM>
 __global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   TLScope tl_scope(p.dbg_ts);
+  // profiling: phase stamps of the first and the last block after the per-block slots
+  // (benchmarks/awq_phases.py; the launcher reserves 8 extra slot pairs)
+  const size_t nblk = (size_t)gridDim.x * gridDim.y * gridDim.z;
+  const size_t bid = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  unsigned long long* ph = (p.dbg_ts != nullptr && threadIdx.x == 0 && (bid == 0 || bid == nblk - 1))
+                               ? p.dbg_ts + 2 * nblk + (bid == 0 ? 0 : 8) : nullptr;
+#define AD_PHASE(i) do { if (ph != nullptr) ph[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+  AD_PHASE(0);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int KQ = p.K >> 7;
   const int nt0 = (blockIdx.x * AD_WAVES + wid) * NTW;  // this wave's first 16-column tile
@@ -735,6 +743,7 @@ __global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
       if (lane < 16) ssq[wid * 16 + lane] = ss;
     }
     lds_barrier();  // LDS image visible; the weight loads stay in flight
+    AD_PHASE(1);
     // per (k-quad, row) sum of the staged (bf16) activations, fixed order
     for (int idx = threadIdx.x; idx < nq * 16; idx += blockDim.x) {
       const int ql = idx >> 4, r = idx & 15;
@@ -751,6 +760,7 @@ __global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
       xsum[idx] = sacc;
     }
     lds_barrier();
+    AD_PHASE(2);
     int g = 0;
     for (; g + 2 <= ngrp; g += 2) {
       load_grp(wb, sb, zb, kq + AD_G);
@@ -761,6 +771,7 @@ __global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
     }
     if (g < ngrp) mma_grp(wa, sa, za, kq);
   }
+  AD_PHASE(3);
   // 3) finish: lane holds D[n = 4(l>>4) + i][m = l & 15] of each tile
   float ss_slice = 0.f;  // this slice's row sum of squares (fixed wave order)
   if constexpr (NORM != 0) {
@@ -777,6 +788,7 @@ __global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
   };
   if (p.splitk == 1) {
     finish(acc, ss_slice);
+    AD_PHASE(4);
     return;
   }
   const int grp = blockIdx.x;  // column group: AD_WAVES * NTW tiles
@@ -796,6 +808,7 @@ __global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
     *flag = last;
   }
   __syncthreads();
+  AD_PHASE(4);
   if (!*flag) return;
   const float* all = p.slabs + (size_t)grp * p.splitk * SLAB;
   f32x4 v[NTW];
@@ -809,6 +822,8 @@ __global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
   if constexpr (NORM != 0)
     for (int z = 0; z < p.splitk; ++z) ss_row += ld_sc1(all + (size_t)z * SLAB + SLOTS * 4 + m);
   finish(v, ss_row);
+  AD_PHASE(5);
+#undef AD_PHASE
 }
 
 // ---- prefill / medium-M tile GEMM (M > 16, bf16 weights) ----
@@ -1031,7 +1046,7 @@ static bool launch_awq_dec(GemmParams p, const GemmArgs& g, hipStream_t st) {
   const int qmax = (KQ + sk - 1) / sk;
   const size_t lds = (size_t)qmax * 4 * 64 * 16 + (size_t)qmax * 16 * 4 + 4 * 16 * 4 + 16;
   if (lds > 150 * 1024) return false;
-  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_dec", groups * sk);
+  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_dec", groups * sk + 8);  // + phase stamps
   hipLaunchKernelGGL((awq_dec_kernel<NTB, EPI, NORM>), dim3(groups, 1, sk), dim3(64 * AD_WAVES), lds, st, p);
   return true;
 }
