@@ -150,3 +150,21 @@ def test_awq_engine_generates():
     assert all(len(s.output_ids) == 12 for s in out.values())
     assert all(0 <= t < eng.arch.vocab_size for s in out.values() for t in s.output_ids)
     assert eng.model.weight_bytes() < _engine().model.weight_bytes()
+
+
+def test_long_prompt_library_prefill_matches_reference():
+    """A 300-token prompt is prefilled in steps of >= 128 tokens, which take the hipBLASLt
+    library path (plain weight copies + separate epilogues); greedy tokens are still the
+    (near-)argmax of the dense fp32 model, teacher-forced, and equal the eager engine's."""
+    from vgate import ops
+    long_prompt = [3 + (j * 29) % 500 for j in range(300)]
+    sp = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
+    eng = _engine()
+    assert eng.model.library_prefill and ops.LIBRARY_MIN_M <= 256
+    g = _run(eng, [("long", long_prompt, sp)])["long"].output_ids
+    e = _run(_engine(enforce_eager=True), [("long", long_prompt, sp)])["long"].output_ids
+    assert g == e
+    logits = eng.model.reference_logits(long_prompt + g[:-1])[len(long_prompt) - 1:]
+    for t, tok in enumerate(g):
+        row = logits[t]
+        assert row[tok] >= row.max() - 0.05 * row.std(), t

@@ -90,6 +90,7 @@ class DecoderModel:
         else:
             from vgate.models.weights import random_init
             random_init(self, seed)
+        self.library_prefill = self._keep_library_copies()
         if self.device.type == "cuda" and os.environ.get("VGATE_FOLD_NORM", "1") != "0":
             self.fold_norms()
         table_len = max(max_model_len, 16) + 1
@@ -101,6 +102,19 @@ class DecoderModel:
         self.tp_overlap_min_tokens = int(os.environ.get("VGATE_TP_OVERLAP_MIN_TOKENS", "256"))
         self.comm_stream = (torch.cuda.Stream(self.device)
                             if self.device.type == "cuda" and self.tp.size > 1 else None)
+
+    def _keep_library_copies(self) -> bool:
+        """Plain weight copies for hipBLASLt prefill GEMMs (ops.linear, M >= 128).
+        VGATE_PREFILL_BLAS: 1 = on, 0 = off, auto (default) = on when the copies take at most
+        10% of the device's memory (Qwen2.5-1.5B 3.1 GB, Llama-3-8B 14 GB; not 70B on one GPU)."""
+        mode = os.environ.get("VGATE_PREFILL_BLAS", "auto")
+        if self.device.type != "cuda" or mode == "0" or self.quant:
+            return False
+        lins = [lin for L in self.layers for lin in (L.qkv, L.o, L.gate_up, L.down)]
+        extra = sum(lin.N * lin.K * 2 for lin in lins)
+        if mode != "1" and extra > 0.1 * torch.cuda.get_device_properties(self.device).total_memory:
+            return False
+        return all([lin.keep_library_copy() for lin in lins])
 
     def fold_norms(self) -> int:
         """Fold every RMSNorm weight into the packed matrix of the GEMM that consumes it

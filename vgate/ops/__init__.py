@@ -132,6 +132,7 @@ class Linear:
         self.kind = "awq" if awq is not None else "dense"
         self.bias = bias
         self.norm_gamma = None  # RMSNorm weight folded into the packed copy (see fold_norm)
+        self.wl = None  # optional plain [N, K] copy for library (hipBLASLt) prefill GEMMs
         if self.kind == "awq":
             q = awq["qint"]
             self.N, self.K = q.shape
@@ -171,7 +172,19 @@ class Linear:
             return False
         g = gamma.to(self.wp.device, torch.float32).reshape(1, self.K // 32, 4, 1, 8)
         self.wp.copy_((self.wp.float() * g).to(torch.bfloat16))
+        if self.wl is not None:
+            self.wl.copy_((self.wl.float() * gamma.to(self.wl.device, torch.float32)[None]).to(torch.bfloat16))
         self.norm_gamma = gamma.detach().clone()
+        return True
+
+    def keep_library_copy(self) -> bool:
+        """Keep a plain [N, K] bf16 copy (original row order) for long prefill steps, which
+        go to hipBLASLt + separate epilogues: at M >= 128 the library MFMA GEMM is 1.3-3x
+        faster than the fragment-packed decode/tile kernels (benchmarks/prefill_blas_probe.py,
+        profiles/r1_prefill_blas_probe.log). Call before fold_norm. Dense GPU weights only."""
+        if self.kind != "dense" or self.wp is None or self.norm_gamma is not None:
+            return False
+        self.wl = self.dense_weight().contiguous()
         return True
 
     @property
@@ -195,6 +208,7 @@ class Linear:
         return w
 
     def nbytes(self) -> int:
+        """Bytes a decode step streams (the library copy is prefill-only)."""
         if self.kind == "awq" and self.w is None:
             return self.wp.numel() * 4 + self.scales.numel() * 4
         t = self.wp if self.wp is not None else self.w
@@ -247,6 +261,8 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
         else:
             out.copy_(ref.linear_ref(xx, wd, lin.bias, residual, out_f32))
         return out
+    if lin.wl is not None and M >= LIBRARY_MIN_M and row_idx is None and not out_f32:
+        return _linear_library(x, lin, out, residual, norm, qkv)
     C = native()
     epi = 3 if qkv is not None else (2 if silu else (1 if out_f32 else 0))
     kw = dict(bias=lin.bias, res=residual, ws=workspace(x.device), waves=waves, splitk=splitk)
@@ -263,6 +279,45 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
     if lin.kind == "awq":
         kw.update(awq_scales=lin.scales, awq_zeros=lin.zeros, group=lin.group)
     C.gemm(x, lin.wp, lin.N, lin.K, out, epi, **kw)
+    return out
+
+
+LIBRARY_MIN_M = int(os.environ.get("VGATE_PREFILL_BLAS_MIN_M", "128"))
+_ONES: dict = {}
+
+
+def _linear_library(x, lin: Linear, out, residual, norm, qkv):
+    """Long-step (prefill) path of :func:`linear`: RMSNorm kernel -> hipBLASLt GEMM on the
+    plain weight copy -> bias / SiLU*mul / RoPE + KV write / residual as separate ops. Same
+    math as the fused kernels up to bf16 rounding of the GEMM output before the epilogue."""
+    xx = x
+    if norm is not None:
+        if lin.norm_gamma is not None:  # gamma is folded into wl: unit-weight RMSNorm
+            key = (str(x.device), lin.K)
+            ones = _ONES.get(key)
+            if ones is None:
+                ones = _ONES[key] = torch.ones(lin.K, dtype=torch.bfloat16, device=x.device)
+            xx = rmsnorm(x[:, :lin.K], ones, float(norm[1]))
+        else:
+            xx = rmsnorm(x[:, :lin.K], norm[0], float(norm[1]))
+    elif x.shape[1] != lin.K:
+        xx = x[:, :lin.K]
+    y = torch.matmul(xx, lin.wl.t())
+    if lin.bias is not None:
+        y += lin.bias
+    if lin.layout == "silu":
+        I = lin.N // 2
+        out.copy_(torch.nn.functional.silu(y[:, :I].float()) * y[:, I:].float())
+        return out
+    if qkv is not None:
+        rope_kv(y, qkv["positions"], qkv["slots"], qkv["cos_sin"], qkv["k_cache"], qkv["v_cache"],
+                qkv["hq"], qkv["hkv"], 128)
+        out.copy_(y[:, : qkv["hq"] * 128])
+        return out
+    if residual is not None:
+        torch.add(y, residual, out=out)
+    else:
+        out.copy_(y)
     return out
 
 
