@@ -39,9 +39,11 @@ def main():
     ap.add_argument("--model", default="Qwen/Qwen2.5-1.5B-Instruct")
     ap.add_argument("--lens", type=int, nargs="+", default=[512, 2048, 4096])
     ap.add_argument("--chunk", type=int, default=2048)
+    ap.add_argument("--quantization", default=None)
     a = ap.parse_args()
     eng = LLMEngine(EngineConfig(model=a.model, max_model_len=max(a.lens) + 16, max_num_seqs=16,
-                                 max_num_batched_tokens=a.chunk, num_kv_blocks=4096))
+                                 max_num_batched_tokens=a.chunk, num_kv_blocks=4096,
+                                 quantization=a.quantization))
     eng.start()
     for L in a.lens:
         ids = [100 + (j * 7919) % 30000 for j in range(L)]
@@ -49,7 +51,7 @@ def main():
         time.sleep(0.5)  # idle: deferred captures
         ts = [one(eng, f"r{L}-{i}", [t + i + 1 for t in ids]) for i in range(3)]
         print(json.dumps({"model": a.model.split("/")[-1], "prompt_len": L, "chunk": a.chunk,
-                          "prefill_blas": os.environ.get("VGATE_PREFILL_BLAS", "auto"),
+                          "prefill_blas": os.environ.get("VGATE_PREFILL_BLAS", "auto"), "quantization": a.quantization,
                           "library_prefill": eng.model.library_prefill,
                           "ttft_ms": round(1e3 * min(ts), 2), "prefill_tok_s": round(L / min(ts))}), flush=True)
     eng.stop()

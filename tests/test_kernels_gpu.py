@@ -644,3 +644,27 @@ def test_library_prefill_path_matches_reference(M, fold):
     ref.rope_kv_ref(qkv, pos, slots, cs, kc2, vc2, hq, hkv, D)
     assert _rel_err(q, qkv[:, : hq * D]) < 2e-2
     assert _rel_err(kc, kc2) < 2e-2 and _rel_err(vc, vc2) < 2e-2
+
+
+@pytest.mark.parametrize("layout", ["plain", "silu"])
+def test_awq_library_prefill_path(layout):
+    """AWQ linear at M >= LIBRARY_MIN_M: the once-dequantized plain copy + hipBLASLt ==
+    the dequantised fp32 reference (the W4A16 kernels have no M > 16 tile path)."""
+    torch.manual_seed(60)
+    M, N, K, g = 256, 2048, 1536, 128
+    q = torch.randint(0, 16, (N, K), dtype=torch.int32)
+    scales = (torch.rand(K // g, N) * 0.02 + 0.005).bfloat16()
+    zeros = torch.randint(0, 16, (K // g, N)).float().bfloat16()
+    wd = ref.awq_dequant_ref(q, scales, zeros, g).to(DEV)
+    lin = ops.Linear(None, awq={"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV), "group": g,
+                                "silu": layout == "silu"})
+    assert lin.keep_library_copy()
+    assert _rel_err(lin.wl.float(), wd.float()) < 1e-2
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    nw = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+    y = ops.linear(x, lin, norm=(nw, 1e-6))
+    xn, _ = ref.rmsnorm_ref(x, nw, 1e-6)
+    if layout == "silu":
+        assert _rel_err(y, ref.silu_mul_linear_ref(xn, wd[: N // 2], wd[N // 2:])) < 2e-2
+    else:
+        assert _rel_err(y, ref.linear_ref(xn, wd)) < 2e-2

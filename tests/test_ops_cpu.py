@@ -97,3 +97,9 @@ def test_native_allocator_if_built():
     c = a.allocate(8)
     assert len(set(c)) == 8
     assert a.lookup(h) == -1
+
+
+def test_unpack_awq_inverts_pack():
+    torch.manual_seed(3)
+    q = torch.randint(0, 16, (48, 384), dtype=torch.int32)
+    assert torch.equal(ops.unpack_awq(ops.pack_awq(q), 48, 384), q)

@@ -108,7 +108,7 @@ class DecoderModel:
         VGATE_PREFILL_BLAS: 1 = on, 0 = off, auto (default) = on when the copies take at most
         10% of the device's memory (Qwen2.5-1.5B 3.1 GB, Llama-3-8B 14 GB; not 70B on one GPU)."""
         mode = os.environ.get("VGATE_PREFILL_BLAS", "auto")
-        if self.device.type != "cuda" or mode == "0" or self.quant:
+        if self.device.type != "cuda" or mode == "0":
             return False
         lins = [lin for L in self.layers for lin in (L.qkv, L.o, L.gate_up, L.down)]
         extra = sum(lin.N * lin.K * 2 for lin in lins)

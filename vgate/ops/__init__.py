@@ -75,6 +75,16 @@ def interleave_gate_up(w_gate: torch.Tensor, w_up: torch.Tensor) -> torch.Tensor
     return torch.stack([w_gate.reshape(I // 16, 16, K), w_up.reshape(I // 16, 16, K)], 1).reshape(2 * I, K)
 
 
+def unpack_awq(packed: torch.Tensor, N: int, K: int) -> torch.Tensor:
+    """Inverse of :func:`pack_awq`: int32 [N/16, K/128, 64, 4] -> int4 values [N, K] (int32)."""
+    w = packed.to(torch.int64) & 0xFFFFFFFF
+    w = w.reshape(N // 16, K // 128, 4, 16, 4)  # nt, kq, g, r, u
+    j = torch.arange(8, dtype=torch.int64, device=packed.device)
+    shifts = (j & 1) * 16 + (j >> 1) * 4
+    q = (w[..., None] >> shifts) & 0xF  # nt, kq, g, r, u, j
+    return q.permute(0, 3, 1, 4, 2, 5).reshape(N, K).to(torch.int32)
+
+
 def pack_awq(qint: torch.Tensor) -> torch.Tensor:
     """int4 values [N, K] (0..15) -> int32 [N/16, K/128, 64, 4]; word u of lane l holds the 8
     values W[16nt + (l&15)][128kq + 32u + 8(l>>4) + j], j = 0..7, with the EVEN j in the low
@@ -181,9 +191,22 @@ class Linear:
         """Keep a plain [N, K] bf16 copy (original row order) for long prefill steps, which
         go to hipBLASLt + separate epilogues: at M >= 128 the library MFMA GEMM is 1.3-3x
         faster than the fragment-packed decode/tile kernels (benchmarks/prefill_blas_probe.py,
-        profiles/r1_prefill_blas_probe.log). Call before fold_norm. Dense GPU weights only."""
-        if self.kind != "dense" or self.wp is None or self.norm_gamma is not None:
+        profiles/r1_prefill_blas_probe.log). Call before fold_norm. GPU weights only; AWQ
+        weights are dequantized once (the W4A16 kernels have no M > 16 tile path: prefill of
+        an AWQ model was 4.6x slower than bf16, profiles/r1_ttft_awq.log)."""
+        if self.wp is None or self.norm_gamma is not None:
             return False
+        if self.kind == "awq":
+            q = unpack_awq(self.wp, self.N, self.K)  # permuted row order, like scales / zeros
+            g = torch.arange(self.K, device=q.device) // self.group
+            w = (q.float() * self.scales.float()[g].t() - self.zeros.float()[g].t()).to(torch.bfloat16)
+            perm = row_permutation(self.N, self.layout)
+            if perm is not None:
+                out = torch.empty_like(w)
+                out[perm.to(w.device)] = w
+                w = out
+            self.wl = w.contiguous()
+            return True
         self.wl = self.dense_weight().contiguous()
         return True
 
@@ -261,7 +284,8 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
         else:
             out.copy_(ref.linear_ref(xx, wd, lin.bias, residual, out_f32))
         return out
-    if lin.wl is not None and M >= LIBRARY_MIN_M and row_idx is None and not out_f32:
+    if (lin.wl is not None and M >= (LIBRARY_MIN_M_AWQ if lin.kind == "awq" else LIBRARY_MIN_M) and row_idx is None
+            and not out_f32):
         return _linear_library(x, lin, out, residual, norm, qkv)
     C = native()
     epi = 3 if qkv is not None else (2 if silu else (1 if out_f32 else 0))
@@ -283,6 +307,9 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
 
 
 LIBRARY_MIN_M = int(os.environ.get("VGATE_PREFILL_BLAS_MIN_M", "128"))
+# the W4A16 kernels are decode kernels (no tile path above M = 16): hand AWQ steps to the
+# library copy earlier
+LIBRARY_MIN_M_AWQ = int(os.environ.get("VGATE_PREFILL_BLAS_MIN_M_AWQ", "32"))
 _ONES: dict = {}
 
 
