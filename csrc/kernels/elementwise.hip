@@ -1,6 +1,8 @@
 // Memory-bound kernels: RMSNorm (+fused residual add), embedding gather,
 // NeoX RoPE + paged KV-cache write. All bf16 traffic is 16-B vectorised
 // (cdna_hip_programming.md Guideline 13); trig comes from a host-built table.
+#include <algorithm>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -111,7 +113,8 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ qkv,
                                                        const float* __restrict__ cos_sin,
                                                        bf16_t* __restrict__ k_cache,
                                                        bf16_t* __restrict__ v_cache, int Hq,
-                                                       int Hkv, int D, int BS) {
+                                                       int Hkv, int D, int BS, bf16_t* __restrict__ q_out,
+                                                       int ldq) {
   const int t = blockIdx.x;
   const int pos = positions[t];
   const int slot = slots ? slots[t] : -1;
@@ -145,8 +148,14 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ qkv,
     uint2 p1, p2;
     p1.x = pack_bf2(o1[0], o1[1]); p1.y = pack_bf2(o1[2], o1[3]);
     p2.x = pack_bf2(o2[0], o2[1]); p2.y = pack_bf2(o2[2], o2[3]);
-    *reinterpret_cast<uint2*>(base + i0) = p1;
-    *reinterpret_cast<uint2*>(base + half + i0) = p2;
+    if (q_out == nullptr) {  // in place
+      *reinterpret_cast<uint2*>(base + i0) = p1;
+      *reinterpret_cast<uint2*>(base + half + i0) = p2;
+    } else if (h < Hq) {  // rotated q straight into the attention input (k only goes to the cache)
+      bf16_t* qd = q_out + (size_t)t * ldq + h * D;
+      *reinterpret_cast<uint2*>(qd + i0) = p1;
+      *reinterpret_cast<uint2*>(qd + half + i0) = p2;
+    }
     if (h >= Hq && slot >= 0) {
       const int kh = h - Hq;
       bf16_t* dst = k_cache + (((size_t)blk * Hkv + kh) * BS + off) * D;
@@ -168,10 +177,35 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ qkv,
 
 void launch_rope_kv(uint16_t* qkv, const int32_t* positions, const int32_t* slots,
                     const float* cos_sin, uint16_t* k_cache, uint16_t* v_cache, int T, int Hq,
-                    int Hkv, int D, int BS, hipStream_t st) {
+                    int Hkv, int D, int BS, hipStream_t st, uint16_t* q_out, int ldq) {
   if (T <= 0) return;
   hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(256), 0, st, qkv, positions, slots, cos_sin,
-                     k_cache, v_cache, Hq, Hkv, D, BS);
+                     k_cache, v_cache, Hq, Hkv, D, BS, q_out, ldq);
+}
+
+// out[m, i] = silu(y[m, i]) * y[m, I + i] (fp32 math, bf16 out): the SiLU*mul epilogue of the
+// library (hipBLASLt) gate_up GEMM. 8 columns per thread, 16-B accesses; I % 8 == 0.
+__global__ __launch_bounds__(256) void silu_mul_kernel(const bf16_t* __restrict__ y, int ldy, bf16_t* __restrict__ out,
+                                                       int ldo, int I, int M) {
+  const int per_row = I >> 3;
+  const size_t n = (size_t)M * per_row;
+  for (size_t it = (size_t)blockIdx.x * blockDim.x + threadIdx.x; it < n; it += (size_t)gridDim.x * blockDim.x) {
+    const int m = (int)(it / per_row), c = (int)(it % per_row) * 8;
+    const bf16_t* r = y + (size_t)m * ldy;
+    float g[8], u[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(r + c), g);
+    unpack8(*reinterpret_cast<const uint4*>(r + I + c), u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = g[j] / (1.f + __expf(-g[j])) * u[j];
+    *reinterpret_cast<uint4*>(out + (size_t)m * ldo + c) = pack8(o);
+  }
+}
+
+void launch_silu_mul(const uint16_t* y, int ldy, uint16_t* out, int ldo, int I, int M, hipStream_t st) {
+  if (M <= 0 || I <= 0) return;
+  const size_t n = (size_t)M * (I >> 3);
+  const int blocks = (int)std::min<size_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(silu_mul_kernel, dim3(blocks), dim3(256), 0, st, y, ldy, out, ldo, I, M);
 }
 
 // Read-only sweep of a byte range with the DEFAULT cache policy (not nt): the lines land in

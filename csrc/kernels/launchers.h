@@ -84,7 +84,9 @@ void launch_prefetch(const void* p, size_t bytes, int blocks, hipStream_t st);
 // k_cache/v_cache: [num_blocks, Hkv, BS, D]; slot < 0 => skip write.
 void launch_rope_kv(uint16_t* qkv, const int32_t* positions, const int32_t* slots,
                     const float* cos_sin, uint16_t* k_cache, uint16_t* v_cache, int T, int Hq,
-                    int Hkv, int D, int BS, hipStream_t st);
+                    int Hkv, int D, int BS, hipStream_t st,
+                    uint16_t* q_out = nullptr, int ldq = 0);
+void launch_silu_mul(const uint16_t* y, int ldy, uint16_t* out, int ldo, int I, int M, hipStream_t st);
 
 struct AttnArgs {
   const uint16_t* q;  // [T, Hq, D] with row stride q_stride (elements, per token)

@@ -155,7 +155,7 @@ void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vsta
 
 void rope_kv(Tensor& qkv, const Tensor& positions, const c10::optional<Tensor>& slots,
              const Tensor& cos_sin, Tensor& k_cache, Tensor& v_cache, int64_t Hq, int64_t Hkv,
-             int64_t D) {
+             int64_t D, const c10::optional<Tensor>& q_out) {
   CHECK_DEV(qkv); CHECK_DEV(positions); CHECK_DEV(cos_sin);
   CHECK_DT(qkv, torch::kBFloat16); CHECK_DT(positions, torch::kInt32);
   CHECK_DT(cos_sin, torch::kFloat32);
@@ -168,11 +168,32 @@ void rope_kv(Tensor& qkv, const Tensor& positions, const c10::optional<Tensor>& 
   }
   const int BS = (int)k_cache.size(2);
   TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == D, "rope_kv: cache shape");
+  uint16_t* qo = nullptr;
+  int ldq = 0;
+  if (q_out.has_value() && q_out->defined()) {
+    CHECK_DEV(*q_out); CHECK_DT(*q_out, torch::kBFloat16); CHECK_LASTDIM(*q_out);
+    TORCH_CHECK(q_out->dim() == 2 && q_out->size(0) >= qkv.size(0) && q_out->size(1) >= Hq * D, "rope_kv: q_out shape");
+    qo = reinterpret_cast<uint16_t*>(q_out->data_ptr());
+    ldq = (int)q_out->stride(0);
+  }
   c10::DeviceGuard guard(qkv.device());
   vgate::launch_rope_kv(bf16p_mut(qkv), reinterpret_cast<const int32_t*>(positions.data_ptr()), sp,
                         reinterpret_cast<const float*>(cos_sin.data_ptr()), bf16p_mut(k_cache),
                         bf16p_mut(v_cache), (int)qkv.size(0), (int)Hq, (int)Hkv, (int)D, BS,
-                        cur_stream());
+                        cur_stream(), qo, ldq);
+}
+
+// out [M, I] = silu(y[:, :I]) * y[:, I:2I]
+void silu_mul(const Tensor& y, Tensor& out) {
+  CHECK_DEV(y); CHECK_DEV(out);
+  CHECK_DT(y, torch::kBFloat16); CHECK_DT(out, torch::kBFloat16);
+  CHECK_LASTDIM(y); CHECK_LASTDIM(out);
+  const int64_t I = out.size(1);
+  TORCH_CHECK(y.dim() == 2 && out.dim() == 2 && y.size(1) == 2 * I && out.size(0) == y.size(0) && I % 8 == 0,
+              "silu_mul: y [M, 2I], out [M, I], I % 8 == 0");
+  c10::DeviceGuard guard(y.device());
+  vgate::launch_silu_mul(bf16p(y), (int)y.stride(0), bf16p_mut(out), (int)out.stride(0), (int)I, (int)y.size(0),
+                         cur_stream());
 }
 
 vgate::AttnArgs attn_common(const Tensor& q, int64_t q_stride, const Tensor& k_cache,
@@ -414,7 +435,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding", &embedding, "vocab-sharded embedding gather (negative ids: previous step's samples)",
         py::arg("ids"), py::arg("table"), py::arg("out"), py::arg("vstart") = 0, py::arg("prev") = py::none());
   m.def("rmsnorm", &rmsnorm, "RMSNorm with optional fused residual add");
-  m.def("rope_kv", &rope_kv, "NeoX RoPE + paged KV-cache write");
+  m.def("rope_kv", &rope_kv, "NeoX RoPE + paged KV-cache write (rotated q in place or into q_out)",
+        py::arg("qkv"), py::arg("positions"), py::arg("slots"), py::arg("cos_sin"), py::arg("k_cache"),
+        py::arg("v_cache"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"), py::arg("q_out") = py::none());
+  m.def("silu_mul", &silu_mul, "out = silu(y[:, :I]) * y[:, I:] (library gate_up epilogue)");
   m.def("attn_decode", &attn_decode, "paged split-K decode attention");
   m.def("attn_prefill", &attn_prefill, "paged varlen causal prefill attention");
   m.def("sample", &sample, "temperature/top-k/top-p sampling (segmented Gumbel-max + exact rejection)",

@@ -315,8 +315,9 @@ _ONES: dict = {}
 
 def _linear_library(x, lin: Linear, out, residual, norm, qkv):
     """Long-step (prefill) path of :func:`linear`: RMSNorm kernel -> hipBLASLt GEMM on the
-    plain weight copy -> bias / SiLU*mul / RoPE + KV write / residual as separate ops. Same
-    math as the fused kernels up to bf16 rounding of the GEMM output before the epilogue."""
+    plain weight copy, then bias / residual adds, and SiLU*mul or RoPE + KV write (+ q
+    placement) as one epilogue kernel each. Same math as the fused kernels up to where the
+    bf16 roundings fall."""
     xx = x
     if norm is not None:
         if lin.norm_gamma is not None:  # gamma is folded into wl: unit-weight RMSNorm
@@ -329,17 +330,21 @@ def _linear_library(x, lin: Linear, out, residual, norm, qkv):
             xx = rmsnorm(x[:, :lin.K], norm[0], float(norm[1]))
     elif x.shape[1] != lin.K:
         xx = x[:, :lin.K]
-    y = torch.matmul(xx, lin.wl.t())
+    wt = lin.wl.t()
+    C = native()
+    if lin.layout == "silu":
+        y = torch.mm(xx, wt)
+        C.silu_mul(y, out)  # one fused epilogue kernel
+        return out
+    # plain GEMM + separate adds: hipBLASLt's beta = 1 / bias-epilogue variants (addmm) made
+    # an eagerly-run step differ bitwise from its captured replay (algorithm choice), which
+    # the deferred-capture engine must not see (tests/test_engine_gpu.py)
+    y = torch.mm(xx, wt)
     if lin.bias is not None:
         y += lin.bias
-    if lin.layout == "silu":
-        I = lin.N // 2
-        out.copy_(torch.nn.functional.silu(y[:, :I].float()) * y[:, I:].float())
-        return out
     if qkv is not None:
-        rope_kv(y, qkv["positions"], qkv["slots"], qkv["cos_sin"], qkv["k_cache"], qkv["v_cache"],
-                qkv["hq"], qkv["hkv"], 128)
-        out.copy_(y[:, : qkv["hq"] * 128])
+        C.rope_kv(y, qkv["positions"], qkv["slots"], qkv["cos_sin"], qkv["k_cache"], qkv["v_cache"],
+                  qkv["hq"], qkv["hkv"], 128, out)  # rotated q written straight into out
         return out
     if residual is not None:
         torch.add(y, residual, out=out)
