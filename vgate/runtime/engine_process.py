@@ -17,9 +17,10 @@ use (add_request with callbacks, abort, embed, snapshot, healthy, stop), so
 :class:`SeqView` carrying the fields the backend reads. This mirrors the reference's
 vLLM deployment, whose EngineCore also runs in a separate process
 (reference benchmarks/run_report.py:89-93). TP > 1 keeps the in-process engine (rank 0
-drives its followers directly). Measured on the MI355X headline bench: equal throughput
-to the in-process engine (profiles/r1_engine_process_vs_inprocess.log) — the GIL is not
-the bottleneck at this load — so it is opt-in, for isolation.
+drives its followers directly). Measured on MI355X (profiles/r1_bench_concurrency_sweep.log):
+equal throughput at the headline's 8 concurrent clients, +6% at 64 and +28% at 128
+(372 -> 477 req/s) — at high request rates the HTTP side's Python work holds the shared
+GIL long enough to stall the engine's step loop.
 """
 from __future__ import annotations
 

@@ -133,15 +133,24 @@ class ModelRunner:
         qs[0] = 0
         for s, (seq, n) in enumerate(batch.items):
             c0 = seq.num_computed
-            toks = seq.all_ids[c0: c0 + n]
-            ids[t: t + n] = toks
-            if pending_slots and toks[-1] < 0:  # unresolved sample of the previous step
-                ids[t + n - 1] = -(pending_slots[seq.seq_id] + 1)
-            p = np.arange(c0, c0 + n, dtype=np.int32)
-            pos[t: t + n] = p
-            blocks = np.asarray(seq.blocks, dtype=np.int32)
-            slots[t: t + n] = blocks[p // bs] * bs + (p % bs)
-            nb = len(seq.blocks)
+            blocks = seq.blocks
+            if n == 1:  # decode row: O(1) scalar writes (no per-step copy of the context)
+                P = len(seq.prompt_ids)
+                tok = seq.output_ids[c0 - P] if c0 >= P else seq.prompt_ids[c0]
+                if pending_slots and tok < 0:  # unresolved sample of the previous step
+                    tok = -(pending_slots[seq.seq_id] + 1)
+                ids[t] = tok
+                pos[t] = c0
+                slots[t] = blocks[c0 // bs] * bs + c0 % bs
+            else:
+                toks = seq.ids_slice(c0, c0 + n)
+                ids[t: t + n] = toks
+                if pending_slots and toks[-1] < 0:
+                    ids[t + n - 1] = -(pending_slots[seq.seq_id] + 1)
+                p = np.arange(c0, c0 + n, dtype=np.int32)
+                pos[t: t + n] = p
+                slots[t: t + n] = np.asarray(blocks, dtype=np.int32)[p // bs] * bs + (p % bs)
+            nb = len(blocks)
             bt[s, :nb] = blocks
             ctx = c0 + n
             cl[s] = ctx

@@ -56,6 +56,15 @@ class Sequence:
     def all_ids(self) -> list[int]:
         return self.prompt_ids + self.output_ids if self.output_ids else self.prompt_ids
 
+    def ids_slice(self, a: int, b: int) -> list[int]:
+        """all_ids[a:b] without concatenating the whole prompt and output."""
+        P = len(self.prompt_ids)
+        if b <= P:
+            return self.prompt_ids[a:b]
+        if a >= P:
+            return self.output_ids[a - P: b - P]
+        return self.prompt_ids[a:] + self.output_ids[: b - P]
+
     @property
     def total_len(self) -> int:
         return len(self.prompt_ids) + len(self.output_ids)
