@@ -553,7 +553,7 @@ __device__ __forceinline__ bf16x8 raw8(uint32_t q) {
 }
 
 template <int MB, int NTB, int EPI, int NORM>
-__global__ __launch_bounds__(1024) void awq_gemm_kernel(GemmParams p) {
+__global__ __launch_bounds__(512) void awq_gemm_kernel(GemmParams p) {  // <= 8 waves: 256 VGPRs for the chunked loads
   extern __shared__ __attribute__((aligned(16))) char smem[];
   TLScope tl_scope(p.dbg_ts);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -581,31 +581,68 @@ __global__ __launch_bounds__(1024) void awq_gemm_kernel(GemmParams p) {
     ssr[mb] = 0.f;
   }
   const bf16_t* nw_ptr = p.norm_w ? p.norm_w + 8 * (lane >> 4) : nullptr;
-  for (int kq = qbeg; kq < qend; ++kq) {
-    uint4 w[NTB];
+  // Chunks of up to QC k-quads: EVERY load of a chunk (int4 weights, activations, RMSNorm
+  // gamma, group scales / zeros) is issued before any is consumed, so a wave's k-range costs
+  // ceil(n / QC) memory round trips instead of one per k-quad — in the engine the
+  // activations arrive cold from the previous kernel (qkv 9.8 -> see profiles/r1_awq_*).
+  constexpr int QC = MB == 1 ? 4 : (MB == 2 ? 2 : 1);
+  for (int kc = qbeg; kc < qend; kc += QC) {
+    uint4 w[QC][NTB];
+    uint4 a[QC][4][MB];
+    uint4 gm[QC][4];
+    float sc[QC][NTB][4], zc[QC][NTB][4];
 #pragma unroll
-    for (int j = 0; j < NTB; ++j) w[j] = ld_nt16(p.wp + ((size_t)(nt0 + j) * KQ + kq) * 64 + lane);
-    uint4 a[4][MB];
+    for (int c = 0; c < QC; ++c) {
+      const int kq = min(kc + c, qend - 1);  // clamped re-load past the end: never consumed
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) {
-        a[u][mb] = xok[mb] ? *reinterpret_cast<const uint4*>(xrow[mb] + (kq * 4 + u) * 32) : make_uint4(0, 0, 0, 0);
-        if constexpr (NORM) a[u][mb] = norm_frag<NORM>(a[u][mb], nw_ptr, (kq * 4 + u) * 32, ssr[mb]);
-      }
-#pragma unroll
-    for (int j = 0; j < NTB; ++j) {
-      const int n = (nt0 + j) * 16 + (lane & 15);
-      const uint32_t wq[4] = {w[j].x, w[j].y, w[j].z, w[j].w};
+      for (int j = 0; j < NTB; ++j) w[c][j] = ld_nt16(p.wp + ((size_t)(nt0 + j) * KQ + kq) * 64 + lane);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int k = (kq * 4 + u) * 32 + 8 * (lane >> 4);
-        const int gi = k / p.group;
-        const float s = bf2f(p.scales[(size_t)gi * p.N + n]);
-        const float sz = bf2f(p.zeros[(size_t)gi * p.N + n]);
-        const bf16x8 wf = dq8(wq[u], s, sz);
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(wf, as_bf16x8(a[u][mb]), acc[mb][j]);
+        for (int mb = 0; mb < MB; ++mb)
+          a[c][u][mb] = xok[mb] ? *reinterpret_cast<const uint4*>(xrow[mb] + (kq * 4 + u) * 32) : make_uint4(0, 0, 0, 0);
+        if constexpr (NORM == 1) gm[c][u] = *reinterpret_cast<const uint4*>(nw_ptr + (kq * 4 + u) * 32);
+      }
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) {
+        const int n = (nt0 + j) * 16 + (lane & 15);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int gi = ((kq * 4 + u) * 32 + 8 * (lane >> 4)) / p.group;
+          sc[c][j][u] = bf2f(p.scales[(size_t)gi * p.N + n]);
+          zc[c][j][u] = bf2f(p.zeros[(size_t)gi * p.N + n]);
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < QC; ++c) {
+      if (kc + c >= qend) break;  // wave-uniform
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+          if constexpr (NORM) {
+            float f[8], g[8];
+            unpack8(a[c][u][mb], f);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ssr[mb] += f[j] * f[j];
+            if constexpr (NORM == 1) {
+              unpack8(gm[c][u], g);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) f[j] *= g[j];
+              a[c][u][mb] = pack8(f);
+            }
+          }
+        }
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) {
+        const uint32_t wq[4] = {w[c][j].x, w[c][j].y, w[c][j].z, w[c][j].w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bf16x8 wf = dq8(wq[u], sc[c][j][u], zc[c][j][u]);
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(wf, as_bf16x8(a[c][u][mb]), acc[mb][j]);
+        }
       }
     }
   }
@@ -658,6 +695,16 @@ __global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
   for (int i = 0; i < XMAX; ++i) {
     const int t = 4 * i + wid;  // k-step of the slice
     xr[i] = (t < nst && xrow_m < p.M) ? ld16(xrow + (q0 * 4 + t) * 32) : make_uint4(0, 0, 0, 0);
+  }
+  // RMSNorm gamma of the same k-steps, issued with the activations (loading it inside the
+  // staging loop added a dependent round trip: gate_up 16 us in the engine)
+  uint4 gr[NORM == 1 ? XMAX : 1];
+  if constexpr (NORM == 1) {
+#pragma unroll
+    for (int i = 0; i < XMAX; ++i) {
+      const int t = 4 * i + wid;
+      gr[i] = t < nst ? ld16(p.norm_w + (q0 * 4 + t) * 32 + 8 * (lane >> 4)) : make_uint4(0, 0, 0, 0);
+    }
   }
   // 2) weight stream: this wave's NTW tiles over the block's k-quads. Per k-quad and tile:
   //    P = sum over the quad's 4 MFMAs of raw8(w) . x, then acc += s (x) P - (128 s + s z) X
@@ -728,7 +775,7 @@ __global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
           for (int j = 0; j < 8; ++j) ss += a[j] * a[j];
           if constexpr (NORM == 1) {
             float g8[8];
-            unpack8(ld16(p.norm_w + (q0 * 4 + t) * 32 + 8 * (lane >> 4)), g8);
+            unpack8(gr[i], g8);
 #pragma unroll
             for (int j = 0; j < 8; ++j) a[j] *= g8[j];
             v = pack8(a);
@@ -996,6 +1043,7 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
   const int mchunks = (g.M + 16 * MB - 1) / (16 * MB);
   const int ksteps = AWQ ? g.K / 128 : g.K / 32;
   Plan pl = plan(nblk, mchunks, ksteps, MB, NTB, g.waves, g.splitk);
+  if (AWQ && pl.waves > 8) pl.waves = 8;  // awq_gemm_kernel: __launch_bounds__(512)
   const size_t need_slab = (size_t)nblk * mchunks * pl.splitk * (MB * NTB * 64 * 16 + (NORM ? 16 * MB * 4 : 0));
   if (pl.splitk > 1 && (g.slabs == nullptr || need_slab > g.slab_bytes || nblk * mchunks > g.max_counters))
     pl.splitk = 1;  // workspace too small: fall back to one slice (still correct)
