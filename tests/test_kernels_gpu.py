@@ -646,7 +646,7 @@ def test_library_prefill_path_matches_reference(M, fold):
     assert _rel_err(kc, kc2) < 2e-2 and _rel_err(vc, vc2) < 2e-2
 
 
-@pytest.mark.parametrize("layout", ["plain", "silu"])
+@pytest.mark.parametrize("layout", ["plain", "silu", "qkv"])
 def test_awq_library_prefill_path(layout):
     """AWQ linear at M >= LIBRARY_MIN_M: the once-dequantized plain copy + hipBLASLt ==
     the dequantised fp32 reference (the W4A16 kernels have no M > 16 tile path)."""
@@ -656,14 +656,31 @@ def test_awq_library_prefill_path(layout):
     scales = (torch.rand(K // g, N) * 0.02 + 0.005).bfloat16()
     zeros = torch.randint(0, 16, (K // g, N)).float().bfloat16()
     wd = ref.awq_dequant_ref(q, scales, zeros, g).to(DEV)
-    lin = ops.Linear(None, awq={"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV), "group": g,
-                                "silu": layout == "silu"})
-    assert lin.keep_library_copy()
-    assert _rel_err(lin.wl.float(), wd.float()) < 1e-2
+    awq = {"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV), "group": g, "silu": layout == "silu"}
+    if layout == "qkv":
+        awq["layout"] = "qkv"
+    lin = ops.Linear(None, awq=awq)
+    assert lin.layout == layout and lin.keep_library_copy()
+    assert _rel_err(lin.wl.float(), wd.float()) < 1e-2  # original row order restored
     x = torch.randn(M, K, device=DEV).bfloat16()
     nw = (torch.rand(K, device=DEV) + 0.5).bfloat16()
-    y = ops.linear(x, lin, norm=(nw, 1e-6))
     xn, _ = ref.rmsnorm_ref(x, nw, 1e-6)
+    if layout == "qkv":  # hq = 12, hkv = 2 heads of 128 -> N = 2048
+        D, BS, hq, hkv = 128, 16, 12, 2
+        pos = torch.randint(0, 1000, (M,), dtype=torch.int32, device=DEV)
+        slots = torch.randperm(64 * BS, device=DEV)[:M].int()
+        cs = ref.rope_cos_sin(1024, D, 1e6, device=DEV)
+        kc = torch.zeros(64, hkv, BS, D, device=DEV).bfloat16()
+        vc = torch.zeros_like(kc)
+        qo = ops.linear(x, lin, norm=(nw, 1e-6), qkv=dict(positions=pos, slots=slots, cos_sin=cs, k_cache=kc,
+                                                          v_cache=vc, hq=hq, hkv=hkv))
+        qkv = ref.linear_ref(xn, wd)
+        kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+        ref.rope_kv_ref(qkv, pos, slots, cs, kc2, vc2, hq, hkv, D)
+        assert _rel_err(qo, qkv[:, : hq * D]) < 2e-2
+        assert _rel_err(kc, kc2) < 2e-2 and _rel_err(vc, vc2) < 2e-2
+        return
+    y = ops.linear(x, lin, norm=(nw, 1e-6))
     if layout == "silu":
         assert _rel_err(y, ref.silu_mul_linear_ref(xn, wd[: N // 2], wd[N // 2:])) < 2e-2
     else:
