@@ -223,6 +223,8 @@ def main():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # single node: gloo over loopback, independent of whether the hostname resolves
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         dist.init_process_group("gloo")  # coordination only: replicas share no tensors
         dist_ok = True
     try:
