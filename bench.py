@@ -127,8 +127,10 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
         if dist_ok:
             import torch.distributed as dist
             dist.barrier()
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
+        # this rank's GPU explicitly: the bare call syncs the calling thread's current device,
+        # which is cuda:0 unless this thread happened to construct the engine
+        if not args.engine_process and torch.cuda.is_available():
+            torch.cuda.synchronize(local)
 
     per_step = args.requests_per_step
     key = BENCH_KEY if args.security else None
