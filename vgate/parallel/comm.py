@@ -88,7 +88,12 @@ def init_tp(tp_size: int, backend: str | None = None) -> TPGroup:
         _TP = TPGroup()
         return _TP
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # an already-initialised default group decides (e.g. gloo carrying GPU tensors when
+        # several ranks share one GPU in tests); otherwise RCCL on GPUs, gloo on CPU
+        if dist.is_initialized():
+            backend = dist.get_backend()
+        else:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
     if not dist.is_initialized():
         from datetime import timedelta
 
@@ -108,7 +113,8 @@ def init_tp(tp_size: int, backend: str | None = None) -> TPGroup:
         if rank in ranks:
             grp = g
     _TP = TPGroup(rank=rank % tp_size, size=tp_size, group=grp, backend=backend)
-    if backend == "nccl" and os.environ.get("VGATE_CUSTOM_AR", "1") != "0":
+    # the one-shot kernel maps peer buffers over IPC; the group only exchanges the handles
+    if torch.cuda.is_available() and os.environ.get("VGATE_CUSTOM_AR", "1") != "0":
         from vgate.parallel.custom_allreduce import maybe_create
 
         dev = torch.device("cuda", torch.cuda.current_device())

@@ -111,8 +111,11 @@ class LLMEngine:
         self.scheduler = Scheduler(self.kvm, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len)
         part = cfg.part_size or 512
         part = min(1024, max(32, (part + 31) // 32 * 32))
+        # a gloo group (ranks sharing one GPU in tests) runs its collectives on the host:
+        # they cannot be captured into a hipGraph
+        eager = cfg.enforce_eager or (self.tp.size > 1 and self.tp.backend != "nccl")
         self.runner = ModelRunner(self.model, self.kv_caches, cfg.max_num_seqs, cfg.max_num_batched_tokens,
-                                  cfg.max_model_len, cfg.block_size, cfg.enforce_eager, part,
+                                  cfg.max_model_len, cfg.block_size, eager, part,
                                   cfg.graph_token_buckets)
         self.tokenizer = load_tokenizer(weights, cfg.tokenizer, self.arch)
         self.stats = EngineStats()
