@@ -161,13 +161,22 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
     await asyncio.sleep(0.3)  # the engine core's stats snapshot is pushed every 0.25 s
     while callable(stats) and stats().get("pending_captures", 0) and time.perf_counter() - t_cap < 120:
         await asyncio.sleep(0.05)
+    eng = app.state.vgate.engine
+    inner = getattr(eng.backend, "engine", None)
+    if hasattr(inner, "reset_peaks"):
+        inner.reset_peaks()
+    snap0 = eng.backend.stats() if hasattr(eng.backend, "stats") else {}
     barrier()
     t0 = time.perf_counter()
     lat, fails, tokens, _ = await load(per_step * args.steps, 0)
     barrier()
     wall = time.perf_counter() - t0
-    eng = app.state.vgate.engine
     snap = eng.backend.stats() if hasattr(eng.backend, "stats") else {}
+    # timed-region forensics (p99): eager (graph-miss) steps and captures INSIDE the timed region
+    snap = dict(snap)
+    for k in ("graph_misses_eager", "graph_captures", "steps", "graph_hits"):
+        if k in snap and k in snap0:
+            snap[f"timed_{k}"] = snap[k] - snap0[k]
     server.should_exit = True
     await srv_task
     return {"lat": lat, "fails": fails, "tokens": tokens, "wall": wall, "boot_s": boot_s,
@@ -268,6 +277,14 @@ def main():
             "engine_avg_cycle_ms": allr[0]["engine"].get("avg_cycle_ms"),
             "engine_avg_gpu_ms": allr[0]["engine"].get("avg_gpu_ms"),
             "boot_s": round(max(r["boot_s"] for r in allr), 1),
+            "max_s": round(max(lat), 4) if lat else 0.0,
+            "timed_engine_steps": allr[0]["engine"].get("timed_steps"),
+            "timed_eager_steps": allr[0]["engine"].get("timed_graph_misses_eager"),
+            "timed_graph_captures": allr[0]["engine"].get("timed_graph_captures"),
+            "max_gpu_step_ms": allr[0]["engine"].get("max_gpu_step_ms"),
+            "max_gpu_step_bucket": allr[0]["engine"].get("max_gpu_step_bucket"),
+            "max_cycle_ms": allr[0]["engine"].get("max_cycle_ms"),
+            "max_cycle_tokens_seqs": allr[0]["engine"].get("max_cycle_tokens_seqs"),
         }
         print(json.dumps(out), flush=True)
     if dist_ok:

@@ -146,6 +146,19 @@ __device__ __forceinline__ void st_sc1_f4(float* p, float a, float b, float c, f
 __device__ __forceinline__ f32x4 ld_sc1_f4(const float* p) {
   return f32x4{ld_sc1(p), ld_sc1(p + 1), ld_sc1(p + 2), ld_sc1(p + 3)};
 }
+// Bulk hand-off payloads: ONE 16-B write-through (sc1) vector store / sc1 load per lane through a
+// buffer descriptor (four dword sc1 stores of the same bytes are 3-20x slower to publish:
+// cdna_hip_programming.md Guideline 16, Pitfall 7). `base` must be wave-uniform (a kernel
+// argument or a blockIdx-derived pointer), the per-lane part goes in the byte offset.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void st_sc1_x4(float* base, uint32_t off_bytes, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, rsrc_of(base), off_bytes, 0, 16 /* sc1 */);
+}
+__device__ __forceinline__ f32x4 ld_sc1_x4(const float* base, uint32_t off_bytes) {
+  return __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(base), off_bytes, 0, 16 /* sc1 */);
+}
 // all of this thread's stores have reached the device-coherent level
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 

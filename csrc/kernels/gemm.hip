@@ -44,6 +44,7 @@
 namespace vgate {
 
 enum GemmEpi : int { EPI_BF16 = 0, EPI_F32 = 1, EPI_SILU = 2, EPI_QKV = 3 };
+constexpr int SK_MAX = 8;  // split-K slices per tile (the combine issues all slices' loads at once)
 
 struct GemmParams {
   const bf16_t* x; int lda; int M; const int32_t* row_idx;
@@ -96,11 +97,20 @@ __device__ __forceinline__ uint4 norm_frag(uint4 a, const bf16_t* w, int k0, flo
 // the RoPE cos/sin row of the position, issued once the first weight group is in flight),
 // so the epilogue after the reduction is pure ALU + stores instead of a dependent
 // positions -> cos_sin load chain behind the whole GEMM (benchmarks/qkv_probe.py).
+// QKV tile layout (ops.row_permutation "qkv"): tile t of head h (16 columns) holds the head's
+// columns 8t..8t+7 (lane groups 0, 1) and their NeoX rotation partners 64+8t..64+8t+7 (groups
+// 2, 3), so a rotation pair sits on lanes l and l ^ 32 of ONE tile (exchanged by permlane32).
+// qkv_rot: rotation index (0..63) of the lane's first column; qkv_col: that column in [q|k|v].
+__device__ __forceinline__ int qkv_rot(int nt, int nsub) { return 8 * (nt & 7) + (nsub & 4); }
+__device__ __forceinline__ int qkv_col(int nt, int nsub) {
+  return (nt >> 3) * 128 + (nsub >= 8 ? 64 : 0) + qkv_rot(nt, nsub);
+}
+
 // (plain scalar members: an array member keeps the whole struct in scratch)
 template <int NTB>
 struct EpiPre {
   uint2 r0, r1;  // EPI_BF16: residual words of tile 0 / 1 (4 bf16 each)
-  uint2 b0, b1;  // EPI_BF16 / EPI_F32: bias words of tile 0 / 1; EPI_QKV: bias of d.. / 64+d..
+  uint2 b0, b1;  // EPI_BF16 / EPI_F32: bias words of tile 0 / 1; EPI_QKV: bias of the lane's 4 columns
   float4 cs, sn;
   int pos, slot;
 };
@@ -109,12 +119,9 @@ template <int NTB, int EPI>
 __device__ __forceinline__ void epi_pre_a(const GemmParams& p, EpiPre<NTB>& e, int m, int nt0, int nsub) {
   m = m < p.M ? m : p.M - 1;
   if constexpr (EPI == EPI_QKV) {
-    const int head = nt0 >> 3;
-    const int d = ((nt0 >> 1) & 3) * 16 + nsub;
     e.pos = p.positions[m];
     e.slot = p.slots[m];
-    e.b0 = p.bias ? *reinterpret_cast<const uint2*>(p.bias + head * 128 + d) : make_uint2(0, 0);
-    e.b1 = p.bias ? *reinterpret_cast<const uint2*>(p.bias + head * 128 + 64 + d) : make_uint2(0, 0);
+    e.b0 = p.bias ? *reinterpret_cast<const uint2*>(p.bias + qkv_col(nt0, nsub)) : make_uint2(0, 0);
   } else if constexpr (EPI == EPI_BF16 || EPI == EPI_F32) {
 #pragma unroll
     for (int j = 0; j < NTB; ++j) {
@@ -130,7 +137,7 @@ __device__ __forceinline__ void epi_pre_a(const GemmParams& p, EpiPre<NTB>& e, i
 template <int NTB, int EPI>
 __device__ __forceinline__ void epi_pre_b(const GemmParams& p, EpiPre<NTB>& e, int nt0, int nsub) {
   if constexpr (EPI == EPI_QKV) {
-    const int d = ((nt0 >> 1) & 3) * 16 + nsub;
+    const int d = qkv_rot(nt0, nsub);
     const float* cs = p.cos_sin + (size_t)e.pos * 128;
     e.cs = *reinterpret_cast<const float4*>(cs + d);
     e.sn = *reinterpret_cast<const float4*>(cs + 64 + d);
@@ -144,9 +151,14 @@ __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 
 // `e` = operands prefetched at launch (decode kernel) when `have`, else loaded here.
 // `have` is a compile-time choice: a runtime select between a prefetched register value
 // and a load becomes a select of ADDRESSES that puts the prefetch struct in scratch.
+// `valid`: row m < M. Every lane of the wave calls in (the QKV pair exchange is a cross-lane
+// op); only valid rows store.
 template <int NTB, int EPI, bool have>
 __device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[NTB], int m, int nt0, int nsub,
-                                         const EpiPre<NTB> e) {
+                                         const EpiPre<NTB> e, bool valid) {
+  if constexpr (EPI != EPI_QKV) {
+    if (!valid) return;
+  }
   if constexpr (EPI == EPI_SILU) {
     const int n = (nt0 >> 1) * 16 + nsub;
     float o[4];
@@ -157,55 +169,47 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[N
     pk.y = pack_bf2(o[2], o[3]);
     *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + n) = pk;
   } else if constexpr (EPI == EPI_QKV) {
-    // tiles (nt0, nt0+1) = original tiles (8h + t, 8h + t + 4) of head h: columns d and d + 64
+    static_assert(NTB == 1, "QKV tiles carry their rotation partners (see qkv_col)");
     const int head = nt0 >> 3;
-    const int d = ((nt0 >> 1) & 3) * 16 + nsub;  // rotation index 0..63
-    uint2 w1, w2;
+    const int d = qkv_rot(nt0, nsub);  // rotation index of this lane's 4 columns
+    const bool upper = nsub >= 8;      // partner half (d + 64)
+    uint2 w;
     float4 cs, sn;
     int slot;
     if constexpr (have) {
-      w1 = e.b0; w2 = e.b1; cs = e.cs; sn = e.sn; slot = e.slot;
+      w = e.b0; cs = e.cs; sn = e.sn; slot = e.slot;
     } else {
-      w1 = p.bias ? *reinterpret_cast<const uint2*>(p.bias + head * 128 + d) : make_uint2(0, 0);
-      w2 = p.bias ? *reinterpret_cast<const uint2*>(p.bias + head * 128 + 64 + d) : make_uint2(0, 0);
-      const float* cp = p.cos_sin + (size_t)p.positions[m] * 128;
+      const int mm = m < p.M ? m : p.M - 1;
+      w = p.bias ? *reinterpret_cast<const uint2*>(p.bias + qkv_col(nt0, nsub)) : make_uint2(0, 0);
+      const float* cp = p.cos_sin + (size_t)p.positions[mm] * 128;
       cs = *reinterpret_cast<const float4*>(cp + d);
       sn = *reinterpret_cast<const float4*>(cp + 64 + d);
-      slot = p.slots[m];
+      slot = p.slots[mm];
     }
-    const float b1[4] = {bf_lo(w1.x), bf_hi(w1.x), bf_lo(w1.y), bf_hi(w1.y)};
-    const float b2[4] = {bf_lo(w2.x), bf_hi(w2.x), bf_lo(w2.y), bf_hi(w2.y)};
-    float x1[4], x2[4];
+    const float b[4] = {bf_lo(w.x), bf_hi(w.x), bf_lo(w.y), bf_hi(w.y)};
+    float x[4], xp[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      x1[i] = bf2f(f2bf(v[0][i] + b1[i]));  // qkv is bf16 in the reference: round before rotating
-      x2[i] = bf2f(f2bf(v[NTB - 1][i] + b2[i]));
-    }
+    for (int i = 0; i < 4; ++i) x[i] = bf2f(f2bf(v[0][i] + b[i]));  // qkv is bf16 in the reference: round before rotating
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xp[i] = xor32(x[i]);  // the partner column's value (all 64 lanes active)
     if (head < p.hq + p.hkv) {  // q or k: NeoX rotation
       const float cc[4] = {cs.x, cs.y, cs.z, cs.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float a = x1[i], b = x2[i];
-        x1[i] = a * cc[i] - b * ss[i];
-        x2[i] = b * cc[i] + a * ss[i];
-      }
+      for (int i = 0; i < 4; ++i) x[i] = upper ? x[i] * cc[i] + xp[i] * ss[i] : x[i] * cc[i] - xp[i] * ss[i];
     }
-    uint2 p1, p2;
-    p1.x = pack_bf2(x1[0], x1[1]); p1.y = pack_bf2(x1[2], x1[3]);
-    p2.x = pack_bf2(x2[0], x2[1]); p2.y = pack_bf2(x2[2], x2[3]);
+    if (!valid) return;
+    uint2 pk;
+    pk.x = pack_bf2(x[0], x[1]);
+    pk.y = pack_bf2(x[2], x[3]);
+    const int dcol = (upper ? 64 : 0) + d;  // column inside the head
     if (head < p.hq) {
-      bf16_t* q = reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + head * 128 + d;
-      *reinterpret_cast<uint2*>(q) = p1;
-      *reinterpret_cast<uint2*>(q + 64) = p2;
-    } else {
-      if (slot >= 0) {
-        const bool is_k = head < p.hq + p.hkv;
-        const int kh = is_k ? head - p.hq : head - p.hq - p.hkv;
-        bf16_t* dst = (is_k ? p.k_cache : p.v_cache) +
-                      (((size_t)(slot / p.bs) * p.hkv + kh) * p.bs + (slot % p.bs)) * 128 + d;
-        *reinterpret_cast<uint2*>(dst) = p1;
-        *reinterpret_cast<uint2*>(dst + 64) = p2;
-      }
+      *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + head * 128 + dcol) = pk;
+    } else if (slot >= 0) {
+      const bool is_k = head < p.hq + p.hkv;
+      const int kh = is_k ? head - p.hq : head - p.hq - p.hkv;
+      bf16_t* dst = (is_k ? p.k_cache : p.v_cache) +
+                    (((size_t)(slot / p.bs) * p.hkv + kh) * p.bs + (slot % p.bs)) * 128 + dcol;
+      *reinterpret_cast<uint2*>(dst) = pk;
     }
   } else {
 #pragma unroll
@@ -286,7 +290,7 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
     // 1) this slice's partial tile -> fp32 slab [tile][slice][SLOTS]; under NORM also the
     //    slice's per-row partial sum of squares -> [tile][slice][16*MB] after all slabs
     //    (the row scale is applied to the summed tile: y = rsqrt(sum ss / K + eps) * sum acc)
-    f32x4* slab = reinterpret_cast<f32x4*>(p.slabs) + ((size_t)tile * p.splitk + blockIdx.z) * SLOTS;
+    const uint32_t slab_off = (uint32_t)(((size_t)tile * p.splitk + blockIdx.z) * SLOTS * 16);  // bytes
     float* ssq_all = p.slabs + (size_t)gridDim.x * gridDim.y * p.splitk * SLOTS * 4;
     if constexpr (NORM) {
       if (threadIdx.x < 16 * MB) {
@@ -309,7 +313,7 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
           for (int b = 0; b < NTB; ++b)
             if (a == mb && b == j) t = acc[a][b];
       }
-      st_sc1_f4(reinterpret_cast<float*>(slab + s), t[0], t[1], t[2], t[3]);
+      st_sc1_x4(p.slabs, slab_off + (uint32_t)s * 16u, t);
     }
     // 2) publish: every wave drains its sc1 stores, then one ticket (no cache-wide fence)
     drain_stores();
@@ -322,27 +326,40 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
     }
     __syncthreads();
     if (!*flag) return;
-    // 3) the last arriver sums every slice's slab (device-coherent sc1 loads)
-    const float* all = p.slabs + (size_t)tile * p.splitk * SLOTS * 4;
+    // 3) the last arriver sums every slice's slab (device-coherent 16-B sc1 loads). All
+    //    slices' loads are issued before the first is consumed (indices clamped, surplus
+    //    masked): a runtime-trip loop of dependent loads costs one memory round trip per slice.
+    const uint32_t all_off = (uint32_t)((size_t)tile * p.splitk * SLOTS * 16);
     for (int s = threadIdx.x; s < MB * 64; s += blockDim.x) {
       const int mb = s >> 6, l = s & 63;
       const int m = m_base + mb * 16 + (l & 15);
       f32x4 v[NTB];
 #pragma unroll
       for (int j = 0; j < NTB; ++j) {
-        f32x4 t = {0.f, 0.f, 0.f, 0.f};
-        for (int z = 0; z < p.splitk; ++z) t += ld_sc1_f4(all + ((size_t)z * SLOTS + (mb * NTB + j) * 64 + l) * 4);
+        f32x4 r[SK_MAX];
+#pragma unroll
+        for (int z = 0; z < SK_MAX; ++z)
+          r[z] = ld_sc1_x4(p.slabs, all_off + (uint32_t)(((min(z, p.splitk - 1)) * SLOTS + (mb * NTB + j) * 64 + l) * 16));
+        f32x4 t = r[0];
+#pragma unroll
+        for (int z = 1; z < SK_MAX; ++z)
+          if (z < p.splitk) t += r[z];
         v[j] = t;
       }
       if constexpr (NORM) {
-        float ss = 0.f;  // fixed slice order: bit-reproducible
-        for (int z = 0; z < p.splitk; ++z)
-          ss += ld_sc1(ssq_all + ((size_t)tile * p.splitk + z) * 16 * MB + mb * 16 + (l & 15));
+        float sv[SK_MAX];
+#pragma unroll
+        for (int z = 0; z < SK_MAX; ++z)
+          sv[z] = ld_sc1(ssq_all + ((size_t)tile * p.splitk + min(z, p.splitk - 1)) * 16 * MB + mb * 16 + (l & 15));
+        float ss = sv[0];  // fixed slice order: bit-reproducible
+#pragma unroll
+        for (int z = 1; z < SK_MAX; ++z)
+          if (z < p.splitk) ss += sv[z];
         const float sc = rsqrtf(ss / (float)p.K + p.eps);
 #pragma unroll
         for (int j = 0; j < NTB; ++j) v[j] *= sc;
       }
-      if (m < p.M) epilogue<NTB, EPI, PRE>(p, v, m, nt0, 4 * (l >> 4), pre);
+      epilogue<NTB, EPI, PRE>(p, v, m, nt0, 4 * (l >> 4), pre, m < p.M);
     }
     return;
   }
@@ -369,7 +386,7 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
 #pragma unroll
       for (int j = 0; j < NTB; ++j) v[j] *= sc;
     }
-    if (m < p.M) epilogue<NTB, EPI, PRE>(p, v, m, nt0, 4 * (l >> 4), pre);
+    epilogue<NTB, EPI, PRE>(p, v, m, nt0, 4 * (l >> 4), pre, m < p.M);
   }
 }
 
@@ -661,6 +678,7 @@ __global__ __launch_bounds__(512) void awq_gemm_kernel(GemmParams p) {  // <= 8 
 // clamped). Split-K slices meet at a per-column-group ticket (sc1 slabs, last arriver sums).
 constexpr int AD_WAVES = 4;
 constexpr int AD_G = 2;  // k-quads (128 k) per register group
+constexpr int AD_SK_MAX = 16;  // split-K slices (<= 16 staged k-quads per slice: K <= 32768)
 
 template <int NTW, int EPI, int NORM>
 __global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
@@ -831,7 +849,7 @@ __global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
 #pragma unroll
       for (int j = 0; j < NTW; ++j) v[j] *= rs;
     }
-    if (m < p.M) epilogue<NTW, EPI, false>(p, v, m, nt0, nsub, EpiPre<NTW>{});
+    epilogue<NTW, EPI, false>(p, v, m, nt0, nsub, EpiPre<NTW>{}, m < p.M);
   };
   if (p.splitk == 1) {
     finish(acc, ss_slice);
@@ -842,9 +860,9 @@ __global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
   constexpr int SLOTS = AD_WAVES * NTW * 64;
   constexpr int SLAB = SLOTS * 4 + 16;  // floats per (group, slice): tiles + per-row ssq
   float* slab = p.slabs + ((size_t)grp * p.splitk + blockIdx.z) * SLAB;
+  const uint32_t slab_off = (uint32_t)(((size_t)grp * p.splitk + blockIdx.z) * SLAB * 4);  // bytes
 #pragma unroll
-  for (int j = 0; j < NTW; ++j)
-    st_sc1_f4(slab + ((wid * NTW + j) * 64 + lane) * 4, acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+  for (int j = 0; j < NTW; ++j) st_sc1_x4(p.slabs, slab_off + (uint32_t)((wid * NTW + j) * 64 + lane) * 16u, acc[j]);
   if (NORM != 0 && wid == 0 && lane < 16) st_sc1(slab + SLOTS * 4 + lane, ss_slice);
   drain_stores();
   __syncthreads();
@@ -858,16 +876,30 @@ __global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
   AD_PHASE(4);
   if (!*flag) return;
   const float* all = p.slabs + (size_t)grp * p.splitk * SLAB;
+  const uint32_t all_off = (uint32_t)((size_t)grp * p.splitk * SLAB * 4);
   f32x4 v[NTW];
 #pragma unroll
   for (int j = 0; j < NTW; ++j) {
-    f32x4 t = {0.f, 0.f, 0.f, 0.f};
-    for (int z = 0; z < p.splitk; ++z) t += ld_sc1_f4(all + (size_t)z * SLAB + ((wid * NTW + j) * 64 + lane) * 4);
+    f32x4 r[AD_SK_MAX];
+#pragma unroll
+    for (int z = 0; z < AD_SK_MAX; ++z)
+      r[z] = ld_sc1_x4(p.slabs, all_off + (uint32_t)(min(z, p.splitk - 1) * SLAB * 4 + ((wid * NTW + j) * 64 + lane) * 16));
+    f32x4 t = r[0];
+#pragma unroll
+    for (int z = 1; z < AD_SK_MAX; ++z)
+      if (z < p.splitk) t += r[z];
     v[j] = t;
   }
   float ss_row = 0.f;
-  if constexpr (NORM != 0)
-    for (int z = 0; z < p.splitk; ++z) ss_row += ld_sc1(all + (size_t)z * SLAB + SLOTS * 4 + m);
+  if constexpr (NORM != 0) {
+    float sv[AD_SK_MAX];
+#pragma unroll
+    for (int z = 0; z < AD_SK_MAX; ++z) sv[z] = ld_sc1(all + (size_t)min(z, p.splitk - 1) * SLAB + SLOTS * 4 + m);
+    ss_row = sv[0];
+#pragma unroll
+    for (int z = 1; z < AD_SK_MAX; ++z)
+      if (z < p.splitk) ss_row += sv[z];
+  }
   finish(v, ss_row);
   AD_PHASE(5);
 #undef AD_PHASE
@@ -1007,7 +1039,7 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(GemmParams p) {
 #pragma unroll
       for (int j = 0; j < NTW; ++j) v[j] *= sc;
     }
-    if (m < p.M) epilogue<NTW, EPI, false>(p, v, m, nt0, 4 * (lane >> 4), EpiPre<NTW>{});
+    epilogue<NTW, EPI, false>(p, v, m, nt0, 4 * (lane >> 4), EpiPre<NTW>{}, m < p.M);
   }
 }
 
@@ -1032,6 +1064,8 @@ static Plan plan(int nblk, int mchunks, int ksteps, int MB, int NTB, int force_w
   while (w > 1 && w * MB * NTB > 64) w >>= 1;
   if (force_s > 0) s = force_s;
   if (force_w > 0) w = force_w;
+  if (s > SK_MAX) s = SK_MAX;
+  while (s > 1 && ksteps / s < 1) s >>= 1;
   if (MB == 1 && w > 8) w = 8;  // pipelined decode kernel: __launch_bounds__(512)
   return {w, s};
 }
@@ -1088,6 +1122,7 @@ static bool launch_awq_dec(GemmParams p, const GemmArgs& g, hipStream_t st) {
   sk = sk > KQ / 2 ? KQ / 2 : sk;
   sk = sk < 1 ? 1 : sk;
   if ((KQ + sk - 1) / sk > 16) sk = (KQ + 15) / 16;  // staging holds <= 16 k-quads per slice
+  if (sk > AD_SK_MAX) return false;
   const size_t need_slab = (size_t)groups * sk * (AD_WAVES * NTB * 64 * 16 + 64);
   if (sk > 1 && (g.slabs == nullptr || need_slab > g.slab_bytes || groups > g.max_counters)) sk = 1;
   p.splitk = sk;
@@ -1141,7 +1176,7 @@ static void launch_dispatch(GemmParams p, const GemmArgs& g, hipStream_t st) {
   } while (0)
   switch (g.epi) {
     case EPI_SILU: VG_NORM(2, EPI_SILU); break;
-    case EPI_QKV: VG_NORM(2, EPI_QKV); break;
+    case EPI_QKV: VG_NORM(1, EPI_QKV); break;
     case EPI_F32:
       if constexpr (!AWQ) {
         if (g.ntb == 4 && ntiles % 4 == 0 && g.M <= 16) { VG_NORM(4, EPI_F32); break; }

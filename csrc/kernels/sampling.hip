@@ -56,7 +56,7 @@ __device__ __forceinline__ void philox4(uint64_t seed, uint64_t offset, uint32_t
 }
 
 constexpr int SAMPLE_THREADS = 256;
-constexpr int SAMPLE_MAX_BLOCKS = 256;  // B * NSEG bound (co-residency of a row's blocks)
+constexpr int SAMPLE_MAX_BLOCKS = 1024;  // B * NSEG bound: 4 blocks of 256 threads per CU, all co-resident
 constexpr float LOG2E_S = 1.4426950408889634f;
 
 // Per-(row, segment) partial, 8 words.
@@ -121,17 +121,25 @@ __device__ __forceinline__ void block_reduce_acc(Acc& a, float c, Acc* red) {
 
 // Per-row meeting point of the NSEG blocks after pass `gen` (1-based).
 // Returns false if the wait gave up (caller falls back to the argmax).
+// The poll is an atomic read-modify-write (fetch_add 0): it is performed at the device
+// coherence point, so it can never spin on a copy of the counter line that an earlier poll
+// left in this XCD's L2 (plain or sc1 polls of a counter that OTHER XCDs bump by atomics were
+// seen to stall a row for tens to hundreds of ms: profiles/r2_sampler_stall.txt). One agent
+// acquire after the match, then the row's partials are read.
 __device__ __forceinline__ bool row_meet(uint32_t* ctr, uint32_t target, int* ok_flag) {
   drain_stores();  // this block's sc1 partial stores are device-visible before it arrives
   __syncthreads();
   if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     int ok = 1;
     uint32_t spins = 0;
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 22)) { ok = 0; break; }  // ~seconds: never hang the GPU
+    while (v < target) {
+      __builtin_amdgcn_s_sleep(2);
+      v = __hip_atomic_fetch_add(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (++spins > (1u << 20)) { ok = 0; break; }  // bounded: never hang the GPU
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     *ok_flag = ok;
   }
   __syncthreads();
@@ -286,7 +294,7 @@ int sample_segments(int B, int V) {
   int nseg = SAMPLE_MAX_BLOCKS / (B > 0 ? B : 1);
   if (force > 0 && force < nseg) nseg = force;
   if (nseg > SAMPLE_THREADS) nseg = SAMPLE_THREADS;  // the merge loads one partial per thread
-  const int cap = V4 / 1024;  // >= 4096 logits per segment
+  const int cap = V4 / 256;  // >= 1024 logits per segment
   if (nseg > cap) nseg = cap;
   return nseg < 1 ? 1 : nseg;
 }

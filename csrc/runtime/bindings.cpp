@@ -324,8 +324,9 @@ void sample(const Tensor& logits, const c10::optional<Tensor>& temperature,
   s.out = reinterpret_cast<int32_t*>(out.data_ptr());
   s.out_logprob = const_cast<float*>(static_cast<const float*>(fp(out_logprob, torch::kFloat32)));
   if (ws.has_value() && ws->defined()) {
-    // [0, 512): row counters (2 per row, B <= 256 in segmented mode); [512, 2560): partials
-    TORCH_CHECK(ws->scalar_type() == torch::kInt32 && ws->is_cuda() && ws->numel() >= 2560, "sample: ws must be int32[>=2560]");
+    // [0, 512): row counters (2 per row, B <= 256 in segmented mode); [512, 8704): partials
+    // (8 words per block, B * nseg <= 1024 blocks)
+    TORCH_CHECK(ws->scalar_type() == torch::kInt32 && ws->is_cuda() && ws->numel() >= 8704, "sample: ws must be int32[>=8704]");
     if (vgate::sample_segments(s.B, s.V) > 1) {
       s.sync = reinterpret_cast<uint32_t*>(ws->data_ptr());
       s.parts = reinterpret_cast<float*>(ws->data_ptr()) + 512;

@@ -322,7 +322,7 @@ def test_sample_logprob():
 
 # ---------------------------------------------------------------- fused GEMM v2
 @pytest.mark.parametrize("M,N,K", [(8, 1536, 1536), (8, 1536, 8960), (40, 2048, 1536), (200, 512, 1024)])
-@pytest.mark.parametrize("splitk", [1, 4])
+@pytest.mark.parametrize("splitk", [1, 4, 8])
 def test_gemm_splitk_residual_inplace(M, N, K, splitk):
     torch.manual_seed(10)
     x = torch.randn(M, K, device=DEV).bfloat16()

@@ -297,3 +297,64 @@ async def test_health_checker_stalled_resolver_does_not_block_probes():
     await asyncio.sleep(0.2)
     assert len(probes) >= 3  # probing kept ticking while DNS was wedged
     await hc.stop()
+
+
+# ---------------------------------------------------------------- engine-aware health
+class _FaultyBackend(DryRunBackend):
+    """Dry-run backend with the native backend's health hook (fault injection)."""
+
+    def __init__(self):
+        super().__init__()
+        self.ok = True
+
+    def healthy(self) -> bool:
+        return self.ok
+
+
+async def test_worker_health_fails_when_engine_faults_and_gateway_demotes():
+    be = _FaultyBackend()
+    wapp = _worker_app(be)
+    async with wapp.router.lifespan_context(wapp):
+        async with httpx.AsyncClient(transport=httpx.ASGITransport(app=wapp), base_url="http://w") as c:
+            r = await c.get("/health")
+            assert r.status_code == 200 and r.json()["status"] == "ok" and r.json()["role"] == "worker"
+        reg = WorkerRegistry([W1], failure_threshold=2, success_threshold=2)
+        hc = WorkerHealthChecker(reg, interval_seconds=0.02, timeout_seconds=0.5,
+                                 transport=httpx.ASGITransport(app=wapp))
+        await hc.start()
+        assert reg.healthy_endpoints() == [W1]
+        be.ok = False  # inject an engine fault: the worker's /health turns 503
+        async with httpx.AsyncClient(transport=httpx.ASGITransport(app=wapp), base_url="http://w") as c:
+            r = await c.get("/health")
+            assert r.status_code == 503 and r.json()["status"] == "unhealthy"
+        for _ in range(100):
+            if not reg.healthy_endpoints():
+                break
+            await asyncio.sleep(0.02)
+        assert reg.healthy_endpoints() == []  # demoted within failure_threshold probes
+        be.ok = True  # recovery needs success_threshold probes
+        for _ in range(100):
+            if reg.healthy_endpoints():
+                break
+            await asyncio.sleep(0.02)
+        assert reg.healthy_endpoints() == [W1]
+        await hc.stop()
+
+
+def test_native_backend_watchdog_is_configurable():
+    import time
+    from vgate.backends.native import NativeBackend
+
+    class _Eng:
+        healthy = True
+        last_step_wall = time.monotonic() - 5.0
+
+        def has_unfinished(self):
+            return True
+
+    nb = NativeBackend(_Eng(), watchdog_seconds=10.0)
+    assert nb.healthy()
+    nb.watchdog_seconds = 2.0  # work pending and no step for 5 s: a hung queue
+    assert not nb.healthy()
+    _Eng.has_unfinished = lambda self: False  # idle engines are never flagged
+    assert nb.healthy()

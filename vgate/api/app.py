@@ -217,6 +217,17 @@ def create_app(config: Optional[VGateConfig] = None, engine: Optional[VGateEngin
     # -------------------------------------------------------------- routes
     @app.get("/health", summary="Health Check")
     async def health_check():
+        # Liveness of THIS process's engine: a local native engine that faulted (a step raised,
+        # or the step watchdog saw no progress for model.watchdog_seconds with work pending) fails
+        # the probe with 503, so a gateway's WorkerHealthChecker demotes the worker after
+        # failure_threshold probes (reference main.py:288-295 is static).
+        eng = st.engine
+        if eng is not None and not eng.is_remote:
+            h = getattr(eng.backend, "healthy", None)
+            if callable(h) and not h():
+                detail = getattr(getattr(eng.backend, "engine", None), "last_error", None) or "engine unhealthy"
+                return _json({"status": "unhealthy", "version": version, "role": config.role,
+                              "detail": str(detail)}, 503)
         return {"status": "ok", "version": version, "role": config.role}
 
     @app.get("/ready", summary="Readiness")
@@ -436,12 +447,25 @@ async def _engine_metrics_loop(st: AppState, period: float = 1.0):
             s = stats()
             if not s:
                 continue
+            drain = getattr(getattr(b, "engine", None), "drain_step_times", None)
+            if callable(drain):
+                for ms in drain():
+                    M.ENGINE_STEP_SECONDS.observe(ms / 1e3)
+            h = getattr(b, "healthy", None)
+            if callable(h):
+                M.ENGINE_HEALTHY.set(1 if h() else 0)
+            M.ENGINE_GRAPH_HIT_RATIO.set(s.get("graph_hit_ratio", 0.0))
+            drain_ar = getattr(getattr(b, "engine", None), "drain_allreduce_times", None)
+            if callable(drain_ar):
+                for ms in drain_ar():
+                    M.ENGINE_ALLREDUCE_SECONDS.observe(ms / 1e3)
             M.ENGINE_RUNNING.set(s.get("running", 0))
             M.ENGINE_WAITING.set(s.get("waiting", 0))
             M.ENGINE_KV_USAGE.set(s.get("kv_usage", 0.0))
             for key, ctr in (("prefill_tokens", M.ENGINE_PREFILL_TOKENS), ("decode_tokens", M.ENGINE_DECODE_TOKENS),
                              ("graph_hits", M.ENGINE_GRAPH_REPLAYS), ("preemptions", M.ENGINE_PREEMPTIONS),
-                             ("prefix_cache_hits", M.ENGINE_PREFIX_HITS)):
+                             ("prefix_cache_hits", M.ENGINE_PREFIX_HITS),
+                             ("graph_misses_eager", M.ENGINE_EAGER_STEPS)):
                 v = s.get(key, 0)
                 d = v - last.get(key, 0)
                 if d > 0:

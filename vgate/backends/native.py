@@ -48,12 +48,14 @@ class NativeBackend:
     supports_concurrent_calls = True
     supports_streaming = True
 
-    def __init__(self, engine=None):
+    def __init__(self, engine=None, watchdog_seconds: float = 60.0):
         self.engine = engine
+        self.watchdog_seconds = float(watchdog_seconds)
 
     # ------------------------------------------------------------------ setup
     def load_model(self, model_config: ModelConfig) -> None:
         from vgate.runtime.engine import LLMEngine
+        self.watchdog_seconds = float(getattr(model_config, "watchdog_seconds", self.watchdog_seconds))
         cfg = engine_config_from(model_config)
         if getattr(model_config, "engine_process", False) and cfg.tensor_parallel_size == 1:
             from vgate.runtime.engine_process import EngineProcessClient
@@ -182,8 +184,8 @@ class NativeBackend:
             return False
         if not self.engine.healthy:
             return False
-        # watchdog: work pending but no step completed for a long time => hung queue
-        if self.engine.scheduler.has_work() and time.monotonic() - self.engine.last_step_wall > 60:
+        # watchdog: work pending but no step completed for watchdog_seconds => hung HIP queue
+        if self.engine.has_unfinished() and time.monotonic() - self.engine.last_step_wall > self.watchdog_seconds:
             return False
         return True
 

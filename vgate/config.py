@@ -103,6 +103,8 @@ class ModelConfig(_Section):
     enable_prefix_caching: bool = True
     hip_graph_token_buckets: Optional[list[int]] = None
     attention_partition_size: int = 0  # 0 = auto
+    # step watchdog: with work pending and no step completed for this long, /health fails (503)
+    watchdog_seconds: float = 60.0
 
     @field_validator("engine_type")
     @classmethod

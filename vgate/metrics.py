@@ -99,6 +99,14 @@ ENGINE_DECODE_TOKENS = _metric(Counter, "vgate_engine_decode_tokens_total", "Dec
 ENGINE_GRAPH_REPLAYS = _metric(Counter, "vgate_engine_hipgraph_replays_total", "Steps replayed from a hipGraph")
 ENGINE_PREEMPTIONS = _metric(Counter, "vgate_engine_preemptions_total", "Sequences preempted for KV memory")
 ENGINE_PREFIX_HITS = _metric(Counter, "vgate_engine_prefix_cache_hit_blocks_total", "KV blocks reused from the prefix cache")
+ENGINE_EAGER_STEPS = _metric(Counter, "vgate_engine_eager_steps_total",
+                             "Steps run without a captured hipGraph (first sight of a token/sequence bucket)")
+ENGINE_GRAPH_HIT_RATIO = _metric(Gauge, "vgate_engine_hipgraph_hit_ratio", "hipGraph replays / all steps (lifetime)")
+ENGINE_HEALTHY = _metric(Gauge, "vgate_engine_healthy", "1 while the engine passes its fault and watchdog checks")
+ENGINE_ALLREDUCE_SECONDS = _metric(Histogram, "vgate_engine_allreduce_seconds",
+                                   "Tensor-parallel all-reduce time per decode step (probed on the engine's own "
+                                   "comm path: every layer's two collectives at the decode message size)",
+                                   buckets=[1e-5, 2.5e-5, 5e-5, 1e-4, 2.5e-4, 5e-4, 1e-3, 2.5e-3, 5e-3, 1e-2])
 
 
 def init_app_info(version: str, model: str) -> None:

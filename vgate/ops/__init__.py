@@ -107,8 +107,9 @@ def row_permutation(N: int, layout: str) -> torch.Tensor | None:
     """Row order of the packed weight for a fused epilogue (None = identity).
 
     silu: [G0 U0 G1 U1 ...] 16-row tiles (gate rows then up rows in the dense matrix);
-    qkv : per 128-wide head, tiles [t0 t4 t1 t5 t2 t6 t3 t7] so each block's tile pair
-          holds the NeoX rotation partners d and d + 64.
+    qkv : per 128-wide head, tile t (t = 0..7) = rows 8t..8t+7 then their NeoX rotation
+          partners 64+8t..64+8t+7, so one 16-row tile holds both halves of 8 rotation pairs
+          (the GEMM epilogue exchanges them across lanes l, l^32; csrc/kernels/gemm.hip qkv_col).
     """
     if layout == "silu":
         I = N // 2
@@ -116,9 +117,9 @@ def row_permutation(N: int, layout: str) -> torch.Tensor | None:
         return t.reshape(-1)
     if layout == "qkv":
         assert N % 128 == 0
-        order = torch.tensor([0, 4, 1, 5, 2, 6, 3, 7])
         heads = N // 128
-        t = torch.arange(N).reshape(heads, 8, 16)[:, order]
+        tile = torch.arange(128).reshape(2, 8, 8).permute(1, 0, 2).reshape(8, 16)
+        t = torch.arange(heads)[:, None, None] * 128 + tile[None]
         return t.reshape(-1)
     return None
 
@@ -143,6 +144,11 @@ class Linear:
         self.bias = bias
         self.norm_gamma = None  # RMSNorm weight folded into the packed copy (see fold_norm)
         self.wl = None  # optional plain [N, K] copy for library (hipBLASLt) prefill GEMMs
+        # decode-GEMM decomposition for M <= 16 steps (0 = the launcher's heuristic): set by the
+        # model from the measured per-shape table (benchmarks/decode_sweep.py)
+        self.dec_waves = 0
+        self.dec_splitk = 0
+        self.dec_ntb = 0
         if self.kind == "awq":
             q = awq["qint"]
             self.N, self.K = q.shape
@@ -289,7 +295,10 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
         return _linear_library(x, lin, out, residual, norm, qkv)
     C = native()
     epi = 3 if qkv is not None else (2 if silu else (1 if out_f32 else 0))
-    kw = dict(bias=lin.bias, res=residual, ws=workspace(x.device), waves=waves, splitk=splitk)
+    ntb = 0
+    if M <= 16 and waves == 0 and splitk == 0:
+        waves, splitk, ntb = lin.dec_waves, lin.dec_splitk, lin.dec_ntb
+    kw = dict(bias=lin.bias, res=residual, ws=workspace(x.device), waves=waves, splitk=splitk, ntb=ntb)
     if norm is not None:
         if lin.norm_gamma is not None:  # gamma lives in the weights: row scale only
             kw.update(rownorm=True, eps=float(norm[1]))
@@ -480,7 +489,7 @@ def sample_workspace(device) -> torch.Tensor:
     key = str(device)
     ws = _SWS.get(key)
     if ws is None:
-        ws = torch.zeros(4096, dtype=torch.int32, device=device)
+        ws = torch.zeros(16384, dtype=torch.int32, device=device)
         _SWS[key] = ws
     return ws
 

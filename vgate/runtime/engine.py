@@ -84,6 +84,8 @@ class EngineStats:
     cycle_time_s: float = 0.0  # schedule + execute + output processing
     requests_finished: int = 0
     last_step_ms: float = 0.0
+    max_cycle_ms: float = 0.0  # slowest schedule -> launch -> collect cycle and its (T, S) bucket
+    max_cycle_bucket: tuple = (0, 0)
     batch_sizes: collections.Counter = field(default_factory=collections.Counter)
 
 
@@ -200,6 +202,8 @@ class LLMEngine:
         if stream:
             seq.detok = IncrementalDecoder(self.tokenizer)
         with self._cv:
+            if not self.has_unfinished():  # the step watchdog measures from the first work on
+                self.last_step_wall = time.monotonic()
             self._inbox.append(seq)
             self._cv.notify()
         return seq
@@ -399,6 +403,10 @@ class LLMEngine:
         st.step_time_s += now - t0
         st.cycle_time_s += now - tc
         st.last_step_ms = 1e3 * (now - t0)
+        cyc = 1e3 * (now - tc)
+        if cyc > st.max_cycle_ms:
+            st.max_cycle_ms = cyc
+            st.max_cycle_bucket = (batch.num_tokens, len(batch.items))
         st.prefill_tokens += batch.num_prefill_tokens
         st.decode_tokens += batch.num_decode
         st.batch_sizes[len(batch.items)] += 1
@@ -565,6 +573,17 @@ class LLMEngine:
             self._broadcast_header(-1, 0, 0)
 
     # ------------------------------------------------------------------- stats
+    def drain_step_times(self) -> list[float]:
+        """Device time (ms) of every step collected since the last call (metrics loop)."""
+        r = self.runner
+        out, r.step_gpu_ms = r.step_gpu_ms, []
+        return out
+
+    def reset_peaks(self) -> None:
+        """Restart the slowest-step trackers (a benchmark's timed region starts here)."""
+        self.runner.max_gpu_ms, self.runner.max_gpu_bucket, self.runner.max_gpu_eager = 0.0, (0, 0), False
+        self.stats.max_cycle_ms, self.stats.max_cycle_bucket = 0.0, (0, 0)
+
     def snapshot(self) -> dict:
         st = self.stats
         return {
@@ -580,6 +599,13 @@ class LLMEngine:
             "graphs_captured": len(self.runner.graphs), "graph_hits": self.runner.graph_hits,
             "graph_misses_eager": self.runner.graph_misses,
             "pending_captures": len(self.runner.pending_captures),
+            "graph_captures": self.runner.captures,
+            "graph_hit_ratio": round(self.runner.graph_hits / max(1, self.runner.graph_hits + self.runner.graph_misses), 4),
+            "max_gpu_step_ms": round(self.runner.max_gpu_ms, 3),
+            "max_gpu_step_bucket": list(self.runner.max_gpu_bucket),
+            "max_gpu_step_eager": self.runner.max_gpu_eager,
+            "max_cycle_ms": round(st.max_cycle_ms, 3),
+            "max_cycle_tokens_seqs": list(st.max_cycle_bucket),
             "preemptions": self.scheduler.num_preemptions, "prefix_cache_hits": int(getattr(self.kvm.alloc, "hits", 0)),
             "healthy": self.healthy,
         }

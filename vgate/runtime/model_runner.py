@@ -60,6 +60,8 @@ class StepHandle:
     samples: list[bool]    # item consumes its sampled token
     toks: list[int] | None  # already known (CPU path)
     t_launch: float
+    bucket: tuple = (0, 0)  # (T, S) graph bucket of the step
+    eager: bool = False     # ran without a captured graph (first sight of its bucket)
 
 
 class ModelRunner:
@@ -109,6 +111,11 @@ class ModelRunner:
         self.gpu_ms = 0.0  # device time of replayed steps (upload -> sampled ids on host)
         self.host_ms = 0.0  # host time of execute() outside the device wait
         self.gpu_steps = 0
+        self.captures = 0  # hipGraph captures so far (start-up warm-up + deferred + on-miss)
+        self.max_gpu_ms = 0.0  # slowest step's device time and its bucket (p99 forensics)
+        self.max_gpu_bucket = (0, 0)
+        self.max_gpu_eager = False
+        self.step_gpu_ms: list[float] = []  # device time per collected step, drained by the metrics loop
 
     # ----------------------------------------------------------------- buckets
     def _bucket(self, buckets, n):
@@ -217,6 +224,7 @@ class ModelRunner:
                 self._forward_sample(view)
             execs.append(g)
         torch.cuda.synchronize()
+        self.captures += 1
         self.capture_seconds += time.perf_counter() - t0
         log.debug("captured hipGraph T=%d S=%d in %.1f ms", T, S, 1e3 * (time.perf_counter() - t0))
         return execs[0] if len(execs) == 1 else _GraphRing(execs)
@@ -256,6 +264,7 @@ class ModelRunner:
             saved = self.out_tokens.clone()
             g = self.graphs[(T, S)] = self._capture(T, S)
             self.out_tokens.copy_(saved)
+        eager = g is None
         if g is not None:
             self.graph_hits += 1
             g.replay()
@@ -273,15 +282,20 @@ class ModelRunner:
         self.out_hosts[k][:ns].copy_(self.out_tokens[:ns], non_blocking=True)
         self.dones[k].record()
         self.host_ms += 1e3 * (time.perf_counter() - t_host)
-        return StepHandle(k, ns, samples, None, t_host)
+        return StepHandle(k, ns, samples, None, t_host, (T, S), eager)
 
     def collect(self, h: "StepHandle") -> list[int]:
         """Wait for a launched step and return its sampled ids (one per batch item)."""
         if h.toks is not None:
             return h.toks
         self.dones[h.k].synchronize()
-        self.gpu_ms += self.started[h.k].elapsed_time(self.dones[h.k])
+        ms = self.started[h.k].elapsed_time(self.dones[h.k])
+        self.gpu_ms += ms
         self.gpu_steps += 1
+        if ms > self.max_gpu_ms:
+            self.max_gpu_ms, self.max_gpu_bucket, self.max_gpu_eager = ms, h.bucket, h.eager
+        if len(self.step_gpu_ms) < 65536:
+            self.step_gpu_ms.append(ms)
         return self.out_hosts[h.k][: h.ns].tolist()
 
     @torch.inference_mode()
