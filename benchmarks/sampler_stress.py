@@ -24,10 +24,13 @@ def main():
     ap.add_argument("--groups", type=int, default=200)
     ap.add_argument("--per-group", type=int, default=100)
     ap.add_argument("--vocab", type=int, default=151936)
+    ap.add_argument("--nseg", default="16,32,64,128", help="caps on segments per row to sweep")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     res = {}
-    for B in (1, 2, 8, 32):
+    caps = [int(c) for c in a.nseg.split(",")]
+    for cap, B in [(c, b) for c in caps for b in (1, 8, 32)]:
+        ops.native().set_sample_nseg(cap)
         torch.manual_seed(B)
         logits = torch.randn(B, a.vocab, device=dev) * 0.8
         temp = torch.full((B,), 0.7, device=dev)
@@ -50,9 +53,10 @@ def main():
             e.synchronize()
             times.append(1e3 * s.elapsed_time(e) / a.per_group)
         times.sort()
-        res[f"B{B}"] = {"median_us": round(times[len(times) // 2], 2), "max_group_avg_us": round(times[-1], 2),
-                        "nseg": ops.native().sample_segments(B, a.vocab) if hasattr(ops.native(), "sample_segments") else None}
-        print(json.dumps({"B": B, **res[f"B{B}"]}), flush=True)
+        res[f"cap{cap}_B{B}"] = {"median_us": round(times[len(times) // 2], 2),
+                                 "max_group_avg_us": round(times[-1], 2),
+                                 "nseg": ops.native().sample_segments(B, a.vocab)}
+        print(json.dumps({"cap": cap, "B": B, **res[f"cap{cap}_B{B}"]}), flush=True)
     print(json.dumps({"sampler_stress": res}), flush=True)
 
 

@@ -73,8 +73,14 @@ def main():
             rows.append({"kernel": name, "blocks": nb, "ran": 0})
             continue
         st, en = blk[ok, 0], blk[ok, 1]
+        d = ((en - st).float() / TICKS_PER_US).sort().values
+        s0 = ((st - st.min()).float() / TICKS_PER_US).sort().values
+        e0 = ((en - st.min()).float() / TICKS_PER_US).sort().values
+        q = lambda v, f: float(v[min(len(v) - 1, int(f * len(v)))])  # noqa: E731
         rows.append({"kernel": name, "blocks": nb, "ran": int(ok.sum()), "t0": int(st.min()), "t1": int(en.max()),
-                     "dur_med": float((en - st).float().median()) / TICKS_PER_US})
+                     "dur_med": q(d, 0.5), "dur_p10": q(d, 0.1), "dur_p90": q(d, 0.9), "dur_max": q(d, 1.0),
+                     "start_p90": q(s0, 0.9), "start_max": q(s0, 1.0), "end_p10": q(e0, 0.1), "end_p50": q(e0, 0.5),
+                     "end_p90": q(e0, 0.9)})
     live = [x for x in rows if x.get("ran")]
     live.sort(key=lambda x: x["t0"])
     T0 = live[0]["t0"]
@@ -84,6 +90,8 @@ def main():
         x["span_us"] = (x["t1"] - x["t0"]) / TICKS_PER_US
         x["gap_after_us"] = ((live[i + 1]["t0"] - x["t1"]) / TICKS_PER_US) if i + 1 < len(live) else 0.0
         g = agg[(x["kernel"], x["blocks"])]
+        for k in ("dur_med", "dur_p10", "dur_p90", "dur_max", "start_p90", "start_max", "end_p10", "end_p50", "end_p90"):
+            g[k] = g.get(k, 0.0) + x[k]
         g["n"] += 1
         g["span_us"] += x["span_us"]
         g["gap_after_us"] += x["gap_after_us"]
@@ -92,7 +100,9 @@ def main():
     summary = {"batch": a.batch, "ctx": a.ctx, "kv_blocks": eng.num_blocks, "launches": len(live), "step_us": round(total, 1), "sum_span_us": round(spans, 1),
                "sum_gap_us": round(total - spans, 1),
                "per_kernel": {f"{k[0]}[{k[1]}]": {"n": v["n"], "avg_span_us": round(v["span_us"] / v["n"], 2),
-                                                  "avg_gap_after_us": round(v["gap_after_us"] / v["n"], 2)}
+                                                  "avg_gap_after_us": round(v["gap_after_us"] / v["n"], 2),
+                                                  **{k: round(v[k] / v["n"], 2) for k in ("dur_p10", "dur_med", "dur_p90",
+                                                     "dur_max", "start_p90", "start_max", "end_p10", "end_p50", "end_p90")}}
                               for k, v in sorted(agg.items(), key=lambda kv: -kv[1]["span_us"])}}
     print(json.dumps(summary), flush=True)
     for x in live[:14]:

@@ -162,6 +162,22 @@ __device__ __forceinline__ f32x4 ld_sc1_x4(const float* base, uint32_t off_bytes
 // all of this thread's stores have reached the device-coherent level
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// LDS-DMA of one 16-B piece per lane (global_load_lds_dwordx4; the wave's 64 pieces land at
+// lds_addr + 16 * lane). Written as inline asm so hipcc's alias analysis does not treat the
+// in-flight DMA as an LDS write that every later ds_read must wait for (it emits vmcnt(0) in
+// front of the first ds_read of the OTHER ring buffer otherwise, which serialises the stage
+// pipeline). The caller owns the vmcnt bookkeeping (cdna_hip_programming.md §5.7 item 1).
+// lds_addr must be wave-uniform; M0 is saved / restored inside the statement.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_addr) : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
+  // generic -> LDS address-space cast (addrspacecast: the aperture offset), then its 32 bits
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(p);
+}
+
 // Workgroup barrier for LDS hand-offs that leaves global loads in flight: __syncthreads()
 // is a release/acquire fence, which on gfx9 waits vmcnt(0) and so drains every outstanding
 // weight prefetch; this waits only for this wave's LDS traffic (lgkmcnt) and then barriers.

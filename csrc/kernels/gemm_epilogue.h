@@ -1,0 +1,214 @@
+// Shared pieces of the fragment-packed GEMM family (gemm.hip: decode / tile kernels,
+// gemm_prefill.hip: the LDS-tiled prefill kernel): launch parameters, the per-row epilogue
+// (bias, residual, SiLU*mul, f32 logits, QKV bias + NeoX RoPE + paged-KV write) and its
+// launch-time operand prefetch. Every kernel produces D = W x X^T with the MFMA orientation
+// "lane holds D[n = 4(l>>4)+i][m = l&15]", so one epilogue serves all of them.
+#pragma once
+#include "common.h"
+#include "launchers.h"
+
+namespace vgate {
+
+enum GemmEpi : int { EPI_BF16 = 0, EPI_F32 = 1, EPI_SILU = 2, EPI_QKV = 3 };
+constexpr int SK_MAX = 8;  // split-K slices per tile (the combine issues all slices' loads at once)
+
+struct GemmParams {
+  const bf16_t* x; int lda; int M; const int32_t* row_idx;
+  const uint4* wp; int N; int K;
+  const bf16_t* norm_w; float eps;  // norm_w null under NORM = gamma folded into W (row scale only)
+  const bf16_t* bias; const bf16_t* res; int ldr;
+  void* out; int ldo;
+  int splitk; float* slabs; uint32_t* counters;
+  const int32_t* positions; const int32_t* slots; const float* cos_sin;
+  bf16_t* k_cache; bf16_t* v_cache; int hq; int hkv; int bs;
+  const bf16_t* scales; const bf16_t* zeros; int group;
+  unsigned long long* dbg_ts;  // per-block [start, end] realtime stamps (profiling), or null
+};
+
+__device__ __forceinline__ int row_of(const GemmParams& p, int m) {
+  m = m < p.M ? m : p.M - 1;  // clamp: duplicated rows are computed but never stored
+  return p.row_idx ? p.row_idx[m] : m;
+}
+
+// LDS carve (one dynamic array; Guideline 17): [reduce | ssq[nw][16*MB] | flag]
+template <int MB, int NTB>
+__host__ __device__ constexpr int red_bytes(int nw) { return nw > 1 ? nw * MB * NTB * 64 * 16 : 0; }
+template <int MB>
+__host__ __device__ constexpr int ssq_bytes(int nw) { return nw * MB * 16 * 4; }
+
+// NORM: one A fragment (8 elements of row m at column k0): accumulate x^2 for the
+// deferred row scale and return bf16(x * w) for the MFMA. With gamma folded into the
+// packed weight at load time (w == null) the fragment passes through unchanged and no
+// gamma bytes are fetched (they would double the per-k-step vector-memory requests).
+template <int MODE>  // 1: gamma in registers, 2: gamma folded into W (row scale only)
+__device__ __forceinline__ uint4 norm_frag(uint4 a, const bf16_t* w, int k0, float& ss) {
+  float f[8];
+  unpack8(a, f);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
+  if constexpr (MODE == 2) {
+    return a;
+  } else {
+    const uint4 wv = *reinterpret_cast<const uint4*>(w + k0);
+    float g[8];
+    unpack8(wv, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] *= g[j];
+    return pack8(f);
+  }
+}
+
+// ---- epilogue operands that do not depend on the GEMM result ----
+// The decode kernel loads them at launch (phase A: row / bias / residual words, phase B:
+// the RoPE cos/sin row of the position, issued once the first weight group is in flight),
+// so the epilogue after the reduction is pure ALU + stores instead of a dependent
+// positions -> cos_sin load chain behind the whole GEMM (benchmarks/qkv_probe.py).
+// QKV tile layout (ops.row_permutation "qkv"): tile t of head h (16 columns) holds the head's
+// columns 8t..8t+7 (lane groups 0, 1) and their NeoX rotation partners 64+8t..64+8t+7 (groups
+// 2, 3), so a rotation pair sits on lanes l and l ^ 32 of ONE tile (exchanged by permlane32).
+// qkv_rot: rotation index (0..63) of the lane's first column; qkv_col: that column in [q|k|v].
+__device__ __forceinline__ int qkv_rot(int nt, int nsub) { return 8 * (nt & 7) + (nsub & 4); }
+__device__ __forceinline__ int qkv_col(int nt, int nsub) {
+  return (nt >> 3) * 128 + (nsub >= 8 ? 64 : 0) + qkv_rot(nt, nsub);
+}
+
+// (plain scalar members: an array member keeps the whole struct in scratch)
+template <int NTB>
+struct EpiPre {
+  uint2 r0, r1;  // EPI_BF16: residual words of tile 0 / 1 (4 bf16 each)
+  uint2 b0, b1;  // EPI_BF16 / EPI_F32: bias words of tile 0 / 1; EPI_QKV: bias of the lane's 4 columns
+  float4 cs, sn;
+  int pos, slot;
+};
+
+template <int NTB, int EPI>
+__device__ __forceinline__ void epi_pre_a(const GemmParams& p, EpiPre<NTB>& e, int m, int nt0, int nsub) {
+  m = m < p.M ? m : p.M - 1;
+  if constexpr (EPI == EPI_QKV) {
+    e.pos = p.positions[m];
+    e.slot = p.slots[m];
+    e.b0 = p.bias ? *reinterpret_cast<const uint2*>(p.bias + qkv_col(nt0, nsub)) : make_uint2(0, 0);
+  } else if constexpr (EPI == EPI_BF16 || EPI == EPI_F32) {
+#pragma unroll
+    for (int j = 0; j < NTB; ++j) {
+      const int n = (nt0 + j) * 16 + nsub;
+      const uint2 b = p.bias ? *reinterpret_cast<const uint2*>(p.bias + n) : make_uint2(0, 0);
+      uint2 r = make_uint2(0, 0);
+      if constexpr (EPI == EPI_BF16) r = p.res ? *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldr + n) : r;
+      if (j == 0) { e.b0 = b; e.r0 = r; } else { e.b1 = b; e.r1 = r; }
+    }
+  }
+}
+
+template <int NTB, int EPI>
+__device__ __forceinline__ void epi_pre_b(const GemmParams& p, EpiPre<NTB>& e, int nt0, int nsub) {
+  if constexpr (EPI == EPI_QKV) {
+    const int d = qkv_rot(nt0, nsub);
+    const float* cs = p.cos_sin + (size_t)e.pos * 128;
+    e.cs = *reinterpret_cast<const float4*>(cs + d);
+    e.sn = *reinterpret_cast<const float4*>(cs + 64 + d);
+  }
+}
+
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// ---- epilogue for one (row m, 4 columns) group; v[j] are the NTB reduced tiles ----
+// `e` = operands prefetched at launch (decode kernel) when `have`, else loaded here.
+// `have` is a compile-time choice: a runtime select between a prefetched register value
+// and a load becomes a select of ADDRESSES that puts the prefetch struct in scratch.
+// `valid`: row m < M. Every lane of the wave calls in (the QKV pair exchange is a cross-lane
+// op); only valid rows store.
+template <int NTB, int EPI, bool have>
+__device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[NTB], int m, int nt0, int nsub,
+                                         const EpiPre<NTB> e, bool valid) {
+  if constexpr (EPI != EPI_QKV) {
+    if (!valid) return;
+  }
+  if constexpr (EPI == EPI_SILU) {
+    const int n = (nt0 >> 1) * 16 + nsub;
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = silu(v[0][i]) * v[NTB - 1][i];
+    uint2 pk;
+    pk.x = pack_bf2(o[0], o[1]);
+    pk.y = pack_bf2(o[2], o[3]);
+    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + n) = pk;
+  } else if constexpr (EPI == EPI_QKV) {
+    static_assert(NTB == 1, "QKV tiles carry their rotation partners (see qkv_col)");
+    const int head = nt0 >> 3;
+    const int d = qkv_rot(nt0, nsub);  // rotation index of this lane's 4 columns
+    const bool upper = nsub >= 8;      // partner half (d + 64)
+    uint2 w;
+    float4 cs, sn;
+    int slot;
+    if constexpr (have) {
+      w = e.b0; cs = e.cs; sn = e.sn; slot = e.slot;
+    } else {
+      const int mm = m < p.M ? m : p.M - 1;
+      w = p.bias ? *reinterpret_cast<const uint2*>(p.bias + qkv_col(nt0, nsub)) : make_uint2(0, 0);
+      const float* cp = p.cos_sin + (size_t)p.positions[mm] * 128;
+      cs = *reinterpret_cast<const float4*>(cp + d);
+      sn = *reinterpret_cast<const float4*>(cp + 64 + d);
+      slot = p.slots[mm];
+    }
+    const float b[4] = {bf_lo(w.x), bf_hi(w.x), bf_lo(w.y), bf_hi(w.y)};
+    float x[4], xp[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = bf2f(f2bf(v[0][i] + b[i]));  // qkv is bf16 in the reference: round before rotating
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xp[i] = xor32(x[i]);  // the partner column's value (all 64 lanes active)
+    if (head < p.hq + p.hkv) {  // q or k: NeoX rotation
+      const float cc[4] = {cs.x, cs.y, cs.z, cs.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x[i] = upper ? x[i] * cc[i] + xp[i] * ss[i] : x[i] * cc[i] - xp[i] * ss[i];
+    }
+    if (!valid) return;
+    uint2 pk;
+    pk.x = pack_bf2(x[0], x[1]);
+    pk.y = pack_bf2(x[2], x[3]);
+    const int dcol = (upper ? 64 : 0) + d;  // column inside the head
+    if (head < p.hq) {
+      *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + head * 128 + dcol) = pk;
+    } else if (slot >= 0) {
+      const bool is_k = head < p.hq + p.hkv;
+      const int kh = is_k ? head - p.hq : head - p.hq - p.hkv;
+      bf16_t* dst = (is_k ? p.k_cache : p.v_cache) +
+                    (((size_t)(slot / p.bs) * p.hkv + kh) * p.bs + (slot % p.bs)) * 128 + dcol;
+      *reinterpret_cast<uint2*>(dst) = pk;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NTB; ++j) {
+      const int n = (nt0 + j) * 16 + nsub;
+      float o[4] = {v[j][0], v[j][1], v[j][2], v[j][3]};
+      if (p.bias) {
+        uint2 b;
+        if constexpr (have) b = j == 0 ? e.b0 : e.b1;
+        else b = *reinterpret_cast<const uint2*>(p.bias + n);
+        o[0] += bf_lo(b.x); o[1] += bf_hi(b.x);
+        o[2] += bf_lo(b.y); o[3] += bf_hi(b.y);
+      }
+      if constexpr (EPI == EPI_F32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.out) + (size_t)m * p.ldo + n) =
+            make_float4(o[0], o[1], o[2], o[3]);
+      } else {
+        if (p.res) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] = bf2f(f2bf(o[i]));  // torch: (x@W).bf16() + res
+          uint2 r;
+          if constexpr (have) r = j == 0 ? e.r0 : e.r1;
+          else r = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldr + n);
+          o[0] += bf_lo(r.x); o[1] += bf_hi(r.x);
+          o[2] += bf_lo(r.y); o[3] += bf_hi(r.y);
+        }
+        uint2 pk;
+        pk.x = pack_bf2(o[0], o[1]);
+        pk.y = pack_bf2(o[2], o[3]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + n) = pk;
+      }
+    }
+  }
+}
+
+}  // namespace vgate

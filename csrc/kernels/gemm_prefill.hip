@@ -1,0 +1,275 @@
+// LDS-tiled MFMA GEMM for prefill / long steps (M >= 128) on gfx950 — the hand-written
+// replacement of the hipBLASLt path, on the SAME fragment-packed weights the decode kernels
+// stream (no second plain copy of any weight is kept).
+//
+//   out[m][n] = epilogue( rowscale(m) * sum_k x[m][k] * W[n][k] )
+//
+// Both operands are staged global -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave
+// instruction) into a 2-deep ring, BK = 64 (two 32-deep MFMA k-steps per stage):
+//   * W: the packed layout Wp[nt][kt][lane][8] IS the MFMA A-fragment order, so one 1 KiB
+//     piece (one 16-column tile x one k-step) lands lane-linear and every wave reads its
+//     fragments back with conflict-free ds_read_b128 (lane l at +16 l) — no swizzle needed;
+//   * x: each 1 KiB piece gathers the B fragments of 16 rows x 32 k (per-lane source address =
+//     row m0 + (l & 15), column 8 (l >> 4)), so the LDS image is fragment-major too.
+// Pipeline (cdna_hip_programming.md §5 'glds vs register staging', first row): the stage t+1
+// DMA is issued before stage t's ds_reads + MFMAs, one vmcnt(0) + barrier per stage.
+// Block tile BM x BN over 4 waves (2 x 2), wave tile (BM/2) x (BN/2) in 16x16x32 bf16 MFMAs,
+// orientation D = W(A) . X(B): lane holds D[n = 4(l>>4)+i][m = l&15], so the epilogues of the
+// decode kernels (gemm_epilogue.h: bias, residual, SiLU*mul pairs, QKV RoPE + KV write) are
+// reused unchanged. The RMSNorm in front of qkv / gate_up runs as the deferred row scale
+// (gamma folded into W at load time): x^2 is accumulated from the B fragments the MFMAs read.
+// Grid: 1-D, XCD-aware bijective remap, m-blocks fastest so the blocks that share a weight
+// column panel run back to back on one XCD (one HBM read of the panel per XCD L2).
+#include "gemm_epilogue.h"
+
+namespace vgate {
+
+template <int BM, int BN, int EPI, int NORM, int NTB>
+__global__ __launch_bounds__(256, 2) void gemm_prefill_kernel(GemmParams p) {
+  static_assert(BM % 32 == 0 && BN % 32 == 0, "2 x 2 waves of 16-multiple tiles");
+  constexpr int KS = 2;                      // 32-deep k-steps per stage (BK = 64)
+  constexpr int WTN = BN / 16, XTM = BM / 16;  // 16-wide tiles per block
+  constexpr int NT = WTN / 2, MT = XTM / 2;    // per wave
+  constexpr int PIECES = (WTN + XTM) * KS;     // 1 KiB pieces per stage
+  static_assert(PIECES % 4 == 0, "pieces split evenly over 4 waves");
+  constexpr int PPW = PIECES / 4;              // per wave
+  constexpr int STAGE = PIECES * 1024;
+  static_assert(NT % NTB == 0, "epilogue tile groups");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  TLScope tl_scope(p.dbg_ts);
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int KT = p.K >> 5;
+  const int nk_all = p.K >> 6;  // stages (K % 64 == 0, host-checked)
+  // split-K (small tile grids): blockIdx.y = K slice; partials go to the reduce kernel
+  const int z = blockIdx.y, nz = gridDim.y;
+  const int kst0 = (nk_all * z) / nz, nk = (nk_all * (z + 1)) / nz - kst0;
+  // XCD-aware logical block id (bijective for any grid size), then m fastest
+  const int mblocks = (p.M + BM - 1) / BM;
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int m0 = (wgid % mblocks) * BM;
+  const int nt_blk = (wgid / mblocks) * WTN;  // first 16-column tile of the block
+  // this wave's DMA pieces: piece f < WTN*KS is W tile f / KS at k-step f % KS, else x
+  // m-tile (f - WTN*KS) / KS. Source addresses per lane, advanced by one stage per iteration.
+  const char* src[PPW];
+  int step[PPW];  // bytes per stage
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int f = wid * PPW + i;
+    if (f < WTN * KS) {
+      const int nt = nt_blk + f / KS, ks = f % KS;
+      src[i] = reinterpret_cast<const char*>(p.wp) + (((size_t)nt * KT + 2 * kst0 + ks) * 64 + lane) * 16;
+      step[i] = KS * 1024;
+    } else {
+      const int g = f - WTN * KS;
+      const int mt = g / KS, ks = g % KS;
+      int row = m0 + mt * 16 + (lane & 15);
+      row = row < p.M ? row : p.M - 1;  // rows past M repeat row M-1 (never stored)
+      src[i] = reinterpret_cast<const char*>(p.x + (size_t)row * p.lda + kst0 * 64 + ks * 32 + 8 * (lane >> 4));
+      step[i] = 64 * 2;
+    }
+  }
+  const uint32_t lds0 = lds_addr_of(smem);
+  auto issue = [&](int stage, int buf) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int f = wid * PPW + i;  // wave-uniform LDS destination (M0): lane l lands at +16 l
+      glds16(src[i] + (size_t)stage * step[i], __builtin_amdgcn_readfirstlane(lds0 + buf * STAGE + f * 1024));
+    }
+  };
+  f32x4 acc[NT][MT];
+#pragma unroll
+  for (int a = 0; a < NT; ++a)
+#pragma unroll
+    for (int b = 0; b < MT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ss[MT];
+#pragma unroll
+  for (int b = 0; b < MT; ++b) ss[b] = 0.f;
+
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nk) issue(t + 1, buf ^ 1);
+    const char* sb = smem + buf * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      uint4 wa[NT], xb[MT];
+#pragma unroll
+      for (int a = 0; a < NT; ++a)
+        wa[a] = *reinterpret_cast<const uint4*>(sb + ((wn * NT + a) * KS + ks) * 1024 + lane * 16);
+#pragma unroll
+      for (int b = 0; b < MT; ++b)
+        xb[b] = *reinterpret_cast<const uint4*>(sb + (WTN * KS + (wm * MT + b) * KS + ks) * 1024 + lane * 16);
+      if constexpr (NORM == 2) {
+#pragma unroll
+        for (int b = 0; b < MT; ++b) {
+          float f[8];
+          unpack8(xb[b], f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss[b] += f[j] * f[j];
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < NT; ++a)
+#pragma unroll
+        for (int b = 0; b < MT; ++b) acc[a][b] = mfma16(as_bf16x8(wa[a]), as_bf16x8(xb[b]), acc[a][b]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (nz > 1) {
+    // fp32 partial of this K slice -> slabs [z][M][N] (row-major, the lane's 4 columns as one
+    // 16-B store) and its rows' partial sums of squares -> [z][M] after the tiles; the reduce
+    // kernel sums the slices in a fixed order (bit-reproducible) and runs the epilogue
+    float* part = p.slabs + (size_t)z * p.M * p.N;
+    float* ssq = p.slabs + (size_t)nz * p.M * p.N + (size_t)z * p.M;
+#pragma unroll
+    for (int b = 0; b < MT; ++b) {
+      const int m = m0 + wm * (BM / 2) + b * 16 + (lane & 15);
+      if constexpr (NORM == 2) {
+        float s2 = ss[b];
+        s2 += xor16(s2);
+        s2 += xor32(s2);
+        if (wn == 0 && lane < 16 && m < p.M) ssq[m] = s2;
+      }
+      if (m < p.M) {
+#pragma unroll
+        for (int a = 0; a < NT; ++a) {
+          const int n = (nt_blk + wn * NT + a) * 16 + 4 * (lane >> 4);
+          *reinterpret_cast<f32x4*>(part + (size_t)m * p.N + n) = acc[a][b];
+        }
+      }
+    }
+    return;
+  }
+  // epilogue straight from the accumulators: row m = m0 + wm*(BM/2) + 16 b + (l & 15)
+#pragma unroll
+  for (int b = 0; b < MT; ++b) {
+    const int m = m0 + wm * (BM / 2) + b * 16 + (lane & 15);
+    float sc = 1.f;
+    if constexpr (NORM == 2) {
+      float s2 = ss[b];
+      s2 += xor16(s2);
+      s2 += xor32(s2);
+      sc = rsqrtf(s2 / (float)p.K + p.eps);
+    }
+#pragma unroll
+    for (int a = 0; a < NT; a += NTB) {
+      f32x4 v[NTB];
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) v[j] = acc[a + j][b] * sc;
+      epilogue<NTB, EPI, false>(p, v, m, nt_blk + wn * NT + a, 4 * (lane >> 4), EpiPre<NTB>{}, m < p.M);
+    }
+  }
+}
+
+// Split-K combine: one wave per (16 rows, NTB tiles): the slices' partials summed in slice
+// order, the row scale from the summed slice sums of squares, then the shared epilogue.
+template <int EPI, int NORM, int NTB>
+__global__ __launch_bounds__(256) void prefill_reduce_kernel(GemmParams p, int nz) {
+  TLScope tl_scope(p.dbg_ts);
+  const int lane = threadIdx.x & 63;
+  const int grp = blockIdx.x * 4 + (threadIdx.x >> 6);  // (row block, tile group), tile group fastest
+  const int ngrp = p.N / (16 * NTB);
+  if (grp >= ((p.M + 15) / 16) * ngrp) return;  // wave-uniform
+  const int m = (grp / ngrp) * 16 + (lane & 15);
+  const int nt0 = (grp % ngrp) * NTB;
+  const int nsub = 4 * (lane >> 4);
+  const int mm = m < p.M ? m : p.M - 1;
+  f32x4 v[NTB];
+#pragma unroll
+  for (int j = 0; j < NTB; ++j) v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float s2 = 0.f;
+  for (int z = 0; z < nz; ++z) {
+    const float* part = p.slabs + (size_t)z * p.M * p.N + (size_t)mm * p.N;
+#pragma unroll
+    for (int j = 0; j < NTB; ++j) v[j] += *reinterpret_cast<const f32x4*>(part + (nt0 + j) * 16 + nsub);
+    if constexpr (NORM == 2) s2 += p.slabs[(size_t)nz * p.M * p.N + (size_t)z * p.M + mm];
+  }
+  if constexpr (NORM == 2) {
+    const float sc = rsqrtf(s2 / (float)p.K + p.eps);
+#pragma unroll
+    for (int j = 0; j < NTB; ++j) v[j] *= sc;
+  }
+  epilogue<NTB, EPI, false>(p, v, m, nt0, nsub, EpiPre<NTB>{}, m < p.M);
+}
+
+template <int BM, int BN, int EPI, int NORM, int NTB>
+static void launch_prefill_cfg(const GemmParams& p, int nz, hipStream_t st) {
+  constexpr int STAGE = (BN / 16 + BM / 16) * 2 * 1024;
+  const int blocks = ((p.M + BM - 1) / BM) * (p.N / BN);
+  GemmParams q = p;
+  if (q.dbg_ts == nullptr) q.dbg_ts = tl_take("gemm_prefill", blocks * nz);
+  hipLaunchKernelGGL((gemm_prefill_kernel<BM, BN, EPI, NORM, NTB>), dim3(blocks, nz), dim3(256), 2 * STAGE, st, q);
+  if (nz > 1) {
+    const int groups = ((p.M + 15) / 16) * (p.N / (16 * NTB));
+    GemmParams r = p;
+    r.dbg_ts = tl_take("prefill_reduce", (groups + 3) / 4);
+    hipLaunchKernelGGL((prefill_reduce_kernel<EPI, NORM, NTB>), dim3((groups + 3) / 4), dim3(256), 0, st, r, nz);
+  }
+}
+
+// Tile shape: 128 x 128 when that grid covers the chip, else 128 x 64 (narrow N: o_proj,
+// down, 70B/TP shards). A grid still under ~200 blocks is split along K (>= 4 stages of 64 per
+// slice, <= 8 slices, partials within the workspace) and combined by prefill_reduce_kernel.
+// Returns false for shapes the kernel does not take (the caller keeps the N-split tile
+// kernel): K % 64, N % 64, a row gather, the gamma-in-registers RMSNorm mode.
+template <int EPI, int NORM>
+static bool launch_prefill_epi(const GemmParams& p, int force_bn, int force_sk, size_t slab_bytes, hipStream_t st) {
+  constexpr int NTB = EPI == EPI_SILU ? 2 : 1;
+  if (p.K % 64 != 0 || p.N % 64 != 0 || p.row_idx != nullptr) return false;
+  const int mb = (p.M + 127) / 128;
+  bool wide = p.N % 128 == 0 && mb * (p.N / 128) >= 240;
+  if (force_bn == 128) wide = p.N % 128 == 0;
+  if (force_bn == 64) wide = false;
+  const int blocks = mb * (p.N / (wide ? 128 : 64));
+  int nz = 1;
+  if (force_sk > 0) {
+    nz = force_sk;
+  } else if (blocks < 200) {
+    nz = (256 + blocks - 1) / blocks;
+    nz = nz > 8 ? 8 : nz;
+  }
+  const int nk = p.K / 64;
+  while (nz > 1 && nk / nz < 4) --nz;
+  const size_t need = ((size_t)nz * p.M * p.N + (size_t)nz * p.M) * 4;
+  if (nz > 1 && (p.slabs == nullptr || need > slab_bytes)) nz = 1;
+  if (wide) launch_prefill_cfg<128, 128, EPI, NORM, NTB>(p, nz, st);
+  else launch_prefill_cfg<128, 64, EPI, NORM, NTB>(p, nz, st);
+  return true;
+}
+
+bool launch_gemm_prefill(const GemmArgs& g, hipStream_t st) {
+  if (g.M <= 0) return true;
+  const int norm = g.norm_w != nullptr ? 1 : (g.rownorm ? 2 : 0);
+  if (norm == 1) return false;
+  GemmParams p{};
+  p.x = g.x; p.lda = g.lda; p.M = g.M; p.row_idx = g.row_idx;
+  p.wp = reinterpret_cast<const uint4*>(g.wp); p.N = g.N; p.K = g.K;
+  p.norm_w = nullptr; p.eps = g.eps;
+  p.bias = g.bias; p.res = g.res; p.ldr = g.ldr;
+  p.out = g.out; p.ldo = g.ldo;
+  p.splitk = 1;
+  p.slabs = g.slabs;
+  p.positions = g.positions; p.slots = g.slots; p.cos_sin = g.cos_sin;
+  p.k_cache = g.k_cache; p.v_cache = g.v_cache; p.hq = g.hq; p.hkv = g.hkv; p.bs = g.bs;
+  p.dbg_ts = g.dbg_ts;
+  const int fb = g.ntb;      // reused as the forced tile width (0 = heuristic, 64 / 128)
+  const int fs = g.splitk;   // forced K slices (0 = heuristic)
+#define VG_PF(E)                                                                                         \
+  return norm == 2 ? launch_prefill_epi<E, 2>(p, fb, fs, g.slab_bytes, st)                               \
+                   : launch_prefill_epi<E, 0>(p, fb, fs, g.slab_bytes, st)
+  switch (g.epi) {
+    case EPI_SILU: VG_PF(EPI_SILU);
+    case EPI_QKV: VG_PF(EPI_QKV);
+    case EPI_F32: VG_PF(EPI_F32);
+    default: VG_PF(EPI_BF16);
+  }
+#undef VG_PF
+}
+
+}  // namespace vgate

@@ -27,6 +27,8 @@ struct GemmArgs {
   int waves;          // 0 = heuristic
   int splitk;         // 0 = heuristic
   int ntb;            // 16-column tiles per block for plain / f32 epilogues (0 = heuristic; 1, 2, 4)
+  int path;           // M > 16 dense: 0 auto (prefill kernel at M >= 128), 1 force prefill kernel,
+                      // -1 never (tile / decode kernels)
   float* slabs;       // split-K fp32 partial slabs (workspace) or null
   size_t slab_bytes;
   uint32_t* counters; // split-K arrival tickets, zero-initialised, self-resetting
@@ -48,6 +50,9 @@ struct GemmArgs {
   unsigned long long* dbg_ts;
 };
 void launch_gemm(const GemmArgs& g, hipStream_t st);
+// LDS-tiled prefill GEMM (gemm_prefill.hip) for long steps; returns false for a shape / mode it
+// does not take (caller falls back). g.ntb: forced tile width (0 heuristic, 64, 128).
+bool launch_gemm_prefill(const GemmArgs& g, hipStream_t st);
 
 // ---- custom one-shot all-reduce over xGMI peer memory (allreduce.hip) ----
 // bases[p]: rank p's IPC-mapped allocation = [AR_SIGNAL_BYTES signal area][2 x max_bytes data];
@@ -146,6 +151,7 @@ struct SampleArgs {
 };
 void launch_sample(const SampleArgs& s, hipStream_t st);
 int sample_segments(int B, int V);
+void set_sample_nseg(int n);  // cap on segments per row (0 = B*NSEG <= 1024 bound only)
 
 // Custom one-shot all-reduce over IPC-mapped peer buffers (xGMI).
 struct AllReduceArgs {

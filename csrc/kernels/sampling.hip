@@ -56,7 +56,7 @@ __device__ __forceinline__ void philox4(uint64_t seed, uint64_t offset, uint32_t
 }
 
 constexpr int SAMPLE_THREADS = 256;
-constexpr int SAMPLE_MAX_BLOCKS = 1024;  // B * NSEG bound: 4 blocks of 256 threads per CU, all co-resident
+constexpr int SAMPLE_MAX_BLOCKS = 256;  // B * NSEG bound: one block per CU, all co-resident
 constexpr float LOG2E_S = 1.4426950408889634f;
 
 // Per-(row, segment) partial, 8 words.
@@ -121,11 +121,14 @@ __device__ __forceinline__ void block_reduce_acc(Acc& a, float c, Acc* red) {
 
 // Per-row meeting point of the NSEG blocks after pass `gen` (1-based).
 // Returns false if the wait gave up (caller falls back to the argmax).
-// The poll is an atomic read-modify-write (fetch_add 0): it is performed at the device
-// coherence point, so it can never spin on a copy of the counter line that an earlier poll
-// left in this XCD's L2 (plain or sc1 polls of a counter that OTHER XCDs bump by atomics were
-// seen to stall a row for tens to hundreds of ms: profiles/r2_sampler_stall.txt). One agent
-// acquire after the match, then the row's partials are read.
+// Arrive with one agent-scope atomic add; poll the counter with relaxed sc1 loads (s_sleep
+// between polls: a read-modify-write poll from every block of a row queues behind the
+// arrivals at the memory-side atomic unit and was 4x slower at 1024 blocks); every partial is
+// stored and loaded sc1, so no cache-wide acquire is needed. The partials live in two
+// buffers by pass parity (see parts_even / parts_odd): without that, a fast block's NEXT-pass
+// partial could overwrite one a slow block was still merging, the blocks of a row then took
+// different accept / reject decisions and the ones left waiting spun to the give-up bound
+// (the 60-470 ms sampler launches of profiles/r2_bench1_kernels.txt).
 __device__ __forceinline__ bool row_meet(uint32_t* ctr, uint32_t target, int* ok_flag) {
   drain_stores();  // this block's sc1 partial stores are device-visible before it arrives
   __syncthreads();
@@ -134,12 +137,10 @@ __device__ __forceinline__ bool row_meet(uint32_t* ctr, uint32_t target, int* ok
     int ok = 1;
     uint32_t spins = 0;
     while (v < target) {
-      __builtin_amdgcn_s_sleep(2);
-      v = __hip_atomic_fetch_add(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (++spins > (1u << 20)) { ok = 0; break; }  // bounded: never hang the GPU
+      __builtin_amdgcn_s_sleep(1);
+      v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (++spins > (1u << 22)) { ok = 0; break; }  // bounded: never hang the GPU
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     *ok_flag = ok;
   }
   __syncthreads();
@@ -168,7 +169,11 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
   const float topp = a.top_p ? a.top_p[row] : 1.f;
   const bool use_k = topk > 0 && topk < a.V;
   const bool use_p = topp < 1.f;
-  SamplePart* parts = reinterpret_cast<SamplePart*>(a.parts) + (size_t)row * nseg;
+  // two partial buffers by pass parity: a block that has passed meet g may already publish
+  // pass g+1 while a slower block of its row is still reading pass g's partials; it cannot
+  // reach pass g+2 before every block has arrived at meet g+1, i.e. finished reading g
+  SamplePart* parts_even = reinterpret_cast<SamplePart*>(a.parts) + (size_t)row * nseg;
+  SamplePart* parts_odd = parts_even + (size_t)SAMPLE_MAX_BLOCKS;
   uint32_t* ctr = a.sync ? a.sync + row : nullptr;
 
   // One sweep of this block's segment (8 float4 loads in flight per thread).
@@ -222,6 +227,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
     bool ok = true;
     if (nseg > 1) {
       if (tid == 0) {  // device-coherent (sc1) stores: read by the row's other blocks in-launch
+        SamplePart* parts = (gen & 1) ? parts_odd : parts_even;
         float* w = reinterpret_cast<float*>(parts + seg);
         st_sc1(w + 0, acc.mx); st_sc1(w + 1, acc.z); st_sc1(w + 2, __int_as_float(acc.amx));
         st_sc1(w + 3, acc.gk); st_sc1(w + 4, __int_as_float(acc.gi)); st_sc1(w + 5, acc.cnt);
@@ -231,6 +237,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
       if (ok) {  // all partials loaded at once (one per thread), then a fixed-shape tree
         Acc r = acc_init();
         if (tid < nseg) {
+          const SamplePart* parts = (gen & 1) ? parts_odd : parts_even;
           const float* w = reinterpret_cast<const float*>(parts + tid);
           r = Acc{ld_sc1(w + 0), ld_sc1(w + 1), __float_as_int(ld_sc1(w + 2)), ld_sc1(w + 3),
                   __float_as_int(ld_sc1(w + 4)), ld_sc1(w + 5), ld_sc1(w + 6)};
@@ -285,12 +292,16 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
   }
 }
 
+int g_sample_nseg = 64;  // segments per row cap (set_sample_nseg; measured: benchmarks/sampler_stress.py)
+void set_sample_nseg(int n) { g_sample_nseg = n; }
+
 int sample_segments(int B, int V) {
   const int V4 = V >> 2;
-  static const int force = [] {
+  static const int env_force = [] {
     const char* e = getenv("VGATE_SAMPLE_NSEG");  // experiments only (bounded below)
     return e ? atoi(e) : 0;
   }();
+  const int force = g_sample_nseg > 0 ? g_sample_nseg : env_force;
   int nseg = SAMPLE_MAX_BLOCKS / (B > 0 ? B : 1);
   if (force > 0 && force < nseg) nseg = force;
   if (nseg > SAMPLE_THREADS) nseg = SAMPLE_THREADS;  // the merge loads one partial per thread

@@ -60,5 +60,6 @@ class BlockAllocator {
 };
 
 void bind_runtime(pybind11::module_& m);
+void bind_step_ring(pybind11::module_& m);  // step_ring.cpp
 
 }  // namespace vgate

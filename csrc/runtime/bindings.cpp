@@ -54,7 +54,7 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
           const c10::optional<Tensor>& cos_sin, const c10::optional<Tensor>& k_cache,
           const c10::optional<Tensor>& v_cache, int64_t hq, int64_t hkv,
           const c10::optional<Tensor>& awq_scales, const c10::optional<Tensor>& awq_zeros, int64_t group,
-          bool rownorm, const c10::optional<Tensor>& dbg_ts, int64_t ntb) {
+          bool rownorm, const c10::optional<Tensor>& dbg_ts, int64_t ntb, int64_t path) {
   CHECK_DEV(x); CHECK_DEV(wp); CHECK_DEV(out);
   CHECK_DT(x, torch::kBFloat16);
   CHECK_LASTDIM(x); CHECK_LASTDIM(out);
@@ -99,7 +99,7 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
   g.ldr = g.res ? (int)res->stride(0) : 0;
   if (g.res) TORCH_CHECK(res->size(0) >= M && res->size(1) >= N, "gemm: residual shape");
   g.out = out.data_ptr(); g.ldo = (int)out.stride(0);
-  g.epi = (int)epi; g.waves = (int)waves; g.splitk = (int)splitk; g.ntb = (int)ntb;
+  g.epi = (int)epi; g.waves = (int)waves; g.splitk = (int)splitk; g.ntb = (int)ntb; g.path = (int)path;
   if (ws.has_value() && ws->defined()) {
     CHECK_DEV(*ws); CHECK_DT(*ws, torch::kInt32);
     TORCH_CHECK(ws->numel() > 65536 * 2, "gemm: workspace too small");
@@ -324,9 +324,9 @@ void sample(const Tensor& logits, const c10::optional<Tensor>& temperature,
   s.out = reinterpret_cast<int32_t*>(out.data_ptr());
   s.out_logprob = const_cast<float*>(static_cast<const float*>(fp(out_logprob, torch::kFloat32)));
   if (ws.has_value() && ws->defined()) {
-    // [0, 512): row counters (2 per row, B <= 256 in segmented mode); [512, 8704): partials
-    // (8 words per block, B * nseg <= 1024 blocks)
-    TORCH_CHECK(ws->scalar_type() == torch::kInt32 && ws->is_cuda() && ws->numel() >= 8704, "sample: ws must be int32[>=8704]");
+    // [0, 512): row counters (2 per row, B <= 256 in segmented mode); [512, ...): partials
+    // (8 words per block, B * nseg <= 256 blocks (1024 allowed), two buffers by pass parity)
+    TORCH_CHECK(ws->scalar_type() == torch::kInt32 && ws->is_cuda() && ws->numel() >= 16896, "sample: ws must be int32[>=16896]");
     if (vgate::sample_segments(s.B, s.V) > 1) {
       s.sync = reinterpret_cast<uint32_t*>(ws->data_ptr());
       s.parts = reinterpret_cast<float*>(ws->data_ptr()) + 512;
@@ -427,7 +427,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("slots") = py::none(), py::arg("cos_sin") = py::none(), py::arg("k_cache") = py::none(),
         py::arg("v_cache") = py::none(), py::arg("hq") = 0, py::arg("hkv") = 0,
         py::arg("awq_scales") = py::none(), py::arg("awq_zeros") = py::none(), py::arg("group") = 128,
-        py::arg("rownorm") = false, py::arg("dbg_ts") = py::none(), py::arg("ntb") = 0);
+        py::arg("rownorm") = false, py::arg("dbg_ts") = py::none(), py::arg("ntb") = 0, py::arg("path") = 0);
   m.def("attention", &attention, "unified paged attention: decode (partitions merged in-launch) + varlen prefill tiles",
         py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),
@@ -445,6 +445,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("sample", &sample, "temperature/top-k/top-p sampling (segmented Gumbel-max + exact rejection)",
         py::arg("logits"), py::arg("temperature"), py::arg("top_p"), py::arg("top_k"), py::arg("seeds"),
         py::arg("offsets"), py::arg("out"), py::arg("out_logprob") = py::none(), py::arg("ws") = py::none());
+  m.def("sample_segments", &vgate::sample_segments, "blocks per row the sampler uses for (B, V)");
+  m.def("set_sample_nseg", &vgate::set_sample_nseg, "cap the sampler's segments per row (experiments)");
   m.def("prefetch", &prefetch, "read a tensor once with the default cache policy (MALL warm-up)",
         py::arg("t"), py::arg("blocks") = 256);
   m.def("ar_alloc", &ar_alloc, "uncached device allocation for the custom all-reduce (zeroed)");
@@ -459,6 +461,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("timeline_stop", &vgate::tl_stop, "stop handing out timeline slots; returns the slots used");
   m.def("timeline_entries", &timeline_entries, "(kernel, offset, blocks) per launch since timeline_start");
   vgate::bind_runtime(m);
+  vgate::bind_step_ring(m);
   py::class_<vgate::ShardedLRU>(m, "ShardedLRU", "sharded LRU of bytes values (result cache backend 'native')")
       .def(py::init<int64_t, int64_t>(), py::arg("capacity"), py::arg("shards") = 16)
       .def("get", [](vgate::ShardedLRU& c, const std::string& k) -> py::object {

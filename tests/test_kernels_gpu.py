@@ -685,3 +685,58 @@ def test_awq_library_prefill_path(layout):
         assert _rel_err(y, ref.silu_mul_linear_ref(xn, wd[: N // 2], wd[N // 2:])) < 2e-2
     else:
         assert _rel_err(y, ref.linear_ref(xn, wd)) < 2e-2
+
+
+@pytest.mark.parametrize("M", [128, 200, 1024, 4096])
+@pytest.mark.parametrize("bn,sk", [(0, 0), (64, 0), (128, 0), (64, 3)])
+def test_prefill_lds_gemm_all_epilogues(M, bn, sk):
+    """The LDS-tiled MFMA prefill kernel (gemm_prefill.hip, path=1) on the decode kernels'
+    fragment-packed weights, against the fp32 references: plain + in-place residual,
+    folded-norm SiLU*mul, folded-norm QKV + bias + RoPE + paged KV write (rows past M masked,
+    M not a multiple of the 128-row tile), for both tile widths and the heuristic, and with
+    K split over blocks (partials + the deterministic reduce kernel; the heuristic splits the
+    small grids of M = 128 / 200 by itself)."""
+    torch.manual_seed(70 + M + bn)
+    H, D, BS, hq, hkv, I = 1536, 128, 16, 12, 2, 1024
+    x = (torch.randn(M, H, device=DEV) * 1.5).bfloat16()
+    nw = (torch.rand(H, device=DEV) + 0.5).bfloat16()
+    # plain + residual (o_proj / down class), K = 2 x H to cover a longer K loop
+    K2 = 2 * H
+    x2 = torch.randn(M, K2, device=DEV).bfloat16()
+    w = (torch.randn(H, K2, device=DEV) / math.sqrt(K2)).bfloat16()
+    res = torch.randn(M, H, device=DEV).bfloat16()
+    out = res.clone()
+    ops.native().gemm(x2, ops.Linear(w).wp, H, K2, out, 0, res=out, ws=ops.workspace(DEV), path=1, ntb=bn,
+                      splitk=sk)
+    assert _rel_err(out, ref.linear_ref(x2, w, None, res)) < 1e-2
+    # SiLU*mul with the folded RMSNorm (gate_up class)
+    wg = (torch.randn(I, H, device=DEV) / math.sqrt(H)).bfloat16()
+    wu = (torch.randn(I, H, device=DEV) / math.sqrt(H)).bfloat16()
+    gu = ops.Linear(torch.cat([wg, wu]), layout="silu")
+    assert gu.fold_norm(nw)
+    h = torch.empty(M, I, dtype=torch.bfloat16, device=DEV)
+    ops.native().gemm(x, gu.wp, 2 * I, H, h, 2, ws=ops.workspace(DEV), rownorm=True, eps=1e-6, path=1, ntb=bn,
+                      splitk=sk)
+    xn, _ = ref.rmsnorm_ref(x, nw, 1e-6)
+    assert _rel_err(h, ref.silu_mul_linear_ref(xn, wg, wu)) < 2e-2
+    # QKV + bias + RoPE + paged KV write with the folded norm
+    N = (hq + 2 * hkv) * D
+    wq = (torch.randn(N, H, device=DEV) / math.sqrt(H)).bfloat16()
+    b = (torch.randn(N, device=DEV) * 0.1).bfloat16()
+    pos = torch.randint(0, 4096, (M,), dtype=torch.int32, device=DEV)
+    nblk = (M + BS - 1) // BS + 8
+    slots = torch.randperm(nblk * BS, device=DEV)[:M].int()
+    slots[min(4, M - 1)] = -1
+    cs = ref.rope_cos_sin(4096, D, 1e6, device=DEV)
+    kc = torch.zeros(nblk, hkv, BS, D, device=DEV).bfloat16()
+    vc = torch.zeros_like(kc)
+    lq = ops.Linear(wq, bias=b, layout="qkv")
+    assert lq.fold_norm(nw)
+    q = torch.empty(M, hq * D, dtype=torch.bfloat16, device=DEV)
+    ops.native().gemm(x, lq.wp, N, H, q, 3, bias=b, ws=ops.workspace(DEV), rownorm=True, eps=1e-6, positions=pos,
+                      slots=slots, cos_sin=cs, k_cache=kc, v_cache=vc, hq=hq, hkv=hkv, path=1, ntb=bn, splitk=sk)
+    qkv = ref.linear_ref(xn, wq, b)
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    ref.rope_kv_ref(qkv, pos, slots, cs, kc2, vc2, hq, hkv, D)
+    assert _rel_err(q, qkv[:, : hq * D]) < 2e-2
+    assert _rel_err(kc, kc2) < 2e-2 and _rel_err(vc, vc2) < 2e-2

@@ -44,7 +44,7 @@ def _generate(eng):
     return done
 
 
-def _worker(rank, world, port, path, q, overlap_min=None):
+def _worker(rank, world, port, path, q, overlap_min=None, embed_ids=None):
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                           MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -56,6 +56,9 @@ def _worker(rank, world, port, path, q, overlap_min=None):
         assert eng.model.num_heads_local * world == eng.arch.num_heads
         if rank == 0:
             out = _generate(eng)
+            if embed_ids is not None:  # the followers run the same hidden-states forward
+                vec, n = eng.embed(prompt_ids=embed_ids)
+                out = {"gen": out, "embed": vec}
             eng.shutdown_followers()
             q.put(("ok", out))
         else:
@@ -90,6 +93,43 @@ def test_tp2_matches_tp1(tmp_path, overlap_min):
     assert tp_out == ref
 
 
+def _run_group(world, path, **kw):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, path, q), kwargs=kw) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=280) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    errs = [r[1] for r in results if r[0] == "err"]
+    assert not errs, errs[0]
+    return next(r[1] for r in results if r[1] is not None)
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("world", [4, 8])
+def test_tp4_tp8_match_tp1_with_kv_replication_vocab_padding_and_embed(tmp_path, world):
+    """TP 4 / 8 over gloo (one process per rank, the shared-memory step ring carrying every plan):
+    2 KV heads replicated over 4 / 8 ranks, a 500-token vocabulary padded to whole 16-row
+    shards per rank; greedy tokens == TP=1 and the embedding (hidden-states forward that the
+    followers join) == TP=1's."""
+    base = LLMEngine(EngineConfig(model="tiny-tp8", device="cpu", max_model_len=256, max_num_seqs=8,
+                                  max_num_batched_tokens=64, num_kv_blocks=128, warmup=False, seed=3))
+    path = str(tmp_path / "ckpt")
+    save_checkpoint(base.model, path)
+    ref_eng = LLMEngine(_cfg(path, 1))
+    ref = _generate(ref_eng)
+    eids = [7, 9, 11, 13, 200, 300, 499]
+    ref_vec, _ = ref_eng.embed(prompt_ids=eids)
+    out = _run_group(world, path, embed_ids=eids)
+    assert out["gen"] == ref
+    a, b = torch.tensor(out["embed"]), torch.tensor(ref_vec)
+    # the row-parallel partial sums are rounded to bf16 per rank before the all-reduce
+    assert torch.allclose(a, b, atol=3e-3) and torch.nn.functional.cosine_similarity(a, b, 0) > 0.999
+
+
 def test_tp_group_routes_small_allreduce_to_custom_ar():
     """TPGroup.all_reduce: a tensor the custom all-reduce accepts goes to it (one-shot xGMI
     kernel, tests/test_custom_allreduce_gpu.py), anything else to torch.distributed."""
@@ -121,7 +161,7 @@ def _failing_worker(rank, world, port, path, q):
     if rank == 1:
         def boom(*a, **k):
             raise RuntimeError("injected follower fault")
-        eng._run_step = boom
+        eng.runner.follow_step = boom
         eng.follower_loop()  # exits the process with status 1
         q.put(("returned", None))
         return

@@ -41,7 +41,8 @@ def engine_config_from(model_config: ModelConfig):
         enforce_eager=model_config.enforce_eager, enable_prefix_caching=model_config.enable_prefix_caching,
         seed=model_config.seed, block_size=model_config.kv_block_size,
         part_size=model_config.attention_partition_size,
-        graph_token_buckets=model_config.hip_graph_token_buckets)
+        graph_token_buckets=model_config.hip_graph_token_buckets,
+        warmup_max_tokens=model_config.graph_warmup_max_tokens, warmup_max_seqs=model_config.graph_warmup_max_seqs)
 
 
 class NativeBackend:

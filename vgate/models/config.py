@@ -79,6 +79,10 @@ PRESETS: dict[str, ModelArch] = {
                       tie_embeddings=True, max_position=4096, bos_token_id=1, eos_token_ids=(2,)),
     "tiny-llama": ModelArch("tiny-llama", "llama", 256, 2, 4, 1, 128, 384, 1024, 1e-5, 5e5,
                             max_position=4096, bos_token_id=1, eos_token_ids=(2,)),
+    # TP tests up to 8 ranks: 8 query heads, 2 KV heads (replicated at TP 4 / 8), a vocabulary
+    # that is not a multiple of 16 * 8 (padded vocab shards)
+    "tiny-tp8": ModelArch("tiny-tp8", "qwen2", 256, 2, 8, 2, 128, 1024, 500, 1e-6, 1e4, qkv_bias=True,
+                          tie_embeddings=True, max_position=4096, bos_token_id=1, eos_token_ids=(2,)),
 }
 
 _ALIASES = [
@@ -91,6 +95,7 @@ _ALIASES = [
     ("llama-3-8b", "llama-3-8b"),
     ("meta-llama-3-8b", "llama-3-8b"),
     ("tiny-llama", "tiny-llama"),
+    ("tiny-tp8", "tiny-tp8"),
     ("tiny", "tiny"),
 ]
 

@@ -104,15 +104,17 @@ class DecoderModel:
                             if self.device.type == "cuda" and self.tp.size > 1 else None)
 
     def _keep_library_copies(self) -> bool:
-        """Plain weight copies for hipBLASLt prefill GEMMs (ops.linear, M >= 128).
-        VGATE_PREFILL_BLAS: 1 = on, 0 = off, auto (default) = on when the copies take at most
-        10% of the device's memory (Qwen2.5-1.5B 3.1 GB, Llama-3-8B 14 GB; not 70B on one GPU)."""
-        mode = os.environ.get("VGATE_PREFILL_BLAS", "auto")
-        if self.device.type != "cuda" or mode == "0":
+        """Plain weight copies for hipBLASLt prefill GEMMs (ops.linear, M >= 128) — a comparison
+        mode only for bf16 weights: by default their long steps run the hand-written LDS-tiled
+        MFMA kernel (csrc/kernels/gemm_prefill.hip) on the packed weights, no second copy kept.
+        VGATE_PREFILL_BLAS: "awq" (default) = copies for AWQ int4 layers only (their W4A16
+        kernels have no long-step path yet), "1" = every layer, "0" = none."""
+        mode = os.environ.get("VGATE_PREFILL_BLAS", "awq")
+        if self.device.type != "cuda" or mode == "0" or (mode == "awq" and self.quant != "awq"):
             return False
         lins = [lin for L in self.layers for lin in (L.qkv, L.o, L.gate_up, L.down)]
         extra = sum(lin.N * lin.K * 2 for lin in lins)
-        if mode != "1" and extra > 0.1 * torch.cuda.get_device_properties(self.device).total_memory:
+        if mode not in ("1", "awq") and extra > 0.1 * torch.cuda.get_device_properties(self.device).total_memory:
             return False
         return all([lin.keep_library_copy() for lin in lins])
 

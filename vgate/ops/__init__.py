@@ -259,7 +259,8 @@ def workspace(device) -> torch.Tensor:
 
 def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
            residual: torch.Tensor | None = None, out_f32: bool = False, waves: int = 0, splitk: int = 0,
-           norm: tuple | None = None, row_idx: torch.Tensor | None = None, qkv: dict | None = None) -> torch.Tensor:
+           norm: tuple | None = None, row_idx: torch.Tensor | None = None, qkv: dict | None = None,
+           path: int = 0) -> torch.Tensor:
     """out = epilogue(prologue(x) @ W^T).
 
     norm=(w, eps): fused RMSNorm of x rows (deferred row scale, see gemm.hip); row_idx: gather rows of x first;
@@ -298,7 +299,7 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
     ntb = 0
     if M <= 16 and waves == 0 and splitk == 0:
         waves, splitk, ntb = lin.dec_waves, lin.dec_splitk, lin.dec_ntb
-    kw = dict(bias=lin.bias, res=residual, ws=workspace(x.device), waves=waves, splitk=splitk, ntb=ntb)
+    kw = dict(bias=lin.bias, res=residual, ws=workspace(x.device), waves=waves, splitk=splitk, ntb=ntb, path=path)
     if norm is not None:
         if lin.norm_gamma is not None:  # gamma lives in the weights: row scale only
             kw.update(rownorm=True, eps=float(norm[1]))
@@ -489,7 +490,7 @@ def sample_workspace(device) -> torch.Tensor:
     key = str(device)
     ws = _SWS.get(key)
     if ws is None:
-        ws = torch.zeros(16384, dtype=torch.int32, device=device)
+        ws = torch.zeros(32768, dtype=torch.int32, device=device)
         _SWS[key] = ws
     return ws
 

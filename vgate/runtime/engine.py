@@ -7,9 +7,11 @@ No executor thread is held per request — this removes the reference's
 thread-pool ceiling by construction.
 
 Tensor parallelism: TP rank 0 runs the scheduler; followers run
-:meth:`LLMEngine.follower_loop`, receiving each step's metadata buffer by an
-RCCL broadcast (device to device) and replaying the same hipGraph bucket, so all
-ranks stay in lock-step without any Python object traffic on the hot path.
+:meth:`LLMEngine.follower_loop`, receiving each step's metadata through a host
+shared-memory ring (native ``StepRing``, csrc/runtime/step_ring.cpp) and replaying
+the same hipGraph bucket, so all ranks stay in lock-step with no collective, no
+device sync and no Python object traffic on the hot path; rank 0 schedules
+asynchronously (step t+1 queued before step t is post-processed) under TP too.
 """
 from __future__ import annotations
 
@@ -59,6 +61,11 @@ class EngineConfig:
     async_scheduling: bool = True  # GPU, TP=1: queue step t+1 before post-processing step t
     graph_token_buckets: list[int] | None = None
     warmup: bool = True
+    # start-up hipGraph capture: every token bucket <= warmup_max_tokens x every sequence bucket
+    # <= warmup_max_seqs (S <= T), so the mixed prefill+decode steps of a serving load replay
+    # graphs instead of running eagerly (eager steps were the p99 tail: profiles/r2_bench*.log)
+    warmup_max_tokens: int = 256
+    warmup_max_seqs: int = 16
     arch_overrides: dict | None = None
 
     def resolve_device(self) -> torch.device:
@@ -133,7 +140,14 @@ class LLMEngine:
         # collectives), so buckets are captured on first use there, not deferred to idle time
         self.runner.defer_capture = self.tp.size == 1
         self.capture_idle_s = 0.05
-        self.async_sched = bool(cfg.async_scheduling and self.device.type == "cuda" and self.tp.size == 1)
+        self.async_sched = bool(cfg.async_scheduling and self.device.type == "cuda")
+        self.ring = None
+        self._ring_closed = False
+        self._ar_check_every = 1 if self.tp.is_first else 64
+        self._steps_since_check = 0
+        self._ar_ms: list[float] = []
+        if self.tp.size > 1:
+            self._init_ring()
         self._inflight = None  # (batch, handle) of the launched, not yet post-processed step
         self._calls: collections.deque = collections.deque()  # (fn, future) run on the engine thread
         self.last_error: str | None = None
@@ -171,7 +185,9 @@ class LLMEngine:
         if self._running:
             return
         if self.cfg.warmup and self.runner.use_graphs:
-            secs = self.runner.warmup([1, 2, 4, 8, 16], [1, 2, 4, 8])
+            tb = [t for t in self.runner.t_buckets if t <= self.cfg.warmup_max_tokens]
+            sb = [b for b in self.runner.s_buckets if b <= self.cfg.warmup_max_seqs]
+            secs = self.runner.warmup(tb, sb)
             log.info("pre-captured %d hipGraphs in %.2fs", len(self.runner.graphs), secs)
         self._running = True
         self._thread = threading.Thread(target=self._loop, name="vgate-engine", daemon=True)
@@ -239,6 +255,8 @@ class LLMEngine:
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
         while self._running:
+            if self.ring is not None:
+                self.ring.heartbeat()
             if self.runner.pending_captures and self._idle():
                 # buckets first seen under load ran eagerly; capture them once the engine has
                 # stayed idle for a moment (not in the microseconds between two requests of a
@@ -272,8 +290,7 @@ class LLMEngine:
                 for seq in list(self.scheduler.running) + list(self.scheduler.waiting):
                     self.scheduler.remove(seq)
                     self._finish(seq, "error", notify_sched=False, error=self.last_error)
-        if self.tp.size > 1 and self.tp.is_first:
-            self._broadcast_header(-1, 0, 0)
+        self.shutdown_followers()
 
     # ------------------------------------------------------------- side calls
     def _run_calls(self) -> None:
@@ -349,10 +366,8 @@ class LLMEngine:
         if batch.empty:
             return 0
         t0 = time.perf_counter()
-        if self.tp.size > 1:
-            toks, samples = self._execute_tp(batch)
-        else:
-            toks, samples = self.runner.execute(batch)
+        toks, samples = self.runner.execute(batch)
+        self._check_collectives()
         for seq, n in batch.items:
             seq.num_computed += n
         self._process(batch, toks, samples, t0, tc, resolve=False)
@@ -391,6 +406,7 @@ class LLMEngine:
         batch, h, tc = entry
         with range_("vgate.collect"):
             toks = self.runner.collect(h)
+        self._check_collectives()
         with range_("vgate.process"):
             self._process(batch, toks, h.samples, h.t_launch, tc, resolve=True)
 
@@ -489,88 +505,88 @@ class LLMEngine:
             seq.callback("error" if error else "finish", seq, error)
 
     # ----------------------------------------------------------- tensor parallel
-    def _broadcast_header(self, T: int, S: int, ns: int) -> None:
-        import torch.distributed as dist
-        hdr = torch.tensor([T, S, ns], dtype=torch.int64,
-                           device=self.device if self.tp.backend == "nccl" else "cpu")
-        dist.broadcast(hdr, src=self._tp_src(), group=self.tp.group)
+    RING_PLAN, RING_EMBED, RING_CAPTURE, RING_STOP = 0, 1, 2, 3
 
-    def _tp_src(self) -> int:
-        import torch.distributed as dist
-        return dist.get_global_rank(self.tp.group, 0) if self.tp.group is not None else 0
+    def _init_ring(self) -> None:
+        """Create (rank 0) / attach (followers) the group's shared-memory step ring. Rank 0 picks
+        a unique name and hands it to the group once over the process group; from then on every
+        step plan travels through the ring (csrc/runtime/step_ring.cpp)."""
+        from vgate import ops
+        C = ops.native()
+        name = None
+        if self.tp.is_first:
+            name = f"/vgate_ring_{os.getpid()}_{id(self) & 0xffffff:x}"
+            self.ring = C.StepRing(name, True, slots=int(os.environ.get("VGATE_TP_RING_SLOTS", "8")),
+                                   slot_bytes=self.runner.meta.nbytes, followers=self.tp.size - 1)
+        name = self.tp.broadcast_object(name)
+        if not self.tp.is_first:
+            self.ring = C.StepRing(name, False)
+        self.tp.barrier()
+        self.runner.on_plan = self._publish if self.tp.is_first else None
 
-    def _execute_tp(self, batch):
-        """Rank-0 side: run the step locally after shipping its metadata to the followers."""
-        import torch.distributed as dist
-        r = self.runner
-        ns, nt = len(batch.items), batch.num_tokens
-        T = r._bucket(r.t_buckets, nt) if r.gpu else nt
-        S = r._bucket(r.s_buckets, ns) if r.gpu else ns
-        r.meta.select(0)
-        samples = r._fill(batch, T, S)
-        r.meta.upload(ns)
-        self._broadcast_header(T, S, ns)
-        n = r.meta.used_bytes(ns)
-        dist.broadcast(r.meta.dev[:n], src=self._tp_src(), group=self.tp.group)
-        toks = self._run_step(T, S, ns, nt)
-        return toks, samples
+    def _publish(self, T: int, S: int, ns: int, nt: int, mode: int) -> None:
+        """Rank 0: ship the step plan now in the runner's host metadata buffer to the followers."""
+        m = self.runner.meta
+        n = m.used_bytes(ns) if mode != self.RING_CAPTURE else m.used_bytes(0)
+        timeout = float(os.environ.get("VGATE_TP_TIMEOUT_S", "120"))
+        if not self.ring.publish(T, S, ns, nt, mode, m.host, n, timeout):
+            raise RuntimeError(f"TP step ring: a follower made no progress for {timeout:.0f}s")
 
-    def _run_step(self, T, S, ns, nt):
-        r = self.runner
-        if r.use_graphs:
-            g = r.graphs.get((T, S))
-            if g is None:
-                g = r._capture(T, S)
-                r.graphs[(T, S)] = g
-            g.replay()
-        else:
-            view = r.meta.view(T, S)
-            view.num_tokens, view.num_seqs = nt, ns
-            if r.gpu:
-                r._forward_sample(view)
-            else:
-                logits = self.model.forward(view, self.kv_caches, r.part_size)
-                r.out_tokens[:S] = logits.argmax(-1).int()  # CPU TP path is greedy-only (tests)
-        if r.gpu:
-            r.out_hosts[0][:ns].copy_(r.out_tokens[:ns], non_blocking=True)
-            r.dones[0].record()
-            r.dones[0].synchronize()
-            return r.out_hosts[0][:ns].tolist()
-        return r.out_tokens[:ns].tolist()
+    def _check_collectives(self) -> None:
+        """Fail the step (engine unhealthy) if the custom all-reduce gave up waiting for a peer
+        since the last check: its bounded spin reduces stale peer data after a timeout, so the
+        error word is the only signal (rank 0 every step, followers every 64 steps)."""
+        ar = self.tp.custom_ar
+        if ar is None:
+            return
+        self._steps_since_check += 1
+        if self._steps_since_check >= self._ar_check_every:
+            self._steps_since_check = 0
+            ar.check()
 
     def follower_loop(self) -> None:
-        """TP ranks > 0: execute whatever rank 0 schedules, until it broadcasts T < 0."""
-        import torch.distributed as dist
+        """TP ranks > 0: execute whatever rank 0 publishes on the step ring, until it stops."""
         torch.set_grad_enabled(False)
-        r = self.runner
         try:
-            self._follow(r, dist)
+            self._follow()
         except BaseException:  # noqa: BLE001 - a TP group is one failure domain
-            # rank 0 would otherwise wait in its next collective until the process-group
-            # timeout: exit now, so the launcher (torchrun) tears the whole group down and the
-            # gateway's health checks take this worker out of rotation
+            # rank 0 would otherwise wait for this rank (ring back-pressure / collectives) until
+            # its timeout: exit now, so the launcher (torchrun) tears the whole group down and
+            # the gateway's health checks take this worker out of rotation
             log.exception("TP follower rank %d failed; exiting so the TP group is torn down", self.tp.rank)
             logging.shutdown()
             os._exit(1)
 
-    def _follow(self, r, dist) -> None:
+    def _follow(self) -> None:
+        r = self.runner
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        f = self.tp.rank - 1
+        timeout = float(os.environ.get("VGATE_TP_TIMEOUT_S", "120"))
         while True:
-            hdr = torch.zeros(3, dtype=torch.int64, device=self.device if self.tp.backend == "nccl" else "cpu")
-            dist.broadcast(hdr, src=self._tp_src(), group=self.tp.group)
-            T, S, ns = (int(v) for v in hdr.tolist())
-            if T < 0:
+            buf = r.follower_host_buffer()
+            T, S, ns, nt, mode, _ = self.ring.wait(f, buf, timeout)
+            if mode == -2:
+                raise RuntimeError(f"TP step ring: no heartbeat from rank 0 for {timeout:.0f}s")
+            if mode in (-1, self.RING_STOP):
                 return
-            n = r.meta.used_bytes(ns)
-            buf = r.meta.dev[:n]
-            dist.broadcast(buf, src=self._tp_src(), group=self.tp.group)
-            if not r.gpu:
-                r.meta.host[:n].copy_(buf)
-            nt = int(r.meta.h["query_start"][ns]) if not r.gpu else 0
-            self._run_step(T, S, ns, nt)
+            r.follow_step(T, S, ns, nt, mode)
+            self.last_step_wall = time.monotonic()
+            if mode == self.RING_PLAN:
+                self.stats.steps += 1
+                self._check_collectives()
 
     def shutdown_followers(self) -> None:
-        if self.tp.size > 1 and self.tp.is_first:
-            self._broadcast_header(-1, 0, 0)
+        if self.tp.size > 1 and self.tp.is_first and self.ring is not None and not self._ring_closed:
+            self._ring_closed = True
+            try:
+                self.ring.publish(0, 0, 0, 0, self.RING_STOP, self.runner.meta.host, 0, 5.0)
+            finally:
+                self.ring.close()
+
+    def drain_allreduce_times(self) -> list[float]:
+        out, self._ar_ms = self._ar_ms, []
+        return out
 
     # ------------------------------------------------------------------- stats
     def drain_step_times(self) -> list[float]:

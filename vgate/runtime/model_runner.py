@@ -116,6 +116,9 @@ class ModelRunner:
         self.max_gpu_bucket = (0, 0)
         self.max_gpu_eager = False
         self.step_gpu_ms: list[float] = []  # device time per collected step, drained by the metrics loop
+        # TP rank 0: called with (T, S, ns, nt, mode) once a step's metadata is in the host buffer
+        # (before the step runs) -> the engine publishes it on the shared-memory step ring
+        self.on_plan = None
 
     # ----------------------------------------------------------------- buckets
     def _bucket(self, buckets, n):
@@ -253,6 +256,8 @@ class ModelRunner:
             self.meta_copied[k].synchronize()
         self.meta.select(k)
         samples = self._fill(batch, T, S, pending_slots)
+        if self.on_plan is not None:
+            self.on_plan(T, S, ns, nt, 0)
         self.started[k].record()
         self.meta.upload(ns)
         self.meta_copied[k].record()
@@ -308,6 +313,8 @@ class ModelRunner:
         else:
             self.meta.select(0)
         self._fill(batch, nt, ns)
+        if self.on_plan is not None:  # TP: the followers run the same hidden-states forward
+            self.on_plan(nt, ns, ns, nt, 1)
         self.meta.upload(ns)
         view = self.meta.view(nt, ns)
         view.num_tokens, view.num_seqs = nt, ns
@@ -319,6 +326,8 @@ class ModelRunner:
         ns, nt = len(batch.items), batch.num_tokens
         self.meta.select(0)
         samples = self._fill(batch, nt, ns)
+        if self.on_plan is not None:
+            self.on_plan(nt, ns, ns, nt, 0)
         self.meta.upload(ns)
         view = self.meta.view(nt, ns)
         view.num_tokens, view.num_seqs = nt, ns
@@ -344,9 +353,68 @@ class ModelRunner:
                 if S > T or (T, S) in self.graphs:
                     continue
                 self._fill_padding(T, S)
+                if self.on_plan is not None:  # TP: every rank captures the same bucket in step
+                    self.on_plan(T, S, 0, 0, 2)
                 self.meta.upload(0)
                 self.graphs[(T, S)] = self._capture(T, S)
         return time.perf_counter() - t0
+
+    # ------------------------------------------------------------ TP followers
+    def follower_host_buffer(self):
+        """The pinned host buffer the next ring entry is copied into (double-buffered like
+        launch(): buffer k may still feed the H2D copy of two steps back)."""
+        if not self.gpu:
+            self.meta.select(0)
+            return self.meta.host
+        k = self._k
+        if self._meta_pending[k]:
+            self.meta_copied[k].synchronize()
+        self.meta.select(k)
+        return self.meta.host
+
+    @torch.inference_mode()
+    def follow_step(self, T: int, S: int, ns: int, nt: int, mode: int):
+        """Run rank 0's step from the metadata just copied into follower_host_buffer():
+        mode 0 = a step (graph replay, captured on first sight exactly as rank 0 does), 1 = the
+        hidden-states forward of an embedding request, 2 = capture bucket (T, S) (start-up
+        warm-up). Returns nothing: followers never read their sampled tokens on the host (their
+        sampler output only resolves the next step's pending ids on the device)."""
+        if not self.gpu:
+            view = self.meta.view(T, S)
+            view.num_tokens, view.num_seqs = nt, ns
+            view.prev_tokens = None
+            if mode == 1:
+                self.model.forward(view, self.kv, self.part_size, return_hidden=True)
+            elif mode == 0:
+                logits = self.model.forward(view, self.kv, self.part_size)
+                self.out_tokens[:S] = logits.argmax(-1).int()
+            return
+        k = self._k
+        if mode == 2:
+            self.meta.upload(0)
+            if (T, S) not in self.graphs:
+                self.graphs[(T, S)] = self._capture(T, S)
+            return
+        self._k ^= 1
+        self.meta.upload(ns)
+        self.meta_copied[k].record()
+        self._meta_pending[k] = True
+        view = self.meta.view(T, S)
+        view.num_tokens, view.num_seqs = nt, ns
+        if mode == 1:
+            view.prev_tokens = None
+            self.model.forward(view, self.kv, self.part_size, return_hidden=True)
+            return
+        g = self.graphs.get((T, S)) if self.use_graphs else None
+        if g is None and self.use_graphs:
+            saved = self.out_tokens.clone()
+            g = self.graphs[(T, S)] = self._capture(T, S)
+            self.out_tokens.copy_(saved)
+        if g is not None:
+            self.graph_hits += 1
+            g.replay()
+        else:
+            self._forward_sample(view)
 
     def capture_pending(self, max_graphs: int = 64) -> int:
         """Capture the buckets that ran eagerly since the last call (most frequent first).
