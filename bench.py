@@ -12,6 +12,8 @@ JSON). One "step" = ``--requests-per-step`` requests (40 = the reference run).
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+    ... bench.py --gpus N --tp T   # N/T replicas, each a T-way tensor-parallel engine (RCCL / xGMI):
+                                   # rank 0 of each TP group serves HTTP, the others follow its steps
 """
 from __future__ import annotations
 
@@ -81,7 +83,20 @@ async def run_load(port: int, n: int, concurrency: int, max_tokens: int, rank: i
     return lat, fails, tokens, wall
 
 
-async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=None):
+def engine_model_cfg(args, rank: int, local: int) -> dict:
+    import torch
+    return {"model_id": args.model, "quantization": args.quantization, "engine_type": "native",
+            "random_init": True, "max_model_len": 2048, "max_num_seqs": 256,
+            "max_num_batched_tokens": 2048, "num_kv_blocks": args.kv_blocks, "enforce_eager": args.eager,
+            # device_count() does not initialise HIP: with --engine-process the parent must
+            # not touch the GPU before it spawns the engine core
+            "device": f"cuda:{local}" if torch.cuda.device_count() > 0 else "cpu",
+            # every rank of a TP group uses the same seed (one replica); replicas differ
+            "seed": 1234 + rank // args.tp, "tensor_parallel_size": args.tp,
+            "engine_process": bool(args.engine_process) and args.tp == 1}
+
+
+async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=None, group=None):
     import torch
     import uvicorn
 
@@ -91,13 +106,7 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cfg = VGateConfig(
         role="gateway",
-        model={"model_id": args.model, "quantization": args.quantization, "engine_type": "native",
-               "random_init": True, "max_model_len": 2048, "max_num_seqs": 256,
-               "max_num_batched_tokens": 2048, "num_kv_blocks": args.kv_blocks, "enforce_eager": args.eager,
-               # device_count() does not initialise HIP: with --engine-process the parent must
-               # not touch the GPU before it spawns the engine core
-               "device": f"cuda:{local}" if torch.cuda.device_count() > 0 else "cpu", "seed": 1234 + rank,
-               "engine_process": bool(args.engine_process)},
+        model=engine_model_cfg(args, rank, local),
         batch={"max_batch_size": args.concurrency},
         cache={"enabled": True, "maxsize": 1000},
         logging={"level": "WARNING", "json_format": True},
@@ -126,7 +135,7 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
     def barrier():
         if dist_ok:
             import torch.distributed as dist
-            dist.barrier()
+            dist.barrier(group=group)
         # this rank's GPU explicitly: the bare call syncs the calling thread's current device,
         # which is cuda:0 unless this thread happened to construct the engine
         if not args.engine_process and torch.cuda.is_available():
@@ -183,6 +192,17 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
             "n": per_step * args.steps, "engine": snap}
 
 
+def run_follower(args, rank: int) -> None:
+    """A TP follower rank: the same engine config as its group's serving rank, then the step loop."""
+    from vgate.backends.native import engine_config_from
+    from vgate.config import ModelConfig
+    from vgate.runtime.engine import LLMEngine
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    eng = LLMEngine(engine_config_from(ModelConfig(**engine_model_cfg(args, rank, local))))
+    eng.follower_loop()
+
+
 def client_loop():
     """--client-proc: one JSON load command per stdin line -> one JSON result per stdout line."""
     for line in sys.stdin:
@@ -196,6 +216,7 @@ def client_loop():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree of each replica (divides the world)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--concurrency", type=int, default=8)
@@ -225,29 +246,46 @@ def main():
 
     # start the load-client process before anything here touches the GPU
     client = None
-    if args.client_process:
+    is_follower = args.tp > 1 and int(os.environ.get("RANK", "0")) % args.tp != 0
+    if args.client_process and not is_follower:
         client = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--client-proc"],
                                   stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world % args.tp:
+        raise SystemExit(f"--tp {args.tp} does not divide the world size {world}")
+    dp = world // args.tp
     dist_ok = False
+    leaders = None  # process group of the serving ranks (rank 0 of every TP group)
     if world > 1:
+        import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # single node: gloo over loopback, independent of whether the hostname resolves
         os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
-        dist.init_process_group("gloo")  # coordination only: replicas share no tensors
+        # DP replicas share no tensors (gloo coordinates them); TP groups run RCCL over xGMI
+        backend = "nccl" if args.tp > 1 and torch.cuda.device_count() > 0 else "gloo"
+        dist.init_process_group(backend)
+        if args.tp > 1:
+            leaders = dist.new_group(list(range(0, world, args.tp)), backend="gloo")
         dist_ok = True
-    try:
-        res = asyncio.run(serve_and_bench(args, rank, world, dist_ok, client))
-    finally:
-        if client is not None:
-            client.stdin.close()
-            client.wait(timeout=30)
+    if args.tp > 1 and rank % args.tp:
+        # TP follower: join its group's engine and execute rank 0's steps until it shuts down
+        run_follower(args, rank)
+        res = None
+    else:
+        try:
+            res = asyncio.run(serve_and_bench(args, rank, world, dist_ok, client, group=leaders))
+        finally:
+            if client is not None:
+                client.stdin.close()
+                client.wait(timeout=30)
     if dist_ok:
         import torch.distributed as dist
         allr = [None] * world
+        dist.barrier()
         dist.all_gather_object(allr, res)
+        allr = [r for r in allr if r is not None]
     else:
         allr = [res]
     if rank == 0:
@@ -265,8 +303,9 @@ def main():
             "config": {"model": model_name, "quantization": args.quantization or "none",
                        "security_rate_limiter": bool(args.security),
                        "load_client": "separate process" if args.client_process else "in-process",
-                       "engine_core": "separate process" if args.engine_process else "in-process", "global_batch": args.concurrency * world,
-                       "seq_len": args.max_tokens, "parallelism": f"dp{world}",
+                       "engine_core": "separate process" if args.engine_process else "in-process", "global_batch": args.concurrency * dp,
+                       "seq_len": args.max_tokens,
+                       "parallelism": f"dp{dp}" if args.tp == 1 else f"dp{dp}xtp{args.tp}",
                        "concurrency_per_gpu": args.concurrency, "max_tokens": args.max_tokens,
                        "requests_per_step_per_gpu": args.requests_per_step},
             "p50_s": round(pct(lat, 50), 4), "p99_s": round(pct(lat, 99), 4),

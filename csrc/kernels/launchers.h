@@ -59,6 +59,9 @@ bool launch_gemm_prefill(const GemmArgs& g, hipStream_t st);
 // bf16 in/out (may alias), nbytes % 16 == 0, nbytes <= max_bytes
 constexpr int64_t AR_SIGNAL_BYTES = 65536;
 void launch_custom_allreduce(const void* in, void* out, int64_t nbytes, char* const* bases, int rank, int world,
+                             int64_t max_bytes, hipStream_t st, int two_shot = 0);
+// all-gather over the same buffers: out = [rank 0's in | rank 1's in | ...] (nbytes each)
+void launch_custom_allgather(const void* in, void* out, int64_t nbytes, char* const* bases, int rank, int world,
                              int64_t max_bytes, hipStream_t st);
 
 // ---- launch timeline (profiling; csrc/runtime/timeline.cpp, benchmarks/timeline.py) ----

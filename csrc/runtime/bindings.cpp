@@ -392,14 +392,14 @@ void ar_close(int64_t ptr) { HIP_OK(hipIpcCloseMemHandle(reinterpret_cast<void*>
 // error word of the own signal area (a wait timed out); clears it
 int64_t ar_error(int64_t own_base) {
   uint32_t v = 0, z = 0;
-  const size_t off = 64 * 8 * 4 + 64 * 4;  // ArSignal::error
+  const size_t off = 64 * 8 * 4 + 64 * 4;  // ArSignal::error (allreduce.hip)
   HIP_OK(hipMemcpy(&v, reinterpret_cast<char*>(own_base) + off, 4, hipMemcpyDeviceToHost));
   if (v) HIP_OK(hipMemcpy(reinterpret_cast<char*>(own_base) + off, &z, 4, hipMemcpyHostToDevice));
   return v;
 }
 
 void custom_allreduce(const Tensor& inp, Tensor& out, const std::vector<int64_t>& bases, int64_t rank,
-                      int64_t max_bytes) {
+                      int64_t max_bytes, int64_t two_shot) {
   CHECK_DEV(inp); CHECK_DEV(out);
   CHECK_DT(inp, torch::kBFloat16); CHECK_DT(out, torch::kBFloat16);
   TORCH_CHECK(inp.is_contiguous() && out.is_contiguous() && inp.numel() == out.numel(), "custom_allreduce: contiguous, same size");
@@ -411,6 +411,23 @@ void custom_allreduce(const Tensor& inp, Tensor& out, const std::vector<int64_t>
   for (int i = 0; i < world; ++i) b[i] = reinterpret_cast<char*>(bases[i]);
   c10::DeviceGuard guard(inp.device());
   vgate::launch_custom_allreduce(inp.data_ptr(), out.data_ptr(), nbytes, b.data(), (int)rank, world, max_bytes,
+                                 cur_stream(), (int)two_shot);
+}
+
+void custom_allgather(const Tensor& inp, Tensor& out, const std::vector<int64_t>& bases, int64_t rank,
+                      int64_t max_bytes) {
+  CHECK_DEV(inp); CHECK_DEV(out);
+  TORCH_CHECK(inp.is_contiguous() && out.is_contiguous() && inp.scalar_type() == out.scalar_type(),
+              "custom_allgather: contiguous, same dtype");
+  const int world = (int)bases.size();
+  const int64_t nbytes = inp.numel() * inp.element_size();
+  TORCH_CHECK(world >= 1 && world <= 8 && rank >= 0 && rank < world, "custom_allgather: world 1..8");
+  TORCH_CHECK(nbytes % 16 == 0 && nbytes <= max_bytes, "custom_allgather: bytes ", nbytes, " (need %16, <= ", max_bytes, ")");
+  TORCH_CHECK(out.numel() == inp.numel() * world, "custom_allgather: out must hold world x input");
+  std::vector<char*> b(world);
+  for (int i = 0; i < world; ++i) b[i] = reinterpret_cast<char*>(bases[i]);
+  c10::DeviceGuard guard(inp.device());
+  vgate::launch_custom_allgather(inp.data_ptr(), out.data_ptr(), nbytes, b.data(), (int)rank, world, max_bytes,
                                  cur_stream());
 }
 
@@ -456,6 +473,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("ar_close", &ar_close);
   m.def("ar_error", &ar_error, "read-and-clear the wait-timeout word of the own signal area");
   m.def("custom_allreduce", &custom_allreduce, "one-shot bf16 all-reduce over IPC-mapped peer buffers",
+        py::arg("inp"), py::arg("out"), py::arg("bases"), py::arg("rank"), py::arg("max_bytes"),
+        py::arg("two_shot") = 0);
+  m.def("custom_allgather", &custom_allgather, "all-gather over IPC-mapped peer buffers (rank-major output)",
         py::arg("inp"), py::arg("out"), py::arg("bases"), py::arg("rank"), py::arg("max_bytes"));
   m.def("timeline_start", &timeline_start, "start a launch timeline in an int64 device buffer (zero it first)");
   m.def("timeline_stop", &vgate::tl_stop, "stop handing out timeline slots; returns the slots used");

@@ -188,6 +188,14 @@ class StepRing {
   }
 
   void heartbeat() { hdr_->heartbeat_ns.v.store(now_ns(), std::memory_order_relaxed); }
+  // drop the segment's name once every follower has mapped it: the mappings stay valid and no
+  // /dev/shm entry outlives the group, however its processes end
+  void unlink() {
+    if (owner_) {
+      shm_unlink(name_.c_str());
+      owner_ = false;
+    }
+  }
   void close_ring() { hdr_->closed.v.store(1, std::memory_order_release); }
   int64_t published() const { return (int64_t)hdr_->seq.v.load(std::memory_order_acquire); }
   int64_t acked(int64_t f) const { return (int64_t)hdr_->ack[f].v.load(std::memory_order_acquire); }
@@ -234,6 +242,7 @@ void bind_step_ring(pybind11::module_& m) {
       .def("wait", &StepRing::wait, py::arg("follower"), py::arg("out"), py::arg("timeout_s") = 0.0)
       .def("heartbeat", &StepRing::heartbeat)
       .def("close", &StepRing::close_ring)
+      .def("unlink", &StepRing::unlink)
       .def("published", &StepRing::published)
       .def("acked", &StepRing::acked)
       .def_property_readonly("slots", &StepRing::slots)

@@ -17,7 +17,7 @@ REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step
 
 @pytest.mark.timeout(600)
 def test_bench_two_ranks_cpu(tmp_path):
-    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="2")
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="2", VGATE_DRY_RUN="false")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29541", str(ROOT / "bench.py"), "--gpus", "2",
            "--steps", "1", "--warmup", "1", "--model", "tiny", "--max-tokens", "4", "--requests-per-step", "4",
@@ -34,3 +34,22 @@ def test_bench_two_ranks_cpu(tmp_path):
     assert r["value"] > 0 and r["failures"] == 0
     # value = total requests over the slowest rank's wall time
     assert abs(r["value"] - 8 / (r["ms_per_step"] / 1e3)) / r["value"] < 0.02
+
+
+@pytest.mark.timeout(600)
+def test_bench_tensor_parallel_two_ranks_cpu(tmp_path):
+    """--tp 2: ONE replica whose TP follower rank executes the serving rank's steps (shared-memory
+    step ring, gloo collectives on CPU); the JSON line reports dp1xtp2 and the replica's load."""
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="2", VGATE_DRY_RUN="false")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29543", str(ROOT / "bench.py"), "--gpus", "2", "--tp", "2",
+           "--steps", "1", "--warmup", "1", "--model", "tiny-tp8", "--max-tokens", "4", "--requests-per-step", "4",
+           "--kv-blocks", "256", "--port", "18310"]
+    p = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=540)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert REQUIRED <= set(r)
+    assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp1xtp2" and r["config"]["global_batch"] == 8
+    assert r["value"] > 0 and r["failures"] == 0

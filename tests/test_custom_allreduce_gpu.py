@@ -30,7 +30,7 @@ def _expect(xs):
     return acc.bfloat16()
 
 
-def _worker(rank, port, q):
+def _worker(rank, port, q, WORLD=2, two_shot=0):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
         import torch.distributed as dist
@@ -47,9 +47,9 @@ def _worker(rank, port, q):
                 t = xs[rank].to(dev)
                 if rep == 1:
                     out = torch.empty_like(t)
-                    ar.all_reduce(t, out)
+                    ar.all_reduce(t, out, two_shot=two_shot)
                 else:
-                    out = ar.all_reduce(t)
+                    out = ar.all_reduce(t, two_shot=two_shot)
                 torch.cuda.synchronize()
                 ar.check()
                 assert torch.equal(out.cpu(), _expect(xs)), (rank, n, rep)
@@ -59,13 +59,13 @@ def _worker(rank, port, q):
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            ar.all_reduce(static.clone())  # warm-up outside capture
+            ar.all_reduce(static.clone(), two_shot=two_shot)  # warm-up outside capture
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         dist.barrier()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            res = ar.all_reduce(static)
+            res = ar.all_reduce(static, two_shot=two_shot)
         for rep in range(4):
             it += 1
             xs = _inputs(n, it, WORLD)
@@ -90,17 +90,20 @@ def _free_port():
 
 
 @pytest.mark.timeout(240)
-def test_custom_allreduce_two_processes_one_gpu():
+@pytest.mark.parametrize("world,two_shot", [(2, 0), (2, 1), (3, -1), (3, 1)])
+def test_custom_allreduce_processes_one_gpu(world, two_shot):
+    """One-shot (-1 / auto at 2 ranks) and two-shot (reduce-scatter + all-gather, 1) forms, 2 and
+    3 ranks sharing the GPU: bit-exact vs the fp32 rank-order sum, eager and graph-replayed."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, port, q, world, two_shot)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
-    for _ in range(WORLD):
+    for _ in range(world):
         r, msg = q.get(timeout=200)
         res[r] = msg
     for p in procs:
         p.join(timeout=60)
-    assert res == {0: "ok", 1: "ok"}, res
+    assert res == {r: "ok" for r in range(world)}, res

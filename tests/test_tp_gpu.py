@@ -22,6 +22,9 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 
 PROMPTS = {f"p{i}": [5 + (i * 37 + j * 11) % 400 for j in range(6 + 7 * i)] for i in range(4)}
+# >= 256 prompt tokens: the row-parallel GEMMs run in row chunks with each chunk's all-reduce on
+# the comm stream (fork / join through events) through the custom kernel
+PROMPTS["long"] = [3 + (j * 29) % 500 for j in range(300)]
 
 
 def _free_port() -> int:
@@ -30,12 +33,12 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _cfg(path, tp):
+def _cfg(path, tp, eager=False):
     from vgate.runtime.engine import EngineConfig
 
-    return EngineConfig(model=path, device="cuda:0", tensor_parallel_size=tp, max_model_len=256, max_num_seqs=8,
-                        max_num_batched_tokens=64, num_kv_blocks=128, warmup=False, seed=0,
-                        enforce_eager=tp > 1)
+    return EngineConfig(model=path, device="cuda:0", tensor_parallel_size=tp, max_model_len=512, max_num_seqs=8,
+                        max_num_batched_tokens=320, num_kv_blocks=256, warmup=False, seed=0,
+                        enforce_eager=eager)
 
 
 def _generate(eng):
@@ -54,7 +57,7 @@ def _generate(eng):
     return done
 
 
-def _worker(rank, world, port, path, q):
+def _worker(rank, world, port, path, q, eager=False):
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                           MASTER_PORT=str(port), VGATE_TP_TIMEOUT_S="60")
@@ -64,14 +67,16 @@ def _worker(rank, world, port, path, q):
 
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        eng = LLMEngine(_cfg(path, world))
+        eng = LLMEngine(_cfg(path, world, eager))
         assert eng.tp.size == world and eng.tp.rank == rank and eng.tp.backend == "gloo"
+        eng.runner.defer_capture = False
         assert eng.model.num_heads_local * world == eng.arch.num_heads
         if rank == 0:
             out = _generate(eng)
-            used_ar = eng.tp.custom_ar is not None
+            used_ar = eng.tp.custom_ar is not None and eng.tp.custom_ar.calls > 0
+            graphs = len(eng.runner.graphs)
             eng.shutdown_followers()
-            q.put(("ok", (out, used_ar)))
+            q.put(("ok", (out, used_ar, graphs)))
         else:
             eng.follower_loop()
             q.put(("ok", None))
@@ -80,7 +85,10 @@ def _worker(rank, world, port, path, q):
 
 
 @pytest.mark.timeout(300)
-def test_tp2_on_gpu_matches_tp1(tmp_path):
+@pytest.mark.parametrize("eager", [False, True])
+def test_tp2_on_gpu_matches_tp1(tmp_path, eager):
+    """graph == eager == TP=1: with every decode collective on the IPC kernels (all-reduce and the
+    logits all-gather) a gloo TP group replays captured hipGraphs for the buckets they cover."""
     from vgate.models.weights import save_checkpoint
     from vgate.runtime.engine import EngineConfig, LLMEngine
 
@@ -88,7 +96,7 @@ def test_tp2_on_gpu_matches_tp1(tmp_path):
                                  max_num_batched_tokens=64, num_kv_blocks=128, warmup=False, seed=0))
     path = str(tmp_path / "ckpt")
     save_checkpoint(src.model, path)
-    ref_eng = LLMEngine(_cfg(path, 1))
+    ref_eng = LLMEngine(_cfg(path, 1, True))
     ref = _generate(ref_eng)
     assert set(ref) == set(PROMPTS) and all(len(v) == 8 for v in ref.values())
     del ref_eng
@@ -97,7 +105,7 @@ def test_tp2_on_gpu_matches_tp1(tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, path, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, path, q, eager)) for r in range(2)]
     for p in procs:
         p.start()
     try:
@@ -109,6 +117,7 @@ def test_tp2_on_gpu_matches_tp1(tmp_path):
                 p.kill()
     errs = [r[1] for r in results if r[0] == "err"]
     assert not errs, errs[0]
-    tp_out, used_ar = next(r[1] for r in results if r[1] is not None)
-    assert used_ar, "the custom all-reduce was not set up between the two ranks"
+    tp_out, used_ar, graphs = next(r[1] for r in results if r[1] is not None)
+    assert used_ar, "the custom all-reduce was not used between the two ranks"
     assert tp_out == ref
+    assert (graphs > 0) == (not eager), graphs

@@ -5,10 +5,11 @@ only two collectives per transformer layer (after the row-parallel o_proj and
 down_proj) plus one all-reduce after the vocab-parallel embedding and one
 all-gather of the vocab-sharded logits — the Megatron layout of SURVEY.md §2.3.1.
 
-Small decode-sized all-reduces (<= ``VGATE_CUSTOM_AR_MAX_BYTES``, 4 MiB) go to the custom
-one-shot xGMI kernel (:mod:`vgate.parallel.custom_allreduce`) when it is
-available (all ranks on one node with peer access); larger ones, and every
-collective under the gloo backend (CPU tests), go through torch.distributed.
+All-reduces up to ``VGATE_CUSTOM_AR_MAX_BYTES`` (8 MiB) go to the custom xGMI kernels
+(:mod:`vgate.parallel.custom_allreduce`: one-shot to 512 KiB, two-shot above) and the
+logits all-gather to its IPC all-gather, when they are available (all ranks on one node
+with peer access); larger messages, and every collective of a CPU (gloo) group, go
+through torch.distributed.
 All collectives issue on the current stream, so they are hipGraph-capturable.
 """
 from __future__ import annotations
@@ -51,6 +52,9 @@ class TPGroup:
         if self.size == 1:
             return t
         t = t.contiguous()
+        if self.custom_ar is not None and self.custom_ar.should_gather(t):
+            out = self.custom_ar.all_gather(t)
+            return out.movedim(0, -2).reshape(*t.shape[:-1], self.size * t.shape[-1])
         out = torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         if self.backend == "gloo":
             parts = list(out.unbind(0))
@@ -58,6 +62,10 @@ class TPGroup:
         else:
             dist.all_gather_into_tensor(out, t, group=self.group)
         return out.movedim(0, -2).reshape(*t.shape[:-1], self.size * t.shape[-1])
+
+    def custom_bytes(self) -> int:
+        """Largest message the IPC collectives take (0 without them)."""
+        return self.custom_ar.max_bytes if self.custom_ar is not None else 0
 
     def broadcast_object(self, obj, src: int = 0):
         if self.size == 1:
@@ -72,6 +80,15 @@ class TPGroup:
 
 
 _TP: TPGroup | None = None
+
+
+def normalize_backend(name: str) -> str:
+    """A default group initialised without an explicit backend reports a compound string such as
+    'cpu:gloo,cuda:nccl': its GPU collectives run on RCCL, so treat it as 'nccl'."""
+    name = str(name)
+    if "nccl" in name:
+        return "nccl"
+    return "gloo" if "gloo" in name else name
 
 
 def init_tp(tp_size: int, backend: str | None = None) -> TPGroup:
@@ -91,7 +108,7 @@ def init_tp(tp_size: int, backend: str | None = None) -> TPGroup:
         # an already-initialised default group decides (e.g. gloo carrying GPU tensors when
         # several ranks share one GPU in tests); otherwise RCCL on GPUs, gloo on CPU
         if dist.is_initialized():
-            backend = dist.get_backend()
+            backend = normalize_backend(dist.get_backend())
         else:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
     if not dist.is_initialized():
@@ -112,14 +129,14 @@ def init_tp(tp_size: int, backend: str | None = None) -> TPGroup:
         g = dist.new_group(ranks, backend=backend) if world != tp_size else dist.group.WORLD
         if rank in ranks:
             grp = g
-    _TP = TPGroup(rank=rank % tp_size, size=tp_size, group=grp, backend=backend)
+    _TP = TPGroup(rank=rank % tp_size, size=tp_size, group=grp, backend=normalize_backend(backend))
     # the one-shot kernel maps peer buffers over IPC; the group only exchanges the handles
     if torch.cuda.is_available() and os.environ.get("VGATE_CUSTOM_AR", "1") != "0":
         from vgate.parallel.custom_allreduce import maybe_create
 
         dev = torch.device("cuda", torch.cuda.current_device())
         _TP.custom_ar = maybe_create(grp, _TP.rank, tp_size, dev,
-                                     max_bytes=int(os.environ.get("VGATE_CUSTOM_AR_MAX_BYTES", str(4 << 20))))
+                                     max_bytes=int(os.environ.get("VGATE_CUSTOM_AR_MAX_BYTES", str(8 << 20))))
     return _TP
 
 

@@ -1,4 +1,5 @@
-"""Custom one-shot all-reduce over xGMI peer memory for decode-sized TP collectives.
+"""Custom one-shot / two-shot all-reduce over xGMI peer memory for decode- and chunk-sized
+TP collectives.
 
 Each rank owns one uncached device allocation (``ar_alloc``: a signal area plus two
 ``max_bytes`` data buffers); the ranks exchange ``hipIpcMemHandle``s once over the
@@ -77,9 +78,22 @@ class CustomAllReduce:
         return (t.dtype == torch.bfloat16 and t.is_contiguous() and t.device == self.device and nbytes % 16 == 0
                 and 0 < nbytes <= self.max_bytes)
 
-    def all_reduce(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    def all_reduce(self, t: torch.Tensor, out: torch.Tensor | None = None, two_shot: int = 0) -> torch.Tensor:
+        """Sum over the group; one-shot up to 512 KiB, two-shot (reduce-scatter + all-gather over
+        the direct links) above; two_shot = 1 / -1 forces one form (tests)."""
         out = t if out is None else out
-        self.C.custom_allreduce(t, out, self.bases, self.rank, self.max_bytes)
+        self.C.custom_allreduce(t, out, self.bases, self.rank, self.max_bytes, two_shot)
+        self.calls += 1
+        return out
+
+    def should_gather(self, t: torch.Tensor) -> bool:
+        nbytes = t.numel() * t.element_size()
+        return t.is_contiguous() and t.device == self.device and nbytes % 16 == 0 and 0 < nbytes <= self.max_bytes
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """[...] per rank -> [world, ...] in rank order (IPC kernel, capturable)."""
+        out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        self.C.custom_allgather(t, out, self.bases, self.rank, self.max_bytes)
         self.calls += 1
         return out
 
@@ -103,11 +117,10 @@ def maybe_create(group, rank: int, world: int, device: torch.device, max_bytes: 
     access, else None (callers fall back to RCCL)."""
     if world < 2 or world > MAX_RANKS or device.type != "cuda":
         return None
-    ok = True
-    n = torch.cuda.device_count()
-    for d in range(n):
-        if d != device.index and not torch.cuda.can_device_access_peer(device.index, d):
-            ok = False
+    # peer access is needed only between the devices of THIS group's ranks
+    devs = [None] * world
+    dist.all_gather_object(devs, device.index, group=group)
+    ok = all(d == device.index or torch.cuda.can_device_access_peer(device.index, d) for d in devs)
     flags = [None] * world
     dist.all_gather_object(flags, ok, group=group)
     if not all(flags):

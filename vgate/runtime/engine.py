@@ -120,12 +120,18 @@ class LLMEngine:
         self.scheduler = Scheduler(self.kvm, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len)
         part = cfg.part_size or 512
         part = min(1024, max(32, (part + 31) // 32 * 32))
-        # a gloo group (ranks sharing one GPU in tests) runs its collectives on the host:
-        # they cannot be captured into a hipGraph
-        eager = cfg.enforce_eager or (self.tp.size > 1 and self.tp.backend != "nccl")
+        # a gloo group (ranks sharing one GPU in tests) runs its collectives on the host, which a
+        # hipGraph cannot capture: such a group replays graphs only for the buckets whose every
+        # collective fits the IPC kernels (custom all-reduce / all-gather), and runs the rest eagerly
+        gloo_tp = self.tp.size > 1 and self.tp.backend != "nccl"
+        eager = cfg.enforce_eager or (gloo_tp and self.tp.custom_ar is None)
         self.runner = ModelRunner(self.model, self.kv_caches, cfg.max_num_seqs, cfg.max_num_batched_tokens,
                                   cfg.max_model_len, cfg.block_size, eager, part,
                                   cfg.graph_token_buckets)
+        if gloo_tp and not eager:
+            cap = self.tp.custom_bytes()
+            H, vloc = self.arch.hidden_size, self.model.shard.vocab
+            self.runner.graph_ok = lambda T, S: T * H * 2 <= cap and S * vloc * 4 <= cap
         self.tokenizer = load_tokenizer(weights, cfg.tokenizer, self.arch)
         self.stats = EngineStats()
         self._inbox: collections.deque = collections.deque()
@@ -521,7 +527,9 @@ class LLMEngine:
         name = self.tp.broadcast_object(name)
         if not self.tp.is_first:
             self.ring = C.StepRing(name, False)
-        self.tp.barrier()
+        self.tp.barrier()  # every follower has mapped the segment
+        if self.tp.is_first:
+            self.ring.unlink()
         self.runner.on_plan = self._publish if self.tp.is_first else None
 
     def _publish(self, T: int, S: int, ns: int, nt: int, mode: int) -> None:

@@ -83,6 +83,7 @@ class ModelRunner:
         self.max_seqs = max_num_seqs
         self.meta = StepMeta(self.max_tokens, self.max_seqs, self.max_blocks, self.device)
         self.use_graphs = self.gpu and not enforce_eager
+        self.graph_ok = lambda T, S: True  # per-bucket veto (TP groups without capturable collectives)
         self.graphs: dict[tuple[int, int], tuple] = {}
         self.pool = None
         self.out_tokens = torch.zeros(self.max_seqs, dtype=torch.int32, device=self.device)
@@ -262,8 +263,9 @@ class ModelRunner:
         self.meta.upload(ns)
         self.meta_copied[k].record()
         self._meta_pending[k] = True
-        g = self.graphs.get((T, S)) if self.use_graphs else None
-        if g is None and self.use_graphs and not self.defer_capture:
+        graphs = self.use_graphs and self.graph_ok(T, S)
+        g = self.graphs.get((T, S)) if graphs else None
+        if g is None and graphs and not self.defer_capture:
             # the capture's eager warm-up samples into out_tokens, which this step may
             # still have to read (ids < 0): keep the previous step's samples aside
             saved = self.out_tokens.clone()
@@ -274,7 +276,7 @@ class ModelRunner:
             self.graph_hits += 1
             g.replay()
         else:
-            if self.use_graphs and not self.defer_capture_failed:
+            if graphs and not self.defer_capture_failed:
                 # first sight of this bucket under load: run it eagerly (a few ms of launch
                 # overhead) and capture it when the engine is next idle (capture_pending) —
                 # a capture (eager warm-up + record, ~0.1-0.5 s) would stall every in-flight
@@ -350,7 +352,7 @@ class ModelRunner:
         t0 = time.perf_counter()
         for T in token_buckets or []:
             for S in seq_buckets or [1]:
-                if S > T or (T, S) in self.graphs:
+                if S > T or (T, S) in self.graphs or not self.graph_ok(T, S):
                     continue
                 self._fill_padding(T, S)
                 if self.on_plan is not None:  # TP: every rank captures the same bucket in step
@@ -405,8 +407,9 @@ class ModelRunner:
             view.prev_tokens = None
             self.model.forward(view, self.kv, self.part_size, return_hidden=True)
             return
-        g = self.graphs.get((T, S)) if self.use_graphs else None
-        if g is None and self.use_graphs:
+        graphs = self.use_graphs and self.graph_ok(T, S)
+        g = self.graphs.get((T, S)) if graphs else None
+        if g is None and graphs:
             saved = self.out_tokens.clone()
             g = self.graphs[(T, S)] = self._capture(T, S)
             self.out_tokens.copy_(saved)
