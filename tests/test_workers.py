@@ -170,6 +170,45 @@ async def test_gateway_to_real_worker_app_unary_and_stream():
         await be.aclose()
 
 
+def _free_port() -> int:
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+async def test_remote_backend_aiohttp_path_over_real_sockets():
+    """The serving path (no injected transport): aiohttp pool against a real uvicorn worker —
+    unary, SSE stream, a refused endpoint skipped (connect failure is the one retried case) and
+    a non-200 surfaced without retry."""
+    import time as _time
+
+    import uvicorn
+    wapp = _worker_app()
+    port, dead = _free_port(), _free_port()
+    srv = uvicorn.Server(uvicorn.Config(wapp, host="127.0.0.1", port=port, log_level="error"))
+    th = threading.Thread(target=srv.run, daemon=True)
+    th.start()
+    t0 = _time.time()
+    while not srv.started and _time.time() - t0 < 20:
+        await asyncio.sleep(0.05)
+    try:
+        live, refused = f"http://127.0.0.1:{port}", f"http://127.0.0.1:{dead}"
+        be = RemoteBackend(WorkerConfig(endpoints=[refused, live], routing="round_robin"))
+        rs = await asyncio.gather(*(be.agenerate(f"p{i}", {"max_tokens": 4}) for i in range(16)))
+        assert all(r["text"] == f"[dry-run] echo: p{i}" for i, r in enumerate(rs))
+        pieces = [c async for c in be.stream_generate("one two three", {"max_tokens": 8})]
+        assert "".join(c["delta"] for c in pieces) == "[dry-run] echo: one two three"
+        assert be.registry.healthy_endpoints() == [live]  # refused one demoted by the retries
+        bad = RemoteBackend(WorkerConfig(endpoints=[live + "/nope"]))
+        with pytest.raises(RemoteInferenceError, match="404"):
+            await bad.agenerate("x", {"max_tokens": 1})
+        await be.aclose()
+        await bad.aclose()
+    finally:
+        srv.should_exit = True
+        th.join(timeout=10)
+
+
 async def test_full_gateway_over_worker_streaming_end_to_end():
     wapp = _worker_app()
     async with wapp.router.lifespan_context(wapp):

@@ -210,7 +210,7 @@ def create_app(config: Optional[VGateConfig] = None, engine: Optional[VGateEngin
     app.add_middleware(SecurityMiddleware, config=config.security)
     app.add_middleware(ObservabilityMiddleware)
 
-    def gateway_only() -> None:
+    async def gateway_only() -> None:  # async: a sync dependency costs a threadpool hop per request
         if is_worker:
             raise HTTPException(status_code=404, detail="Not available in worker role; call the gateway instead")
 

@@ -1,14 +1,20 @@
 """Gateway -> worker transport (HTTP/JSON, drop-in wire contract of ``/internal/generate``).
 
 Re-designed vs the reference (``remote_backend.py``):
-* **async**: one pooled ``httpx.AsyncClient``; a request awaits its worker call on
-  the event loop instead of pinning an executor thread — the measured
-  20-thread / ~180 req/s gateway ceiling disappears by construction;
+* **async**: a request awaits its worker call on the event loop instead of pinning an
+  executor thread — the reference's 20-thread / ~180 req/s gateway ceiling
+  (reference benchmarks/results/scaling.md:160-181) disappears by construction;
+* **aiohttp connection pool** on the serving path: httpx's pool re-scans every
+  connection for every queued request (``_assign_requests_to_connections``), which
+  under 64+ in-flight worker calls cost the gateway ~5 ms of CPU per request and
+  made throughput FALL as offered load rose (benchmarks/results/scaling.md,
+  "Saturation"); aiohttp's per-host keep-alive pool is O(1) per request. httpx is
+  used only when a test injects an ``httpx`` transport (ASGI/mock workers);
 * **streaming pass-through**: ``stream_generate`` proxies the worker's
   ``/internal/generate_stream`` SSE stream (the reference returned 501);
 * **trace propagation**: W3C ``traceparent`` header on every worker call.
 
-Retry policy is unchanged (the safe one): only ``ConnectError`` moves to another
+Retry policy is unchanged (the safe one): only a connect failure moves to another
 worker (nothing was delivered); timeouts / mid-request errors / non-200 /
 malformed results fail without retry so one client request never costs two
 generations; exhausting the pool raises :class:`NoHealthyWorkersError` (503).
@@ -18,9 +24,10 @@ a private loop).
 from __future__ import annotations
 
 import asyncio
+import contextlib
 import json
 import time
-from typing import Any, AsyncIterator, Dict, List, Optional
+from typing import Any, AsyncIterator, Dict, List, Optional, Tuple
 
 import httpx
 
@@ -35,7 +42,102 @@ tracer = get_tracer(__name__)
 
 
 class RemoteInferenceError(RuntimeError):
-    """A worker received the request but did not produce a usable result."""
+    """A worker was reached but the call failed (non-retryable: it may have run)."""
+
+
+class _ConnectFailed(Exception):
+    """Nothing reached the worker: safe to retry on another one."""
+
+
+class _RequestFailed(Exception):
+    """The request may have been delivered: never retried."""
+
+
+class _AiohttpTransport:
+    """Serving-path HTTP client: one aiohttp session (keep-alive pool) per event loop."""
+
+    def __init__(self, cfg: WorkerConfig, headers: dict):
+        import aiohttp
+        self._aiohttp = aiohttp
+        self._session = aiohttp.ClientSession(
+            connector=aiohttp.TCPConnector(limit=cfg.max_connections, limit_per_host=0, ttl_dns_cache=300),
+            timeout=aiohttp.ClientTimeout(total=cfg.timeout_seconds, connect=cfg.connect_timeout_seconds),
+            headers=headers)
+
+    async def post_json(self, url: str, body: dict, headers: dict) -> Tuple[int, bytes]:
+        a = self._aiohttp
+        try:
+            async with self._session.post(url, json=body, headers=headers) as r:
+                return r.status, await r.read()
+        except a.ClientConnectorError as e:
+            raise _ConnectFailed(type(e).__name__) from e
+        except (a.ClientError, asyncio.TimeoutError) as e:
+            raise _RequestFailed(type(e).__name__) from e
+
+    @contextlib.asynccontextmanager
+    async def stream_lines(self, url: str, body: dict, headers: dict):
+        a = self._aiohttp
+        try:
+            cm = self._session.post(url, json=body, headers=headers)
+            try:
+                r = await cm.__aenter__()
+            except a.ClientConnectorError as e:
+                raise _ConnectFailed(type(e).__name__) from e
+
+            async def lines():
+                try:
+                    async for raw in r.content:
+                        yield raw.decode("utf-8", "replace").rstrip("\r\n")
+                except (a.ClientError, asyncio.TimeoutError) as e:
+                    raise _RequestFailed(type(e).__name__) from e
+            try:
+                yield r.status, (await r.read() if r.status != 200 else b""), lines()
+            finally:
+                await cm.__aexit__(None, None, None)
+        except (_ConnectFailed, _RequestFailed, RemoteInferenceError):
+            raise
+        except (a.ClientError, asyncio.TimeoutError) as e:
+            raise _RequestFailed(type(e).__name__) from e
+
+    async def aclose(self) -> None:
+        await self._session.close()
+
+
+class _HttpxTransport:
+    """Test-path HTTP client over an injected httpx transport (ASGI app / mock handler)."""
+
+    def __init__(self, cfg: WorkerConfig, headers: dict, transport: httpx.AsyncBaseTransport):
+        self._c = httpx.AsyncClient(
+            transport=transport, headers=headers,
+            timeout=httpx.Timeout(cfg.timeout_seconds, connect=cfg.connect_timeout_seconds))
+
+    async def post_json(self, url: str, body: dict, headers: dict) -> Tuple[int, bytes]:
+        try:
+            r = await self._c.post(url, json=body, headers=headers)
+        except httpx.ConnectError as e:
+            raise _ConnectFailed(type(e).__name__) from e
+        except httpx.RequestError as e:
+            raise _RequestFailed(type(e).__name__) from e
+        return r.status_code, r.content
+
+    @contextlib.asynccontextmanager
+    async def stream_lines(self, url: str, body: dict, headers: dict):
+        try:
+            async with self._c.stream("POST", url, json=body, headers=headers) as r:
+                async def lines():
+                    try:
+                        async for ln in r.aiter_lines():
+                            yield ln
+                    except httpx.RequestError as e:
+                        raise _RequestFailed(type(e).__name__) from e
+                yield r.status_code, (await r.aread() if r.status_code != 200 else b""), lines()
+        except httpx.ConnectError as e:
+            raise _ConnectFailed(type(e).__name__) from e
+        except httpx.RequestError as e:
+            raise _RequestFailed(type(e).__name__) from e
+
+    async def aclose(self) -> None:
+        await self._c.aclose()
 
 
 class RemoteBackend:
@@ -60,17 +162,12 @@ class RemoteBackend:
             "timeout_seconds": worker_config.timeout_seconds, "authenticated": bool(worker_config.api_key),
             "routing": worker_config.routing}})
 
-    def _client(self) -> httpx.AsyncClient:
+    def _client(self):
         loop = asyncio.get_running_loop()
         c = self._clients.get(loop)
         if c is None:
-            limits = httpx.Limits(max_connections=self.config.max_connections,
-                                  max_keepalive_connections=self.config.max_connections)
-            kw = dict(timeout=httpx.Timeout(self.config.timeout_seconds, connect=self.config.connect_timeout_seconds),
-                      headers=self._headers, limits=limits)
-            if self._transport is not None:
-                kw["transport"] = self._transport
-            c = httpx.AsyncClient(**kw)
+            c = (_HttpxTransport(self.config, self._headers, self._transport) if self._transport is not None
+                 else _AiohttpTransport(self.config, self._headers))
             self._clients[loop] = c
         return c
 
@@ -99,30 +196,31 @@ class RemoteBackend:
                 t0 = time.perf_counter()
                 self.registry.begin(ep)
                 try:
-                    resp = await client.post(f"{ep}/internal/generate",
-                                             json={"prompts": prompts, "sampling_params": sampling_params},
-                                             headers=headers)
-                except httpx.ConnectError as e:
+                    status, raw = await client.post_json(f"{ep}/internal/generate",
+                                                         {"prompts": prompts, "sampling_params": sampling_params},
+                                                         headers)
+                except _ConnectFailed as e:
                     self.registry.record_failure(ep)
                     WORKER_REQUESTS.labels(worker=ep, outcome="connect_error").inc()
                     tried.add(ep)
                     last_connect = e
                     continue
-                except httpx.RequestError as e:
+                except _RequestFailed as e:
                     self.registry.record_failure(ep)
                     WORKER_REQUESTS.labels(worker=ep, outcome="request_error").inc()
                     span.set_attribute("error", True)
-                    raise RemoteInferenceError(f"worker at {ep} failed mid-request: {type(e).__name__}") from e
+                    raise RemoteInferenceError(f"worker at {ep} failed mid-request: {e}") from e
                 finally:
                     self.registry.end(ep)
                     WORKER_LATENCY.labels(worker=ep).observe(time.perf_counter() - t0)
-                if resp.status_code != 200:
+                if status != 200:
                     self.registry.record_failure(ep)
                     WORKER_REQUESTS.labels(worker=ep, outcome="http_error").inc()
                     span.set_attribute("error", True)
-                    raise RemoteInferenceError(f"worker at {ep} returned {resp.status_code}: {resp.text[:200]}")
+                    raise RemoteInferenceError(f"worker at {ep} returned {status}: "
+                                               f"{raw[:200].decode('utf-8', 'replace')}")
                 try:
-                    results = resp.json().get("results")
+                    results = json.loads(raw).get("results")
                 except (ValueError, AttributeError):
                     results = None
                 if not isinstance(results, list) or len(results) != len(prompts):
@@ -167,15 +265,14 @@ class RemoteBackend:
                 WORKER_RETRIES.labels(worker=ep).inc()
             self.registry.begin(ep)
             try:
-                async with client.stream("POST", f"{ep}/internal/generate_stream",
-                                         json={"prompt": prompt, "sampling_params": sampling_params},
-                                         headers=headers) as resp:
-                    if resp.status_code != 200:
+                async with client.stream_lines(f"{ep}/internal/generate_stream",
+                                               {"prompt": prompt, "sampling_params": sampling_params},
+                                               headers) as (status, err_body, lines):
+                    if status != 200:
                         self.registry.record_failure(ep)
                         WORKER_REQUESTS.labels(worker=ep, outcome="http_error").inc()
-                        body = (await resp.aread())[:200]
-                        raise RemoteInferenceError(f"worker at {ep} returned {resp.status_code}: {body!r}")
-                    async for line in resp.aiter_lines():
+                        raise RemoteInferenceError(f"worker at {ep} returned {status}: {err_body[:200]!r}")
+                    async for line in lines:
                         if not line.startswith("data:"):
                             continue
                         data = line[5:].strip()
@@ -188,15 +285,15 @@ class RemoteBackend:
                 self.registry.record_success(ep)
                 WORKER_REQUESTS.labels(worker=ep, outcome="success").inc()
                 return
-            except httpx.ConnectError:
+            except _ConnectFailed:
                 self.registry.record_failure(ep)
                 WORKER_REQUESTS.labels(worker=ep, outcome="connect_error").inc()
                 tried.add(ep)
                 continue
-            except httpx.RequestError as e:
+            except _RequestFailed as e:
                 self.registry.record_failure(ep)
                 WORKER_REQUESTS.labels(worker=ep, outcome="request_error").inc()
-                raise RemoteInferenceError(f"worker at {ep} failed mid-stream: {type(e).__name__}") from e
+                raise RemoteInferenceError(f"worker at {ep} failed mid-stream: {e}") from e
             finally:
                 self.registry.end(ep)
         raise NoHealthyWorkersError("no healthy worker available for streaming")
