@@ -104,7 +104,7 @@ def sweep(M=8, quick=False):
     return out
 
 
-def attention_bench(S=8, ctx=64, Hq=12, Hkv=2, D=128, part=2048, max_len=2048):
+def attention_bench(S=8, ctx=64, Hq=12, Hkv=2, D=128, part=2048, max_len=4096):
     """Decode attention (S sequences, 1 query token each) through the unified kernel."""
     bs, nblk = 16, 4096
     kc = torch.randn(nblk, Hkv, bs, D, device="cuda").bfloat16()
@@ -250,9 +250,12 @@ def main():
     if a.only == "gemm":
         sweep(a.M, a.quick)
         return
-    for ctx in (64, 512, 2048):
+    for ctx in (64, 256, 512, 1024, 2048, 4096):
         for part in (64, 128, 256, 512):
-            print(json.dumps(attention_bench(ctx=ctx, part=part)), flush=True)
+            r = attention_bench(ctx=ctx, part=part)
+            kv = 8 * 2 * ctx * 128 * 2 * 2  # S x Hkv x ctx x D x (K, V) x bf16
+            r["attention_decode"]["TBps"] = round(kv / r["attention_decode"]["us"] / 1e6, 2)
+            print(json.dumps(r), flush=True)
     if a.only == "attn":
         return
     print(json.dumps(sampler_bench()), flush=True)

@@ -28,9 +28,10 @@
 //                   (no prologue pass, no serial latency before the weight stream) and
 //                   applied per row in the epilogue (RMSNorm never runs as a kernel);
 //   row_idx       : rows gathered by index (LM head reads only sampled rows);
-//   epilogues     : +bias, +residual (in place), SiLU(gate)*up (tile pairs),
+//   epilogues     : +bias, +residual (in place), SiLU(gate)*up,
 //                   f32 logits, and QKV: bias + NeoX RoPE + paged KV-cache write
-//                   (tile pairs (j, j+4) of one head hold rotation partners d, d+64).
+//                   (one 16-column tile holds 8 rotation pairs / 8 gate-up pairs; the
+//                   partners sit on lanes l, l ^ 32, see gemm_epilogue.h).
 //
 // Orientation: D = Wfrag(A) x xfrag(B) -> lane holds D[n = 4(l>>4)+i][m = l&15]:
 // 4 consecutive output columns of one row -> 8-byte stores.
@@ -851,7 +852,10 @@ struct Plan { int waves, splitk; };
 // long K (down_proj: 96 tiles x 280 k-steps, 16 waves x 2 slices).
 static Plan plan(int nblk, int mchunks, int ksteps, int MB, int NTB, int force_w, int force_s) {
   const int blocks = nblk * mchunks;
-  int w = blocks >= 512 ? 4 : 8;
+  // >= 1024 one-tile blocks (gate_up at 1120 self-contained SiLU tiles): 2 waves, i.e. more
+  // resident blocks per CU (in-engine sweep: 1291.8 vs 1348.9 us per step at 4 waves,
+  // profiles/r2_decode_sweep_gate_up.log)
+  int w = blocks >= 1024 && NTB == 1 ? 2 : blocks >= 512 ? 4 : 8;
   int s = 1;
   if (blocks < 256 && ksteps >= 192) {
     w = 16;
@@ -937,8 +941,7 @@ static void launch_m(GemmParams p, const GemmArgs& g, hipStream_t st) {
     if (launch_awq_dec<NTB, EPI, NORM>(p, g, st)) return;
   }
   if constexpr (!AWQ) {
-    // M > 16: N-split tile kernel with a shared LDS copy of x (see gemm_tile_kernel);
-    // paired epilogues (silu / qkv) keep their tile pairs inside one wave (NTW = 2)
+    // M > 16: N-split tile kernel with a shared LDS copy of x (see gemm_tile_kernel)
     const int ntiles = g.N / 16;
     constexpr int NTW = NTB;
     const int tblocks = ntiles % (TG_WAVES * NTW) == 0
@@ -972,7 +975,10 @@ static void launch_dispatch(GemmParams p, const GemmArgs& g, hipStream_t st) {
     else launch_m<NTB_, EPI_, 0, AWQ>(p, g, st);                                \
   } while (0)
   switch (g.epi) {
-    case EPI_SILU: VG_NORM(2, EPI_SILU); break;
+    case EPI_SILU:  // self-contained 16-column tiles (8 gate + 8 up, see the epilogue)
+      if constexpr (AWQ) VG_NORM(2, EPI_SILU);
+      else VG_NORM(1, EPI_SILU);
+      break;
     case EPI_QKV: VG_NORM(1, EPI_QKV); break;
     case EPI_F32:
       if constexpr (!AWQ) {

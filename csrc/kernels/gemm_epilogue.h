@@ -122,18 +122,29 @@ __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 
 template <int NTB, int EPI, bool have>
 __device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[NTB], int m, int nt0, int nsub,
                                          const EpiPre<NTB> e, bool valid) {
-  if constexpr (EPI != EPI_QKV) {
+  if constexpr (EPI != EPI_QKV && EPI != EPI_SILU) {
     if (!valid) return;
   }
   if constexpr (EPI == EPI_SILU) {
-    const int n = (nt0 >> 1) * 16 + nsub;
-    float o[4];
+    // SiLU tile layout (ops.row_permutation "silu"): tile t holds gate columns 8t..8t+7 (lane
+    // groups 0, 1) and their up partners (groups 2, 3), so a pair sits on lanes l and l ^ 32 of
+    // ONE tile: every tile is self-contained and a decode block can own a single tile.
+    const bool gate = nsub < 8;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = silu(v[0][i]) * v[NTB - 1][i];
-    uint2 pk;
-    pk.x = pack_bf2(o[0], o[1]);
-    pk.y = pack_bf2(o[2], o[3]);
-    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + n) = pk;
+    for (int j = 0; j < NTB; ++j) {
+      float o[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float up = xor32(v[j][i]);  // all 64 lanes active
+        o[i] = silu(v[j][i]) * up;
+      }
+      if (valid && gate) {
+        uint2 pk;
+        pk.x = pack_bf2(o[0], o[1]);
+        pk.y = pack_bf2(o[2], o[3]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + (nt0 + j) * 8 + nsub) = pk;
+      }
+    }
   } else if constexpr (EPI == EPI_QKV) {
     static_assert(NTB == 1, "QKV tiles carry their rotation partners (see qkv_col)");
     const int head = nt0 >> 3;

@@ -220,7 +220,7 @@ static void launch_prefill_cfg(const GemmParams& p, int nz, hipStream_t st) {
 // kernel): K % 64, N % 64, a row gather, the gamma-in-registers RMSNorm mode.
 template <int EPI, int NORM>
 static bool launch_prefill_epi(const GemmParams& p, int force_bn, int force_sk, size_t slab_bytes, hipStream_t st) {
-  constexpr int NTB = EPI == EPI_SILU ? 2 : 1;
+  constexpr int NTB = 1;  // every epilogue works on self-contained 16-column tiles
   if (p.K % 64 != 0 || p.N % 64 != 0 || p.row_idx != nullptr) return false;
   const int mb = (p.M + 127) / 128;
   bool wide = p.N % 128 == 0 && mb * (p.N / 128) >= 240;

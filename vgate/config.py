@@ -107,7 +107,7 @@ class ModelConfig(_Section):
     watchdog_seconds: float = 60.0
     # hipGraphs captured at start-up: token buckets <= graph_warmup_max_tokens x sequence buckets
     # <= graph_warmup_max_seqs (others are captured the first time the engine is idle)
-    graph_warmup_max_tokens: int = 256
+    graph_warmup_max_tokens: int = 512
     graph_warmup_max_seqs: int = 16
 
     @field_validator("engine_type")

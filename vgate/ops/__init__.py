@@ -106,14 +106,17 @@ def pack_awq(qint: torch.Tensor) -> torch.Tensor:
 def row_permutation(N: int, layout: str) -> torch.Tensor | None:
     """Row order of the packed weight for a fused epilogue (None = identity).
 
-    silu: [G0 U0 G1 U1 ...] 16-row tiles (gate rows then up rows in the dense matrix);
+    silu: tile t = gate rows 8t..8t+7 then up rows 8t..8t+7 (rows [gate; up] in the dense
+          matrix), so one 16-row tile holds 8 SiLU pairs on lanes l, l^32 and a decode block
+          can own a single tile (gemm_epilogue.h);
     qkv : per 128-wide head, tile t (t = 0..7) = rows 8t..8t+7 then their NeoX rotation
           partners 64+8t..64+8t+7, so one 16-row tile holds both halves of 8 rotation pairs
           (the GEMM epilogue exchanges them across lanes l, l^32; csrc/kernels/gemm.hip qkv_col).
     """
     if layout == "silu":
         I = N // 2
-        t = torch.arange(2 * I).reshape(2, I // 16, 16).transpose(0, 1)
+        assert I % 8 == 0
+        t = torch.arange(2 * I).reshape(2, I // 8, 8).transpose(0, 1)
         return t.reshape(-1)
     if layout == "qkv":
         assert N % 128 == 0

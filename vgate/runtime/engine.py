@@ -64,7 +64,7 @@ class EngineConfig:
     # start-up hipGraph capture: every token bucket <= warmup_max_tokens x every sequence bucket
     # <= warmup_max_seqs (S <= T), so the mixed prefill+decode steps of a serving load replay
     # graphs instead of running eagerly (eager steps were the p99 tail: profiles/r2_bench*.log)
-    warmup_max_tokens: int = 256
+    warmup_max_tokens: int = 512
     warmup_max_seqs: int = 16
     arch_overrides: dict | None = None
 
