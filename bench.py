@@ -52,7 +52,7 @@ def pct(xs, p):
 async def run_load(port: int, n: int, concurrency: int, max_tokens: int, rank: int, start_idx: int,
                    model: str = "Qwen/Qwen2.5-1.5B-Instruct", api_key: str | None = None):
     import aiohttp
-    lat, fails, tokens = [], 0, 0
+    lat, starts, fails, tokens = [], [], 0, 0
     sem = asyncio.Semaphore(concurrency)
     url = f"http://127.0.0.1:{port}/v1/chat/completions"
     conn = aiohttp.TCPConnector(limit=concurrency * 2)
@@ -76,11 +76,12 @@ async def run_load(port: int, n: int, concurrency: int, max_tokens: int, rank: i
                 except Exception:  # noqa: BLE001
                     fails += 1
                 lat.append(time.perf_counter() - t0)
+                starts.append(t0 - t_run)
 
-        t0 = time.perf_counter()
+        t_run = t0 = time.perf_counter()
         await asyncio.gather(*(one(i) for i in range(n)))
         wall = time.perf_counter() - t0
-    return lat, fails, tokens, wall
+    return lat, fails, tokens, wall, starts
 
 
 def engine_model_cfg(args, rank: int, local: int) -> dict:
@@ -158,7 +159,7 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
         if not line:
             raise RuntimeError("load client exited")
         r = json.loads(line)
-        return r["lat"], r["fails"], r["tokens"], r["wall"]
+        return r["lat"], r["fails"], r["tokens"], r["wall"], r.get("starts", [])
 
     # warmup (also captures the hipGraph buckets this load uses)
     if args.warmup > 0:
@@ -176,8 +177,31 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
         inner.reset_peaks()
     snap0 = eng.backend.stats() if hasattr(eng.backend, "stats") else {}
     barrier()
+    # server event-loop lag during the timed region (a stalled loop delays every response)
+    lag = {"max_ms": 0.0, "at_s": 0.0}
+
+    async def lag_monitor(t_ref):
+        while True:
+            t = time.perf_counter()
+            await asyncio.sleep(0.005)
+            d = 1e3 * (time.perf_counter() - t - 0.005)
+            if d > lag["max_ms"]:
+                lag["max_ms"], lag["at_s"] = d, t - t_ref
+    import gc
+    gcs = {"max_ms": 0.0, "n2": 0, "t": 0.0}
+
+    def gc_cb(phase, info):
+        if phase == "start":
+            gcs["t"] = time.perf_counter()
+        elif info.get("generation") == 2 or time.perf_counter() - gcs["t"] > 0.005:
+            gcs["n2"] += info.get("generation") == 2
+            gcs["max_ms"] = max(gcs["max_ms"], 1e3 * (time.perf_counter() - gcs["t"]))
+    gc.callbacks.append(gc_cb)
     t0 = time.perf_counter()
-    lat, fails, tokens, _ = await load(per_step * args.steps, 0)
+    mon = asyncio.create_task(lag_monitor(t0))
+    lat, fails, tokens, _, starts = await load(per_step * args.steps, 0)
+    mon.cancel()
+    gc.callbacks.remove(gc_cb)
     barrier()
     wall = time.perf_counter() - t0
     snap = eng.backend.stats() if hasattr(eng.backend, "stats") else {}
@@ -188,7 +212,11 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
             snap[f"timed_{k}"] = snap[k] - snap0[k]
     server.should_exit = True
     await srv_task
+    slow = sorted(zip(lat, starts), reverse=True)[:8]
     return {"lat": lat, "fails": fails, "tokens": tokens, "wall": wall, "boot_s": boot_s,
+            "slowest": [[round(st, 3), round(la, 4)] for la, st in slow],
+            "loop_lag_max_ms": round(lag["max_ms"], 2), "loop_lag_at_s": round(lag["at_s"], 3),
+            "gc_gen2_collections": gcs["n2"], "gc_max_pause_ms": round(gcs["max_ms"], 2),
             "n": per_step * args.steps, "engine": snap}
 
 
@@ -207,9 +235,9 @@ def client_loop():
     """--client-proc: one JSON load command per stdin line -> one JSON result per stdout line."""
     for line in sys.stdin:
         c = json.loads(line)
-        lat, fails, tokens, wall = asyncio.run(run_load(c["port"], c["n"], c["concurrency"], c["max_tokens"],
+        lat, fails, tokens, wall, starts = asyncio.run(run_load(c["port"], c["n"], c["concurrency"], c["max_tokens"],
                                                         c["rank"], c["start_idx"], c["model"], c["api_key"]))
-        sys.stdout.write(json.dumps({"lat": lat, "fails": fails, "tokens": tokens, "wall": wall}) + "\n")
+        sys.stdout.write(json.dumps({"lat": lat, "fails": fails, "tokens": tokens, "wall": wall, "starts": starts}) + "\n")
         sys.stdout.flush()
 
 
@@ -324,6 +352,11 @@ def main():
             "max_gpu_step_bucket": allr[0]["engine"].get("max_gpu_step_bucket"),
             "max_cycle_ms": allr[0]["engine"].get("max_cycle_ms"),
             "max_cycle_tokens_seqs": allr[0]["engine"].get("max_cycle_tokens_seqs"),
+            # p99 forensics: the slowest requests as [start offset s, latency s] (rank 0) and
+            # the serving event loop's worst lag inside the timed region
+            "slowest_requests": allr[0].get("slowest"),
+            "loop_lag_max_ms": allr[0].get("loop_lag_max_ms"), "loop_lag_at_s": allr[0].get("loop_lag_at_s"),
+            "gc_gen2_collections": allr[0].get("gc_gen2_collections"), "gc_max_pause_ms": allr[0].get("gc_max_pause_ms"),
         }
         print(json.dumps(out), flush=True)
     if dist_ok:
