@@ -1,6 +1,7 @@
-"""Decode-attention phase timing on the MI355X: s_memtime stamps written by block (0,0,0)
-of the unified attention kernel (AttnArgs::dbg_ts) — entry, metadata loaded, chunk loop
-done, merge/store done — to see where a short-context decode launch spends its time.
+"""Decode-attention phase timing on the MI355X: 100 MHz s_memrealtime stamps written by wave 0
+of block (sequence 0, KV head 0, partition 0) of the unified attention kernel (AttnArgs::dbg_ts):
+entry (0) -> metadata loaded (1) -> first chunk's K/V landed (4) -> chunk loop done (2) ->
+waves' partials in LDS (5) -> merged output stored (3). Medians over 50 launches, in us.
 
     python benchmarks/attn_phases.py
 """
@@ -24,7 +25,7 @@ def main():
     S, Hq, Hkv, D, bs, nblk = 8, 12, 2, 128, 16, 4096
     kc = torch.randn(nblk, Hkv, bs, D, device="cuda").bfloat16()
     vc = torch.randn(nblk, Hkv, bs, D, device="cuda").bfloat16()
-    for ctx in (32, 64, 128, 256):
+    for ctx in (32, 64, 128, 256, 512):
         maxb = 2048 // bs
         bt = torch.randperm(nblk, device="cuda")[: S * maxb].view(S, maxb).int().contiguous()
         cl = torch.full((S,), ctx, dtype=torch.int32, device="cuda")
@@ -33,29 +34,24 @@ def main():
         out = torch.empty(S, Hq * D, device="cuda").bfloat16()
         ts = torch.full((S,), -1, dtype=torch.int32, device="cuda")
         tq = torch.zeros(S, dtype=torch.int32, device="cuda")
-        part = 256
+        part = 512
         P = 2048 // part
         po = torch.empty(S, Hq, P, D, device="cuda")
         pml = torch.empty(S, Hq, P, 2, device="cuda")
         dbg = torch.zeros(16, dtype=torch.int64, device="cuda")
         ph = []
-        for _ in range(30):
+        for _ in range(50):
             dbg.zero_()
             C.attention(q, Hq * D, kc, vc, bt, cl, qs, ts, tq, out, po, pml, Hq, Hkv, part, 1 / math.sqrt(D), 0,
                         ops.attn_tickets(q.device), dbg)
             torch.cuda.synchronize()
-            d = dbg.cpu().tolist()
-            ph.append(d)
-        # clock rate from the 100 MHz realtime stamps
-        rates = [(x[3] - x[0]) / max(1, (x[7] - x[6])) * 100.0 for x in ph if x[7] > x[6]]  # ticks per us
-        rate = statistics.median(rates) if rates else 2400.0
+            ph.append(dbg.cpu().tolist())
+
         def us(i, j):
-            return round(statistics.median((x[j] - x[i]) / rate for x in ph), 3)
-        rec = {"ctx": ctx, "ticks_per_us": round(rate, 1), "meta_us": us(0, 1), "loop_us": us(1, 2),
-               "merge_store_us": us(2, 3), "total_block_us": us(0, 3)}
-        if ctx > 32:  # chunk-1 sub-phases: loads landed -> QK -> softmax -> V to LDS -> PV
-            rec.update(qk_us=us(8, 9), softmax_us=us(9, 10), v_lds_us=us(10, 11), pv_us=us(11, 12))
-        print(json.dumps(rec), flush=True)
+            return round(statistics.median((x[j] - x[i]) / 100.0 for x in ph), 3)
+        print(json.dumps({"ctx": ctx, "meta_us": us(0, 1), "first_kv_us": us(1, 4), "loop_rest_us": us(4, 2),
+                          "partials_to_lds_us": us(2, 5), "merge_store_us": us(5, 3), "total_block_us": us(0, 3)}),
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -152,7 +152,7 @@ __host__ __device__ constexpr int attn_lds_bytes(int nw) {
 #define ATTN_STAMP(i)                                                                          \
   do {                                                                                         \
     if (a.dbg_ts != nullptr && threadIdx.x == 0 && s == 0 && h == 0 && part == 0)              \
-      a.dbg_ts[i] = __builtin_amdgcn_s_memtime();                                              \
+      a.dbg_ts[i] = __builtin_amdgcn_s_memrealtime();                                          \
   } while (0)
 
 __device__ __forceinline__ void load_k_regs(uint4 (&kf)[8], const bf16_t* kb0, const bf16_t* kb1, int lane) {
@@ -216,6 +216,10 @@ __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, in
   };
   auto consume = [&](const uint4 (&kf)[8], const uint4 (&vr)[8], int j) {
     const int tb = pstart + (wid + j * nw) * CHUNK;
+    if (j == 0 && a.dbg_ts != nullptr) {  // profiling: the first chunk's K / V have landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ATTN_STAMP(4);
+    }
     f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) s0 = mfma16(as_bf16x8(kf[kk]), as_bf16x8(qf[kk]), s0);
@@ -262,29 +266,52 @@ __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, in
     }
   }
   __syncthreads();
-  // one thread per (query column, 8 d): rescale and sum the waves' partials
+  ATTN_STAMP(5);
+  // one thread per (query column, 8 d): rescale and sum the waves' partials. Unrolled over the
+  // (<= 8) waves with every LDS read issued before the arithmetic: the loop with a per-wave
+  // `continue` serialised ~12 dependent LDS round trips (merge + store 1.1 us of a 4.6 us block
+  // at ctx 64, benchmarks/attn_phases.py). Fixed wave order: bit-reproducible.
   const int items = G * 16;
   float M = -INFINITY, L = 0.f;
   float acc[8];
   const int it = threadIdx.x;
   const int icol = it >> 4, d0 = (it & 15) * 8;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
   if (it < items) {
-    for (int w = 0; w < nw; ++w) M = fmaxf(M, mlp[(w * 16 + icol) * 2]);
+    float mw[16];
+#pragma unroll
+    for (int w = 0; w < 16; ++w) mw[w] = mlp[((w < nw ? w : 0) * 16 + icol) * 2];
+#pragma unroll
+    for (int w = 0; w < 16; ++w)
+      if (w < nw) M = fmaxf(M, mw[w]);
     const float Mref = M == -INFINITY ? 0.f : M;
+    for (int base = 0; base < nw; base += 8) {  // <= 2 passes (G <= 16)
+      float lw[8];
+      f32x4 v0[8], v1[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    for (int w = 0; w < nw; ++w) {
-      const float wl = mlp[(w * 16 + icol) * 2 + 1];
-      if (!(wl > 0.f)) continue;
-      const float e = __builtin_amdgcn_exp2f(mlp[(w * 16 + icol) * 2] - Mref);
-      L += wl * e;
-      const float* row = opart + w * (16 * D_) + icol * D_;
-      const f32x4 v0 = *reinterpret_cast<const f32x4*>(row + 4 * ((d0 >> 2) ^ icol));
-      const f32x4 v1 = *reinterpret_cast<const f32x4*>(row + 4 * (((d0 >> 2) + 1) ^ icol));
+      for (int i = 0; i < 8; ++i) {
+        const int ww = base + i < nw ? base + i : base;  // clamped: surplus slots weighted 0 below
+        lw[i] = mlp[(ww * 16 + icol) * 2 + 1];
+        const float* row = opart + ww * (16 * D_) + icol * D_;
+        v0[i] = *reinterpret_cast<const f32x4*>(row + 4 * ((d0 >> 2) ^ icol));
+        v1[i] = *reinterpret_cast<const f32x4*>(row + 4 * (((d0 >> 2) + 1) ^ icol));
+      }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc[j] += e * v0[j];
-        acc[4 + j] += e * v1[j];
+      for (int i = 0; i < 8; ++i) {
+        const int w = base + i;
+        // a wave without tokens has l = 0 and m = -inf: weight exactly 0 (no 0 * inf)
+        float mv = mw[0];
+#pragma unroll
+        for (int k = 1; k < 16; ++k)
+          if (k == w) mv = mw[k];
+        const float e = (w < nw && lw[i] > 0.f) ? __builtin_amdgcn_exp2f(mv - Mref) : 0.f;
+        L += lw[i] * e;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[j] += e * v0[i][j];
+          acc[4 + j] += e * v1[i][j];
+        }
       }
     }
   }

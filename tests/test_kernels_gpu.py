@@ -142,7 +142,7 @@ def _make_cache(num_blocks, Hkv, D=128, BS=16, seed=0):
     return kc, vc
 
 
-@pytest.mark.parametrize("Hq,Hkv", [(12, 2), (32, 8), (8, 1), (64, 8)])
+@pytest.mark.parametrize("Hq,Hkv", [(12, 2), (32, 8), (8, 1), (64, 8), (32, 2)])
 @pytest.mark.parametrize("ctxs", [[1, 7, 33, 100], [513, 2048, 1500, 64], [5]])
 def test_attention_decode(Hq, Hkv, ctxs):
     torch.manual_seed(6)
