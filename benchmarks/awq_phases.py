@@ -1,6 +1,6 @@
 """Phase stamps of the AWQ decode kernel (awq_dec_kernel, first and last block): x staged
-(1), activation row sums (2), weight stream + MFMAs done (3), split-K publish / epilogue
-(4), combine (5) — microseconds from the block's start, Qwen2.5-1.5B shapes at M = 8,
+(1), LDS barrier passed (2), weight stream + MFMAs done (3), epilogue done (4),
+split-K combine (5) — microseconds from the block's start, Qwen2.5-1.5B shapes at M = 8,
 weights cycled through > 400 MB so every launch streams from HBM.
 
     python benchmarks/awq_phases.py
@@ -36,7 +36,7 @@ def main():
         x = torch.randn(M, K, device=dev).bfloat16()
         epi = 2 if layout == "silu" else 0
         out = torch.empty(M, N // 2 if epi == 2 else N, device=dev, dtype=torch.bfloat16)
-        for sk in (0, 1, 2, 4, 8):
+        for sk in (0, 2):
             buf = torch.zeros(1 << 20, dtype=torch.int64, device=dev)
             reps = 12
             rows = []
@@ -44,7 +44,8 @@ def main():
                 L = lins[i % ncopy]
                 buf.zero_()
                 C.timeline_start(buf)
-                C.gemm(x, L.wp, N, K, out, epi, ws=ws, splitk=sk, awq_scales=L.scales, awq_zeros=L.zeros, group=g)
+                C.gemm(x, L.wp, N, K, out, epi, ws=ws, splitk=sk, awq_scales=L.scales, awq_zeros=L.zeros, group=g,
+                       awq_szp=L.szp)
                 C.timeline_stop()
                 torch.cuda.synchronize()
                 ents = C.timeline_entries()

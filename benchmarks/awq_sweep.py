@@ -16,6 +16,40 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import torch  # noqa: E402
 
 from benchmarks.mall_probe import timeline_graph  # noqa: E402
+
+
+def block_stats(C, fn):
+    """One launch in a graph with timeline slots: per-block duration / start percentiles (us)."""
+    buf = torch.zeros(1 << 16, dtype=torch.int64, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    C.timeline_start(buf)
+    with torch.cuda.graph(g, stream=s):
+        fn()
+    used = C.timeline_stop()
+    ents = C.timeline_entries()
+    out = {}
+    for _ in range(3):
+        buf.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+    t = buf[:used].view(-1, 2).cpu().double()
+    for name, off, nb in ents:
+        blk = t[off // 2: off // 2 + nb]
+        blk = blk[blk[:, 0] > 0]
+        if len(blk) == 0:
+            continue
+        st = (blk[:, 0] - blk[:, 0].min()) / 100.0
+        du = (blk[:, 1] - blk[:, 0]) / 100.0
+        q = lambda v, p: round(float(v.quantile(p)), 2)  # noqa: E731
+        out = {"blocks": len(blk), "dur_p10": q(du, 0.1), "dur_med": q(du, 0.5), "dur_p90": q(du, 0.9),
+               "dur_max": round(float(du.max()), 2), "start_p90": q(st, 0.9), "start_max": round(float(st.max()), 2),
+               "span": round(float((blk[:, 1].max() - blk[:, 0].min()) / 100.0), 2)}
+    return out
 from vgate import ops  # noqa: E402
 
 SHAPES = [("qkv", 2048, 1536, "plain"), ("o_proj", 1536, 1536, "plain"), ("gate_up", 17920, 1536, "silu"),
@@ -23,11 +57,15 @@ SHAPES = [("qkv", 2048, 1536, "plain"), ("o_proj", 1536, 1536, "plain"), ("gate_
 
 
 def main():
+    import os
     C = ops.native()
-    M, g = 8, 128
+    M, g = int(os.environ.get("AWQ_SWEEP_M", "8")), 128
+    only = os.environ.get("AWQ_SWEEP_SHAPES")
     dev = torch.device("cuda")
     ws = ops.workspace(dev)
     for name, N, K, layout in SHAPES:
+        if only and name not in only.split(","):
+            continue
         q = torch.randint(0, 16, (N, K), dtype=torch.int32, device=dev)
         scales = (torch.rand(K // g, N, device=dev) * 0.02 + 0.005).bfloat16()
         zeros = torch.randint(0, 16, (K // g, N), device=dev).float().bfloat16()
@@ -39,16 +77,24 @@ def main():
         epi = 2 if layout == "silu" else 0
         out = torch.empty(M, N // 2 if epi == 2 else N, device=dev, dtype=torch.bfloat16)
         rows = []
-        for waves, sk in [(0, 0), (0, 1), (0, 2), (0, 3), (0, 4), (0, 6), (0, 8), (4, 0), (8, 0), (8, 2)]:
+        # ntb: 0 = launcher's choice (awq_stream_kernel), -1 = LDS-staged awq_dec_kernel,
+        # -2 = K-split awq_gemm_kernel
+        for waves, sk, ntb in [(0, 0, 0), (2, 0, 0), (4, 0, 0), (8, 0, 0), (0, 2, 0), (0, 4, 0), (0, 0, -1),
+                               (4, 0, -2)]:
             def fns():
                 for i in range(12):
                     L = lins[i % ncopy]
                     C.gemm(x, L.wp, N, K, out, epi, res=None if epi else res, ws=ws, waves=waves, splitk=sk,
-                           awq_scales=L.scales, awq_zeros=L.zeros, group=g)
+                           awq_scales=L.scales, awq_zeros=L.zeros, group=g, awq_szp=L.szp, ntb=ntb)
             spans, wall = timeline_graph(C, fns)
             vals = [v for vs in spans.values() for v in vs]
-            rows.append({"waves": waves, "splitk": sk, "span_us": round(sum(vals[1:]) / (len(vals) - 1), 2),
-                         "wall_us": round(wall / 12, 2)})
+            w_us = wall / 12
+            L0 = lins[0]
+            bs = block_stats(C, lambda: C.gemm(x, L0.wp, N, K, out, epi, res=None if epi else res, ws=ws, waves=waves,
+                                               splitk=sk, awq_scales=L0.scales, awq_zeros=L0.zeros, group=g,
+                                               awq_szp=L0.szp, ntb=ntb))
+            rows.append({"waves": waves, "splitk": sk, "ntb": ntb, "span_us": round(sum(vals[1:]) / (len(vals) - 1), 2),
+                         "wall_us": round(w_us, 2), "eff_TBps": round(lins[0].nbytes() / w_us / 1e6, 2), "blocks": bs})
         print(json.dumps({"shape": name, "N": N, "K": K, "rows": rows}), flush=True)
 
 

@@ -39,6 +39,8 @@
 // AWQ W4A16 variant: int4 weights in the same fragment order, 4 k-tiles per 16-B
 // lane load ([nt][kt/4][lane][4] uint32, nibble j = element j), group-wise
 // (scale, scale*zero) applied in registers before the bf16 MFMA.
+#include <cstdlib>
+
 #include "gemm_epilogue.h"
 
 namespace vgate {
@@ -464,26 +466,34 @@ __global__ __launch_bounds__(512) void awq_gemm_kernel(GemmParams p) {  // <= 8 
   gemm_finish<MB, NTB, EPI, NORM, false>(p, acc, ssr, smem, m_base, nt0, EpiPre<NTB>{});
 }
 
-// ---- AWQ W4A16 decode (M <= 16): waves split N and share ONE LDS copy of the activations ----
-// With int4 weights a 16-B lane load carries 4 k-steps of one 16-column tile, while the
-// matching activation fragments are 4 x 16 B: a K-split kernel (waves split K, every wave
-// its own x range) moves 2-4x more activation than weight bytes through the vector-memory
-// pipe. Here a block = 4 waves x NTW tiles, the activation slice of the block's K-slice is
-// staged once into LDS in MFMA B-fragment order (ds_read_b128 per k-step, off the vector
-// memory pipe; RMSNorm gamma applied while staging, the row sum of squares over the FULL row
-// so a split-K slice needs no ssq hand-off) and each wave streams only int4 weights + group
-// scales, software-pipelined G k-quads ahead (ping-pong register groups, partial last group
-// clamped). Split-K slices meet at a per-column-group ticket (sc1 slabs, last arriver sums).
+// ---- AWQ W4A16 decode (M <= 16): every weight byte of the launch in flight at once ----
+// int4 decode is pure latency x bytes-in-flight: 13.8 MB of gate_up int4 at ~2 us of HBM
+// latency needs ~12 MB outstanding to run at 6 TB/s (Little's law). The previous kernel
+// pipelined 2 k-quads per wave (16 KB per block, 140 blocks: 2.2 MB in flight -> 1.0 TB/s,
+// profiles/r1_awq_bench_kernel_summary.txt). Here each wave owns NTW tiles x the block's
+// k-slice (<= AQ_KQ k-quads) and issues ALL of its int4 fragments and packed group scales
+// before the first MFMA; a launch covers every tile, so the whole matrix is requested in the
+// first ~microsecond.
+//
+// Block = AD_WAVES waves x NTW tiles; grid.z = K slices. The activation slice is staged ONCE
+// per block into LDS in MFMA B-fragment order (RMSNorm gamma applied while staging; the row sum
+// of squares over the FULL row so a K-slice needs no ssq hand-off) with the per-(k-quad, row)
+// activation sums X that the raw-nibble trick needs:
+//   sum_k x (v - z) s = s * sum_k x (128 + v)  -  (128 s + s z) * X       (one group per k-quad)
+// where (128 + v) is built as bf16 straight from the nibbles (raw8, 4 ALU per 8 weights).
+// Group scales arrive fragment-packed (ops.pack_awq_sz: [nt][kq][lane group][s0..3, sz0..3]):
+// ONE 16-B load per (tile, k-quad) instead of two 8-B ones. Split-K slices meet at a per-group
+// ticket (sc1 slabs, last arriver sums).
 constexpr int AD_WAVES = 4;
-constexpr int AD_G = 2;  // k-quads (128 k) per register group
-constexpr int AD_SK_MAX = 16;  // split-K slices (<= 16 staged k-quads per slice: K <= 32768)
+constexpr int AQ_KQ = 12;      // (k-quads per slice) x NTW held in flight: 2 x 12 uint4 per lane
+constexpr int AD_SK_MAX = 16;  // split-K slices
 
 template <int NTW, int EPI, int NORM>
-__global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
+__global__ __launch_bounds__(256, 1) void awq_dec_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   TLScope tl_scope(p.dbg_ts);
   // profiling: phase stamps of the first and the last block after the per-block slots
-  // (benchmarks/awq_phases.py; the launcher reserves 8 extra slot pairs)
+  // (benchmarks/awq_sweep.py; the launcher reserves 8 extra slot pairs)
   const size_t nblk = (size_t)gridDim.x * gridDim.y * gridDim.z;
   const size_t bid = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
   unsigned long long* ph = (p.dbg_ts != nullptr && threadIdx.x == 0 && (bid == 0 || bid == nblk - 1))
@@ -494,152 +504,128 @@ __global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
   const int KQ = p.K >> 7;
   const int nt0 = (blockIdx.x * AD_WAVES + wid) * NTW;  // this wave's first 16-column tile
   const int q0 = (KQ * blockIdx.z) / p.splitk, q1 = (KQ * (blockIdx.z + 1)) / p.splitk;
-  const int nq = q1 - q0, nst = nq * 4;  // k-quads / k-steps of the slice
+  const int nq = q1 - q0, nst = nq * 4;  // k-quads / k-steps of the slice (nq <= AQ_KQ / NTW, host-checked)
+  constexpr int GQ = AQ_KQ / NTW;        // k-quads held per wave
   uint4* xs = reinterpret_cast<uint4*>(smem);                             // [nst][64] B fragments
-  float* xsum = reinterpret_cast<float*>(smem + (size_t)nst * 64 * 16);  // [nq][16] per-group row sums
-  float* ssq = xsum + nq * 16;                                            // [4 waves][16] slice sums of squares
+  float* xsum = reinterpret_cast<float*>(smem + (size_t)nst * 64 * 16);  // [nq][4 waves][16] row-sum partials
+  float* ssq = xsum + nq * 64;                                            // [4 waves][16] slice sums of squares
   int* flag = reinterpret_cast<int*>(ssq + 4 * 16);
   const int m = lane & 15, nsub = 4 * (lane >> 4);
-  // 1) activation slice -> registers (issued FIRST, so waiting for it leaves the weights that
-  //    follow in flight), then the first weight groups, then the LDS image of the slice.
-  //    Thread t stages fragment f = i * 256 + t: lane t & 63, k-step 4i + (t >> 6).
-  constexpr int XMAX = 16;  // k-steps per thread (slices of <= 16 k-quads, checked on the host)
+  // 1) activation slice -> registers (issued first: the staging below waits for these alone and
+  //    leaves every weight load in flight). Thread t stages fragment f = i * 256 + t: lane t & 63,
+  //    k-step 4i + (t >> 6).
+  constexpr int XMAX = GQ;  // k-steps per thread (4 waves x XMAX = 4 GQ k-steps)
+  // Loads are UNCONDITIONAL (clamped k-step, value masked after the load): a load behind a
+  // runtime branch makes the compiler give up its vmcnt count and wait for EVERY outstanding
+  // load — all the weights below — before the staging (measured: 6 us blocks for 48 KB).
   uint4 xr[XMAX];
-  const int xrow_m = lane & 15;
-  const bf16_t* xrow = p.x + (size_t)row_of(p, min(xrow_m, p.M - 1)) * p.lda + 8 * (lane >> 4);
+  const bf16_t* xrow = p.x + (size_t)row_of(p, min(m, p.M - 1)) * p.lda + 8 * (lane >> 4);
 #pragma unroll
-  for (int i = 0; i < XMAX; ++i) {
-    const int t = 4 * i + wid;  // k-step of the slice
-    xr[i] = (t < nst && xrow_m < p.M) ? ld16(xrow + (q0 * 4 + t) * 32) : make_uint4(0, 0, 0, 0);
-  }
-  // RMSNorm gamma of the same k-steps, issued with the activations (loading it inside the
-  // staging loop added a dependent round trip: gate_up 16 us in the engine)
+  for (int i = 0; i < XMAX; ++i) xr[i] = ld16(xrow + (q0 * 4 + min(4 * i + wid, nst - 1)) * 32);
   uint4 gr[NORM == 1 ? XMAX : 1];
   if constexpr (NORM == 1) {
 #pragma unroll
-    for (int i = 0; i < XMAX; ++i) {
-      const int t = 4 * i + wid;
-      gr[i] = t < nst ? ld16(p.norm_w + (q0 * 4 + t) * 32 + 8 * (lane >> 4)) : make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < XMAX; ++i) gr[i] = ld16(p.norm_w + (q0 * 4 + min(4 * i + wid, nst - 1)) * 32 + 8 * (lane >> 4));
+  }
+  // x first, ALONE: issued together with the weights, every CU's x requests queue behind the
+  // whole launch's weight misses and the staging starts only when the weights have landed
+  // (x staged at 4.5 us of a 7 us block, benchmarks/awq_phases.py); one L2 / MALL round trip
+  // up front instead lets the staging overlap the weight stream
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // 2) the wave's whole weight slice + its packed group scales, all issued now (indices past the
+  //    slice re-read its last k-quad: issued unconditionally, never consumed)
+  uint4 w[GQ][NTW], sz[GQ][NTW];
+  const uint4* szp = reinterpret_cast<const uint4*>(p.szp);  // [N/16][KQ][4][16 B]
+#pragma unroll
+  for (int g = 0; g < GQ; ++g) {
+    const int kq = q0 + min(g, nq - 1);
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      w[g][j] = ld_nt16(p.wp + ((size_t)(nt0 + j) * KQ + kq) * 64 + lane);
+      sz[g][j] = szp[((size_t)(nt0 + j) * KQ + kq) * 4 + (lane >> 4)];
     }
   }
-  // 2) weight stream: this wave's NTW tiles over the block's k-quads. Per k-quad and tile:
-  //    P = sum over the quad's 4 MFMAs of raw8(w) . x, then acc += s (x) P - (128 s + s z) X
-  //    with s, s z of the lane's 4 output columns and X the row's activation sum (one group
-  //    per k-quad: group % 128 == 0, checked on the host)
+  // 3) the activation image (x * gamma under NORM == 1), this wave's slice sum of squares and the
+  //    per-(k-quad, row) activation sums X, all from registers: k-quad i is exactly the 4 k-steps
+  //    4i + wave of the four waves, so X = sum over (8 elements, 4 lane groups, 4 waves)
+  float* xsw = xsum;  // [nq][4 waves][16] partial sums, folded over the waves in step 4
+  const bool mok = m < p.M;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < XMAX; ++i) {
+    const int t = 4 * i + wid;
+    uint4 v = (mok && i < nq) ? xr[i] : make_uint4(0, 0, 0, 0);  // clamped duplicates past the slice add 0
+    float a[8];
+    unpack8(v, a);
+    if constexpr (NORM != 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += a[j] * a[j];
+      if constexpr (NORM == 1) {
+        float g8[8];
+        unpack8(gr[i], g8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] *= g8[j];
+        v = pack8(a);
+        unpack8(v, a);  // X must sum the bf16 values the MFMA sees
+      }
+    }
+    float xs8 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xs8 += a[j];
+    xs8 += xor16(xs8);
+    xs8 += xor32(xs8);
+    if (i < nq) {  // wave-uniform (stores only)
+      xs[t * 64 + lane] = v;
+      if (lane < 16) xsw[(i * 4 + wid) * 16 + lane] = xs8;
+    }
+  }
+  if constexpr (NORM != 0) {
+    ss += xor16(ss);
+    ss += xor32(ss);
+    if (lane < 16) ssq[wid * 16 + lane] = ss;
+  }
+  AD_PHASE(1);
+  lds_barrier();  // LDS image visible; the weight loads stay in flight
+  AD_PHASE(2);
+  // 4) consume in issue order (the compiler's vmcnt waits stay partial: k-quad g needs only
+  //    the loads issued before it)
   f32x4 acc[NTW];
 #pragma unroll
   for (int j = 0; j < NTW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto load_grp = [&](uint4 (&w)[AD_G][NTW], uint2 (&sv)[AD_G][NTW], uint2 (&zv)[AD_G][NTW], int kq0) {
 #pragma unroll
-    for (int g = 0; g < AD_G; ++g) {
-      const int kq = min(kq0 + g, q1 - 1);
-      const size_t gi = (size_t)((kq * 128) / p.group) * p.N;
+  for (int g = 0; g < GQ; ++g) {
+    // predicated, not `break`: a multi-exit loop is not fully unrolled at GQ = 12 and the
+    // register arrays w / sz then live in scratch (400 B per lane)
+    if (g < nq) {  // wave-uniform
+    f32x4 pr[NTW];
 #pragma unroll
-      for (int j = 0; j < NTW; ++j) {
-        w[g][j] = ld_nt16(p.wp + ((size_t)(nt0 + j) * KQ + kq) * 64 + lane);
-        sv[g][j] = *reinterpret_cast<const uint2*>(p.scales + gi + (nt0 + j) * 16 + nsub);
-        zv[g][j] = *reinterpret_cast<const uint2*>(p.zeros + gi + (nt0 + j) * 16 + nsub);
-      }
-    }
-  };
-  auto mma_grp = [&](const uint4 (&w)[AD_G][NTW], const uint2 (&sv)[AD_G][NTW], const uint2 (&zv)[AD_G][NTW],
-                     int kq0) {
+    for (int j = 0; j < NTW; ++j) pr[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int g = 0; g < AD_G; ++g) {
-      const int kq = kq0 + g;
-      if (kq >= q1) break;  // wave-uniform
-      const int t0 = (kq - q0) * 4;
-      f32x4 pr[NTW];
-#pragma unroll
-      for (int j = 0; j < NTW; ++j) pr[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const bf16x8 xb = as_bf16x8(xs[(t0 + u) * 64 + lane]);
-#pragma unroll
-        for (int j = 0; j < NTW; ++j) {
-          const uint32_t q = u == 0 ? w[g][j].x : u == 1 ? w[g][j].y : u == 2 ? w[g][j].z : w[g][j].w;
-          pr[j] = mfma16(raw8(q), xb, pr[j]);
-        }
-      }
-      const float X = xsum[(kq - q0) * 16 + m];
+    for (int u = 0; u < 4; ++u) {
+      const bf16x8 xb = as_bf16x8(xs[(g * 4 + u) * 64 + lane]);
 #pragma unroll
       for (int j = 0; j < NTW; ++j) {
-        const float s4[4] = {bf_lo(sv[g][j].x), bf_hi(sv[g][j].x), bf_lo(sv[g][j].y), bf_hi(sv[g][j].y)};
-        const float z4[4] = {bf_lo(zv[g][j].x), bf_hi(zv[g][j].x), bf_lo(zv[g][j].y), bf_hi(zv[g][j].y)};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[j][i] = fmaf(s4[i], pr[j][i], fmaf(-fmaf(128.f, s4[i], z4[i]), X, acc[j][i]));
+        const uint32_t q = u == 0 ? w[g][j].x : u == 1 ? w[g][j].y : u == 2 ? w[g][j].z : w[g][j].w;
+        pr[j] = mfma16(raw8(q), xb, pr[j]);
       }
     }
-  };
-  const int ngrp = (nq + AD_G - 1) / AD_G;
-  {
-    uint4 wa[AD_G][NTW], wb[AD_G][NTW];
-    uint2 sa[AD_G][NTW], sb[AD_G][NTW], za[AD_G][NTW], zb[AD_G][NTW];
-    int kq = q0;
-    if (ngrp > 0) load_grp(wa, sa, za, kq);
-    // the activation image (x * gamma under NORM == 1) and this wave's slice sum of squares
-    float ss = 0.f;
+    const float X = ((xsw[(g * 4 + 0) * 16 + m] + xsw[(g * 4 + 1) * 16 + m]) + xsw[(g * 4 + 2) * 16 + m]) +
+                    xsw[(g * 4 + 3) * 16 + m];  // fixed wave order
 #pragma unroll
-    for (int i = 0; i < XMAX; ++i) {
-      const int t = 4 * i + wid;
-      if (t < nst) {
-        uint4 v = xr[i];
-        if constexpr (NORM != 0) {
-          float a[8];
-          unpack8(v, a);
+    for (int j = 0; j < NTW; ++j) {
+      const float s4[4] = {bf_lo(sz[g][j].x), bf_hi(sz[g][j].x), bf_lo(sz[g][j].y), bf_hi(sz[g][j].y)};
+      const float z4[4] = {bf_lo(sz[g][j].z), bf_hi(sz[g][j].z), bf_lo(sz[g][j].w), bf_hi(sz[g][j].w)};
 #pragma unroll
-          for (int j = 0; j < 8; ++j) ss += a[j] * a[j];
-          if constexpr (NORM == 1) {
-            float g8[8];
-            unpack8(gr[i], g8);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) a[j] *= g8[j];
-            v = pack8(a);
-          }
-        }
-        xs[t * 64 + lane] = v;
-      }
+      for (int i = 0; i < 4; ++i) acc[j][i] = fmaf(s4[i], pr[j][i], fmaf(-fmaf(128.f, s4[i], z4[i]), X, acc[j][i]));
     }
-    if constexpr (NORM != 0) {
-      ss += xor16(ss);
-      ss += xor32(ss);
-      if (lane < 16) ssq[wid * 16 + lane] = ss;
-    }
-    lds_barrier();  // LDS image visible; the weight loads stay in flight
-    AD_PHASE(1);
-    // per (k-quad, row) sum of the staged (bf16) activations, fixed order
-    for (int idx = threadIdx.x; idx < nq * 16; idx += blockDim.x) {
-      const int ql = idx >> 4, r = idx & 15;
-      float sacc = 0.f;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          float a[8];
-          unpack8(xs[(ql * 4 + u) * 64 + g4 * 16 + r], a);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) sacc += a[j];
-        }
-      xsum[idx] = sacc;
-    }
-    lds_barrier();
-    AD_PHASE(2);
-    int g = 0;
-    for (; g + 2 <= ngrp; g += 2) {
-      load_grp(wb, sb, zb, kq + AD_G);
-      mma_grp(wa, sa, za, kq);
-      if (g + 2 < ngrp) load_grp(wa, sa, za, kq + 2 * AD_G);
-      mma_grp(wb, sb, zb, kq + AD_G);
-      kq += 2 * AD_G;
-    }
-    if (g < ngrp) mma_grp(wa, sa, za, kq);
+  }
   }
   AD_PHASE(3);
-  // 3) finish: lane holds D[n = 4(l>>4) + i][m = l & 15] of each tile
+  // 5) finish: lane holds D[n = 4(l>>4) + i][m = l & 15] of each tile
   float ss_slice = 0.f;  // this slice's row sum of squares (fixed wave order)
   if constexpr (NORM != 0) {
 #pragma unroll
-    for (int w = 0; w < AD_WAVES; ++w) ss_slice += ssq[w * 16 + m];
+    for (int ww = 0; ww < AD_WAVES; ++ww) ss_slice += ssq[ww * 16 + m];
   }
   auto finish = [&](f32x4 (&v)[NTW], float ss_row) {
     if constexpr (NORM != 0) {
@@ -671,7 +657,6 @@ __global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
     *flag = last;
   }
   __syncthreads();
-  AD_PHASE(4);
   if (!*flag) return;
   const float* all = p.slabs + (size_t)grp * p.splitk * SLAB;
   const uint32_t all_off = (uint32_t)((size_t)grp * p.splitk * SLAB * 4);
@@ -701,6 +686,209 @@ __global__ __launch_bounds__(256) void awq_dec_kernel(GemmParams p) {
   finish(v, ss_row);
   AD_PHASE(5);
 #undef AD_PHASE
+}
+
+// ---- AWQ W4A16 decode, weight-streaming form (M <= 16) ----
+// The bf16 decode kernel's decomposition applied to int4: a block = ONE 16-column tile, its
+// waves split K, every wave streams its own k-quads with software-pipelined (ping-pong) groups
+// of U k-quads: int4 fragment + packed (s, s*z) + its own activation fragments per k-quad, all
+// issued one group ahead. No LDS staging (the staged kernel's x round trip sat on every
+// block's critical path: x staged 3.6-4.5 us into a 7 us block, benchmarks/awq_phases.py), no
+// per-block xsum pass: the per-(k-quad, row) activation sum X of the raw-nibble identity
+//   sum_k x (v - z) s = s * sum_k x (128 + v) - (128 s + s z) * X
+// comes from the fragments already in registers (8 values per lane per k-step, folded over the
+// 4 lane groups with two cross-lane adds). XP activation packing (M <= 16/XP rows: one 16-B load
+// covers XP k-steps) as in gemm_kernel. Cross-wave reduction, deferred RMSNorm row scale,
+// split-K slabs and the epilogue are gemm_finish's.
+template <int U, int EPI, int NORM, int XP, bool PP>
+__global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
+  constexpr int R = 16 / XP;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  TLScope tl_scope(p.dbg_ts);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int KQ = p.K >> 7;
+  const int nt0 = blockIdx.x;
+  const int s0 = (KQ * blockIdx.z) / p.splitk, s1 = (KQ * (blockIdx.z + 1)) / p.splitk;
+  const int qbeg = s0 + ((s1 - s0) * wid) / nw;
+  const int qend = s0 + ((s1 - s0) * (wid + 1)) / nw;
+  const int r16 = lane & 15;
+  const int mrow = XP > 1 ? r16 % R : r16;
+  const bool xok = mrow < p.M;
+  const bf16_t* xrow = p.x + (size_t)row_of(p, mrow) * p.lda + 8 * (lane >> 4) + (XP > 1 ? (r16 / R) * 32 : 0);
+  const uint4* wbase = p.wp + (size_t)nt0 * KQ * 64 + lane;
+  const uint4* szbase = reinterpret_cast<const uint4*>(p.szp) + (size_t)nt0 * KQ * 4 + (lane >> 4);
+  // RMSNorm gamma (NORM == 1): packed exactly like the activations (it depends on the column only),
+  // loaded with them one group ahead and applied before the unpack
+  const bf16_t* grow = p.norm_w ? p.norm_w + 8 * (lane >> 4) + (XP > 1 ? (r16 / R) * 32 : 0) : nullptr;
+  f32x4 acc[1][1] = {{f32x4{0.f, 0.f, 0.f, 0.f}}};
+  float ssr[1] = {0.f};
+  constexpr int XL = 4 / XP;  // activation loads per k-quad
+  const uint32_t lom = r16 < R ? ~0u : 0u;
+  constexpr int GL = NORM == 1 ? XL : 1;
+  auto load_grp = [&](uint4 (&w)[U], uint4 (&sz)[U], uint4 (&xa)[U][XL], uint4 (&ga)[U][GL], int kq0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kq = min(kq0 + u, qend - 1);  // clamped: issued unconditionally, masked in mma
+      w[u] = ld_nt16(wbase + (size_t)kq * 64);
+      sz[u] = (p.probe & 2) ? make_uint4(0x3c003c00u, 0x3c003c00u, 0, 0) : szbase[(size_t)kq * 4];
+#pragma unroll
+      for (int v = 0; v < XL; ++v)
+        xa[u][v] = (xok && !(p.probe & 1)) ? *reinterpret_cast<const uint4*>(xrow + (kq * 4 + v * XP) * 32)
+                                           : make_uint4(0, 0, 0, 0);
+      if constexpr (NORM == 1) {
+#pragma unroll
+        for (int v = 0; v < XL; ++v) ga[u][v] = *reinterpret_cast<const uint4*>(grow + (kq * 4 + v * XP) * 32);
+      }
+    }
+  };
+  // the 4 unpacked B fragments of one k-quad from its XP-packed loads
+  auto unpack4 = [&](const uint4 (&src)[XL], uint4 (&b)[4]) {
+#pragma unroll
+    for (int v = 0; v < XL; ++v) {
+      const uint4 t = src[v];
+      if constexpr (XP == 1) {
+        b[v] = t;
+      } else {
+        b[v * XP] = and_mask(t, lom);
+        b[v * XP + 1] = and_mask(row_ror<R>(t), lom);
+        if constexpr (XP == 4) {
+          b[v * XP + 2] = and_mask(row_ror<2 * R>(t), lom);
+          b[v * XP + 3] = and_mask(row_ror<3 * R>(t), lom);
+        }
+      }
+    }
+  };
+  auto mma_grp = [&](const uint4 (&w)[U], const uint4 (&sz)[U], const uint4 (&xa)[U][XL], const uint4 (&ga)[U][GL],
+                     int kq0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kq = kq0 + u;
+      const bool live = kq < qend;  // wave-uniform: a partial last group adds nothing
+      uint4 b[4];
+      if constexpr (NORM == 1) {
+        // sum of squares over the RAW activations (unpacked: lane l <-> row l & 15, as
+        // gemm_finish folds it), the MFMA operand is bf16(x * gamma)
+        uint4 raw[4];
+        unpack4(xa[u], raw);
+        uint4 xg[XL];
+#pragma unroll
+        for (int v = 0; v < XL; ++v) {
+          float f[8], g8[8];
+          unpack8(xa[u][v], f);
+          unpack8(ga[u][v], g8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] *= g8[j];
+          xg[v] = pack8(f);
+        }
+        unpack4(xg, b);
+        if (live) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            float f[8];
+            unpack8(raw[t], f);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ssr[0] += f[j] * f[j];
+          }
+        }
+      } else {
+        unpack4(xa[u], b);
+      }
+      if (!live) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) b[t] = make_uint4(0, 0, 0, 0);
+      }
+      float X = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float f[8];
+        unpack8(b[t], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) X += f[j];
+      }
+      X += xor16(X);
+      X += xor32(X);
+      f32x4 pr = {0.f, 0.f, 0.f, 0.f};
+      pr = mfma16(raw8(w[u].x), as_bf16x8(b[0]), pr);
+      pr = mfma16(raw8(w[u].y), as_bf16x8(b[1]), pr);
+      pr = mfma16(raw8(w[u].z), as_bf16x8(b[2]), pr);
+      pr = mfma16(raw8(w[u].w), as_bf16x8(b[3]), pr);
+      const float s4[4] = {bf_lo(sz[u].x), bf_hi(sz[u].x), bf_lo(sz[u].y), bf_hi(sz[u].y)};
+      const float z4[4] = {bf_lo(sz[u].z), bf_hi(sz[u].z), bf_lo(sz[u].w), bf_hi(sz[u].w)};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[0][0][i] = fmaf(s4[i], pr[i], fmaf(-fmaf(128.f, s4[i], z4[i]), X, acc[0][0][i]));
+    }
+  };
+  int kq = qbeg;
+  const int ngrp = (qend - qbeg + U - 1) / U;
+  if constexpr (!PP) {
+    // ONE group covering the wave's whole k-range (host-checked: <= U k-quads): every load of
+    // the wave in flight at once, one memory round trip per block
+    uint4 wa[U], sa[U], xa[U][XL], gaa[U][GL];
+    load_grp(wa, sa, xa, gaa, kq);
+    mma_grp(wa, sa, xa, gaa, kq);
+  } else if (ngrp > 0) {
+    uint4 wa[U], sa[U], xa[U][XL], gaa[U][GL], wb[U], sb[U], xb[U][XL], gab[U][GL];
+    load_grp(wa, sa, xa, gaa, kq);
+    int g = 0;
+    for (; g + 2 <= ngrp; g += 2) {
+      load_grp(wb, sb, xb, gab, kq + U);
+      mma_grp(wa, sa, xa, gaa, kq);
+      if (g + 2 < ngrp) load_grp(wa, sa, xa, gaa, kq + 2 * U);
+      mma_grp(wb, sb, xb, gab, kq + U);
+      kq += 2 * U;
+    }
+    if (g < ngrp) mma_grp(wa, sa, xa, gaa, kq);
+  }
+  gemm_finish<1, 1, EPI, NORM, false>(p, acc, ssr, smem, 0, nt0, EpiPre<1>{});
+}
+
+// ---- AWQ prefill operand: int4 fragments -> bf16 fragments (same fragment order) ----
+// Long AWQ steps run the LDS-tiled bf16 prefill kernel (gemm_prefill.hip) on a per-call scratch
+// copy of ONE matrix, dequantised here in the packed layout the kernel reads: lane l's k-step
+// fragment of tile nt is element-wise (v - z) * s [* gamma_k] of the int4 fragment that the decode
+// kernels feed to the MFMA as raw8. Folding the RMSNorm gamma in here turns the gamma-in-registers
+// prologue (which the prefill kernel does not take) into the row-scale-only mode. No bf16 copy of
+// the model is kept: the scratch is the largest single matrix (gate_up: 55 MB for Qwen2.5-1.5B).
+// One thread per (tile, k-quad, lane): 16 B int4 in, 4 x 16 B bf16 out.
+__global__ __launch_bounds__(256) void awq_dequant_packed_kernel(const uint4* __restrict__ wq,
+                                                                 const bf16_t* __restrict__ scales,
+                                                                 const bf16_t* __restrict__ sz,
+                                                                 const bf16_t* __restrict__ gamma, uint4* __restrict__ out,
+                                                                 int N, int K, int group) {
+  const int KQ = K >> 7;
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // ((nt * KQ) + kq) * 64 + lane
+  if (idx >= (size_t)(N >> 4) * KQ * 64) return;
+  const int lane = (int)(idx & 63);
+  const size_t tq = idx >> 6;
+  const int kq = (int)(tq % KQ), nt = (int)(tq / KQ);
+  const int n = nt * 16 + (lane & 15);
+  const uint4 q = wq[idx];
+  const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int k0 = (kq * 4 + u) * 32 + 8 * (lane >> 4);
+    const int g = k0 / group;
+    const float s = bf2f(scales[(size_t)g * N + n]), zs = bf2f(sz[(size_t)g * N + n]);
+    float f[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (float)((qw[u] >> ((j & 1) * 16 + 4 * (j >> 1))) & 0xF) * s - zs;
+    if (gamma != nullptr) {
+      float g8[8];
+      unpack8(*reinterpret_cast<const uint4*>(gamma + k0), g8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= g8[j];
+    }
+    out[(((size_t)nt * (K >> 5)) + kq * 4 + u) * 64 + lane] = pack8(f);
+  }
+}
+
+void launch_awq_dequant(const void* wq, const uint16_t* scales, const uint16_t* sz, const uint16_t* gamma,
+                        void* out, int N, int K, int group, hipStream_t st) {
+  const size_t n = (size_t)(N / 16) * (K / 128) * 64;
+  hipLaunchKernelGGL(awq_dequant_packed_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     reinterpret_cast<const uint4*>(wq), reinterpret_cast<const bf16_t*>(scales),
+                     reinterpret_cast<const bf16_t*>(sz), reinterpret_cast<const bf16_t*>(gamma),
+                     reinterpret_cast<uint4*>(out), N, K, group);
 }
 
 // ---- prefill / medium-M tile GEMM (M > 16, bf16 weights) ----
@@ -904,41 +1092,89 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
   }
 }
 
-// AWQ decode (M <= 16): column groups of AD_WAVES x NTW tiles, K split so the grid covers the
-// chip (>= 256 blocks where K allows >= 2 k-quads per slice)
+// AWQ decode (M <= 16): column groups of AD_WAVES x NTW tiles, the K slices chosen so the grid
+// covers the chip and every slice fits the all-in-flight register budget (<= AQ_KQ k-quads).
+// Needs the fragment-packed scales (p.zeros = ops.pack_awq_sz, group 128).
 template <int NTB, int EPI, int NORM>
 static bool launch_awq_dec(GemmParams p, const GemmArgs& g, hipStream_t st) {
   const int ntiles = g.N / 16;
-  if (g.M > 16 || ntiles % (AD_WAVES * NTB) != 0 || g.waves > 0 || g.group % 128 != 0) return false;
-  // measured (benchmarks/awq_sweep.py, profiles/r1_awq_sweep.log, Qwen2.5-1.5B shapes, M = 8):
-  // the LDS-staged kernel wins for long K (down: 11.4 vs 18 us) and wide N (gate_up at one
-  // slice: 10.5 vs 12.1 us); for narrow N x short K (qkv, o_proj) its staging prologue costs
-  // more than the activation traffic it saves and the K-split kernel keeps them (4.8 vs 7.0 us)
-  const bool wide = g.N >= 8192, deep = g.K >= 4096;
-  if (g.splitk <= 0 && !wide && !deep) return false;
+  if (g.M > 16 || ntiles % (AD_WAVES * NTB) != 0 || g.waves > 0 || g.group != 128 || g.awq_szp == nullptr)
+    return false;
+  // narrow N x short K (qkv / o_proj: 1-1.5 MB of int4) is one round trip whichever way it is
+  // cut; the K-split kernel (waves split K, no LDS staging) has the shorter block (3.1 vs 4.3 us,
+  // profiles/r2_awq_sweep.log) — unless a slice count is forced
+  if (g.splitk <= 0 && g.N < 8192 && g.K < 4096) return false;
   const int groups = ntiles / (AD_WAVES * NTB);
   const int KQ = g.K / 128;
-  int sk = g.splitk > 0 ? g.splitk : (wide && !deep) ? 1 : (256 + groups - 1) / groups;
-  if (g.splitk <= 0 && sk > 8) sk = 8;  // more slices only add hand-off traffic (sweep)
-  sk = sk > KQ / 2 ? KQ / 2 : sk;
-  sk = sk < 1 ? 1 : sk;
-  if ((KQ + sk - 1) / sk > 16) sk = (KQ + 15) / 16;  // staging holds <= 16 k-quads per slice
-  if (sk > AD_SK_MAX) return false;
+  const int gq = AQ_KQ / NTB;  // k-quads a wave holds in flight
+  int sk = (KQ + gq - 1) / gq;  // slices the register budget needs
+  if (g.splitk > 0) sk = sk > g.splitk ? sk : g.splitk;
+  else
+    while (groups * sk < 128 && KQ / (2 * sk) >= 3) sk *= 2;  // narrow N: spread over more CUs
+  if (sk > AD_SK_MAX || sk > KQ) return false;
   const size_t need_slab = (size_t)groups * sk * (AD_WAVES * NTB * 64 * 16 + 64);
-  if (sk > 1 && (g.slabs == nullptr || need_slab > g.slab_bytes || groups > g.max_counters)) sk = 1;
+  if (sk > 1 && (g.slabs == nullptr || need_slab > g.slab_bytes || groups > g.max_counters)) return false;
   p.splitk = sk;
   const int qmax = (KQ + sk - 1) / sk;
-  const size_t lds = (size_t)qmax * 4 * 64 * 16 + (size_t)qmax * 16 * 4 + 4 * 16 * 4 + 16;
-  if (lds > 150 * 1024) return false;
+  const size_t lds = (size_t)qmax * 4 * 64 * 16 + (size_t)qmax * 64 * 4 + 4 * 16 * 4 + 16;
   if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_dec", groups * sk + 8);  // + phase stamps
   hipLaunchKernelGGL((awq_dec_kernel<NTB, EPI, NORM>), dim3(groups, 1, sk), dim3(64 * AD_WAVES), lds, st, p);
+  return true;
+}
+
+// AWQ decode through awq_stream_kernel: one tile per block, waves split K, K slices across
+// blocks only when the tiles alone leave the chip under-filled. g.waves > 0 forces the wave
+// count (sweeps); returns false when the packed scales are missing (group != 128).
+template <int EPI, int NORM>
+static bool launch_awq_stream(GemmParams p, const GemmArgs& g, hipStream_t st) {
+  if (g.M > 16 || g.group != 128 || g.awq_szp == nullptr || g.ntb == -1) return false;
+  // narrow N x short K (qkv / o_proj, 1-1.5 MB of int4): the K-split awq_gemm_kernel's block is
+  // shortest (5.7 vs 6.1 us wall, profiles/r2_awq_sweep.log)
+  if (g.splitk <= 0 && g.waves <= 0 && g.N < 8192 && g.K < 4096) return false;
+  const int ntiles = g.N / 16;
+  const int KQ = g.K / 128;
+  int sk = g.splitk > 0 ? g.splitk : 1;
+  if (g.splitk <= 0)
+    while (ntiles * sk < 256 && KQ / (2 * sk) >= 12) sk *= 2;  // narrow N x deep K (down_proj)
+  if (sk > SK_MAX || sk > KQ) return false;
+  // waves: enough that each holds its whole k-range in one register group (<= AS_U k-quads),
+  // else (forced wave count / very deep K) the ping-pong pipeline
+  constexpr int AS_U = 6;
+  const int qslice = (KQ + sk - 1) / sk;
+  int w = g.waves > 0 ? g.waves : (qslice + AS_U - 1) / AS_U;
+  if (w > 8) w = 8;
+  const bool one = (qslice + w - 1) / w <= AS_U;
+  const size_t need_slab = (size_t)ntiles * sk * (64 * 16 + (NORM ? 16 * 4 : 0));
+  if (sk > 1 && (g.slabs == nullptr || need_slab > g.slab_bytes || ntiles > g.max_counters)) return false;
+  p.splitk = sk;
+  {
+    static const int probe = [] { const char* e = getenv("VGATE_AWQ_PROBE"); return e ? atoi(e) : 0; }();
+    p.probe = probe;
+  }
+  const size_t lds = red_bytes<1, 1>(w) + ssq_bytes<1>(w) + 16;
+  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_stream", ntiles * sk);
+  dim3 grid(ntiles, 1, sk), block(64 * w);
+  // ping-pong groups of 2 k-quads (4 spilled to scratch) when one group cannot hold the range
+#define VG_AS(XP_)                                                                                  \
+  do {                                                                                              \
+    if (one) hipLaunchKernelGGL((awq_stream_kernel<AS_U, EPI, NORM, XP_, false>), grid, block, lds, st, p); \
+    else hipLaunchKernelGGL((awq_stream_kernel<2, EPI, NORM, XP_, true>), grid, block, lds, st, p);       \
+  } while (0)
+  if (g.M <= 4) VG_AS(4);
+  else if (g.M <= 8) VG_AS(2);
+  else VG_AS(1);
+#undef VG_AS
   return true;
 }
 
 template <int NTB, int EPI, int NORM, bool AWQ>
 static void launch_m(GemmParams p, const GemmArgs& g, hipStream_t st) {
   if constexpr (AWQ) {
-    if (launch_awq_dec<NTB, EPI, NORM>(p, g, st)) return;
+    // g.ntb: -1 forces the LDS-staged kernel, -2 the K-split awq_gemm_kernel (sweeps / tests)
+    if constexpr (NORM != 2) {  // (the gamma-folded row-scale mode has no int4 form)
+      if (g.ntb != -2 && launch_awq_stream<EPI, NORM>(p, g, st)) return;
+      if (g.ntb != -2 && launch_awq_dec<NTB, EPI, NORM>(p, g, st)) return;
+    }
   }
   if constexpr (!AWQ) {
     // M > 16: N-split tile kernel with a shared LDS copy of x (see gemm_tile_kernel)
@@ -975,10 +1211,7 @@ static void launch_dispatch(GemmParams p, const GemmArgs& g, hipStream_t st) {
     else launch_m<NTB_, EPI_, 0, AWQ>(p, g, st);                                \
   } while (0)
   switch (g.epi) {
-    case EPI_SILU:  // self-contained 16-column tiles (8 gate + 8 up, see the epilogue)
-      if constexpr (AWQ) VG_NORM(2, EPI_SILU);
-      else VG_NORM(1, EPI_SILU);
-      break;
+    case EPI_SILU: VG_NORM(1, EPI_SILU); break;  // self-contained 16-column tiles (8 gate + 8 up)
     case EPI_QKV: VG_NORM(1, EPI_QKV); break;
     case EPI_F32:
       if constexpr (!AWQ) {
@@ -1007,7 +1240,7 @@ static GemmParams to_params(const GemmArgs& g) {
   p.slabs = g.slabs; p.counters = g.counters;
   p.positions = g.positions; p.slots = g.slots; p.cos_sin = g.cos_sin;
   p.k_cache = g.k_cache; p.v_cache = g.v_cache; p.hq = g.hq; p.hkv = g.hkv; p.bs = g.bs;
-  p.scales = g.scales; p.zeros = g.zeros; p.group = g.group;
+  p.scales = g.scales; p.zeros = g.zeros; p.group = g.group; p.szp = g.awq_szp;
   p.dbg_ts = g.dbg_ts;
   return p;
 }

@@ -22,6 +22,8 @@ struct GemmParams {
   const int32_t* positions; const int32_t* slots; const float* cos_sin;
   bf16_t* k_cache; bf16_t* v_cache; int hq; int hkv; int bs;
   const bf16_t* scales; const bf16_t* zeros; int group;
+  const bf16_t* szp;  // AWQ decode: fragment-packed (scale, scale * zero) [N/16][K/128][4][8]
+  int probe;          // profiling only (benchmarks/awq_sweep.py): 1 = skip activation loads, 2 = skip scale loads
   unsigned long long* dbg_ts;  // per-block [start, end] realtime stamps (profiling), or null
 };
 

@@ -43,6 +43,7 @@ struct GemmArgs {
   int hkv;
   int bs;
   // AWQ
+  const uint16_t* awq_szp = nullptr;  // AWQ decode: fragment-packed (s, s*z) [N/16][K/128][4][8]
   const uint16_t* scales;  // [K/group][N] bf16
   const uint16_t* zeros;   // [K/group][N] bf16 (= scale * zero)
   int group;
@@ -53,6 +54,9 @@ void launch_gemm(const GemmArgs& g, hipStream_t st);
 // LDS-tiled prefill GEMM (gemm_prefill.hip) for long steps; returns false for a shape / mode it
 // does not take (caller falls back). g.ntb: forced tile width (0 heuristic, 64, 128).
 bool launch_gemm_prefill(const GemmArgs& g, hipStream_t st);
+// AWQ int4 fragments -> bf16 fragment-packed copy (optionally gamma-folded) for the prefill kernel
+void launch_awq_dequant(const void* wq, const uint16_t* scales, const uint16_t* sz, const uint16_t* gamma,
+                        void* out, int N, int K, int group, hipStream_t st);
 
 // ---- custom one-shot all-reduce over xGMI peer memory (allreduce.hip) ----
 // bases[p]: rank p's IPC-mapped allocation = [AR_SIGNAL_BYTES signal area][2 x max_bytes data];

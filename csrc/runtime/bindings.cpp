@@ -54,7 +54,8 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
           const c10::optional<Tensor>& cos_sin, const c10::optional<Tensor>& k_cache,
           const c10::optional<Tensor>& v_cache, int64_t hq, int64_t hkv,
           const c10::optional<Tensor>& awq_scales, const c10::optional<Tensor>& awq_zeros, int64_t group,
-          bool rownorm, const c10::optional<Tensor>& dbg_ts, int64_t ntb, int64_t path) {
+          bool rownorm, const c10::optional<Tensor>& dbg_ts, int64_t ntb, int64_t path,
+          const c10::optional<Tensor>& awq_szp) {
   CHECK_DEV(x); CHECK_DEV(wp); CHECK_DEV(out);
   CHECK_DT(x, torch::kBFloat16);
   CHECK_LASTDIM(x); CHECK_LASTDIM(out);
@@ -76,7 +77,7 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
   if (ridx) M = row_idx->numel();
   const int64_t ncols = (epi == 2) ? N / 2 : N;
   if (epi == 1) CHECK_DT(out, torch::kFloat32); else CHECK_DT(out, torch::kBFloat16);
-  if (epi == 2 || epi == 3) TORCH_CHECK((N / 16) % 2 == 0, "paired-tile epilogue needs an even tile count");
+  if (epi == 3) TORCH_CHECK((N / 16) % 2 == 0, "qkv epilogue needs an even tile count");
   if (epi == 3) {
     TORCH_CHECK(N == (hq + 2 * hkv) * 128, "qkv epilogue: N must be (hq + 2 hkv) * 128");
     TORCH_CHECK(out.size(1) >= hq * 128, "qkv epilogue: q out cols");
@@ -115,9 +116,30 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
   g.v_cache = opt_ptr<uint16_t>(v_cache, torch::kBFloat16, "v_cache");
   g.hq = (int)hq; g.hkv = (int)hkv; g.bs = k_cache.has_value() && k_cache->defined() ? (int)k_cache->size(2) : 16;
   g.scales = opt_bf16(awq_scales); g.zeros = opt_bf16(awq_zeros); g.group = (int)group;
+  if (awq_szp.has_value() && awq_szp->defined()) {
+    CHECK_DEV(*awq_szp); CHECK_DT(*awq_szp, torch::kBFloat16);
+    TORCH_CHECK(group == 128 && awq_szp->numel() == N / 16 * (K / 128) * 32, "awq_szp: [N/16][K/128][4][8], group 128");
+    g.awq_szp = reinterpret_cast<const uint16_t*>(awq_szp->data_ptr());
+  }
   c10::DeviceGuard guard(x.device());
   if (awq) vgate::launch_awq_gemm(g, cur_stream());
   else vgate::launch_gemm(g, cur_stream());
+}
+
+// AWQ int4 packed weight -> bf16 packed weight (same fragment order / row permutation)
+void awq_dequant(const Tensor& wq, const Tensor& scales, const Tensor& sz, int64_t N, int64_t K, int64_t group,
+                 Tensor& out, const c10::optional<Tensor>& gamma) {
+  CHECK_DEV(wq); CHECK_DEV(scales); CHECK_DEV(sz); CHECK_DEV(out);
+  CHECK_DT(wq, torch::kInt32); CHECK_DT(scales, torch::kBFloat16); CHECK_DT(sz, torch::kBFloat16);
+  CHECK_DT(out, torch::kBFloat16);
+  TORCH_CHECK(N % 16 == 0 && K % 128 == 0 && K % group == 0 && group % 32 == 0, "awq_dequant: N/K/group");
+  TORCH_CHECK(wq.numel() == N * K / 8 && out.numel() >= N * K, "awq_dequant: sizes");
+  TORCH_CHECK(scales.size(0) == K / group && scales.size(1) == N && sz.sizes() == scales.sizes(), "awq_dequant: scales");
+  const uint16_t* g = opt_bf16(gamma);
+  if (g) TORCH_CHECK(gamma->numel() == K, "awq_dequant: gamma has K elements");
+  c10::DeviceGuard guard(wq.device());
+  vgate::launch_awq_dequant(wq.data_ptr(), bf16p(scales), bf16p(sz), g, out.data_ptr(), (int)N, (int)K, (int)group,
+                            cur_stream());
 }
 
 // y = rmsnorm(x [+ res]) * w ; res (if given) is updated in place to x + res
@@ -444,7 +466,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("slots") = py::none(), py::arg("cos_sin") = py::none(), py::arg("k_cache") = py::none(),
         py::arg("v_cache") = py::none(), py::arg("hq") = 0, py::arg("hkv") = 0,
         py::arg("awq_scales") = py::none(), py::arg("awq_zeros") = py::none(), py::arg("group") = 128,
-        py::arg("rownorm") = false, py::arg("dbg_ts") = py::none(), py::arg("ntb") = 0, py::arg("path") = 0);
+        py::arg("rownorm") = false, py::arg("dbg_ts") = py::none(), py::arg("ntb") = 0, py::arg("path") = 0,
+        py::arg("awq_szp") = py::none());
   m.def("attention", &attention, "unified paged attention: decode (partitions merged in-launch) + varlen prefill tiles",
         py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),
@@ -456,6 +479,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("rope_kv", &rope_kv, "NeoX RoPE + paged KV-cache write (rotated q in place or into q_out)",
         py::arg("qkv"), py::arg("positions"), py::arg("slots"), py::arg("cos_sin"), py::arg("k_cache"),
         py::arg("v_cache"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"), py::arg("q_out") = py::none());
+  m.def("awq_dequant", &awq_dequant, "AWQ int4 packed -> bf16 fragment-packed (prefill operand; optional gamma fold)",
+        py::arg("wq"), py::arg("scales"), py::arg("sz"), py::arg("N"), py::arg("K"), py::arg("group"), py::arg("out"),
+        py::arg("gamma") = py::none());
   m.def("silu_mul", &silu_mul, "out = silu(y[:, :I]) * y[:, I:] (library gate_up epilogue)");
   m.def("attn_decode", &attn_decode, "paged split-K decode attention");
   m.def("attn_prefill", &attn_prefill, "paged varlen causal prefill attention");

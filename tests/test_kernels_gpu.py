@@ -424,6 +424,58 @@ def test_awq_decode_kernel_shapes(M, g, sk):
     assert _rel_err(ys, ref.silu_mul_linear_ref(x, wd[: N // 2], wd[N // 2:])) < 2e-2
 
 
+@pytest.mark.parametrize("kernel", [0, -1, -2])
+@pytest.mark.parametrize("N,K", [(17920, 1536), (1536, 8960), (2048, 1536)])
+def test_awq_decode_kernels_each(kernel, N, K):
+    """Every AWQ decode kernel on the Qwen2.5-1.5B shapes (M = 8, group 128, RMSNorm gamma in
+    registers): 0 = launcher's choice (awq_stream_kernel for wide N / deep K), -1 = LDS-staged
+    awq_dec_kernel, -2 = K-split awq_gemm_kernel; == the dequantised fp32 reference."""
+    torch.manual_seed(N + K + kernel)
+    M, g = 8, 128
+    q = torch.randint(0, 16, (N, K), dtype=torch.int32)
+    scales = (torch.rand(K // g, N) * 0.02 + 0.005).bfloat16()
+    zeros = torch.randint(0, 16, (K // g, N)).float().bfloat16()
+    wd = ref.awq_dequant_ref(q, scales, zeros, g).to(DEV)
+    silu = N == 17920
+    lin = ops.Linear(None, awq={"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV), "group": g,
+                                "silu": silu})
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    nw = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+    xn, _ = ref.rmsnorm_ref(x, nw, 1e-6)
+    out = torch.empty(M, N // 2 if silu else N, device=DEV, dtype=torch.bfloat16)
+    ops.native().gemm(x, lin.wp, N, K, out, 2 if silu else 0, norm_w=nw, eps=1e-6, ws=ops.workspace(x.device),
+                      awq_scales=lin.scales, awq_zeros=lin.zeros, group=g, awq_szp=lin.szp,
+                      waves=4 if kernel == -2 else 0, ntb=kernel)
+    want = ref.silu_mul_linear_ref(xn, wd[: N // 2], wd[N // 2:]) if silu else ref.linear_ref(xn, wd)
+    assert _rel_err(out, want) < 2e-2
+
+
+@pytest.mark.parametrize("M", [40, 256])
+def test_awq_prefill_dequant_path(M):
+    """Long AWQ steps: int4 -> bf16 fragment-packed scratch (gamma folded) + the bf16 prefill /
+    tile kernels, for plain + residual, SiLU and norm; no library copy exists."""
+    torch.manual_seed(77 + M)
+    g, K = 128, 1536
+    for N, silu in ((1536, False), (2048, True)):
+        q = torch.randint(0, 16, (N, K), dtype=torch.int32)
+        scales = (torch.rand(K // g, N) * 0.02 + 0.005).bfloat16()
+        zeros = torch.randint(0, 16, (K // g, N)).float().bfloat16()
+        wd = ref.awq_dequant_ref(q, scales, zeros, g).to(DEV)
+        lin = ops.Linear(None, awq={"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV), "group": g,
+                                    "silu": silu})
+        assert lin.wl is None
+        x = torch.randn(M, K, device=DEV).bfloat16()
+        nw = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+        xn, _ = ref.rmsnorm_ref(x, nw, 1e-6)
+        if silu:
+            y = ops.linear(x, lin, norm=(nw, 1e-6))
+            assert _rel_err(y, ref.silu_mul_linear_ref(xn, wd[: N // 2], wd[N // 2:])) < 2e-2
+        else:
+            res = torch.randn(M, N, device=DEV).bfloat16()
+            y = ops.linear(x, lin, residual=res.clone(), norm=(nw, 1e-6))
+            assert _rel_err(y, ref.linear_ref(xn, wd, None, res)) < 2e-2
+
+
 @pytest.mark.parametrize("Hq,Hkv", [(12, 2), (32, 8), (64, 8)])
 def test_unified_attention_mixed_batch(Hq, Hkv):
     """decode rows (qlen 1, incl. split-K partitions) + prefill chunks in one launch."""

@@ -64,6 +64,8 @@ class ResultCache:
                     return None
                 self.hits += 1
                 CACHE_HITS.inc()
+                if logger.isEnabledFor(10):
+                    logger.debug("Cache hit", extra={"extra_data": {"cache_key": key[:8]}})
                 return json.loads(raw)
             async with self._lock:
                 val = self._data.get(key)
@@ -76,6 +78,8 @@ class ResultCache:
                 self.hits += 1
                 CACHE_HITS.inc()
                 span.set_attribute("hit", True)
+                if logger.isEnabledFor(10):  # DEBUG; the check keeps the hot path free of record building
+                    logger.debug("Cache hit", extra={"extra_data": {"cache_key": key[:8]}})
                 return copy.deepcopy(val)
 
     async def put(self, key: str, value: dict[str, Any]) -> None:

@@ -91,6 +91,11 @@ class DecoderModel:
             from vgate.models.weights import random_init
             random_init(self, seed)
         self.library_prefill = self._keep_library_copies()
+        if self.device.type == "cuda" and self.quant == "awq" and not self.library_prefill:
+            # long AWQ steps: int4 -> bf16 dequant of one matrix at a time into a shared scratch
+            # (ops.linear), sized once here so graph capture never allocates
+            lins = [lin for L in self.layers for lin in (L.qkv, L.o, L.gate_up, L.down)]
+            ops.reserve_awq_scratch(self.device, max(lin.N * lin.K for lin in lins if lin.kind == "awq"))
         if self.device.type == "cuda" and os.environ.get("VGATE_FOLD_NORM", "1") != "0":
             self.fold_norms()
         table_len = max(max_model_len, 16) + 1
@@ -107,9 +112,10 @@ class DecoderModel:
         """Plain weight copies for hipBLASLt prefill GEMMs (ops.linear, M >= 128) — a comparison
         mode only for bf16 weights: by default their long steps run the hand-written LDS-tiled
         MFMA kernel (csrc/kernels/gemm_prefill.hip) on the packed weights, no second copy kept.
-        VGATE_PREFILL_BLAS: "awq" (default) = copies for AWQ int4 layers only (their W4A16
-        kernels have no long-step path yet), "1" = every layer, "0" = none."""
-        mode = os.environ.get("VGATE_PREFILL_BLAS", "awq")
+        AWQ int4 layers keep no copy either: a long step dequantises one matrix at a time into a
+        shared scratch and runs the same prefill kernel (ops.linear). VGATE_PREFILL_BLAS: "0"
+        (default) = none, "awq" = copies for AWQ layers only, "1" = every layer."""
+        mode = os.environ.get("VGATE_PREFILL_BLAS", "0")
         if self.device.type != "cuda" or mode == "0" or (mode == "awq" and self.quant != "awq"):
             return False
         lins = [lin for L in self.layers for lin in (L.qkv, L.o, L.gate_up, L.down)]

@@ -103,6 +103,16 @@ def pack_awq(qint: torch.Tensor) -> torch.Tensor:
     return words.to(torch.int32).contiguous()
 
 
+def pack_awq_sz(scales: torch.Tensor, sz: torch.Tensor) -> torch.Tensor:
+    """Group scales in the AWQ decode kernel's fragment order (csrc/kernels/gemm.hip awq_dec_kernel):
+    [N/16][K/128][4 lane groups][s(4 cols), s*z(4 cols)] bf16, so the lanes of a 16-lane group load
+    their 4 columns' scale AND zero term with ONE 16-B load per (tile, k-quad). Group 128 only."""
+    G, N = scales.shape
+    s4 = scales.t().reshape(N // 16, 4, 4, G).permute(0, 3, 1, 2)  # [nt][g][lane group][4]
+    z4 = sz.t().reshape(N // 16, 4, 4, G).permute(0, 3, 1, 2)
+    return torch.cat([s4, z4], dim=-1).to(torch.bfloat16).contiguous()  # [nt][g][4][8]
+
+
 def row_permutation(N: int, layout: str) -> torch.Tensor | None:
     """Row order of the packed weight for a fused epilogue (None = identity).
 
@@ -167,6 +177,7 @@ class Linear:
                 self.wp = pack_awq(q)
                 self.scales = scales.to(torch.bfloat16).contiguous()
                 self.zeros = (scales.float() * zeros.float()).to(torch.bfloat16).contiguous()
+                self.szp = pack_awq_sz(self.scales, self.zeros) if self.group == 128 else None
                 self.w = None
             else:
                 self.w = ref.awq_dequant_ref(q, scales, zeros, self.group)
@@ -242,7 +253,8 @@ class Linear:
     def nbytes(self) -> int:
         """Bytes a decode step streams (the library copy is prefill-only)."""
         if self.kind == "awq" and self.w is None:
-            return self.wp.numel() * 4 + self.scales.numel() * 4
+            n = self.wp.numel() * 4 + self.scales.numel() * 4  # int4 + (s, s*z) bf16 per group
+            return n + (self.szp.numel() * 2 if getattr(self, "szp", None) is not None else 0)
         t = self.wp if self.wp is not None else self.w
         return t.numel() * t.element_size()
 
@@ -299,6 +311,8 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
         return _linear_library(x, lin, out, residual, norm, qkv)
     C = native()
     epi = 3 if qkv is not None else (2 if silu else (1 if out_f32 else 0))
+    if lin.kind == "awq" and M >= AWQ_DEQUANT_MIN_M and row_idx is None and waves == 0 and splitk == 0:
+        return _linear_awq_dequant(x, lin, out, residual, norm, qkv, epi, M)
     ntb = 0
     if M <= 16 and waves == 0 and splitk == 0:
         waves, splitk, ntb = lin.dec_waves, lin.dec_splitk, lin.dec_ntb
@@ -315,11 +329,42 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
                   k_cache=qkv["k_cache"], v_cache=qkv["v_cache"], hq=qkv["hq"], hkv=qkv["hkv"])
     if lin.kind == "awq":
         kw.update(awq_scales=lin.scales, awq_zeros=lin.zeros, group=lin.group)
+        if getattr(lin, "szp", None) is not None:
+            kw["awq_szp"] = lin.szp
     C.gemm(x, lin.wp, lin.N, lin.K, out, epi, **kw)
     return out
 
 
 LIBRARY_MIN_M = int(os.environ.get("VGATE_PREFILL_BLAS_MIN_M", "128"))
+# AWQ steps with at least this many rows run dequant-to-scratch + the bf16 prefill / tile kernels
+AWQ_DEQUANT_MIN_M = int(os.environ.get("VGATE_AWQ_DEQUANT_MIN_M", "32"))
+_AWQ_SCRATCH: dict = {}
+
+
+def reserve_awq_scratch(device, numel: int) -> torch.Tensor:
+    """The per-device bf16 scratch one dequantised AWQ matrix lives in during a long step."""
+    key = str(device)
+    t = _AWQ_SCRATCH.get(key)
+    if t is None or t.numel() < numel:
+        t = _AWQ_SCRATCH[key] = torch.empty(numel, dtype=torch.bfloat16, device=device)
+    return t
+
+
+def _linear_awq_dequant(x, lin: "Linear", out, residual, norm, qkv, epi, M):
+    """Long AWQ step: int4 -> bf16 fragment-packed scratch (RMSNorm gamma folded in), then the
+    bf16 kernels with the row-scale-only RMSNorm mode — same epilogues, no resident bf16 copy."""
+    C = native()
+    scratch = reserve_awq_scratch(x.device, lin.N * lin.K)[: lin.N * lin.K]
+    gamma = norm[0] if norm is not None else None
+    C.awq_dequant(lin.wp, lin.scales, lin.zeros, lin.N, lin.K, lin.group, scratch, gamma)
+    kw = dict(bias=lin.bias, res=residual, ws=workspace(x.device))
+    if norm is not None:
+        kw.update(rownorm=True, eps=float(norm[1]))
+    if qkv is not None:
+        kw.update(positions=qkv["positions"], slots=qkv["slots"], cos_sin=qkv["cos_sin"],
+                  k_cache=qkv["k_cache"], v_cache=qkv["v_cache"], hq=qkv["hq"], hkv=qkv["hkv"])
+    C.gemm(x, scratch, lin.N, lin.K, out, epi, **kw)
+    return out
 # the W4A16 kernels are decode kernels (no tile path above M = 16): hand AWQ steps to the
 # library copy earlier
 LIBRARY_MIN_M_AWQ = int(os.environ.get("VGATE_PREFILL_BLAS_MIN_M_AWQ", "32"))
@@ -504,6 +549,6 @@ def softmax_scale(head_dim: int) -> float:
 
 __all__ = [
     "native", "native_available", "pack_weight", "unpack_weight", "interleave_gate_up", "pack_awq",
-    "Linear", "linear", "attention", "workspace", "row_permutation", "rmsnorm", "embedding", "rope_kv", "attention_decode", "attention_prefill",
+    "Linear", "linear", "attention", "workspace", "row_permutation", "reserve_awq_scratch", "pack_awq_sz", "rmsnorm", "embedding", "rope_kv", "attention_decode", "attention_prefill",
     "prefill_tiles", "sample", "softmax_scale", "ref",
 ]
