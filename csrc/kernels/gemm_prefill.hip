@@ -20,6 +20,8 @@
 // (gamma folded into W at load time): x^2 is accumulated from the B fragments the MFMAs read.
 // Grid: 1-D, XCD-aware bijective remap, m-blocks fastest so the blocks that share a weight
 // column panel run back to back on one XCD (one HBM read of the panel per XCD L2).
+#include <cstdlib>
+
 #include "gemm_epilogue.h"
 
 namespace vgate {
@@ -167,6 +169,164 @@ __global__ __launch_bounds__(256, 2) void gemm_prefill_kernel(GemmParams p) {
   }
 }
 
+// ---- v2: deeper pipeline, bigger block tile ----
+// Same operand staging (LDS-DMA of fragment-major 1 KiB pieces, conflict-free ds_read_b128),
+// epilogues and split-K contract as gemm_prefill_kernel, but
+//   * an NS-deep stage ring: stage t + NS - 1 is issued before stage t is consumed, with ONE
+//     counted vmcnt wait + s_barrier per stage (no vmcnt(0): the NS-2 younger stages stay in
+//     flight). The 2-deep ring waited for the stage it had just issued every 64 k, so each
+//     stage paid a full L2 / HBM round trip (~0.5-1 us) against ~0.4 us of MFMA work;
+//   * WM x WN waves (8: 512 threads) on a BM x BN = 256 x 128 tile, wave tile 64 x 64: twice the
+//     MFMA work per staged byte of the 128 x 128 tile and one block per CU (144 KiB ring).
+// Past the last stage the ring keeps issuing (clamped duplicate loads into buffers that are never
+// read again), so every wait count is a compile-time constant.
+template <int BM, int BN, int WM, int WN, int NS, int EPI, int NORM, int NTB>
+__global__ __launch_bounds__(64 * WM * WN, 1) void gemm_prefill2_kernel(GemmParams p) {
+  constexpr int NW = WM * WN;
+  constexpr int KS = 2;                        // 32-deep k-steps per stage (BK = 64)
+  constexpr int WTN = BN / 16, XTM = BM / 16;  // 16-wide tiles per block
+  constexpr int NT = WTN / WN, MT = XTM / WM;  // per wave
+  constexpr int PIECES = (WTN + XTM) * KS;     // 1 KiB pieces per stage
+  static_assert(PIECES % NW == 0, "pieces split evenly over the waves");
+  constexpr int PPW = PIECES / NW;
+  constexpr int STAGE = PIECES * 1024;
+  static_assert(NT % NTB == 0 && NS >= 2 && NS <= 4, "tile groups / ring depth");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  TLScope tl_scope(p.dbg_ts);
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int KT = p.K >> 5;
+  const int nk_all = p.K >> 6;
+  const int z = blockIdx.y, nz = gridDim.y;
+  const int kst0 = (nk_all * z) / nz, nk = (nk_all * (z + 1)) / nz - kst0;
+  const int mblocks = (p.M + BM - 1) / BM;
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int m0 = (wgid % mblocks) * BM;
+  const int nt_blk = (wgid / mblocks) * WTN;
+  const char* src[PPW];
+  int step[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int f = wid * PPW + i;
+    if (f < WTN * KS) {
+      const int nt = nt_blk + f / KS, ks = f % KS;
+      src[i] = reinterpret_cast<const char*>(p.wp) + (((size_t)nt * KT + 2 * kst0 + ks) * 64 + lane) * 16;
+      step[i] = KS * 1024;
+    } else {
+      const int g = f - WTN * KS;
+      const int mt = g / KS, ks = g % KS;
+      int row = m0 + mt * 16 + (lane & 15);
+      row = row < p.M ? row : p.M - 1;
+      src[i] = reinterpret_cast<const char*>(p.x + (size_t)row * p.lda + kst0 * 64 + ks * 32 + 8 * (lane >> 4));
+      step[i] = 64 * 2;
+    }
+  }
+  const uint32_t lds0 = lds_addr_of(smem);
+  auto issue = [&](int stage, int buf) {
+    const int st = stage < nk ? stage : nk - 1;  // past the end: a clamped duplicate, never read
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int f = wid * PPW + i;
+      glds16(src[i] + (size_t)st * step[i], __builtin_amdgcn_readfirstlane(lds0 + buf * STAGE + f * 1024));
+    }
+  };
+  f32x4 acc[NT][MT];
+#pragma unroll
+  for (int a = 0; a < NT; ++a)
+#pragma unroll
+    for (int b = 0; b < MT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ss[MT];
+#pragma unroll
+  for (int b = 0; b < MT; ++b) ss[b] = 0.f;
+
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0) issue(s0, s0);
+  for (int t = 0; t < nk; ++t) {
+    // stage t landed (this wave's pieces; the NS-2 younger stages may still be in flight), then
+    // every wave's pieces (barrier) — which also retires the reads of the buffer refilled next
+    if constexpr (NS == 2) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (NS == 3) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(PPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * PPW) : "memory");
+    issue(t + NS - 1, (t + NS - 1) % NS);
+    const char* sb = smem + (t % NS) * STAGE;
+    // every fragment of the stage read up front (both k-steps): the second k-step's reads are in
+    // flight under the first one's MFMAs instead of exposing the LDS latency per k-step
+    uint4 wall[KS][NT], xall[KS][MT];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+      for (int a = 0; a < NT; ++a)
+        wall[ks][a] = *reinterpret_cast<const uint4*>(sb + ((wn * NT + a) * KS + ks) * 1024 + lane * 16);
+#pragma unroll
+      for (int b = 0; b < MT; ++b)
+        xall[ks][b] = *reinterpret_cast<const uint4*>(sb + (WTN * KS + (wm * MT + b) * KS + ks) * 1024 + lane * 16);
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const uint4 (&wa)[NT] = wall[ks];
+      const uint4 (&xb)[MT] = xall[ks];
+      if constexpr (NORM == 2) {
+#pragma unroll
+        for (int b = 0; b < MT; ++b) {
+          float f[8];
+          unpack8(xb[b], f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss[b] += f[j] * f[j];
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < NT; ++a)
+#pragma unroll
+        for (int b = 0; b < MT; ++b) acc[a][b] = mfma16(as_bf16x8(wa[a]), as_bf16x8(xb[b]), acc[a][b]);
+    }
+    // the next iteration's barrier orders these ds_reads before the buffer is refilled
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing duplicate DMAs
+  if (nz > 1) {
+    float* part = p.slabs + (size_t)z * p.M * p.N;
+    float* ssq = p.slabs + (size_t)nz * p.M * p.N + (size_t)z * p.M;
+#pragma unroll
+    for (int b = 0; b < MT; ++b) {
+      const int m = m0 + wm * (BM / WM) + b * 16 + (lane & 15);
+      if constexpr (NORM == 2) {
+        float s2 = ss[b];
+        s2 += xor16(s2);
+        s2 += xor32(s2);
+        if (wn == 0 && lane < 16 && m < p.M) ssq[m] = s2;
+      }
+      if (m < p.M) {
+#pragma unroll
+        for (int a = 0; a < NT; ++a) {
+          const int n = (nt_blk + wn * NT + a) * 16 + 4 * (lane >> 4);
+          *reinterpret_cast<f32x4*>(part + (size_t)m * p.N + n) = acc[a][b];
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int b = 0; b < MT; ++b) {
+    const int m = m0 + wm * (BM / WM) + b * 16 + (lane & 15);
+    float sc = 1.f;
+    if constexpr (NORM == 2) {
+      float s2 = ss[b];
+      s2 += xor16(s2);
+      s2 += xor32(s2);
+      sc = rsqrtf(s2 / (float)p.K + p.eps);
+    }
+#pragma unroll
+    for (int a = 0; a < NT; a += NTB) {
+      f32x4 v[NTB];
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) v[j] = acc[a + j][b] * sc;
+      epilogue<NTB, EPI, false>(p, v, m, nt_blk + wn * NT + a, 4 * (lane >> 4), EpiPre<NTB>{}, m < p.M);
+    }
+  }
+}
+
 // Split-K combine: one wave per (16 rows, NTB tiles): the slices' partials summed in slice
 // order, the row scale from the summed slice sums of squares, then the shared epilogue.
 template <int EPI, int NORM, int NTB>
@@ -196,6 +356,28 @@ __global__ __launch_bounds__(256) void prefill_reduce_kernel(GemmParams p, int n
     for (int j = 0; j < NTB; ++j) v[j] *= sc;
   }
   epilogue<NTB, EPI, false>(p, v, m, nt0, nsub, EpiPre<NTB>{}, m < p.M);
+}
+
+template <int EPI, int NORM, int NTB>
+static void launch_prefill2_cfg(const GemmParams& p, int nz, hipStream_t st) {
+  constexpr int BM = 256, BN = 128, WM = 4, WN = 2, NS = 3;
+  constexpr int STAGE = (BN / 16 + BM / 16) * 2 * 1024;
+  const int blocks = ((p.M + BM - 1) / BM) * (p.N / BN);
+  GemmParams q = p;
+  if (q.dbg_ts == nullptr) q.dbg_ts = tl_take("gemm_prefill2", blocks * nz);
+  auto kern = gemm_prefill2_kernel<BM, BN, WM, WN, NS, EPI, NORM, NTB>;
+  static bool attr = [&] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               NS * STAGE) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL(kern, dim3(blocks, nz), dim3(64 * WM * WN), NS * STAGE, st, q);
+  if (nz > 1) {
+    const int groups = ((p.M + 15) / 16) * (p.N / (16 * NTB));
+    GemmParams r = p;
+    r.dbg_ts = tl_take("prefill_reduce", (groups + 3) / 4);
+    hipLaunchKernelGGL((prefill_reduce_kernel<EPI, NORM, NTB>), dim3((groups + 3) / 4), dim3(256), 0, st, r, nz);
+  }
 }
 
 template <int BM, int BN, int EPI, int NORM, int NTB>
@@ -238,6 +420,18 @@ static bool launch_prefill_epi(const GemmParams& p, int force_bn, int force_sk, 
   while (nz > 1 && nk / nz < 4) --nz;
   const size_t need = ((size_t)nz * p.M * p.N + (size_t)nz * p.M) * 4;
   if (nz > 1 && (p.slabs == nullptr || need > slab_bytes)) nz = 1;
+  // v2 (256 x 128, 3-deep ring) when its grid still covers the chip without split-K
+  static const int v2_mode = [] { const char* e = getenv("VGATE_PREFILL_V2"); return e ? atoi(e) : 1; }();
+  const int blocks_v2 = ((p.M + 255) / 256) * (p.N % 128 == 0 ? p.N / 128 : 0);
+  if (v2_mode != 0 && force_bn == 0 && force_sk == 0 && blocks_v2 >= 200) {
+    launch_prefill2_cfg<EPI, NORM, NTB>(p, 1, st);
+    return true;
+  }
+  if (force_bn == 256) {  // forced (tests / sweeps), split-K as chosen above
+    if (p.N % 128 != 0) return false;
+    launch_prefill2_cfg<EPI, NORM, NTB>(p, nz, st);
+    return true;
+  }
   if (wide) launch_prefill_cfg<128, 128, EPI, NORM, NTB>(p, nz, st);
   else launch_prefill_cfg<128, 64, EPI, NORM, NTB>(p, nz, st);
   return true;

@@ -740,7 +740,7 @@ def test_awq_library_prefill_path(layout):
 
 
 @pytest.mark.parametrize("M", [128, 200, 1024, 4096])
-@pytest.mark.parametrize("bn,sk", [(0, 0), (64, 0), (128, 0), (64, 3)])
+@pytest.mark.parametrize("bn,sk", [(0, 0), (64, 0), (128, 0), (64, 3), (256, 0), (256, 2)])
 def test_prefill_lds_gemm_all_epilogues(M, bn, sk):
     """The LDS-tiled MFMA prefill kernel (gemm_prefill.hip, path=1) on the decode kernels'
     fragment-packed weights, against the fp32 references: plain + in-place residual,
