@@ -193,6 +193,35 @@ def test_attention_prefill_chunked(Hq, Hkv):
     assert _rel_err(out.view(T, Hq, D), r) < 2e-2
 
 
+@pytest.mark.parametrize("Hq,Hkv", [(12, 2), (32, 8)])
+@pytest.mark.parametrize("qlens,ctxs", [([2048], [2048]), ([4096], [4096]), ([1024, 2048], [3072, 2048])])
+def test_attention_prefill_long(Hq, Hkv, qlens, ctxs):
+    """Prefill attention at prompt lengths 2048 / 4096 (whole prompt in one step) and a chunked
+    prefill (1024 new queries against 2048 cached tokens) next to a fresh 2048 prompt, against
+    the fp32 reference."""
+    torch.manual_seed(71 + sum(qlens))
+    D = 128
+    S = len(qlens)
+    maxb = max(ctxs) // 16
+    nblk = S * maxb + 4
+    kc, vc = _make_cache(nblk, Hkv, seed=2)
+    bt = (torch.randperm(nblk)[: S * maxb]).reshape(S, maxb).int().to(DEV)
+    qs = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32, device=DEV)
+    T = int(qs[-1])
+    cl = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
+    stride = (Hq + 2 * Hkv) * D
+    qkv = torch.randn(T, stride, device=DEV).bfloat16()
+    ts, tq = ops.prefill_tiles(qlens)
+    ts = torch.tensor(ts, dtype=torch.int32, device=DEV)
+    tq = torch.tensor(tq, dtype=torch.int32, device=DEV)
+    out = torch.zeros(T, Hq * D, device=DEV).bfloat16()
+    scale = 1 / math.sqrt(D)
+    ops.attention_prefill(qkv, stride, kc, vc, bt, cl, qs, ts, tq, out, Hq, Hkv, scale)
+    q = qkv[:, : Hq * D].reshape(T, Hq, D)
+    r = ref.attention_ref(q, kc, vc, bt, cl, qs.cpu(), Hq, Hkv, scale)
+    assert _rel_err(out.view(T, Hq, D), r) < 2e-2
+
+
 def test_sample_greedy_and_topk1():
     torch.manual_seed(8)
     B, V = 6, 151936
