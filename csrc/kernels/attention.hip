@@ -16,8 +16,7 @@
 //            4-row x 16-col transposed gather delivers exactly that k-order.
 // The LDS image of V is XOR-swizzled on 8-B chunks (chunk ^= 4*(row&7)), which
 // makes the transposed reads conflict-free (cdna_hip_programming.md T10).
-#include "common.h"
-#include "launchers.h"
+#include "gemm_epilogue.h"
 
 namespace vgate {
 
@@ -168,6 +167,27 @@ __device__ __forceinline__ void load_k_regs(uint4 (&kf)[8], const bf16_t* kb0, c
 // 16 cols x 128 d = the same 8 KiB) | [nw][16][2] (m, l) | flag
 __host__ __device__ constexpr int dec_ml_off(int nw) { return nw * CHUNK * D_ * 2; }
 
+// Output stores. SC1: write-through (device-coherent) stores, for a consumer that reads the
+// result inside the same launch (attn_o_kernel: the o_proj blocks load it with sc1 loads)
+template <bool SC1>
+__device__ __forceinline__ void out_store16(bf16_t* base, size_t elem, uint4 v) {
+  if constexpr (SC1) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4, v), rsrc_of(base), (uint32_t)(elem * 2), 0, 16);
+  } else {
+    *reinterpret_cast<uint4*>(base + elem) = v;
+  }
+}
+template <bool SC1>
+__device__ __forceinline__ void out_store8(bf16_t* base, size_t elem, uint2 v) {
+  if constexpr (SC1) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, rsrc_of(base), (uint32_t)(elem * 2), 0, 16);
+  } else {
+    *reinterpret_cast<uint2*>(base + elem) = v;
+  }
+}
+
+template <bool SC1 = false>
 __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, int part, char* smem) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   ATTN_STAMP(0);
@@ -324,7 +344,7 @@ __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, in
       pk.y = pack_bf2(acc[2] * inv, acc[3] * inv);
       pk.z = pack_bf2(acc[4] * inv, acc[5] * inv);
       pk.w = pack_bf2(acc[6] * inv, acc[7] * inv);
-      *reinterpret_cast<uint4*>(a.out + (size_t)qbeg * a.out_stride + (size_t)hq * D_ + d0) = pk;
+      out_store16<SC1>(a.out, (size_t)qbeg * a.out_stride + (size_t)hq * D_ + d0, pk);
     }
     ATTN_STAMP(3);
     return;
@@ -368,11 +388,10 @@ __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, in
       r[0] += w * v[0]; r[1] += w * v[1]; r[2] += w * v[2]; r[3] += w * v[3];
     }
     const float iv = LL > 0.f ? 1.f / LL : 0.f;
-    bf16_t* op = a.out + (size_t)qbeg * a.out_stride + (size_t)hh * D_ + dd;
     uint2 pk;
     pk.x = pack_bf2(r[0] * iv, r[1] * iv);
     pk.y = pack_bf2(r[2] * iv, r[3] * iv);
-    *reinterpret_cast<uint2*>(op) = pk;
+    out_store8<SC1>(a.out, (size_t)qbeg * a.out_stride + (size_t)hh * D_ + dd, pk);
   }
 }
 
@@ -403,6 +422,7 @@ __global__ __launch_bounds__(128) void attn_decode_reduce_kernel(AttnArgs a) {
 // One block per (16-query tile, KV head); wave w < G owns query head h*G + w and
 // its 16 query columns; every wave walks the same KV chunks, V is staged once per
 // block into a double-buffered LDS image (one barrier per chunk).
+template <bool SC1 = false>
 __device__ __forceinline__ void prefill_body(const AttnArgs& a, int tile, int h, char* smem) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nthr = blockDim.x;
@@ -468,14 +488,14 @@ __device__ __forceinline__ void prefill_body(const AttnArgs& a, int tile, int h,
   l += __shfl_xor(l, 32, 64);
   if (!qok) return;
   const float inv = l > 0.f ? 1.f / l : 0.f;
-  bf16_t* op = a.out + (size_t)(qs + qi) * a.out_stride + (size_t)hq * D_;
+  const size_t orow = (size_t)(qs + qi) * a.out_stride + (size_t)hq * D_;
   const int g = lane >> 4;
 #pragma unroll
   for (int mt = 0; mt < 8; ++mt) {
     uint2 pk;
     pk.x = pack_bf2(o[mt][0] * inv, o[mt][1] * inv);
     pk.y = pack_bf2(o[mt][2] * inv, o[mt][3] * inv);
-    *reinterpret_cast<uint2*>(op + 16 * mt + 4 * g) = pk;
+    out_store8<SC1>(a.out, orow + 16 * mt + 4 * g, pk);
   }
 }
 
@@ -518,6 +538,142 @@ void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
     b.tl = tl_take("attn_reduce", dec_seqs * a.Hq);
     hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(dec_seqs, a.Hq), dim3(128), 0, st, b);
   }
+}
+
+// ------------------------------------------------- attention + o_proj in one launch ----
+// A decode step's o_proj streams 4.7-33 MB of weights that do not depend on the attention
+// output, yet as its own launch it starts only after the attention grid has drained (a kernel
+// boundary) and then pays its first HBM round trip. attn_o_kernel runs both as block roles of
+// ONE grid: blocks [0, nA) are the attention blocks of launch_attention (decode partitions +
+// prefill tiles, KV-head major), blocks [nA, nA + nO) are o_proj column tiles. An o_proj block
+// loads its whole weight k-range into registers and prefetches its residual words at launch —
+// overlapped with attention — then waits for the attention blocks' arrivals and finishes with
+// one round trip for the activations.
+//
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1 table):
+// every attention output byte is stored write-through (sc1, 16 / 8 B), each attention block's
+// waves drain their stores (vmcnt(0)) and meet at a barrier, then one lane adds 1 to
+// sync[0] (agent-scope atomic); one lane of each o_proj block polls sync[0] with sc1 loads
+// (s_sleep between polls, bounded), the block meets at a barrier and loads the activations
+// with sc1 loads only. The last o_proj block to finish (sync[32] ticket) zeroes both words,
+// so the counters are ready for the next launch (graph replays included). Producers never
+// wait on consumers and the host launches the fused form only when the whole grid is
+// co-resident (occupancy x CUs), so no dispatch order is assumed.
+constexpr int AO_SYNC_STRIDE = 32;  // sync words on separate 128-B lines
+
+template <int KMAX>
+__device__ __forceinline__ void oproj_tile(const GemmParams& p, int tile, uint32_t* sync, uint32_t nA, uint32_t nO,
+                                           char* smem) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int KT = p.K >> 5;
+  const int kbeg = (KT * wid) / nw, kend = (KT * (wid + 1)) / nw;  // host: kend - kbeg <= KMAX
+  const int r16 = lane & 15;
+  // 1) the wave's whole weight range in flight at launch (clamped duplicates past kend)
+  const uint4* wb = p.wp + (size_t)tile * KT * 64 + lane;
+  uint4 w[KMAX];
+#pragma unroll
+  for (int u = 0; u < KMAX; ++u) w[u] = ld_nt16(wb + (size_t)min(kbeg + u, kend - 1) * 64);
+  EpiPre<1> pre;
+  if (wid == 0) epi_pre_a<1, EPI_BF16>(p, pre, r16, tile, 4 * (lane >> 4));
+  // 2) wait for every attention block
+  if (threadIdx.x == 0) {
+    uint32_t spins = 0;
+    while (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nA) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 20)) break;  // bounded: never hang the GPU (the result is then wrong)
+    }
+  }
+  __syncthreads();
+  // 3) activations: rows r16 < M of this wave's k-range, device-coherent loads
+  const bool xok = r16 < p.M;
+  const uint32_t xoff = (uint32_t)(((size_t)r16 * p.lda + 8 * (lane >> 4)) * 2);
+  uint4 xa[KMAX];
+#pragma unroll
+  for (int u = 0; u < KMAX; ++u) {
+    const f32x4 v = ld_sc1_x4(reinterpret_cast<const float*>(p.x), xoff + (uint32_t)(min(kbeg + u, kend - 1) * 64));
+    xa[u] = (xok && kbeg + u < kend) ? __builtin_bit_cast(uint4, v) : make_uint4(0, 0, 0, 0);
+  }
+  f32x4 acc[1][1] = {{f32x4{0.f, 0.f, 0.f, 0.f}}};
+#pragma unroll
+  for (int u = 0; u < KMAX; ++u) acc[0][0] = mfma16(as_bf16x8(w[u]), as_bf16x8(xa[u]), acc[0][0]);
+  const float ssr[1] = {0.f};
+  gemm_finish<1, 1, EPI_BF16, 0, true>(p, acc, ssr, smem, 0, tile, pre);
+  // 4) the last o_proj block re-arms the counters for the next launch
+  if (threadIdx.x == 0) {
+    const uint32_t d = __hip_atomic_fetch_add(sync + AO_SYNC_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == nO - 1) {
+      __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sync + AO_SYNC_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(512) void attn_o_kernel(AttnArgs a, int dec_seqs, int dec_blocks, int nx, GemmParams p,
+                                                     uint32_t* sync, int nO) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  TLScope tl_scope(a.tl);
+  const int nA = nx * a.Hkv;
+  const int b = blockIdx.x;
+  if (b < nA) {
+    const int bx = b % nx, h = b / nx;
+    if (bx < dec_blocks) decode_block<true>(a, bx % dec_seqs, h, bx / dec_seqs, smem);
+    else prefill_body<true>(a, bx - dec_blocks, h, smem);
+    drain_stores();  // this wave's write-through output stores are device-visible
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  oproj_tile<KMAX>(p, b - nA, sync, (uint32_t)nA, (uint32_t)nO, smem);
+}
+
+static int cu_count() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    return v > 0 ? v : 1;
+  }();
+  return n;
+}
+
+template <int KMAX>
+static int ao_resident(int threads, size_t lds) {  // co-resident blocks of the fused grid (fixed launch shape)
+  static const int cap = [threads, lds] {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_o_kernel<KMAX>, threads, lds) != hipSuccess) return 0;
+    return n * cu_count();
+  }();
+  return cap;
+}
+
+bool launch_attention_o(const AttnArgs& a, int dec_seqs, const GemmArgs& g, uint32_t* sync, hipStream_t st) {
+  const int G = a.Hq / a.Hkv;
+  const int tiles = a.num_tiles > 0 ? a.num_tiles : 0;
+  const int dec_blocks = dec_seqs > 0 ? dec_seqs * a.num_parts : 0;
+  const int nx = dec_blocks + tiles;
+  if (sync == nullptr || g.M <= 0 || g.M > 16 || nx <= 0 || G > 8 || g.K % 32 != 0 || g.N % 16 != 0) return false;
+  if (dec_seqs > 0 && a.num_parts > 1 && a.tickets == nullptr) return false;  // needs the in-launch merge
+  if (g.epi != EPI_BF16 || g.row_idx != nullptr || g.norm_w != nullptr || g.rownorm) return false;
+  constexpr int NW = 8;
+  const int KT = g.K / 32;
+  const int per = (KT + NW - 1) / NW;
+  if (per > 16) return false;
+  const int nA = nx * a.Hkv, nO = g.N / 16;
+  const size_t lds = (size_t)(attn_lds_bytes(NW) > red_bytes<1, 1>(NW) + ssq_bytes<1>(NW) + 16
+                                  ? attn_lds_bytes(NW) : red_bytes<1, 1>(NW) + ssq_bytes<1>(NW) + 16);
+  const int cap = per <= 8 ? ao_resident<8>(64 * NW, lds) : ao_resident<16>(64 * NW, lds);
+  if (nA + nO > cap) return false;
+  GemmParams p{};
+  p.x = g.x; p.lda = g.lda; p.M = g.M; p.wp = reinterpret_cast<const uint4*>(g.wp); p.N = g.N; p.K = g.K;
+  p.bias = g.bias; p.res = g.res; p.ldr = g.ldr; p.out = g.out; p.ldo = g.ldo; p.splitk = 1;
+  AttnArgs b = a;
+  b.tl = tl_take("attn_o", nA + nO);
+  if (per <= 8)
+    hipLaunchKernelGGL(attn_o_kernel<8>, dim3(nA + nO), dim3(64 * NW), lds, st, b, dec_seqs, dec_blocks, nx, p, sync, nO);
+  else
+    hipLaunchKernelGGL(attn_o_kernel<16>, dim3(nA + nO), dim3(64 * NW), lds, st, b, dec_seqs, dec_blocks, nx, p, sync, nO);
+  return true;
 }
 
 void launch_attn_decode(const AttnArgs& a, hipStream_t st) {

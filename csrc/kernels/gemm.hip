@@ -45,151 +45,6 @@
 
 namespace vgate {
 
-// ---- cross-wave reduction, optional in-launch split-K combine, epilogue ----
-// Row scale of the deferred RMSNorm: the waves' partial sums of squares (LDS, fixed
-// summation order -> bit-reproducible) -> rsqrt(mean + eps).
-template <int MB>
-__device__ __forceinline__ float row_scale(const GemmParams& p, const float* ssqw, int r) {
-  const int nw = blockDim.x >> 6;
-  float ss = 0.f;
-  for (int w = 0; w < nw; ++w) ss += ssqw[w * 16 * MB + r];
-  return rsqrtf(ss / (float)p.K + p.eps);
-}
-
-// PRE: the epilogue thread of item s = threadIdx.x (MB == 1 decode: wave 0, one item each)
-// prefetched its operands at launch (EpiPre)
-template <int MB, int NTB, int EPI, int NORM, bool PRE>
-__device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB][NTB], const float (&ssr)[MB],
-                                            char* smem, int m_base, int nt0, const EpiPre<NTB> pre) {
-  static_assert(!PRE || MB == 1, "prefetched epilogue operands are a decode-kernel mode");
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  constexpr int SLOTS = MB * NTB * 64;  // f32x4 slots per block tile
-  f32x4* red4 = reinterpret_cast<f32x4*>(smem);
-  float* ssqw = reinterpret_cast<float*>(smem + red_bytes<MB, NTB>(nw));
-  int* flag = reinterpret_cast<int*>(smem + red_bytes<MB, NTB>(nw) + ssq_bytes<MB>(nw));
-  if constexpr (NORM) {
-    // lanes l, l^16, l^32, l^48 hold the same row: fold them, publish one value per row
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
-      float v = ssr[mb];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      if (lane < 16) ssqw[wid * 16 * MB + mb * 16 + lane] = v;
-    }
-    if (nw == 1) __syncthreads();
-  }
-  if (nw > 1) {
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-      for (int j = 0; j < NTB; ++j) red4[wid * SLOTS + (mb * NTB + j) * 64 + lane] = acc[mb][j];
-    __syncthreads();
-  }
-  const int tile = blockIdx.y * gridDim.x + blockIdx.x;
-  if (p.splitk > 1) {
-    // 1) this slice's partial tile -> fp32 slab [tile][slice][SLOTS]; under NORM also the
-    //    slice's per-row partial sum of squares -> [tile][slice][16*MB] after all slabs
-    //    (the row scale is applied to the summed tile: y = rsqrt(sum ss / K + eps) * sum acc)
-    const uint32_t slab_off = (uint32_t)(((size_t)tile * p.splitk + blockIdx.z) * SLOTS * 16);  // bytes
-    float* ssq_all = p.slabs + (size_t)gridDim.x * gridDim.y * p.splitk * SLOTS * 4;
-    if constexpr (NORM) {
-      if (threadIdx.x < 16 * MB) {
-        float ss = 0.f;
-        for (int w = 0; w < nw; ++w) ss += ssqw[w * 16 * MB + threadIdx.x];
-        st_sc1(ssq_all + ((size_t)tile * p.splitk + blockIdx.z) * 16 * MB + threadIdx.x, ss);
-      }
-    }
-    for (int s = threadIdx.x; s < SLOTS; s += blockDim.x) {
-      f32x4 t;
-      if (nw > 1) {
-        t = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int w = 0; w < nw; ++w) t += red4[w * SLOTS + s];
-      } else {
-        const int mb = s / (NTB * 64), j = (s / 64) % NTB;
-        t = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int a = 0; a < MB; ++a)
-#pragma unroll
-          for (int b = 0; b < NTB; ++b)
-            if (a == mb && b == j) t = acc[a][b];
-      }
-      st_sc1_x4(p.slabs, slab_off + (uint32_t)s * 16u, t);
-    }
-    // 2) publish: every wave drains its sc1 stores, then one ticket (no cache-wide fence)
-    drain_stores();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const uint32_t old = __hip_atomic_fetch_add(p.counters + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = (old == (uint32_t)(p.splitk - 1));
-      if (last) __hip_atomic_store(p.counters + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = last;
-    }
-    __syncthreads();
-    if (!*flag) return;
-    // 3) the last arriver sums every slice's slab (device-coherent 16-B sc1 loads). All
-    //    slices' loads are issued before the first is consumed (indices clamped, surplus
-    //    masked): a runtime-trip loop of dependent loads costs one memory round trip per slice.
-    const uint32_t all_off = (uint32_t)((size_t)tile * p.splitk * SLOTS * 16);
-    for (int s = threadIdx.x; s < MB * 64; s += blockDim.x) {
-      const int mb = s >> 6, l = s & 63;
-      const int m = m_base + mb * 16 + (l & 15);
-      f32x4 v[NTB];
-#pragma unroll
-      for (int j = 0; j < NTB; ++j) {
-        f32x4 r[SK_MAX];
-#pragma unroll
-        for (int z = 0; z < SK_MAX; ++z)
-          r[z] = ld_sc1_x4(p.slabs, all_off + (uint32_t)(((min(z, p.splitk - 1)) * SLOTS + (mb * NTB + j) * 64 + l) * 16));
-        f32x4 t = r[0];
-#pragma unroll
-        for (int z = 1; z < SK_MAX; ++z)
-          if (z < p.splitk) t += r[z];
-        v[j] = t;
-      }
-      if constexpr (NORM) {
-        float sv[SK_MAX];
-#pragma unroll
-        for (int z = 0; z < SK_MAX; ++z)
-          sv[z] = ld_sc1(ssq_all + ((size_t)tile * p.splitk + min(z, p.splitk - 1)) * 16 * MB + mb * 16 + (l & 15));
-        float ss = sv[0];  // fixed slice order: bit-reproducible
-#pragma unroll
-        for (int z = 1; z < SK_MAX; ++z)
-          if (z < p.splitk) ss += sv[z];
-        const float sc = rsqrtf(ss / (float)p.K + p.eps);
-#pragma unroll
-        for (int j = 0; j < NTB; ++j) v[j] *= sc;
-      }
-      epilogue<NTB, EPI, PRE>(p, v, m, nt0, 4 * (l >> 4), pre, m < p.M);
-    }
-    return;
-  }
-  for (int s = threadIdx.x; s < MB * 64; s += blockDim.x) {
-    const int mb = s >> 6, l = s & 63;
-    const int m = m_base + mb * 16 + (l & 15);
-    f32x4 v[NTB];
-    if (nw > 1) {
-#pragma unroll
-      for (int j = 0; j < NTB; ++j) {
-        f32x4 t = {0.f, 0.f, 0.f, 0.f};
-        for (int w = 0; w < nw; ++w) t += red4[w * SLOTS + (mb * NTB + j) * 64 + l];
-        v[j] = t;
-      }
-    } else {
-#pragma unroll
-      for (int mm = 0; mm < MB; ++mm)
-        if (mm == mb)
-#pragma unroll
-          for (int j = 0; j < NTB; ++j) v[j] = acc[mm][j];
-    }
-    if constexpr (NORM) {
-      const float sc = row_scale<MB>(p, ssqw, mb * 16 + (l & 15));
-#pragma unroll
-      for (int j = 0; j < NTB; ++j) v[j] *= sc;
-    }
-    epilogue<NTB, EPI, PRE>(p, v, m, nt0, 4 * (l >> 4), pre, m < p.M);
-  }
-}
-
 // Rotate a 16-B fragment across lanes within each 16-lane DPP row: lane r <- lane (r + S) % 16.
 template <int S>
 __device__ __forceinline__ uint4 row_ror(uint4 v) {

@@ -139,6 +139,11 @@ void launch_attn_prefill(const AttnArgs& a, hipStream_t st);
 // with a single query token do work) + prefill tiles (tile_seq < 0 = padding).
 void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st);
 
+// Decode attention + the o_proj GEMM (EPI_BF16, optional residual, M <= 16) as block roles of
+// one launch (attention.hip attn_o_kernel). sync: >= 64 zeroed, self-resetting uint32 words.
+// Returns false (nothing launched) when the shapes / grid do not fit the fused form.
+bool launch_attention_o(const AttnArgs& a, int dec_seqs, const GemmArgs& g, uint32_t* sync, hipStream_t st);
+
 struct SampleArgs {
   const float* logits;  // [B, V] f32, row stride ldl
   int ldl;

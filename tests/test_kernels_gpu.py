@@ -535,6 +535,62 @@ def test_unified_attention_mixed_batch(Hq, Hkv):
         assert _rel_err(out.view(T, Hq, D), r) < 2e-2
 
 
+@pytest.mark.parametrize("Hq,Hkv,N", [(12, 2, 1536), (32, 8, 1024), (8, 1, 2048), (64, 8, 512)])
+@pytest.mark.parametrize("qlens,ctxs", [([1] * 8, [40, 1, 700, 33, 1500, 64, 2, 129]),
+                                        ([1, 1, 3, 1, 5], [100, 513, 20, 9, 37]), ([1], [5])])
+@pytest.mark.parametrize("residual,bias", [(True, False), (False, True)])
+def test_attention_o_fused(Hq, Hkv, N, qlens, ctxs, residual, bias):
+    """attention + o_proj (+residual / bias) as one launch == the two-launch path == fp32
+    references; repeated launches exercise the self-resetting arrival counters."""
+    torch.manual_seed(21)
+    D, BS = 128, 16
+    S = len(qlens)
+    maxb = 128
+    nblk = S * maxb + 4
+    kc, vc = _make_cache(nblk, Hkv, seed=5)
+    bt = (torch.randperm(nblk)[: S * maxb]).reshape(S, maxb).int().to(DEV)
+    qs = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32, device=DEV)
+    T = int(qs[-1])
+    cl = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
+    q = torch.randn(T, Hq * D, device=DEV).bfloat16()
+    ts, tq = ops.prefill_tiles([ql if ql > 1 else 0 for ql in qlens])
+    ts = torch.tensor(ts + [-1], dtype=torch.int32, device=DEV)
+    tq = torch.tensor(tq + [0], dtype=torch.int32, device=DEV)
+    K = Hq * D
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device=DEV).bfloat16() if bias else None
+    lin = ops.Linear(w, bias=b)
+    resid0 = torch.randn(T, N, device=DEV).bfloat16()
+    scale = 1 / math.sqrt(D)
+    part = 512
+    P = (maxb * BS + part - 1) // part
+    po = torch.empty(S, Hq, P, D, device=DEV)
+    pml = torch.empty(S, Hq, P, 2, device=DEV)
+    a_ref = ref.attention_ref(q.view(T, Hq, D), kc, vc, bt, cl, qs.cpu(), Hq, Hkv, scale).reshape(T, K)
+    # two-launch path
+    out2 = torch.zeros(T, K, device=DEV).bfloat16()
+    y2 = resid0.clone()
+    ops.attention(q, K, kc, vc, bt, cl, qs, ts, tq, out2, po, pml, Hq, Hkv, part, scale)
+    ops.linear(out2, lin, out=y2, residual=y2 if residual else None)
+    for _ in range(3):
+        out = torch.zeros(T, K, device=DEV).bfloat16()
+        y = resid0.clone()
+        fused = ops.attention_o(q, K, kc, vc, bt, cl, qs, ts, tq, out, po, pml, Hq, Hkv, part, scale, lin, y,
+                                residual=residual, force=True)
+        if not fused:  # grid larger than the co-resident capacity: the caller's two launches run
+            # (decode grids of 8 KV heads x 8 sequences x 4 partitions, or K = 8192 deeper than
+            # one register group per wave)
+            assert Hkv == 8, "the Qwen-shaped decode steps must take the fused form"
+            return
+        assert _rel_err(out, a_ref) < 2e-2
+        # the fused grid runs attention with 8 waves per block (merge order differs from 6 waves)
+        assert _rel_err(out, out2) < 5e-3
+        y_ref = ref.linear_ref(out, w, b, resid0 if residual else None)
+        assert _rel_err(y, y_ref) < 1e-2
+        assert _rel_err(y, y2) < 5e-3
+    assert int(ops.attn_o_sync(DEV).abs().sum()) == 0  # counters re-armed
+
+
 @pytest.mark.parametrize("T", [5, 40])
 @pytest.mark.parametrize("waves", [1, 4, 16])
 def test_deferred_norm_all_wave_counts(T, waves):

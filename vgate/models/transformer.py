@@ -218,9 +218,17 @@ class DecoderModel:
             ops.linear(resid, L.qkv, out=q, norm=(L.in_norm, eps),
                        qkv=dict(positions=sv.positions, slots=sv.slots, cos_sin=self.cos_sin, k_cache=kc,
                                 v_cache=vc, hq=sh.hq, hkv=sh.hkv))
-            ops.attention(q, sh.hq * D, kc, vc, sv.block_tables, sv.context_lens, sv.query_start, sv.tile_seq,
-                          sv.tile_q0, attn, part_o, part_ml, sh.hq, sh.hkv, part_size, self.scale)
-            self._row_parallel(attn, L.o, resid, first)
+            # attention and o_proj (+ residual) as one launch when VGATE_FUSE_ATTN_O=1 (decode-sized
+            # steps; measured slower, off by default: ops.attention_o); otherwise two launches
+            if ops.attention_o(q, sh.hq * D, kc, vc, sv.block_tables, sv.context_lens, sv.query_start, sv.tile_seq,
+                               sv.tile_q0, attn, part_o, part_ml, sh.hq, sh.hkv, part_size, self.scale, L.o, resid,
+                               residual=first):
+                if tp.size > 1:
+                    tp.all_reduce(resid)
+            else:
+                ops.attention(q, sh.hq * D, kc, vc, sv.block_tables, sv.context_lens, sv.query_start, sv.tile_seq,
+                              sv.tile_q0, attn, part_o, part_ml, sh.hq, sh.hkv, part_size, self.scale)
+                self._row_parallel(attn, L.o, resid, first)
             ops.linear(resid, L.gate_up, out=mlp, norm=(L.post_norm, eps))
             self._row_parallel(mlp, L.down, resid, first)
         if return_hidden:

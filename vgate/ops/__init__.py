@@ -423,6 +423,42 @@ def attention(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_s
     return out
 
 
+def attention_o(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start, tile_seq, tile_q0, out,
+                part_o, part_ml, Hq: int, Hkv: int, part_size: int, scale: float, lin: "Linear", y: torch.Tensor,
+                residual: bool, force: bool = False) -> bool:
+    """attention(...) then ``y = out @ W_o^T (+ y if residual)`` as ONE launch (decode-sized steps):
+    the o_proj blocks stream their weights while the attention blocks run and take the attention
+    output over an in-launch hand-off (csrc/kernels/attention.hip attn_o_kernel). Returns False
+    and launches nothing when the fused form does not apply (GPU only; the caller then runs
+    :func:`attention` and :func:`linear`).
+
+    Off by default (VGATE_FUSE_ATTN_O=1 or ``force`` enables it): measured on the MI355X, the
+    fused launch is SLOWER than the two launches (Qwen2.5-1.5B decode, batch 8: 13.5 vs 11.8 us
+    per layer, profiles/r2_attn_o_fusion_negative.log) — the o_proj weight burst delays the
+    latency-bound attention blocks by 2-3 us and the flag hand-off plus the activation round trip
+    after the last attention block (~4 us) costs as much as the kernel boundary it replaces."""
+    if not _gpu(q) or lin.kind != "dense" or lin.wp is None or out.shape[0] > 16:
+        return False
+    if not force and os.environ.get("VGATE_FUSE_ATTN_O", "0") != "1":
+        return False
+    return bool(native().attention_o(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start, tile_seq,
+                                     tile_q0, out, part_o, part_ml, Hq, Hkv, part_size, scale,
+                                     attn_tickets(q.device), lin.wp, lin.N, lin.K, y, y if residual else None,
+                                     lin.bias, attn_o_sync(q.device)))
+
+
+_AO_SYNC: dict = {}
+
+
+def attn_o_sync(device) -> torch.Tensor:
+    """Self-resetting arrival counters of the fused attention + o_proj launch (zeroed once)."""
+    key = str(device)
+    t = _AO_SYNC.get(key)
+    if t is None:
+        t = _AO_SYNC[key] = torch.zeros(64, dtype=torch.int32, device=device)
+    return t
+
+
 _TICKETS: dict = {}
 
 
@@ -520,6 +556,7 @@ def attention_prefill(q, q_stride, k_cache, v_cache, block_tables, context_lens,
 
 def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, offsets=None,
            out=None, out_logprob=None, generators=None):
+    """Temperature / top-k / top-p sampling per row (csrc/kernels/sampling.hip)."""
     B = logits.shape[0]
     if out is None:
         out = torch.empty(B, dtype=torch.int32, device=logits.device)
@@ -549,6 +586,6 @@ def softmax_scale(head_dim: int) -> float:
 
 __all__ = [
     "native", "native_available", "pack_weight", "unpack_weight", "interleave_gate_up", "pack_awq",
-    "Linear", "linear", "attention", "workspace", "row_permutation", "reserve_awq_scratch", "pack_awq_sz", "rmsnorm", "embedding", "rope_kv", "attention_decode", "attention_prefill",
+    "Linear", "linear", "attention", "attention_o", "workspace", "row_permutation", "reserve_awq_scratch", "pack_awq_sz", "rmsnorm", "embedding", "rope_kv", "attention_decode", "attention_prefill",
     "prefill_tiles", "sample", "softmax_scale", "ref",
 ]
