@@ -66,6 +66,26 @@ def main():
     rnd = torch.randn(B, V, device=dev) * 2
     res["randn2_T0.7_top_p0.9"] = round(graph_time(lambda: orig(rnd, temp, topp, topk, seeds, offs, out=out)), 2)
     print(json.dumps({"sampler_probe": stats, "sampler_us": res}), flush=True)
+    # segments per row (B * nseg blocks): more segments = less sweep work per block, more arrivals
+    # per meeting
+    C = ops.native()
+    for cap in (16, 32, 64, 128):
+        C.set_sample_nseg(cap)
+        r = {"nseg": C.sample_segments(B, V)}
+        for name, t, tp in (("T0.7_top_p0.9", temp, topp), ("greedy", torch.zeros_like(temp), topp)):
+            r[name] = round(graph_time(lambda: orig(logits, t, tp, topk, seeds, offs, out=out)), 2)
+        print(json.dumps({"nseg_cap": cap, **r}), flush=True)
+    C.set_sample_nseg(64)
+    # pass kernels (pass 0 + R rejection rounds as launches, last-arriver merges) vs the in-launch
+    # meetings only (-1)
+    for rl in (-1, 0, 1, 2, 3):
+        C.set_sample_round_launches(rl)
+        r = {"round_launches": rl}
+        for name, t, tp in (("T0.7_top_p0.9", temp, topp), ("T0.7", temp, torch.ones_like(topp)),
+                            ("greedy", torch.zeros_like(temp), topp)):
+            r[name] = round(graph_time(lambda: orig(logits, t, tp, topk, seeds, offs, out=out)), 2)
+        print(json.dumps(r), flush=True)
+    C.set_sample_round_launches(2)
 
 
 if __name__ == "__main__":

@@ -180,7 +180,10 @@ __global__ __launch_bounds__(256, 2) void gemm_prefill_kernel(GemmParams p) {
 //     MFMA work per staged byte of the 128 x 128 tile and one block per CU (144 KiB ring).
 // Past the last stage the ring keeps issuing (clamped duplicate loads into buffers that are never
 // read again), so every wait count is a compile-time constant.
-template <int BM, int BN, int WM, int WN, int NS, int EPI, int NORM, int NTB>
+// SCHED (k-loop schedule): 0 = the stage's DMA issued before its reads + MFMAs; 1 = + MFMAs at raised
+// wave priority (s_setprio 1: the MFMA-issuing wave wins the SIMD's arbitration over the other wave's
+// LDS reads / DMA issue); 2 = 1 + the stage's DMA issue split in two, half in front of each k-step
+template <int BM, int BN, int WM, int WN, int NS, int EPI, int NORM, int NTB, int SCHED = 0>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_prefill2_kernel(GemmParams p) {
   constexpr int NW = WM * WN;
   constexpr int KS = 2;                        // 32-deep k-steps per stage (BK = 64)
@@ -224,14 +227,16 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_prefill2_kernel(GemmPara
     }
   }
   const uint32_t lds0 = lds_addr_of(smem);
-  auto issue = [&](int stage, int buf) {
+  auto issue_part = [&](int stage, int buf, int i0, int i1) {
     const int st = stage < nk ? stage : nk - 1;  // past the end: a clamped duplicate, never read
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
+      if (i < i0 || i >= i1) continue;  // compile-time after unrolling
       const int f = wid * PPW + i;
       glds16(src[i] + (size_t)st * step[i], __builtin_amdgcn_readfirstlane(lds0 + buf * STAGE + f * 1024));
     }
   };
+  auto issue = [&](int stage, int buf) { issue_part(stage, buf, 0, PPW); };
   f32x4 acc[NT][MT];
 #pragma unroll
   for (int a = 0; a < NT; ++a)
@@ -249,7 +254,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_prefill2_kernel(GemmPara
     if constexpr (NS == 2) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     else if constexpr (NS == 3) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(PPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * PPW) : "memory");
-    issue(t + NS - 1, (t + NS - 1) % NS);
+    if constexpr (SCHED < 2) issue(t + NS - 1, (t + NS - 1) % NS);
+    else issue_part(t + NS - 1, (t + NS - 1) % NS, 0, PPW / 2);
     const char* sb = smem + (t % NS) * STAGE;
     // every fragment of the stage read up front (both k-steps): the second k-step's reads are in
     // flight under the first one's MFMAs instead of exposing the LDS latency per k-step
@@ -276,10 +282,14 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_prefill2_kernel(GemmPara
           for (int j = 0; j < 8; ++j) ss[b] += f[j] * f[j];
         }
       }
+      if constexpr (SCHED == 2)
+        if (ks == 1) issue_part(t + NS - 1, (t + NS - 1) % NS, PPW / 2, PPW);
+      if constexpr (SCHED >= 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int a = 0; a < NT; ++a)
 #pragma unroll
         for (int b = 0; b < MT; ++b) acc[a][b] = mfma16(as_bf16x8(wa[a]), as_bf16x8(xb[b]), acc[a][b]);
+      if constexpr (SCHED >= 1) __builtin_amdgcn_s_setprio(0);
     }
     // the next iteration's barrier orders these ds_reads before the buffer is refilled
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -327,6 +337,209 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_prefill2_kernel(GemmPara
   }
 }
 
+// ---- v4: 256 x 256 tile in four phases per K-tile ----
+// 8 waves, wave (wr = wid >> 2, wc = wid & 3) owns n-tiles 8 wr .. 8 wr + 7 (two halves n0 / n1 of 4)
+// x m-tiles 4 wc .. 4 wc + 3 (halves m0 / m1 of 2). A K-tile (BK = 64, 64 KiB: 16 W + 16 x tiles x
+// 2 k-steps) is consumed in four phases, one 64 x 32 output quadrant x K = 64 (16 MFMAs) each, in
+// the order (n0, m0) (n0, m1) (n1, m1) (n1, m0): phase 0 first needs W n0 + x m0, phase 1 x m1,
+// phase 2 W n1, phase 3 nothing new (x m0 kept in registers). The next K-tile's LDS-DMA is issued
+// in the same three groups, group g in phase g (into the other buffer, free since the previous
+// K-tile's phase-0 barrier), so every piece has a whole K-tile (four phases) to land and each
+// phase waits with a compile-time counted vmcnt (pieces issued after its group) + raw s_barrier —
+// never vmcnt(0) in the loop (cdna_hip_programming.md §5 'The 256² 8-phase template').
+// Group sizes per wave: 4 / 2 / 2 pieces -> the waits of phases 0 / 1 / 2: vmcnt(4) / (6) / (6).
+// BN = 128: the same schedule on a 256 x 128 tile (wave 64 n x 64 m, 8 MFMAs per phase, 96 KiB;
+// groups 3 / 2 / 1 pieces per wave -> vmcnt(3) / (4) / (5)).
+template <int BN, int EPI, int NORM, int NTB>
+__global__ __launch_bounds__(512, 1) void gemm_prefill4_kernel(GemmParams p) {
+  constexpr int BM = 256, KS = 2;
+  constexpr int WTN = BN / 16, XTM = BM / 16;  // W + x tiles per block (16 / 8 + 16)
+  constexpr int NWN = WTN / 2, NH = NWN / 2;   // n-tiles per wave, per n-half
+  constexpr int STAGE = (WTN + XTM) * KS * 1024;
+  constexpr int G0 = 4 * NH + 16, G1 = 16, G2 = 4 * NH;  // pieces per group (block)
+  constexpr int P0 = G0 / 8, P1 = G1 / 8, P2 = G2 / 8;  // per wave
+  constexpr int PPW = P0 + P1 + P2;
+  static_assert(G0 % 8 == 0 && G2 % 8 == 0 && (BN == 256 || BN == 128), "pieces split over 8 waves");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  TLScope tl_scope(p.dbg_ts);
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int KT = p.K >> 5;
+  const int nk_all = p.K >> 6;
+  const int z = blockIdx.y, nz = gridDim.y;
+  const int kst0 = (nk_all * z) / nz, nk = (nk_all * (z + 1)) / nz - kst0;
+  const int mblocks = (p.M + BM - 1) / BM;
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int m0 = (wgid % mblocks) * BM;
+  const int nt_blk = (wgid / mblocks) * WTN;
+  // this wave's pieces: entries of the group lists (block-local tile, k-step; W or x)
+  //   group 0: the n0 W tiles of both wave rows, then x tiles {4c, 4c + 1}, x 2 k-steps
+  //   group 1: x tiles {4c + 2, 4c + 3} x 2
+  //   group 2: the n1 W tiles x 2
+  const char* src[PPW];
+  int step[PPW];
+  uint32_t dst[PPW];
+  const uint32_t lds0 = lds_addr_of(smem);
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    int e, isw, t;
+    if (i < P0) {
+      e = wid * P0 + i;
+      if (e < 4 * NH) {
+        isw = 1;
+        const int tw = e >> 1;
+        t = (tw / NH) * NWN + tw % NH;
+      } else {
+        isw = 0;
+        const int tile8 = (e - 4 * NH) >> 1;
+        t = 4 * (tile8 >> 1) + (tile8 & 1);
+      }
+    } else if (i < P0 + P1) {
+      e = wid * P1 + (i - P0);
+      isw = 0;
+      const int tile8 = e >> 1;
+      t = 4 * (tile8 >> 1) + 2 + (tile8 & 1);
+    } else {
+      e = wid * P2 + (i - P0 - P1);
+      isw = 1;
+      const int tw = e >> 1;
+      t = (tw / NH) * NWN + NH + tw % NH;
+    }
+    const int ks = e & 1;
+    if (isw) {
+      src[i] = reinterpret_cast<const char*>(p.wp) + (((size_t)(nt_blk + t) * KT + 2 * kst0 + ks) * 64 + lane) * 16;
+      step[i] = KS * 1024;
+      dst[i] = (uint32_t)((t * KS + ks) * 1024);
+    } else {
+      int row = m0 + t * 16 + (lane & 15);
+      row = row < p.M ? row : p.M - 1;
+      src[i] = reinterpret_cast<const char*>(p.x + (size_t)row * p.lda + kst0 * 64 + ks * 32 + 8 * (lane >> 4));
+      step[i] = 64 * 2;
+      dst[i] = (uint32_t)((WTN * KS + t * KS + ks) * 1024);
+    }
+  }
+  auto issue_group = [&](int g, int stage, int buf) {
+    const int st = stage < nk ? stage : nk - 1;  // past the end: clamped duplicates, never read
+    const int i0 = g == 0 ? 0 : g == 1 ? P0 : P0 + P1, i1 = g == 0 ? P0 : g == 1 ? P0 + P1 : PPW;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      if (i < i0 || i >= i1) continue;
+      glds16(src[i] + (size_t)st * step[i], __builtin_amdgcn_readfirstlane(lds0 + buf * STAGE + dst[i]));
+    }
+  };
+  f32x4 acc[NWN][4];
+#pragma unroll
+  for (int a = 0; a < NWN; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ss[4] = {0.f, 0.f, 0.f, 0.f};
+  uint4 wf[KS][NH], x0[KS][2], x1[KS][2];
+  auto read_w = [&](const char* sb, int half) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int a = 0; a < NH; ++a)
+        wf[ks][a] = *reinterpret_cast<const uint4*>(sb + ((wr * NWN + half * NH + a) * KS + ks) * 1024 + lane * 16);
+  };
+  auto read_x = [&](const char* sb, int half, uint4 (&xf)[KS][2]) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        xf[ks][b] = *reinterpret_cast<const uint4*>(sb + (WTN * KS + (wc * 4 + half * 2 + b) * KS + ks) * 1024 + lane * 16);
+    if constexpr (NORM == 2) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          float f[8];
+          unpack8(xf[ks][b], f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss[half * 2 + b] += f[j] * f[j];
+        }
+    }
+  };
+  auto quadrant = [&](int nh, int mh, const uint4 (&xf)[KS][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int a = 0; a < NH; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[nh * NH + a][mh * 2 + b] = mfma16(as_bf16x8(wf[ks][a]), as_bf16x8(xf[ks][b]), acc[nh * NH + a][mh * 2 + b]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  issue_group(0, 0, 0);
+  issue_group(1, 0, 0);
+  issue_group(2, 0, 0);
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    const char* sb = smem + buf * STAGE;
+    // phase 0: (n0, m0) — group 0 of this K-tile (groups 1, 2 issued after it)
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(P1 + P2) : "memory");
+    read_w(sb, 0);
+    read_x(sb, 0, x0);
+    issue_group(0, t + 1, buf ^ 1);
+    quadrant(0, 0, x0);
+    // phase 1: (n0, m1) — group 1 (issued after it: group 2 of this tile, group 0 of the next)
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(P2 + P0) : "memory");
+    read_x(sb, 1, x1);
+    issue_group(1, t + 1, buf ^ 1);
+    quadrant(0, 1, x1);
+    // phase 2: (n1, m1) — group 2 (issued after it: groups 0, 1 of the next tile)
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(P0 + P1) : "memory");
+    read_w(sb, 1);
+    issue_group(2, t + 1, buf ^ 1);
+    quadrant(1, 1, x1);
+    // phase 3: (n1, m0) from registers
+    quadrant(1, 0, x0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing duplicate DMAs
+  if (nz > 1) {
+    float* part = p.slabs + (size_t)z * p.M * p.N;
+    float* ssq = p.slabs + (size_t)nz * p.M * p.N + (size_t)z * p.M;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int m = m0 + wc * 64 + b * 16 + (lane & 15);
+      if constexpr (NORM == 2) {
+        float s2 = ss[b];
+        s2 += xor16(s2);
+        s2 += xor32(s2);
+        if (wr == 0 && lane < 16 && m < p.M) ssq[m] = s2;
+      }
+      if (m < p.M) {
+#pragma unroll
+        for (int a = 0; a < NWN; ++a) {
+          const int n = (nt_blk + wr * NWN + a) * 16 + 4 * (lane >> 4);
+          *reinterpret_cast<f32x4*>(part + (size_t)m * p.N + n) = acc[a][b];
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int m = m0 + wc * 64 + b * 16 + (lane & 15);
+    float sc = 1.f;
+    if constexpr (NORM == 2) {
+      float s2 = ss[b];
+      s2 += xor16(s2);
+      s2 += xor32(s2);
+      sc = rsqrtf(s2 / (float)p.K + p.eps);
+    }
+#pragma unroll
+    for (int a = 0; a < NWN; a += NTB) {
+      f32x4 v[NTB];
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) v[j] = acc[a + j][b] * sc;
+      epilogue<NTB, EPI, false>(p, v, m, nt_blk + wr * NWN + a, 4 * (lane >> 4), EpiPre<NTB>{}, m < p.M);
+    }
+  }
+}
+
 // Split-K combine: one wave per (16 rows, NTB tiles): the slices' partials summed in slice
 // order, the row scale from the summed slice sums of squares, then the shared epilogue.
 template <int EPI, int NORM, int NTB>
@@ -358,20 +571,50 @@ __global__ __launch_bounds__(256) void prefill_reduce_kernel(GemmParams p, int n
   epilogue<NTB, EPI, false>(p, v, m, nt0, nsub, EpiPre<NTB>{}, m < p.M);
 }
 
-template <int EPI, int NORM, int NTB>
-static void launch_prefill2_cfg(const GemmParams& p, int nz, hipStream_t st) {
-  constexpr int BM = 256, BN = 128, WM = 4, WN = 2, NS = 3;
+template <int EPI, int NORM, int NTB, int BM = 256, int BN = 128, int WM = 4, int WN = 2, int NS = 3, int SCHED = 0>
+static void launch_prefill2_one(const GemmParams& p, int nz, hipStream_t st) {
   constexpr int STAGE = (BN / 16 + BM / 16) * 2 * 1024;
   const int blocks = ((p.M + BM - 1) / BM) * (p.N / BN);
   GemmParams q = p;
   if (q.dbg_ts == nullptr) q.dbg_ts = tl_take("gemm_prefill2", blocks * nz);
-  auto kern = gemm_prefill2_kernel<BM, BN, WM, WN, NS, EPI, NORM, NTB>;
+  auto kern = gemm_prefill2_kernel<BM, BN, WM, WN, NS, EPI, NORM, NTB, SCHED>;
   static bool attr = [&] {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                NS * STAGE) == hipSuccess;
   }();
   (void)attr;
   hipLaunchKernelGGL(kern, dim3(blocks, nz), dim3(64 * WM * WN), NS * STAGE, st, q);
+  if (nz > 1) {
+    const int groups = ((p.M + 15) / 16) * (p.N / (16 * NTB));
+    GemmParams r = p;
+    r.dbg_ts = tl_take("prefill_reduce", (groups + 3) / 4);
+    hipLaunchKernelGGL((prefill_reduce_kernel<EPI, NORM, NTB>), dim3((groups + 3) / 4), dim3(256), 0, st, r, nz);
+  }
+}
+
+template <int EPI, int NORM, int NTB, int BM = 256, int BN = 128, int WM = 4, int WN = 2, int NS = 3>
+static void launch_prefill2_cfg(const GemmParams& p, int nz, hipStream_t st) {
+  // measured (profiles/r2_prefill_gemm_sched.log): MFMAs at raised priority +5-7 % on the 256 x 256
+  // tile, neutral on 256 x 128; the split DMA issue neutral to negative
+  static const int sched = [] { const char* e = getenv("VGATE_PREFILL_SCHED"); return e ? atoi(e) : 1; }();
+  if (sched == 1) launch_prefill2_one<EPI, NORM, NTB, BM, BN, WM, WN, NS, 1>(p, nz, st);
+  else if (sched == 2) launch_prefill2_one<EPI, NORM, NTB, BM, BN, WM, WN, NS, 2>(p, nz, st);
+  else launch_prefill2_one<EPI, NORM, NTB, BM, BN, WM, WN, NS, 0>(p, nz, st);
+}
+
+template <int EPI, int NORM, int NTB, int BN = 256>
+static void launch_prefill4_cfg(const GemmParams& p, int nz, hipStream_t st) {
+  constexpr int STAGE = (BN / 16 + 16) * 2 * 1024;
+  const int blocks = ((p.M + 255) / 256) * (p.N / BN);
+  GemmParams q = p;
+  if (q.dbg_ts == nullptr) q.dbg_ts = tl_take("gemm_prefill4", blocks * nz);
+  auto kern = gemm_prefill4_kernel<BN, EPI, NORM, NTB>;
+  static bool attr = [&] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               2 * STAGE) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL(kern, dim3(blocks, nz), dim3(512), 2 * STAGE, st, q);
   if (nz > 1) {
     const int groups = ((p.M + 15) / 16) * (p.N / (16 * NTB));
     GemmParams r = p;
@@ -420,16 +663,44 @@ static bool launch_prefill_epi(const GemmParams& p, int force_bn, int force_sk, 
   while (nz > 1 && nk / nz < 4) --nz;
   const size_t need = ((size_t)nz * p.M * p.N + (size_t)nz * p.M) * 4;
   if (nz > 1 && (p.slabs == nullptr || need > slab_bytes)) nz = 1;
-  // v2 (256 x 128, 3-deep ring) when its grid still covers the chip without split-K
+  // 256 x 256 when its grid covers ~3/4 of the chip, else v2 (256 x 128, 3-deep ring)
+  // when its grid still covers the chip without split-K (profiles/r2_prefill_gemm_sched.log: the
+  // 256-square tile +20-35 % at >= 192 blocks, up to -30 % at 128)
   static const int v2_mode = [] { const char* e = getenv("VGATE_PREFILL_V2"); return e ? atoi(e) : 1; }();
+  const int blocks_v3 = ((p.M + 255) / 256) * (p.N % 256 == 0 ? p.N / 256 : 0);
   const int blocks_v2 = ((p.M + 255) / 256) * (p.N % 128 == 0 ? p.N / 128 : 0);
-  if (v2_mode != 0 && force_bn == 0 && force_sk == 0 && blocks_v2 >= 200) {
-    launch_prefill2_cfg<EPI, NORM, NTB>(p, 1, st);
+  if (v2_mode != 0 && force_bn == 0 && force_sk == 0 && blocks_v3 >= 180) {
+    // the 4-phase 256 x 256 kernel (v4: +7-22 % over the same tile with one barrier per K-tile,
+    // profiles/r2_prefill_gemm_v4.log); VGATE_PREFILL_V2=3 keeps the one-barrier tile
+    if (v2_mode == 3) launch_prefill2_cfg<EPI, NORM, NTB, 256, 256, 4, 2, 2>(p, 1, st);
+    else launch_prefill4_cfg<EPI, NORM, NTB>(p, 1, st);
+    return true;
+  }
+  if (v2_mode != 0 && force_bn == 0 && force_sk == 0 && blocks_v2 >= 192) {
+    // the 4-phase kernel on 256 x 128 (+0-8 % over the 3-deep-ring v2 at 192-256 blocks,
+    // profiles/r2_prefill_gemm_v4.log); VGATE_PREFILL_V2=3 keeps v2
+    if (v2_mode == 3) launch_prefill2_cfg<EPI, NORM, NTB>(p, 1, st);
+    else launch_prefill4_cfg<EPI, NORM, NTB, 128>(p, 1, st);
     return true;
   }
   if (force_bn == 256) {  // forced (tests / sweeps), split-K as chosen above
     if (p.N % 128 != 0) return false;
     launch_prefill2_cfg<EPI, NORM, NTB>(p, nz, st);
+    return true;
+  }
+  if (force_bn == 512) {  // 256 x 256 block tile, 8 waves of 64 (m) x 128 (n), 2-deep ring (sweeps)
+    if (p.N % 256 != 0) return false;
+    launch_prefill2_cfg<EPI, NORM, NTB, 256, 256, 4, 2, 2>(p, nz, st);
+    return true;
+  }
+  if (force_bn == 1024) {  // v4: the 4-phase 256 x 256 kernel (sweeps / tests)
+    if (p.N % 256 != 0) return false;
+    launch_prefill4_cfg<EPI, NORM, NTB>(p, nz, st);
+    return true;
+  }
+  if (force_bn == 768) {  // v4 on a 256 x 128 tile (sweeps / tests)
+    if (p.N % 128 != 0) return false;
+    launch_prefill4_cfg<EPI, NORM, NTB, 128>(p, nz, st);
     return true;
   }
   if (wide) launch_prefill_cfg<128, 128, EPI, NORM, NTB>(p, nz, st);

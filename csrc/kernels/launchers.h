@@ -160,10 +160,15 @@ struct SampleArgs {
   float* parts;              // [B * nseg][8] partials (B * nseg <= 256)
   uint32_t* sync;            // [2 * B] zero-initialised, self-resetting row counters
   unsigned long long* tl;    // launch timeline slot (set by the launcher), or null
+  // pass-kernel mode (sampling.hip sample_pass0_kernel): per-row state [B][8 words] and
+  // zero-initialised, self-resetting arrival tickets [B]; null -> in-launch meetings only
+  struct RowState* state = nullptr;
+  uint32_t* tickets = nullptr;
 };
 void launch_sample(const SampleArgs& s, hipStream_t st);
 int sample_segments(int B, int V);
 void set_sample_nseg(int n);  // cap on segments per row (0 = B*NSEG <= 1024 bound only)
+void set_sample_round_launches(int n);  // rejection rounds run as launches (0 = pass 0 only)
 
 // Custom one-shot all-reduce over IPC-mapped peer buffers (xGMI).
 struct AllReduceArgs {

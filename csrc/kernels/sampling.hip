@@ -82,7 +82,190 @@ __device__ __forceinline__ bool row_meet(uint32_t* ctr, uint32_t target, int* ok
   return *ok_flag != 0;
 }
 
-__global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
+// Per-row sampling parameters (row-uniform).
+struct RowParams {
+  float T, c, cn, topp;
+  bool greedy, use_k, use_p;
+  int topk;
+  uint64_t seed, off;
+};
+
+__device__ __forceinline__ RowParams row_params(const SampleArgs& a, int row) {
+  RowParams r;
+  r.T = a.temperature ? a.temperature[row] : 0.f;
+  r.greedy = !(r.T > 1e-5f);
+  r.c = r.greedy ? LOG2E_S : LOG2E_S / r.T;  // log2-domain scale
+  r.cn = r.greedy ? 1.f : 1.f / r.T;         // natural-domain scale (Gumbel keys)
+  r.seed = a.seeds ? a.seeds[row] : 0ull;
+  r.off = a.offsets ? (uint64_t)a.offsets[row] : 0ull;
+  r.topk = a.top_k ? a.top_k[row] : -1;
+  r.topp = a.top_p ? a.top_p[row] : 1.f;
+  r.use_k = r.topk > 0 && r.topk < a.V;
+  r.use_p = r.topp < 1.f;
+  return r;
+}
+
+// One sweep of float4 range [v_lo, v_hi) of a row by this block (8 float4 loads in flight per
+// thread). mode 0: max / Z / argmax + Gumbel keys; mode 1: acceptance statistics of candidate
+// value xj (count and mass of x > xj, mass relative to the row max rmx) + Gumbel keys restricted
+// to x > xj with the noise of `round`.
+__device__ __forceinline__ void sweep_range(const float4* x4, int v_lo, int v_hi, int mode, float xj, float rmx,
+                                            uint32_t round, const RowParams& rp, Acc& acc) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int v0 = v_lo + tid; v0 < v_hi; v0 += nt * 8) {
+    float4 q[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int vi = v0 + u * nt;
+      q[u] = x4[vi < v_hi ? vi : v_hi - 1];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int vi = v0 + u * nt;
+      if (vi >= v_hi) break;
+      const float e[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+      float uu[4] = {0.5f, 0.5f, 0.5f, 0.5f};
+      if (!rp.greedy) philox4(rp.seed, rp.off, (uint32_t)vi, round, uu);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float v = e[j];
+        const int i = 4 * vi + j;
+        if (mode == 0) {
+          if (v > acc.mx) {
+            acc.z = (acc.mx == -INFINITY ? 0.f : acc.z * exp2f((acc.mx - v) * rp.c)) + 1.f;
+            acc.mx = v;
+            acc.amx = i;
+          } else if (v > -INFINITY) {
+            acc.z += exp2f((v - acc.mx) * rp.c);
+          }
+        } else if (v > xj) {
+          acc.cnt += 1.f;
+          acc.q += exp2f((v - rmx) * rp.c);
+        }
+        if (!rp.greedy && (mode == 0 || v > xj) && v > -INFINITY) {
+          // accurate logs: a fast log rounding -log(u) to 0 near u = 1 would make an infinite key
+          const float g = v * rp.cn - logf(fmaxf(-logf(uu[j]), 1e-30f));
+          if (g > acc.gk) { acc.gk = g; acc.gi = i; }
+        }
+      }
+    }
+  }
+}
+
+// ---- pass kernels: a kernel boundary instead of an in-launch meeting ----
+// The segmented kernel's meetings (every block of a row arrives, then polls until the last
+// one has) cost ~0.5 us per arriving block (sampler_probe: 18 us greedy / 35 us top-p at 32
+// segments, 143 us at 128). Here a pass is its own launch: each block publishes its partial
+// (sc1 stores, drained) and takes one arrival ticket; the LAST block of the row — told by the
+// value its atomic returned, nobody waits — merges the partials in fixed segment order and
+// decides. The decision travels to the next launch in a per-row state word (kernel boundary).
+//   sample_pass0_kernel: pass 0; greedy / plain-temperature rows are final here, top-k / top-p
+//                        rows leave their Gumbel candidate pending;
+//   sample_round_kernel: acceptance test of the pending candidate (one rejection round);
+//   sample_kernel(resume): rows still pending after the round launches continue with the
+//                        in-launch rounds (rare).
+struct RowState {
+  float mx, z;  // pass-0 row max and Z
+  int amx;      // pass-0 argmax (fallback)
+  int j;        // pending candidate
+  int status;   // 1 = pending acceptance of j, 0 = out[row] written
+  int pad[3];
+};
+
+// publish this block's merged Acc (thread 0 holds it) and take the row's ticket; returns true in
+// the row's last-arriving block, whose thread 0 then holds the fixed-order merge of all segments
+__device__ __forceinline__ bool publish_last(Acc& acc, SamplePart* parts, uint32_t* ticket, int seg, int nseg, float c,
+                                             Acc* red, int* flag) {
+  if (threadIdx.x == 0) {
+    float* w = reinterpret_cast<float*>(parts + seg);
+    st_sc1(w + 0, acc.mx); st_sc1(w + 1, acc.z); st_sc1(w + 2, __int_as_float(acc.amx));
+    st_sc1(w + 3, acc.gk); st_sc1(w + 4, __int_as_float(acc.gi)); st_sc1(w + 5, acc.cnt);
+    st_sc1(w + 6, acc.q);
+    drain_stores();
+    const uint32_t old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (uint32_t)(nseg - 1);
+    if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return false;
+  Acc r = acc_init();
+  if (threadIdx.x < nseg) {
+    const float* w = reinterpret_cast<const float*>(parts + threadIdx.x);
+    r = Acc{ld_sc1(w + 0), ld_sc1(w + 1), __float_as_int(ld_sc1(w + 2)), ld_sc1(w + 3),
+            __float_as_int(ld_sc1(w + 4)), ld_sc1(w + 5), ld_sc1(w + 6)};
+  }
+  block_reduce_acc(r, c, red);
+  if (threadIdx.x == 0) acc = r;
+  return true;
+}
+
+__device__ __forceinline__ void finish_row(const SampleArgs& a, int row, int chosen, float mx, float z, float c) {
+  a.out[row] = chosen;
+  if (a.out_logprob) a.out_logprob[row] = ((a.logits[(size_t)row * a.ldl + chosen] - mx) * c - log2f(z)) / LOG2E_S;
+}
+
+__global__ __launch_bounds__(SAMPLE_THREADS) void sample_pass0_kernel(SampleArgs a) {
+  TLScope tl_scope(a.tl);
+  __shared__ Acc red[SAMPLE_THREADS / 64];
+  __shared__ int flag;
+  const int seg = blockIdx.x, nseg = gridDim.x, row = blockIdx.y;
+  const int V4 = a.V >> 2;
+  const int v_lo = (int)(((long long)V4 * seg) / nseg), v_hi = (int)(((long long)V4 * (seg + 1)) / nseg);
+  const RowParams rp = row_params(a, row);
+  Acc acc = acc_init();
+  sweep_range(reinterpret_cast<const float4*>(a.logits + (size_t)row * a.ldl), v_lo, v_hi, 0, 0.f, 0.f, 0u, rp, acc);
+  block_reduce_acc(acc, rp.c, red);
+  SamplePart* parts = reinterpret_cast<SamplePart*>(a.parts) + (size_t)row * nseg;
+  if (!publish_last(acc, parts, a.tickets + row, seg, nseg, rp.c, red, &flag)) return;
+  if (threadIdx.x == 0) {
+    RowState& st = a.state[row];
+    st.mx = acc.mx; st.z = acc.z; st.amx = acc.amx;
+    if (!rp.greedy && (rp.use_k || rp.use_p) && acc.gi >= 0) {
+      st.j = acc.gi;
+      st.status = 1;
+    } else {
+      st.status = 0;
+      finish_row(a, row, rp.greedy || acc.gi < 0 ? acc.amx : acc.gi, acc.mx, acc.z, rp.c);
+    }
+  }
+}
+
+__global__ __launch_bounds__(SAMPLE_THREADS) void sample_round_kernel(SampleArgs a, uint32_t round) {
+  TLScope tl_scope(a.tl);
+  __shared__ Acc red[SAMPLE_THREADS / 64];
+  __shared__ int flag;
+  const int seg = blockIdx.x, nseg = gridDim.x, row = blockIdx.y;
+  const RowState st = a.state[row];
+  if (st.status != 1) return;  // row-uniform
+  const int V4 = a.V >> 2;
+  const int v_lo = (int)(((long long)V4 * seg) / nseg), v_hi = (int)(((long long)V4 * (seg + 1)) / nseg);
+  const RowParams rp = row_params(a, row);
+  const float* x = a.logits + (size_t)row * a.ldl;
+  const float xj = x[st.j];
+  Acc acc = acc_init();
+  sweep_range(reinterpret_cast<const float4*>(x), v_lo, v_hi, 1, xj, st.mx, round, rp, acc);
+  block_reduce_acc(acc, rp.c, red);
+  SamplePart* parts = reinterpret_cast<SamplePart*>(a.parts) + (size_t)row * nseg;
+  if (!publish_last(acc, parts, a.tickets + row, seg, nseg, rp.c, red, &flag)) return;
+  if (threadIdx.x == 0) {
+    RowState& s = a.state[row];
+    const bool ok_k = !rp.use_k || acc.cnt < (float)rp.topk;
+    const bool ok_p = !rp.use_p || acc.q < rp.topp * st.z;
+    if (ok_k && ok_p) {
+      s.status = 0;
+      finish_row(a, row, st.j, st.mx, st.z, rp.c);
+    } else if (acc.gi < 0) {
+      s.status = 0;
+      finish_row(a, row, st.amx, st.mx, st.z, rp.c);
+    } else {
+      s.j = acc.gi;  // next candidate, drawn from {x > x_j}
+    }
+  }
+}
+
+// resume > 0: only rows the pass kernels left pending (state), from rejection round `resume` on
+__global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a, uint32_t resume) {
   TLScope tl_scope(a.tl);
   __shared__ Acc red[SAMPLE_THREADS / 64];
   __shared__ Acc merged;
@@ -93,68 +276,20 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
   const int v_lo = (int)(((long long)V4 * seg) / nseg), v_hi = (int)(((long long)V4 * (seg + 1)) / nseg);
   const float* x = a.logits + (size_t)row * a.ldl;
   const float4* x4 = reinterpret_cast<const float4*>(x);
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const float T = a.temperature ? a.temperature[row] : 0.f;
-  const bool greedy = !(T > 1e-5f);
-  const float c = greedy ? LOG2E_S : LOG2E_S / T;  // log2-domain scale
-  const float cn = greedy ? 1.f : 1.f / T;         // natural-domain scale (Gumbel keys)
-  const uint64_t seed = a.seeds ? a.seeds[row] : 0ull;
-  const uint64_t off = a.offsets ? (uint64_t)a.offsets[row] : 0ull;
-  const int topk = a.top_k ? a.top_k[row] : -1;
-  const float topp = a.top_p ? a.top_p[row] : 1.f;
-  const bool use_k = topk > 0 && topk < a.V;
-  const bool use_p = topp < 1.f;
+  const int tid = threadIdx.x;
+  RowState st{};
+  if (resume > 0) {
+    st = a.state[row];
+    if (st.status != 1) return;  // row-uniform: decided by the pass kernels
+  }
+  const RowParams rp = row_params(a, row);
+  const float c = rp.c;
   // two partial buffers by pass parity: a block that has passed meet g may already publish
   // pass g+1 while a slower block of its row is still reading pass g's partials; it cannot
   // reach pass g+2 before every block has arrived at meet g+1, i.e. finished reading g
   SamplePart* parts_even = reinterpret_cast<SamplePart*>(a.parts) + (size_t)row * nseg;
   SamplePart* parts_odd = parts_even + (size_t)SAMPLE_MAX_BLOCKS;
   uint32_t* ctr = a.sync ? a.sync + row : nullptr;
-
-  // One sweep of this block's segment (8 float4 loads in flight per thread).
-  // mode 0: max/Z/argmax + Gumbel; mode 1: acceptance stats for xj + Gumbel restricted to x > xj.
-  // `rmx` is the ROW max of pass 0 (the reference of Z): it must not be read from `merged`,
-  // which holds the previous round's acceptance partial (mx = -inf) from round 2 on.
-  auto sweep = [&](int mode, float xj, float rmx, uint32_t round, Acc& acc) {
-    for (int v0 = v_lo + tid; v0 < v_hi; v0 += nt * 8) {
-      float4 q[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int vi = v0 + u * nt;
-        q[u] = x4[vi < v_hi ? vi : v_hi - 1];
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int vi = v0 + u * nt;
-        if (vi >= v_hi) break;
-        const float e[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
-        float uu[4] = {0.5f, 0.5f, 0.5f, 0.5f};
-        if (!greedy) philox4(seed, off, (uint32_t)vi, round, uu);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float v = e[j];
-          const int i = 4 * vi + j;
-          if (mode == 0) {
-            if (v > acc.mx) {
-              acc.z = (acc.mx == -INFINITY ? 0.f : acc.z * exp2f((acc.mx - v) * c)) + 1.f;
-              acc.mx = v;
-              acc.amx = i;
-            } else if (v > -INFINITY) {
-              acc.z += exp2f((v - acc.mx) * c);
-            }
-          } else if (v > xj) {
-            acc.cnt += 1.f;
-            acc.q += exp2f((v - rmx) * c);
-          }
-          if (!greedy && (mode == 0 || v > xj) && v > -INFINITY) {
-            // accurate logs: a fast log rounding -log(u) to 0 near u = 1 would make an infinite key
-            const float g = v * cn - logf(fmaxf(-logf(uu[j]), 1e-30f));
-            if (g > acc.gk) { acc.gk = g; acc.gi = i; }
-          }
-        }
-      }
-    }
-  };
 
   // publish this block's partial and merge all segments of the row (fixed order)
   auto exchange = [&](Acc& acc, uint32_t gen) -> bool {
@@ -187,25 +322,30 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
     return ok;
   };
 
-  Acc acc = acc_init();
-  sweep(0, 0.f, 0.f, 0u, acc);
-  bool ok = exchange(acc, 1);
-  const float mx = merged.mx, z = merged.z;
-  int chosen = merged.amx;
-  uint32_t gen = 1;
-  if (ok && !greedy) {
-    int j = merged.gi;
-    if (use_k || use_p) {
-      const float pmass = topp * z;
-      for (uint32_t round = 1; round <= 64 && j >= 0; ++round) {
+  float mx, z;
+  int chosen, j;
+  uint32_t gen = 0, round0 = 1;
+  bool ok = true;
+  if (resume == 0) {
+    Acc acc = acc_init();
+    sweep_range(x4, v_lo, v_hi, 0, 0.f, 0.f, 0u, rp, acc);
+    ok = exchange(acc, ++gen);
+    mx = merged.mx; z = merged.z; chosen = merged.amx; j = merged.gi;
+  } else {
+    mx = st.mx; z = st.z; chosen = st.amx; j = st.j;
+    round0 = resume;
+  }
+  if (ok && !rp.greedy) {
+    if (rp.use_k || rp.use_p) {
+      const float pmass = rp.topp * z;
+      for (uint32_t round = round0; round <= 64 && j >= 0; ++round) {
         const float xj = x[j];
-        Acc st = acc_init();
-        sweep(1, xj, mx, round, st);
-        ++gen;
-        ok = exchange(st, gen);
+        Acc acc = acc_init();
+        sweep_range(x4, v_lo, v_hi, 1, xj, mx, round, rp, acc);
+        ok = exchange(acc, ++gen);
         if (!ok) { j = -1; break; }
-        const bool ok_k = !use_k || merged.cnt < (float)topk;
-        const bool ok_p = !use_p || merged.q < pmass;
+        const bool ok_k = !rp.use_k || merged.cnt < (float)rp.topk;
+        const bool ok_p = !rp.use_p || merged.q < pmass;
         if (ok_k && ok_p) break;
         j = merged.gi;  // next candidate, drawn from {x > x_j}
       }
@@ -213,11 +353,11 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
     if (j >= 0) chosen = j;
   }
   if (seg == 0 && tid == 0) {
-    a.out[row] = chosen;
-    if (a.out_logprob) a.out_logprob[row] = ((x[chosen] - mx) * c - log2f(z)) / LOG2E_S;
+    finish_row(a, row, chosen, mx, z, c);
+    if (resume > 0) a.state[row].status = 0;
   }
   // self-reset for the next launch: the last block of the row to leave zeroes the counters
-  if (nseg > 1 && tid == 0) {
+  if (nseg > 1 && gen > 0 && tid == 0) {
     uint32_t* done = a.sync + a.B;
     const uint32_t d = __hip_atomic_fetch_add(done + row, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (d == (uint32_t)nseg - 1) {
@@ -245,13 +385,31 @@ int sample_segments(int B, int V) {
   return nseg < 1 ? 1 : nseg;
 }
 
+int g_sample_round_launches = 1;  // rejection rounds as their own launches before the in-launch fallback
+void set_sample_round_launches(int n) { g_sample_round_launches = n < -1 ? -1 : n; }  // -1: meetings only
+
 void launch_sample(const SampleArgs& s, hipStream_t st) {
   if (s.B <= 0) return;
   int nseg = sample_segments(s.B, s.V);
   if (s.parts == nullptr || s.sync == nullptr) nseg = 1;
   SampleArgs a = s;
+  static const bool meet_only = getenv("VGATE_SAMPLE_MEET") != nullptr;  // experiments: the in-launch kernel
+  if (nseg > 1 && s.state != nullptr && s.tickets != nullptr && g_sample_round_launches >= 0 && !meet_only) {
+    // pass 0 and the first rejection rounds as launches (last-arriver merges, no meetings),
+    // then the in-launch rounds for rows still pending
+    a.tl = tl_take("sample_pass0", nseg * s.B);
+    hipLaunchKernelGGL(sample_pass0_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, a);
+    for (int r = 1; r <= g_sample_round_launches; ++r) {
+      a.tl = tl_take("sample_round", nseg * s.B);
+      hipLaunchKernelGGL(sample_round_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, a, (uint32_t)r);
+    }
+    a.tl = tl_take("sample_resume", nseg * s.B);
+    hipLaunchKernelGGL(sample_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, a,
+                       (uint32_t)(g_sample_round_launches + 1));
+    return;
+  }
   a.tl = tl_take("sample", nseg * s.B);
-  hipLaunchKernelGGL(sample_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, a);
+  hipLaunchKernelGGL(sample_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, a, 0u);
 }
 
 }  // namespace vgate

@@ -33,7 +33,10 @@ __device__ __forceinline__ void philox4(uint64_t seed, uint64_t offset, uint32_t
 }
 
 constexpr int SAMPLE_THREADS = 256;
-constexpr int SAMPLE_MAX_BLOCKS = 256;  // B * NSEG bound: one block per CU, all co-resident
+// B * NSEG bound: one block per CU, all co-resident (more segments per row measured slower:
+// nseg 16 / 32 / 64 / 128 -> 38.7 / 35.2 / 55.8 / 143 us for 8 rows at top-p 0.9,
+// profiles/r2_sampler_nseg_sweep.log)
+constexpr int SAMPLE_MAX_BLOCKS = 256;
 constexpr float LOG2E_S = 1.4426950408889634f;
 
 // Per-(row, segment) partial, 8 words.

@@ -395,10 +395,15 @@ void sample(const Tensor& logits, const c10::optional<Tensor>& temperature,
   if (ws.has_value() && ws->defined()) {
     // [0, 512): row counters (2 per row, B <= 256 in segmented mode); [512, ...): partials
     // (8 words per block, B * nseg <= 256 blocks (1024 allowed), two buffers by pass parity)
+    // [20480, 22528): per-row pass state (8 words, B <= 256); [22528, 22784): pass tickets
     TORCH_CHECK(ws->scalar_type() == torch::kInt32 && ws->is_cuda() && ws->numel() >= 16896, "sample: ws must be int32[>=16896]");
     if (vgate::sample_segments(s.B, s.V) > 1) {
       s.sync = reinterpret_cast<uint32_t*>(ws->data_ptr());
       s.parts = reinterpret_cast<float*>(ws->data_ptr()) + 512;
+      if (ws->numel() >= 22784 && s.B <= 256) {
+        s.state = reinterpret_cast<vgate::RowState*>(reinterpret_cast<int32_t*>(ws->data_ptr()) + 20480);
+        s.tickets = reinterpret_cast<uint32_t*>(ws->data_ptr()) + 22528;
+      }
     }
   }
   c10::DeviceGuard guard(logits.device());
@@ -543,6 +548,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("offsets"), py::arg("out"), py::arg("out_logprob") = py::none(), py::arg("ws") = py::none());
   m.def("sample_segments", &vgate::sample_segments, "blocks per row the sampler uses for (B, V)");
   m.def("set_sample_nseg", &vgate::set_sample_nseg, "cap the sampler's segments per row (experiments)");
+  m.def("set_sample_round_launches", &vgate::set_sample_round_launches,
+        "rejection rounds the sampler runs as their own launches before the in-launch fallback (experiments)");
   m.def("prefetch", &prefetch, "read a tensor once with the default cache policy (MALL warm-up)",
         py::arg("t"), py::arg("blocks") = 256);
   m.def("ar_alloc", &ar_alloc, "uncached device allocation for the custom all-reduce (zeroed)");
