@@ -78,7 +78,7 @@ def main():
     C.set_sample_nseg(64)
     # pass kernels (pass 0 + R rejection rounds as launches, last-arriver merges) vs the in-launch
     # meetings only (-1)
-    for rl in (-1, 0, 1, 2, 3):
+    for rl in (-1, 0, 1, 2):
         C.set_sample_round_launches(rl)
         r = {"round_launches": rl}
         for name, t, tp in (("T0.7_top_p0.9", temp, topp), ("T0.7", temp, torch.ones_like(topp)),

@@ -250,7 +250,8 @@ __global__ __launch_bounds__(512) void awq_gemm_kernel(GemmParams p) {  // <= 8 
     const int m = m_base + mb * 16 + (lane & 15);
     xok[mb] = m < p.M;
     xrow[mb] = p.x + (size_t)row_of(p, m) * p.lda + 8 * (lane >> 4);
-    ssr[mb] = 0.f;
+    // NORM 3: the producer's sums of squares (wave 0 of slice 0 carries them into gemm_finish)
+    ssr[mb] = (NORM == 3 && wid == 0 && blockIdx.z == 0) ? prenorm_ss(p, m, lane >> 4) : 0.f;
   }
   const bf16_t* nw_ptr = p.norm_w ? p.norm_w + 8 * (lane >> 4) : nullptr;
   // Chunks of up to QC k-quads: EVERY load of a chunk (int4 weights, activations, RMSNorm
@@ -293,7 +294,7 @@ __global__ __launch_bounds__(512) void awq_gemm_kernel(GemmParams p) {  // <= 8 
       for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb) {
-          if constexpr (NORM) {
+          if constexpr (NORM == 1 || NORM == 2) {
             float f[8], g[8];
             unpack8(a[c][u][mb], f);
 #pragma unroll
@@ -576,7 +577,8 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
   // loaded with them one group ahead and applied before the unpack
   const bf16_t* grow = p.norm_w ? p.norm_w + 8 * (lane >> 4) + (XP > 1 ? (r16 / R) * 32 : 0) : nullptr;
   f32x4 acc[1][1] = {{f32x4{0.f, 0.f, 0.f, 0.f}}};
-  float ssr[1] = {0.f};
+  // NORM 3: the producer's sums of squares of row r16 (wave 0 of slice 0 carries them into gemm_finish)
+  float ssr[1] = {(NORM == 3 && wid == 0 && blockIdx.z == 0) ? prenorm_ss(p, r16, lane >> 4) : 0.f};
   constexpr int XL = 4 / XP;  // activation loads per k-quad
   const uint32_t lom = r16 < R ? ~0u : 0u;
   constexpr int GL = NORM == 1 ? XL : 1;
@@ -952,6 +954,7 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
 // Needs the fragment-packed scales (p.zeros = ops.pack_awq_sz, group 128).
 template <int NTB, int EPI, int NORM>
 static bool launch_awq_dec(GemmParams p, const GemmArgs& g, hipStream_t st) {
+  if constexpr (NORM == 3) return false;  // the staged kernel applies gamma while staging
   const int ntiles = g.N / 16;
   if (g.M > 16 || ntiles % (AD_WAVES * NTB) != 0 || g.waves > 0 || g.group != 128 || g.awq_szp == nullptr)
     return false;
@@ -1056,13 +1059,14 @@ static void launch_m(GemmParams p, const GemmArgs& g, hipStream_t st) {
 
 template <bool AWQ>
 static void launch_dispatch(GemmParams p, const GemmArgs& g, hipStream_t st) {
-  const int norm = g.norm_w != nullptr ? 1 : (g.rownorm ? 2 : 0);
+  const int norm = g.norm_w != nullptr ? 1 : (g.rownorm ? 2 : (g.ssp_in != nullptr ? 3 : 0));
   const int ntiles = g.N / 16;
   const bool pair = ntiles % 2 == 0 && ntiles >= 1024;
 #define VG_NORM(NTB_, EPI_)                                                     \
   do {                                                                          \
     if (norm == 1) launch_m<NTB_, EPI_, 1, AWQ>(p, g, st);                      \
     else if (norm == 2 && !AWQ) launch_m<NTB_, EPI_, 2, AWQ>(p, g, st);         \
+    else if (norm == 3 && AWQ) launch_m<NTB_, EPI_, 3, AWQ>(p, g, st);          \
     else launch_m<NTB_, EPI_, 0, AWQ>(p, g, st);                                \
   } while (0)
   switch (g.epi) {
@@ -1097,6 +1101,7 @@ static GemmParams to_params(const GemmArgs& g) {
   p.k_cache = g.k_cache; p.v_cache = g.v_cache; p.hq = g.hq; p.hkv = g.hkv; p.bs = g.bs;
   p.scales = g.scales; p.zeros = g.zeros; p.group = g.group; p.szp = g.awq_szp;
   p.dbg_ts = g.dbg_ts;
+  p.hg = g.hg; p.hg_gamma = g.hg_gamma; p.ssp_out = g.ssp_out; p.ssp_in = g.ssp_in; p.ssn = g.ssn;
   return p;
 }
 

@@ -24,6 +24,11 @@ struct GemmParams {
   const bf16_t* scales; const bf16_t* zeros; int group;
   const bf16_t* szp;  // AWQ decode: fragment-packed (scale, scale * zero) [N/16][K/128][4][8]
   int probe;          // profiling only (benchmarks/awq_sweep.py): 1 = skip activation loads, 2 = skip scale loads
+  // RMSNorm hand-off for the int4 consumers (decode, TP = 1). Producer (EPI_BF16 residual GEMMs:
+  // o_proj, down_proj): hg = bf16(h * gamma) of the output rows h it stores, and per-(row, 16-column
+  // tile) sums of squares of h -> ssp_out [M][N/16]. Consumer (NORM == 3): x = hg (gamma already
+  // applied), row scale rsqrt(sum of ssp_in[m][0..ssn) / K + eps) — no gamma loads, no x^2 pass.
+  bf16_t* hg; const bf16_t* hg_gamma; float* ssp_out; const float* ssp_in; int ssn;
   unsigned long long* dbg_ts;  // per-block [start, end] realtime stamps (profiling), or null
 };
 
@@ -115,6 +120,72 @@ __device__ __forceinline__ void epi_pre_b(const GemmParams& p, EpiPre<NTB>& e, i
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
+// EPI_BF16 with the RMSNorm hand-off (p.hg): out = bf16(bf16(acc) + bias + res) as the plain
+// epilogue, plus hg = bf16(out * gamma) and the tile's sum of out^2 (lane groups folded, group 0
+// stores ssp_out[m][tile]).
+template <int NTB, bool have>
+__device__ __forceinline__ void epilogue_norm_out(const GemmParams& p, const f32x4 (&v)[NTB], int m, int nt0, int nsub,
+                                                  const EpiPre<NTB> e, bool valid) {
+#pragma unroll
+  for (int j = 0; j < NTB; ++j) {
+    const int n = (nt0 + j) * 16 + nsub;
+    float o[4] = {v[j][0], v[j][1], v[j][2], v[j][3]};
+    float s2 = 0.f;
+    if (valid) {
+      if (p.bias) {
+        uint2 b;
+        if constexpr (have) b = j == 0 ? e.b0 : e.b1;
+        else b = *reinterpret_cast<const uint2*>(p.bias + n);
+        o[0] += bf_lo(b.x); o[1] += bf_hi(b.x);
+        o[2] += bf_lo(b.y); o[3] += bf_hi(b.y);
+      }
+      if (p.res) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = bf2f(f2bf(o[i]));  // torch: (x@W).bf16() + res
+        uint2 r;
+        if constexpr (have) r = j == 0 ? e.r0 : e.r1;
+        else r = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldr + n);
+        o[0] += bf_lo(r.x); o[1] += bf_hi(r.x);
+        o[2] += bf_lo(r.y); o[3] += bf_hi(r.y);
+      }
+      uint2 pk;
+      pk.x = pack_bf2(o[0], o[1]);
+      pk.y = pack_bf2(o[2], o[3]);
+      *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + n) = pk;
+      const float h4[4] = {bf_lo(pk.x), bf_hi(pk.x), bf_lo(pk.y), bf_hi(pk.y)};  // the stored values
+      const uint2 g = *reinterpret_cast<const uint2*>(p.hg_gamma + n);
+      const float g4[4] = {bf_lo(g.x), bf_hi(g.x), bf_lo(g.y), bf_hi(g.y)};
+      uint2 hk;
+      hk.x = pack_bf2(h4[0] * g4[0], h4[1] * g4[1]);
+      hk.y = pack_bf2(h4[2] * g4[2], h4[3] * g4[3]);
+      *reinterpret_cast<uint2*>(p.hg + (size_t)m * p.ldo + n) = hk;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s2 += h4[i] * h4[i];
+    }
+    s2 += xor16(s2);
+    s2 += xor32(s2);
+    if (valid && nsub == 0) p.ssp_out[(size_t)m * (p.N >> 4) + nt0 + j] = s2;
+  }
+}
+
+// NORM == 3 consumer: this lane's share of the producer's per-tile sums of squares of row m (the
+// lanes l, l^16, l^32, l^48 of a row each sum a quarter; gemm_finish folds them like the x^2 partials).
+__device__ __forceinline__ float prenorm_ss(const GemmParams& p, int m, int quarter) {
+  if (m >= p.M) return 0.f;
+  const float* s = p.ssp_in + (size_t)m * p.ssn;
+  const int q0 = (p.ssn * quarter) >> 2, q1 = (p.ssn * (quarter + 1)) >> 2;
+  float acc = 0.f;
+  for (int t0 = q0; t0 < q1; t0 += 8) {
+    float r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) r[u] = s[min(t0 + u, q1 - 1)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (t0 + u < q1) acc += r[u];
+  }
+  return acc;
+}
+
 // ---- epilogue for one (row m, 4 columns) group; v[j] are the NTB reduced tiles ----
 // `e` = operands prefetched at launch (decode kernel) when `have`, else loaded here.
 // `have` is a compile-time choice: a runtime select between a prefetched register value
@@ -124,6 +195,12 @@ __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 
 template <int NTB, int EPI, bool have>
 __device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[NTB], int m, int nt0, int nsub,
                                          const EpiPre<NTB> e, bool valid) {
+  if constexpr (EPI == EPI_BF16) {
+    if (p.hg != nullptr) {  // every lane calls in: the tile's sum of squares is a cross-lane fold
+      epilogue_norm_out<NTB, have>(p, v, m, nt0, nsub, e, valid);
+      return;
+    }
+  }
   if constexpr (EPI != EPI_QKV && EPI != EPI_SILU) {
     if (!valid) return;
   }

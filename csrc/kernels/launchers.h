@@ -49,6 +49,14 @@ struct GemmArgs {
   int group;
   // profiling only: per-block [start, end] s_memrealtime stamps (2 x blocks u64), or null
   unsigned long long* dbg_ts;
+  // RMSNorm hand-off to the int4 consumers (decode, M <= 16; gemm_epilogue.h GemmParams::hg):
+  // producer (epi 0): hg [M, N] bf16 = out * hg_gamma, ssp_out [M][N/16] f32 per-tile sums of out^2;
+  // consumer (AWQ): x is hg, ssp_in [M][ssn] the producer's sums (gamma not re-applied)
+  uint16_t* hg = nullptr;
+  const uint16_t* hg_gamma = nullptr;
+  float* ssp_out = nullptr;
+  const float* ssp_in = nullptr;
+  int ssn = 0;
 };
 void launch_gemm(const GemmArgs& g, hipStream_t st);
 // LDS-tiled prefill GEMM (gemm_prefill.hip) for long steps; returns false for a shape / mode it

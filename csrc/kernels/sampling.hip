@@ -205,9 +205,10 @@ __device__ __forceinline__ void finish_row(const SampleArgs& a, int row, int cho
   if (a.out_logprob) a.out_logprob[row] = ((a.logits[(size_t)row * a.ldl + chosen] - mx) * c - log2f(z)) / LOG2E_S;
 }
 
-__global__ __launch_bounds__(SAMPLE_THREADS) void sample_pass0_kernel(SampleArgs a) {
+template <int NT>
+__global__ __launch_bounds__(NT) void sample_pass0_kernel(SampleArgs a) {
   TLScope tl_scope(a.tl);
-  __shared__ Acc red[SAMPLE_THREADS / 64];
+  __shared__ Acc red[NT / 64];
   __shared__ int flag;
   const int seg = blockIdx.x, nseg = gridDim.x, row = blockIdx.y;
   const int V4 = a.V >> 2;
@@ -231,9 +232,10 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_pass0_kernel(SampleArgs
   }
 }
 
-__global__ __launch_bounds__(SAMPLE_THREADS) void sample_round_kernel(SampleArgs a, uint32_t round) {
+template <int NT>
+__global__ __launch_bounds__(NT) void sample_round_kernel(SampleArgs a, uint32_t round) {
   TLScope tl_scope(a.tl);
-  __shared__ Acc red[SAMPLE_THREADS / 64];
+  __shared__ Acc red[NT / 64];
   __shared__ int flag;
   const int seg = blockIdx.x, nseg = gridDim.x, row = blockIdx.y;
   const RowState st = a.state[row];
@@ -385,7 +387,7 @@ int sample_segments(int B, int V) {
   return nseg < 1 ? 1 : nseg;
 }
 
-int g_sample_round_launches = 1;  // rejection rounds as their own launches before the in-launch fallback
+int g_sample_round_launches = 2;  // rejection rounds as their own launches before the in-launch fallback
 void set_sample_round_launches(int n) { g_sample_round_launches = n < -1 ? -1 : n; }  // -1: meetings only
 
 void launch_sample(const SampleArgs& s, hipStream_t st) {
@@ -397,11 +399,18 @@ void launch_sample(const SampleArgs& s, hipStream_t st) {
   if (nseg > 1 && s.state != nullptr && s.tickets != nullptr && g_sample_round_launches >= 0 && !meet_only) {
     // pass 0 and the first rejection rounds as launches (last-arriver merges, no meetings),
     // then the in-launch rounds for rows still pending
+    // pass block width (experiments): 512 / 1024 threads measured no faster than 256 — a pass is
+    // bound by its memory round trips, not the sweep's Philox + log work (profiles/r2_sampler_nseg_sweep.log)
+    static const int nt = [] { const char* e = getenv("VGATE_SAMPLE_THREADS"); return e ? atoi(e) : 256; }();
     a.tl = tl_take("sample_pass0", nseg * s.B);
-    hipLaunchKernelGGL(sample_pass0_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, a);
+    if (nt == 256) hipLaunchKernelGGL(sample_pass0_kernel<256>, dim3(nseg, s.B), dim3(256), 0, st, a);
+    else if (nt == 512) hipLaunchKernelGGL(sample_pass0_kernel<512>, dim3(nseg, s.B), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL(sample_pass0_kernel<1024>, dim3(nseg, s.B), dim3(1024), 0, st, a);
     for (int r = 1; r <= g_sample_round_launches; ++r) {
       a.tl = tl_take("sample_round", nseg * s.B);
-      hipLaunchKernelGGL(sample_round_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, a, (uint32_t)r);
+      if (nt == 256) hipLaunchKernelGGL(sample_round_kernel<256>, dim3(nseg, s.B), dim3(256), 0, st, a, (uint32_t)r);
+      else if (nt == 512) hipLaunchKernelGGL(sample_round_kernel<512>, dim3(nseg, s.B), dim3(512), 0, st, a, (uint32_t)r);
+      else hipLaunchKernelGGL(sample_round_kernel<1024>, dim3(nseg, s.B), dim3(1024), 0, st, a, (uint32_t)r);
     }
     a.tl = tl_take("sample_resume", nseg * s.B);
     hipLaunchKernelGGL(sample_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, a,

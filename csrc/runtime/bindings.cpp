@@ -55,7 +55,9 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
           const c10::optional<Tensor>& v_cache, int64_t hq, int64_t hkv,
           const c10::optional<Tensor>& awq_scales, const c10::optional<Tensor>& awq_zeros, int64_t group,
           bool rownorm, const c10::optional<Tensor>& dbg_ts, int64_t ntb, int64_t path,
-          const c10::optional<Tensor>& awq_szp) {
+          const c10::optional<Tensor>& awq_szp, const c10::optional<Tensor>& hg_out,
+          const c10::optional<Tensor>& hg_gamma, const c10::optional<Tensor>& ssp_out,
+          const c10::optional<Tensor>& ssp_in) {
   CHECK_DEV(x); CHECK_DEV(wp); CHECK_DEV(out);
   CHECK_DT(x, torch::kBFloat16);
   CHECK_LASTDIM(x); CHECK_LASTDIM(out);
@@ -120,6 +122,25 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
     CHECK_DEV(*awq_szp); CHECK_DT(*awq_szp, torch::kBFloat16);
     TORCH_CHECK(group == 128 && awq_szp->numel() == N / 16 * (K / 128) * 32, "awq_szp: [N/16][K/128][4][8], group 128");
     g.awq_szp = reinterpret_cast<const uint16_t*>(awq_szp->data_ptr());
+  }
+  if (hg_out.has_value() && hg_out->defined()) {
+    // producer of the int4 consumers' RMSNorm hand-off: decode rows, bf16 residual epilogue
+    TORCH_CHECK(epi == 0 && M <= 16 && hg_gamma.has_value() && ssp_out.has_value(), "hg_out: epi 0, M <= 16, gamma, ssp_out");
+    CHECK_DEV(*hg_out); CHECK_DT(*hg_out, torch::kBFloat16); CHECK_LASTDIM(*hg_out);
+    TORCH_CHECK(hg_out->stride(0) == out.stride(0) && hg_out->size(0) >= M && hg_out->size(1) >= N, "hg_out: like out");
+    TORCH_CHECK(hg_gamma->numel() == N, "hg_gamma: N elements");
+    CHECK_DEV(*ssp_out); CHECK_DT(*ssp_out, torch::kFloat32);
+    TORCH_CHECK(ssp_out->numel() >= M * (N / 16), "ssp_out: [M][N/16]");
+    g.hg = reinterpret_cast<uint16_t*>(hg_out->data_ptr());
+    g.hg_gamma = opt_bf16(hg_gamma);
+    g.ssp_out = reinterpret_cast<float*>(ssp_out->data_ptr());
+  }
+  if (ssp_in.has_value() && ssp_in->defined()) {
+    TORCH_CHECK(awq && M <= 16 && !g.norm_w && !rownorm, "ssp_in: int4 decode consumers without another norm mode");
+    CHECK_DEV(*ssp_in); CHECK_DT(*ssp_in, torch::kFloat32);
+    TORCH_CHECK(ssp_in->numel() >= M * (K / 16), "ssp_in: [M][K/16]");
+    g.ssp_in = reinterpret_cast<const float*>(ssp_in->data_ptr());
+    g.ssn = (int)(K / 16);
   }
   c10::DeviceGuard guard(x.device());
   if (awq) vgate::launch_awq_gemm(g, cur_stream());
@@ -519,7 +540,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("v_cache") = py::none(), py::arg("hq") = 0, py::arg("hkv") = 0,
         py::arg("awq_scales") = py::none(), py::arg("awq_zeros") = py::none(), py::arg("group") = 128,
         py::arg("rownorm") = false, py::arg("dbg_ts") = py::none(), py::arg("ntb") = 0, py::arg("path") = 0,
-        py::arg("awq_szp") = py::none());
+        py::arg("awq_szp") = py::none(), py::arg("hg_out") = py::none(), py::arg("hg_gamma") = py::none(),
+        py::arg("ssp_out") = py::none(), py::arg("ssp_in") = py::none());
   m.def("attention", &attention, "unified paged attention: decode (partitions merged in-launch) + varlen prefill tiles",
         py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),

@@ -453,6 +453,49 @@ def test_awq_decode_kernel_shapes(M, g, sk):
     assert _rel_err(ys, ref.silu_mul_linear_ref(x, wd[: N // 2], wd[N // 2:])) < 2e-2
 
 
+@pytest.mark.parametrize("M", [1, 5, 8, 16])
+@pytest.mark.parametrize("producer", ["dense", "awq"])
+def test_awq_norm_handoff(M, producer):
+    """RMSNorm hand-off of the int4 decode path: a residual GEMM writes out, hg = bf16(out * gamma)
+    and per-16-column sums of out^2; the int4 consumers (qkv K-split kernel, SiLU stream kernel,
+    split-K) read hg with the row scale from those sums == the gamma-in-registers mode."""
+    torch.manual_seed(90 + M)
+    H, Kin, g = 1536, 2048, 128
+    x = torch.randn(M, Kin, device=DEV).bfloat16()
+    res = torch.randn(M, H, device=DEV).bfloat16()
+    gamma = (torch.rand(H, device=DEV) + 0.5).bfloat16()
+    if producer == "dense":
+        wo = (torch.randn(H, Kin, device=DEV) / math.sqrt(Kin)).bfloat16()
+        lo = ops.Linear(wo)
+        h_ref = ref.linear_ref(x, wo, None, res)
+    else:
+        qo = torch.randint(0, 16, (H, Kin), dtype=torch.int32)
+        so = (torch.rand(Kin // g, H) * 0.004 + 0.001).bfloat16()
+        zo = torch.randint(0, 16, (Kin // g, H)).float().bfloat16()
+        lo = ops.Linear(None, kind="awq", awq={"qint": qo, "scales": so.to(DEV), "zeros": zo.to(DEV), "group": g})
+        h_ref = ref.linear_ref(x, ref.awq_dequant_ref(qo, so, zo, g).to(DEV), None, res)
+    h = res.clone()
+    hg = torch.empty(M, H, dtype=torch.bfloat16, device=DEV)
+    ssp = torch.empty(M, H // 16, dtype=torch.float32, device=DEV)
+    ops.linear(x, lo, out=h, residual=h, norm_out=(hg, ssp, gamma))
+    assert _rel_err(h, h_ref) < 2e-2
+    assert torch.equal(hg, (h.float() * gamma.float()).bfloat16())
+    torch.testing.assert_close(ssp, h.float().pow(2).reshape(M, H // 16, 16).sum(-1), rtol=1e-5, atol=1e-4)
+    for N, layout, sk in [(2048, "qkv", 0), (2 * 4480, "silu", 0), (1536, "plain", 3)]:
+        q = torch.randint(0, 16, (N, H), dtype=torch.int32)
+        sc = (torch.rand(H // g, N) * 0.004 + 0.001).bfloat16()
+        zz = torch.randint(0, 16, (H // g, N)).float().bfloat16()
+        lin = ops.Linear(None, kind="awq", awq={"qint": q, "scales": sc.to(DEV), "zeros": zz.to(DEV), "group": g,
+                                                "layout": layout})
+        if layout == "qkv":
+            continue  # covered through the engine (needs the cache operands); plain + silu here
+        out_n = torch.empty(M, lin.out_features, dtype=torch.bfloat16, device=DEV)
+        out_h = torch.empty_like(out_n)
+        ops.linear(h, lin, out=out_n, norm=(gamma, 1e-6), splitk=sk)
+        ops.linear(hg, lin, out=out_h, prenorm=(ssp, 1e-6), splitk=sk)
+        assert _rel_err(out_h, out_n) < 1e-2, (layout, _rel_err(out_h, out_n))
+
+
 @pytest.mark.parametrize("kernel", [0, -1, -2])
 @pytest.mark.parametrize("N,K", [(17920, 1536), (1536, 8960), (2048, 1536)])
 def test_awq_decode_kernels_each(kernel, N, K):

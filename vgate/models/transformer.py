@@ -149,7 +149,7 @@ class DecoderModel:
         return n
 
     # ---------------------------------------------------------------- forward
-    def _row_parallel(self, x: torch.Tensor, lin, resid: torch.Tensor, first: bool) -> None:
+    def _row_parallel(self, x: torch.Tensor, lin, resid: torch.Tensor, first: bool, norm_out: tuple | None = None) -> None:
         """resid = all_reduce(x @ W^T [+ resid on TP rank 0]) for a row-parallel linear
         (o_proj / down_proj). With TP and >= tp_overlap_min_tokens rows the GEMM runs in
         row chunks (multiples of 16) and each chunk's all-reduce is issued on the comm
@@ -161,7 +161,7 @@ class DecoderModel:
         T = x.shape[0]
         nch = self.tp_overlap_chunks if tp.size > 1 and T >= self.tp_overlap_min_tokens else 1
         if nch <= 1:
-            ops.linear(x, lin, out=resid, residual=resid if first else None)
+            ops.linear(x, lin, out=resid, residual=resid if first else None, norm_out=norm_out)
             if tp.size > 1:
                 tp.all_reduce(resid)
             return
@@ -213,14 +213,26 @@ class DecoderModel:
         part_ml = torch.empty(S, sh.hq, P, 2, dtype=torch.float32, device=dev)
         first = tp.is_first
         eps = a.rms_eps
+        # int4 decode steps: the residual GEMMs (o_proj, down_proj) hand the NEXT RMSNorm over —
+        # h * gamma plus per-tile sums of h^2 — so the int4 qkv / gate_up kernels read normed rows
+        # (no gamma loads, no x^2 pass; ops.linear norm_out / prenorm)
+        hand = (self.quant == "awq" and tp.size == 1 and T <= 16
+                and os.environ.get("VGATE_AWQ_NORM_HANDOFF", "1") != "0")
+        if hand:
+            hg = torch.empty(T, a.hidden_size, dtype=torch.bfloat16, device=dev)
+            ssp = torch.empty(T, a.hidden_size // 16, dtype=torch.float32, device=dev)
+        nl = len(self.layers)
         for li, L in enumerate(self.layers):
             kc, vc = kv_caches[li]
-            ops.linear(resid, L.qkv, out=q, norm=(L.in_norm, eps),
-                       qkv=dict(positions=sv.positions, slots=sv.slots, cos_sin=self.cos_sin, k_cache=kc,
-                                v_cache=vc, hq=sh.hq, hkv=sh.hkv))
+            qkv_args = dict(positions=sv.positions, slots=sv.slots, cos_sin=self.cos_sin, k_cache=kc, v_cache=vc,
+                            hq=sh.hq, hkv=sh.hkv)
+            if hand and li > 0:
+                ops.linear(hg, L.qkv, out=q, prenorm=(ssp, eps), qkv=qkv_args)
+            else:
+                ops.linear(resid, L.qkv, out=q, norm=(L.in_norm, eps), qkv=qkv_args)
             # attention and o_proj (+ residual) as one launch when VGATE_FUSE_ATTN_O=1 (decode-sized
             # steps; measured slower, off by default: ops.attention_o); otherwise two launches
-            if ops.attention_o(q, sh.hq * D, kc, vc, sv.block_tables, sv.context_lens, sv.query_start, sv.tile_seq,
+            if not hand and ops.attention_o(q, sh.hq * D, kc, vc, sv.block_tables, sv.context_lens, sv.query_start, sv.tile_seq,
                                sv.tile_q0, attn, part_o, part_ml, sh.hq, sh.hkv, part_size, self.scale, L.o, resid,
                                residual=first):
                 if tp.size > 1:
@@ -228,9 +240,13 @@ class DecoderModel:
             else:
                 ops.attention(q, sh.hq * D, kc, vc, sv.block_tables, sv.context_lens, sv.query_start, sv.tile_seq,
                               sv.tile_q0, attn, part_o, part_ml, sh.hq, sh.hkv, part_size, self.scale)
-                self._row_parallel(attn, L.o, resid, first)
-            ops.linear(resid, L.gate_up, out=mlp, norm=(L.post_norm, eps))
-            self._row_parallel(mlp, L.down, resid, first)
+                self._row_parallel(attn, L.o, resid, first, norm_out=(hg, ssp, L.post_norm) if hand else None)
+            if hand:
+                ops.linear(hg, L.gate_up, out=mlp, prenorm=(ssp, eps))
+            else:
+                ops.linear(resid, L.gate_up, out=mlp, norm=(L.post_norm, eps))
+            nxt = (hg, ssp, self.layers[li + 1].in_norm) if hand and li + 1 < nl else None
+            self._row_parallel(mlp, L.down, resid, first, norm_out=nxt)
         if return_hidden:
             return resid
         logits = ops.linear(resid, self.lm_head, out_f32=True, norm=(self.final_norm, eps), row_idx=sv.sample_idx)

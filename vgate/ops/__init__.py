@@ -275,8 +275,13 @@ def workspace(device) -> torch.Tensor:
 def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
            residual: torch.Tensor | None = None, out_f32: bool = False, waves: int = 0, splitk: int = 0,
            norm: tuple | None = None, row_idx: torch.Tensor | None = None, qkv: dict | None = None,
-           path: int = 0) -> torch.Tensor:
+           path: int = 0, norm_out: tuple | None = None, prenorm: tuple | None = None) -> torch.Tensor:
     """out = epilogue(prologue(x) @ W^T).
+
+    RMSNorm hand-off to the int4 decode kernels (GPU, <= 16 rows, TP = 1; gemm_epilogue.h):
+    norm_out=(hg, ssp, gamma) on a residual GEMM also writes hg = out * gamma and per-16-column
+    sums of out^2 into ssp; prenorm=(ssp, eps) on an AWQ consumer whose x IS that hg applies the
+    row scale from ssp (no gamma loads or x^2 pass in the int4 kernel).
 
     norm=(w, eps): fused RMSNorm of x rows (deferred row scale, see gemm.hip); row_idx: gather rows of x first;
     qkv=dict(positions, slots, cos_sin, k_cache, v_cache, hq, hkv): fused bias + RoPE +
@@ -331,6 +336,10 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
         kw.update(awq_scales=lin.scales, awq_zeros=lin.zeros, group=lin.group)
         if getattr(lin, "szp", None) is not None:
             kw["awq_szp"] = lin.szp
+    if norm_out is not None:
+        kw.update(hg_out=norm_out[0], ssp_out=norm_out[1], hg_gamma=norm_out[2])
+    if prenorm is not None:
+        kw.update(ssp_in=prenorm[0], eps=float(prenorm[1]))
     C.gemm(x, lin.wp, lin.N, lin.K, out, epi, **kw)
     return out
 
