@@ -78,9 +78,12 @@ def main():
         out = torch.empty(M, N // 2 if epi == 2 else N, device=dev, dtype=torch.bfloat16)
         rows = []
         # ntb: 0 = launcher's choice (awq_stream_kernel), -1 = LDS-staged awq_dec_kernel,
-        # -2 = K-split awq_gemm_kernel
-        for waves, sk, ntb in [(0, 0, 0), (2, 0, 0), (4, 0, 0), (8, 0, 0), (0, 2, 0), (0, 4, 0), (0, 0, -1),
-                               (4, 0, -2)]:
+        # -2 = K-split awq_gemm_kernel, 1 / 2 / 4 = awq_stream_kernel with that many tiles per block
+        cfgs = [(0, 0, 0), (2, 0, 0), (4, 0, 0), (8, 0, 0), (0, 2, 0), (0, 4, 0), (0, 0, -1), (4, 0, -2),
+                (0, 0, 1), (0, 0, 2), (0, 0, 4), (8, 0, 4), (0, 2, 2), (0, 2, 4), (0, 4, 4)]
+        if os.environ.get("AWQ_SWEEP_CFGS"):
+            cfgs = [tuple(int(v) for v in c.split(":")) for c in os.environ["AWQ_SWEEP_CFGS"].split(",")]
+        for waves, sk, ntb in cfgs:
             def fns():
                 for i in range(12):
                     L = lins[i % ncopy]

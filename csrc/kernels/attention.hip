@@ -253,7 +253,15 @@ __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, in
     pv_update(o, vl, pb, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
-  if (myn > 0) {
+  if (myn == 1) {
+    // one chunk (every wave of a context <= 32 * nw): a single load round, no look-ahead. The
+    // ping-pong below would re-read the chunk twice more (clamped look-ahead issues), tripling
+    // the KV bytes the block's CU moves (first K/V landed 2.5 -> 1.9 us at ctx 128 with the
+    // re-reads cut, benchmarks/attn_phases.py)
+    uint4 ka[8], va[8];
+    issue(ka, va, 0);
+    consume(ka, va, 0);
+  } else if (myn > 1) {
     // Loads are issued UNCONDITIONALLY (an index past the end re-reads the last chunk):
     // straight-line issue lets the compiler keep partial vmcnt waits across the back-edge.
     uint4 ka[8], va[8], kb[8], vb[8];
@@ -264,6 +272,8 @@ __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, in
       issue(ka, va, min(j + 2, myn - 1));
       if (j + 1 < myn) consume(kb, vb, j + 1);
     }
+  }
+  if (myn > 0) {
     l += xor16(l);
     l += xor32(l);
   }

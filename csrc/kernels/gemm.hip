@@ -556,14 +556,20 @@ __global__ __launch_bounds__(256, 1) void awq_dec_kernel(GemmParams p) {
 // 4 lane groups with two cross-lane adds). XP activation packing (M <= 16/XP rows: one 16-B load
 // covers XP k-steps) as in gemm_kernel. Cross-wave reduction, deferred RMSNorm row scale,
 // split-K slabs and the epilogue are gemm_finish's.
-template <int U, int EPI, int NORM, int XP, bool PP>
+//
+// NTB > 1: a block owns NTB adjacent tiles and every wave streams its k-quads of all of them with
+// ONE set of activation loads. At M = 8 a k-quad's activations (2 KiB per wave) outweigh its int4
+// tile fragment (1 KiB), so one-tile blocks move twice as many activation bytes through the CU as
+// weight bytes; NTB = 4 cuts that to half.
+template <int U, int EPI, int NORM, int XP, bool PP, int NTB>
 __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
+  static_assert(NTB == 1 || (!PP && EPI != EPI_QKV), "multi-tile blocks: one-group form, tiles without partners");
   constexpr int R = 16 / XP;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   TLScope tl_scope(p.dbg_ts);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int KQ = p.K >> 7;
-  const int nt0 = blockIdx.x;
+  const int nt0 = blockIdx.x * NTB;
   const int s0 = (KQ * blockIdx.z) / p.splitk, s1 = (KQ * (blockIdx.z + 1)) / p.splitk;
   const int qbeg = s0 + ((s1 - s0) * wid) / nw;
   const int qend = s0 + ((s1 - s0) * (wid + 1)) / nw;
@@ -576,18 +582,23 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
   // RMSNorm gamma (NORM == 1): packed exactly like the activations (it depends on the column only),
   // loaded with them one group ahead and applied before the unpack
   const bf16_t* grow = p.norm_w ? p.norm_w + 8 * (lane >> 4) + (XP > 1 ? (r16 / R) * 32 : 0) : nullptr;
-  f32x4 acc[1][1] = {{f32x4{0.f, 0.f, 0.f, 0.f}}};
+  f32x4 acc[1][NTB];
+#pragma unroll
+  for (int j = 0; j < NTB; ++j) acc[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // NORM 3: the producer's sums of squares of row r16 (wave 0 of slice 0 carries them into gemm_finish)
   float ssr[1] = {(NORM == 3 && wid == 0 && blockIdx.z == 0) ? prenorm_ss(p, r16, lane >> 4) : 0.f};
   constexpr int XL = 4 / XP;  // activation loads per k-quad
   const uint32_t lom = r16 < R ? ~0u : 0u;
   constexpr int GL = NORM == 1 ? XL : 1;
-  auto load_grp = [&](uint4 (&w)[U], uint4 (&sz)[U], uint4 (&xa)[U][XL], uint4 (&ga)[U][GL], int kq0) {
+  auto load_grp = [&](uint4 (&w)[U][NTB], uint4 (&sz)[U][NTB], uint4 (&xa)[U][XL], uint4 (&ga)[U][GL], int kq0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int kq = min(kq0 + u, qend - 1);  // clamped: issued unconditionally, masked in mma
-      w[u] = ld_nt16(wbase + (size_t)kq * 64);
-      sz[u] = (p.probe & 2) ? make_uint4(0x3c003c00u, 0x3c003c00u, 0, 0) : szbase[(size_t)kq * 4];
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) {
+        w[u][j] = ld_nt16(wbase + ((size_t)j * KQ + kq) * 64);
+        sz[u][j] = (p.probe & 2) ? make_uint4(0x3c003c00u, 0x3c003c00u, 0, 0) : szbase[((size_t)j * KQ + kq) * 4];
+      }
 #pragma unroll
       for (int v = 0; v < XL; ++v)
         xa[u][v] = (xok && !(p.probe & 1)) ? *reinterpret_cast<const uint4*>(xrow + (kq * 4 + v * XP) * 32)
@@ -615,8 +626,8 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
       }
     }
   };
-  auto mma_grp = [&](const uint4 (&w)[U], const uint4 (&sz)[U], const uint4 (&xa)[U][XL], const uint4 (&ga)[U][GL],
-                     int kq0) {
+  auto mma_grp = [&](const uint4 (&w)[U][NTB], const uint4 (&sz)[U][NTB], const uint4 (&xa)[U][XL],
+                     const uint4 (&ga)[U][GL], int kq0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int kq = kq0 + u;
@@ -664,15 +675,19 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
       }
       X += xor16(X);
       X += xor32(X);
-      f32x4 pr = {0.f, 0.f, 0.f, 0.f};
-      pr = mfma16(raw8(w[u].x), as_bf16x8(b[0]), pr);
-      pr = mfma16(raw8(w[u].y), as_bf16x8(b[1]), pr);
-      pr = mfma16(raw8(w[u].z), as_bf16x8(b[2]), pr);
-      pr = mfma16(raw8(w[u].w), as_bf16x8(b[3]), pr);
-      const float s4[4] = {bf_lo(sz[u].x), bf_hi(sz[u].x), bf_lo(sz[u].y), bf_hi(sz[u].y)};
-      const float z4[4] = {bf_lo(sz[u].z), bf_hi(sz[u].z), bf_lo(sz[u].w), bf_hi(sz[u].w)};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[0][0][i] = fmaf(s4[i], pr[i], fmaf(-fmaf(128.f, s4[i], z4[i]), X, acc[0][0][i]));
+      for (int j = 0; j < NTB; ++j) {
+        f32x4 pr = {0.f, 0.f, 0.f, 0.f};
+        pr = mfma16(raw8(w[u][j].x), as_bf16x8(b[0]), pr);
+        pr = mfma16(raw8(w[u][j].y), as_bf16x8(b[1]), pr);
+        pr = mfma16(raw8(w[u][j].z), as_bf16x8(b[2]), pr);
+        pr = mfma16(raw8(w[u][j].w), as_bf16x8(b[3]), pr);
+        const uint4 q = sz[u][j];
+        const float s4[4] = {bf_lo(q.x), bf_hi(q.x), bf_lo(q.y), bf_hi(q.y)};
+        const float z4[4] = {bf_lo(q.z), bf_hi(q.z), bf_lo(q.w), bf_hi(q.w)};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[0][j][i] = fmaf(s4[i], pr[i], fmaf(-fmaf(128.f, s4[i], z4[i]), X, acc[0][j][i]));
+      }
     }
   };
   int kq = qbeg;
@@ -680,11 +695,11 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
   if constexpr (!PP) {
     // ONE group covering the wave's whole k-range (host-checked: <= U k-quads): every load of
     // the wave in flight at once, one memory round trip per block
-    uint4 wa[U], sa[U], xa[U][XL], gaa[U][GL];
+    uint4 wa[U][NTB], sa[U][NTB], xa[U][XL], gaa[U][GL];
     load_grp(wa, sa, xa, gaa, kq);
     mma_grp(wa, sa, xa, gaa, kq);
   } else if (ngrp > 0) {
-    uint4 wa[U], sa[U], xa[U][XL], gaa[U][GL], wb[U], sb[U], xb[U][XL], gab[U][GL];
+    uint4 wa[U][NTB], sa[U][NTB], xa[U][XL], gaa[U][GL], wb[U][NTB], sb[U][NTB], xb[U][XL], gab[U][GL];
     load_grp(wa, sa, xa, gaa, kq);
     int g = 0;
     for (; g + 2 <= ngrp; g += 2) {
@@ -696,7 +711,7 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
     }
     if (g < ngrp) mma_grp(wa, sa, xa, gaa, kq);
   }
-  gemm_finish<1, 1, EPI, NORM, false>(p, acc, ssr, smem, 0, nt0, EpiPre<1>{});
+  gemm_finish<1, NTB, EPI, NORM, false>(p, acc, ssr, smem, 0, nt0, EpiPre<NTB>{});
 }
 
 // ---- AWQ prefill operand: int4 fragments -> bf16 fragments (same fragment order) ----
@@ -980,48 +995,68 @@ static bool launch_awq_dec(GemmParams p, const GemmArgs& g, hipStream_t st) {
   return true;
 }
 
-// AWQ decode through awq_stream_kernel: one tile per block, waves split K, K slices across
+// AWQ decode through awq_stream_kernel: blocks of NTB tiles, waves split K, K slices across
 // blocks only when the tiles alone leave the chip under-filled. g.waves > 0 forces the wave
-// count (sweeps); returns false when the packed scales are missing (group != 128).
+// count (sweeps), g.ntb = 1 / 2 / 4 the tiles per block (0: the launcher's choice); returns false
+// when the packed scales are missing (group != 128).
+template <int EPI, int NORM, int NTB>
+static void launch_awq_stream_ntb(GemmParams p, dim3 grid, int w, bool one, size_t lds, hipStream_t st, int M) {
+  // register groups: NTB x U k-quads of weights + scales in flight per wave
+  constexpr int U1 = NTB == 1 ? 6 : NTB == 2 ? 4 : 3;
+#define VG_AS(XP_)                                                                                        \
+  do {                                                                                                    \
+    if (one || NTB > 1) hipLaunchKernelGGL((awq_stream_kernel<U1, EPI, NORM, XP_, false, NTB>), grid, dim3(64 * w), lds, st, p); \
+    else hipLaunchKernelGGL((awq_stream_kernel<2, EPI, NORM, XP_, true, 1>), grid, dim3(64 * w), lds, st, p);        \
+  } while (0)
+  if (M <= 4) VG_AS(4);
+  else if (M <= 8) VG_AS(2);
+  else VG_AS(1);
+#undef VG_AS
+}
+
 template <int EPI, int NORM>
 static bool launch_awq_stream(GemmParams p, const GemmArgs& g, hipStream_t st) {
-  if (g.M > 16 || g.group != 128 || g.awq_szp == nullptr || g.ntb == -1) return false;
+  if (g.M > 16 || g.group != 128 || g.awq_szp == nullptr || g.ntb < 0) return false;
   // narrow N x short K (qkv / o_proj, 1-1.5 MB of int4): the K-split awq_gemm_kernel's block is
   // shortest (5.7 vs 6.1 us wall, profiles/r2_awq_sweep.log)
-  if (g.splitk <= 0 && g.waves <= 0 && g.N < 8192 && g.K < 4096) return false;
+  if (g.splitk <= 0 && g.waves <= 0 && g.ntb <= 0 && g.N < 8192 && g.K < 4096) return false;
   const int ntiles = g.N / 16;
   const int KQ = g.K / 128;
+  // tiles per block: forced, or 2 for wide N (gate_up, 17920 x 1536 at M = 8: 9.0 us span at 2
+  // tiles vs 9.5 at 1 and 10.0 at 4, profiles/r2_awq_sweep_ntb.log — fewer activation bytes, but
+  // 4-tile blocks leave too few waves in flight)
+  int ntb = g.ntb > 0 ? g.ntb : (EPI != EPI_QKV && ntiles % 2 == 0 && ntiles / 2 >= 512 ? 2 : 1);
+  if (EPI == EPI_QKV || (ntb != 1 && ntb != 2 && ntb != 4) || ntiles % ntb != 0) ntb = 1;
+  const int nblk = ntiles / ntb;
   int sk = g.splitk > 0 ? g.splitk : 1;
   if (g.splitk <= 0)
-    while (ntiles * sk < 256 && KQ / (2 * sk) >= 12) sk *= 2;  // narrow N x deep K (down_proj)
+    while (nblk * sk < 256 && KQ / (2 * sk) >= 12) sk *= 2;  // narrow N x deep K (down_proj)
   if (sk > SK_MAX || sk > KQ) return false;
-  // waves: enough that each holds its whole k-range in one register group (<= AS_U k-quads),
-  // else (forced wave count / very deep K) the ping-pong pipeline
-  constexpr int AS_U = 6;
+  // waves: enough that each holds its whole k-range in one register group (<= U k-quads),
+  // else (NTB == 1 only: forced wave count / very deep K) the ping-pong pipeline
+  const int U1 = ntb == 1 ? 6 : ntb == 2 ? 4 : 3;
   const int qslice = (KQ + sk - 1) / sk;
-  int w = g.waves > 0 ? g.waves : (qslice + AS_U - 1) / AS_U;
+  int w = g.waves > 0 ? g.waves : (qslice + U1 - 1) / U1;
   if (w > 8) w = 8;
-  const bool one = (qslice + w - 1) / w <= AS_U;
-  const size_t need_slab = (size_t)ntiles * sk * (64 * 16 + (NORM ? 16 * 4 : 0));
-  if (sk > 1 && (g.slabs == nullptr || need_slab > g.slab_bytes || ntiles > g.max_counters)) return false;
+  const bool one = (qslice + w - 1) / w <= U1;
+  if (!one && ntb > 1) return false;
+  const size_t need_slab = (size_t)nblk * sk * (ntb * 64 * 16 + (NORM ? 16 * 4 : 0));
+  if (sk > 1 && (g.slabs == nullptr || need_slab > g.slab_bytes || nblk > g.max_counters)) return false;
   p.splitk = sk;
   {
     static const int probe = [] { const char* e = getenv("VGATE_AWQ_PROBE"); return e ? atoi(e) : 0; }();
     p.probe = probe;
   }
-  const size_t lds = red_bytes<1, 1>(w) + ssq_bytes<1>(w) + 16;
-  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_stream", ntiles * sk);
-  dim3 grid(ntiles, 1, sk), block(64 * w);
-  // ping-pong groups of 2 k-quads (4 spilled to scratch) when one group cannot hold the range
-#define VG_AS(XP_)                                                                                  \
-  do {                                                                                              \
-    if (one) hipLaunchKernelGGL((awq_stream_kernel<AS_U, EPI, NORM, XP_, false>), grid, block, lds, st, p); \
-    else hipLaunchKernelGGL((awq_stream_kernel<2, EPI, NORM, XP_, true>), grid, block, lds, st, p);       \
-  } while (0)
-  if (g.M <= 4) VG_AS(4);
-  else if (g.M <= 8) VG_AS(2);
-  else VG_AS(1);
-#undef VG_AS
+  const size_t lds = (size_t)w * ntb * 64 * 16 * (w > 1) + ssq_bytes<1>(w) + 16;
+  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_stream", nblk * sk);
+  const dim3 grid(nblk, 1, sk);
+  if constexpr (EPI == EPI_QKV) {
+    launch_awq_stream_ntb<EPI, NORM, 1>(p, grid, w, one, lds, st, g.M);
+  } else {
+    if (ntb == 4) launch_awq_stream_ntb<EPI, NORM, 4>(p, grid, w, one, lds, st, g.M);
+    else if (ntb == 2) launch_awq_stream_ntb<EPI, NORM, 2>(p, grid, w, one, lds, st, g.M);
+    else launch_awq_stream_ntb<EPI, NORM, 1>(p, grid, w, one, lds, st, g.M);
+  }
   return true;
 }
 

@@ -496,12 +496,13 @@ def test_awq_norm_handoff(M, producer):
         assert _rel_err(out_h, out_n) < 1e-2, (layout, _rel_err(out_h, out_n))
 
 
-@pytest.mark.parametrize("kernel", [0, -1, -2])
+@pytest.mark.parametrize("kernel", [0, -1, -2, 2, 4])
 @pytest.mark.parametrize("N,K", [(17920, 1536), (1536, 8960), (2048, 1536)])
 def test_awq_decode_kernels_each(kernel, N, K):
     """Every AWQ decode kernel on the Qwen2.5-1.5B shapes (M = 8, group 128, RMSNorm gamma in
     registers): 0 = launcher's choice (awq_stream_kernel for wide N / deep K), -1 = LDS-staged
-    awq_dec_kernel, -2 = K-split awq_gemm_kernel; == the dequantised fp32 reference."""
+    awq_dec_kernel, -2 = K-split awq_gemm_kernel, 2 / 4 = awq_stream_kernel with that many tiles
+    per block; == the dequantised fp32 reference."""
     torch.manual_seed(N + K + kernel)
     M, g = 8, 128
     q = torch.randint(0, 16, (N, K), dtype=torch.int32)
@@ -520,6 +521,53 @@ def test_awq_decode_kernels_each(kernel, N, K):
                       waves=4 if kernel == -2 else 0, ntb=kernel)
     want = ref.silu_mul_linear_ref(xn, wd[: N // 2], wd[N // 2:]) if silu else ref.linear_ref(xn, wd)
     assert _rel_err(out, want) < 2e-2
+
+
+@pytest.mark.parametrize("ntb", [1, 2, 4])
+@pytest.mark.parametrize("M", [1, 8, 16])
+@pytest.mark.parametrize("sk", [0, 2])
+def test_awq_stream_multitile(ntb, M, sk):
+    """awq_stream_kernel with NTB tiles per block (one set of activation loads per k-quad for
+    all tiles): plain + residual, SiLU pairs, gamma in registers and the RMSNorm hand-off
+    (hg / per-tile sums of squares written by the epilogue), with and without split-K
+    == the dequantised fp32 reference and the one-tile form."""
+    torch.manual_seed(300 + 10 * ntb + M + sk)
+    C = ops.native()
+    ws = ops.workspace(torch.device(DEV))
+    N, K, g = 4096, 1536, 128
+    q = torch.randint(0, 16, (N, K), dtype=torch.int32)
+    scales = (torch.rand(K // g, N) * 0.02 + 0.005).bfloat16()
+    zeros = torch.randint(0, 16, (K // g, N)).float().bfloat16()
+    wd = ref.awq_dequant_ref(q, scales, zeros, g).to(DEV)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    res = torch.randn(M, N, device=DEV).bfloat16()
+    awq = {"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV), "group": g}
+    lin = ops.Linear(None, awq=dict(awq))
+    kw = dict(ws=ws, awq_scales=lin.scales, awq_zeros=lin.zeros, group=g, awq_szp=lin.szp, splitk=sk)
+    outs = {}
+    for t in (1, ntb):
+        out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        C.gemm(x, lin.wp, N, K, out, 0, res=res, ntb=t, **kw)
+        outs[t] = out
+    assert _rel_err(outs[ntb], ref.linear_ref(x, wd, None, res)) < 2e-2
+    assert _rel_err(outs[ntb], outs[1]) < 1e-2  # wave k-split differs with the tile count
+    # RMSNorm gamma in registers + SiLU pairs
+    silu = ops.Linear(None, awq=dict(awq, silu=True))
+    nw = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+    xn, _ = ref.rmsnorm_ref(x, nw, 1e-6)
+    ys = torch.empty(M, N // 2, device=DEV, dtype=torch.bfloat16)
+    C.gemm(x, silu.wp, N, K, ys, 2, norm_w=nw, eps=1e-6, ntb=ntb,
+           **dict(kw, awq_scales=silu.scales, awq_zeros=silu.zeros, awq_szp=silu.szp))
+    assert _rel_err(ys, ref.silu_mul_linear_ref(xn, wd[: N // 2], wd[N // 2:])) < 2e-2
+    # hand-off epilogue: h = x W^T + res, hg = bf16(h * gamma), per-16-column sums of h^2
+    gamma = (torch.rand(N, device=DEV) + 0.5).bfloat16()
+    h = res.clone()
+    hg = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ssp = torch.empty(M, N // 16, dtype=torch.float32, device=DEV)
+    C.gemm(x, lin.wp, N, K, h, 0, res=h, ntb=ntb, hg_out=hg, hg_gamma=gamma, ssp_out=ssp, **kw)
+    assert torch.equal(h, outs[ntb])
+    assert torch.equal(hg, (h.float() * gamma.float()).bfloat16())
+    torch.testing.assert_close(ssp, h.float().pow(2).reshape(M, N // 16, 16).sum(-1), rtol=1e-5, atol=1e-4)
 
 
 @pytest.mark.parametrize("M", [40, 256])
