@@ -27,7 +27,8 @@ from vgate.runtime.sampling_params import SamplingParams  # noqa: E402
 CANDIDATES = {
     "qkv": [(0, 0, 0), (8, 1, 0), (4, 1, 0), (8, 2, 0), (4, 2, 0), (4, 4, 0), (2, 4, 0), (8, 4, 0)],
     "o": [(0, 0, 0), (8, 1, 1), (4, 1, 1), (8, 2, 1), (4, 2, 1), (4, 3, 1), (4, 4, 1), (2, 4, 1), (8, 4, 1)],
-    "gate_up": [(0, 0, 0), (4, 1, 0), (2, 1, 0), (1, 1, 0), (2, 2, 0)],
+    "gate_up": [(0, 0, 0), (4, 1, 0), (2, 1, 0), (1, 1, 0), (2, 2, 0), (2, 1, 2), (4, 1, 2), (8, 1, 2), (4, 1, 4),
+                (8, 1, 4)],
     "down": [(0, 0, 0), (8, 2, 1), (8, 3, 1), (8, 4, 1), (4, 4, 1), (4, 6, 1), (4, 8, 1), (8, 8, 1),
              (2, 8, 1)],
     "lm_head": [(0, 0, 0), (8, 1, 2), (4, 1, 2), (2, 1, 2), (1, 1, 2), (4, 1, 4), (2, 1, 1), (4, 1, 1)],

@@ -1105,7 +1105,13 @@ static void launch_dispatch(GemmParams p, const GemmArgs& g, hipStream_t st) {
     else launch_m<NTB_, EPI_, 0, AWQ>(p, g, st);                                \
   } while (0)
   switch (g.epi) {
-    case EPI_SILU: VG_NORM(1, EPI_SILU); break;  // self-contained 16-column tiles (8 gate + 8 up)
+    case EPI_SILU:  // self-contained 16-column tiles (8 gate + 8 up); g.ntb 2 / 4: tiles per block (sweeps)
+      if constexpr (!AWQ) {
+        if (g.ntb == 4 && ntiles % 4 == 0 && g.M <= 16) { VG_NORM(4, EPI_SILU); break; }
+        if (g.ntb == 2 && ntiles % 2 == 0 && g.M <= 16) { VG_NORM(2, EPI_SILU); break; }
+      }
+      VG_NORM(1, EPI_SILU);
+      break;
     case EPI_QKV: VG_NORM(1, EPI_QKV); break;
     case EPI_F32:
       if constexpr (!AWQ) {

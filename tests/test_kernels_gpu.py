@@ -71,6 +71,13 @@ def test_gemm_silu(M):
     y = ops.linear(x, lin)
     assert y.shape == (M, I)
     assert _rel_err(y, ref.silu_mul_linear_ref(x, wg, wu)) < 1e-2
+    if M <= 16:  # decode blocks of 2 / 4 SiLU tiles (forced), with the RMSNorm prologue
+        nw = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+        xn, _ = ref.rmsnorm_ref(x, nw, 1e-6)
+        for ntb, waves in [(2, 2), (2, 4), (4, 4)]:
+            lin.dec_waves, lin.dec_splitk, lin.dec_ntb = waves, 1, ntb
+            yt = ops.linear(x, lin, norm=(nw, 1e-6))
+            assert _rel_err(yt, ref.silu_mul_linear_ref(xn, wg, wu)) < 1e-2, (ntb, waves)
 
 
 def test_gemm_asymmetric_identity():
