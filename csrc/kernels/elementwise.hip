@@ -234,4 +234,25 @@ void launch_prefetch(const void* p, size_t bytes, int blocks, hipStream_t st) {
                      nullptr, tl_take("prefetch", blocks));
 }
 
+// Host <-> device copies of the step loop as a kernel on the compute queue. Per decode step the
+// engine moves ~40 KB of step metadata to the device and the sampled ids back; as hipMemcpyAsync
+// the metadata went through an SDMA engine, and the compute queue <-> SDMA hand-offs left the GPU
+// idle for ~25-40 us between two steps (benchmarks/trace_gaps.py: sampler end -> 9 us -> D2H blit
+// -> 11 us -> SDMA H2D -> 10 us -> next step). Here every 16-B piece is one load + one store by its
+// own thread (all in flight at once: one PCIe round trip); pinned host memory is device-mapped.
+// Stores to host memory are made system-visible before the kernel ends.
+__global__ __launch_bounds__(256) void copy16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, int n16,
+                                                     int to_host) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n16) dst[i] = src[i];
+  if (to_host) __threadfence_system();
+}
+
+void launch_copy16(const void* src, void* dst, size_t bytes, bool to_host, hipStream_t st) {
+  const int n16 = (int)(bytes / 16);
+  if (n16 <= 0) return;
+  hipLaunchKernelGGL(copy16_kernel, dim3((n16 + 255) / 256), dim3(256), 0, st, reinterpret_cast<const uint4*>(src),
+                     reinterpret_cast<uint4*>(dst), n16, to_host ? 1 : 0);
+}
+
 }  // namespace vgate

@@ -432,6 +432,30 @@ void sample(const Tensor& logits, const c10::optional<Tensor>& temperature,
 }
 
 // Warm the memory-side cache with a tensor's bytes (default-policy read sweep, nothing written).
+// Copy the first `nbytes` (rounded up to 16, within both tensors) between a pinned host tensor and
+// a device tensor with a kernel on the current stream (no SDMA engine hand-off, see elementwise.hip).
+static void* device_view(const Tensor& t) {
+  if (t.is_cuda()) return t.data_ptr();
+  TORCH_CHECK(t.is_pinned(), "kernel_copy: host tensor must be pinned");
+  void* d = nullptr;
+  TORCH_CHECK(hipHostGetDevicePointer(&d, t.data_ptr(), 0) == hipSuccess && d != nullptr,
+              "kernel_copy: pinned host memory is not device-mapped");
+  return d;
+}
+
+void kernel_copy(Tensor& dst, const Tensor& src, int64_t nbytes) {
+  TORCH_CHECK(dst.is_contiguous() && src.is_contiguous(), "kernel_copy: contiguous tensors");
+  TORCH_CHECK(dst.is_cuda() != src.is_cuda(), "kernel_copy: one host (pinned) and one device tensor");
+  const int64_t n = (nbytes + 15) / 16 * 16;
+  TORCH_CHECK(n <= (int64_t)(dst.numel() * dst.element_size()) && n <= (int64_t)(src.numel() * src.element_size()),
+              "kernel_copy: 16-B rounded size exceeds a tensor");
+  const Tensor& dev = dst.is_cuda() ? dst : src;
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0,
+              "kernel_copy: 16-B aligned tensors");
+  c10::DeviceGuard guard(dev.device());
+  vgate::launch_copy16(device_view(src), device_view(dst), (size_t)n, !dst.is_cuda(), cur_stream());
+}
+
 void prefetch(const Tensor& t, int64_t blocks) {
   CHECK_DEV(t);
   TORCH_CHECK(t.is_contiguous(), "prefetch: contiguous tensor");
@@ -572,6 +596,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_sample_nseg", &vgate::set_sample_nseg, "cap the sampler's segments per row (experiments)");
   m.def("set_sample_round_launches", &vgate::set_sample_round_launches,
         "rejection rounds the sampler runs as their own launches before the in-launch fallback (experiments)");
+  m.def("kernel_copy", &kernel_copy, "pinned host <-> device copy by a kernel on the current stream (no SDMA)",
+        py::arg("dst"), py::arg("src"), py::arg("nbytes"));
   m.def("prefetch", &prefetch, "read a tensor once with the default cache policy (MALL warm-up)",
         py::arg("t"), py::arg("blocks") = 256);
   m.def("ar_alloc", &ar_alloc, "uncached device allocation for the custom all-reduce (zeroed)");

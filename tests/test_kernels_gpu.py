@@ -976,3 +976,23 @@ def test_prefill_lds_gemm_all_epilogues(M, bn, sk):
     ref.rope_kv_ref(qkv, pos, slots, cs, kc2, vc2, hq, hkv, D)
     assert _rel_err(q, qkv[:, : hq * D]) < 2e-2
     assert _rel_err(kc, kc2) < 2e-2 and _rel_err(vc, vc2) < 2e-2
+
+
+def test_kernel_copy_host_device_round_trip():
+    """ops.host_device_copy: pinned host -> device and device -> pinned host by the copy kernel
+    (16-B pieces, sizes rounded up to 16 inside both tensors), ordered on the current stream."""
+    C = ops.native()
+    src = torch.randint(0, 2**31 - 1, (4096,), dtype=torch.int32).pin_memory()
+    dev = torch.zeros(4096, dtype=torch.int32, device=DEV)
+    back = torch.zeros(4096, dtype=torch.int32).pin_memory()
+    for nbytes in (16, 4000, 16384):
+        dev.zero_()
+        back.zero_()
+        C.kernel_copy(dev, src, nbytes)
+        C.kernel_copy(back, dev, nbytes)
+        torch.cuda.synchronize()
+        n = (nbytes + 15) // 16 * 4
+        assert torch.equal(back[:n], src[:n]), nbytes
+        assert int(back[n:].abs().sum()) == 0 and int(dev[n:].abs().sum()) == 0
+    with pytest.raises(RuntimeError):
+        C.kernel_copy(dev, src, 4096 * 4 + 16)  # past the tensors

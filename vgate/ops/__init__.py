@@ -576,6 +576,22 @@ def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, offsets
     return out
 
 
+KERNEL_COPY = os.environ.get("VGATE_KERNEL_COPY", "1") != "0"
+
+
+def host_device_copy(dst: torch.Tensor, src: torch.Tensor, nbytes: int) -> None:
+    """Copy the first ``nbytes`` between a pinned host tensor and a device tensor on the current
+    stream. GPU: a kernel on the compute queue (csrc/kernels/elementwise.hip copy16_kernel), so the
+    step loop's metadata upload and sampled-id download take no SDMA engine hand-off; both tensors
+    must hold ``nbytes`` rounded up to 16. ``VGATE_KERNEL_COPY=0``: hipMemcpyAsync."""
+    if KERNEL_COPY and (dst.is_cuda or src.is_cuda) and native_available():
+        native().kernel_copy(dst, src, int(nbytes))
+        return
+    d8 = dst.view(torch.uint8) if dst.dtype != torch.uint8 else dst
+    s8 = src.view(torch.uint8) if src.dtype != torch.uint8 else src
+    d8[:nbytes].copy_(s8[:nbytes], non_blocking=True)
+
+
 _SWS: dict = {}
 
 
@@ -596,5 +612,5 @@ def softmax_scale(head_dim: int) -> float:
 __all__ = [
     "native", "native_available", "pack_weight", "unpack_weight", "interleave_gate_up", "pack_awq",
     "Linear", "linear", "attention", "attention_o", "workspace", "row_permutation", "reserve_awq_scratch", "pack_awq_sz", "rmsnorm", "embedding", "rope_kv", "attention_decode", "attention_prefill",
-    "prefill_tiles", "sample", "softmax_scale", "ref",
+    "prefill_tiles", "sample", "softmax_scale", "ref", "host_device_copy",
 ]

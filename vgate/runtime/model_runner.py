@@ -86,16 +86,21 @@ class ModelRunner:
         self.graph_ok = lambda T, S: True  # per-bucket veto (TP groups without capturable collectives)
         self.graphs: dict[tuple[int, int], tuple] = {}
         self.pool = None
-        self.out_tokens = torch.zeros(self.max_seqs, dtype=torch.int32, device=self.device)
+        # rounded up to 4 ids: the sampled-id download moves 16-B pieces (ops.host_device_copy)
+        self.out_tokens = torch.zeros((self.max_seqs + 3) // 4 * 4, dtype=torch.int32, device=self.device)
         self.meta.prev_tokens = self.out_tokens if self.gpu else None
         self._k = 0  # double-buffer index of the next launch
         if self.gpu:
-            self.out_hosts = [torch.zeros(self.max_seqs, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+            self.out_hosts = [torch.zeros(self.out_tokens.numel(), dtype=torch.int32, pin_memory=True)
+                              for _ in range(2)]
             self.stream = torch.cuda.Stream(self.device)
-            self.started = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-            self.dones = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-            self.meta_copied = [torch.cuda.Event() for _ in range(2)]
+            # per-step device time from timing events (VGATE_STEP_TIMING=0: plain completion events)
+            self.step_timing = os.environ.get("VGATE_STEP_TIMING", "1") != "0"
+            self.started = [torch.cuda.Event(enable_timing=self.step_timing) for _ in range(2)]
+            self.dones = [torch.cuda.Event(enable_timing=self.step_timing) for _ in range(2)]
+            self.meta_copied = [torch.cuda.Event() for _ in range(2)]  # TP followers (they never collect)
             self._meta_pending = [False, False]
+            self._uncollected = [False, False]  # launch() of buffer k whose step is not collected yet
         else:
             self.out_hosts = [self.out_tokens]
         self.graph_hits = 0
@@ -253,16 +258,19 @@ class ModelRunner:
         t_host = time.perf_counter()
         k = self._k
         self._k ^= 1
-        if self._meta_pending[k]:  # host buffer k still feeding an H2D copy two steps back
-            self.meta_copied[k].synchronize()
+        if self._uncollected[k]:
+            # host buffers k (metadata, sampled ids) still belong to the step two back: wait for it
+            # (the engine loop collects a step before launching the one after next, so this is rare;
+            # no per-step event after the upload: every event record is a marker packet in the queue)
+            self.dones[k].synchronize()
         self.meta.select(k)
         samples = self._fill(batch, T, S, pending_slots)
         if self.on_plan is not None:
             self.on_plan(T, S, ns, nt, 0)
-        self.started[k].record()
+        if self.step_timing:
+            self.started[k].record()
         self.meta.upload(ns)
-        self.meta_copied[k].record()
-        self._meta_pending[k] = True
+        self._uncollected[k] = True
         graphs = self.use_graphs and self.graph_ok(T, S)
         g = self.graphs.get((T, S)) if graphs else None
         if g is None and graphs and not self.defer_capture:
@@ -286,7 +294,7 @@ class ModelRunner:
             view = self.meta.view(T, S)
             view.num_tokens, view.num_seqs = nt, ns
             self._forward_sample(view)
-        self.out_hosts[k][:ns].copy_(self.out_tokens[:ns], non_blocking=True)
+        ops.host_device_copy(self.out_hosts[k], self.out_tokens, 4 * ns)
         self.dones[k].record()
         self.host_ms += 1e3 * (time.perf_counter() - t_host)
         return StepHandle(k, ns, samples, None, t_host, (T, S), eager)
@@ -296,14 +304,17 @@ class ModelRunner:
         if h.toks is not None:
             return h.toks
         self.dones[h.k].synchronize()
-        ms = self.started[h.k].elapsed_time(self.dones[h.k])
-        self.gpu_ms += ms
-        self.gpu_steps += 1
-        if ms > self.max_gpu_ms:
-            self.max_gpu_ms, self.max_gpu_bucket, self.max_gpu_eager = ms, h.bucket, h.eager
-        if len(self.step_gpu_ms) < 65536:
-            self.step_gpu_ms.append(ms)
-        return self.out_hosts[h.k][: h.ns].tolist()
+        if self.step_timing:
+            ms = self.started[h.k].elapsed_time(self.dones[h.k])
+            self.gpu_ms += ms
+            self.gpu_steps += 1
+            if ms > self.max_gpu_ms:
+                self.max_gpu_ms, self.max_gpu_bucket, self.max_gpu_eager = ms, h.bucket, h.eager
+            if len(self.step_gpu_ms) < 65536:
+                self.step_gpu_ms.append(ms)
+        toks = self.out_hosts[h.k][: h.ns].tolist()
+        self._uncollected[h.k] = False
+        return toks
 
     @torch.inference_mode()
     def hidden_states(self, batch: ScheduledBatch) -> torch.Tensor:

@@ -13,6 +13,8 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
+from vgate import ops
+
 
 def _align(n: int, a: int = 16) -> int:
     return (n + a - 1) // a * a
@@ -99,8 +101,9 @@ class StepMeta:
     def upload(self, num_seqs: int, stream=None) -> None:
         if self.dev is self.host:
             return
-        n = self.used_bytes(num_seqs)
-        self.dev[:n].copy_(self.host[:n], non_blocking=True)
+        # a copy kernel on the compute queue, not an SDMA copy (ops.host_device_copy); nbytes is a
+        # multiple of 16, so the 16-B rounded prefix stays inside both buffers
+        ops.host_device_copy(self.dev, self.host, self.used_bytes(num_seqs))
 
     def view(self, T: int, S: int) -> StepView:
         d = self.d
