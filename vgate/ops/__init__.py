@@ -162,6 +162,9 @@ class Linear:
         self.dec_waves = 0
         self.dec_splitk = 0
         self.dec_ntb = 0
+        # prefill (M >= 128) tile / K-slice choice per M bucket, measured at engine start-up
+        # (tune_prefill); empty = the launcher's heuristic
+        self.prefill_plan: dict[int, tuple[int, int]] = {}
         if self.kind == "awq":
             q = awq["qint"]
             self.N, self.K = q.shape
@@ -321,6 +324,10 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
     ntb = 0
     if M <= 16 and waves == 0 and splitk == 0:
         waves, splitk, ntb = lin.dec_waves, lin.dec_splitk, lin.dec_ntb
+    elif M >= 128 and waves == 0 and splitk == 0 and path == 0 and lin.prefill_plan and lin.kind == "dense":
+        cfg = lin.prefill_plan.get(_plan_bucket(lin.prefill_plan, M))
+        if cfg is not None and cfg != (0, 0):
+            ntb, splitk, path = cfg[0], cfg[1], 1
     kw = dict(bias=lin.bias, res=residual, ws=workspace(x.device), waves=waves, splitk=splitk, ntb=ntb, path=path)
     if norm is not None:
         if lin.norm_gamma is not None:  # gamma lives in the weights: row scale only
@@ -576,6 +583,71 @@ def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, offsets
     return out
 
 
+def _plan_bucket(plan: dict, M: int):
+    """Smallest planned M >= M (a step's rows are padded up to its graph bucket), else None."""
+    keys = [k for k in plan if k >= M]
+    return min(keys) if keys else None
+
+
+# (tile code, K slices) candidates of the prefill kernels (csrc/kernels/gemm_prefill.hip
+# launch_prefill_epi): 0 = the launcher's heuristic, 64 / 128 = 128 x 64 / 128 x 128 tiles,
+# 256 = 256 x 128 3-deep ring, 768 / 1024 = the 4-phase 256 x 128 / 256 x 256 kernels
+PREFILL_CANDIDATES = [(0, 0), (64, 0), (128, 0), (128, 4), (256, 0), (256, 4), (256, 6), (768, 0), (768, 4),
+                      (768, 6), (1024, 0), (1024, 2), (1024, 6)]
+
+
+def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = 0.05) -> dict:
+    """Start-up measurement of the prefill GEMM decomposition per (N, K) shape and M bucket.
+
+    The launcher's tile / K-split heuristic misses by up to 1.8x at mid M, where the grid of
+    one tile shape needs a second partial round on 256 CUs and another's does not (Qwen2.5-1.5B
+    gate_up at M = 384: 64 us heuristic vs 35 us for 128 x 128 tiles; down at M = 512: 56 vs
+    40 us, profiles/r2_prefill_tile_sweep.log). Every candidate is timed on random operands of
+    the layer's shape (plain epilogue, all candidates are exact kernels of the same product);
+    the heuristic is kept unless a candidate beats it by more than ``margin``. The plan is
+    shared by every dense Linear of the same shape. Returns {(N, K): {M: (tile, slices)}}."""
+    dense = [lin for lin in lins if lin.kind == "dense" and getattr(lin, "wp", None) is not None and lin.wp.is_cuda]
+    if not dense or not native_available():
+        return {}
+    C = native()
+    dev = dense[0].wp.device
+    ws = workspace(dev)
+    plans: dict = {}
+    for lin in dense:
+        key = (lin.N, lin.K)
+        if key in plans:
+            lin.prefill_plan = plans[key]
+            continue
+        plan = {}
+        g = torch.Generator(device=dev)
+        g.manual_seed(lin.N + lin.K)
+        for M in ms:
+            x = torch.rand(M, lin.K, device=dev, generator=g).bfloat16()
+            out = torch.empty(M, lin.N, dtype=torch.bfloat16, device=dev)
+            times = {}
+            for bn, sk in PREFILL_CANDIDATES:
+                def run():
+                    C.gemm(x, lin.wp, lin.N, lin.K, out, 0, ws=ws, path=1, ntb=bn, splitk=sk)
+                try:
+                    run()
+                except RuntimeError:
+                    continue
+                s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s0.record()
+                for _ in range(iters):
+                    run()
+                s1.record()
+                s1.synchronize()
+                times[(bn, sk)] = s0.elapsed_time(s1) / iters
+            if (0, 0) not in times:
+                continue
+            best = min(times, key=times.get)
+            plan[M] = best if times[best] < (1.0 - margin) * times[(0, 0)] else (0, 0)
+        plans[key] = plan
+        lin.prefill_plan = plan
+    return plans
+
+
 KERNEL_COPY = os.environ.get("VGATE_KERNEL_COPY", "1") != "0"
 
 
@@ -612,5 +684,5 @@ def softmax_scale(head_dim: int) -> float:
 __all__ = [
     "native", "native_available", "pack_weight", "unpack_weight", "interleave_gate_up", "pack_awq",
     "Linear", "linear", "attention", "attention_o", "workspace", "row_permutation", "reserve_awq_scratch", "pack_awq_sz", "rmsnorm", "embedding", "rope_kv", "attention_decode", "attention_prefill",
-    "prefill_tiles", "sample", "softmax_scale", "ref", "host_device_copy",
+    "prefill_tiles", "sample", "softmax_scale", "ref", "host_device_copy", "tune_prefill",
 ]

@@ -25,6 +25,7 @@ from dataclasses import dataclass, field
 
 import torch
 
+from vgate import ops
 from vgate.models.config import resolve_arch
 from vgate.models.transformer import DecoderModel
 from vgate.parallel.comm import TPGroup, init_tp
@@ -66,6 +67,9 @@ class EngineConfig:
     # graphs instead of running eagerly (eager steps were the p99 tail: profiles/r2_bench*.log)
     warmup_max_tokens: int = 512
     warmup_max_seqs: int = 16
+    # GPU: time the prefill GEMM decompositions per layer shape and token bucket >= 128 at start-up
+    # (ops.tune_prefill) instead of relying on the launcher's heuristic alone
+    prefill_autotune: bool = os.environ.get("VGATE_PREFILL_AUTOTUNE", "1") != "0"
     arch_overrides: dict | None = None
 
     def resolve_device(self) -> torch.device:
@@ -128,6 +132,14 @@ class LLMEngine:
         self.runner = ModelRunner(self.model, self.kv_caches, cfg.max_num_seqs, cfg.max_num_batched_tokens,
                                   cfg.max_model_len, cfg.block_size, eager, part,
                                   cfg.graph_token_buckets)
+        self.prefill_plans: dict = {}
+        if self.device.type == "cuda" and cfg.prefill_autotune:
+            t1 = time.perf_counter()
+            ms = [t for t in self.runner.t_buckets if t >= 128]
+            lins = [lin for L in self.model.layers for lin in (L.qkv, L.o, L.gate_up, L.down)]
+            self.prefill_plans = ops.tune_prefill(lins, ms)
+            log.info("prefill GEMM plans for %d shapes x %d buckets in %.2fs: %s", len(self.prefill_plans), len(ms),
+                     time.perf_counter() - t1, {f"{n}x{k}": p for (n, k), p in self.prefill_plans.items()})
         if gloo_tp and not eager:
             cap = self.tp.custom_bytes()
             H, vloc = self.arch.hidden_size, self.model.shard.vocab
