@@ -324,7 +324,7 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
     ntb = 0
     if M <= 16 and waves == 0 and splitk == 0:
         waves, splitk, ntb = lin.dec_waves, lin.dec_splitk, lin.dec_ntb
-    elif M >= 128 and waves == 0 and splitk == 0 and path == 0 and lin.prefill_plan and lin.kind == "dense":
+    elif M >= 128 and waves == 0 and splitk == 0 and path == 0 and lin.prefill_plan and lin.kind == "dense":  # (AWQ: below)
         cfg = lin.prefill_plan.get(_plan_bucket(lin.prefill_plan, M))
         if cfg is not None and cfg != (0, 0):
             ntb, splitk, path = cfg[0], cfg[1], 1
@@ -379,6 +379,10 @@ def _linear_awq_dequant(x, lin: "Linear", out, residual, norm, qkv, epi, M):
     if qkv is not None:
         kw.update(positions=qkv["positions"], slots=qkv["slots"], cos_sin=qkv["cos_sin"],
                   k_cache=qkv["k_cache"], v_cache=qkv["v_cache"], hq=qkv["hq"], hkv=qkv["hkv"])
+    if M >= 128 and lin.prefill_plan:
+        cfg = lin.prefill_plan.get(_plan_bucket(lin.prefill_plan, M))
+        if cfg is not None and cfg != (0, 0):
+            kw.update(ntb=cfg[0], splitk=cfg[1], path=1)
     C.gemm(x, scratch, lin.N, lin.K, out, epi, **kw)
     return out
 # the W4A16 kernels are decode kernels (no tile path above M = 16): hand AWQ steps to the
@@ -605,15 +609,16 @@ def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = 0.05
     40 us, profiles/r2_prefill_tile_sweep.log). Every candidate is timed on random operands of
     the layer's shape (plain epilogue, all candidates are exact kernels of the same product);
     the heuristic is kept unless a candidate beats it by more than ``margin``. The plan is
-    shared by every dense Linear of the same shape. Returns {(N, K): {M: (tile, slices)}}."""
-    dense = [lin for lin in lins if lin.kind == "dense" and getattr(lin, "wp", None) is not None and lin.wp.is_cuda]
-    if not dense or not native_available():
+    shared by every Linear of the same shape (AWQ layers: the plan of their bf16 dequant scratch).
+    Returns {(N, K): {M: (tile, slices)}}."""
+    cand = [lin for lin in lins if getattr(lin, "wp", None) is not None and lin.wp.is_cuda]
+    if not cand or not native_available():
         return {}
     C = native()
-    dev = dense[0].wp.device
+    dev = cand[0].wp.device
     ws = workspace(dev)
     plans: dict = {}
-    for lin in dense:
+    for lin in cand:
         key = (lin.N, lin.K)
         if key in plans:
             lin.prefill_plan = plans[key]
@@ -621,13 +626,17 @@ def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = 0.05
         plan = {}
         g = torch.Generator(device=dev)
         g.manual_seed(lin.N + lin.K)
+        # AWQ layers run their long steps on a bf16 fragment-packed dequant scratch of the same
+        # shape (_linear_awq_dequant): time a random bf16 matrix in that layout
+        wp = lin.wp if lin.kind == "dense" else pack_weight(
+            (torch.rand(lin.N, lin.K, device=dev, generator=g) * 2 - 1).bfloat16())
         for M in ms:
             x = torch.rand(M, lin.K, device=dev, generator=g).bfloat16()
             out = torch.empty(M, lin.N, dtype=torch.bfloat16, device=dev)
             times = {}
             for bn, sk in PREFILL_CANDIDATES:
                 def run():
-                    C.gemm(x, lin.wp, lin.N, lin.K, out, 0, ws=ws, path=1, ntb=bn, splitk=sk)
+                    C.gemm(x, wp, lin.N, lin.K, out, 0, ws=ws, path=1, ntb=bn, splitk=sk)
                 try:
                     run()
                 except RuntimeError:
