@@ -248,6 +248,21 @@ __global__ __launch_bounds__(256) void copy16_kernel(const uint4* __restrict__ s
   if (to_host) __threadfence_system();
 }
 
+// The step graph's last node: the sampled ids of the step -> slot `*slot` of a pinned host ring
+// (device-mapped), so the host reads them once the graph has completed, with no copy launched
+// after the graph (the graph-end -> next-dispatch boundary was ~9 us of the gap between steps).
+__global__ __launch_bounds__(64) void ids_to_host_kernel(const int32_t* __restrict__ ids, int32_t* __restrict__ ring,
+                                                         const int32_t* __restrict__ slot, int stride, int n) {
+  const int s = *slot;
+  for (int i = threadIdx.x; i < n; i += 64) ring[(size_t)s * stride + i] = ids[i];
+  __threadfence_system();
+}
+
+void launch_ids_to_host(const int32_t* ids, int32_t* ring, const int32_t* slot, int stride, int n, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(ids_to_host_kernel, dim3(1), dim3(64), 0, st, ids, ring, slot, stride, n);
+}
+
 void launch_copy16(const void* src, void* dst, size_t bytes, bool to_host, hipStream_t st) {
   const int n16 = (int)(bytes / 16);
   if (n16 <= 0) return;

@@ -456,6 +456,16 @@ void kernel_copy(Tensor& dst, const Tensor& src, int64_t nbytes) {
   vgate::launch_copy16(device_view(src), device_view(dst), (size_t)n, !dst.is_cuda(), cur_stream());
 }
 
+void ids_to_host(const Tensor& ids, Tensor& ring, const Tensor& slot, int64_t n) {
+  CHECK_DEV(ids); CHECK_DEV(slot);
+  CHECK_DT(ids, torch::kInt32); CHECK_DT(ring, torch::kInt32); CHECK_DT(slot, torch::kInt32);
+  TORCH_CHECK(ring.dim() == 2 && ring.is_contiguous() && !ring.is_cuda(), "ids_to_host: ring = pinned int32 [slots, stride]");
+  TORCH_CHECK(n >= 0 && n <= ids.numel() && n <= ring.size(1), "ids_to_host: n exceeds ids or a ring slot");
+  c10::DeviceGuard guard(ids.device());
+  vgate::launch_ids_to_host(reinterpret_cast<const int32_t*>(ids.data_ptr()), reinterpret_cast<int32_t*>(device_view(ring)),
+                            reinterpret_cast<const int32_t*>(slot.data_ptr()), (int)ring.size(1), (int)n, cur_stream());
+}
+
 void prefetch(const Tensor& t, int64_t blocks) {
   CHECK_DEV(t);
   TORCH_CHECK(t.is_contiguous(), "prefetch: contiguous tensor");
@@ -598,6 +608,8 @@ PYBIND11_MODULE(_C, m) {
         "rejection rounds the sampler runs as their own launches before the in-launch fallback (experiments)");
   m.def("kernel_copy", &kernel_copy, "pinned host <-> device copy by a kernel on the current stream (no SDMA)",
         py::arg("dst"), py::arg("src"), py::arg("nbytes"));
+  m.def("ids_to_host", &ids_to_host, "sampled ids -> slot *slot of a pinned host ring (graph-capturable, device-read slot)",
+        py::arg("ids"), py::arg("ring"), py::arg("slot"), py::arg("n"));
   m.def("prefetch", &prefetch, "read a tensor once with the default cache policy (MALL warm-up)",
         py::arg("t"), py::arg("blocks") = 256);
   m.def("ar_alloc", &ar_alloc, "uncached device allocation for the custom all-reduce (zeroed)");

@@ -62,6 +62,7 @@ class StepHandle:
     t_launch: float
     bucket: tuple = (0, 0)  # (T, S) graph bucket of the step
     eager: bool = False     # ran without a captured graph (first sight of its bucket)
+    timed: bool = False     # a start event was recorded (device time of sampled steps)
 
 
 class ModelRunner:
@@ -91,8 +92,13 @@ class ModelRunner:
         self.meta.prev_tokens = self.out_tokens if self.gpu else None
         self._k = 0  # double-buffer index of the next launch
         if self.gpu:
-            self.out_hosts = [torch.zeros(self.out_tokens.numel(), dtype=torch.int32, pin_memory=True)
-                              for _ in range(2)]
+            # pinned ring the step graph's last node writes the sampled ids into (slot = the
+            # launch's double-buffer index, read by the kernel from the step metadata)
+            self.out_ring = torch.zeros(2, self.out_tokens.numel(), dtype=torch.int32, pin_memory=True)
+            self.out_hosts = [self.out_ring[0], self.out_ring[1]]
+            self._launches = 0
+            # VGATE_RING_IDS=0: copy the ids after the graph instead (A/B experiments)
+            self.ring_ids = os.environ.get("VGATE_RING_IDS", "1") != "0"
             self.stream = torch.cuda.Stream(self.device)
             # per-step device time from timing events (VGATE_STEP_TIMING=0: plain completion events)
             self.step_timing = os.environ.get("VGATE_STEP_TIMING", "1") != "0"
@@ -114,7 +120,7 @@ class ModelRunner:
         self.pending_captures: dict[tuple[int, int], int] = {}
         self.defer_capture_failed = False  # a deferred capture raised: stop queueing more
         self.capture_seconds = 0.0
-        self.gpu_ms = 0.0  # device time of replayed steps (upload -> sampled ids on host)
+        self.gpu_ms = 0.0  # device time of every 8th step (upload -> sampled ids on host)
         self.host_ms = 0.0  # host time of execute() outside the device wait
         self.gpu_steps = 0
         self.captures = 0  # hipGraph captures so far (start-up warm-up + deferred + on-miss)
@@ -208,6 +214,8 @@ class ModelRunner:
         logits = self.model.forward(view, self.kv, self.part_size)
         ops.sample(logits, view.temperature, view.top_p, view.top_k, view.seeds, view.offsets,
                    out=self.out_tokens[: view.S])
+        if self.gpu and self.ring_ids:  # last node of the step graph: sampled ids -> pinned ring slot
+            ops.native().ids_to_host(self.out_tokens, self.out_ring, view.ring_slot, view.S)
         return logits
 
     def _capture(self, T: int, S: int):
@@ -265,9 +273,13 @@ class ModelRunner:
             self.dones[k].synchronize()
         self.meta.select(k)
         samples = self._fill(batch, T, S, pending_slots)
+        self.meta.h["ring_slot"][0] = k
         if self.on_plan is not None:
             self.on_plan(T, S, ns, nt, 0)
-        if self.step_timing:
+        # device time of every 8th step (an event record is a marker packet in the queue)
+        timed = self.step_timing and self._launches % 8 == 0
+        self._launches += 1
+        if timed:
             self.started[k].record()
         self.meta.upload(ns)
         self._uncollected[k] = True
@@ -294,17 +306,18 @@ class ModelRunner:
             view = self.meta.view(T, S)
             view.num_tokens, view.num_seqs = nt, ns
             self._forward_sample(view)
-        ops.host_device_copy(self.out_hosts[k], self.out_tokens, 4 * ns)
+        if not self.ring_ids:
+            ops.host_device_copy(self.out_hosts[k], self.out_tokens, 4 * ns)
         self.dones[k].record()
         self.host_ms += 1e3 * (time.perf_counter() - t_host)
-        return StepHandle(k, ns, samples, None, t_host, (T, S), eager)
+        return StepHandle(k, ns, samples, None, t_host, (T, S), eager, timed)
 
     def collect(self, h: "StepHandle") -> list[int]:
         """Wait for a launched step and return its sampled ids (one per batch item)."""
         if h.toks is not None:
             return h.toks
         self.dones[h.k].synchronize()
-        if self.step_timing:
+        if h.timed:
             ms = self.started[h.k].elapsed_time(self.dones[h.k])
             self.gpu_ms += ms
             self.gpu_steps += 1

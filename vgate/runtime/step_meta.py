@@ -38,6 +38,7 @@ class StepView:
     top_k: torch.Tensor
     seeds: torch.Tensor
     offsets: torch.Tensor
+    ring_slot: torch.Tensor | None = None  # [1]: slot of the pinned ring the step's sampled ids go to
     prev_tokens: torch.Tensor | None = None  # previous step's sampled ids (ids < 0 refer into it)
     num_tokens: int = 0
     num_seqs: int = 0
@@ -56,7 +57,8 @@ class StepMeta:
             ("ids", np.int32, self.T), ("positions", np.int32, self.T), ("slots", np.int32, self.T),
             ("query_start", np.int32, self.S + 1), ("context_lens", np.int32, self.S),
             ("tile_seq", np.int32, self.tiles), ("tile_q0", np.int32, self.tiles),
-            ("sample_idx", np.int32, self.S), ("block_tables", np.int32, self.S * max_blocks),
+            ("sample_idx", np.int32, self.S), ("ring_slot", np.int32, 4),
+            ("block_tables", np.int32, self.S * max_blocks),
         ]
         off = 0
         self.layout = {}
@@ -113,4 +115,5 @@ class StepMeta:
             tile_seq=d["tile_seq"][: T // 16 + S], tile_q0=d["tile_q0"][: T // 16 + S],
             sample_idx=d["sample_idx"][:S], block_tables=d["block_tables"].view(self.S, self.max_blocks)[:S],
             temperature=d["temperature"][:S], top_p=d["top_p"][:S], top_k=d["top_k"][:S],
-            seeds=d["seeds"][:S], offsets=d["offsets"][:S], prev_tokens=self.prev_tokens)
+            seeds=d["seeds"][:S], offsets=d["offsets"][:S], ring_slot=d["ring_slot"][:1],
+            prev_tokens=self.prev_tokens)
