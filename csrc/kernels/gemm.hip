@@ -953,12 +953,22 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
   else if constexpr (MB == 1) {
     constexpr int U = NTB == 1 ? 8 : 4;
     const int KT = g.K / 32;
+    // one-tile blocks: register groups of 6 k-steps when that wastes fewer issue slots on the
+    // clamped re-reads of a partial last group than groups of 8 (qkv / o_proj: 6 k-steps per wave
+    // -> one group of 6 instead of 8 with 2 re-reads; down_proj: 17-18 -> 3 x 6 instead of 3 x 8).
+    // Every re-read is a 1 KiB wave load the CU's address unit spends on nothing.
+    static const int force_u = [] { const char* e = getenv("VGATE_DEC_U"); return e ? atoi(e) : 0; }();
+    const int kpw = (KT / pl.splitk + pl.waves - 1) / pl.waves;
+    const bool u6 = NTB == 1 && g.M > 4 && (force_u == 6 || (force_u == 0 && (kpw + 5) / 6 * 6 < (kpw + 7) / 8 * 8));
     if (g.M <= 4 && KT % 4 == 0)
       hipLaunchKernelGGL((gemm_kernel<MB, NTB, U, EPI, NORM, true, 4>), grid, block, lds, st, p);
-    else if (g.M <= 8 && KT % 2 == 0)
-      hipLaunchKernelGGL((gemm_kernel<MB, NTB, U, EPI, NORM, true, 2>), grid, block, lds, st, p);
-    else
-      hipLaunchKernelGGL((gemm_kernel<MB, NTB, U, EPI, NORM, true, 1>), grid, block, lds, st, p);
+    else if (g.M <= 8 && KT % 2 == 0) {
+      if (u6) hipLaunchKernelGGL((gemm_kernel<MB, NTB, NTB == 1 ? 6 : U, EPI, NORM, true, 2>), grid, block, lds, st, p);
+      else hipLaunchKernelGGL((gemm_kernel<MB, NTB, U, EPI, NORM, true, 2>), grid, block, lds, st, p);
+    } else {
+      if (u6) hipLaunchKernelGGL((gemm_kernel<MB, NTB, NTB == 1 ? 6 : U, EPI, NORM, true, 1>), grid, block, lds, st, p);
+      else hipLaunchKernelGGL((gemm_kernel<MB, NTB, U, EPI, NORM, true, 1>), grid, block, lds, st, p);
+    }
   } else {
     hipLaunchKernelGGL((gemm_kernel<MB, NTB, MB == 4 ? 2 : 4, EPI, NORM, false, 1>), grid, block, lds, st, p);
   }
