@@ -224,7 +224,7 @@ __device__ __forceinline__ bf16x8 raw8(uint32_t q) {
   return as_bf16x8(r);
 }
 
-template <int MB, int NTB, int EPI, int NORM>
+template <int MB, int NTB, int EPI, int NORM, int QC_ = 0>
 __global__ __launch_bounds__(512) void awq_gemm_kernel(GemmParams p) {  // <= 8 waves: 256 VGPRs for the chunked loads
   extern __shared__ __attribute__((aligned(16))) char smem[];
   TLScope tl_scope(p.dbg_ts);
@@ -258,7 +258,8 @@ __global__ __launch_bounds__(512) void awq_gemm_kernel(GemmParams p) {  // <= 8 
   // gamma, group scales / zeros) is issued before any is consumed, so a wave's k-range costs
   // ceil(n / QC) memory round trips instead of one per k-quad — in the engine the
   // activations arrive cold from the previous kernel (qkv 9.8 -> see profiles/r1_awq_*).
-  constexpr int QC = MB == 1 ? 4 : (MB == 2 ? 2 : 1);
+  // QC_ > 0: the launcher's chunk size (3 when every wave owns 3 k-quads: no clamped re-load)
+  constexpr int QC = QC_ > 0 ? QC_ : (MB == 1 ? 4 : (MB == 2 ? 2 : 1));
   for (int kc = qbeg; kc < qend; kc += QC) {
     uint4 w[QC][NTB];
     uint4 a[QC][4][MB];
@@ -948,8 +949,14 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
   if (p.dbg_ts == nullptr)
     p.dbg_ts = tl_take(AWQ ? "awq_gemm" : (EPI == EPI_QKV ? "gemm_qkv" : EPI == EPI_SILU ? "gemm_gate_up"
                                             : EPI == EPI_F32 ? "gemm_f32" : "gemm"), nblk * mchunks * pl.splitk);
-  if constexpr (AWQ)
-    hipLaunchKernelGGL((awq_gemm_kernel<MB, NTB, EPI, NORM>), grid, block, lds, st, p);
+  if constexpr (AWQ) {
+    // chunks of 3 k-quads when every wave's range is exactly 3 (K = 1536 over 4 waves): a chunk of
+    // 4 would re-load a clamped fourth k-quad (weights, 4 activation rows, 8 scale / zero words)
+    const int KQ = g.K / 128;
+    const bool qc3 = MB == 1 && KQ % (pl.splitk * pl.waves) == 0 && KQ / (pl.splitk * pl.waves) == 3;
+    if (qc3) hipLaunchKernelGGL((awq_gemm_kernel<MB, NTB, EPI, NORM, MB == 1 ? 3 : 0>), grid, block, lds, st, p);
+    else hipLaunchKernelGGL((awq_gemm_kernel<MB, NTB, EPI, NORM>), grid, block, lds, st, p);
+  }
   else if constexpr (MB == 1) {
     constexpr int U = NTB == 1 ? 8 : 4;
     const int KT = g.K / 32;
@@ -1010,12 +1017,17 @@ static bool launch_awq_dec(GemmParams p, const GemmArgs& g, hipStream_t st) {
 // count (sweeps), g.ntb = 1 / 2 / 4 the tiles per block (0: the launcher's choice); returns false
 // when the packed scales are missing (group != 128).
 template <int EPI, int NORM, int NTB>
-static void launch_awq_stream_ntb(GemmParams p, dim3 grid, int w, bool one, size_t lds, hipStream_t st, int M) {
+static void launch_awq_stream_ntb(GemmParams p, dim3 grid, int w, bool one, bool small, size_t lds, hipStream_t st,
+                                  int M) {
   // register groups: NTB x U k-quads of weights + scales in flight per wave
   constexpr int U1 = NTB == 1 ? 6 : NTB == 2 ? 4 : 3;
+  // one-tile blocks whose waves own <= 3 k-quads: groups of 3 (a group of 6 would re-load 3+
+  // clamped k-quads of weights, scales and activations per wave)
+  const bool u3 = NTB == 1 && one && small;
 #define VG_AS(XP_)                                                                                        \
   do {                                                                                                    \
-    if (one || NTB > 1) hipLaunchKernelGGL((awq_stream_kernel<U1, EPI, NORM, XP_, false, NTB>), grid, dim3(64 * w), lds, st, p); \
+    if (u3) hipLaunchKernelGGL((awq_stream_kernel<3, EPI, NORM, XP_, false, 1>), grid, dim3(64 * w), lds, st, p); \
+    else if (one || NTB > 1) hipLaunchKernelGGL((awq_stream_kernel<U1, EPI, NORM, XP_, false, NTB>), grid, dim3(64 * w), lds, st, p); \
     else hipLaunchKernelGGL((awq_stream_kernel<2, EPI, NORM, XP_, true, 1>), grid, dim3(64 * w), lds, st, p);        \
   } while (0)
   if (M <= 4) VG_AS(4);
@@ -1060,12 +1072,13 @@ static bool launch_awq_stream(GemmParams p, const GemmArgs& g, hipStream_t st) {
   const size_t lds = (size_t)w * ntb * 64 * 16 * (w > 1) + ssq_bytes<1>(w) + 16;
   if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_stream", nblk * sk);
   const dim3 grid(nblk, 1, sk);
+  const bool small = (qslice + w - 1) / w <= 3;
   if constexpr (EPI == EPI_QKV) {
-    launch_awq_stream_ntb<EPI, NORM, 1>(p, grid, w, one, lds, st, g.M);
+    launch_awq_stream_ntb<EPI, NORM, 1>(p, grid, w, one, small, lds, st, g.M);
   } else {
-    if (ntb == 4) launch_awq_stream_ntb<EPI, NORM, 4>(p, grid, w, one, lds, st, g.M);
-    else if (ntb == 2) launch_awq_stream_ntb<EPI, NORM, 2>(p, grid, w, one, lds, st, g.M);
-    else launch_awq_stream_ntb<EPI, NORM, 1>(p, grid, w, one, lds, st, g.M);
+    if (ntb == 4) launch_awq_stream_ntb<EPI, NORM, 4>(p, grid, w, one, small, lds, st, g.M);
+    else if (ntb == 2) launch_awq_stream_ntb<EPI, NORM, 2>(p, grid, w, one, small, lds, st, g.M);
+    else launch_awq_stream_ntb<EPI, NORM, 1>(p, grid, w, one, small, lds, st, g.M);
   }
   return true;
 }

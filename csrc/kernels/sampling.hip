@@ -113,11 +113,13 @@ __device__ __forceinline__ void sweep_range(const float4* x4, int v_lo, int v_hi
                                             uint32_t round, const RowParams& rp, Acc& acc) {
   const int tid = threadIdx.x, nt = blockDim.x;
   for (int v0 = v_lo + tid; v0 < v_hi; v0 += nt * 8) {
+    // lanes past the range load nothing (a clamped re-read of the last float4 cost a wave load
+    // per lane: ~40 % of a 32-segment pass's loads at V = 152k)
     float4 q[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int vi = v0 + u * nt;
-      q[u] = x4[vi < v_hi ? vi : v_hi - 1];
+      q[u] = vi < v_hi ? x4[vi] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
