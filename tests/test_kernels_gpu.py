@@ -996,3 +996,24 @@ def test_kernel_copy_host_device_round_trip():
         assert int(back[n:].abs().sum()) == 0 and int(dev[n:].abs().sum()) == 0
     with pytest.raises(RuntimeError):
         C.kernel_copy(dev, src, 4096 * 4 + 16)  # past the tensors
+
+
+def test_tune_prefill_plans_match_heuristic_results():
+    """ops.tune_prefill: plans for every planned M bucket, and a planned (tile, K-slices) linear
+    gives the launcher's result within bf16 split-K rounding for plain / SiLU / residual layers."""
+    torch.manual_seed(71)
+    K = 1536
+    lins = [ops.Linear((torch.randn(2048, K, device=DEV) / math.sqrt(K)).bfloat16()),
+            ops.Linear((torch.randn(2 * 2240, K, device=DEV) / math.sqrt(K)).bfloat16(), kind="silu")]
+    plans = ops.tune_prefill(lins, [128, 384])
+    assert set(plans) == {(2048, K), (2 * 2240, K)}
+    for lin in lins:
+        assert set(lin.prefill_plan) == {128, 384}
+        for M in (100, 384):  # 100 rows: below the prefill path, the plan is not consulted
+            x = torch.randn(M, K, device=DEV).bfloat16()
+            res = torch.randn(M, lin.out_features, device=DEV).bfloat16() if lin.layout == "plain" else None
+            y = ops.linear(x, lin, residual=res)
+            plan, lin.prefill_plan = lin.prefill_plan, {}
+            y0 = ops.linear(x, lin, residual=res)
+            lin.prefill_plan = plan
+            assert _rel_err(y, y0) < 1e-2, (lin.layout, M)

@@ -103,3 +103,28 @@ def test_unpack_awq_inverts_pack():
     torch.manual_seed(3)
     q = torch.randint(0, 16, (48, 384), dtype=torch.int32)
     assert torch.equal(ops.unpack_awq(ops.pack_awq(q), 48, 384), q)
+
+
+def test_prefill_plan_bucket_lookup():
+    """A step's rows are padded up to its graph bucket: the plan of the smallest planned M >= M
+    applies; larger M than any planned bucket keeps the launcher's heuristic (None)."""
+    plan = {128: (128, 0), 384: (128, 4), 512: (1024, 0)}
+    assert ops._plan_bucket(plan, 128) == 128
+    assert ops._plan_bucket(plan, 200) == 384
+    assert ops._plan_bucket(plan, 512) == 512
+    assert ops._plan_bucket(plan, 513) is None
+    assert ops._plan_bucket({}, 64) is None
+
+
+def test_tune_prefill_without_gpu_is_a_no_op():
+    lin = ops.Linear(torch.randn(64, 64).bfloat16())
+    assert ops.tune_prefill([lin], [128, 256]) == {}
+    assert lin.prefill_plan == {}
+
+
+def test_host_device_copy_cpu_fallback():
+    """Without a GPU tensor the helper is a plain prefix copy (the CPU engine's path)."""
+    src = torch.arange(64, dtype=torch.int32)
+    dst = torch.zeros(64, dtype=torch.int32)
+    ops.host_device_copy(dst, src, 40)
+    assert torch.equal(dst[:10], src[:10]) and int(dst[10:].abs().sum()) == 0
