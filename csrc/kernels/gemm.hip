@@ -82,10 +82,11 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   TLScope tl_scope(p.dbg_ts);
   const int KT = p.K >> 5;
-  const int nt0 = blockIdx.x * NTB;
+  const SplitPos sp = split_pos(p);
+  const int nt0 = (p.tail_full > 0 ? sp.tile : (int)blockIdx.x) * NTB;
   const int m_base = blockIdx.y * 16 * MB;
   // this block's k-slice, then this wave's contiguous range inside it
-  const int s0 = (KT * blockIdx.z) / p.splitk, s1 = (KT * (blockIdx.z + 1)) / p.splitk;
+  const int s0 = (KT * sp.slice) / sp.nsl, s1 = (KT * (sp.slice + 1)) / sp.nsl;
   int kbeg = s0 + ((s1 - s0) * wid) / nw;
   int kend = s0 + ((s1 - s0) * (wid + 1)) / nw;
   if constexpr (XP > 1) {  // waves take whole packs of XP k-steps (K % (32 * XP) == 0 on host)
@@ -570,8 +571,9 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
   TLScope tl_scope(p.dbg_ts);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int KQ = p.K >> 7;
-  const int nt0 = blockIdx.x * NTB;
-  const int s0 = (KQ * blockIdx.z) / p.splitk, s1 = (KQ * (blockIdx.z + 1)) / p.splitk;
+  const SplitPos sp = split_pos(p);  // (tail split: the last tiles run as K halves)
+  const int nt0 = (p.tail_full > 0 ? sp.tile : (int)blockIdx.x) * NTB;
+  const int s0 = (KQ * sp.slice) / sp.nsl, s1 = (KQ * (sp.slice + 1)) / sp.nsl;
   const int qbeg = s0 + ((s1 - s0) * wid) / nw;
   const int qend = s0 + ((s1 - s0) * (wid + 1)) / nw;
   const int r16 = lane & 15;
@@ -587,7 +589,7 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
 #pragma unroll
   for (int j = 0; j < NTB; ++j) acc[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // NORM 3: the producer's sums of squares of row r16 (wave 0 of slice 0 carries them into gemm_finish)
-  float ssr[1] = {(NORM == 3 && wid == 0 && blockIdx.z == 0) ? prenorm_ss(p, r16, lane >> 4) : 0.f};
+  float ssr[1] = {(NORM == 3 && wid == 0 && sp.slice == 0) ? prenorm_ss(p, r16, lane >> 4) : 0.f};
   constexpr int XL = 4 / XP;  // activation loads per k-quad
   const uint32_t lom = r16 < R ? ~0u : 0u;
   constexpr int GL = NORM == 1 ? XL : 1;
@@ -905,6 +907,19 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(GemmParams p) {
 // ------------------------------------------------------------------ host side
 struct Plan { int waves, splitk; };
 
+int g_tail_split = -1;  // -1: VGATE_TAIL_SPLIT (default on); 0 / 1: set_tail_split (tests)
+void set_tail_split(int on) { g_tail_split = on; }
+
+static int cu_count_gemm() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+
 // Decomposition from the MI355X sweep (benchmarks/micro_gpu.py, M=8, in-graph timing;
 // profiles/r1_gemm_sweep.log): 8 waves per block without split-K is best for the
 // small projections (qkv 3.5 us, o_proj 3.6 us — at the ~1.8 us launch floor plus one
@@ -940,15 +955,35 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
   const int ksteps = AWQ ? g.K / 128 : g.K / 32;
   Plan pl = plan(nblk, mchunks, ksteps, MB, NTB, g.waves, g.splitk);
   if (AWQ && pl.waves > 8) pl.waves = 8;  // awq_gemm_kernel: __launch_bounds__(512)
+  // Tail split (decode, wide N): q * ncu + r one-tile blocks put q + 1 tiles on r CUs and q on the
+  // rest, and the launch lasts as long as the q + 1 CUs; cutting the r tail tiles into K halves
+  // (combined by gemm_finish's last-arriver slab hand-off) leaves every CU q tiles + at most one
+  // half (gate_up: 1120 tiles = 4 x 256 + 96). VGATE_TAIL_SPLIT=0/1 (sweeps)
+  static const int tail_env = [] { const char* e = getenv("VGATE_TAIL_SPLIT"); return e ? atoi(e) : 1; }();
+  const int tail_mode = g_tail_split >= 0 ? g_tail_split : tail_env;
+  const int ncu = cu_count_gemm();
+  int grid_x = nblk;
+  p.tail_full = 0;
+  if (!AWQ && MB == 1 && tail_mode != 0 && pl.splitk == 1 && mchunks == 1 && g.waves <= 0 && g.splitk <= 0 &&
+      nblk > ncu && nblk % ncu != 0 && nblk % ncu <= ncu / 2) {
+    const int tail = nblk % ncu;
+    const size_t need = (size_t)(nblk + tail) * 2 * (NTB * 64 * 16 + (NORM ? 16 * 4 : 0));
+    if (g.slabs != nullptr && need <= g.slab_bytes && nblk <= g.max_counters) {
+      p.tail_full = nblk - tail;
+      grid_x = nblk + tail;
+      pl.splitk = 2;  // slab stride: at most 2 slices per tile
+    }
+  }
   const size_t need_slab = (size_t)nblk * mchunks * pl.splitk * (MB * NTB * 64 * 16 + (NORM ? 16 * MB * 4 : 0));
-  if (pl.splitk > 1 && (g.slabs == nullptr || need_slab > g.slab_bytes || nblk * mchunks > g.max_counters))
+  if (p.tail_full == 0 && pl.splitk > 1 &&
+      (g.slabs == nullptr || need_slab > g.slab_bytes || nblk * mchunks > g.max_counters))
     pl.splitk = 1;  // workspace too small: fall back to one slice (still correct)
   p.splitk = pl.splitk;
   const size_t lds = red_bytes<MB, NTB>(pl.waves) + ssq_bytes<MB>(pl.waves) + 16;
-  dim3 grid(nblk, mchunks, pl.splitk), block(64 * pl.waves);
+  dim3 grid(grid_x, mchunks, p.tail_full > 0 ? 1 : pl.splitk), block(64 * pl.waves);
   if (p.dbg_ts == nullptr)
     p.dbg_ts = tl_take(AWQ ? "awq_gemm" : (EPI == EPI_QKV ? "gemm_qkv" : EPI == EPI_SILU ? "gemm_gate_up"
-                                            : EPI == EPI_F32 ? "gemm_f32" : "gemm"), nblk * mchunks * pl.splitk);
+                                            : EPI == EPI_F32 ? "gemm_f32" : "gemm"), (int)(grid.x * grid.y * grid.z));
   if constexpr (AWQ) {
     // chunks of 3 k-quads when every wave's range is exactly 3 (K = 1536 over 4 waves): a chunk of
     // 4 would re-load a clamped fourth k-quad (weights, 4 activation rows, 8 scale / zero words)
@@ -965,8 +1000,11 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
     // -> one group of 6 instead of 8 with 2 re-reads; down_proj: 17-18 -> 3 x 6 instead of 3 x 8).
     // Every re-read is a 1 KiB wave load the CU's address unit spends on nothing.
     static const int force_u = [] { const char* e = getenv("VGATE_DEC_U"); return e ? atoi(e) : 0; }();
-    const int kpw = (KT / pl.splitk + pl.waves - 1) / pl.waves;
-    const bool u6 = NTB == 1 && g.M > 4 && (force_u == 6 || (force_u == 0 && (kpw + 5) / 6 * 6 < (kpw + 7) / 8 * 8));
+    // (tail split: the full tiles' and the halves' per-wave ranges both count)
+    const int kpw = (KT / (p.tail_full > 0 ? 1 : pl.splitk) + pl.waves - 1) / pl.waves;
+    const int kph = p.tail_full > 0 ? (KT / 2 + pl.waves - 1) / pl.waves : 0;
+    auto slots = [&](int u) { return (kpw + u - 1) / u * u + (kph + u - 1) / u * u; };
+    const bool u6 = NTB == 1 && g.M > 4 && (force_u == 6 || (force_u == 0 && slots(6) < slots(8)));
     if (g.M <= 4 && KT % 4 == 0)
       hipLaunchKernelGGL((gemm_kernel<MB, NTB, U, EPI, NORM, true, 4>), grid, block, lds, st, p);
     else if (g.M <= 8 && KT % 2 == 0) {
@@ -1064,14 +1102,29 @@ static bool launch_awq_stream(GemmParams p, const GemmArgs& g, hipStream_t st) {
   if (!one && ntb > 1) return false;
   const size_t need_slab = (size_t)nblk * sk * (ntb * 64 * 16 + (NORM ? 16 * 4 : 0));
   if (sk > 1 && (g.slabs == nullptr || need_slab > g.slab_bytes || nblk > g.max_counters)) return false;
+  // tail split as in launch_one (gate_up at 2 tiles per block: 560 = 2 x 256 + 48 blocks)
+  p.tail_full = 0;
+  int grid_x = nblk;
+  {
+    static const int tail_env = [] { const char* e = getenv("VGATE_TAIL_SPLIT"); return e ? atoi(e) : 1; }();
+    const int ncu = cu_count_gemm();
+    const int tail = nblk % ncu;
+    const size_t need = (size_t)(nblk + tail) * 2 * (ntb * 64 * 16 + (NORM ? 16 * 4 : 0));
+    if ((g_tail_split >= 0 ? g_tail_split : tail_env) != 0 && sk == 1 && g.waves <= 0 && g.splitk <= 0 && nblk > ncu &&
+        tail != 0 && tail <= ncu / 2 && g.slabs != nullptr && need <= g.slab_bytes && nblk <= g.max_counters) {
+      p.tail_full = nblk - tail;
+      grid_x = nblk + tail;
+      sk = 2;  // slab stride
+    }
+  }
   p.splitk = sk;
   {
     static const int probe = [] { const char* e = getenv("VGATE_AWQ_PROBE"); return e ? atoi(e) : 0; }();
     p.probe = probe;
   }
   const size_t lds = (size_t)w * ntb * 64 * 16 * (w > 1) + ssq_bytes<1>(w) + 16;
-  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_stream", nblk * sk);
-  const dim3 grid(nblk, 1, sk);
+  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_stream", p.tail_full > 0 ? grid_x : nblk * sk);
+  const dim3 grid(grid_x, 1, p.tail_full > 0 ? 1 : sk);
   const bool small = (qslice + w - 1) / w <= 3;
   if constexpr (EPI == EPI_QKV) {
     launch_awq_stream_ntb<EPI, NORM, 1>(p, grid, w, one, small, lds, st, g.M);

@@ -30,7 +30,26 @@ struct GemmParams {
   // applied), row scale rsqrt(sum of ssp_in[m][0..ssn) / K + eps) — no gamma loads, no x^2 pass.
   bf16_t* hg; const bf16_t* hg_gamma; float* ssp_out; const float* ssp_in; int ssn;
   unsigned long long* dbg_ts;  // per-block [start, end] realtime stamps (profiling), or null
+  // tail split (decode, one m-chunk): blocks [0, tail_full) own one column tile each over the full K;
+  // the remaining tiles are cut into 2 K halves (blocks tail_full + 2 j + {0, 1} -> tile tail_full + j),
+  // so a grid of q * 256 + r tiles runs as q whole tiles + r / 128 halves per CU instead of q or q + 1
+  // whole tiles. 0 = off (grid = (tiles, m-chunks, splitk)).
+  int tail_full;
 };
+
+// (column-tile block, K slice, slices) of this block: the grid decomposition of gemm_finish's hand-off
+struct SplitPos {
+  int tile, slice, nsl;
+};
+__device__ __forceinline__ SplitPos split_pos(const GemmParams& p) {
+  if (p.tail_full > 0) {
+    const int b = blockIdx.x;
+    if (b < p.tail_full) return SplitPos{b, 0, 1};
+    const int j = b - p.tail_full;
+    return SplitPos{p.tail_full + (j >> 1), j & 1, 2};
+  }
+  return SplitPos{(int)(blockIdx.y * gridDim.x + blockIdx.x), (int)blockIdx.z, p.splitk};
+}
 
 __device__ __forceinline__ int row_of(const GemmParams& p, int m) {
   m = m < p.M ? m : p.M - 1;  // clamp: duplicated rows are computed but never stored
@@ -341,18 +360,19 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
       for (int j = 0; j < NTB; ++j) red4[wid * SLOTS + (mb * NTB + j) * 64 + lane] = acc[mb][j];
     __syncthreads();
   }
-  const int tile = blockIdx.y * gridDim.x + blockIdx.x;
-  if (p.splitk > 1) {
+  const SplitPos sp = split_pos(p);
+  const int tile = sp.tile;
+  if (sp.nsl > 1) {
     // 1) this slice's partial tile -> fp32 slab [tile][slice][SLOTS]; under NORM also the
     //    slice's per-row partial sum of squares -> [tile][slice][16*MB] after all slabs
     //    (the row scale is applied to the summed tile: y = rsqrt(sum ss / K + eps) * sum acc)
-    const uint32_t slab_off = (uint32_t)(((size_t)tile * p.splitk + blockIdx.z) * SLOTS * 16);  // bytes
+    const uint32_t slab_off = (uint32_t)(((size_t)tile * p.splitk + sp.slice) * SLOTS * 16);  // bytes
     float* ssq_all = p.slabs + (size_t)gridDim.x * gridDim.y * p.splitk * SLOTS * 4;
     if constexpr (NORM) {
       if (threadIdx.x < 16 * MB) {
         float ss = 0.f;
         for (int w = 0; w < nw; ++w) ss += ssqw[w * 16 * MB + threadIdx.x];
-        st_sc1(ssq_all + ((size_t)tile * p.splitk + blockIdx.z) * 16 * MB + threadIdx.x, ss);
+        st_sc1(ssq_all + ((size_t)tile * p.splitk + sp.slice) * 16 * MB + threadIdx.x, ss);
       }
     }
     for (int s = threadIdx.x; s < SLOTS; s += blockDim.x) {
@@ -376,7 +396,7 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
     __syncthreads();
     if (threadIdx.x == 0) {
       const uint32_t old = __hip_atomic_fetch_add(p.counters + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = (old == (uint32_t)(p.splitk - 1));
+      const int last = (old == (uint32_t)(sp.nsl - 1));
       if (last) __hip_atomic_store(p.counters + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *flag = last;
     }
@@ -395,22 +415,22 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
         f32x4 r[SK_MAX];
 #pragma unroll
         for (int z = 0; z < SK_MAX; ++z)
-          r[z] = ld_sc1_x4(p.slabs, all_off + (uint32_t)(((min(z, p.splitk - 1)) * SLOTS + (mb * NTB + j) * 64 + l) * 16));
+          r[z] = ld_sc1_x4(p.slabs, all_off + (uint32_t)(((min(z, sp.nsl - 1)) * SLOTS + (mb * NTB + j) * 64 + l) * 16));
         f32x4 t = r[0];
 #pragma unroll
         for (int z = 1; z < SK_MAX; ++z)
-          if (z < p.splitk) t += r[z];
+          if (z < sp.nsl) t += r[z];
         v[j] = t;
       }
       if constexpr (NORM) {
         float sv[SK_MAX];
 #pragma unroll
         for (int z = 0; z < SK_MAX; ++z)
-          sv[z] = ld_sc1(ssq_all + ((size_t)tile * p.splitk + min(z, p.splitk - 1)) * 16 * MB + mb * 16 + (l & 15));
+          sv[z] = ld_sc1(ssq_all + ((size_t)tile * p.splitk + min(z, sp.nsl - 1)) * 16 * MB + mb * 16 + (l & 15));
         float ss = sv[0];  // fixed slice order: bit-reproducible
 #pragma unroll
         for (int z = 1; z < SK_MAX; ++z)
-          if (z < p.splitk) ss += sv[z];
+          if (z < sp.nsl) ss += sv[z];
         const float sc = rsqrtf(ss / (float)p.K + p.eps);
 #pragma unroll
         for (int j = 0; j < NTB; ++j) v[j] *= sc;

@@ -99,6 +99,7 @@ void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, 
 // Default-policy read sweep of [p, p + bytes) over `blocks` workgroups (MALL warm-up).
 void launch_prefetch(const void* p, size_t bytes, int blocks, hipStream_t st);
 // bytes % 16 == 0; src / dst device pointers (pinned host memory: its device-mapped address)
+void set_tail_split(int on);  // decode GEMM tail split on / off (-1: VGATE_TAIL_SPLIT env, default on)
 void launch_copy16(const void* src, void* dst, size_t bytes, bool to_host, hipStream_t st);
 // ids[0, n) -> ring[*slot * stride + i] (ring: device-mapped pinned host memory)
 void launch_ids_to_host(const int32_t* ids, int32_t* ring, const int32_t* slot, int stride, int n, hipStream_t st);

@@ -608,6 +608,7 @@ PYBIND11_MODULE(_C, m) {
         "rejection rounds the sampler runs as their own launches before the in-launch fallback (experiments)");
   m.def("kernel_copy", &kernel_copy, "pinned host <-> device copy by a kernel on the current stream (no SDMA)",
         py::arg("dst"), py::arg("src"), py::arg("nbytes"));
+  m.def("set_tail_split", &vgate::set_tail_split, "decode GEMM tail split: 1 on, 0 off, -1 environment (tests / sweeps)");
   m.def("ids_to_host", &ids_to_host, "sampled ids -> slot *slot of a pinned host ring (graph-capturable, device-read slot)",
         py::arg("ids"), py::arg("ring"), py::arg("slot"), py::arg("n"));
   m.def("prefetch", &prefetch, "read a tensor once with the default cache policy (MALL warm-up)",

@@ -1017,3 +1017,36 @@ def test_tune_prefill_plans_match_heuristic_results():
             y0 = ops.linear(x, lin, residual=res)
             lin.prefill_plan = plan
             assert _rel_err(y, y0) < 1e-2, (lin.layout, M)
+
+
+@pytest.mark.parametrize("M", [1, 8, 16])
+def test_decode_gemm_tail_split(M):
+    """Decode GEMMs over more column tiles than CUs (q * CUs + r, r <= CUs / 2) cut the r tail tiles
+    into K halves combined by the last-arriver slab hand-off: == the one-slice grid within split-K
+    rounding for residual, SiLU (folded-norm row scale) and the row-gathered f32 LM-head form."""
+    C = ops.native()
+    torch.manual_seed(500 + M)
+    K = 1536
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    N = 16 * (4 * ncu + 96)  # 4 tiles per CU + a 96-tile tail
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    res = torch.randn(M, N, device=DEV).bfloat16()
+    nw = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+    xn, _ = ref.rmsnorm_ref(x, nw, 1e-6)
+    cases = [("plain", dict(residual=res), ref.linear_ref(x, w, None, res)),
+             ("silu", dict(norm=(nw, 1e-6)), ref.silu_mul_linear_ref(xn, w[: N // 2], w[N // 2:])),
+             ("f32", dict(out_f32=True, norm=(nw, 1e-6)), ref.linear_ref(xn, w, out_f32=True))]
+    try:
+        for kind, kw, want in cases:
+            lin = ops.Linear(w, kind="silu" if kind == "silu" else "plain")
+            if kind == "silu":
+                lin.fold_norm(nw)
+            outs = []
+            for on in (1, 0):
+                C.set_tail_split(on)
+                outs.append(ops.linear(x, lin, **kw))
+            assert _rel_err(outs[0], want) < 2e-2, kind
+            assert _rel_err(outs[0], outs[1]) < 1e-2, kind
+    finally:
+        C.set_tail_split(-1)

@@ -25,6 +25,7 @@ def native():
     try:
         from vgate import _C as mod  # type: ignore
         _C = mod
+        _configure(mod)
     except ImportError as e:  # pragma: no cover - depends on build state
         if os.environ.get("VGATE_AUTOBUILD", "1") == "1":
             try:
@@ -35,6 +36,7 @@ def native():
                 import build as _build  # type: ignore
                 _build.build(verbose=False)
                 _C = importlib.import_module("vgate._C")
+                _configure(_C)
                 return _C
             except Exception as e2:  # noqa: BLE001
                 _C_ERR = e2
@@ -42,6 +44,14 @@ def native():
             _C_ERR = e
         raise RuntimeError(f"vgate native extension unavailable: {_C_ERR}") from _C_ERR
     return _C
+
+
+def _configure(mod) -> None:
+    """Runtime knobs of the extension that default from the environment on the Python side.
+    VGATE_TAIL_SPLIT: decode GEMMs over q * CUs + r column tiles run the r tail tiles as K halves
+    (csrc/kernels/gemm.hip launch_one / launch_awq_stream)."""
+    if hasattr(mod, "set_tail_split"):
+        mod.set_tail_split(int(os.environ.get("VGATE_TAIL_SPLIT", "0")))
 
 
 def native_available() -> bool:
