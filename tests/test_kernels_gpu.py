@@ -1049,4 +1049,4 @@ def test_decode_gemm_tail_split(M):
             assert _rel_err(outs[0], want) < 2e-2, kind
             assert _rel_err(outs[0], outs[1]) < 1e-2, kind
     finally:
-        C.set_tail_split(-1)
+        ops._configure(C)  # back to the process default (VGATE_TAIL_SPLIT)
