@@ -49,9 +49,14 @@ def native():
 def _configure(mod) -> None:
     """Runtime knobs of the extension that default from the environment on the Python side.
     VGATE_TAIL_SPLIT: decode GEMMs over q * CUs + r column tiles run the r tail tiles as K halves
-    (csrc/kernels/gemm.hip launch_one / launch_awq_stream)."""
+    (csrc/kernels/gemm.hip launch_one / launch_awq_stream; measured slower, off by default:
+    profiles/r2_tail_split_negative.log)."""
     if hasattr(mod, "set_tail_split"):
         mod.set_tail_split(int(os.environ.get("VGATE_TAIL_SPLIT", "0")))
+    # VGATE_SAMPLE_ROUND_LAUNCHES: top-k / top-p rejection rounds run as their own launches before
+    # the in-launch fallback (csrc/kernels/sampling.hip launch_sample; unset = the built-in 2)
+    if "VGATE_SAMPLE_ROUND_LAUNCHES" in os.environ and hasattr(mod, "set_sample_round_launches"):
+        mod.set_sample_round_launches(int(os.environ["VGATE_SAMPLE_ROUND_LAUNCHES"]))
 
 
 def native_available() -> bool:
