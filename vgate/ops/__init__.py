@@ -54,9 +54,11 @@ def _configure(mod) -> None:
     if hasattr(mod, "set_tail_split"):
         mod.set_tail_split(int(os.environ.get("VGATE_TAIL_SPLIT", "0")))
     # VGATE_SAMPLE_ROUND_LAUNCHES: top-k / top-p rejection rounds run as their own launches before
-    # the in-launch fallback (csrc/kernels/sampling.hip launch_sample; unset = the built-in 2)
-    if "VGATE_SAMPLE_ROUND_LAUNCHES" in os.environ and hasattr(mod, "set_sample_round_launches"):
-        mod.set_sample_round_launches(int(os.environ["VGATE_SAMPLE_ROUND_LAUNCHES"]))
+    # the in-launch fallback (csrc/kernels/sampling.hip launch_sample). 1: the bench A/B measured
+    # 93.1 / 93.2 req/s at 1 vs 92.3 / 93.0 at 2 and 92.4 at 3, sampler_probe 31.1 vs 32.5 us
+    # (profiles/r2_sampler_round_launches.log)
+    if hasattr(mod, "set_sample_round_launches"):
+        mod.set_sample_round_launches(int(os.environ.get("VGATE_SAMPLE_ROUND_LAUNCHES", "1")))
 
 
 def native_available() -> bool:
