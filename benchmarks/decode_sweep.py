@@ -25,12 +25,14 @@ from vgate.runtime.engine import EngineConfig, LLMEngine  # noqa: E402
 from vgate.runtime.sampling_params import SamplingParams  # noqa: E402
 
 CANDIDATES = {
-    "qkv": [(0, 0, 0), (8, 1, 0), (4, 1, 0), (8, 2, 0), (4, 2, 0), (4, 4, 0), (2, 4, 0), (8, 4, 0)],
-    "o": [(0, 0, 0), (8, 1, 1), (4, 1, 1), (8, 2, 1), (4, 2, 1), (4, 3, 1), (4, 4, 1), (2, 4, 1), (8, 4, 1)],
-    "gate_up": [(0, 0, 0), (4, 1, 0), (2, 1, 0), (1, 1, 0), (2, 2, 0), (2, 1, 2), (4, 1, 2), (8, 1, 2), (4, 1, 4),
-                (8, 1, 4)],
+    "qkv": [(0, 0, 0), (8, 1, 0), (4, 1, 0), (8, 2, 0), (4, 2, 0), (4, 4, 0), (2, 4, 0), (8, 4, 0), (2, 2, 0),
+            (1, 4, 0)],
+    "o": [(0, 0, 0), (8, 1, 1), (4, 1, 1), (8, 2, 1), (4, 2, 1), (4, 3, 1), (4, 4, 1), (2, 4, 1), (8, 4, 1),
+          (2, 8, 1), (1, 8, 1)],
+    "gate_up": [(0, 0, 0), (4, 1, 0), (2, 1, 0), (1, 1, 0), (8, 1, 0), (2, 2, 0), (1, 2, 0), (2, 1, 2), (4, 1, 2),
+                (8, 1, 2), (4, 1, 4), (8, 1, 4)],
     "down": [(0, 0, 0), (8, 2, 1), (8, 3, 1), (8, 4, 1), (4, 4, 1), (4, 6, 1), (4, 8, 1), (8, 8, 1),
-             (2, 8, 1)],
+             (2, 8, 1), (1, 8, 1), (4, 5, 1), (8, 6, 1), (2, 6, 1)],
     "lm_head": [(0, 0, 0), (8, 1, 2), (4, 1, 2), (2, 1, 2), (1, 1, 2), (4, 1, 4), (2, 1, 1), (4, 1, 1)],
 }
 
@@ -76,6 +78,7 @@ def main():
     ap.add_argument("--iters", type=int, default=100)
     ap.add_argument("--kinds", default="qkv,o,gate_up,down,lm_head")
     ap.add_argument("--quantization", default=None)
+    ap.add_argument("--baseline-only", action="store_true", help="time the default plans only")
     a = ap.parse_args()
     eng = LLMEngine(EngineConfig(model=a.model, device="cuda:0", max_model_len=2048, max_num_seqs=64,
                                  max_num_batched_tokens=2048, num_kv_blocks=2048, warmup=False,
@@ -91,6 +94,10 @@ def main():
         eng.step()
     base = time_step(eng, a.iters)
     print(json.dumps({"baseline_us": round(base, 1)}), flush=True)
+    if a.baseline_only:
+        for _ in range(2):
+            print(json.dumps({"repeat_us": round(time_step(eng, a.iters), 1)}), flush=True)
+        return
     best = {}
     for kind in a.kinds.split(","):
         res = []

@@ -28,12 +28,15 @@
 //
 // hipGraph-capturable: all addresses are fixed kernel arguments, the epoch lives in
 // device memory.
+#include <cstddef>
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 
 namespace vgate {
 
-constexpr int AR_BLOCKS = 64;
+constexpr int AR_BLOCKS = 128;  // signal-area capacity; a launch uses ar_blocks() of them
 constexpr int AR_MAX_RANKS = 8;
 constexpr int AR_THREADS = 512;
 constexpr unsigned AR_SPIN_LIMIT = 1u << 22;  // ~4M uncached polls: seconds, not minutes
@@ -42,7 +45,12 @@ struct ArSignal {
   uint32_t flags[AR_BLOCKS][AR_MAX_RANKS];
   uint32_t epoch[AR_BLOCKS];
   uint32_t error;
-  uint32_t pad[AR_BLOCKS - 1];
+  // collective time accounting (metrics: vgate_engine_allreduce_seconds): block 0 of every call
+  // adds its entry -> exit span in 100 MHz s_memrealtime ticks (wraps; the host takes deltas)
+  // and bumps the call count; the step graph's last node copies both to the host with the ids
+  uint32_t ticks;
+  uint32_t calls;
+  uint32_t pad[AR_BLOCKS - 3];
   uint32_t flags2[AR_BLOCKS][AR_MAX_RANKS];  // two-shot: "my reduced slice is in my buffer"
   uint32_t flags3[AR_BLOCKS][AR_MAX_RANKS];  // all-gather: "my input slice is in my buffer"
 };
@@ -52,18 +60,48 @@ struct ArPeers {
   char* base[AR_MAX_RANKS];  // every rank's mapped allocation (own one included)
 };
 
+// block 0, thread 0: the call's span (entry -> exit, peers' waits included) into the own signal area
+struct ArClock {
+  ArSignal* me;
+  unsigned long long t0;
+  __device__ __forceinline__ explicit ArClock(ArSignal* s) : me(s), t0(0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) t0 = __builtin_amdgcn_s_memrealtime();
+  }
+  __device__ __forceinline__ ~ArClock() {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      const uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t0);
+      __hip_atomic_fetch_add(&me->ticks, dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&me->calls, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+};
+
+// blocks per call: VGATE_AR_BLOCKS (16..128, read once per process, so every rank of a group
+// launched with the same environment agrees; benchmarks/ar_bench.py sweeps it), default 64
+static int ar_blocks() {
+  static const int n = [] {
+    const char* e = getenv("VGATE_AR_BLOCKS");
+    int v = e ? atoi(e) : 64;
+    if (v < 8) v = 8;
+    if (v > AR_BLOCKS) v = AR_BLOCKS;
+    return v;
+  }();
+  return n;
+}
+
 __global__ __launch_bounds__(AR_THREADS) void ar_one_shot_kernel(const uint4* in, uint4* out,  // may alias
                                                                ArPeers peers, int rank, int world,
                                                                int64_t n16, int64_t max_bytes) {
-  const int b = blockIdx.x, tid = threadIdx.x;
+  const int b = blockIdx.x, tid = threadIdx.x, nblk = gridDim.x;
   ArSignal* me = reinterpret_cast<ArSignal*>(peers.base[rank]);
+  const ArClock clk(me);
   __shared__ uint32_t s_epoch;
   if (tid == 0) s_epoch = me->epoch[b] + 1;
   __syncthreads();
   const uint32_t e = s_epoch;
   const int64_t par_off = AR_SIGNAL_BYTES + (int64_t)(e & 1) * max_bytes;
   // this block's slice of 16-byte vectors
-  const int64_t per = (n16 + AR_BLOCKS - 1) / AR_BLOCKS;
+  const int64_t per = (n16 + nblk - 1) / nblk;
   const int64_t i0 = (int64_t)b * per, i1 = min(n16, i0 + per);
   uint4* mine = reinterpret_cast<uint4*>(peers.base[rank] + par_off);
   for (int64_t i = i0 + tid; i < i1; i += AR_THREADS) mine[i] = in[i];
@@ -139,8 +177,9 @@ __device__ __forceinline__ void ar_wait_all(uint32_t (*flags)[AR_MAX_RANKS], int
 // e+1 (writing the other parity) before I arrive there, i.e. before I finished reading call e.
 __global__ __launch_bounds__(AR_THREADS) void ar_two_shot_kernel(const uint4* in, uint4* out, ArPeers peers,
                                                                int rank, int world, int64_t n16, int64_t max_bytes) {
-  const int b = blockIdx.x, tid = threadIdx.x;
+  const int b = blockIdx.x, tid = threadIdx.x, nblk = gridDim.x;
   ArSignal* me = reinterpret_cast<ArSignal*>(peers.base[rank]);
+  const ArClock clk(me);
   __shared__ uint32_t s_epoch;
   if (tid == 0) s_epoch = me->epoch[b] + 1;
   __syncthreads();
@@ -148,7 +187,7 @@ __global__ __launch_bounds__(AR_THREADS) void ar_two_shot_kernel(const uint4* in
   const int64_t par_off = AR_SIGNAL_BYTES + (int64_t)(e & 1) * max_bytes;
   auto slice = [&](int r, int64_t& a, int64_t& z) {  // sub-range b of rank r's slice
     const int64_t s0 = n16 * r / world, s1 = n16 * (r + 1) / world;
-    const int64_t per = (s1 - s0 + AR_BLOCKS - 1) / AR_BLOCKS;
+    const int64_t per = (s1 - s0 + nblk - 1) / nblk;
     a = min(s1, s0 + (int64_t)b * per);
     z = min(s1, a + per);
   };
@@ -214,14 +253,15 @@ __global__ __launch_bounds__(AR_THREADS) void ar_two_shot_kernel(const uint4* in
 // the call is captured into the TP decode hipGraphs (a gloo or RCCL all-gather is not needed).
 __global__ __launch_bounds__(AR_THREADS) void ar_all_gather_kernel(const uint4* in, uint4* out, ArPeers peers,
                                                                  int rank, int world, int64_t n16, int64_t max_bytes) {
-  const int b = blockIdx.x, tid = threadIdx.x;
+  const int b = blockIdx.x, tid = threadIdx.x, nblk = gridDim.x;
   ArSignal* me = reinterpret_cast<ArSignal*>(peers.base[rank]);
+  const ArClock clk(me);
   __shared__ uint32_t s_epoch;
   if (tid == 0) s_epoch = me->epoch[b] + 1;
   __syncthreads();
   const uint32_t e = s_epoch;
   const int64_t par_off = AR_SIGNAL_BYTES + (int64_t)(e & 1) * max_bytes;
-  const int64_t per = (n16 + AR_BLOCKS - 1) / AR_BLOCKS;
+  const int64_t per = (n16 + nblk - 1) / nblk;
   const int64_t i0 = min(n16, (int64_t)b * per), i1 = min(n16, i0 + per);
   uint4* mine = reinterpret_cast<uint4*>(peers.base[rank] + par_off);
   for (int64_t i = i0 + tid; i < i1; i += AR_THREADS) mine[i] = in[i];
@@ -239,11 +279,16 @@ __global__ __launch_bounds__(AR_THREADS) void ar_all_gather_kernel(const uint4* 
   if (tid == 0) me->epoch[b] = e;
 }
 
+int64_t ar_error_offset() { return (int64_t)offsetof(ArSignal, error); }
+int64_t ar_blocks_used() { return ar_blocks(); }
+static_assert(offsetof(ArSignal, ticks) == offsetof(ArSignal, error) + 4 && offsetof(ArSignal, calls) == offsetof(ArSignal, error) + 8,
+              "ids_to_host copies {error, ticks, calls} as consecutive words");
+
 void launch_custom_allgather(const void* in, void* out, int64_t nbytes, char* const* bases, int rank, int world,
                              int64_t max_bytes, hipStream_t st) {
   ArPeers peers{};
   for (int p = 0; p < world && p < AR_MAX_RANKS; ++p) peers.base[p] = bases[p];
-  hipLaunchKernelGGL(ar_all_gather_kernel, dim3(AR_BLOCKS), dim3(AR_THREADS), 0, st,
+  hipLaunchKernelGGL(ar_all_gather_kernel, dim3(ar_blocks()), dim3(AR_THREADS), 0, st,
                      reinterpret_cast<const uint4*>(in), reinterpret_cast<uint4*>(out), peers, rank, world,
                      nbytes / 16, max_bytes);
 }
@@ -257,11 +302,11 @@ void launch_custom_allreduce(const void* in, void* out, int64_t nbytes, char* co
   // one-shot, > 0 forces two-shot (tests)
   const bool two = two_shot > 0 || (two_shot == 0 && world > 2 && nbytes > (512 << 10));
   if (two)
-    hipLaunchKernelGGL(ar_two_shot_kernel, dim3(AR_BLOCKS), dim3(AR_THREADS), 0, st,
+    hipLaunchKernelGGL(ar_two_shot_kernel, dim3(ar_blocks()), dim3(AR_THREADS), 0, st,
                        reinterpret_cast<const uint4*>(in), reinterpret_cast<uint4*>(out), peers, rank, world,
                        nbytes / 16, max_bytes);
   else
-    hipLaunchKernelGGL(ar_one_shot_kernel, dim3(AR_BLOCKS), dim3(AR_THREADS), 0, st,
+    hipLaunchKernelGGL(ar_one_shot_kernel, dim3(ar_blocks()), dim3(AR_THREADS), 0, st,
                        reinterpret_cast<const uint4*>(in), reinterpret_cast<uint4*>(out), peers, rank, world,
                        nbytes / 16, max_bytes);
 }

@@ -1,0 +1,8 @@
+// EPI_QKV instantiations of the decode / small-M GEMM family (gemm_decode.h), one translation unit
+// per epilogue so the kernel variants compile in parallel (csrc/build.py).
+#include "gemm_decode.h"
+
+namespace vgate {
+template void dispatch_epi<EPI_QKV, false>(GemmParams, const GemmArgs&, hipStream_t);
+template void dispatch_epi<EPI_QKV, true>(GemmParams, const GemmArgs&, hipStream_t);
+}  // namespace vgate

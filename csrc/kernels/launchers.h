@@ -75,6 +75,9 @@ void launch_custom_allreduce(const void* in, void* out, int64_t nbytes, char* co
 // all-gather over the same buffers: out = [rank 0's in | rank 1's in | ...] (nbytes each)
 void launch_custom_allgather(const void* in, void* out, int64_t nbytes, char* const* bases, int rank, int world,
                              int64_t max_bytes, hipStream_t st);
+// byte offsets in the signal area: the sticky wait-timeout word, then {ticks, calls} (ArSignal)
+int64_t ar_error_offset();
+int64_t ar_blocks_used();
 
 // ---- launch timeline (profiling; csrc/runtime/timeline.cpp, benchmarks/timeline.py) ----
 // While a timeline is active every launcher takes 2 x blocks u64 stamps for its kernel
@@ -99,10 +102,14 @@ void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, 
 // Default-policy read sweep of [p, p + bytes) over `blocks` workgroups (MALL warm-up).
 void launch_prefetch(const void* p, size_t bytes, int blocks, hipStream_t st);
 // bytes % 16 == 0; src / dst device pointers (pinned host memory: its device-mapped address)
-void set_tail_split(int on);  // decode GEMM tail split on / off (-1: VGATE_TAIL_SPLIT env, default on)
+void set_tail_split(int on);
+void set_dec_u(int u);  // decode GEMM register group: 0 auto, -1 round-2 rule, 6/8/10/12 forced, -100 env  // decode GEMM tail split on / off (-1: VGATE_TAIL_SPLIT env, default on)
 void launch_copy16(const void* src, void* dst, size_t bytes, bool to_host, hipStream_t st);
-// ids[0, n) -> ring[*slot * stride + i] (ring: device-mapped pinned host memory)
-void launch_ids_to_host(const int32_t* ids, int32_t* ring, const int32_t* slot, int stride, int n, hipStream_t st);
+// ids[0, n) -> ring[*slot * stride + i] (ring: device-mapped pinned host memory); with `ar` (the
+// own custom all-reduce signal area's error word, or null) also its {error, ticks, calls} words ->
+// ring[*slot * stride + stride - 4 + {0, 1, 2}] (the TP collective health / time, no host sync)
+void launch_ids_to_host(const int32_t* ids, int32_t* ring, const int32_t* slot, int stride, int n, hipStream_t st,
+                        const uint32_t* ar = nullptr);
 
 // NeoX RoPE on q,k inside the fused qkv buffer + paged KV-cache write.
 // qkv: [T, (Hq + 2*Hkv) * D]; cos_sin: [max_pos, D] f32 (cos | sin halves)

@@ -456,14 +456,17 @@ void kernel_copy(Tensor& dst, const Tensor& src, int64_t nbytes) {
   vgate::launch_copy16(device_view(src), device_view(dst), (size_t)n, !dst.is_cuda(), cur_stream());
 }
 
-void ids_to_host(const Tensor& ids, Tensor& ring, const Tensor& slot, int64_t n) {
+void ids_to_host(const Tensor& ids, Tensor& ring, const Tensor& slot, int64_t n, int64_t ar_base) {
   CHECK_DEV(ids); CHECK_DEV(slot);
   CHECK_DT(ids, torch::kInt32); CHECK_DT(ring, torch::kInt32); CHECK_DT(slot, torch::kInt32);
   TORCH_CHECK(ring.dim() == 2 && ring.is_contiguous() && !ring.is_cuda(), "ids_to_host: ring = pinned int32 [slots, stride]");
   TORCH_CHECK(n >= 0 && n <= ids.numel() && n <= ring.size(1), "ids_to_host: n exceeds ids or a ring slot");
+  TORCH_CHECK(ar_base == 0 || n <= ring.size(1) - 4, "ids_to_host: the all-reduce words need the slot's last 4 ints");
+  const uint32_t* ar = ar_base ? reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(ar_base) + vgate::ar_error_offset())
+                               : nullptr;
   c10::DeviceGuard guard(ids.device());
   vgate::launch_ids_to_host(reinterpret_cast<const int32_t*>(ids.data_ptr()), reinterpret_cast<int32_t*>(device_view(ring)),
-                            reinterpret_cast<const int32_t*>(slot.data_ptr()), (int)ring.size(1), (int)n, cur_stream());
+                            reinterpret_cast<const int32_t*>(slot.data_ptr()), (int)ring.size(1), (int)n, cur_stream(), ar);
 }
 
 void prefetch(const Tensor& t, int64_t blocks) {
@@ -521,7 +524,7 @@ void ar_close(int64_t ptr) { HIP_OK(hipIpcCloseMemHandle(reinterpret_cast<void*>
 // error word of the own signal area (a wait timed out); clears it
 int64_t ar_error(int64_t own_base) {
   uint32_t v = 0, z = 0;
-  const size_t off = 64 * 8 * 4 + 64 * 4;  // ArSignal::error (allreduce.hip)
+  const size_t off = (size_t)vgate::ar_error_offset();
   HIP_OK(hipMemcpy(&v, reinterpret_cast<char*>(own_base) + off, 4, hipMemcpyDeviceToHost));
   if (v) HIP_OK(hipMemcpy(reinterpret_cast<char*>(own_base) + off, &z, 4, hipMemcpyHostToDevice));
   return v;
@@ -609,8 +612,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("kernel_copy", &kernel_copy, "pinned host <-> device copy by a kernel on the current stream (no SDMA)",
         py::arg("dst"), py::arg("src"), py::arg("nbytes"));
   m.def("set_tail_split", &vgate::set_tail_split, "decode GEMM tail split: 1 on, 0 off, -1 environment (tests / sweeps)");
+  m.def("set_dec_u", &vgate::set_dec_u, "decode GEMM register group: 0 auto, -1 round-2 rule, 6/8/10/12 forced, -100 environment");
   m.def("ids_to_host", &ids_to_host, "sampled ids -> slot *slot of a pinned host ring (graph-capturable, device-read slot)",
-        py::arg("ids"), py::arg("ring"), py::arg("slot"), py::arg("n"));
+        py::arg("ids"), py::arg("ring"), py::arg("slot"), py::arg("n"), py::arg("ar_base") = 0);
   m.def("prefetch", &prefetch, "read a tensor once with the default cache policy (MALL warm-up)",
         py::arg("t"), py::arg("blocks") = 256);
   m.def("ar_alloc", &ar_alloc, "uncached device allocation for the custom all-reduce (zeroed)");
@@ -619,6 +623,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("ar_open", &ar_open, "map a peer's ar_alloc buffer (hipIpcOpenMemHandle)");
   m.def("ar_close", &ar_close);
   m.def("ar_error", &ar_error, "read-and-clear the wait-timeout word of the own signal area");
+  m.def("ar_blocks", &vgate::ar_blocks_used, "workgroups per custom all-reduce call (VGATE_AR_BLOCKS)");
   m.def("custom_allreduce", &custom_allreduce, "one-shot bf16 all-reduce over IPC-mapped peer buffers",
         py::arg("inp"), py::arg("out"), py::arg("bases"), py::arg("rank"), py::arg("max_bytes"),
         py::arg("two_shot") = 0);

@@ -1050,3 +1050,42 @@ def test_decode_gemm_tail_split(M):
             assert _rel_err(outs[0], outs[1]) < 1e-2, kind
     finally:
         ops._configure(C)  # back to the process default (VGATE_TAIL_SPLIT)
+
+
+@pytest.mark.parametrize("M", [3, 8, 12])
+def test_decode_gemm_register_groups_bit_identical(M):
+    """The decode GEMM's register group size (k-steps per in-flight group: auto, the round-2
+    rule, forced 6 / 8 / 10 / 12) changes only how the loads are batched, never the per-wave
+    accumulation order: every size gives the same bits, and matches the fp32 reference
+    (down_proj shape with residual + split-K, gate_up SiLU with folded RMSNorm)."""
+    C = ops.native()
+    torch.manual_seed(70 + M)
+    try:
+        for N, K, kind, waves, splitk in ((1536, 8960, "plain", 8, 2), (1024, 1536, "silu", 2, 1),
+                                          (2048, 1536, "plain", 8, 1)):
+            x = torch.randn(M, K, device=DEV).bfloat16()
+            w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+            g = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+            lin = ops.Linear(w, kind=kind) if kind == "silu" else ops.Linear(w)
+            if kind == "silu":
+                lin.fold_norm(g)
+            res = torch.randn(M, N // (2 if kind == "silu" else 1), device=DEV).bfloat16()
+            outs = []
+            for u in (0, -1, 6, 8, 10, 12):
+                C.set_dec_u(u)
+                if kind == "silu":
+                    y = ops.linear(x, lin, norm=(g, 1e-6), waves=waves, splitk=splitk)
+                else:
+                    y = res.clone()
+                    ops.linear(x, lin, out=y, residual=y, waves=waves, splitk=splitk)
+                outs.append(y)
+            for u, y in zip((0, -1, 6, 8, 10, 12), outs):
+                assert torch.equal(y, outs[0]), (N, K, kind, u)
+            if kind == "silu":
+                xn, _ = ref.rmsnorm_ref(x.cpu(), g.cpu(), 1e-6)
+                r = ref.silu_mul_linear_ref(xn, w.cpu()[: N // 2], w.cpu()[N // 2:])
+            else:
+                r = ref.linear_ref(x.cpu(), w.cpu(), None, res.cpu())
+            assert _rel_err(outs[0].float().cpu(), r.float()) < 1e-2, (N, K, kind)
+    finally:
+        C.set_dec_u(-100)

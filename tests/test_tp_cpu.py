@@ -191,3 +191,61 @@ def test_tp_follower_fault_tears_down_group(tmp_path):
     kind, val = q.get(timeout=200)
     assert kind == "rank0" and val != "no error", (kind, val)
     procs[0].join(timeout=60)
+
+
+def _idle_worker(rank, world, port, path, q, idle_s):
+    try:
+        os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(port), VGATE_TP_TIMEOUT_S="2")
+        torch.set_num_threads(1)
+        eng = LLMEngine(_cfg(path, world))
+        if rank != 0:
+            eng.follower_loop()  # os._exit(1) if it sees no heartbeat for 2 s
+            q.put(("ok", None))
+            return
+        import threading
+        import time as _t
+        eng.start()  # the serving loop: idle, waiting for requests
+        _t.sleep(idle_s)
+        done, ev = {}, threading.Event()
+
+        def cb(kind, seq, payload):
+            if kind in ("finish", "error"):
+                done[seq.request_id] = (kind, list(seq.output_ids))
+                if len(done) == len(PROMPTS):
+                    ev.set()
+
+        sp = SamplingParams(temperature=0.0, max_tokens=4, ignore_eos=True)
+        for rid, ids in PROMPTS.items():
+            eng.add_request(rid, params=sp, callback=cb, prompt_ids=ids)
+        ok = ev.wait(60)
+        eng.stop()
+        q.put(("ok", {"finished": ok, "done": done}))
+    except Exception:  # noqa: BLE001
+        q.put(("err", traceback.format_exc()))
+
+
+@pytest.mark.timeout(300)
+def test_tp_group_survives_idle_longer_than_timeout(tmp_path):
+    """ROUND-2 ADVICE (high): rank 0 must stamp the step-ring heartbeat while its serving loop
+    idles, else every follower's ring wait times out after VGATE_TP_TIMEOUT_S and the group
+    tears itself down. Idle 5 s at a 2 s timeout, then serve: every request completes."""
+    ref_eng = LLMEngine(EngineConfig(model="tiny", device="cpu", max_model_len=256, max_num_seqs=8,
+                                     max_num_batched_tokens=64, num_kv_blocks=128, warmup=False, seed=0))
+    path = str(tmp_path / "ckpt")
+    save_checkpoint(ref_eng.model, path)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_idle_worker, args=(r, 2, port, path, q, 5.0)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=200) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    errs = [r[1] for r in results if r[0] == "err"]
+    assert not errs, errs[0]
+    out = next(r[1] for r in results if r[1] is not None)
+    assert out["finished"], out
+    assert all(kind == "finish" and len(ids) == 4 for kind, ids in out["done"].values()), out
+    assert procs[1].exitcode == 0

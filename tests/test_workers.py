@@ -397,3 +397,47 @@ def test_native_backend_watchdog_is_configurable():
     assert not nb.healthy()
     _Eng.has_unfinished = lambda self: False  # idle engines are never flagged
     assert nb.healthy()
+
+
+async def test_aiohttp_stream_outlives_timeout_and_carries_long_lines():
+    """ROUND-2 ADVICE (medium): an SSE pass-through is bounded by the silence between chunks
+    (worker.timeout_seconds), not by its total lifetime, and a delta line over aiohttp's 64 KiB
+    readline limit is delivered instead of raising. The mock worker streams for ~3x the timeout."""
+    import json as _json
+    import time as _time
+
+    import uvicorn
+    from fastapi import FastAPI
+    from fastapi.responses import StreamingResponse
+
+    app = FastAPI()
+    big = "x" * (100 * 1024)
+
+    @app.post("/internal/generate_stream")
+    async def gen_stream():
+        async def body():
+            for i in range(12):
+                await asyncio.sleep(0.25)
+                yield f"data: {_json.dumps({'delta': str(i), 'num_tokens': i + 1})}\n\n"
+            yield f"data: {_json.dumps({'delta': big, 'num_tokens': 13})}\n\n"
+            yield "data: [DONE]\n\n"
+        return StreamingResponse(body(), media_type="text/event-stream")
+
+    port = _free_port()
+    srv = uvicorn.Server(uvicorn.Config(app, host="127.0.0.1", port=port, log_level="error"))
+    th = threading.Thread(target=srv.run, daemon=True)
+    th.start()
+    t0 = _time.time()
+    while not srv.started and _time.time() - t0 < 20:
+        await asyncio.sleep(0.05)
+    try:
+        be = RemoteBackend(WorkerConfig(endpoints=[f"http://127.0.0.1:{port}"], timeout_seconds=1.0))
+        t1 = _time.time()
+        pieces = [c async for c in be.stream_generate("p", {"max_tokens": 13})]
+        assert _time.time() - t1 > 2.5  # longer than timeout_seconds, still served
+        assert [c["delta"] for c in pieces[:12]] == [str(i) for i in range(12)]
+        assert pieces[-1]["delta"] == big
+        await be.aclose()
+    finally:
+        srv.should_exit = True
+        th.join(timeout=10)

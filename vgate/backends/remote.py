@@ -59,6 +59,10 @@ class _AiohttpTransport:
     def __init__(self, cfg: WorkerConfig, headers: dict):
         import aiohttp
         self._aiohttp = aiohttp
+        # SSE pass-through: no bound on the stream's lifetime (a long generation is legitimate),
+        # timeout_seconds bounds the silence between two chunks instead
+        self._stream_timeout = aiohttp.ClientTimeout(total=None, connect=cfg.connect_timeout_seconds,
+                                                     sock_read=cfg.timeout_seconds)
         self._session = aiohttp.ClientSession(
             connector=aiohttp.TCPConnector(limit=cfg.max_connections, limit_per_host=0, ttl_dns_cache=300),
             timeout=aiohttp.ClientTimeout(total=cfg.timeout_seconds, connect=cfg.connect_timeout_seconds),
@@ -78,17 +82,28 @@ class _AiohttpTransport:
     async def stream_lines(self, url: str, body: dict, headers: dict):
         a = self._aiohttp
         try:
-            cm = self._session.post(url, json=body, headers=headers)
+            cm = self._session.post(url, json=body, headers=headers, timeout=self._stream_timeout)
             try:
                 r = await cm.__aenter__()
             except a.ClientConnectorError as e:
                 raise _ConnectFailed(type(e).__name__) from e
 
             async def lines():
+                # own line splitting over raw chunks: aiohttp's readline() raises ValueError on a
+                # line over its 64 KiB limit (one large SSE delta would kill the stream)
+                buf = b""
                 try:
-                    async for raw in r.content:
-                        yield raw.decode("utf-8", "replace").rstrip("\r\n")
-                except (a.ClientError, asyncio.TimeoutError) as e:
+                    async for chunk in r.content.iter_any():
+                        buf += chunk
+                        while True:
+                            nl = buf.find(b"\n")
+                            if nl < 0:
+                                break
+                            line, buf = buf[:nl], buf[nl + 1:]
+                            yield line.decode("utf-8", "replace").rstrip("\r")
+                    if buf:
+                        yield buf.decode("utf-8", "replace").rstrip("\r")
+                except (a.ClientError, asyncio.TimeoutError, ValueError) as e:
                     raise _RequestFailed(type(e).__name__) from e
             try:
                 yield r.status, (await r.read() if r.status != 200 else b""), lines()

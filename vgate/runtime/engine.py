@@ -290,6 +290,8 @@ class LLMEngine:
                         self.runner.pending_captures.clear()
             with self._cv:
                 while self._running and self._idle() and not self.runner.pending_captures:
+                    if self.ring is not None:  # an idle TP group must not look dead to its followers
+                        self.ring.heartbeat()
                     self._cv.wait(timeout=0.5)
                 if self._idle():
                     continue  # idle with captures pending: back to the capture check
@@ -553,11 +555,21 @@ class LLMEngine:
             raise RuntimeError(f"TP step ring: a follower made no progress for {timeout:.0f}s")
 
     def _check_collectives(self) -> None:
-        """Fail the step (engine unhealthy) if the custom all-reduce gave up waiting for a peer
-        since the last check: its bounded spin reduces stale peer data after a timeout, so the
-        error word is the only signal (rank 0 every step, followers every 64 steps)."""
+        """Fail the step (engine unhealthy) if the custom all-reduce gave up waiting for a peer:
+        its bounded spin reduces stale peer data after a timeout, so the error word is the only
+        signal. Every rank, every step, with no device sync: the step graph's last node copies the
+        sticky error word (and the collective time counters) into the pinned ids ring
+        (ModelRunner.collective_words), so the check is a host memory read (ROUND-2 ADVICE: the
+        blocking hipMemcpy of ``ar.check()`` serialised rank 0 with its in-flight step)."""
         ar = self.tp.custom_ar
         if ar is None:
+            return
+        if self.runner.gpu and self.runner.ar_base:
+            err, secs, calls = self.runner.collective_words()
+            if calls and len(self._ar_ms) < 65536:
+                self._ar_ms.append(1e3 * secs)
+            if err:
+                raise RuntimeError("custom all-reduce: a peer did not arrive within the spin limit")
             return
         self._steps_since_check += 1
         if self._steps_since_check >= self._ar_check_every:

@@ -94,8 +94,14 @@ class ModelRunner:
         if self.gpu:
             # pinned ring the step graph's last node writes the sampled ids into (slot = the
             # launch's double-buffer index, read by the kernel from the step metadata)
-            self.out_ring = torch.zeros(2, self.out_tokens.numel(), dtype=torch.int32, pin_memory=True)
+            # (+4 ints per slot: the custom all-reduce's {error, ticks, calls} words, copied by the
+            # same node, so the TP collective check and its time need no host <-> device sync)
+            self.out_ring = torch.zeros(2, self.out_tokens.numel() + 4, dtype=torch.int32, pin_memory=True)
             self.out_hosts = [self.out_ring[0], self.out_ring[1]]
+            ar = getattr(getattr(model, "tp", None), "custom_ar", None)
+            self.ar_base = int(ar.own) if ar is not None and getattr(ar, "own", None) else 0
+            self._ar_last = (0, 0)  # (ticks, calls) at the last read
+            self._last_collected: int | None = None
             self._launches = 0
             # VGATE_RING_IDS=0: copy the ids after the graph instead (A/B experiments)
             self.ring_ids = os.environ.get("VGATE_RING_IDS", "1") != "0"
@@ -215,7 +221,7 @@ class ModelRunner:
         ops.sample(logits, view.temperature, view.top_p, view.top_k, view.seeds, view.offsets,
                    out=self.out_tokens[: view.S])
         if self.gpu and self.ring_ids:  # last node of the step graph: sampled ids -> pinned ring slot
-            ops.native().ids_to_host(self.out_tokens, self.out_ring, view.ring_slot, view.S)
+            ops.native().ids_to_host(self.out_tokens, self.out_ring, view.ring_slot, view.S, self.ar_base)
         return logits
 
     def _capture(self, T: int, S: int):
@@ -327,7 +333,26 @@ class ModelRunner:
                 self.step_gpu_ms.append(ms)
         toks = self.out_hosts[h.k][: h.ns].tolist()
         self._uncollected[h.k] = False
+        self._last_collected = h.k
         return toks
+
+    def collective_words(self, k: int | None = None) -> tuple[int, float, int]:
+        """(error, seconds, calls) of the custom all-reduce since the previous call, from the words
+        the step graph's last node copied into ring slot ``k`` (default: the last launched one).
+        No device sync: a slot holds a completed step's copy (or an older one; the error word is
+        sticky, so a timeout is reported at most two steps late). (0, 0.0, 0) without TP."""
+        if not self.gpu or not self.ar_base:
+            return 0, 0.0, 0
+        if k is None:  # rank 0: the step just collected; followers (never collect): the last launched
+            k = self._last_collected if self._last_collected is not None else self._k ^ 1
+        w = self.out_ring[k]
+        err, ticks, calls = int(w[-4]), int(w[-3]) & 0xFFFFFFFF, int(w[-2]) & 0xFFFFFFFF
+        t0, c0 = self._ar_last
+        dc = (calls - c0) & 0xFFFFFFFF
+        if dc == 0 or dc > 1 << 30:  # nothing new in this slot (or an older slot than the last read)
+            return err, 0.0, 0
+        self._ar_last = (ticks, calls)
+        return err, ((ticks - t0) & 0xFFFFFFFF) / 1e8, dc
 
     @torch.inference_mode()
     def hidden_states(self, batch: ScheduledBatch) -> torch.Tensor:
