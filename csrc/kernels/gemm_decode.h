@@ -2,6 +2,7 @@
 // translation units (gemm_epi_*.hip) so the ~200 kernel instantiations compile in parallel.
 // Design notes: gemm.hip (file comment).
 #pragma once
+#include <algorithm>
 #include <cstdlib>
 
 #include "gemm_epilogue.h"
@@ -94,7 +95,8 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
     for (int u = 0; u < U; u += XP)  // packed: slot u holds the raw load for k-steps u..u+XP-1
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb)
-        a[u][mb] = xok[mb] ? *reinterpret_cast<const uint4*>(xrow[mb] + min(k0 + u, kend - XP) * 32) : make_uint4(0, 0, 0, 0);
+        a[u][mb] = (xok[mb] && !(p.probe & 1)) ? *reinterpret_cast<const uint4*>(xrow[mb] + min(k0 + u, kend - XP) * 32)
+                                               : make_uint4(0, 0, 0, 0);
   };
   auto unpack_grp = [&](uint4 (&a)[U][MB]) {
     if constexpr (XP > 1) {
@@ -166,6 +168,165 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
   }
   if (epi_thr && !pre_b) epi_pre_b<NTB, EPI>(p, pre, nt0, 4 * (lane >> 4));
   gemm_finish<MB, NTB, EPI, NORM, MB == 1>(p, acc, ssr, smem, m_base, nt0, pre);
+}
+
+// ---- balanced decode GEMM: every CU streams the same bytes (wide N, M <= 16) ----
+// A one-tile-per-block grid of q * ncu + r tiles (gate_up: 1120 = 4 x 256 + 96) leaves r CUs with
+// one tile more than the rest, and the launch lasts as long as those CUs (block durations 8.3 ->
+// 12.4 us, profiles/r3_head0_timeline.log). Here the grid is ONE block per CU (LDS-pinned): block b
+// owns full tiles [q b, q b + q), WPT waves per tile splitting its K, and P = r S / ncu PIECES of the
+// r tail tiles, each tail tile cut into S k-slices (gate_up: S = 8, 3 pieces of 6 k-steps per CU),
+// so every CU moves q tiles + r / ncu of a tile. The pieces run on P extra waves that start with the
+// launch and own nothing else: piece -> sc1 slab -> drain -> ticket, and the piece whose ticket comes
+// last sums the S slabs in piece order and runs the epilogue — all while the full tiles still stream,
+// so the cross-CU combine is off the launch's critical path (a combine at the END costs ~3 us:
+// splitk-seam, MI355X_MICROARCH.md). Fixed summation orders: bit-reproducible.
+template <int U, int EPI, int NORM, int XP>
+__device__ __forceinline__ void bal_stream(const GemmParams& p, const uint4* wbase, int kbeg, int kend, f32x4& acc,
+                                           float& ssr, const bf16_t* xrow, bool xok, int r16) {
+  constexpr int R = 16 / XP;
+  auto load_grp = [&](uint4 (&b)[U], uint4 (&a)[U], int k0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) b[u] = ld_nt16(wbase + (size_t)min(k0 + u, kend - 1) * 64);
+#pragma unroll
+    for (int u = 0; u < U; u += XP)
+      a[u] = (xok && !(p.probe & 1)) ? *reinterpret_cast<const uint4*>(xrow + min(k0 + u, kend - XP) * 32)
+                                     : make_uint4(0, 0, 0, 0);
+  };
+  auto mma_grp = [&](const uint4 (&b)[U], uint4 (&a)[U], int k0) {
+    if constexpr (XP > 1) {
+      const uint32_t lom = r16 < R ? ~0u : 0u;
+#pragma unroll
+      for (int u = 0; u < U; u += XP) {
+        const uint4 v = a[u];
+        const uint4 v1 = row_ror<R>(v);
+        a[u] = and_mask(v, lom);
+        a[u + 1] = and_mask(v1, lom);
+        if constexpr (XP == 4) {
+          const uint4 v2 = row_ror<2 * R>(v), v3 = row_ror<3 * R>(v);
+          a[u + 2] = and_mask(v2, lom);
+          a[u + 3] = and_mask(v3, lom);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (k0 + u >= kend) a[u] = make_uint4(0, 0, 0, 0);
+    if constexpr (NORM == 2) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) a[u] = norm_frag<2>(a[u], nullptr, 0, ssr);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = mfma16(as_bf16x8(b[u]), as_bf16x8(a[u]), acc);
+  };
+  const int ngrp = (kend - kbeg + U - 1) / U;
+  if (ngrp <= 0) return;
+  int kt = kbeg;
+  uint4 b0[U], a0[U], b1[U], a1[U];
+  load_grp(b0, a0, kt);
+  int g = 0;
+  for (; g + 2 <= ngrp; g += 2) {
+    load_grp(b1, a1, kt + U);
+    mma_grp(b0, a0, kt);
+    if (g + 2 < ngrp) load_grp(b0, a0, kt + 2 * U);
+    mma_grp(b1, a1, kt + U);
+    kt += 2 * U;
+  }
+  if (g < ngrp) mma_grp(b0, a0, kt);
+}
+
+// BalArgs packed into GemmParams' spare fields by the launcher: q = full tiles per block, S = slices
+// per tail tile, P = pieces per block, WPT = waves per full tile (blockDim = 64 (q WPT + P))
+template <int U, int EPI, int NORM, int XP>
+__global__ __launch_bounds__(768) void gemm_bal_kernel(GemmParams p, int q, int S, int P, int WPT) {
+  static_assert(NORM == 0 || NORM == 2, "balanced decode GEMM: no norm, or the folded-gamma row scale");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  TLScope tl_scope(p.dbg_ts);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int KT = p.K >> 5;
+  const int ncu = gridDim.x, b = blockIdx.x;
+  const int r16 = lane & 15, m = r16;
+  const int mrow = XP > 1 ? r16 % (16 / XP) : r16;
+  const bool xok = mrow < p.M;
+  const bf16_t* xrow = p.x + (size_t)row_of(p, mrow) * p.lda + 8 * (lane >> 4) + (XP > 1 ? (r16 / (16 / XP)) * 32 : 0);
+  const int nfull = q * WPT;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float ssr = 0.f;
+  f32x4* red = reinterpret_cast<f32x4*>(smem);                       // [nfull][64]
+  float* ssq = reinterpret_cast<float*>(smem + (size_t)nfull * 1024);  // [nfull][16]
+  if (wid >= nfull) {
+    // ---- a piece of a tail tile: k-slice (piece % S) of tail tile q ncu + piece / S ----
+    const int piece = P * b + (wid - nfull);
+    const int tt = q * ncu + piece / S, slice = piece % S;
+    const int kl = KT / S;
+    const uint4* wbase = p.wp + (size_t)tt * KT * 64 + lane;
+    bal_stream<U, EPI, NORM, XP>(p, wbase, slice * kl, slice * kl + kl, acc, ssr, xrow, xok, r16);
+    float ss = ssr;
+    if constexpr (NORM) {
+      ss += xor16(ss);
+      ss += xor32(ss);
+    }
+    // slab [tail tile][slice]: 64 lanes x 16 B partial tile + 16 row sums of squares
+    constexpr int SLAB = 64 * 4 + 16;  // floats
+    const int tidx = tt - q * ncu;
+    float* slab = p.slabs + ((size_t)tidx * S + slice) * SLAB;
+    st_sc1_x4(p.slabs, (uint32_t)(((size_t)tidx * S + slice) * SLAB * 4 + lane * 16), acc);
+    if (NORM && lane < 16) st_sc1(slab + 256 + lane, ss);
+    drain_stores();
+    uint32_t old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(p.counters + tidx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old != (uint32_t)(S - 1)) return;
+    if (lane == 0) __hip_atomic_store(p.counters + tidx, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // last arriver: all S slabs in slice order (every load issued before the first add)
+    const uint32_t base = (uint32_t)((size_t)tidx * S * SLAB * 4);
+    f32x4 r[SK_MAX];
+#pragma unroll
+    for (int z = 0; z < SK_MAX; ++z) r[z] = ld_sc1_x4(p.slabs, base + (uint32_t)(min(z, S - 1) * SLAB * 4 + lane * 16));
+    float sv[SK_MAX];
+    if constexpr (NORM) {
+#pragma unroll
+      for (int z = 0; z < SK_MAX; ++z) sv[z] = ld_sc1(p.slabs + (size_t)tidx * S * SLAB + min(z, S - 1) * SLAB + 256 + m);
+    }
+    f32x4 v[1] = {r[0]};
+    float ss_row = NORM ? sv[0] : 0.f;
+#pragma unroll
+    for (int z = 1; z < SK_MAX; ++z)
+      if (z < S) {
+        v[0] += r[z];
+        if constexpr (NORM) ss_row += sv[z];
+      }
+    if constexpr (NORM) v[0] *= rsqrtf(ss_row / (float)p.K + p.eps);
+    epilogue<1, EPI, false>(p, v, m, tt, 4 * (lane >> 4), EpiPre<1>{}, m < p.M);
+    return;
+  }
+  // ---- a k-range of a full tile ----
+  const int tile = q * b + wid / WPT, part = wid % WPT;
+  const int kr = KT / WPT;
+  const uint4* wbase = p.wp + (size_t)tile * KT * 64 + lane;
+  bal_stream<U, EPI, NORM, XP>(p, wbase, part * kr, part * kr + kr, acc, ssr, xrow, xok, r16);
+  red[wid * 64 + lane] = acc;
+  if constexpr (NORM) {
+    float ss = ssr;
+    ss += xor16(ss);
+    ss += xor32(ss);
+    if (lane < 16) ssq[wid * 16 + lane] = ss;
+  }
+  // the tile's WPT waves meet (LDS only: the piece waves never join, so a named barrier is not
+  // needed — every full-tile wave passes this point once, the piece waves have exited or never wait)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (part != 0) return;
+  const int w0 = wid;
+  f32x4 v[1] = {red[w0 * 64 + lane]};
+  float ss_row = NORM ? ssq[w0 * 16 + m] : 0.f;
+  for (int w = 1; w < WPT; ++w) {
+    v[0] += red[(w0 + w) * 64 + lane];
+    if constexpr (NORM) ss_row += ssq[(w0 + w) * 16 + m];
+  }
+  if constexpr (NORM) v[0] *= rsqrtf(ss_row / (float)p.K + p.eps);
+  epilogue<1, EPI, false>(p, v, m, tile, 4 * (lane >> 4), EpiPre<1>{}, m < p.M);
 }
 
 // ---- AWQ W4A16 ----
@@ -823,6 +984,7 @@ struct Plan { int waves, splitk; };
 
 extern int g_tail_split;  // gemm.hip: -1 = VGATE_TAIL_SPLIT; 0 / 1: set_tail_split (tests)
 extern int g_dec_u;       // gemm.hip: -100 = VGATE_DEC_U; else the forced decode register group size
+extern int g_dec_bal;     // gemm.hip: -1 = VGATE_DEC_BAL; 0 / 1: the balanced decode GEMM off / on
 
 inline int cu_count_gemm() {
   static const int n = [] {
@@ -874,6 +1036,57 @@ static void launch_dec_u(int u, dim3 grid, dim3 block, size_t lds, hipStream_t s
   hipLaunchKernelGGL((gemm_kernel<MB, NTB, U, EPI, NORM, true, XP>), grid, block, lds, st, p);
 }
 
+// Balanced decode GEMM (gemm_bal_kernel) when the shape fits it: wide N (>= one tile per CU), the
+// tail tiles cut into S | KT slices whose pieces spread evenly over the CUs, <= 12 waves per block
+// (the pipelined stream needs ~160 VGPRs: 3 waves per SIMD; at 16 waves it spilled and ran 2x slower).
+// Returns false (caller launches the one-tile-per-block kernel) otherwise, or when switched off
+// (set_dec_bal / VGATE_DEC_BAL=0).
+template <int EPI, int NORM>
+static bool launch_bal(GemmParams p, const GemmArgs& g, hipStream_t st) {
+  if constexpr (!(EPI == EPI_SILU || EPI == EPI_BF16 || EPI == EPI_F32) || !(NORM == 0 || NORM == 2)) {
+    return false;
+  } else {
+    static const int env_bal = [] { const char* e = getenv("VGATE_DEC_BAL"); return e ? atoi(e) : 0; }();
+    if ((g_dec_bal >= 0 ? g_dec_bal : env_bal) == 0) return false;
+    if (g.M > 16 || g.waves > 0 || g.splitk > 0 || g.ntb > 0 || g.row_idx != nullptr || g.slabs == nullptr) return false;
+    const int ncu = cu_count_gemm();
+    const int ntiles = g.N / 16, KT = g.K / 32;
+    const int q = ntiles / ncu, r = ntiles % ncu;
+    if (q < 1) return false;
+    const int xp = g.M <= 4 && KT % 4 == 0 ? 4 : (g.M <= 8 && KT % 2 == 0 ? 2 : 1);
+    int S = 0;
+    if (r == 0) {
+      S = 1;
+    } else {
+      for (int c : {2, 4, 8})
+        if (c <= SK_MAX && (r * c) % ncu == 0 && KT % c == 0 && (KT / c) % xp == 0) { S = c; break; }
+    }
+    if (S == 0) return false;
+    const int P = r == 0 ? 0 : r * S / ncu;
+    int WPT = 0;
+    for (int c : {4, 3, 2, 1})
+      if (KT % c == 0 && (KT / c) % xp == 0 && q * c + P <= 12) { WPT = c; break; }
+    if (WPT == 0) return false;
+    constexpr int SLAB = 64 * 4 + 16;
+    if ((size_t)r * S * SLAB * 4 > g.slab_bytes || r > g.max_counters) return false;
+    const int nw = q * WPT + P;
+    // >= 80 KiB of LDS: one block per CU, so the per-CU byte count is what the grid says
+    const size_t lds = std::max<size_t>((size_t)q * WPT * (1024 + 64), 80 * 1024 + 16);
+    if (p.dbg_ts == nullptr) p.dbg_ts = tl_take(EPI == EPI_SILU ? "gemm_bal_gate_up" : "gemm_bal", ncu);
+    p.splitk = 1;
+    p.tail_full = 0;
+    const int kr = KT / WPT, kl = r ? KT / S : 0;
+    auto slots = [&](int u) { return q * WPT * ((kr + u - 1) / u * u) + P * ((kl + u - 1) / u * u); };
+    const bool u6 = xp != 4 && slots(6) < slots(8);
+#define VG_BAL(UU, XP_) hipLaunchKernelGGL((gemm_bal_kernel<UU, EPI, NORM, XP_>), dim3(ncu), dim3(64 * nw), lds, st, p, q, S, P, WPT)
+    if (xp == 4) VG_BAL(8, 4);
+    else if (xp == 2) { if (u6) VG_BAL(6, 2); else VG_BAL(8, 2); }
+    else { if (u6) VG_BAL(6, 1); else VG_BAL(8, 1); }
+#undef VG_BAL
+    return true;
+  }
+}
+
 template <int MB, int NTB, int EPI, int NORM, bool AWQ>
 static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
   const int ntiles = g.N / 16;
@@ -920,6 +1133,9 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
     else hipLaunchKernelGGL((awq_gemm_kernel<MB, NTB, EPI, NORM>), grid, block, lds, st, p);
   }
   else if constexpr (MB == 1) {
+    if constexpr (NTB == 1) {
+      if (p.tail_full == 0 && pl.splitk == 1 && launch_bal<EPI, NORM>(p, g, st)) return;
+    }
     constexpr int U = NTB == 1 ? 8 : 4;
     const int KT = g.K / 32;
     // One-tile blocks: the register group size U is chosen per launch so that a wave's whole

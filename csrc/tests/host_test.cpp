@@ -4,8 +4,10 @@
 // GPU sanitizers are unavailable on this pool, so the host code is checked here.
 //
 // Covers: BlockAllocator (alloc/free/refcounts, prefix-cache register/lookup/eviction,
-// concurrent stats queries while allocating) and ShardedLRU (capacity / LRU order /
-// overwrite / erase, and a multi-thread get/put hammer with an exact accounting check).
+// concurrent stats queries while allocating), ShardedLRU (capacity / LRU order /
+// overwrite / erase, and a multi-thread get/put hammer with an exact accounting check) and the
+// lock-free shared-memory StepRing (one publisher thread, several follower threads: every payload
+// byte checked, back-pressure on a ring smaller than the run, close, heartbeat timeout).
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -13,8 +15,11 @@
 #include <thread>
 #include <vector>
 
+#include <unistd.h>
+
 #include "../runtime/allocator.h"
 #include "../runtime/lru_cache.h"
+#include "../runtime/step_ring.h"
 
 #define CHECK(c)                                                             \
   do {                                                                       \
@@ -111,10 +116,59 @@ static void test_lru_threads() {
   CHECK(c.hits() + c.misses() == gets.load());
 }
 
+static void test_step_ring() {
+  using vgate::StepRingCore;
+  const std::string name = "/vgate_host_test_" + std::to_string((long)getpid());
+  const int steps = 3000, followers = 3;
+  StepRingCore leader(name, true, /*slots=*/4, /*slot_bytes=*/4096, followers);
+  std::vector<std::thread> ts;
+  std::atomic<int> bad{0};
+  for (int f = 0; f < followers; ++f) {
+    ts.emplace_back([&, f] {
+      StepRingCore me(name, false, 0, 0, 0);
+      std::vector<unsigned char> buf(4096);
+      for (int i = 1; i <= steps; ++i) {
+        auto st = me.wait(f, buf.data(), buf.size(), 5.0);
+        if (st.mode != i % 3 || st.T != i || st.nbytes != (i * 37) % 4096) {
+          ++bad;
+          return;
+        }
+        for (int64_t b = 0; b < st.nbytes; ++b)
+          if (buf[b] != (unsigned char)(i + b)) {
+            ++bad;
+            return;
+          }
+      }
+      auto end = me.wait(f, buf.data(), buf.size(), 5.0);
+      if (end.mode != -1) ++bad;  // closed
+    });
+  }
+  std::vector<unsigned char> payload(4096);
+  for (int i = 1; i <= steps; ++i) {
+    const int n = (i * 37) % 4096;
+    for (int b = 0; b < n; ++b) payload[b] = (unsigned char)(i + b);
+    CHECK(leader.publish(i, 0, 0, 0, i % 3, payload.data(), (size_t)n, 5.0));
+  }
+  leader.close_ring();
+  for (auto& t : ts) t.join();
+  CHECK(bad.load() == 0);
+  CHECK(leader.published() == steps);
+  // a follower of a ring whose leader stopped stamping its heartbeat gives up (mode -2)
+  {
+    const std::string n2 = name + "_hb";
+    StepRingCore l2(n2, true, 2, 64, 1);
+    StepRingCore f2(n2, false, 0, 0, 0);
+    unsigned char b[64];
+    auto st = f2.wait(0, b, sizeof(b), 0.05);
+    CHECK(st.mode == -2);
+  }
+}
+
 int main() {
   test_allocator();
   test_lru_basic();
   test_lru_threads();
+  test_step_ring();
   std::printf("host_test: ok\n");
   return 0;
 }

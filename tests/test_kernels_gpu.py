@@ -1089,3 +1089,49 @@ def test_decode_gemm_register_groups_bit_identical(M):
             assert _rel_err(outs[0].float().cpu(), r.float()) < 1e-2, (N, K, kind)
     finally:
         C.set_dec_u(-100)
+
+
+@pytest.mark.parametrize("M", [5, 8, 12, 16])
+def test_balanced_decode_gemm(M):
+    """Balanced decode GEMM (one block per CU: q full tiles + pieces of the tail tiles, combined by
+    the last piece): SiLU with folded RMSNorm on the Qwen2.5-1.5B gate_up shape (1120 tiles), a
+    residual GEMM with 608 tiles and an f32-output one — against the fp32 reference, run-to-run
+    bit-identical, and close to the one-tile-per-block kernel."""
+    C = ops.native()
+    torch.manual_seed(90 + M)
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    try:
+        for N, K, kind in ((17920, 1536, "silu"), ((2 * ncu + 96) * 16, 1536, "plain"),
+                           ((4 * ncu + 64) * 16, 2048, "f32")):
+            x = torch.randn(M, K, device=DEV).bfloat16()
+            w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+            g = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+            lin = ops.Linear(w, kind="silu") if kind == "silu" else ops.Linear(w)
+            res = torch.randn(M, N, device=DEV).bfloat16()
+
+            def run():
+                if kind == "silu":
+                    return ops.linear(x, lin, norm=(g, 1e-6))
+                if kind == "f32":
+                    return ops.linear(x, lin, out_f32=True)
+                y = res.clone()
+                ops.linear(x, lin, out=y, residual=y)
+                return y
+            if kind == "silu":
+                lin.fold_norm(g)
+            C.set_dec_bal(0)
+            y0 = run()
+            C.set_dec_bal(1)
+            y1, y2 = run(), run()
+            assert torch.equal(y1, y2), (N, K, kind)
+            if kind == "silu":
+                xn, _ = ref.rmsnorm_ref(x.cpu(), g.cpu(), 1e-6)
+                r = ref.silu_mul_linear_ref(xn, w.cpu()[: N // 2], w.cpu()[N // 2:])
+            elif kind == "f32":
+                r = ref.linear_ref(x.cpu(), w.cpu(), out_f32=True)
+            else:
+                r = ref.linear_ref(x.cpu(), w.cpu(), None, res.cpu())
+            assert _rel_err(y1.float().cpu(), r.float()) < 1e-2, (N, K, kind)
+            assert _rel_err(y1.float(), y0.float()) < 1e-2, (N, K, kind)
+    finally:
+        C.set_dec_bal(-1)

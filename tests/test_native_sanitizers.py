@@ -1,5 +1,5 @@
-"""Sanitizer tier for the native host runtime: the C++ block allocator and
-sharded LRU (csrc/runtime) are compiled into a host-only test program with
+"""Sanitizer tier for the native host runtime: the C++ block allocator,
+sharded LRU and the lock-free TP step ring (csrc/runtime) are compiled into a host-only test program with
 AddressSanitizer + UndefinedBehaviorSanitizer, and separately with ThreadSanitizer, and
 run on the CPU. (GPU sanitizers / XNACK are not available on this pool: kernels are
 checked by the numerics tier against fp32 references instead.) Also: the native
@@ -29,6 +29,7 @@ def _build_and_run(tmp_path, flags, name):
     exe = tmp_path / name
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", *flags, f"-I{pybind11.get_include()}",
            f"-I{py_inc}", *map(str, SRCS), "-o", str(exe), f"-L{libdir}", f"-lpython{ver}", "-lpthread"]
+    cmd.append("-lrt")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-4000:]
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300,

@@ -135,6 +135,49 @@ def _json(data, status: int = 200, headers: dict | None = None) -> Response:
     return Response(content=json.dumps(data), status_code=status, media_type="application/json", headers=headers)
 
 
+def _install_drain_on_sigterm(config: VGateConfig):
+    """Worker role: SIGTERM first drains (worker_api.begin_drain: /health 503, new generate calls
+    503), waits until the accepted requests finished and drain_seconds passed, and only then hands
+    the signal to the server's own handler (uvicorn: stop accepting, shut down). Returns a callable
+    that restores the previous handler. No-op off the main thread (in-process test clients)."""
+    import signal
+    import threading
+
+    from vgate import worker_api
+    if threading.current_thread() is not threading.main_thread():
+        return lambda: None
+    loop = asyncio.get_running_loop()
+    prev = signal.getsignal(signal.SIGTERM)
+
+    async def finish(sig, frame):
+        await worker_api.wait_drained(config.worker.drain_seconds, config.worker.drain_timeout_seconds)
+        app_logger.info("Worker drained", extra={"extra_data": {"inflight": worker_api.inflight()}})
+        if callable(prev):
+            prev(sig, frame)
+        else:  # default disposition: terminate as SIGTERM would have
+            signal.signal(signal.SIGTERM, signal.SIG_DFL)
+            signal.raise_signal(signal.SIGTERM)
+
+    def on_term(sig, frame):
+        if worker_api.is_draining():
+            return
+        worker_api.begin_drain()
+        loop.call_soon_threadsafe(lambda: asyncio.ensure_future(finish(sig, frame)))
+
+    try:
+        signal.signal(signal.SIGTERM, on_term)
+    except (ValueError, OSError):
+        return lambda: None
+
+    def restore():
+        try:
+            if signal.getsignal(signal.SIGTERM) is on_term:
+                signal.signal(signal.SIGTERM, prev)
+        except (ValueError, OSError):
+            pass
+    return restore
+
+
 def create_app(config: Optional[VGateConfig] = None, engine: Optional[VGateEngine] = None) -> FastAPI:
     if config is None:
         config = get_config()
@@ -152,11 +195,17 @@ def create_app(config: Optional[VGateConfig] = None, engine: Optional[VGateEngin
         M.init_app_info(version=version, model=config.model.model_id)
         if is_worker:
             from vgate import worker_api
+            worker_api.reset_drain()
             worker_api.set_engine(st.engine)
+            restore = _install_drain_on_sigterm(config)
             app_logger.info("V-Gate worker started", extra={"extra_data": {
                 "version": version, "model": config.model.model_id, "engine_type": config.model.engine_type}})
             st.engine_metrics_task = asyncio.create_task(_engine_metrics_loop(st))
             yield
+            # shutdown without a SIGTERM first (the server was stopped another way): still drain
+            worker_api.begin_drain()
+            await worker_api.wait_drained(0.0, config.worker.drain_timeout_seconds)
+            restore()
             st.engine_metrics_task.cancel()
             st.engine.backend.shutdown()
             shutdown_tracing()
@@ -222,6 +271,11 @@ def create_app(config: Optional[VGateConfig] = None, engine: Optional[VGateEngin
         # the probe with 503, so a gateway's WorkerHealthChecker demotes the worker after
         # failure_threshold probes (reference main.py:288-295 is static).
         eng = st.engine
+        if is_worker:
+            from vgate import worker_api
+            if worker_api.is_draining():  # SIGTERM: out of every gateway's rotation, finishing what it has
+                return _json({"status": "draining", "version": version, "role": config.role,
+                              "inflight": worker_api.inflight()}, 503)
         if eng is not None and not eng.is_remote:
             h = getattr(eng.backend, "healthy", None)
             if callable(h) and not h():
@@ -234,6 +288,10 @@ def create_app(config: Optional[VGateConfig] = None, engine: Optional[VGateEngin
     async def ready():
         eng = st.engine
         ok, detail = eng is not None, "starting"
+        if is_worker:
+            from vgate import worker_api
+            if worker_api.is_draining():
+                return _json({"status": "unavailable", "detail": "draining"}, 503)
         if eng is not None:
             if eng.is_remote:
                 ok = eng.backend.registry.has_healthy()

@@ -14,8 +14,8 @@ Re-designed vs the reference (``remote_backend.py``):
   ``/internal/generate_stream`` SSE stream (the reference returned 501);
 * **trace propagation**: W3C ``traceparent`` header on every worker call.
 
-Retry policy is unchanged (the safe one): only a connect failure moves to another
-worker (nothing was delivered); timeouts / mid-request errors / non-200 /
+Retry policy (the safe one): only a connect failure or a 503 refusal (a draining worker,
+or one whose engine is not bound yet) moves to another worker (nothing ran); timeouts / mid-request errors / non-200 /
 malformed results fail without retry so one client request never costs two
 generations; exhausting the pool raises :class:`NoHealthyWorkersError` (503).
 The sync ``generate`` is kept for protocol compatibility (runs the coroutine on
@@ -47,6 +47,10 @@ class RemoteInferenceError(RuntimeError):
 
 class _ConnectFailed(Exception):
     """Nothing reached the worker: safe to retry on another one."""
+
+
+class _Refused(Exception):
+    """The worker answered 503 before running anything (draining / not ready): retry elsewhere."""
 
 
 class _RequestFailed(Exception):
@@ -228,6 +232,13 @@ class RemoteBackend:
                 finally:
                     self.registry.end(ep)
                     WORKER_LATENCY.labels(worker=ep).observe(time.perf_counter() - t0)
+                if status == 503:
+                    # 503 = the worker refused before running anything (draining on SIGTERM, engine
+                    # not bound yet): like a refused connection, safe to send to another worker
+                    self.registry.record_failure(ep)
+                    WORKER_REQUESTS.labels(worker=ep, outcome="http_error").inc()
+                    tried.add(ep)
+                    continue
                 if status != 200:
                     self.registry.record_failure(ep)
                     WORKER_REQUESTS.labels(worker=ep, outcome="http_error").inc()
@@ -283,6 +294,8 @@ class RemoteBackend:
                 async with client.stream_lines(f"{ep}/internal/generate_stream",
                                                {"prompt": prompt, "sampling_params": sampling_params},
                                                headers) as (status, err_body, lines):
+                    if status == 503:  # refused before anything ran (draining): try another worker
+                        raise _Refused()
                     if status != 200:
                         self.registry.record_failure(ep)
                         WORKER_REQUESTS.labels(worker=ep, outcome="http_error").inc()
@@ -303,6 +316,11 @@ class RemoteBackend:
             except _ConnectFailed:
                 self.registry.record_failure(ep)
                 WORKER_REQUESTS.labels(worker=ep, outcome="connect_error").inc()
+                tried.add(ep)
+                continue
+            except _Refused:
+                self.registry.record_failure(ep)
+                WORKER_REQUESTS.labels(worker=ep, outcome="http_error").inc()
                 tried.add(ep)
                 continue
             except _RequestFailed as e:

@@ -61,6 +61,12 @@ class WorkerConfig(_Section):
     api_key: Optional[str] = None
     routing: str = "round_robin"  # round_robin | least_inflight
     max_connections: int = 512
+    # worker role, SIGTERM: stay up failing /health (503 "draining") and refusing new
+    # /internal/generate calls (503: the gateway retries them elsewhere) for at least
+    # drain_seconds (>= failure_threshold x health_check_interval_seconds, so every gateway has
+    # demoted this worker), finishing the requests already accepted, at most drain_timeout_seconds
+    drain_seconds: float = 12.0
+    drain_timeout_seconds: float = 120.0
 
     @field_validator("endpoints")
     @classmethod

@@ -674,6 +674,15 @@ def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = 0.05
     return plans
 
 
+def apply_prefill_plans(lins: list, plans: dict) -> None:
+    """Give every Linear the plan measured for its (N, K) shape (plans from :func:`tune_prefill`,
+    e.g. broadcast from TP rank 0)."""
+    for lin in lins:
+        plan = (plans or {}).get((lin.N, lin.K))
+        if plan is not None:
+            lin.prefill_plan = dict(plan)
+
+
 KERNEL_COPY = os.environ.get("VGATE_KERNEL_COPY", "1") != "0"
 
 
@@ -710,5 +719,5 @@ def softmax_scale(head_dim: int) -> float:
 __all__ = [
     "native", "native_available", "pack_weight", "unpack_weight", "interleave_gate_up", "pack_awq",
     "Linear", "linear", "attention", "attention_o", "workspace", "row_permutation", "reserve_awq_scratch", "pack_awq_sz", "rmsnorm", "embedding", "rope_kv", "attention_decode", "attention_prefill",
-    "prefill_tiles", "sample", "softmax_scale", "ref", "host_device_copy", "tune_prefill",
+    "prefill_tiles", "sample", "softmax_scale", "ref", "host_device_copy", "tune_prefill", "apply_prefill_plans",
 ]

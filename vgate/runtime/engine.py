@@ -137,7 +137,14 @@ class LLMEngine:
             t1 = time.perf_counter()
             ms = [t for t in self.runner.t_buckets if t >= 128]
             lins = [lin for L in self.model.layers for lin in (L.qkv, L.o, L.gate_up, L.down)]
-            self.prefill_plans = ops.tune_prefill(lins, ms)
+            if self.tp.size > 1:
+                # rank 0 measures, every rank applies the same plans (per-rank timing noise would
+                # otherwise give TP ranks different tile / K-split choices, and N x the start-up cost)
+                plans = ops.tune_prefill(lins, ms) if self.tp.is_first else None
+                self.prefill_plans = self.tp.broadcast_object(plans)
+                ops.apply_prefill_plans(lins, self.prefill_plans)
+            else:
+                self.prefill_plans = ops.tune_prefill(lins, ms)
             log.info("prefill GEMM plans for %d shapes x %d buckets in %.2fs: %s", len(self.prefill_plans), len(ms),
                      time.perf_counter() - t1, {f"{n}x{k}": p for (n, k), p in self.prefill_plans.items()})
         if gloo_tp and not eager:

@@ -9,6 +9,13 @@ sync backends run in the executor, serialised by a lock if not concurrency-safe.
 
 ``POST /internal/generate_stream`` (new) streams one prompt's deltas as SSE so
 the gateway can proxy ``stream: true`` through remote workers.
+
+Drain (reference ROADMAP.md:399-403: "a terminating worker has to fail its own /health while
+still finishing the requests it already accepted"): :func:`begin_drain` (SIGTERM, or the
+lifespan shutdown) flips the worker to draining — ``/health`` answers 503
+``{"status": "draining"}``, new generate calls get 503 (nothing ran, so the gateway retries
+them on another worker) — and :func:`wait_drained` returns once every accepted request has
+finished (and the minimum drain time has passed, so the gateways' probes saw the 503).
 """
 from __future__ import annotations
 
@@ -30,6 +37,59 @@ router = APIRouter()
 
 _engine = None
 _guard: Optional[asyncio.Lock] = None
+_draining = False
+_drain_started = 0.0
+_inflight = 0
+
+
+def begin_drain() -> None:
+    """Enter the draining state (idempotent)."""
+    global _draining, _drain_started
+    if not _draining:
+        import time
+        _draining = True
+        _drain_started = time.monotonic()
+        logger.info("Worker draining", extra={"extra_data": {"inflight": _inflight}})
+
+
+def is_draining() -> bool:
+    return _draining
+
+
+def inflight() -> int:
+    return _inflight
+
+
+async def wait_drained(min_seconds: float = 0.0, timeout: float = 120.0) -> bool:
+    """Wait until no accepted request is in flight and ``min_seconds`` have passed since
+    :func:`begin_drain`; False if ``timeout`` expired first."""
+    import time
+    t_end = time.monotonic() + timeout
+    while time.monotonic() < t_end:
+        if _inflight == 0 and time.monotonic() - _drain_started >= min_seconds:
+            return True
+        await asyncio.sleep(0.05)
+    return _inflight == 0
+
+
+def reset_drain() -> None:
+    """Back to serving (tests)."""
+    global _draining, _inflight
+    _draining, _inflight = False, 0
+
+
+class _Accepted:
+    """Counts a request from acceptance to its last byte (the drain waits for these)."""
+
+    def __enter__(self):
+        global _inflight
+        _inflight += 1
+        return self
+
+    def __exit__(self, *exc):
+        global _inflight
+        _inflight -= 1
+        return False
 
 
 class WorkerSamplingParams(BaseModel):
@@ -58,10 +118,21 @@ def get_engine():
     return _engine
 
 
+def _refuse_if_draining() -> None:
+    if _draining:
+        raise HTTPException(status_code=503, detail="Worker draining")
+
+
 @router.post("/internal/generate")
 async def internal_generate(body: GenerateRequest, request: Request):
     if _engine is None:
         raise HTTPException(status_code=503, detail="Worker engine not ready")
+    _refuse_if_draining()
+    with _Accepted():
+        return await _generate(body, request)
+
+
+async def _generate(body: GenerateRequest, request: Request):
     backend = _engine.backend
     with attach_traceparent(request.headers.get("traceparent")):
         with tracer.start_as_current_span("worker.generate") as span:
@@ -91,6 +162,7 @@ async def internal_generate(body: GenerateRequest, request: Request):
 async def internal_generate_stream(body: StreamRequest, request: Request):
     if _engine is None:
         raise HTTPException(status_code=503, detail="Worker engine not ready")
+    _refuse_if_draining()
     backend = _engine.backend
     if not getattr(backend, "supports_streaming", False):
         raise HTTPException(status_code=501, detail="worker backend cannot stream")
@@ -98,14 +170,15 @@ async def internal_generate_stream(body: StreamRequest, request: Request):
     sp = backend.create_sampling_params(temperature=sp_in.temperature, top_p=sp_in.top_p, max_tokens=sp_in.max_tokens)
 
     async def gen():
-        try:
-            async for piece in backend.stream_generate(body.prompt, sp):
-                yield f"data: {json.dumps(piece)}\n\n"
-        except (asyncio.CancelledError, GeneratorExit):
-            raise
-        except Exception as e:  # noqa: BLE001
-            INFERENCE_ERRORS.labels(error_type=type(e).__name__).inc()
-            yield f"data: {json.dumps({'error': {'message': str(e), 'type': type(e).__name__}})}\n\n"
-        yield "data: [DONE]\n\n"
+        with _Accepted():  # the stream counts until its last byte
+            try:
+                async for piece in backend.stream_generate(body.prompt, sp):
+                    yield f"data: {json.dumps(piece)}\n\n"
+            except (asyncio.CancelledError, GeneratorExit):
+                raise
+            except Exception as e:  # noqa: BLE001
+                INFERENCE_ERRORS.labels(error_type=type(e).__name__).inc()
+                yield f"data: {json.dumps({'error': {'message': str(e), 'type': type(e).__name__}})}\n\n"
+            yield "data: [DONE]\n\n"
 
     return StreamingResponse(gen(), media_type="text/event-stream")
