@@ -509,6 +509,214 @@ __device__ __forceinline__ void prefill_body(const AttnArgs& a, int tile, int h,
   }
 }
 
+// ------------------------------------------------------- flash prefill ----
+// Causal (chunked-prefill capable) attention of a block of QPB query tokens x the G query heads of
+// one KV head. Waves: (QPB / 32) x G, each owns 32 queries (two 16-query MFMA column tiles) of one
+// head; Q lives in registers. K / V stream through LDS in 64-token chunks, double-buffered and
+// SHARED by every wave of the block (GQA: one K/V byte serves G heads x QPB queries), moved by
+// LDS-DMA (global_load_lds_dwordx4: no VGPRs, every wave issues a share of the 32 1-KiB pieces) —
+// the DMA of chunk c + 1 is issued before chunk c's MFMAs, one barrier per chunk.
+//   S^T = K Q^T (swapped: softmax statistics lane-local, row reductions by two xor-swaps); K image
+//   16-B chunks XOR-swizzled by row & 15 (conflict-free ds_read_b128 of the A operand);
+//   O^T += V^T P^T with V^T read by ds_read_b64_tr_b16 from the 8-B-chunk-swizzled V image and P^T
+//   built in registers (pack_p), as in the decode kernel.
+// The host's 16-query tile list is reused: a block whose tile starts a QPB-aligned group leads it
+// (others exit at once). The host lists the group leaders first, longest causal range first
+// (ops.tile_order), so the working blocks are the grid's first ones, spread over all 8 XCDs and
+// the longest start first. Tokens past the causal bound are masked; pages past the context are
+// not read.
+extern int g_flash_prefill;
+constexpr int FL_KV = 64;
+constexpr int FL_LDS = 4 * FL_KV * D_ * 2;  // K x2 + V x2 (64 KiB)
+
+// fx = this block's index among the launch's prefill blocks; waves past (qpb / 32) x G (a unified
+// launch sized for wider decode blocks) join the DMA and the barriers but own no queries
+__device__ __forceinline__ void flash_body(const AttnArgs& a, int fx, int h, int qpb, char* smem) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int G = a.Hq / a.Hkv;
+  const int tile = fx;  // the host lists group leaders first, longest first (ops.tile_order)
+  const int s = a.tile_seq[tile];
+  if (s < 0) return;
+  const int q0 = a.tile_q0[tile];
+  if (q0 % qpb) return;  // block-uniform: not a group leader
+  const int qs = a.query_start[s];
+  const int qlen = a.query_start[s + 1] - qs;
+  const int ctx = a.context_lens[s];
+  const int hq = h * G + wid % G;
+  const int qw0 = q0 + 32 * (wid / G);
+  const int qhi = min(q0 + qpb, qlen);  // this block's queries: [q0, qhi)
+  const int qlast = min(q0 + qpb, qlen) - 1;
+  const int kv_end = ctx - qlen + qlast + 1;  // the block's causal bound (exclusive)
+  const int nch = (kv_end + FL_KV - 1) / FL_KV;
+  const int col = lane & 15, g4 = lane >> 4;
+  // Q fragments (B operand of S^T = K Q^T): 2 column tiles x 4 k-slices
+  uint4 qf[2][4];
+  int lim[2];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const int qi = qw0 + 16 * ct + col;
+    const bool ok = qi < qhi;
+    lim[ct] = ok ? ctx - qlen + qi + 1 : 0;
+    const bf16_t* qp = a.q + (size_t)(qs + (ok ? qi : 0)) * a.q_stride + (size_t)hq * D_ + 8 * g4;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) qf[ct][kk] = ok ? *reinterpret_cast<const uint4*>(qp + 32 * kk) : make_uint4(0, 0, 0, 0);
+  }
+  const size_t blk_stride = (size_t)a.Hkv * BS_ * D_;
+  const size_t head_off = (size_t)h * BS_ * D_;
+  // the sequence's block-table entries of the causal range, staged in LDS once: a DMA's source page
+  // is then an LDS broadcast read, not a global load whose wait would serialise behind the DMAs
+  // already in flight (vmcnt counts both)
+  int* s_bt = reinterpret_cast<int*>(smem + FL_LDS);
+  const int npg = (kv_end + BS_ - 1) / BS_;
+  {
+    const int* bt = a.block_tables + (size_t)s * a.max_blocks;
+    for (int i = threadIdx.x; i < npg; i += blockDim.x) s_bt[i] = bt[i];
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  // chunk c's 32 DMA pieces (16 K, 16 V) over the block's waves
+  auto issue = [&](int c) {
+    char* kbuf = smem + (c & 1) * (FL_KV * D_ * 2);
+    char* vbuf = smem + 2 * (FL_KV * D_ * 2) + (c & 1) * (FL_KV * D_ * 2);
+    int pg[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pg[j] = __builtin_amdgcn_readfirstlane(s_bt[min(4 * c + j, npg - 1)]);  // past the bound: the last page
+    for (int i = wid; i < 32; i += nw) {
+      const int isv = i >> 4, pi = i & 15;
+      int r, d0;
+      uint32_t dst;
+      if (!isv) {  // K rows 4 pi .. 4 pi + 3; lane -> physical 16-B chunk l & 15 holds logical chunk ^ (row & 15)
+        r = 4 * pi + g4;
+        d0 = 8 * (col ^ (r & 15));
+        dst = lds_addr_of(kbuf + pi * 1024);
+      } else {  // V half pi / 8, rows 4 (pi % 8) .. +3 of that half (v_lds_off's 8-B chunk swizzle)
+        const int rh = 4 * (pi & 7) + g4;
+        r = 32 * (pi >> 3) + rh;
+        d0 = (8 * col) ^ (16 * (rh & 7));
+        dst = lds_addr_of(vbuf + pi * 1024);
+      }
+      // rows of a piece share one page: r / 16 as a function of the (wave-uniform) piece index
+      const int pj = isv ? 2 * (pi >> 3) + ((pi & 7) >> 2) : pi >> 2;
+      const int page = pj == 0 ? pg[0] : pj == 1 ? pg[1] : pj == 2 ? pg[2] : pg[3];
+      const bf16_t* src = (isv ? a.v_cache : a.k_cache) + (size_t)page * blk_stride + head_off + (r & 15) * D_ + d0;
+      glds16(src, __builtin_amdgcn_readfirstlane(dst));
+    }
+  };
+  const float cscale = a.scale * LOG2E;
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  f32x4 o[2][8];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) o[ct][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nch > 0) issue(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Q fragments and chunk 0 landed
+  __builtin_amdgcn_s_barrier();
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) issue(c + 1);  // into the buffer every wave finished reading last iteration
+    const char* kb = smem + (c & 1) * (FL_KV * D_ * 2);
+    const bf16_t* vb = reinterpret_cast<const bf16_t*>(smem + 2 * (FL_KV * D_ * 2) + (c & 1) * (FL_KV * D_ * 2));
+    // S^T tiles: 4 token tiles x 2 column tiles
+    f32x4 st[4][2];
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      st[tt][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+      st[tt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const char* krow = kb + (16 * tt + col) * 256;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const uint4 kf = *reinterpret_cast<const uint4*>(krow + (((4 * kk + g4) ^ col) << 4));
+        st[tt][0] = mfma16(as_bf16x8(kf), as_bf16x8(qf[0][kk]), st[tt][0]);
+        st[tt][1] = mfma16(as_bf16x8(kf), as_bf16x8(qf[1][kk]), st[tt][1]);
+      }
+    }
+    // online softmax per column tile over the 64 tokens (lane: column col, tokens 16 tt + 4 g4 + i)
+    bf16x8 pb[2][2];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      float cmax = -INFINITY;
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int t = c * FL_KV + 16 * tt + 4 * g4 + i;
+          st[tt][ct][i] = t < lim[ct] ? st[tt][ct][i] * cscale : -INFINITY;
+          cmax = fmaxf(cmax, st[tt][ct][i]);
+        }
+      cmax = fmaxf(cmax, xor16(cmax));
+      cmax = fmaxf(cmax, xor32(cmax));
+      const float mn = fmaxf(m[ct], cmax);
+      const float mref = mn == -INFINITY ? 0.f : mn;  // fully masked column: exp2(-inf) = 0, no NaN
+      const float alpha = __builtin_amdgcn_exp2f(m[ct] - mref);
+      float ps = 0.f;
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          st[tt][ct][i] = __builtin_amdgcn_exp2f(st[tt][ct][i] - mref);
+          ps += st[tt][ct][i];
+        }
+      l[ct] = l[ct] * alpha + ps;
+      m[ct] = mn;
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) o[ct][mt] *= alpha;
+      pb[ct][0] = pack_p(st[0][ct], st[1][ct]);
+      pb[ct][1] = pack_p(st[2][ct], st[3][ct]);
+    }
+    // O^T += V^T P^T: each V^T fragment (ds_read_b64_tr_b16) feeds both column tiles
+    const int q = (lane >> 2) & 3, p4 = lane & 3;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const bf16_t* vh = vb + half * (32 * D_);
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) {
+        const int cc = 16 * mt + 4 * p4;
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(vh + v_lds_off(4 * g4 + q, cc)));
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(vh + v_lds_off(16 + 4 * g4 + q, cc)));
+        bf16x8 av;
+        av[0] = lo[0]; av[1] = lo[1]; av[2] = lo[2]; av[3] = lo[3];
+        av[4] = hi[0]; av[5] = hi[1]; av[6] = hi[2]; av[7] = hi[3];
+        o[0][mt] = mfma16(av, pb[0][half], o[0][mt]);
+        o[1][mt] = mfma16(av, pb[1][half], o[1][mt]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of chunk c + 1 landed
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // everyone's; buffer c & 1 free
+  }
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    float ll = l[ct];
+    ll += xor16(ll);
+    ll += xor32(ll);
+    const int qi = qw0 + 16 * ct + col;
+    if (qi >= qhi) continue;
+    const float inv = ll > 0.f ? 1.f / ll : 0.f;
+    const size_t orow = (size_t)(qs + qi) * a.out_stride + (size_t)hq * D_;
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      uint2 pk;
+      pk.x = pack_bf2(o[ct][mt][0] * inv, o[ct][mt][1] * inv);
+      pk.y = pack_bf2(o[ct][mt][2] * inv, o[ct][mt][3] * inv);
+      *reinterpret_cast<uint2*>(a.out + orow + 16 * mt + 4 * g4) = pk;
+    }
+  }
+}
+
+// queries per flash block for a head group of G (<= 8 waves of 32 queries: ~170 VGPRs per wave, so
+// 512-thread blocks; at 12 waves the O / S / Q fragments spilled), 0 = not supported
+static int flash_qpb(const AttnArgs& a) {
+  if (a.D != D_ || a.BS != BS_ || a.Hkv <= 0 || a.Hq % a.Hkv) return 0;
+  const int G = a.Hq / a.Hkv;
+  if (G <= 4) return 64;
+  if (G <= 8) return 32;
+  return 0;
+}
+
+static bool flash_enabled() {
+  static const int v = [] { const char* e = getenv("VGATE_FLASH_PREFILL"); return e ? atoi(e) : 1; }();
+  return g_flash_prefill >= 0 ? g_flash_prefill != 0 : v != 0;
+}
+
 // ------------------------------------------------------------- unified launch ----
 // grid.x = [decode blocks: one per (sequence, partition), partition-major: bx = p*S + s]
 //          ++ [prefill tiles], grid.y = KV heads. One launch serves a decode-only,
@@ -516,13 +724,19 @@ __device__ __forceinline__ void prefill_body(const AttnArgs& a, int tile, int h,
 // MAXT: 512 threads (G <= 8 query heads per KV head) leaves 256 VGPRs per wave for the
 // prefetched K + in-flight V + O accumulators; 1024 only for G > 8.
 template <int MAXT>
-__global__ __launch_bounds__(MAXT) void attn_kernel(AttnArgs a, int dec_seqs, int dec_blocks) {
+__global__ __launch_bounds__(MAXT) void attn_kernel(AttnArgs a, int dec_seqs, int dec_blocks, int flash_qpb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   TLScope tl_scope(a.tl);
   const int bx = blockIdx.x;
   if (bx < dec_blocks) {
     decode_block(a, bx % dec_seqs, blockIdx.y, bx / dec_seqs, smem);  // block = (sequence, partition)
   } else {
+    if constexpr (MAXT <= 512) {
+      if (flash_qpb > 0) {
+        flash_body(a, bx - dec_blocks, blockIdx.y, flash_qpb, smem);
+        return;
+      }
+    }
     prefill_body(a, bx - dec_blocks, blockIdx.y, smem);
   }
 }
@@ -532,18 +746,32 @@ static int attn_waves(const AttnArgs& a) {
   return G > 4 ? G : 4;
 }
 
+int g_flash_prefill = -1;  // -1: VGATE_FLASH_PREFILL (default on); 0 / 1: set_flash_prefill (tests)
+void set_flash_prefill(int on) { g_flash_prefill = on; }
+
 void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
   const int tiles = a.num_tiles > 0 ? a.num_tiles : 0;
-  const int nw = attn_waves(a);
+  int nw = attn_waves(a);
+  // prefill tiles take the flash body (QPB-query blocks, K / V through LDS by DMA) inside the same
+  // launch: its waves (QPB / 32 x G) and 64 KiB of LDS (+ the staged block table) size the blocks
+  const int fq = tiles > 0 && flash_enabled() ? flash_qpb(a) : 0;
+  size_t lds = attn_lds_bytes(nw);
+  if (fq > 0) {
+    const int fw = (fq / 32) * (a.Hq / a.Hkv);
+    nw = nw > fw ? nw : fw;
+    lds = attn_lds_bytes(nw);
+    const size_t fl = (size_t)FL_LDS + (size_t)a.max_blocks * 4;
+    lds = lds > fl ? lds : fl;
+  }
   const int dec_blocks = dec_seqs > 0 ? dec_seqs * a.num_parts : 0;
   const int nx = dec_blocks + tiles;
   if (nx <= 0) return;
   AttnArgs b = a;
   b.tl = tl_take("attention", nx * a.Hkv);
   if (nw <= 8)
-    hipLaunchKernelGGL(attn_kernel<512>, dim3(nx, a.Hkv, 1), dim3(64 * nw), attn_lds_bytes(nw), st, b, dec_seqs, dec_blocks);
+    hipLaunchKernelGGL(attn_kernel<512>, dim3(nx, a.Hkv, 1), dim3(64 * nw), lds, st, b, dec_seqs, dec_blocks, fq);
   else
-    hipLaunchKernelGGL(attn_kernel<1024>, dim3(nx, a.Hkv, 1), dim3(64 * nw), attn_lds_bytes(nw), st, b, dec_seqs, dec_blocks);
+    hipLaunchKernelGGL(attn_kernel<1024>, dim3(nx, a.Hkv, 1), dim3(64 * nw), lds, st, b, dec_seqs, dec_blocks, 0);
   if (dec_seqs > 0 && a.num_parts > 1 && a.tickets == nullptr) {
     b.tl = tl_take("attn_reduce", dec_seqs * a.Hq);
     hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(dec_seqs, a.Hq), dim3(128), 0, st, b);

@@ -50,6 +50,10 @@ void set_tail_split(int on) { g_tail_split = on; }
 int g_dec_u = -100;  // -100: VGATE_DEC_U; else the forced decode register group size (tests, A/B)
 void set_dec_u(int u) { g_dec_u = u; }
 int g_dec_bal = -1;
+int g_awq_lds = -1;
+int g_dec_rot = -1;
+void set_dec_rot(int on) { g_dec_rot = on; }
+void set_awq_lds(int on) { g_awq_lds = on; }
 void set_dec_bal(int on) { g_dec_bal = on; }
 
 VG_EXTERN_EPI(EPI_BF16)
@@ -132,6 +136,8 @@ static GemmParams to_params(const GemmArgs& g) {
   // kernels' activation loads (garbage results) to price them against the weight stream
   static const int probe = [] { const char* e = getenv("VGATE_GEMM_PROBE"); return e ? atoi(e) : 0; }();
   p.probe = probe;
+  static const int rot = [] { const char* e = getenv("VGATE_DEC_ROT"); return e ? atoi(e) : 0; }();
+  p.rot = g_dec_rot >= 0 ? g_dec_rot : rot;
   p.hg = g.hg; p.hg_gamma = g.hg_gamma; p.ssp_out = g.ssp_out; p.ssp_in = g.ssp_in; p.ssn = g.ssn;
   return p;
 }

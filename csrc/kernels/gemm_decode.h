@@ -49,14 +49,16 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
   const SplitPos sp = split_pos(p);
   const int nt0 = (p.tail_full > 0 ? sp.tile : (int)blockIdx.x) * NTB;
   const int m_base = blockIdx.y * 16 * MB;
-  // this block's k-slice, then this wave's contiguous range inside it
+  // this block's k-slice, then this wave's contiguous range inside it (p.rot: range index rotated
+  // by the block index, so the launch's blocks spread their activation requests over the slice)
   const int s0 = (KT * sp.slice) / sp.nsl, s1 = (KT * (sp.slice + 1)) / sp.nsl;
-  int kbeg = s0 + ((s1 - s0) * wid) / nw;
-  int kend = s0 + ((s1 - s0) * (wid + 1)) / nw;
+  const int wr = p.rot ? (wid + (int)blockIdx.x) % nw : wid;
+  int kbeg = s0 + ((s1 - s0) * wr) / nw;
+  int kend = s0 + ((s1 - s0) * (wr + 1)) / nw;
   if constexpr (XP > 1) {  // waves take whole packs of XP k-steps (K % (32 * XP) == 0 on host)
     const int np0 = s0 / XP, np1 = s1 / XP;
-    kbeg = XP * (np0 + ((np1 - np0) * wid) / nw);
-    kend = XP * (np0 + ((np1 - np0) * (wid + 1)) / nw);
+    kbeg = XP * (np0 + ((np1 - np0) * wr) / nw);
+    kend = XP * (np0 + ((np1 - np0) * (wr + 1)) / nw);
   }
   f32x4 acc[MB][NTB];
 #pragma unroll
@@ -152,19 +154,21 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
       mma_grp(b, a, kt);
     }
   } else if (ngrp > 0) {
+    // group g of the wave starts at k-step gk(g); p.rot rotates the group order by the block index
+    const int gr = p.rot ? (int)(blockIdx.x % (unsigned)ngrp) : 0;
+    auto gk = [&](int g) { const int q = g + gr; return kbeg + (q < ngrp ? q : q - ngrp) * U; };
     uint4 b0[U][NTB], a0[U][MB], b1[U][NTB], a1[U][MB];
-    load_grp(b0, a0, kt);
+    load_grp(b0, a0, gk(0));
     if (epi_thr) epi_pre_b<NTB, EPI>(p, pre, nt0, 4 * (lane >> 4));  // dependent on phase A only
     pre_b = true;
     int g = 0;
     for (; g + 2 <= ngrp; g += 2) {
-      load_grp(b1, a1, kt + U);
-      mma_grp(b0, a0, kt);
-      if (g + 2 < ngrp) load_grp(b0, a0, kt + 2 * U);
-      mma_grp(b1, a1, kt + U);
-      kt += 2 * U;
+      load_grp(b1, a1, gk(g + 1));
+      mma_grp(b0, a0, gk(g));
+      if (g + 2 < ngrp) load_grp(b0, a0, gk(g + 2));
+      mma_grp(b1, a1, gk(g + 1));
     }
-    if (g < ngrp) mma_grp(b0, a0, kt);
+    if (g < ngrp) mma_grp(b0, a0, gk(g));
   }
   if (epi_thr && !pre_b) epi_pre_b<NTB, EPI>(p, pre, nt0, 4 * (lane >> 4));
   gemm_finish<MB, NTB, EPI, NORM, MB == 1>(p, acc, ssr, smem, m_base, nt0, pre);
@@ -841,6 +845,123 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
   gemm_finish<1, NTB, EPI, NORM, false>(p, acc, ssr, smem, 0, nt0, EpiPre<NTB>{});
 }
 
+// ---- AWQ W4A16 decode, activation slice shared through LDS (M <= 16) ----
+// At decode batch sizes the activations of a k-quad outweigh its int4 weights (8 rows x 128 k bf16
+// = 2 KiB vs a 1 KiB int4 fragment), so the one-tile-per-block kernels above move 2-3x more bytes
+// of activations and scales through each CU than weight bytes from HBM (awq_stream gate_up spans
+// 9.3 us for 13.8 MB; with its activation and scale loads switched off 6.6 us,
+// profiles/r2_awq_load_probe.log). Here a block owns T adjacent column tiles and one K slice:
+//   * a LOADER wave (the last one) DMAs the slice of x into LDS in MFMA B-fragment order
+//     (global_load_lds_dwordx4: 1 KiB per k-step, no VGPRs), waits for it and arrives at the
+//     block barrier;
+//   * each of the T tile waves issues its WHOLE int4 k-slice and packed group scales (every
+//     weight byte of the launch requested in the first microsecond), joins the barrier without
+//     waiting for them (raw s_barrier: loads stay in flight), then reads x fragments from LDS;
+//   * the raw-nibble identity sum_k x (v - z) s = s sum_k x (128 + v) - (128 s + s z) X gives the
+//     group scale per k-quad after four MFMAs (X = the k-quad's activation sum, from the LDS
+//     fragments); the producer's RMSNorm hand-off (NORM 3) or none (NORM 0);
+//   * S K-slices of a tile meet by slab + ticket (last arriver sums them in slice order).
+// One x slice per block instead of one per tile; T x the activation reuse.
+template <int Q, int EPI, int NORM>
+__global__ __launch_bounds__(576) void awq_lds_kernel(GemmParams p, int T, int S) {
+  static_assert(NORM == 0 || NORM == 3, "awq_lds_kernel: no norm, or the producer's RMSNorm hand-off");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  TLScope tl_scope(p.dbg_ts);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int KQ = p.K >> 7;
+  const int ngroups = (p.N >> 4) / T;
+  const int slice = blockIdx.x / ngroups, grp = blockIdx.x % ngroups;
+  const int q0 = (KQ * slice) / S, q1 = (KQ * (slice + 1)) / S, nq = q1 - q0;
+  const int r16 = lane & 15;
+  uint4* xs = reinterpret_cast<uint4*>(smem);  // [4 nq][64] B fragments of the slice
+  if (wid == T) {
+    // loader: rows >= M repeat row M - 1 (their output columns are never stored)
+    const bf16_t* xr = p.x + (size_t)row_of(p, r16) * p.lda + 8 * (lane >> 4) + (size_t)q0 * 128;
+    // pieces in a block-rotated order: the launch's loaders do not all hit the same x lines at once
+    const int np = 4 * nq, r0 = (int)(blockIdx.x % (unsigned)np);
+    for (int i = 0; i < np; ++i) {
+      const int t = i + r0 < np ? i + r0 : i + r0 - np;
+      glds16(xr + t * 32, __builtin_amdgcn_readfirstlane(lds_addr_of(xs + t * 64)));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    return;
+  }
+  const int nt = grp * T + wid;
+  const uint4* wb = p.wp + (size_t)nt * KQ * 64 + lane;
+  const uint4* sb = reinterpret_cast<const uint4*>(p.szp) + (size_t)nt * KQ * 4 + (lane >> 4);
+  uint4 w[Q], sz[Q];
+#pragma unroll
+  for (int g = 0; g < Q; ++g) {
+    const int kq = q0 + min(g, nq - 1);  // clamped past the slice: issued unconditionally, never consumed
+    w[g] = ld_nt16(wb + (size_t)kq * 64);
+    sz[g] = sb[(size_t)kq * 4];
+  }
+  float ss = 0.f;
+  if constexpr (NORM == 3) {
+    ss = prenorm_ss(p, r16, lane >> 4);
+    ss += xor16(ss);
+    ss += xor32(ss);
+  }
+  asm volatile("s_barrier" ::: "memory");  // x slice in LDS; the weight loads stay in flight
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int g = 0; g < Q; ++g) {
+    if (g < nq) {  // wave-uniform
+      uint4 b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) b[u] = xs[(g * 4 + u) * 64 + lane];
+      float X = 0.f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float f[8];
+        unpack8(b[u], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) X += f[j];
+      }
+      X += xor16(X);
+      X += xor32(X);
+      f32x4 pr = {0.f, 0.f, 0.f, 0.f};
+      pr = mfma16(raw8(w[g].x), as_bf16x8(b[0]), pr);
+      pr = mfma16(raw8(w[g].y), as_bf16x8(b[1]), pr);
+      pr = mfma16(raw8(w[g].z), as_bf16x8(b[2]), pr);
+      pr = mfma16(raw8(w[g].w), as_bf16x8(b[3]), pr);
+      const uint4 q = sz[g];
+      const float s4[4] = {bf_lo(q.x), bf_hi(q.x), bf_lo(q.y), bf_hi(q.y)};
+      const float z4[4] = {bf_lo(q.z), bf_hi(q.z), bf_lo(q.w), bf_hi(q.w)};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = fmaf(s4[i], pr[i], fmaf(-fmaf(128.f, s4[i], z4[i]), X, acc[i]));
+    }
+  }
+  // lane holds D[n = 4 (l >> 4) + i][m = l & 15]; the RMSNorm row scale is linear: per slice
+  if constexpr (NORM == 3) acc *= rsqrtf(ss / (float)p.K + p.eps);
+  const int m = r16, nsub = 4 * (lane >> 4);
+  if (S == 1) {
+    f32x4 v[1] = {acc};
+    epilogue<1, EPI, false>(p, v, m, nt, nsub, EpiPre<1>{}, m < p.M);
+    return;
+  }
+  constexpr int SLAB = 64 * 4;  // floats per (tile, slice)
+  const uint32_t off = (uint32_t)(((size_t)nt * S + slice) * SLAB * 4);
+  st_sc1_x4(p.slabs, off + (uint32_t)lane * 16u, acc);
+  drain_stores();
+  uint32_t old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(p.counters + nt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __builtin_amdgcn_readfirstlane(old);
+  if (old != (uint32_t)(S - 1)) return;
+  if (lane == 0) __hip_atomic_store(p.counters + nt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t base = (uint32_t)((size_t)nt * S * SLAB * 4);
+  constexpr int SMAX = 16;
+  f32x4 r[SMAX];
+#pragma unroll
+  for (int z = 0; z < SMAX; ++z) r[z] = ld_sc1_x4(p.slabs, base + (uint32_t)(min(z, S - 1) * SLAB * 4 + lane * 16));
+  f32x4 v[1] = {r[0]};
+#pragma unroll
+  for (int z = 1; z < SMAX; ++z)
+    if (z < S) v[0] += r[z];
+  epilogue<1, EPI, false>(p, v, m, nt, nsub, EpiPre<1>{}, m < p.M);
+}
+
 // ---- prefill / medium-M tile GEMM (M > 16, bf16 weights) ----
 // The decode kernels split K across the waves of a block, which is right when x is a
 // few rows; once M grows, every wave would re-load x for its own k-range (the activation
@@ -985,6 +1106,7 @@ struct Plan { int waves, splitk; };
 extern int g_tail_split;  // gemm.hip: -1 = VGATE_TAIL_SPLIT; 0 / 1: set_tail_split (tests)
 extern int g_dec_u;       // gemm.hip: -100 = VGATE_DEC_U; else the forced decode register group size
 extern int g_dec_bal;     // gemm.hip: -1 = VGATE_DEC_BAL; 0 / 1: the balanced decode GEMM off / on
+extern int g_awq_lds;     // gemm.hip: -1 = VGATE_AWQ_LDS (default off); 0 / 1: awq_lds_kernel off / on
 
 inline int cu_count_gemm() {
   static const int n = [] {
@@ -1298,11 +1420,63 @@ static bool launch_awq_stream(GemmParams p, const GemmArgs& g, hipStream_t st) {
   return true;
 }
 
+// AWQ decode with the LDS-shared activation slice (awq_lds_kernel) when it applies: M <= 16, group
+// 128 with the packed scales, no RMSNorm or the producer's hand-off (NORM 0 / 3). Picks T tiles
+// per block and S K-slices (<= 16 k-quads each) for the largest grid that stays within one block
+// per CU. Off by default (measured: 1.49 vs 1.34 ms decode step on Qwen-1.5B AWQ, profiles/
+// r3_rot_awq_lds_negative.log); set_awq_lds(1) / VGATE_AWQ_LDS=1 switches it on (tests, A/B).
+template <int EPI, int NORM>
+static bool launch_awq_lds(GemmParams p, const GemmArgs& g, hipStream_t st) {
+  if constexpr (!(NORM == 0 || NORM == 3)) {
+    return false;
+  } else {
+    static const int env = [] { const char* e = getenv("VGATE_AWQ_LDS"); return e ? atoi(e) : 0; }();
+    if ((g_awq_lds >= 0 ? g_awq_lds : env) == 0) return false;
+    if (g.M > 16 || g.group != 128 || g.awq_szp == nullptr || g.waves > 0 || g.splitk > 0 || g.ntb != 0 ||
+        g.row_idx != nullptr || g.K % 128 != 0)
+      return false;
+    const int ncu = cu_count_gemm();
+    const int ntiles = g.N / 16, KQ = g.K / 128;
+    int bestS = 0, bestT = 0, bestB = 0;
+    for (int S = 1; S <= 16 && S <= KQ; ++S) {
+      if ((KQ + S - 1) / S > 16) continue;
+      for (int T = 1; T <= 8; ++T) {
+        if (ntiles % T) continue;
+        const int blocks = S * (ntiles / T);
+        if (blocks > ncu) continue;
+        if (blocks > bestB) { bestB = blocks; bestS = S; bestT = T; }
+      }
+      if (bestB >= ncu * 7 / 8) break;  // the smallest S that nearly fills the chip
+    }
+    if (bestB == 0) return false;
+    const int S = bestS, T = bestT;
+    if (S > 1) {
+      const size_t need = (size_t)ntiles * S * 64 * 16;
+      if (g.slabs == nullptr || need > g.slab_bytes || ntiles > g.max_counters) return false;
+    }
+    p.splitk = S;
+    const int nqmax = (KQ + S - 1) / S;
+    const size_t lds = (size_t)nqmax * 4 * 1024;
+    if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_lds", bestB);
+    const dim3 grid(bestB), block(64 * (T + 1));
+#define VG_AL(QQ) hipLaunchKernelGGL((awq_lds_kernel<QQ, EPI, NORM>), grid, block, lds, st, p, T, S)
+    if (nqmax <= 4) VG_AL(4);
+    else if (nqmax <= 6) VG_AL(6);
+    else if (nqmax <= 8) VG_AL(8);
+    else if (nqmax <= 10) VG_AL(10);
+    else if (nqmax <= 12) VG_AL(12);
+    else VG_AL(16);
+#undef VG_AL
+    return true;
+  }
+}
+
 template <int NTB, int EPI, int NORM, bool AWQ>
 static void launch_m(GemmParams p, const GemmArgs& g, hipStream_t st) {
   if constexpr (AWQ) {
     // g.ntb: -1 forces the LDS-staged kernel, -2 the K-split awq_gemm_kernel (sweeps / tests)
     if constexpr (NORM != 2) {  // (the gamma-folded row-scale mode has no int4 form)
+      if (g.ntb == 0 && launch_awq_lds<EPI, NORM>(p, g, st)) return;
       if (g.ntb != -2 && launch_awq_stream<EPI, NORM>(p, g, st)) return;
       if (g.ntb != -2 && launch_awq_dec<NTB, EPI, NORM>(p, g, st)) return;
     }

@@ -35,6 +35,10 @@ struct GemmParams {
   // so a grid of q * 256 + r tiles runs as q whole tiles + r / 128 halves per CU instead of q or q + 1
   // whole tiles. 0 = off (grid = (tiles, m-chunks, splitk)).
   int tail_full;
+  // decode kernels: rotate which wave of a block takes which k-range (and, inside a wave's range,
+  // the order of its register groups) by the block index, so the blocks of a launch do not all
+  // request the same activation lines at the same instant (VGATE_DEC_ROT, A/B)
+  int rot;
 };
 
 // (column-tile block, K slice, slices) of this block: the grid decomposition of gemm_finish's hand-off

@@ -612,6 +612,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("kernel_copy", &kernel_copy, "pinned host <-> device copy by a kernel on the current stream (no SDMA)",
         py::arg("dst"), py::arg("src"), py::arg("nbytes"));
   m.def("set_tail_split", &vgate::set_tail_split, "decode GEMM tail split: 1 on, 0 off, -1 environment (tests / sweeps)");
+  m.def("set_flash_prefill", &vgate::set_flash_prefill, "flash prefill attention: 1 on, 0 off, -1 environment");
+  m.def("set_dec_rot", &vgate::set_dec_rot, "decode GEMM k-range rotation by block: 1 on, 0 off, -1 environment");
+  m.def("set_awq_lds", &vgate::set_awq_lds, "AWQ decode, LDS-shared activation slice: 1 on, 0 off, -1 environment");
   m.def("set_dec_bal", &vgate::set_dec_bal, "balanced decode GEMM: 1 on, 0 off, -1 environment (VGATE_DEC_BAL)");
   m.def("set_dec_u", &vgate::set_dec_u, "decode GEMM register group: 0 auto, -1 round-2 rule, 6/8/10/12 forced, -100 environment");
   m.def("ids_to_host", &ids_to_host, "sampled ids -> slot *slot of a pinned host ring (graph-capturable, device-read slot)",

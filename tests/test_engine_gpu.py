@@ -171,3 +171,20 @@ def test_long_prompt_prefill_matches_reference(library, monkeypatch):
     for t, tok in enumerate(g):
         row = logits[t]
         assert row[tok] >= row.max() - 0.05 * row.std(), t
+
+
+def test_awq_engine_matches_dequantized_reference():
+    """AWQ engine (int4 decode kernels, graphs) greedy tokens == the teacher-forced dense fp32
+    forward on the dequantised weights (Linear.dense_weight of an int4 layer), within the bf16
+    rounding margin; graph == eager."""
+    eng = _engine(quantization="awq")
+    sp = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True)
+    reqs = [(k, v, sp) for k, v in list(PROMPTS.items())[:3]]
+    g = _run(eng, reqs)
+    e = _run(_engine(quantization="awq", enforce_eager=True), reqs)
+    for k, ids in list(PROMPTS.items())[:3]:
+        assert g[k].output_ids == e[k].output_ids, k
+        logits = eng.model.reference_logits(ids + g[k].output_ids[:-1])[len(ids) - 1:]
+        for t, tok in enumerate(g[k].output_ids):
+            row = logits[t]
+            assert row[tok] >= row.max() - 0.05 * row.std(), (k, t)

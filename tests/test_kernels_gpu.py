@@ -1135,3 +1135,144 @@ def test_balanced_decode_gemm(M):
             assert _rel_err(y1.float(), y0.float()) < 1e-2, (N, K, kind)
     finally:
         C.set_dec_bal(-1)
+
+
+@pytest.mark.parametrize("M", [1, 5, 8, 16])
+def test_awq_lds_kernel(M):
+    """AWQ decode with the LDS-shared activation slice (awq_lds_kernel: a loader wave DMAs x into
+    LDS, T tile waves stream their int4 k-slices; K-slices combined by slab + ticket) on the
+    Qwen2.5-1.5B shapes: plain + residual (down_proj: 8960-deep K, split over slices), SiLU
+    (gate_up), with and without the RMSNorm hand-off == the dequantised fp32 reference and the
+    awq_stream kernel; deterministic run to run."""
+    C = ops.native()
+    torch.manual_seed(120 + M)
+    g = 128
+    try:
+        for N, K, layout in ((17920, 1536, "silu"), (1536, 8960, "plain"), (1536, 1536, "plain")):
+            q = torch.randint(0, 16, (N, K), dtype=torch.int32)
+            sc = (torch.rand(K // g, N) * 0.01 + 0.002).bfloat16()
+            zz = torch.randint(0, 16, (K // g, N)).float().bfloat16()
+            wd = ref.awq_dequant_ref(q, sc, zz, g).to(DEV)
+            lin = ops.Linear(None, kind="awq", awq={"qint": q, "scales": sc.to(DEV), "zeros": zz.to(DEV), "group": g,
+                                                    "layout": layout})
+            x = torch.randn(M, K, device=DEV).bfloat16()
+            res = torch.randn(M, N, device=DEV).bfloat16()
+            outs = {}
+            for on in (1, 0):
+                C.set_awq_lds(on)
+                if layout == "silu":
+                    y = ops.linear(x, lin)
+                    y2 = ops.linear(x, lin)
+                else:
+                    y = res.clone()
+                    ops.linear(x, lin, out=y, residual=y)
+                    y2 = res.clone()
+                    ops.linear(x, lin, out=y2, residual=y2)
+                assert torch.equal(y, y2), (N, K, on)
+                outs[on] = y
+            want = (ref.silu_mul_linear_ref(x, wd[: N // 2], wd[N // 2:]) if layout == "silu"
+                    else ref.linear_ref(x, wd, None, res))
+            assert _rel_err(outs[1], want) < 2e-2, (N, K, _rel_err(outs[1], want))
+            assert _rel_err(outs[1], outs[0]) < 1e-2, (N, K)
+            # RMSNorm hand-off consumer (x = h * gamma, row scale from the producer's sums)
+            if K == 1536:
+                gamma = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+                hg = (x.float() * gamma.float()).bfloat16()
+                ssp = x.float().pow(2).reshape(M, K // 16, 16).sum(-1)
+                o_n = torch.empty(M, lin.out_features, dtype=torch.bfloat16, device=DEV)
+                o_h = torch.empty_like(o_n)
+                C.set_awq_lds(0)
+                ops.linear(x, lin, out=o_n, norm=(gamma, 1e-6))
+                C.set_awq_lds(1)
+                ops.linear(hg, lin, out=o_h, prenorm=(ssp, 1e-6))
+                assert _rel_err(o_h, o_n) < 1e-2, (N, K, _rel_err(o_h, o_n))
+    finally:
+        C.set_awq_lds(-1)
+
+
+@pytest.mark.parametrize("M", [3, 8, 12])
+def test_decode_gemm_block_rotation(M):
+    """Decode GEMM with the k-range / group order rotated by block (set_dec_rot): same product
+    (fp32 reference), deterministic run to run, close to the unrotated kernel."""
+    C = ops.native()
+    torch.manual_seed(150 + M)
+    try:
+        for N, K, kind, waves, splitk in ((1536, 8960, "plain", 8, 2), (17920, 1536, "silu", 2, 1),
+                                          (2048, 1536, "plain", 8, 1)):
+            x = torch.randn(M, K, device=DEV).bfloat16()
+            w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+            g = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+            lin = ops.Linear(w, kind=kind) if kind == "silu" else ops.Linear(w)
+            if kind == "silu":
+                lin.fold_norm(g)
+            res = torch.randn(M, N // (2 if kind == "silu" else 1), device=DEV).bfloat16()
+
+            def run():
+                if kind == "silu":
+                    return ops.linear(x, lin, norm=(g, 1e-6), waves=waves, splitk=splitk)
+                y = res.clone()
+                ops.linear(x, lin, out=y, residual=y, waves=waves, splitk=splitk)
+                return y
+            C.set_dec_rot(0)
+            y0 = run()
+            C.set_dec_rot(1)
+            y1, y2 = run(), run()
+            assert torch.equal(y1, y2)
+            assert _rel_err(y1.float(), y0.float()) < 1e-2, (N, K, kind)
+            if kind == "silu":
+                xn, _ = ref.rmsnorm_ref(x.cpu(), g.cpu(), 1e-6)
+                r = ref.silu_mul_linear_ref(xn, w.cpu()[: N // 2], w.cpu()[N // 2:])
+            else:
+                r = ref.linear_ref(x.cpu(), w.cpu(), None, res.cpu())
+            assert _rel_err(y1.float().cpu(), r.float()) < 1e-2, (N, K, kind)
+    finally:
+        C.set_dec_rot(-1)
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (12, 2), (8, 1), (16, 16)])
+def test_flash_prefill_matches_tile_kernel_and_reference(Hq, Hkv):
+    """Flash prefill (64- / 32-query blocks x the G heads of a KV head, K / V double-buffered in LDS
+    by DMA) == the 16-query tile kernel and the fp32 reference: ragged prompts, chunked prefill
+    against cached tokens, padding tiles of a graph bucket (tile_seq = -1), and a mixed step with
+    decode rows through the unified launch (decode rows keep the decode kernel)."""
+    C = ops.native()
+    torch.manual_seed(200 + Hq + Hkv)
+    D = 128
+    qlens = [1, 33, 64, 65, 200, 1]
+    ctxs = [40, 33, 300, 65, 456, 77]
+    S = len(qlens)
+    maxb = max(ctxs) // 16 + 2
+    nblk = S * maxb + 4
+    kc, vc = _make_cache(nblk, Hkv, seed=5)
+    bt = (torch.randperm(nblk)[: S * maxb]).reshape(S, maxb).int().to(DEV)
+    qs = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32, device=DEV)
+    T = int(qs[-1])
+    cl = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
+    stride = (Hq + 2 * Hkv) * D
+    qkv = torch.randn(T, stride, device=DEV).bfloat16()
+    ts, tq = ops.prefill_tiles(qlens)
+    ts, tq = ts + [-1] * 5, tq + [0] * 5  # a bucket's padding tiles
+    ts = torch.tensor(ts, dtype=torch.int32, device=DEV)
+    tq = torch.tensor(tq, dtype=torch.int32, device=DEV)
+    scale = 1 / math.sqrt(D)
+    outs = []
+    try:
+        for on in (1, 0):
+            C.set_flash_prefill(on)
+            out = torch.zeros(T, Hq * D, device=DEV).bfloat16()
+            ops.attention_prefill(qkv, stride, kc, vc, bt, cl, qs, ts, tq, out, Hq, Hkv, scale)
+            outs.append(out)
+        q = qkv[:, : Hq * D].reshape(T, Hq, D)
+        r = ref.attention_ref(q, kc, vc, bt, cl, qs.cpu(), Hq, Hkv, scale)
+        assert _rel_err(outs[0].view(T, Hq, D), r) < 2e-2
+        assert _rel_err(outs[0], outs[1]) < 1e-2
+        # mixed step: the unified launch with decode rows (query length 1 sequences) and prefill tiles
+        C.set_flash_prefill(1)
+        P = 4
+        po = torch.empty(S, Hq, P, D, device=DEV)
+        pml = torch.empty(S, Hq, P, 2, device=DEV)
+        out = torch.zeros(T, Hq * D, device=DEV).bfloat16()
+        ops.attention(qkv, stride, kc, vc, bt, cl, qs, ts, tq, out, po, pml, Hq, Hkv, 512, scale)
+        assert _rel_err(out.view(T, Hq, D), r) < 2e-2
+    finally:
+        C.set_flash_prefill(-1)

@@ -237,18 +237,22 @@ class Linear:
         if self.wp is None or self.norm_gamma is not None:
             return False
         if self.kind == "awq":
-            q = unpack_awq(self.wp, self.N, self.K)  # permuted row order, like scales / zeros
-            g = torch.arange(self.K, device=q.device) // self.group
-            w = (q.float() * self.scales.float()[g].t() - self.zeros.float()[g].t()).to(torch.bfloat16)
-            perm = row_permutation(self.N, self.layout)
-            if perm is not None:
-                out = torch.empty_like(w)
-                out[perm.to(w.device)] = w
-                w = out
-            self.wl = w.contiguous()
+            self.wl = self._awq_dense().contiguous()
             return True
         self.wl = self.dense_weight().contiguous()
         return True
+
+    def _awq_dense(self) -> torch.Tensor:
+        """int4 -> bf16 (v * s - s * z) in the original row order."""
+        q = unpack_awq(self.wp, self.N, self.K)  # permuted row order, like scales / zeros
+        g = torch.arange(self.K, device=q.device) // self.group
+        w = (q.float() * self.scales.float()[g].t() - self.zeros.float()[g].t()).to(torch.bfloat16)
+        perm = row_permutation(self.N, self.layout)
+        if perm is not None:
+            out = torch.empty_like(w)
+            out[perm.to(w.device)] = w
+            w = out
+        return w
 
     @property
     def out_features(self) -> int:
@@ -258,8 +262,8 @@ class Linear:
         """[N, K] in the ORIGINAL row order (references / checkpoint export)."""
         if self.w is not None:
             return self.w
-        if self.kind == "awq":
-            raise NotImplementedError("AWQ weights are kept packed on the GPU")
+        if self.kind == "awq":  # dequantised bf16 (v - z) * s in the original row order (references)
+            return self._awq_dense()
         w = unpack_weight(self.wp, self.N, self.K)
         if self.norm_gamma is not None:  # un-fold (approximate: W' was rounded to bf16)
             w = (w.float() / self.norm_gamma.to(w.device, torch.float32)[None]).to(torch.bfloat16)
@@ -569,12 +573,26 @@ def attention_decode(q, q_stride, k_cache, v_cache, block_tables, context_lens, 
 
 
 def prefill_tiles(query_lens: list[int]) -> tuple[list[int], list[int]]:
+    """16-query prefill tiles (sequence, first query) in the attention kernel's order: see
+    :func:`tile_order`."""
     seq, q0 = [], []
     for s, ql in enumerate(query_lens):
-        for t in range(0, ql, 16):
+        for t in tile_order(ql):
             seq.append(s)
-            q0.append(t)
+            q0.append(int(t))
     return seq, q0
+
+
+def tile_order(qlen: int):
+    """First queries of a sequence's 16-query tiles, ordered for the flash prefill kernel: tiles
+    starting a 64-query group first, then those starting a 32-query group, then the rest, each class
+    longest causal range first. The flash kernel runs one block per tile and only group leaders
+    work (64 queries for <= 4 heads per KV head, 32 for <= 8), so the working blocks are the first
+    ones of the grid, spread round-robin over the 8 XCDs instead of every 4th block landing on the
+    same two; the 16-query kernel is order-free."""
+    import numpy as _np
+    t = _np.arange(0, qlen, 16, dtype=_np.int32)[::-1]
+    return _np.concatenate([t[t % 64 == 0], t[t % 64 == 32], t[t % 32 != 0]])
 
 
 def attention_prefill(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start,

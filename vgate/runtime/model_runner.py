@@ -186,10 +186,12 @@ class ModelRunner:
             qs[s + 1] = t
             sidx[s] = t - 1
             if n > 1:
-                for q0 in range(0, n, 16):
-                    tseq[ntile] = s
-                    tq0[ntile] = q0
-                    ntile += 1
+                order = ops.tile_order(n)
+                k = len(order)
+                if ntile + k <= len(tseq):
+                    tseq[ntile: ntile + k] = s
+                    tq0[ntile: ntile + k] = order
+                ntile += k
             sp = seq.params
             temp[s] = 0.0 if sp.greedy else sp.temperature
             topp[s] = sp.top_p
