@@ -38,7 +38,6 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--o-tiles", type=int, default=96, help="o_proj column tiles of a fused attn_o launch (N / 16)")
     a = ap.parse_args()
-    C = ops.native()
     eng = LLMEngine(EngineConfig(model=a.model, device="cuda:0", max_model_len=2048, max_num_seqs=a.max_seqs,
                                  max_num_batched_tokens=2048, num_kv_blocks=a.kv_blocks or None, warmup=False,
                                  quantization=a.quantization))
@@ -49,6 +48,31 @@ def main():
     eng._drain_inbox()
     for _ in range(4):  # prefill + a few decode steps (graphs of the decode bucket captured)
         eng.step()
+    summary, live, cap, t = measure(eng)
+    summary.update(batch=a.batch, ctx=a.ctx)
+    print(json.dumps(summary), flush=True)
+    # fused attention + o_proj launches: the two block roles' timings (blocks [0, nb - o_tiles)
+    # are attention, the rest o_proj column tiles), relative to the launch's first block start
+    for name, off, nb in cap:
+        if name != "attn_o":
+            continue
+        blk = t[off // 2: off // 2 + nb]
+        t0 = blk[:, 0].min()
+        nA = nb - a.o_tiles
+        f = lambda v: [round(float(x) / TICKS_PER_US, 2) for x in (v.min(), v.float().median(), v.max())]  # noqa: E731
+        print(json.dumps({"attn_o_roles": {"attn_end_min_med_max": f(blk[:nA, 1] - t0),
+                                           "o_start_min_med_max": f(blk[nA:, 0] - t0),
+                                           "o_end_min_med_max": f(blk[nA:, 1] - t0)}}))
+    for x in live[:14]:
+        print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in x.items() if k not in ("t0", "t1")}))
+    if a.json:
+        Path(a.json).write_text(json.dumps({"summary": summary, "launches": live}, indent=1))
+
+
+def measure(eng):
+    """Re-capture the engine's decode bucket(s) with timeline slots, run one step, and return
+    (summary, launches in start order, captured launch entries, raw stamps)."""
+    C = ops.native()
     r = eng.runner
     torch.cuda.synchronize()
     keys = list(r.graphs.keys())
@@ -98,30 +122,14 @@ def main():
         g["gap_after_us"] += x["gap_after_us"]
     total = (live[-1]["t1"] - T0) / TICKS_PER_US
     spans = sum(x["span_us"] for x in live)
-    summary = {"batch": a.batch, "ctx": a.ctx, "kv_blocks": eng.num_blocks, "launches": len(live), "step_us": round(total, 1), "sum_span_us": round(spans, 1),
+    summary = {"kv_blocks": eng.num_blocks, "launches": len(live), "step_us": round(total, 1), "sum_span_us": round(spans, 1),
                "sum_gap_us": round(total - spans, 1),
                "per_kernel": {f"{k[0]}[{k[1]}]": {"n": v["n"], "avg_span_us": round(v["span_us"] / v["n"], 2),
                                                   "avg_gap_after_us": round(v["gap_after_us"] / v["n"], 2),
                                                   **{k: round(v[k] / v["n"], 2) for k in ("dur_p10", "dur_med", "dur_p90",
                                                      "dur_max", "start_p90", "start_max", "end_p10", "end_p50", "end_p90")}}
                               for k, v in sorted(agg.items(), key=lambda kv: -kv[1]["span_us"])}}
-    print(json.dumps(summary), flush=True)
-    # fused attention + o_proj launches: the two block roles' timings (blocks [0, nb - o_tiles)
-    # are attention, the rest o_proj column tiles), relative to the launch's first block start
-    for name, off, nb in cap:
-        if name != "attn_o":
-            continue
-        blk = t[off // 2: off // 2 + nb]
-        t0 = blk[:, 0].min()
-        nA = nb - a.o_tiles
-        f = lambda v: [round(float(x) / TICKS_PER_US, 2) for x in (v.min(), v.float().median(), v.max())]  # noqa: E731
-        print(json.dumps({"attn_o_roles": {"attn_end_min_med_max": f(blk[:nA, 1] - t0),
-                                           "o_start_min_med_max": f(blk[nA:, 0] - t0),
-                                           "o_end_min_med_max": f(blk[nA:, 1] - t0)}}))
-    for x in live[:14]:
-        print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in x.items() if k not in ("t0", "t1")}))
-    if a.json:
-        Path(a.json).write_text(json.dumps({"summary": summary, "launches": live}, indent=1))
+    return summary, live, cap, t
 
 
 if __name__ == "__main__":

@@ -77,7 +77,18 @@ struct ArClock {
 };
 
 // blocks per call: VGATE_AR_BLOCKS (16..128, read once per process, so every rank of a group
-// launched with the same environment agrees; benchmarks/ar_bench.py sweeps it), default 64
+// launched with the same environment agrees; benchmarks/allreduce_bench.py sweeps it), default 64
+// polls before a wait gives up: VGATE_AR_SPIN_LIMIT (default AR_SPIN_LIMIT; tests shorten it to
+// exercise the timeout path in milliseconds), read once per process
+static uint32_t ar_spin_limit() {
+  static const uint32_t n = [] {
+    const char* e = getenv("VGATE_AR_SPIN_LIMIT");
+    const long v = e ? atol(e) : (long)AR_SPIN_LIMIT;
+    return (uint32_t)(v < 1000 ? 1000 : v);
+  }();
+  return n;
+}
+
 static int ar_blocks() {
   static const int n = [] {
     const char* e = getenv("VGATE_AR_BLOCKS");
@@ -89,9 +100,29 @@ static int ar_blocks() {
   return n;
 }
 
+// wait until every peer arrived at epoch e in `flags` (one lane per peer). A timed-out wait sets
+// the sticky error word and gives up; once it is set, later calls do not wait at all (the group is
+// one failure domain: the engine reads the word after the step and fails it), so a dead peer costs
+// one spin limit, not one per collective of the step.
+__device__ __forceinline__ void ar_wait_all(uint32_t (*flags)[AR_MAX_RANKS], int b, int world, uint32_t e,
+                                            ArSignal* me, uint32_t spin_limit) {
+  const int tid = threadIdx.x;
+  if (tid < world && __hip_atomic_load(&me->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
+    unsigned spins = 0;
+    while ((int32_t)(__hip_atomic_load(&flags[b][tid], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+      if (++spins > spin_limit) {
+        __hip_atomic_store(&me->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(AR_THREADS) void ar_one_shot_kernel(const uint4* in, uint4* out,  // may alias
                                                                ArPeers peers, int rank, int world,
-                                                               int64_t n16, int64_t max_bytes) {
+                                                               int64_t n16, int64_t max_bytes, uint32_t spin_limit) {
   const int b = blockIdx.x, tid = threadIdx.x, nblk = gridDim.x;
   ArSignal* me = reinterpret_cast<ArSignal*>(peers.base[rank]);
   const ArClock clk(me);
@@ -112,17 +143,7 @@ __global__ __launch_bounds__(AR_THREADS) void ar_one_shot_kernel(const uint4* in
     ArSignal* peer = reinterpret_cast<ArSignal*>(peers.base[tid]);
     __hip_atomic_store(&peer->flags[b][rank], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  if (tid < world) {
-    unsigned spins = 0;
-    while ((int32_t)(__hip_atomic_load(&me->flags[b][tid], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
-      if (++spins > AR_SPIN_LIMIT) {
-        __hip_atomic_store(&me->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  __syncthreads();
+  ar_wait_all(me->flags, b, world, e, me, spin_limit);
   // reduce slice b over the ranks (fp32 accumulation, fixed rank order on every rank)
   // every peer's vector is loaded before the first is summed (a runtime-trip loop would wait
   // one xGMI round trip per peer); slots past `world` re-read rank 0 and are masked
@@ -148,22 +169,6 @@ __global__ __launch_bounds__(AR_THREADS) void ar_one_shot_kernel(const uint4* in
   if (tid == 0) me->epoch[b] = e;
 }
 
-__device__ __forceinline__ void ar_wait_all(uint32_t (*flags)[AR_MAX_RANKS], int b, int world, uint32_t e,
-                                            ArSignal* me) {
-  const int tid = threadIdx.x;
-  if (tid < world) {
-    unsigned spins = 0;
-    while ((int32_t)(__hip_atomic_load(&flags[b][tid], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
-      if (++spins > AR_SPIN_LIMIT) {
-        __hip_atomic_store(&me->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  __syncthreads();
-}
-
 // Two-shot all-reduce for the 0.5-8 MiB range (TP prefill chunks, 70B decode at large batch):
 // reduce-scatter then all-gather, each rank moving 2 (n-1)/n of the message over its n-1
 // direct xGMI links instead of the one-shot's (n-1) full copies. Block b owns sub-range b of
@@ -176,7 +181,8 @@ __device__ __forceinline__ void ar_wait_all(uint32_t (*flags)[AR_MAX_RANKS], int
 // Safety of the parity buffers is the one-shot's argument: a peer cannot pass phase 1 of call
 // e+1 (writing the other parity) before I arrive there, i.e. before I finished reading call e.
 __global__ __launch_bounds__(AR_THREADS) void ar_two_shot_kernel(const uint4* in, uint4* out, ArPeers peers,
-                                                               int rank, int world, int64_t n16, int64_t max_bytes) {
+                                                               int rank, int world, int64_t n16, int64_t max_bytes,
+                                                               uint32_t spin_limit) {
   const int b = blockIdx.x, tid = threadIdx.x, nblk = gridDim.x;
   ArSignal* me = reinterpret_cast<ArSignal*>(peers.base[rank]);
   const ArClock clk(me);
@@ -203,7 +209,7 @@ __global__ __launch_bounds__(AR_THREADS) void ar_two_shot_kernel(const uint4* in
     ArSignal* peer = reinterpret_cast<ArSignal*>(peers.base[tid]);
     __hip_atomic_store(&peer->flags[b][rank], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  ar_wait_all(me->flags, b, world, e, me);
+  ar_wait_all(me->flags, b, world, e, me, spin_limit);
   {
     int64_t a, z;
     slice(rank, a, z);
@@ -235,7 +241,7 @@ __global__ __launch_bounds__(AR_THREADS) void ar_two_shot_kernel(const uint4* in
     ArSignal* peer = reinterpret_cast<ArSignal*>(peers.base[tid]);
     __hip_atomic_store(&peer->flags2[b][rank], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  ar_wait_all(me->flags2, b, world, e, me);
+  ar_wait_all(me->flags2, b, world, e, me, spin_limit);
   for (int r = 0; r < world; ++r) {
     if (r == rank) continue;
     int64_t a, z;
@@ -252,7 +258,8 @@ __global__ __launch_bounds__(AR_THREADS) void ar_two_shot_kernel(const uint4* in
 // parity / bounded-wait protocol as the all-reduces, so the three kinds interleave freely and
 // the call is captured into the TP decode hipGraphs (a gloo or RCCL all-gather is not needed).
 __global__ __launch_bounds__(AR_THREADS) void ar_all_gather_kernel(const uint4* in, uint4* out, ArPeers peers,
-                                                                 int rank, int world, int64_t n16, int64_t max_bytes) {
+                                                                 int rank, int world, int64_t n16, int64_t max_bytes,
+                                                                 uint32_t spin_limit) {
   const int b = blockIdx.x, tid = threadIdx.x, nblk = gridDim.x;
   ArSignal* me = reinterpret_cast<ArSignal*>(peers.base[rank]);
   const ArClock clk(me);
@@ -271,7 +278,7 @@ __global__ __launch_bounds__(AR_THREADS) void ar_all_gather_kernel(const uint4* 
     ArSignal* peer = reinterpret_cast<ArSignal*>(peers.base[tid]);
     __hip_atomic_store(&peer->flags3[b][rank], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  ar_wait_all(me->flags3, b, world, e, me);
+  ar_wait_all(me->flags3, b, world, e, me, spin_limit);
   for (int p = 0; p < world; ++p) {
     const uint4* src = p == rank ? in : reinterpret_cast<const uint4*>(peers.base[p] + par_off);
     for (int64_t i = i0 + tid; i < i1; i += AR_THREADS) out[(int64_t)p * n16 + i] = p == rank ? src[i] : ld_nt16(src + i);
@@ -290,7 +297,7 @@ void launch_custom_allgather(const void* in, void* out, int64_t nbytes, char* co
   for (int p = 0; p < world && p < AR_MAX_RANKS; ++p) peers.base[p] = bases[p];
   hipLaunchKernelGGL(ar_all_gather_kernel, dim3(ar_blocks()), dim3(AR_THREADS), 0, st,
                      reinterpret_cast<const uint4*>(in), reinterpret_cast<uint4*>(out), peers, rank, world,
-                     nbytes / 16, max_bytes);
+                     nbytes / 16, max_bytes, ar_spin_limit());
 }
 
 void launch_custom_allreduce(const void* in, void* out, int64_t nbytes, char* const* bases, int rank, int world,
@@ -304,11 +311,11 @@ void launch_custom_allreduce(const void* in, void* out, int64_t nbytes, char* co
   if (two)
     hipLaunchKernelGGL(ar_two_shot_kernel, dim3(ar_blocks()), dim3(AR_THREADS), 0, st,
                        reinterpret_cast<const uint4*>(in), reinterpret_cast<uint4*>(out), peers, rank, world,
-                       nbytes / 16, max_bytes);
+                       nbytes / 16, max_bytes, ar_spin_limit());
   else
     hipLaunchKernelGGL(ar_one_shot_kernel, dim3(ar_blocks()), dim3(AR_THREADS), 0, st,
                        reinterpret_cast<const uint4*>(in), reinterpret_cast<uint4*>(out), peers, rank, world,
-                       nbytes / 16, max_bytes);
+                       nbytes / 16, max_bytes, ar_spin_limit());
 }
 
 }  // namespace vgate

@@ -510,51 +510,58 @@ __device__ __forceinline__ void prefill_body(const AttnArgs& a, int tile, int h,
 }
 
 // ------------------------------------------------------- flash prefill ----
-// Causal (chunked-prefill capable) attention of a block of QPB query tokens x the G query heads of
-// one KV head. Waves: (QPB / 32) x G, each owns 32 queries (two 16-query MFMA column tiles) of one
-// head; Q lives in registers. K / V stream through LDS in 64-token chunks, double-buffered and
-// SHARED by every wave of the block (GQA: one K/V byte serves G heads x QPB queries), moved by
-// LDS-DMA (global_load_lds_dwordx4: no VGPRs, every wave issues a share of the 32 1-KiB pieces) —
-// the DMA of chunk c + 1 is issued before chunk c's MFMAs, one barrier per chunk.
+// Causal (chunked-prefill capable) attention of a block of QPB = 16 CT query tokens x the G query
+// heads of one KV head: G waves, wave w owns head h G + w for all QPB queries (CT 16-query MFMA
+// column tiles); Q lives in registers. K / V stream through LDS in 64-token chunks, double-buffered
+// and SHARED by the block's waves (GQA: one K/V byte serves G heads x QPB queries), moved by LDS-DMA
+// (global_load_lds_dwordx4: no VGPRs, every wave issues a share of the 32 1-KiB pieces) — the DMA
+// of chunk c + 1 is issued before chunk c's MFMAs, one barrier per chunk.
 //   S^T = K Q^T (swapped: softmax statistics lane-local, row reductions by two xor-swaps); K image
 //   16-B chunks XOR-swizzled by row & 15 (conflict-free ds_read_b128 of the A operand);
 //   O^T += V^T P^T with V^T read by ds_read_b64_tr_b16 from the 8-B-chunk-swizzled V image and P^T
 //   built in registers (pack_p), as in the decode kernel.
+// Softmax per chunk: the causal mask only on chunks that cross a query's bound (the others are
+// below every query of the block), the scale folded into the exp2 argument (one fma), and the
+// O / l rescale only when some column's running max moved (wave-uniform test; exact: alpha = 1
+// otherwise).
+// Blocks are small (G waves, 64 KiB of LDS + the staged block table) so two fit a CU: the two
+// blocks' waves on one SIMD drift apart and overlap one's softmax with the other's MFMAs.
 // The host's 16-query tile list is reused: a block whose tile starts a QPB-aligned group leads it
 // (others exit at once). The host lists the group leaders first, longest causal range first
 // (ops.tile_order), so the working blocks are the grid's first ones, spread over all 8 XCDs and
-// the longest start first. Tokens past the causal bound are masked; pages past the context are
-// not read.
+// the longest start first. Pages past the causal bound are not read.
 extern int g_flash_prefill;
 constexpr int FL_KV = 64;
 constexpr int FL_LDS = 4 * FL_KV * D_ * 2;  // K x2 + V x2 (64 KiB)
 
-// fx = this block's index among the launch's prefill blocks; waves past (qpb / 32) x G (a unified
-// launch sized for wider decode blocks) join the DMA and the barriers but own no queries
-__device__ __forceinline__ void flash_body(const AttnArgs& a, int fx, int h, int qpb, char* smem) {
+template <int CT>
+__global__ __launch_bounds__(512, CT == 1 ? 3 : 2) void attn_flash_kernel(AttnArgs a) {
+  constexpr int QPB = 16 * CT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  TLScope tl_scope(a.tl);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int G = a.Hq / a.Hkv;
-  const int tile = fx;  // the host lists group leaders first, longest first (ops.tile_order)
+  const int h = blockIdx.y;
+  const int tile = blockIdx.x;
   const int s = a.tile_seq[tile];
   if (s < 0) return;
   const int q0 = a.tile_q0[tile];
-  if (q0 % qpb) return;  // block-uniform: not a group leader
+  if (q0 % QPB) return;  // block-uniform: not a group leader
   const int qs = a.query_start[s];
   const int qlen = a.query_start[s + 1] - qs;
   const int ctx = a.context_lens[s];
-  const int hq = h * G + wid % G;
-  const int qw0 = q0 + 32 * (wid / G);
-  const int qhi = min(q0 + qpb, qlen);  // this block's queries: [q0, qhi)
-  const int qlast = min(q0 + qpb, qlen) - 1;
-  const int kv_end = ctx - qlen + qlast + 1;  // the block's causal bound (exclusive)
+  const int hq = h * G + wid;
+  const int qhi = min(q0 + QPB, qlen);   // this block's queries: [q0, qhi)
+  const int kv_end = ctx - qlen + qhi;   // the block's causal bound (exclusive)
   const int nch = (kv_end + FL_KV - 1) / FL_KV;
+  const int nfull = max(0, ctx - qlen + q0 + 1) / FL_KV;  // chunks below every query's bound
   const int col = lane & 15, g4 = lane >> 4;
-  // Q fragments (B operand of S^T = K Q^T): 2 column tiles x 4 k-slices
-  uint4 qf[2][4];
-  int lim[2];
+  // Q fragments (B operand of S^T = K Q^T): CT column tiles x 4 k-slices
+  uint4 qf[CT][4];
+  int lim[CT];
 #pragma unroll
-  for (int ct = 0; ct < 2; ++ct) {
-    const int qi = qw0 + 16 * ct + col;
+  for (int ct = 0; ct < CT; ++ct) {
+    const int qi = q0 + 16 * ct + col;
     const bool ok = qi < qhi;
     lim[ct] = ok ? ctx - qlen + qi + 1 : 0;
     const bf16_t* qp = a.q + (size_t)(qs + (ok ? qi : 0)) * a.q_stride + (size_t)hq * D_ + 8 * g4;
@@ -603,12 +610,15 @@ __device__ __forceinline__ void flash_body(const AttnArgs& a, int fx, int h, int
     }
   };
   const float cscale = a.scale * LOG2E;
-  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-  f32x4 o[2][8];
+  float m[CT], l[CT];  // running max (scaled, log2 domain) and sum per column
+  f32x4 o[CT][8];
 #pragma unroll
-  for (int ct = 0; ct < 2; ++ct)
+  for (int ct = 0; ct < CT; ++ct) {
+    m[ct] = -INFINITY;
+    l[ct] = 0.f;
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) o[ct][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   if (nch > 0) issue(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Q fragments and chunk 0 landed
   __builtin_amdgcn_s_barrier();
@@ -616,54 +626,59 @@ __device__ __forceinline__ void flash_body(const AttnArgs& a, int fx, int h, int
     if (c + 1 < nch) issue(c + 1);  // into the buffer every wave finished reading last iteration
     const char* kb = smem + (c & 1) * (FL_KV * D_ * 2);
     const bf16_t* vb = reinterpret_cast<const bf16_t*>(smem + 2 * (FL_KV * D_ * 2) + (c & 1) * (FL_KV * D_ * 2));
-    // S^T tiles: 4 token tiles x 2 column tiles
-    f32x4 st[4][2];
+    // S^T tiles: 4 token tiles x CT column tiles
+    f32x4 st[4][CT];
 #pragma unroll
     for (int tt = 0; tt < 4; ++tt) {
-      st[tt][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-      st[tt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) st[tt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
       const char* krow = kb + (16 * tt + col) * 256;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         const uint4 kf = *reinterpret_cast<const uint4*>(krow + (((4 * kk + g4) ^ col) << 4));
-        st[tt][0] = mfma16(as_bf16x8(kf), as_bf16x8(qf[0][kk]), st[tt][0]);
-        st[tt][1] = mfma16(as_bf16x8(kf), as_bf16x8(qf[1][kk]), st[tt][1]);
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) st[tt][ct] = mfma16(as_bf16x8(kf), as_bf16x8(qf[ct][kk]), st[tt][ct]);
       }
     }
     // online softmax per column tile over the 64 tokens (lane: column col, tokens 16 tt + 4 g4 + i)
-    bf16x8 pb[2][2];
+    const bool masked = c >= nfull;  // block-uniform
+    bf16x8 pb[CT][2];
 #pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
+    for (int ct = 0; ct < CT; ++ct) {
+      if (masked) {
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (c * FL_KV + 16 * tt + 4 * g4 + i >= lim[ct]) st[tt][ct][i] = -INFINITY;
+      }
       float cmax = -INFINITY;
 #pragma unroll
-      for (int tt = 0; tt < 4; ++tt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int t = c * FL_KV + 16 * tt + 4 * g4 + i;
-          st[tt][ct][i] = t < lim[ct] ? st[tt][ct][i] * cscale : -INFINITY;
-          cmax = fmaxf(cmax, st[tt][ct][i]);
-        }
+      for (int tt = 0; tt < 4; ++tt) cmax = fmaxf(cmax, fmaxf(fmaxf(st[tt][ct][0], st[tt][ct][1]), fmaxf(st[tt][ct][2], st[tt][ct][3])));
       cmax = fmaxf(cmax, xor16(cmax));
       cmax = fmaxf(cmax, xor32(cmax));
-      const float mn = fmaxf(m[ct], cmax);
-      const float mref = mn == -INFINITY ? 0.f : mn;  // fully masked column: exp2(-inf) = 0, no NaN
-      const float alpha = __builtin_amdgcn_exp2f(m[ct] - mref);
+      const float mn = fmaxf(m[ct], cmax * cscale);
+      if (__any(mn > m[ct])) {  // wave-uniform: rescale only when a running max moved
+        const float alpha = __builtin_amdgcn_exp2f(m[ct] - (mn == -INFINITY ? 0.f : mn));
+        l[ct] *= alpha;
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) o[ct][mt] *= alpha;
+        m[ct] = mn;
+      }
+      const float mref = m[ct] == -INFINITY ? 0.f : m[ct];  // fully masked column: exp2(-inf) = 0, no NaN
       float ps = 0.f;
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          st[tt][ct][i] = __builtin_amdgcn_exp2f(st[tt][ct][i] - mref);
+          st[tt][ct][i] = __builtin_amdgcn_exp2f(fmaf(st[tt][ct][i], cscale, -mref));
           ps += st[tt][ct][i];
         }
-      l[ct] = l[ct] * alpha + ps;
-      m[ct] = mn;
-#pragma unroll
-      for (int mt = 0; mt < 8; ++mt) o[ct][mt] *= alpha;
+      l[ct] += ps;
       pb[ct][0] = pack_p(st[0][ct], st[1][ct]);
       pb[ct][1] = pack_p(st[2][ct], st[3][ct]);
     }
-    // O^T += V^T P^T: each V^T fragment (ds_read_b64_tr_b16) feeds both column tiles
+    // O^T += V^T P^T: each V^T fragment (ds_read_b64_tr_b16) feeds every column tile
     const int q = (lane >> 2) & 3, p4 = lane & 3;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -676,19 +691,19 @@ __device__ __forceinline__ void flash_body(const AttnArgs& a, int fx, int h, int
         bf16x8 av;
         av[0] = lo[0]; av[1] = lo[1]; av[2] = lo[2]; av[3] = lo[3];
         av[4] = hi[0]; av[5] = hi[1]; av[6] = hi[2]; av[7] = hi[3];
-        o[0][mt] = mfma16(av, pb[0][half], o[0][mt]);
-        o[1][mt] = mfma16(av, pb[1][half], o[1][mt]);
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) o[ct][mt] = mfma16(av, pb[ct][half], o[ct][mt]);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of chunk c + 1 landed
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // everyone's; buffer c & 1 free
   }
 #pragma unroll
-  for (int ct = 0; ct < 2; ++ct) {
+  for (int ct = 0; ct < CT; ++ct) {
     float ll = l[ct];
     ll += xor16(ll);
     ll += xor32(ll);
-    const int qi = qw0 + 16 * ct + col;
+    const int qi = q0 + 16 * ct + col;
     if (qi >= qhi) continue;
     const float inv = ll > 0.f ? 1.f / ll : 0.f;
     const size_t orow = (size_t)(qs + qi) * a.out_stride + (size_t)hq * D_;
@@ -702,13 +717,15 @@ __device__ __forceinline__ void flash_body(const AttnArgs& a, int fx, int h, int
   }
 }
 
-// queries per flash block for a head group of G (<= 8 waves of 32 queries: ~170 VGPRs per wave, so
-// 512-thread blocks; at 12 waves the O / S / Q fragments spilled), 0 = not supported
-static int flash_qpb(const AttnArgs& a) {
+// column tiles per flash wave for a head group of G (0 = not supported): two (32 queries per block)
+// up to G = 4, where 4-wave blocks pair up on a CU; one (16 queries) for G <= 8, which keeps the
+// grid >= 2 blocks per CU at 2k tokens for the 1-2 KV-head layouts (VGATE_FLASH_CT=2 forces two)
+static int flash_ct(const AttnArgs& a) {
   if (a.D != D_ || a.BS != BS_ || a.Hkv <= 0 || a.Hq % a.Hkv) return 0;
   const int G = a.Hq / a.Hkv;
-  if (G <= 4) return 64;
-  if (G <= 8) return 32;
+  if (G <= 4) return 2;
+  static const int force = [] { const char* e = getenv("VGATE_FLASH_CT"); return e ? atoi(e) : 0; }();
+  if (G <= 8) return force == 2 ? 2 : 1;
   return 0;
 }
 
@@ -724,19 +741,13 @@ static bool flash_enabled() {
 // MAXT: 512 threads (G <= 8 query heads per KV head) leaves 256 VGPRs per wave for the
 // prefetched K + in-flight V + O accumulators; 1024 only for G > 8.
 template <int MAXT>
-__global__ __launch_bounds__(MAXT) void attn_kernel(AttnArgs a, int dec_seqs, int dec_blocks, int flash_qpb) {
+__global__ __launch_bounds__(MAXT) void attn_kernel(AttnArgs a, int dec_seqs, int dec_blocks) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   TLScope tl_scope(a.tl);
   const int bx = blockIdx.x;
   if (bx < dec_blocks) {
     decode_block(a, bx % dec_seqs, blockIdx.y, bx / dec_seqs, smem);  // block = (sequence, partition)
   } else {
-    if constexpr (MAXT <= 512) {
-      if (flash_qpb > 0) {
-        flash_body(a, bx - dec_blocks, blockIdx.y, flash_qpb, smem);
-        return;
-      }
-    }
     prefill_body(a, bx - dec_blocks, blockIdx.y, smem);
   }
 }
@@ -750,28 +761,30 @@ int g_flash_prefill = -1;  // -1: VGATE_FLASH_PREFILL (default on); 0 / 1: set_f
 void set_flash_prefill(int on) { g_flash_prefill = on; }
 
 void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
-  const int tiles = a.num_tiles > 0 ? a.num_tiles : 0;
-  int nw = attn_waves(a);
-  // prefill tiles take the flash body (QPB-query blocks, K / V through LDS by DMA) inside the same
-  // launch: its waves (QPB / 32 x G) and 64 KiB of LDS (+ the staged block table) size the blocks
-  const int fq = tiles > 0 && flash_enabled() ? flash_qpb(a) : 0;
-  size_t lds = attn_lds_bytes(nw);
-  if (fq > 0) {
-    const int fw = (fq / 32) * (a.Hq / a.Hkv);
-    nw = nw > fw ? nw : fw;
-    lds = attn_lds_bytes(nw);
-    const size_t fl = (size_t)FL_LDS + (size_t)a.max_blocks * 4;
-    lds = lds > fl ? lds : fl;
+  int tiles = a.num_tiles > 0 ? a.num_tiles : 0;
+  // prefill tiles on the flash kernel (its own launch; a decode-only graph bucket carries no tile
+  // list, StepMeta.view), the unified kernel keeps the decode rows
+  const int ct = tiles > 0 && flash_enabled() ? flash_ct(a) : 0;
+  if (ct > 0) {
+    AttnArgs f = a;
+    f.tl = tl_take("attn_flash", tiles * a.Hkv);
+    const size_t lds = (size_t)FL_LDS + (size_t)a.max_blocks * 4;
+    const dim3 grid(tiles, a.Hkv, 1), block(64 * (a.Hq / a.Hkv));
+    if (ct == 2) hipLaunchKernelGGL(attn_flash_kernel<2>, grid, block, lds, st, f);
+    else hipLaunchKernelGGL(attn_flash_kernel<1>, grid, block, lds, st, f);
+    tiles = 0;
   }
+  const int nw = attn_waves(a);
   const int dec_blocks = dec_seqs > 0 ? dec_seqs * a.num_parts : 0;
   const int nx = dec_blocks + tiles;
   if (nx <= 0) return;
   AttnArgs b = a;
+  b.num_tiles = tiles;
   b.tl = tl_take("attention", nx * a.Hkv);
   if (nw <= 8)
-    hipLaunchKernelGGL(attn_kernel<512>, dim3(nx, a.Hkv, 1), dim3(64 * nw), lds, st, b, dec_seqs, dec_blocks, fq);
+    hipLaunchKernelGGL(attn_kernel<512>, dim3(nx, a.Hkv, 1), dim3(64 * nw), attn_lds_bytes(nw), st, b, dec_seqs, dec_blocks);
   else
-    hipLaunchKernelGGL(attn_kernel<1024>, dim3(nx, a.Hkv, 1), dim3(64 * nw), lds, st, b, dec_seqs, dec_blocks, 0);
+    hipLaunchKernelGGL(attn_kernel<1024>, dim3(nx, a.Hkv, 1), dim3(64 * nw), attn_lds_bytes(nw), st, b, dec_seqs, dec_blocks);
   if (dec_seqs > 0 && a.num_parts > 1 && a.tickets == nullptr) {
     b.tl = tl_take("attn_reduce", dec_seqs * a.Hq);
     hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(dec_seqs, a.Hq), dim3(128), 0, st, b);

@@ -164,3 +164,30 @@ def test_embeddings_match_dense_reference():
     assert v2 == vec
     v3, _ = eng.embed("a different sentence")
     assert torch.nn.functional.cosine_similarity(v, torch.tensor(v3), dim=0).item() < 0.999
+
+
+def test_tile_order_and_decode_only_buckets():
+    """Prefill tiles: group leaders of the flash kernel first, longest first, every tile once; a
+    (T, S) bucket with T <= S carries no tiles (decode-only graphs launch no prefill attention)
+    and a step with a prompt chunk is sent to a token bucket above its sequence bucket."""
+    import numpy as np
+
+    from vgate import ops
+    from vgate.runtime.step_meta import StepMeta
+
+    for lead in (16, 32):
+        o = ops.tile_order(200, lead)
+        assert sorted(o.tolist()) == list(range(0, 200, 16))
+        nl = int((o % lead == 0).sum())
+        assert all(int(t) % lead == 0 for t in o[:nl]) and all(int(t) % lead for t in o[nl:])
+        assert list(o[:nl]) == sorted(o[:nl], reverse=True)
+    assert ops.flash_lead(32, 8) == 32 and ops.flash_lead(12, 2) == 16 and ops.flash_lead(8, 1) == 16
+    assert StepMeta.tile_cap(8, 8) == 0 and StepMeta.tile_cap(4, 8) == 0 and StepMeta.tile_cap(32, 8) == 10
+    eng = LLMEngine(EngineConfig(model="tiny-debug", device="cpu", max_num_seqs=8, max_num_batched_tokens=64,
+                                 num_kv_blocks=64, max_model_len=128))
+    r = eng.runner
+    assert r.t_buckets[-1] > r.s_buckets[-1]
+    for nt, ns in ((6, 4), (9, 8), (8, 8), (64, 8), (5, 1), (3, 3)):
+        T, S = r.bucket_for(nt, ns)
+        assert T >= nt and S >= ns
+        assert (T > S) if nt > ns else True, (nt, ns, T, S)

@@ -1250,7 +1250,7 @@ def test_flash_prefill_matches_tile_kernel_and_reference(Hq, Hkv):
     cl = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
     stride = (Hq + 2 * Hkv) * D
     qkv = torch.randn(T, stride, device=DEV).bfloat16()
-    ts, tq = ops.prefill_tiles(qlens)
+    ts, tq = ops.prefill_tiles(qlens, ops.flash_lead(Hq, Hkv))  # the engine's tile order
     ts, tq = ts + [-1] * 5, tq + [0] * 5  # a bucket's padding tiles
     ts = torch.tensor(ts, dtype=torch.int32, device=DEV)
     tq = torch.tensor(tq, dtype=torch.int32, device=DEV)

@@ -249,3 +249,26 @@ def test_tp_group_survives_idle_longer_than_timeout(tmp_path):
     assert out["finished"], out
     assert all(kind == "finish" and len(ids) == 4 for kind, ids in out["done"].values()), out
     assert procs[1].exitcode == 0
+
+
+def test_simulated_rank_runs_the_rank_shapes_without_a_group():
+    """TPGroup(simulated=True): one process builds rank r's shard of a TP=4 model (no process
+    group, collectives no-ops, the all-gather replicates the shard) and steps it — the per-rank
+    shape bench (benchmarks/tp_rank_bench.py) on one GPU."""
+    from vgate.parallel.comm import TPGroup
+    from vgate.runtime.engine import EngineConfig, LLMEngine
+    from vgate.runtime.sampling_params import SamplingParams
+
+    tp = TPGroup(rank=1, size=4, simulated=True)
+    eng = LLMEngine(EngineConfig(model="tiny", device="cpu", max_model_len=128, max_num_seqs=4,
+                                 max_num_batched_tokens=64, num_kv_blocks=32, warmup=False,
+                                 tensor_parallel_size=4), tp=tp)
+    assert eng.model.num_heads_local * 4 == eng.arch.num_heads and eng.ring is None
+    x = torch.arange(6, dtype=torch.float32).reshape(2, 3)
+    assert torch.equal(tp.all_gather_lastdim(x), torch.cat([x] * 4, -1))
+    assert tp.all_reduce(x) is x
+    done = {}
+    eng.add_request("a", prompt_ids=[3, 4, 5, 6], callback=lambda k, s, p: done.update({s.request_id: s}),
+                    params=SamplingParams(temperature=0.0, max_tokens=3, ignore_eos=True))
+    eng.run_until_idle()
+    assert len(done["a"].output_ids) == 3

@@ -33,15 +33,15 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _cfg(path, tp, eager=False):
+def _cfg(path, tp, eager=False, tokens=320):
     from vgate.runtime.engine import EngineConfig
 
-    return EngineConfig(model=path, device="cuda:0", tensor_parallel_size=tp, max_model_len=512, max_num_seqs=8,
-                        max_num_batched_tokens=320, num_kv_blocks=256, warmup=False, seed=0,
+    return EngineConfig(model=path, device="cuda:0", tensor_parallel_size=tp, max_model_len=1024, max_num_seqs=8,
+                        max_num_batched_tokens=tokens, num_kv_blocks=256, warmup=False, seed=0,
                         enforce_eager=eager)
 
 
-def _generate(eng):
+def _generate(eng, prompts=None):
     from vgate.runtime.sampling_params import SamplingParams
 
     done = {}
@@ -51,28 +51,34 @@ def _generate(eng):
             done[seq.request_id] = list(seq.output_ids)
 
     sp = SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True)
-    for rid, ids in PROMPTS.items():
+    for rid, ids in (prompts or PROMPTS).items():
         eng.add_request(rid, params=sp, callback=cb, prompt_ids=ids)
     eng.run_until_idle()
     return done
 
 
-def _worker(rank, world, port, path, q, eager=False):
+# >= 512 tokens in ONE prefill step: the row-parallel all-reduces of the chunked prefill move
+# 512-token slices through the two-shot kernel (VGATE_AR_TWO_SHOT=1 forces it; at TP = 2 the size
+# rule never picks it)
+LONG = {"long600": [7 + (j * 13) % 450 for j in range(600)], "short": [9, 8, 7, 6, 5]}
+
+
+def _worker(rank, world, port, path, q, eager=False, env=None, tokens=320, prompts=None):
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-                          MASTER_PORT=str(port), VGATE_TP_TIMEOUT_S="60")
+                          MASTER_PORT=str(port), VGATE_TP_TIMEOUT_S="60", **(env or {}))
         import torch.distributed as dist
 
         from vgate.runtime.engine import LLMEngine
 
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        eng = LLMEngine(_cfg(path, world, eager))
+        eng = LLMEngine(_cfg(path, world, eager, tokens))
         assert eng.tp.size == world and eng.tp.rank == rank and eng.tp.backend == "gloo"
         eng.runner.defer_capture = False
         assert eng.model.num_heads_local * world == eng.arch.num_heads
         if rank == 0:
-            out = _generate(eng)
+            out = _generate(eng, prompts)
             used_ar = eng.tp.custom_ar is not None and eng.tp.custom_ar.calls > 0
             graphs = len(eng.runner.graphs)
             eng.shutdown_followers()
@@ -121,3 +127,133 @@ def test_tp2_on_gpu_matches_tp1(tmp_path, eager):
     assert used_ar, "the custom all-reduce was not used between the two ranks"
     assert tp_out == ref
     assert (graphs > 0) == (not eager), graphs
+
+
+def _ckpt(tmp_path):
+    from vgate.models.weights import save_checkpoint
+    from vgate.runtime.engine import EngineConfig, LLMEngine
+
+    src = LLMEngine(EngineConfig(model="tiny", device="cpu", max_model_len=256, max_num_seqs=8,
+                                 max_num_batched_tokens=64, num_kv_blocks=128, warmup=False, seed=0))
+    path = str(tmp_path / "ckpt")
+    save_checkpoint(src.model, path)
+    return path
+
+
+def _spawn(n, target, args_of):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=args_of(r, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    return ctx, q, procs
+
+
+@pytest.mark.timeout(300)
+def test_tp2_two_shot_long_prefill_matches_tp1(tmp_path):
+    """A 600-token prompt in one 640-token prefill step at TP = 2 with every all-reduce forced onto
+    the two-shot kernel (reduce-scatter + all-gather over the peer buffers) == TP = 1."""
+    path = _ckpt(tmp_path)
+    ref_eng = __import__("vgate.runtime.engine", fromlist=["LLMEngine"]).LLMEngine(_cfg(path, 1, True, 640))
+    ref = _generate(ref_eng, LONG)
+    del ref_eng
+    torch.cuda.synchronize()
+    port = _free_port()
+    _, q, procs = _spawn(2, _worker, lambda r, q: (r, 2, port, path, q, False, {"VGATE_AR_TWO_SHOT": "1"}, 640, LONG))
+    try:
+        results = [q.get(timeout=240) for _ in procs]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    errs = [r[1] for r in results if r[0] == "err"]
+    assert not errs, errs[0]
+    tp_out, used_ar, _ = next(r[1] for r in results if r[1] is not None)
+    assert used_ar
+    assert tp_out == ref
+
+
+def _timeout_worker(rank, port, path, q, go):
+    try:
+        os.environ.update(RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(port), VGATE_TP_TIMEOUT_S="60", VGATE_AR_SPIN_LIMIT="20000")
+        import torch.distributed as dist
+
+        from vgate.runtime.engine import LLMEngine
+        from vgate.runtime.sampling_params import SamplingParams
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=2)
+        eng = LLMEngine(_cfg(path, 2))
+        if rank != 0:
+            q.put(("pid", os.getpid()))
+            eng.follower_loop()
+            return
+        eng.runner.defer_capture = False
+        first = _generate(eng, {"a": [5, 6, 7, 8]})
+        assert len(first["a"]) == 8 and eng.healthy
+        eng.start()
+        q.put(("ready", None))
+        go.wait(120)  # the test stopped rank 1
+        done = {}
+        import threading
+        ev = threading.Event()
+
+        def cb(kind, seq, payload):
+            if kind in ("finish", "error"):
+                done[seq.request_id] = (kind, payload)
+                ev.set()
+
+        eng.add_request("b", prompt_ids=[9, 10, 11], callback=cb,
+                        params=SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True))
+        ev.wait(120)
+        q.put(("ok", (done.get("b"), eng.healthy, eng.last_error)))
+        eng._running = False
+        os._exit(0)  # rank 1 is stopped: no orderly shutdown of the group
+    except Exception:  # noqa: BLE001
+        q.put(("err", traceback.format_exc()))
+
+
+@pytest.mark.timeout(300)
+def test_tp2_peer_stops_custom_allreduce_times_out_and_engine_fails(tmp_path):
+    """Timeout path of the custom all-reduce: rank 1 is frozen (SIGSTOP) after a good generation;
+    rank 0's next step waits for it at the first collective, gives up after the spin limit (set
+    short here), every later collective of the step skips the wait (sticky error word), the
+    step's last graph node hands the word to the host, and the engine fails the step: the request
+    ends with an error and the engine reports unhealthy (its /health then answers 503)."""
+    import signal
+
+    path = _ckpt(tmp_path)
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    go = ctx.Event()
+    procs = [ctx.Process(target=_timeout_worker, args=(r, port, path, q, go)) for r in range(2)]
+    for p in procs:
+        p.start()
+    pid1 = None
+    try:
+        got = {}
+        for _ in range(2):
+            kind, val = q.get(timeout=240)
+            assert kind != "err", val
+            got[kind] = val
+        pid1 = got["pid"]
+        os.kill(pid1, signal.SIGSTOP)
+        go.set()
+        kind, val = q.get(timeout=240)
+        assert kind == "ok", val
+        res, healthy, err = val
+        assert res is not None and res[0] == "error", res
+        assert not healthy and "custom all-reduce" in (err or ""), err
+    finally:
+        if pid1 is not None:
+            try:
+                os.kill(pid1, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()

@@ -572,27 +572,33 @@ def attention_decode(q, q_stride, k_cache, v_cache, block_tables, context_lens, 
     return out
 
 
-def prefill_tiles(query_lens: list[int]) -> tuple[list[int], list[int]]:
+def prefill_tiles(query_lens: list[int], lead: int = 32) -> tuple[list[int], list[int]]:
     """16-query prefill tiles (sequence, first query) in the attention kernel's order: see
     :func:`tile_order`."""
     seq, q0 = [], []
     for s, ql in enumerate(query_lens):
-        for t in tile_order(ql):
+        for t in tile_order(ql, lead):
             seq.append(s)
             q0.append(int(t))
     return seq, q0
 
 
-def tile_order(qlen: int):
-    """First queries of a sequence's 16-query tiles, ordered for the flash prefill kernel: tiles
-    starting a 64-query group first, then those starting a 32-query group, then the rest, each class
-    longest causal range first. The flash kernel runs one block per tile and only group leaders
-    work (64 queries for <= 4 heads per KV head, 32 for <= 8), so the working blocks are the first
-    ones of the grid, spread round-robin over the 8 XCDs instead of every 4th block landing on the
-    same two; the 16-query kernel is order-free."""
+def flash_lead(hq: int, hkv: int) -> int:
+    """Queries per flash-prefill block for a head layout (attention.hip flash_ct: two 16-query
+    column tiles per wave up to 4 query heads per KV head, one above)."""
+    return 32 if hq // max(hkv, 1) <= 4 else 16
+
+
+def tile_order(qlen: int, lead: int = 32):
+    """First queries of a sequence's 16-query tiles, ordered for the flash prefill kernel: the
+    tiles that start a ``lead``-query group (the flash blocks that work; the others exit at once)
+    first, longest causal range first, then the rest. The working blocks are then the first ones
+    of the grid, spread round-robin over the 8 XCDs, and the longest start first. Correctness
+    does not depend on the order (the 16-query kernel is order-free, flash blocks find their
+    group from the tile), only the load balance does."""
     import numpy as _np
     t = _np.arange(0, qlen, 16, dtype=_np.int32)[::-1]
-    return _np.concatenate([t[t % 64 == 0], t[t % 64 == 32], t[t % 32 != 0]])
+    return _np.concatenate([t[t % lead == 0], t[t % lead != 0]])
 
 
 def attention_prefill(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start,

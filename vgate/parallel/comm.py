@@ -28,6 +28,10 @@ class TPGroup:
     group: object = None
     backend: str = "none"
     custom_ar: object = None
+    # one process measuring rank `rank` of a `size`-way group on one GPU (benchmarks/tp_rank_bench.py):
+    # the model is sharded exactly as that rank's, every collective is a no-op (the all-gather
+    # replicates the local shard), no process group exists
+    simulated: bool = False
 
     @property
     def is_first(self) -> bool:
@@ -35,7 +39,7 @@ class TPGroup:
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         """In-place sum over the TP group."""
-        if self.size == 1:
+        if self.size == 1 or self.simulated:
             return t
         if self.custom_ar is not None and self.custom_ar.should_use(t):
             return self.custom_ar.all_reduce(t)
@@ -51,6 +55,8 @@ class TPGroup:
         """[..., n] per rank -> [..., n * size] concatenated in rank order."""
         if self.size == 1:
             return t
+        if self.simulated:
+            return t.repeat(*([1] * (t.dim() - 1)), self.size)
         t = t.contiguous()
         if self.custom_ar is not None and self.custom_ar.should_gather(t):
             out = self.custom_ar.all_gather(t)
@@ -68,14 +74,14 @@ class TPGroup:
         return self.custom_ar.max_bytes if self.custom_ar is not None else 0
 
     def broadcast_object(self, obj, src: int = 0):
-        if self.size == 1:
+        if self.size == 1 or self.simulated:
             return obj
         lst = [obj]
         dist.broadcast_object_list(lst, src=src, group=self.group)
         return lst[0]
 
     def barrier(self):
-        if self.size > 1:
+        if self.size > 1 and not self.simulated:
             dist.barrier(group=self.group)
 
 

@@ -72,6 +72,10 @@ class CustomAllReduce:
             self.close()
             raise RuntimeError(f"custom all-reduce setup failed: {[e for e in errs if e]}")
         self.calls = 0
+        # VGATE_AR_TWO_SHOT: 1 forces the two-shot kernel for every all-reduce, -1 the one-shot one,
+        # 0 (default) picks by size (tests force two-shot at TP = 2, where it is never picked)
+        import os
+        self.force = int(os.environ.get("VGATE_AR_TWO_SHOT", "0"))
 
     def should_use(self, t: torch.Tensor) -> bool:
         nbytes = t.numel() * t.element_size()
@@ -82,7 +86,7 @@ class CustomAllReduce:
         """Sum over the group; one-shot up to 512 KiB, two-shot (reduce-scatter + all-gather over
         the direct links) above; two_shot = 1 / -1 forces one form (tests)."""
         out = t if out is None else out
-        self.C.custom_allreduce(t, out, self.bases, self.rank, self.max_bytes, two_shot)
+        self.C.custom_allreduce(t, out, self.bases, self.rank, self.max_bytes, two_shot or self.force)
         self.calls += 1
         return out
 

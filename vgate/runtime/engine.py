@@ -127,7 +127,7 @@ class LLMEngine:
         # a gloo group (ranks sharing one GPU in tests) runs its collectives on the host, which a
         # hipGraph cannot capture: such a group replays graphs only for the buckets whose every
         # collective fits the IPC kernels (custom all-reduce / all-gather), and runs the rest eagerly
-        gloo_tp = self.tp.size > 1 and self.tp.backend != "nccl"
+        gloo_tp = self.tp.size > 1 and self.tp.backend != "nccl" and not self.tp.simulated
         eager = cfg.enforce_eager or (gloo_tp and self.tp.custom_ar is None)
         self.runner = ModelRunner(self.model, self.kv_caches, cfg.max_num_seqs, cfg.max_num_batched_tokens,
                                   cfg.max_model_len, cfg.block_size, eager, part,
@@ -171,7 +171,7 @@ class LLMEngine:
         self._ar_check_every = 1 if self.tp.is_first else 64
         self._steps_since_check = 0
         self._ar_ms: list[float] = []
-        if self.tp.size > 1:
+        if self.tp.size > 1 and not self.tp.simulated:
             self._init_ring()
         self._inflight = None  # (batch, handle) of the launched, not yet post-processed step
         self._calls: collections.deque = collections.deque()  # (fn, future) run on the engine thread
@@ -196,7 +196,7 @@ class LLMEngine:
             n = min(n, max_useful)
         else:
             n = min(max_useful, 4096)
-        if self.tp.size > 1:  # identical pool on every rank
+        if self.tp.size > 1 and not self.tp.simulated:  # identical pool on every rank
             t = torch.tensor([n], device=self.device if self.tp.backend == "nccl" else "cpu")
             import torch.distributed as dist
             dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.tp.group)

@@ -80,10 +80,16 @@ class ModelRunner:
         self.t_buckets = sorted(set(tb + [max_num_batched_tokens]))
         sb = [b for b in DEFAULT_S_BUCKETS if b < max_num_seqs]
         self.s_buckets = sorted(set(sb + [max_num_seqs]))
+        if self.t_buckets[-1] <= self.s_buckets[-1]:
+            # a step with a prompt chunk needs a token bucket above its sequence bucket
+            # (StepMeta.tile_cap): keep one above the largest
+            self.t_buckets.append(self.s_buckets[-1] + 16)
         self.max_tokens = self.t_buckets[-1]
         self.max_seqs = max_num_seqs
         self.meta = StepMeta(self.max_tokens, self.max_seqs, self.max_blocks, self.device)
         self.use_graphs = self.gpu and not enforce_eager
+        sh = getattr(model, "shard", None)
+        self.tile_lead = ops.flash_lead(sh.hq, sh.hkv) if sh is not None else 32
         self.graph_ok = lambda T, S: True  # per-bucket veto (TP groups without capturable collectives)
         self.graphs: dict[tuple[int, int], tuple] = {}
         self.pool = None
@@ -145,6 +151,16 @@ class ModelRunner:
             raise ValueError(f"{n} exceeds the largest bucket {buckets[-1]}")
         return buckets[i]
 
+    def bucket_for(self, nt: int, ns: int) -> tuple[int, int]:
+        """Graph bucket (T, S) of a step with nt tokens over ns sequences. A step with a prompt
+        chunk (nt > ns) gets a token bucket above its sequence bucket: buckets with T <= S carry
+        no prefill tiles (StepMeta.tile_cap), so decode-only graphs launch no prefill attention."""
+        T = self._bucket(self.t_buckets, nt)
+        S = self._bucket(self.s_buckets, ns)
+        if nt > ns and T <= S:
+            T = self._bucket(self.t_buckets, S + 1)
+        return T, S
+
     # ---------------------------------------------------------------- metadata
     def _fill(self, batch: ScheduledBatch, T: int, S: int, pending_slots: dict | None = None) -> list[bool]:
         m = self.meta
@@ -186,7 +202,7 @@ class ModelRunner:
             qs[s + 1] = t
             sidx[s] = t - 1
             if n > 1:
-                order = ops.tile_order(n)
+                order = ops.tile_order(n, self.tile_lead)
                 k = len(order)
                 if ntile + k <= len(tseq):
                     tseq[ntile: ntile + k] = s
@@ -210,7 +226,7 @@ class ModelRunner:
         temp[ns:S] = 0.0
         topp[ns:S] = 1.0
         topk[ns:S] = -1
-        tile_cap = T // 16 + S
+        tile_cap = self.meta.tile_cap(T, S)
         if ntile > tile_cap:
             raise RuntimeError("prefill tile overflow")
         tseq[ntile:tile_cap] = -1
@@ -269,8 +285,7 @@ class ModelRunner:
             return StepHandle(0, len(batch.items), samples, toks, time.perf_counter())
         ns = len(batch.items)
         nt = batch.num_tokens
-        T = self._bucket(self.t_buckets, nt)
-        S = self._bucket(self.s_buckets, ns)
+        T, S = self.bucket_for(nt, ns)
         t_host = time.perf_counter()
         k = self._k
         self._k ^= 1
@@ -499,4 +514,4 @@ class ModelRunner:
         h["temperature"][:S] = 0
         h["top_p"][:S] = 1
         h["top_k"][:S] = -1
-        h["tile_seq"][: T // 16 + S] = -1
+        h["tile_seq"][: self.meta.tile_cap(T, S)] = -1

@@ -107,12 +107,20 @@ class StepMeta:
         # multiple of 16, so the 16-B rounded prefix stays inside both buffers
         ops.host_device_copy(self.dev, self.host, self.used_bytes(num_seqs))
 
+    @staticmethod
+    def tile_cap(T: int, S: int) -> int:
+        """Prefill tiles a (T, S) bucket carries: none when T <= S — a bucket with no more token
+        slots than sequence slots serves decode-only steps (the runner sends a step with a prompt
+        chunk to a token bucket above S), so its graphs launch no prefill attention at all."""
+        return T // 16 + S if T > S else 0
+
     def view(self, T: int, S: int) -> StepView:
         d = self.d
+        nt = self.tile_cap(T, S)
         return StepView(
             T=T, S=S, ids=d["ids"][:T], positions=d["positions"][:T], slots=d["slots"][:T],
             query_start=d["query_start"][: S + 1], context_lens=d["context_lens"][:S],
-            tile_seq=d["tile_seq"][: T // 16 + S], tile_q0=d["tile_q0"][: T // 16 + S],
+            tile_seq=d["tile_seq"][:nt], tile_q0=d["tile_q0"][:nt],
             sample_idx=d["sample_idx"][:S], block_tables=d["block_tables"].view(self.S, self.max_blocks)[:S],
             temperature=d["temperature"][:S], top_p=d["top_p"][:S], top_k=d["top_k"][:S],
             seeds=d["seeds"][:S], offsets=d["offsets"][:S], ring_slot=d["ring_slot"][:1],
