@@ -31,6 +31,14 @@ from vgate.runtime.engine import EngineConfig, LLMEngine  # noqa: E402
 from vgate.runtime.sampling_params import SamplingParams  # noqa: E402
 
 KINDS = ("qkv", "o", "gate_up", "down")
+# (waves, split-K, tiles per block) candidates for the large-K per-rank shapes (0 = heuristic)
+RANK_CANDIDATES = {
+    "qkv": [(0, 0, 0), (8, 1, 0), (8, 2, 0), (8, 3, 0), (8, 4, 0), (8, 6, 0), (8, 8, 0), (4, 4, 0), (4, 8, 0)],
+    "o": [(0, 0, 0), (4, 1, 1), (8, 1, 1), (2, 1, 1), (4, 2, 1), (2, 2, 1), (8, 1, 2), (4, 1, 2)],
+    "gate_up": [(0, 0, 0), (8, 1, 0), (4, 1, 0), (2, 1, 0), (8, 2, 0), (4, 2, 0)],
+    "down": [(0, 0, 0), (8, 1, 1), (4, 1, 1), (8, 2, 1), (4, 2, 1), (8, 4, 1), (8, 1, 2)],
+    "lm_head": [(0, 0, 0), (8, 1, 2), (4, 1, 2), (8, 1, 1), (4, 1, 4)],
+}
 
 
 def layer_kinds(live):
@@ -68,7 +76,10 @@ def main():
     ap.add_argument("--sweep", action="store_true", help="in-context decode decomposition table per projection")
     ap.add_argument("--kinds", default="qkv,o,gate_up,down,lm_head")
     a = ap.parse_args()
-    from decode_sweep import CANDIDATES, set_plan, time_step
+    if a.sweep:  # the sweep's (0, 0, 0) row is the launcher heuristic, not the measured table
+        import os
+        os.environ["VGATE_DECODE_PLANS"] = "0"
+    from decode_sweep import set_plan, time_step
     from timeline import measure
 
     tp = TPGroup(rank=a.rank, size=a.tp, simulated=True)
@@ -117,7 +128,7 @@ def main():
     best = {}
     for kind in a.kinds.split(","):
         res = []
-        for cfg in CANDIDATES[kind]:
+        for cfg in RANK_CANDIDATES[kind]:
             set_plan(eng.model, kind, cfg)
             try:
                 us = time_step(eng, a.iters)

@@ -272,3 +272,23 @@ def test_simulated_rank_runs_the_rank_shapes_without_a_group():
                     params=SamplingParams(temperature=0.0, max_tokens=3, ignore_eos=True))
     eng.run_until_idle()
     assert len(done["a"].output_ids) == 3
+
+
+def test_decode_plan_table_applies_to_matching_shapes():
+    """vgate/models/decode_plans.py: measured per-shape decode decompositions land on the Linear
+    objects whose (N, K, layout, kind) match (the 70B TP=8 rank shapes), nothing else changes."""
+    from types import SimpleNamespace
+
+    from vgate.models import decode_plans
+
+    def lin(N, K, layout="plain", kind="dense"):
+        return SimpleNamespace(N=N, K=K, layout=layout, kind=kind, dec_waves=0, dec_splitk=0, dec_ntb=0)
+
+    L = SimpleNamespace(qkv=lin(1280, 8192, "qkv"), o=lin(8192, 1024), gate_up=lin(7168, 8192, "silu"),
+                        down=lin(8192, 3584))
+    other = SimpleNamespace(qkv=lin(2048, 1536, "qkv"), o=lin(1536, 1536), gate_up=lin(17920, 1536, "silu"),
+                            down=lin(1536, 8960))
+    m = SimpleNamespace(layers=[L, other], lm_head=lin(16032, 8192))
+    assert decode_plans.apply(m) == 5
+    assert (L.gate_up.dec_waves, L.gate_up.dec_splitk) == (4, 1) and L.qkv.dec_splitk == 3
+    assert all(getattr(other, k).dec_waves == 0 for k in ("qkv", "o", "gate_up", "down"))

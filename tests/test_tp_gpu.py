@@ -175,6 +175,11 @@ def test_tp2_two_shot_long_prefill_matches_tp1(tmp_path):
 
 
 def _timeout_worker(rank, port, path, q, go):
+    import sys
+
+    def say(*a):
+        print(f"[rank {rank}]", *a, file=sys.stderr, flush=True)
+
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                           MASTER_PORT=str(port), VGATE_TP_TIMEOUT_S="60", VGATE_AR_SPIN_LIMIT="20000")
@@ -186,6 +191,7 @@ def _timeout_worker(rank, port, path, q, go):
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=2)
         eng = LLMEngine(_cfg(path, 2))
+        say("engine up")
         if rank != 0:
             q.put(("pid", os.getpid()))
             eng.follower_loop()
@@ -193,9 +199,11 @@ def _timeout_worker(rank, port, path, q, go):
         eng.runner.defer_capture = False
         first = _generate(eng, {"a": [5, 6, 7, 8]})
         assert len(first["a"]) == 8 and eng.healthy
+        say("first generation ok")
         eng.start()
         q.put(("ready", None))
         go.wait(120)  # the test stopped rank 1
+        say("peer stopped; submitting")
         done = {}
         import threading
         ev = threading.Event()
@@ -207,9 +215,11 @@ def _timeout_worker(rank, port, path, q, go):
 
         eng.add_request("b", prompt_ids=[9, 10, 11], callback=cb,
                         params=SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True))
-        ev.wait(120)
+        ev.wait(60)
+        say("request done:", done.get("b"), eng.healthy, eng.last_error)
         q.put(("ok", (done.get("b"), eng.healthy, eng.last_error)))
-        eng._running = False
+        q.close()
+        q.join_thread()  # the queue's feeder thread must flush before the hard exit below
         os._exit(0)  # rank 1 is stopped: no orderly shutdown of the group
     except Exception:  # noqa: BLE001
         q.put(("err", traceback.format_exc()))
@@ -236,13 +246,13 @@ def test_tp2_peer_stops_custom_allreduce_times_out_and_engine_fails(tmp_path):
     try:
         got = {}
         for _ in range(2):
-            kind, val = q.get(timeout=240)
+            kind, val = q.get(timeout=150)
             assert kind != "err", val
             got[kind] = val
         pid1 = got["pid"]
         os.kill(pid1, signal.SIGSTOP)
         go.set()
-        kind, val = q.get(timeout=240)
+        kind, val = q.get(timeout=100)
         assert kind == "ok", val
         res, healthy, err = val
         assert res is not None and res[0] == "error", res

@@ -1,0 +1,34 @@
+"""Measured decode-GEMM decompositions (M <= 16) per weight shape, applied to every matching
+Linear at model construction (``Linear.dec_waves / dec_splitk / dec_ntb``; 0 = the launcher's
+heuristic, csrc/kernels/gemm_decode.h ``plan``).
+
+Entries come from in-context sweeps: every candidate (waves per block, K slices, column tiles
+per block) re-captures the decode hipGraph and times the WHOLE step, all other projections at
+their current plan (benchmarks/decode_sweep.py for TP = 1 models, benchmarks/tp_rank_bench.py
+--sweep for one TP rank's shapes). A shape missing here measured best on the heuristic.
+
+Key: (N, K, layout, weight kind) of the packed weight; layout "qkv" / "silu" / "plain".
+"""
+from __future__ import annotations
+
+PLANS: dict[tuple[int, int, str, str], tuple[int, int, int]] = {
+    # Llama-3-70B TP = 8, one rank, batch 8, ctx 128 (profiles/r3_tp8_rank_sweep.log):
+    # per-rank step 5027 -> 4859 us with all five applied
+    (1280, 8192, "qkv", "dense"): (8, 3, 0),     # 80 tiles x 256 k-steps: 240 blocks (heuristic 8 x 2: +33 us)
+    (8192, 1024, "plain", "dense"): (2, 1, 1),   # o_proj
+    (7168, 8192, "silu", "dense"): (4, 1, 0),    # gate_up: 448 one-tile blocks at 4 waves (heuristic 8: +118 us)
+    (8192, 3584, "plain", "dense"): (8, 1, 2),   # down_proj
+    (16032, 8192, "plain", "dense"): (8, 1, 1),  # LM head shard
+}
+
+
+def apply(model) -> int:
+    """Set the measured plan on every Linear of ``model`` whose shape has one; returns how many."""
+    n = 0
+    lins = [lin for L in model.layers for lin in (L.qkv, L.o, L.gate_up, L.down)] + [model.lm_head]
+    for lin in lins:
+        p = PLANS.get((lin.N, lin.K, lin.layout, lin.kind))
+        if p is not None:
+            lin.dec_waves, lin.dec_splitk, lin.dec_ntb = p
+            n += 1
+    return n

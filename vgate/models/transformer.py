@@ -98,6 +98,9 @@ class DecoderModel:
             ops.reserve_awq_scratch(self.device, max(lin.N * lin.K for lin in lins if lin.kind == "awq"))
         if self.device.type == "cuda" and os.environ.get("VGATE_FOLD_NORM", "1") != "0":
             self.fold_norms()
+        if os.environ.get("VGATE_DECODE_PLANS", "1") != "0":  # measured decode decompositions per shape
+            from vgate.models import decode_plans
+            decode_plans.apply(self)
         table_len = max(max_model_len, 16) + 1
         self.cos_sin = ops.ref.rope_cos_sin(table_len, arch.head_dim, arch.rope_theta, arch.rope_scaling,
                                             device=self.device)

@@ -175,7 +175,7 @@ class Linear:
         self.norm_gamma = None  # RMSNorm weight folded into the packed copy (see fold_norm)
         self.wl = None  # optional plain [N, K] copy for library (hipBLASLt) prefill GEMMs
         # decode-GEMM decomposition for M <= 16 steps (0 = the launcher's heuristic): set by the
-        # model from the measured per-shape table (benchmarks/decode_sweep.py)
+        # model from the measured per-shape table (vgate/models/decode_plans.py)
         self.dec_waves = 0
         self.dec_splitk = 0
         self.dec_ntb = 0
