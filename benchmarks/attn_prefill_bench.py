@@ -38,7 +38,7 @@ def main():
             cl = torch.tensor([S], dtype=torch.int32, device=dev)
             stride = (Hq + 2 * Hkv) * D
             qkv = torch.randn(S, stride, device=dev).bfloat16()
-            ts, tq = ops.prefill_tiles([S])
+            ts, tq = ops.prefill_tiles([S], ops.flash_lead(Hq, Hkv))  # the engine's tile order
             ts = torch.tensor(ts, dtype=torch.int32, device=dev)
             tq = torch.tensor(tq, dtype=torch.int32, device=dev)
             out = torch.empty(S, Hq * D, device=dev).bfloat16()

@@ -510,12 +510,16 @@ __device__ __forceinline__ void prefill_body(const AttnArgs& a, int tile, int h,
 }
 
 // ------------------------------------------------------- flash prefill ----
-// Causal (chunked-prefill capable) attention of a block of QPB = 16 CT query tokens x the G query
-// heads of one KV head: G waves, wave w owns head h G + w for all QPB queries (CT 16-query MFMA
-// column tiles); Q lives in registers. K / V stream through LDS in 64-token chunks, double-buffered
-// and SHARED by the block's waves (GQA: one K/V byte serves G heads x QPB queries), moved by LDS-DMA
-// (global_load_lds_dwordx4: no VGPRs, every wave issues a share of the 32 1-KiB pieces) — the DMA
-// of chunk c + 1 is issued before chunk c's MFMAs, one barrier per chunk.
+// Causal (chunked-prefill capable) attention of a block of QPB = 16 CT QG query tokens x the G
+// query heads of one KV head. NW = QG G waves: wave w owns head h G + w % G for the CT 16-query
+// MFMA column tiles of query group w / G; Q lives in registers. K / V stream through LDS in
+// 64-token chunks, SHARED by the block's waves (GQA: one K/V byte serves G heads x QPB queries),
+// moved by LDS-DMA (global_load_lds_dwordx4: no VGPRs; every wave issues P = ceil(32 / NW) of
+// the chunk's 32 1-KiB pieces, padded with repeats of its own last piece so every wave's vmcnt
+// bookkeeping is the same constant). NST-stage ring: chunk c + NST - 1 is issued at the top of
+// iteration c, so a chunk's DMA has NST - 1 chunks of compute to land — with two stages (one
+// chunk ahead) the kernel ran at the DMA's issue-to-land latency per chunk (~3.4 us, 109 us for
+// Llama-3-8B causal 2048, profiles/r3_flash_prefill.log). One barrier per chunk.
 //   S^T = K Q^T (swapped: softmax statistics lane-local, row reductions by two xor-swaps); K image
 //   16-B chunks XOR-swizzled by row & 15 (conflict-free ds_read_b128 of the A operand);
 //   O^T += V^T P^T with V^T read by ds_read_b64_tr_b16 from the 8-B-chunk-swizzled V image and P^T
@@ -524,23 +528,44 @@ __device__ __forceinline__ void prefill_body(const AttnArgs& a, int tile, int h,
 // below every query of the block), the scale folded into the exp2 argument (one fma), and the
 // O / l rescale only when some column's running max moved (wave-uniform test; exact: alpha = 1
 // otherwise).
-// Blocks are small (G waves, 64 KiB of LDS + the staged block table) so two fit a CU: the two
-// blocks' waves on one SIMD drift apart and overlap one's softmax with the other's MFMAs.
 // The host's 16-query tile list is reused: a block whose tile starts a QPB-aligned group leads it
 // (others exit at once). The host lists the group leaders first, longest causal range first
 // (ops.tile_order), so the working blocks are the grid's first ones, spread over all 8 XCDs and
-// the longest start first. Pages past the causal bound are not read.
+// the longest start first. Chunks past the causal bound are not read (the ring's look-ahead past
+// the last chunk re-reads the last one into a free stage).
 extern int g_flash_prefill;
 constexpr int FL_KV = 64;
-constexpr int FL_LDS = 4 * FL_KV * D_ * 2;  // K x2 + V x2 (64 KiB)
+constexpr int FL_STAGE = 2 * FL_KV * D_ * 2;  // K + V of one chunk (32 KiB)
+constexpr int FL_NST_MAX = 4;                 // ring stages (<= 128 KiB: one block per CU)
 
-template <int CT>
-__global__ __launch_bounds__(512, CT == 1 ? 3 : 2) void attn_flash_kernel(AttnArgs a) {
-  constexpr int QPB = 16 * CT;
+// f32 max of values known not to be NaN: one v_max / v_max3 each (fmaxf's IEEE-mode lowering
+// canonicalises every MFMA-produced input first: an extra v_max x, x per value)
+__device__ __forceinline__ float fmax3_(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float fmax_(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+__device__ __forceinline__ constexpr int vm_imm(int n) {  // s_waitcnt vmcnt(n), other counters untouched
+  return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8);
+}
+
+template <int CT, int NW, int FL_NST, bool SWP>
+__global__ __launch_bounds__(64 * NW) void attn_flash_kernel(AttnArgs a, int lazy) {
+  constexpr int P = (32 + NW - 1) / NW;  // DMA pieces per wave per chunk
+  constexpr int FL_LDS = FL_NST * FL_STAGE;
+  static_assert((FL_NST - 2) * P < 64, "vmcnt immediate");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   TLScope tl_scope(a.tl);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int G = a.Hq / a.Hkv;
+  const int QG = NW / G;
+  const int QPB = 16 * CT * QG;
   const int h = blockIdx.y;
   const int tile = blockIdx.x;
   const int s = a.tile_seq[tile];
@@ -550,9 +575,10 @@ __global__ __launch_bounds__(512, CT == 1 ? 3 : 2) void attn_flash_kernel(AttnAr
   const int qs = a.query_start[s];
   const int qlen = a.query_start[s + 1] - qs;
   const int ctx = a.context_lens[s];
-  const int hq = h * G + wid;
-  const int qhi = min(q0 + QPB, qlen);   // this block's queries: [q0, qhi)
-  const int kv_end = ctx - qlen + qhi;   // the block's causal bound (exclusive)
+  const int hq = h * G + wid % G;
+  const int qw0 = q0 + 16 * CT * (wid / G);  // this wave's first query
+  const int qhi = min(q0 + QPB, qlen);       // the block's queries: [q0, qhi)
+  const int kv_end = ctx - qlen + qhi;       // the block's causal bound (exclusive)
   const int nch = (kv_end + FL_KV - 1) / FL_KV;
   const int nfull = max(0, ctx - qlen + q0 + 1) / FL_KV;  // chunks below every query's bound
   const int col = lane & 15, g4 = lane >> 4;
@@ -561,7 +587,7 @@ __global__ __launch_bounds__(512, CT == 1 ? 3 : 2) void attn_flash_kernel(AttnAr
   int lim[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
-    const int qi = q0 + 16 * ct + col;
+    const int qi = qw0 + 16 * ct + col;
     const bool ok = qi < qhi;
     lim[ct] = ok ? ctx - qlen + qi + 1 : 0;
     const bf16_t* qp = a.q + (size_t)(qs + (ok ? qi : 0)) * a.q_stride + (size_t)hq * D_ + 8 * g4;
@@ -579,34 +605,46 @@ __global__ __launch_bounds__(512, CT == 1 ? 3 : 2) void attn_flash_kernel(AttnAr
     const int* bt = a.block_tables + (size_t)s * a.max_blocks;
     for (int i = threadIdx.x; i < npg; i += blockDim.x) s_bt[i] = bt[i];
   }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // Q fragments and the block table
   __builtin_amdgcn_s_barrier();
-  // chunk c's 32 DMA pieces (16 K, 16 V) over the block's waves
+  // chunk c's 32 DMA pieces (16 K, 16 V) over the block's waves, into stage c % NST; past the last
+  // chunk the last one is re-read (the ring keeps NST - 1 chunks in flight, a constant vmcnt).
+  // Piece i of a chunk: K rows 4 i .. 4 i + 3 (i < 16; lane -> physical 16-B chunk l & 15 holds
+  // logical chunk ^ (row & 15)) or V half (i - 16) / 8, rows 4 ((i - 16) % 8) .. + 3 of that half
+  // (v_lds_off's 8-B chunk swizzle). Everything but the 4 pages of the chunk is chunk-invariant:
+  // the lane's element offset inside its page and the piece's page slot / LDS offset are set once.
+  uint32_t loff[P];  // lane's element offset inside the page
+  int pslot[P], pisv[P], pdst[P];  // wave-uniform: page slot 0..3, V?, LDS byte offset in the stage
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    int i = wid + k * NW;
+    if (i >= 32) i = wid + (k - 1) * NW;  // pad: this wave's previous piece again (same bytes, same place)
+    const int isv = i >> 4, pi = i & 15;
+    int r, d0;
+    if (!isv) {
+      r = 4 * pi + g4;
+      d0 = 8 * (col ^ (r & 15));
+    } else {
+      const int rh = 4 * (pi & 7) + g4;
+      r = 32 * (pi >> 3) + rh;
+      d0 = (8 * col) ^ (16 * (rh & 7));
+    }
+    loff[k] = (uint32_t)((r & 15) * D_ + d0);
+    pslot[k] = isv ? 2 * (pi >> 3) + ((pi & 7) >> 2) : pi >> 2;  // rows of a piece share one page
+    pisv[k] = isv;
+    pdst[k] = (isv ? FL_KV * D_ * 2 : 0) + pi * 1024;
+  }
   auto issue = [&](int c) {
-    char* kbuf = smem + (c & 1) * (FL_KV * D_ * 2);
-    char* vbuf = smem + 2 * (FL_KV * D_ * 2) + (c & 1) * (FL_KV * D_ * 2);
+    const uint32_t stage = lds_addr_of(smem) + (uint32_t)((c % FL_NST) * FL_STAGE);
+    const int cc = min(c, nch - 1);
     int pg[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) pg[j] = __builtin_amdgcn_readfirstlane(s_bt[min(4 * c + j, npg - 1)]);  // past the bound: the last page
-    for (int i = wid; i < 32; i += nw) {
-      const int isv = i >> 4, pi = i & 15;
-      int r, d0;
-      uint32_t dst;
-      if (!isv) {  // K rows 4 pi .. 4 pi + 3; lane -> physical 16-B chunk l & 15 holds logical chunk ^ (row & 15)
-        r = 4 * pi + g4;
-        d0 = 8 * (col ^ (r & 15));
-        dst = lds_addr_of(kbuf + pi * 1024);
-      } else {  // V half pi / 8, rows 4 (pi % 8) .. +3 of that half (v_lds_off's 8-B chunk swizzle)
-        const int rh = 4 * (pi & 7) + g4;
-        r = 32 * (pi >> 3) + rh;
-        d0 = (8 * col) ^ (16 * (rh & 7));
-        dst = lds_addr_of(vbuf + pi * 1024);
-      }
-      // rows of a piece share one page: r / 16 as a function of the (wave-uniform) piece index
-      const int pj = isv ? 2 * (pi >> 3) + ((pi & 7) >> 2) : pi >> 2;
-      const int page = pj == 0 ? pg[0] : pj == 1 ? pg[1] : pj == 2 ? pg[2] : pg[3];
-      const bf16_t* src = (isv ? a.v_cache : a.k_cache) + (size_t)page * blk_stride + head_off + (r & 15) * D_ + d0;
-      glds16(src, __builtin_amdgcn_readfirstlane(dst));
+    for (int j = 0; j < 4; ++j) pg[j] = __builtin_amdgcn_readfirstlane(s_bt[min(4 * cc + j, npg - 1)]);  // past the bound: the last page
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int page = pslot[k] == 0 ? pg[0] : pslot[k] == 1 ? pg[1] : pslot[k] == 2 ? pg[2] : pg[3];
+      const bf16_t* base = (pisv[k] ? a.v_cache : a.k_cache) + (size_t)page * blk_stride + head_off;
+      glds16(base + loff[k], stage + (uint32_t)pdst[k]);
     }
   };
   const float cscale = a.scale * LOG2E;
@@ -619,15 +657,10 @@ __global__ __launch_bounds__(512, CT == 1 ? 3 : 2) void attn_flash_kernel(AttnAr
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) o[ct][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  if (nch > 0) issue(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Q fragments and chunk 0 landed
-  __builtin_amdgcn_s_barrier();
-  for (int c = 0; c < nch; ++c) {
-    if (c + 1 < nch) issue(c + 1);  // into the buffer every wave finished reading last iteration
-    const char* kb = smem + (c & 1) * (FL_KV * D_ * 2);
-    const bf16_t* vb = reinterpret_cast<const bf16_t*>(smem + 2 * (FL_KV * D_ * 2) + (c & 1) * (FL_KV * D_ * 2));
-    // S^T tiles: 4 token tiles x CT column tiles
-    f32x4 st[4][CT];
+  const int q = (lane >> 2) & 3, p4 = lane & 3;
+  // S^T tiles of chunk c: 4 token tiles x CT column tiles (K from stage c % NST)
+  auto qk = [&](int c, f32x4 (&st)[4][CT]) {
+    const char* kb = smem + (c % FL_NST) * FL_STAGE;
 #pragma unroll
     for (int tt = 0; tt < 4; ++tt) {
 #pragma unroll
@@ -640,25 +673,32 @@ __global__ __launch_bounds__(512, CT == 1 ? 3 : 2) void attn_flash_kernel(AttnAr
         for (int ct = 0; ct < CT; ++ct) st[tt][ct] = mfma16(as_bf16x8(kf), as_bf16x8(qf[ct][kk]), st[tt][ct]);
       }
     }
-    // online softmax per column tile over the 64 tokens (lane: column col, tokens 16 tt + 4 g4 + i)
+  };
+  // online softmax of chunk c per column tile over its 64 tokens (lane: column col, tokens
+  // 16 tt + 4 g4 + i) -> P^T fragments. SWP: branch-free (mask by select, rescale every chunk),
+  // so the next chunk's QK MFMAs issued before it interleave with this VALU in one basic block
+  auto softmax = [&](int c, f32x4 (&st)[4][CT], bf16x8 (&pb)[CT][2]) {
     const bool masked = c >= nfull;  // block-uniform
-    bf16x8 pb[CT][2];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
-      if (masked) {
+      if (SWP || masked) {
+        // token t = c 64 + 16 tt + 4 g4 + i is masked when t >= lim: i.e. 16 tt + i >= lim - c 64 - 4 g4
+        const int rel = (SWP && !masked ? 0x3fffffff : lim[ct]) - c * FL_KV - 4 * g4;
 #pragma unroll
         for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            if (c * FL_KV + 16 * tt + 4 * g4 + i >= lim[ct]) st[tt][ct][i] = -INFINITY;
+            if (16 * tt + i >= rel) st[tt][ct][i] = -INFINITY;
       }
+      // max without NaN canonicalisation (the scores are finite or -inf): v_max3 chains
       float cmax = -INFINITY;
 #pragma unroll
-      for (int tt = 0; tt < 4; ++tt) cmax = fmaxf(cmax, fmaxf(fmaxf(st[tt][ct][0], st[tt][ct][1]), fmaxf(st[tt][ct][2], st[tt][ct][3])));
-      cmax = fmaxf(cmax, xor16(cmax));
-      cmax = fmaxf(cmax, xor32(cmax));
+      for (int tt = 0; tt < 4; ++tt)
+        cmax = fmax3_(cmax, fmax3_(st[tt][ct][0], st[tt][ct][1], st[tt][ct][2]), st[tt][ct][3]);
+      cmax = fmax_(cmax, xor16(cmax));
+      cmax = fmax_(cmax, xor32(cmax));
       const float mn = fmaxf(m[ct], cmax * cscale);
-      if (__any(mn > m[ct])) {  // wave-uniform: rescale only when a running max moved
+      if (SWP || !lazy || __any(mn > m[ct])) {  // wave-uniform: rescale only when a running max moved
         const float alpha = __builtin_amdgcn_exp2f(m[ct] - (mn == -INFINITY ? 0.f : mn));
         l[ct] *= alpha;
 #pragma unroll
@@ -678,8 +718,10 @@ __global__ __launch_bounds__(512, CT == 1 ? 3 : 2) void attn_flash_kernel(AttnAr
       pb[ct][0] = pack_p(st[0][ct], st[1][ct]);
       pb[ct][1] = pack_p(st[2][ct], st[3][ct]);
     }
-    // O^T += V^T P^T: each V^T fragment (ds_read_b64_tr_b16) feeds every column tile
-    const int q = (lane >> 2) & 3, p4 = lane & 3;
+  };
+  // O^T += V^T P^T of chunk c: each V^T fragment (ds_read_b64_tr_b16) feeds every column tile
+  auto pv = [&](int c, const bf16x8 (&pb)[CT][2]) {
+    const bf16_t* vb = reinterpret_cast<const bf16_t*>(smem + (c % FL_NST) * FL_STAGE + FL_KV * D_ * 2);
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       const bf16_t* vh = vb + half * (32 * D_);
@@ -695,15 +737,58 @@ __global__ __launch_bounds__(512, CT == 1 ? 3 : 2) void attn_flash_kernel(AttnAr
         for (int ct = 0; ct < CT; ++ct) o[ct][mt] = mfma16(av, pb[ct][half], o[ct][mt]);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of chunk c + 1 landed
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // everyone's; buffer c & 1 free
+  };
+  if constexpr (!SWP) {
+    if (nch > 0) {
+#pragma unroll
+      for (int c = 0; c < FL_NST - 1; ++c) issue(c);
+    }
+    __builtin_amdgcn_s_waitcnt(vm_imm((FL_NST - 2) * P));  // chunk 0 landed (this wave's pieces)
+    __builtin_amdgcn_s_barrier();                          // everyone's
+    for (int c = 0; c < nch; ++c) {
+      issue(c + FL_NST - 1);  // into the stage every wave finished reading last iteration
+      f32x4 st[4][CT];
+      bf16x8 pb[CT][2];
+      qk(c, st);
+      softmax(c, st, pb);
+      pv(c, pb);
+      __builtin_amdgcn_s_waitcnt(vm_imm((FL_NST - 2) * P));  // this wave's pieces of chunk c + 1 landed
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // everyone's; stage c % NST free
+    }
+  } else {
+    // software-pipelined: iteration c computes S of chunk c + 1 (MFMA) beside the softmax of chunk c
+    // (VALU), then P V of chunk c. Live stages: c (V), c + 1 (K), c + 2 (landing), c + 3 (issued)
+    static_assert(FL_NST >= 4, "the pipelined loop keeps four chunks resident");
+    if (nch > 0) {
+#pragma unroll
+      for (int c = 0; c < FL_NST - 1; ++c) issue(c);
+    }
+    __builtin_amdgcn_s_waitcnt(vm_imm((FL_NST - 3) * P));  // chunks 0 and 1 landed (this wave's pieces)
+    __builtin_amdgcn_s_barrier();                          // everyone's
+    f32x4 sc[4][CT];
+    if (nch > 0) qk(0, sc);
+    for (int c = 0; c < nch; ++c) {
+      issue(c + FL_NST - 1);  // into stage (c - 1) % NST: every wave finished its P V in iteration c - 1
+      f32x4 sn[4][CT];
+      bf16x8 pb[CT][2];
+      qk(c + 1, sn);  // past the last chunk: the re-read last chunk, discarded
+      softmax(c, sc, pb);
+      pv(c, pb);
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) sc[tt][ct] = sn[tt][ct];
+      __builtin_amdgcn_s_waitcnt(vm_imm((FL_NST - 3) * P));  // this wave's pieces of chunk c + 2 landed
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // everyone's; stage c % NST free
+    }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the look-ahead DMAs drained before the block exits
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
     float ll = l[ct];
     ll += xor16(ll);
     ll += xor32(ll);
-    const int qi = q0 + 16 * ct + col;
+    const int qi = qw0 + 16 * ct + col;
     if (qi >= qhi) continue;
     const float inv = ll > 0.f ? 1.f / ll : 0.f;
     const size_t orow = (size_t)(qs + qi) * a.out_stride + (size_t)hq * D_;
@@ -717,16 +802,19 @@ __global__ __launch_bounds__(512, CT == 1 ? 3 : 2) void attn_flash_kernel(AttnAr
   }
 }
 
-// column tiles per flash wave for a head group of G (0 = not supported): two (32 queries per block)
-// up to G = 4, where 4-wave blocks pair up on a CU; one (16 queries) for G <= 8, which keeps the
-// grid >= 2 blocks per CU at 2k tokens for the 1-2 KV-head layouts (VGATE_FLASH_CT=2 forces two)
-static int flash_ct(const AttnArgs& a) {
-  if (a.D != D_ || a.BS != BS_ || a.Hkv <= 0 || a.Hq % a.Hkv) return 0;
+// flash configuration for a head group of G (ct = 0: not supported): waves NW = 8 when G | 8
+// (G query groups of 8 / G), 6 for G = 3, 6; two 16-query column tiles per wave for G <= 4
+// (Llama: 64-query blocks), one above (16-query blocks keep >= one block per CU at 2k tokens for
+// the 1-2 KV-head layouts; VGATE_FLASH_CT=2 forces two)
+struct FlashCfg { int ct, nw; };
+static FlashCfg flash_cfg(const AttnArgs& a) {
+  if (a.D != D_ || a.BS != BS_ || a.Hkv <= 0 || a.Hq % a.Hkv) return {0, 0};
   const int G = a.Hq / a.Hkv;
-  if (G <= 4) return 2;
+  const int nw = 8 % G == 0 ? 8 : (6 % G == 0 ? 6 : 0);
+  if (nw == 0) return {0, 0};
   static const int force = [] { const char* e = getenv("VGATE_FLASH_CT"); return e ? atoi(e) : 0; }();
-  if (G <= 8) return force == 2 ? 2 : 1;
-  return 0;
+  const int ct = G <= 4 ? 2 : (force == 2 ? 2 : 1);
+  return {ct, nw};
 }
 
 static bool flash_enabled() {
@@ -764,14 +852,29 @@ void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
   int tiles = a.num_tiles > 0 ? a.num_tiles : 0;
   // prefill tiles on the flash kernel (its own launch; a decode-only graph bucket carries no tile
   // list, StepMeta.view), the unified kernel keeps the decode rows
-  const int ct = tiles > 0 && flash_enabled() ? flash_ct(a) : 0;
-  if (ct > 0) {
+  const FlashCfg fc = tiles > 0 && flash_enabled() ? flash_cfg(a) : FlashCfg{0, 0};
+  if (fc.ct > 0) {
     AttnArgs f = a;
     f.tl = tl_take("attn_flash", tiles * a.Hkv);
-    const size_t lds = (size_t)FL_LDS + (size_t)a.max_blocks * 4;
-    const dim3 grid(tiles, a.Hkv, 1), block(64 * (a.Hq / a.Hkv));
-    if (ct == 2) hipLaunchKernelGGL(attn_flash_kernel<2>, grid, block, lds, st, f);
-    else hipLaunchKernelGGL(attn_flash_kernel<1>, grid, block, lds, st, f);
+    // experiments: VGATE_FLASH_NST (ring stages 2 / 3 / 4), VGATE_FLASH_LAZY (0: rescale every chunk)
+    static const int nst = [] { const char* e = getenv("VGATE_FLASH_NST"); const int v = e ? atoi(e) : 2; return v <= 2 ? 2 : 4; }();
+    static const int lazy = [] { const char* e = getenv("VGATE_FLASH_LAZY"); return e ? atoi(e) : 1; }();
+    static const int swp = [] { const char* e = getenv("VGATE_FLASH_SWP"); return e ? atoi(e) : 0; }();
+    const size_t lds = (size_t)(nst == 2 ? 2 : 4) * FL_STAGE + (size_t)a.max_blocks * 4;
+    const size_t lds4 = (size_t)4 * FL_STAGE + (size_t)a.max_blocks * 4;
+    const dim3 grid(tiles, a.Hkv, 1), block(64 * fc.nw);
+#define VG_FL(CT_, NW_)                                                                                      \
+    do {                                                                                                     \
+      if (swp) hipLaunchKernelGGL((attn_flash_kernel<CT_, NW_, 4, true>), grid, block, lds4, st, f, lazy);     \
+      else if (nst == 2) hipLaunchKernelGGL((attn_flash_kernel<CT_, NW_, 2, false>), grid, block, lds, st, f, lazy); \
+      else hipLaunchKernelGGL((attn_flash_kernel<CT_, NW_, 4, false>), grid, block, lds, st, f, lazy);         \
+    } while (0)
+    if (fc.nw == 8) {
+      if (fc.ct == 2) VG_FL(2, 8); else VG_FL(1, 8);
+    } else {
+      if (fc.ct == 2) VG_FL(2, 6); else VG_FL(1, 6);
+    }
+#undef VG_FL
     tiles = 0;
   }
   const int nw = attn_waves(a);

@@ -181,7 +181,8 @@ def test_tile_order_and_decode_only_buckets():
         nl = int((o % lead == 0).sum())
         assert all(int(t) % lead == 0 for t in o[:nl]) and all(int(t) % lead for t in o[nl:])
         assert list(o[:nl]) == sorted(o[:nl], reverse=True)
-    assert ops.flash_lead(32, 8) == 32 and ops.flash_lead(12, 2) == 16 and ops.flash_lead(8, 1) == 16
+    assert ops.flash_lead(32, 8) == 64 and ops.flash_lead(12, 2) == 16 and ops.flash_lead(8, 1) == 16
+    assert ops.flash_lead(16, 16) == 256 and ops.flash_lead(24, 8) == 64
     assert StepMeta.tile_cap(8, 8) == 0 and StepMeta.tile_cap(4, 8) == 0 and StepMeta.tile_cap(32, 8) == 10
     eng = LLMEngine(EngineConfig(model="tiny-debug", device="cpu", max_num_seqs=8, max_num_batched_tokens=64,
                                  num_kv_blocks=64, max_model_len=128))

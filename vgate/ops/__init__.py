@@ -584,9 +584,14 @@ def prefill_tiles(query_lens: list[int], lead: int = 32) -> tuple[list[int], lis
 
 
 def flash_lead(hq: int, hkv: int) -> int:
-    """Queries per flash-prefill block for a head layout (attention.hip flash_ct: two 16-query
-    column tiles per wave up to 4 query heads per KV head, one above)."""
-    return 32 if hq // max(hkv, 1) <= 4 else 16
+    """Queries per flash-prefill block for a head layout (attention.hip flash_cfg: 8 waves when
+    G = hq / hkv divides 8, else 6; two 16-query column tiles per wave up to G = 4, one above;
+    the waves are G heads x NW / G query groups)."""
+    G = max(1, hq // max(hkv, 1))
+    nw = 8 if 8 % G == 0 else (6 if 6 % G == 0 else 0)
+    if nw == 0:
+        return 16
+    return 16 * (2 if G <= 4 else 1) * (nw // G)
 
 
 def tile_order(qlen: int, lead: int = 32):
