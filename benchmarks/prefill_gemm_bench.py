@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--models", default="qwen,llama8b,llama70b_tp8")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--bn", type=int, default=0)
+    ap.add_argument("--tuned", action="store_true",
+                    help="report the decomposition the engine's start-up tuner (ops.tune_prefill) would pick: "
+                         "the fastest of ops.PREFILL_CANDIDATES unless within 5%% of the heuristic")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     C = ops.native()
@@ -61,13 +64,26 @@ def main():
                 x = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()
                 out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
                 ours = timeit(lambda: C.gemm(x, wp, N, K, out, 0, ws=ws, path=1, ntb=a.bn), a.iters)
+                pick = (a.bn, 0)
+                if a.tuned:
+                    t = {}
+                    for bn, sk in ops.PREFILL_CANDIDATES:
+                        try:
+                            t[(bn, sk)] = timeit(lambda: C.gemm(x, wp, N, K, out, 0, ws=ws, path=1, ntb=bn, splitk=sk),
+                                                 a.iters)
+                        except RuntimeError:
+                            continue
+                    best = min(t, key=t.get)
+                    if t[best] < 0.95 * t[(0, 0)]:
+                        pick, ours = best, t[best]
+                    C.gemm(x, wp, N, K, out, 0, ws=ws, path=1, ntb=pick[0], splitk=pick[1])
                 lib = timeit(lambda: torch.mm(x, w.t()), a.iters)
                 err = ((out.float() - (x.float() @ w.float().t())).norm() / (x.float() @ w.float().t()).norm()).item()
                 fl = 2.0 * M * N * K
                 r = {"model": model, "proj": proj, "M": M, "N": N, "K": K, "ours_us": round(ours, 2),
                      "hipblaslt_us": round(lib, 2), "ours_tflops": round(fl / ours / 1e6, 1),
                      "hipblaslt_tflops": round(fl / lib / 1e6, 1), "ratio_vs_lib": round(lib / ours, 3),
-                     "rel_err": round(err, 5)}
+                     "rel_err": round(err, 5), "plan": list(pick)}
                 rows.append(r)
                 print(json.dumps(r), flush=True)
     geo = 1.0

@@ -287,11 +287,14 @@ _WS: dict = {}
 
 
 def workspace(device) -> torch.Tensor:
-    """Per-device GEMM workspace: 64k split-K tickets (zeroed once) + 32 MiB fp32 slabs."""
+    """Per-device GEMM workspace: 64k split-K tickets (zeroed once) + fp32 slabs (256 MiB on a GPU:
+    a K-split prefill GEMM needs slices x M x N x 4 bytes — with 32 MiB the 4-way split of Llama-3-8B
+    down_proj at M = 1024 silently fell back to one slice on 64 tiles; 32 MiB on the CPU)."""
     key = str(device)
     ws = _WS.get(key)
     if ws is None:
-        ws = torch.zeros(65536 + 8 * 2**20, dtype=torch.int32, device=device)
+        slab_words = (64 if torch.device(device).type == "cuda" else 8) * 2**20
+        ws = torch.zeros(65536 + slab_words, dtype=torch.int32, device=device)
         _WS[key] = ws
     return ws
 
@@ -642,8 +645,9 @@ def _plan_bucket(plan: dict, M: int):
 # (tile code, K slices) candidates of the prefill kernels (csrc/kernels/gemm_prefill.hip
 # launch_prefill_epi): 0 = the launcher's heuristic, 64 / 128 = 128 x 64 / 128 x 128 tiles,
 # 256 = 256 x 128 3-deep ring, 768 / 1024 = the 4-phase 256 x 128 / 256 x 256 kernels
-PREFILL_CANDIDATES = [(0, 0), (64, 0), (128, 0), (128, 4), (256, 0), (256, 4), (256, 6), (768, 0), (768, 4),
-                      (768, 6), (1024, 0), (1024, 2), (1024, 6)]
+PREFILL_CANDIDATES = [(0, 0), (64, 0), (128, 0), (128, 2), (128, 4), (256, 0), (256, 4), (256, 6), (768, 0),
+                      (768, 2), (768, 3), (768, 4), (768, 6), (1024, 0), (1024, 2), (1024, 3), (1024, 4),
+                      (1024, 6)]
 
 
 def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = 0.05) -> dict:
