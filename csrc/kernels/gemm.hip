@@ -146,7 +146,10 @@ void launch_gemm(const GemmArgs& g, hipStream_t st) {
   if (g.M <= 0) return;
   // long steps (prefill chunks): the LDS-tiled MFMA kernel (gemm_prefill.hip) on the same packed
   // weights; it declines shapes / modes it does not take
-  if (g.path > 0 || (g.path == 0 && g.M >= 128 && g.waves == 0 && g.splitk == 0)) {
+  // mixed prefill + decode steps (16 < M <= 64): the medium-M kernel when the start-up tuner
+  // measured it faster (path 2, gemm_mid.hip); it declines shapes / modes it does not take
+  if (g.path == 2 && launch_gemm_mid(g, st)) return;
+  if (g.path == 1 || (g.path == 0 && g.M >= 128 && g.waves == 0 && g.splitk == 0)) {
     GemmArgs h = g;
     if (g.path == 0) h.ntb = 0;
     if (launch_gemm_prefill(h, st)) return;

@@ -541,9 +541,12 @@ __global__ __launch_bounds__(512, 1) void gemm_prefill4_kernel(GemmParams p) {
 }
 
 // Split-K combine: one wave per (16 rows, NTB tiles): the slices' partials summed in slice
-// order, the row scale from the summed slice sums of squares, then the shared epilogue.
+// order, the row scale from the summed slice sums of squares, then the shared epilogue. The
+// slices' loads go out in groups of ZG (clamped index, masked add) so a combine costs one memory
+// round trip per ZG slices instead of one per slice.
 template <int EPI, int NORM, int NTB>
 __global__ __launch_bounds__(256) void prefill_reduce_kernel(GemmParams p, int nz) {
+  constexpr int ZG = 8;
   TLScope tl_scope(p.dbg_ts);
   const int lane = threadIdx.x & 63;
   const int grp = blockIdx.x * 4 + (threadIdx.x >> 6);  // (row block, tile group), tile group fastest
@@ -557,11 +560,25 @@ __global__ __launch_bounds__(256) void prefill_reduce_kernel(GemmParams p, int n
 #pragma unroll
   for (int j = 0; j < NTB; ++j) v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float s2 = 0.f;
-  for (int z = 0; z < nz; ++z) {
-    const float* part = p.slabs + (size_t)z * p.M * p.N + (size_t)mm * p.N;
+  for (int z0 = 0; z0 < nz; z0 += ZG) {
+    f32x4 r[ZG][NTB];
+    float q[ZG];
 #pragma unroll
-    for (int j = 0; j < NTB; ++j) v[j] += *reinterpret_cast<const f32x4*>(part + (nt0 + j) * 16 + nsub);
-    if constexpr (NORM == 2) s2 += p.slabs[(size_t)nz * p.M * p.N + (size_t)z * p.M + mm];
+    for (int u = 0; u < ZG; ++u) {
+      const int z = min(z0 + u, nz - 1);
+      const float* part = p.slabs + (size_t)z * p.M * p.N + (size_t)mm * p.N;
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) r[u][j] = *reinterpret_cast<const f32x4*>(part + (nt0 + j) * 16 + nsub);
+      q[u] = NORM == 2 ? p.slabs[(size_t)nz * p.M * p.N + (size_t)z * p.M + mm] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < ZG; ++u) {
+      if (z0 + u < nz) {
+#pragma unroll
+        for (int j = 0; j < NTB; ++j) v[j] += r[u][j];
+        if constexpr (NORM == 2) s2 += q[u];
+      }
+    }
   }
   if constexpr (NORM == 2) {
     const float sc = rsqrtf(s2 / (float)p.K + p.eps);
@@ -570,6 +587,23 @@ __global__ __launch_bounds__(256) void prefill_reduce_kernel(GemmParams p, int n
   }
   epilogue<NTB, EPI, false>(p, v, m, nt0, nsub, EpiPre<NTB>{}, m < p.M);
 }
+
+// the combine launch for p.splitk-free callers (gemm_mid.hip)
+template <int EPI, int NORM, int NTB>
+void launch_prefill_reduce(const GemmParams& p, int nz, hipStream_t st) {
+  const int groups = ((p.M + 15) / 16) * (p.N / (16 * NTB));
+  GemmParams r = p;
+  r.dbg_ts = tl_take("prefill_reduce", (groups + 3) / 4);
+  hipLaunchKernelGGL((prefill_reduce_kernel<EPI, NORM, NTB>), dim3((groups + 3) / 4), dim3(256), 0, st, r, nz);
+}
+#define VG_RED_INST(E)                                                                  \
+  template void launch_prefill_reduce<E, 0, 1>(const GemmParams&, int, hipStream_t);   \
+  template void launch_prefill_reduce<E, 2, 1>(const GemmParams&, int, hipStream_t);
+VG_RED_INST(EPI_BF16)
+VG_RED_INST(EPI_F32)
+VG_RED_INST(EPI_SILU)
+VG_RED_INST(EPI_QKV)
+#undef VG_RED_INST
 
 template <int EPI, int NORM, int NTB, int BM = 256, int BN = 128, int WM = 4, int WN = 2, int NS = 3, int SCHED = 0>
 static void launch_prefill2_one(const GemmParams& p, int nz, hipStream_t st) {

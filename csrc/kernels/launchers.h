@@ -28,7 +28,7 @@ struct GemmArgs {
   int splitk;         // 0 = heuristic
   int ntb;            // 16-column tiles per block for plain / f32 epilogues (0 = heuristic; 1, 2, 4)
   int path;           // M > 16 dense: 0 auto (prefill kernel at M >= 128), 1 force prefill kernel,
-                      // -1 never (tile / decode kernels)
+                      // 2 medium-M kernel (16 < M <= 64), -1 never (tile / decode kernels)
   float* slabs;       // split-K fp32 partial slabs (workspace) or null
   size_t slab_bytes;
   uint32_t* counters; // split-K arrival tickets, zero-initialised, self-resetting
@@ -62,6 +62,9 @@ void launch_gemm(const GemmArgs& g, hipStream_t st);
 // LDS-tiled prefill GEMM (gemm_prefill.hip) for long steps; returns false for a shape / mode it
 // does not take (caller falls back). g.ntb: forced tile width (0 heuristic, 64, 128).
 bool launch_gemm_prefill(const GemmArgs& g, hipStream_t st);
+// medium-M GEMM (gemm_mid.hip, 16 < M <= 64): W = g.waves tiles per block, g.splitk K slices
+// (0 = heuristic); returns false for a shape / mode it does not take (caller falls back)
+bool launch_gemm_mid(const GemmArgs& g, hipStream_t st);
 // AWQ int4 fragments -> bf16 fragment-packed copy (optionally gamma-folded) for the prefill kernel
 void launch_awq_dequant(const void* wq, const uint16_t* scales, const uint16_t* sz, const uint16_t* gamma,
                         void* out, int N, int K, int group, hipStream_t st);

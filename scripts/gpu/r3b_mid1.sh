@@ -1,0 +1,21 @@
+# Round 3 (session 2): medium-M kernel — correctness, standalone shapes, in-engine mixed steps (tuned / forced mid / default)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "mid_gemm or prefill_lds_gemm or tune_prefill" > gpurun_out/r3b_mid1_tests.log 2>&1 || { tail -40 gpurun_out/r3b_mid1_tests.log; exit 1; }
+tail -2 gpurun_out/r3b_mid1_tests.log
+timeout -k 10 300 python -u benchmarks/medium_m_bench.py > gpurun_out/r3b_mid1_mm.log 2>&1 || { tail -30 gpurun_out/r3b_mid1_mm.log; exit 1; }
+python3 - gpurun_out/r3b_mid1_mm.log <<'PY'
+import json, sys
+for l in open(sys.argv[1]):
+    if l.startswith('{'):
+        d = json.loads(l)
+        mids = {k: v for k, v in d["all"].items() if k.startswith("-1")}
+        bm = min(mids, key=mids.get) if mids else None
+        print(d["shape"], d["M"], "default", d["default_us"], "best", d["best"], d["best_us"], "best_mid", bm, mids.get(bm), "mid_heur", mids.get("-14/0"))
+PY
+for m in default mid tuned; do
+timeout -k 10 300 python -u benchmarks/mixed_step.py --medium $m --prompts 16,32,48 > gpurun_out/r3b_mid1_mixed_$m.log 2>&1 || { tail -30 gpurun_out/r3b_mid1_mixed_$m.log; exit 1; }
+grep '^{' gpurun_out/r3b_mid1_mixed_$m.log | cut -c1-600
+done

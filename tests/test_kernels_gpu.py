@@ -978,6 +978,92 @@ def test_prefill_lds_gemm_all_epilogues(M, bn, sk):
     assert _rel_err(kc, kc2) < 2e-2 and _rel_err(vc, vc2) < 2e-2
 
 
+@pytest.mark.parametrize("M", [17, 24, 40, 48, 64])
+@pytest.mark.parametrize("w,s_long,s_short", [(0, 0, 0), (4, 6, 2), (4, 8, 3), (2, 12, 4), (1, 16, 6), (4, 7, 16),
+                                              (8, 0, 0)])
+def test_mid_gemm_all_epilogues(M, w, s_long, s_short):
+    """The medium-M kernel (gemm_mid.hip, path=2: x slice DMA'd into LDS, every weight fragment of a
+    wave's tile slice in flight, K slices combined by the reduce kernel) against the fp32
+    references: plain + in-place residual over a long K (192 k-steps), folded-norm SiLU*mul,
+    folded-norm QKV + bias + RoPE + paged KV write; rows past M (partial m-tiles) masked; the
+    heuristic and forced (tiles per block, K slices) decompositions."""
+    torch.manual_seed(170 + M + 7 * w + s_short)
+    H, D, BS, hq, hkv, I = 1536, 128, 16, 12, 2, 1024
+    C, ws = ops.native(), ops.workspace(DEV)
+    x = (torch.randn(M, H, device=DEV) * 1.5).bfloat16()
+    nw = (torch.rand(H, device=DEV) + 0.5).bfloat16()
+    K2 = 4 * H
+    x2 = torch.randn(M, K2, device=DEV).bfloat16()
+    wd = (torch.randn(H, K2, device=DEV) / math.sqrt(K2)).bfloat16()
+    res = torch.randn(M, H, device=DEV).bfloat16()
+    out = res.clone()
+    C.gemm(x2, ops.Linear(wd).wp, H, K2, out, 0, res=out, ws=ws, path=2, waves=w, splitk=s_long)
+    assert _rel_err(out, ref.linear_ref(x2, wd, None, res)) < 1e-2
+    wg = (torch.randn(I, H, device=DEV) / math.sqrt(H)).bfloat16()
+    wu = (torch.randn(I, H, device=DEV) / math.sqrt(H)).bfloat16()
+    gu = ops.Linear(torch.cat([wg, wu]), layout="silu")
+    assert gu.fold_norm(nw)
+    h = torch.empty(M, I, dtype=torch.bfloat16, device=DEV)
+    C.gemm(x, gu.wp, 2 * I, H, h, 2, ws=ws, rownorm=True, eps=1e-6, path=2, waves=w, splitk=s_short)
+    xn, _ = ref.rmsnorm_ref(x, nw, 1e-6)
+    assert _rel_err(h, ref.silu_mul_linear_ref(xn, wg, wu)) < 2e-2
+    N = (hq + 2 * hkv) * D
+    wq = (torch.randn(N, H, device=DEV) / math.sqrt(H)).bfloat16()
+    b = (torch.randn(N, device=DEV) * 0.1).bfloat16()
+    pos = torch.randint(0, 4096, (M,), dtype=torch.int32, device=DEV)
+    nblk = (M + BS - 1) // BS + 8
+    slots = torch.randperm(nblk * BS, device=DEV)[:M].int()
+    slots[min(4, M - 1)] = -1
+    cs = ref.rope_cos_sin(4096, D, 1e6, device=DEV)
+    kc = torch.zeros(nblk, hkv, BS, D, device=DEV).bfloat16()
+    vc = torch.zeros_like(kc)
+    lq = ops.Linear(wq, bias=b, layout="qkv")
+    assert lq.fold_norm(nw)
+    q = torch.empty(M, hq * D, dtype=torch.bfloat16, device=DEV)
+    C.gemm(x, lq.wp, N, H, q, 3, bias=b, ws=ws, rownorm=True, eps=1e-6, positions=pos, slots=slots, cos_sin=cs,
+           k_cache=kc, v_cache=vc, hq=hq, hkv=hkv, path=2, waves=w, splitk=s_short)
+    qkv = ref.linear_ref(xn, wq, b)
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    ref.rope_kv_ref(qkv, pos, slots, cs, kc2, vc2, hq, hkv, D)
+    assert _rel_err(q, qkv[:, : hq * D]) < 2e-2
+    assert _rel_err(kc, kc2) < 2e-2 and _rel_err(vc, vc2) < 2e-2
+
+
+@pytest.mark.parametrize("M", [20, 32, 48, 64])
+@pytest.mark.parametrize("I,K", [(8960, 1536), (1000 * 8, 2048), (128, 512)])
+def test_mid_wide_gemm_silu(M, I, K):
+    """The wide medium-M kernel (one block per CU owning whole tiles, K in 16-k-step parts met in
+    LDS, x by m-tile pairs): Qwen2.5-1.5B gate_up (1120 tiles: 4-5 per block, idle part-waves in the
+    4-tile blocks), a 1000-tile / 64-k-step shape and a one-block-per-tile one, folded-norm SiLU*mul
+    against the fp32 reference."""
+    torch.manual_seed(300 + M + I)
+    x = (torch.randn(M, K, device=DEV) * 1.5).bfloat16()
+    nw = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+    wg = (torch.randn(I, K, device=DEV) / math.sqrt(K)).bfloat16()
+    wu = (torch.randn(I, K, device=DEV) / math.sqrt(K)).bfloat16()
+    gu = ops.Linear(torch.cat([wg, wu]), layout="silu")
+    assert gu.fold_norm(nw)
+    h = torch.empty(M, I, dtype=torch.bfloat16, device=DEV)
+    ops.native().gemm(x, gu.wp, 2 * I, K, h, 2, ws=ops.workspace(DEV), rownorm=True, eps=1e-6, path=2, waves=8)
+    xn, _ = ref.rmsnorm_ref(x, nw, 1e-6)
+    assert _rel_err(h, ref.silu_mul_linear_ref(xn, wg, wu)) < 2e-2
+
+
+def test_mid_gemm_plans_in_linear():
+    """ops.linear consults a medium bucket's plan: a tuned entry routes 16 < M <= 64 rows to the
+    medium kernel, MEDIUM_DEFAULT keeps the default path, and both agree with the reference."""
+    torch.manual_seed(77)
+    K = 1536
+    lin = ops.Linear((torch.randn(2048, K, device=DEV) / math.sqrt(K)).bfloat16())
+    x = torch.randn(48, K, device=DEV).bfloat16()
+    want = ref.linear_ref(x, lin.dense_weight())
+    for cfg in [ops.MEDIUM_DEFAULT, (ops.MID_BASE - 4, 0), (ops.MID_BASE - 2, 4), (ops.MID_BASE - 8, 0), (64, 0)]:
+        lin.prefill_plan = {48: cfg, 128: (0, 0)}
+        assert _rel_err(ops.linear(x, lin), want) < 1e-2, cfg
+    assert ops._plan_kw((ops.MID_BASE - 4, 3), 48) == dict(path=2, waves=4, splitk=3)
+    assert ops._plan_kw(ops.MEDIUM_DEFAULT, 48) == {}
+
+
 def test_kernel_copy_host_device_round_trip():
     """ops.host_device_copy: pinned host -> device and device -> pinned host by the copy kernel
     (16-B pieces, sizes rounded up to 16 inside both tensors), ordered on the current stream."""

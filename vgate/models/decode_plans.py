@@ -19,6 +19,11 @@ PLANS: dict[tuple[int, int, str, str], tuple[int, int, int]] = {
     (7168, 8192, "silu", "dense"): (4, 1, 0),    # gate_up: 448 one-tile blocks at 4 waves (heuristic 8: +118 us)
     (8192, 3584, "plain", "dense"): (8, 1, 2),   # down_proj
     (16032, 8192, "plain", "dense"): (8, 1, 1),  # LM head shard
+    # Qwen2.5-1.5B AWQ int4, batch 8, ctx 100 (profiles/r3_awq_decode_sweep.log, whole-step replays;
+    # baseline 1287.8 us): qkv on awq_stream_kernel (packed scales, XP-packed activations, 4 waves x 3
+    # k-quads) instead of the K-split awq_gemm_kernel, down_proj in 8 K slices of 4 waves
+    (2048, 1536, "qkv", "awq"): (4, 1, 1),
+    (1536, 8960, "plain", "awq"): (4, 8, 1),
 }
 
 

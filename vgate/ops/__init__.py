@@ -348,10 +348,9 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
     ntb = 0
     if M <= 16 and waves == 0 and splitk == 0:
         waves, splitk, ntb = lin.dec_waves, lin.dec_splitk, lin.dec_ntb
-    elif M >= 128 and waves == 0 and splitk == 0 and path == 0 and lin.prefill_plan and lin.kind == "dense":  # (AWQ: below)
-        cfg = lin.prefill_plan.get(_plan_bucket(lin.prefill_plan, M))
-        if cfg is not None and cfg != (0, 0):
-            ntb, splitk, path = cfg[0], cfg[1], 1
+    elif M > 16 and waves == 0 and splitk == 0 and path == 0 and lin.prefill_plan and lin.kind == "dense":  # (AWQ: below)
+        pk = _plan_kw(lin.prefill_plan.get(_plan_bucket(lin.prefill_plan, M)), M)
+        ntb, splitk, path, waves = pk.get("ntb", 0), pk.get("splitk", 0), pk.get("path", 0), pk.get("waves", 0)
     kw = dict(bias=lin.bias, res=residual, ws=workspace(x.device), waves=waves, splitk=splitk, ntb=ntb, path=path)
     if norm is not None:
         if lin.norm_gamma is not None:  # gamma lives in the weights: row scale only
@@ -403,10 +402,8 @@ def _linear_awq_dequant(x, lin: "Linear", out, residual, norm, qkv, epi, M):
     if qkv is not None:
         kw.update(positions=qkv["positions"], slots=qkv["slots"], cos_sin=qkv["cos_sin"],
                   k_cache=qkv["k_cache"], v_cache=qkv["v_cache"], hq=qkv["hq"], hkv=qkv["hkv"])
-    if M >= 128 and lin.prefill_plan:
-        cfg = lin.prefill_plan.get(_plan_bucket(lin.prefill_plan, M))
-        if cfg is not None and cfg != (0, 0):
-            kw.update(ntb=cfg[0], splitk=cfg[1], path=1)
+    if M > 16 and lin.prefill_plan:
+        kw.update(_plan_kw(lin.prefill_plan.get(_plan_bucket(lin.prefill_plan, M)), M))
     C.gemm(x, scratch, lin.N, lin.K, out, epi, **kw)
     return out
 # the W4A16 kernels are decode kernels (no tile path above M = 16): hand AWQ steps to the
@@ -637,8 +634,10 @@ def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, offsets
 
 
 def _plan_bucket(plan: dict, M: int):
-    """Smallest planned M >= M (a step's rows are padded up to its graph bucket), else None."""
-    keys = [k for k in plan if k >= M]
+    """Smallest planned M >= M (a step's rows are padded up to its graph bucket), else None.
+    Medium rows (M < 128) only take a medium bucket's plan (they are timed against another
+    default path than the prefill buckets)."""
+    keys = [k for k in plan if k >= M and (M >= 128 or k < 128)]
     return min(keys) if keys else None
 
 
@@ -648,6 +647,52 @@ def _plan_bucket(plan: dict, M: int):
 PREFILL_CANDIDATES = [(0, 0), (64, 0), (128, 0), (128, 2), (128, 4), (256, 0), (256, 4), (256, 6), (768, 0),
                       (768, 2), (768, 3), (768, 4), (768, 6), (1024, 0), (1024, 2), (1024, 3), (1024, 4),
                       (1024, 6)]
+# medium-M kernel (csrc/kernels/gemm_mid.hip, 16 < M <= 64) candidates, encoded as tile code
+# MID_BASE - W (W tiles = waves per block) and K slices (0 = its heuristic)
+MID_BASE = -10
+MID_CANDIDATES = [(MID_BASE - w, s) for w in (4, 2) for s in (0, 2, 3, 4, 6, 8, 10, 12, 16)] + [(MID_BASE - 8, 0)]
+_FLUSH: dict = {}
+
+
+def _cold_timer(dev):
+    """Event timer of one launch with the Infinity Cache flushed first: a 512 MiB read sweep evicts
+    the weights a back-to-back repeat would find resident (gate_up's 55 MB fits the 256 MiB cache),
+    so medium-M candidates are ranked by the cold-weight time they take inside a decode step."""
+    buf = _FLUSH.get(str(dev))
+    if buf is None:
+        buf = _FLUSH[str(dev)] = torch.empty(512 * 2**20, dtype=torch.uint8, device=dev)
+    C = native()
+
+    def timed(run, iters):
+        total = 0.0
+        for _ in range(iters):
+            C.prefetch(buf, 1024)
+            s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s0.record()
+            run()
+            s1.record()
+            s1.synchronize()
+            total += s0.elapsed_time(s1)
+        return total / iters
+    return timed
+
+
+def _mid_code(cfg) -> int:
+    """Waves per block of a medium-kernel plan entry, 0 for any other entry."""
+    return MID_BASE - cfg[0] if cfg is not None and cfg[0] <= MID_BASE - 1 else 0
+
+
+def _plan_kw(cfg, M: int) -> dict:
+    """C.gemm keyword overrides of a plan entry (empty: the default path)."""
+    if cfg is None or cfg == MEDIUM_DEFAULT or (cfg == (0, 0) and M >= 128):
+        return {}
+    w = _mid_code(cfg)
+    if w:
+        return dict(path=2, waves=w, splitk=cfg[1])
+    return dict(ntb=cfg[0], splitk=cfg[1], path=1)
+
+
+MEDIUM_DEFAULT = (-1, -1)  # medium-M plan entry: keep the default (decode / tile kernel) path
 
 
 def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = 0.05) -> dict:
@@ -660,6 +705,13 @@ def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = 0.05
     the layer's shape (plain epilogue, all candidates are exact kernels of the same product);
     the heuristic is kept unless a candidate beats it by more than ``margin``. The plan is
     shared by every Linear of the same shape (AWQ layers: the plan of their bf16 dequant scratch).
+
+    Medium buckets (16 < M < 128: the mixed steps of a serving load, one prompt chunk beside the
+    decode rows) are timed against the DEFAULT path at that M too (the K-split decode kernels /
+    the LDS tile kernel, which stream the weights with one or two k-step groups in flight: a
+    Qwen2.5-1.5B step with a 48-token prompt took 2.77 ms against 1.24 ms for pure decode,
+    profiles/r3_mixed_step.log); the entry is :data:`MEDIUM_DEFAULT` unless a prefill
+    decomposition beats that path by more than ``margin``.
     Returns {(N, K): {M: (tile, slices)}}."""
     cand = [lin for lin in lins if getattr(lin, "wp", None) is not None and lin.wp.is_cuda]
     if not cand or not native_available():
@@ -684,12 +736,16 @@ def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = 0.05
             x = torch.rand(M, lin.K, device=dev, generator=g).bfloat16()
             out = torch.empty(M, lin.N, dtype=torch.bfloat16, device=dev)
             times = {}
-            for bn, sk in PREFILL_CANDIDATES:
+            cold = _cold_timer(dev) if M < 128 else None
+            for bn, sk in PREFILL_CANDIDATES + (MID_CANDIDATES if 16 < M <= 64 else []):
                 def run():
-                    C.gemm(x, wp, lin.N, lin.K, out, 0, ws=ws, path=1, ntb=bn, splitk=sk)
+                    C.gemm(x, wp, lin.N, lin.K, out, 0, ws=ws, **_plan_kw((bn, sk), M))
                 try:
                     run()
                 except RuntimeError:
+                    continue
+                if cold is not None:
+                    times[(bn, sk)] = cold(run, iters)
                     continue
                 s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s0.record()
@@ -701,6 +757,14 @@ def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = 0.05
             if (0, 0) not in times:
                 continue
             best = min(times, key=times.get)
+            if M < 128:
+                # medium bucket: against the default path (M > 16 rows -> decode / tile kernels)
+                def run_default():
+                    C.gemm(x, wp, lin.N, lin.K, out, 0, ws=ws)
+                run_default()
+                t_def = cold(run_default, iters)
+                plan[M] = best if times[best] < (1.0 - margin) * t_def else MEDIUM_DEFAULT
+                continue
             plan[M] = best if times[best] < (1.0 - margin) * times[(0, 0)] else (0, 0)
         plans[key] = plan
         lin.prefill_plan = plan

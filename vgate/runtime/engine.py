@@ -135,7 +135,8 @@ class LLMEngine:
         self.prefill_plans: dict = {}
         if self.device.type == "cuda" and cfg.prefill_autotune:
             t1 = time.perf_counter()
-            ms = [t for t in self.runner.t_buckets if t >= 128]
+            # prefill buckets (>= 128 rows) and the medium buckets of mixed prefill + decode steps
+            ms = [t for t in self.runner.t_buckets if t > 16]
             lins = [lin for L in self.model.layers for lin in (L.qkv, L.o, L.gate_up, L.down)]
             if self.tp.size > 1:
                 # rank 0 measures, every rank applies the same plans (per-rank timing noise would
