@@ -29,8 +29,8 @@ CANDIDATES = {
             (1, 4, 0)],
     "o": [(0, 0, 0), (8, 1, 1), (4, 1, 1), (8, 2, 1), (4, 2, 1), (4, 3, 1), (4, 4, 1), (2, 4, 1), (8, 4, 1),
           (2, 8, 1), (1, 8, 1)],
-    "gate_up": [(0, 0, 0), (4, 1, 0), (2, 1, 0), (1, 1, 0), (8, 1, 0), (2, 2, 0), (1, 2, 0), (2, 1, 2), (4, 1, 2),
-                (8, 1, 2), (4, 1, 4), (8, 1, 4)],
+    "gate_up": [(0, 0, 0), (0, 0, -8), (4, 1, 0), (2, 1, 0), (1, 1, 0), (8, 1, 0), (2, 2, 0), (1, 2, 0), (2, 1, 2),
+                (4, 1, 2), (8, 1, 2), (4, 1, 4), (8, 1, 4)],
     "down": [(0, 0, 0), (8, 2, 1), (8, 3, 1), (8, 4, 1), (4, 4, 1), (4, 6, 1), (4, 8, 1), (8, 8, 1),
              (2, 8, 1), (1, 8, 1), (4, 5, 1), (8, 6, 1), (2, 6, 1)],
     "lm_head": [(0, 0, 0), (8, 1, 2), (4, 1, 2), (2, 1, 2), (1, 1, 2), (4, 1, 4), (2, 1, 1), (4, 1, 1)],
@@ -54,7 +54,7 @@ def lins(model, kind):
     return [getattr(L, attr) for L in model.layers]
 
 
-def set_plan(model, kind, cfg):
+def set_plan(model, kind, cfg):  # ntb -8: the wide medium kernel (ops.WIDE_DECODE)
     for lin in lins(model, kind):
         lin.dec_waves, lin.dec_splitk, lin.dec_ntb = cfg
 

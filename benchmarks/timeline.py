@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--max-seqs", type=int, default=64)
     ap.add_argument("--quantization", default=None)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--mixed", type=int, default=0, help="time a MIXED step: one prompt of this many tokens "
+                    "beside the decode rows (benchmarks/mixed_step.py)")
+    ap.add_argument("--wide-gate-up", action="store_true", help="medium buckets: the wide medium kernel for gate_up")
     ap.add_argument("--o-tiles", type=int, default=96, help="o_proj column tiles of a fused attn_o launch (N / 16)")
     a = ap.parse_args()
     eng = LLMEngine(EngineConfig(model=a.model, device="cuda:0", max_model_len=2048, max_num_seqs=a.max_seqs,
@@ -48,6 +51,15 @@ def main():
     eng._drain_inbox()
     for _ in range(4):  # prefill + a few decode steps (graphs of the decode bucket captured)
         eng.step()
+    if a.wide_gate_up:
+        for L in eng.model.layers:
+            for m in list(L.gate_up.prefill_plan):
+                if 16 < m <= 64:
+                    L.gate_up.prefill_plan[m] = (ops.MID_BASE - 8, 0)
+    if a.mixed:
+        eng.add_request("mixed", prompt_ids=[200 + (j * 13) % 5000 for j in range(a.mixed)],
+                        params=SamplingParams(temperature=0.7, top_p=0.9, max_tokens=1))
+        eng._drain_inbox()
     summary, live, cap, t = measure(eng)
     summary.update(batch=a.batch, ctx=a.ctx)
     print(json.dumps(summary), flush=True)

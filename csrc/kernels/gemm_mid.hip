@@ -135,11 +135,12 @@ __global__ __launch_bounds__(256) void gemm_mid_kernel(GemmParams p) {
 // through LDS, a PAIR of m-tiles (32 rows x full K, 2 KB per k-step) at a time: the weights stay
 // in registers while the second pair is DMA'd in. The parts of a tile meet in LDS (fixed part
 // order: bit-reproducible) and the part-0 wave runs the epilogue.
-template <int MTP, int EPI, int NORM>
+template <int MT, int EPI, int NORM>
 __global__ __launch_bounds__(1024) void gemm_midw_kernel(GemmParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // x [KT][2][64][16 B] | red, ssq
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // x [KT][PH][64][16 B] | red, ssq
   TLScope tl_scope(p.dbg_ts);
-  constexpr int MT = 2 * MTP;
+  constexpr int PH = MT == 1 ? 1 : 2;  // m-tiles per x phase
+  constexpr int NPH = (MT + PH - 1) / PH;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nw = blockDim.x >> 6;
@@ -160,13 +161,13 @@ __global__ __launch_bounds__(1024) void gemm_midw_kernel(GemmParams p) {
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) ss[mt] = 0.f;
 #pragma unroll
-  for (int ph = 0; ph < MTP; ++ph) {
-    if (ph > 0) __builtin_amdgcn_s_barrier();  // every wave is done reading the previous pair
-    // x pieces of m-tiles (2 ph, 2 ph + 1): piece f = (k-step f >> 1, m-tile 2 ph + (f & 1))
-    for (int f = wid; f < 2 * KT; f += nw) {
-      int row = (2 * ph + (f & 1)) * 16 + (lane & 15);
+  for (int ph = 0; ph < NPH; ++ph) {
+    if (ph > 0) __builtin_amdgcn_s_barrier();  // every wave is done reading the previous phase's x
+    // x pieces of m-tiles (PH ph ..): piece f = (k-step f / PH, m-tile PH ph + f % PH)
+    for (int f = wid; f < PH * KT; f += nw) {
+      int row = (PH * ph + f % PH) * 16 + (lane & 15);
       row = row < p.M ? row : p.M - 1;
-      glds16(p.x + (size_t)row * p.lda + (size_t)(f >> 1) * 32 + 8 * (lane >> 4),
+      glds16(p.x + (size_t)row * p.lda + (size_t)(f / PH) * 32 + 8 * (lane >> 4),
              __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)f * 1024u));
     }
     if (ph == 0) {
@@ -187,22 +188,39 @@ __global__ __launch_bounds__(1024) void gemm_midw_kernel(GemmParams p) {
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         if (u < nks) {
-          const uint4 x0 = xs[((kb + u) * 2 + 0) * 64 + lane], x1 = xs[((kb + u) * 2 + 1) * 64 + lane];
-          if constexpr (NORM == 2) {
-            float f0[8], f1[8];
-            unpack8(x0, f0);
-            unpack8(x1, f1);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              ss[2 * ph] += f0[j] * f0[j];
-              ss[2 * ph + 1] += f1[j] * f1[j];
+          for (int i = 0; i < PH; ++i) {
+            if (PH * ph + i < MT) {
+              const uint4 xv = xs[((kb + u) * PH + i) * 64 + lane];
+              if constexpr (NORM == 2) {
+                float f[8];
+                unpack8(xv, f);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) ss[PH * ph + i] += f[j] * f[j];
+              }
+              acc[PH * ph + i] = mfma16(as_bf16x8(w[u]), as_bf16x8(xv), acc[PH * ph + i]);
             }
           }
-          acc[2 * ph] = mfma16(as_bf16x8(w[u]), as_bf16x8(x0), acc[2 * ph]);
-          acc[2 * ph + 1] = mfma16(as_bf16x8(w[u]), as_bf16x8(x1), acc[2 * ph + 1]);
         }
       }
     }
+  }
+  const int nsub = 4 * (lane >> 4);
+  if (KP == 1) {  // one part per tile: the epilogue straight from the accumulators
+    if (!active) return;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = mt * 16 + (lane & 15);
+      f32x4 v[1] = {acc[mt]};
+      if constexpr (NORM == 2) {
+        float s2 = ss[mt];
+        s2 += xor16(s2);
+        s2 += xor32(s2);
+        v[0] *= rsqrtf(s2 / (float)p.K + p.eps);
+      }
+      epilogue<1, EPI, false>(p, v, m, nt, nsub, EpiPre<1>{}, m < p.M);
+    }
+    return;
   }
   // parts meet in LDS: red [wave][mt][64] f32x4, then ssq [wave][mt][16]
   __syncthreads();
@@ -222,7 +240,6 @@ __global__ __launch_bounds__(1024) void gemm_midw_kernel(GemmParams p) {
   }
   __syncthreads();
   if (!active || part != 0) return;
-  const int nsub = 4 * (lane >> 4);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int m = mt * 16 + (lane & 15);
@@ -299,7 +316,7 @@ static bool launch_midw_epi(const GemmParams& p, hipStream_t st) {
   if (KT > 64 || KP * tmax > 16 || ntiles < nb) return false;
   const int MT = (p.M + 15) / 16;
   const dim3 grid(nb), block(64 * KP * tmax);
-  const size_t lds = std::max<size_t>((size_t)KT * 2 * 1024, (size_t)KP * tmax * (4 * 1024 + 4 * 64));
+  const size_t lds = std::max<size_t>((size_t)KT * (MT == 1 ? 1 : 2) * 1024, (size_t)KP * tmax * MT * (1024 + 64));
   GemmParams q = p;
   if (q.dbg_ts == nullptr) q.dbg_ts = tl_take("gemm_midw", nb);
 #define VG_MW(P_)                                                                                      \
@@ -311,14 +328,18 @@ static bool launch_midw_epi(const GemmParams& p, hipStream_t st) {
     (void)attr;                                                                                        \
     hipLaunchKernelGGL(kern, grid, block, lds, st, q);                                                 \
   } while (0)
-  if (MT <= 2) VG_MW(1);
-  else VG_MW(2);
+  if (MT == 1) VG_MW(1);
+  else if (MT == 2) VG_MW(2);
+  else if (MT == 3) VG_MW(3);
+  else VG_MW(4);
 #undef VG_MW
   return true;
 }
 
 bool launch_gemm_mid(const GemmArgs& g, hipStream_t st) {
-  if (g.M <= 16 || g.M > 64 || g.row_idx != nullptr || g.norm_w != nullptr || g.N % 16 != 0 || g.K % 32 != 0)
+  // (the wide form also takes decode batches, M <= 16: one m-tile, one x phase)
+  if ((g.M <= 16 && g.waves != 8) || g.M > 64 || g.row_idx != nullptr || g.norm_w != nullptr || g.N % 16 != 0 ||
+      g.K % 32 != 0)
     return false;
   GemmParams p{};
   p.x = g.x; p.lda = g.lda; p.M = g.M; p.row_idx = nullptr;

@@ -1029,7 +1029,7 @@ def test_mid_gemm_all_epilogues(M, w, s_long, s_short):
     assert _rel_err(kc, kc2) < 2e-2 and _rel_err(vc, vc2) < 2e-2
 
 
-@pytest.mark.parametrize("M", [20, 32, 48, 64])
+@pytest.mark.parametrize("M", [1, 8, 16, 20, 32, 48, 64])
 @pytest.mark.parametrize("I,K", [(8960, 1536), (1000 * 8, 2048), (128, 512)])
 def test_mid_wide_gemm_silu(M, I, K):
     """The wide medium-M kernel (one block per CU owning whole tiles, K in 16-k-step parts met in
