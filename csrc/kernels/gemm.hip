@@ -159,6 +159,8 @@ void launch_gemm(const GemmArgs& g, hipStream_t st) {
 
 void launch_awq_gemm(const GemmArgs& g, hipStream_t st) {
   if (g.M <= 0) return;
+  // decode on the wide int4 kernel (one block per CU owning whole tiles): g.ntb == -8 (a decode plan)
+  if (g.ntb == -8 && launch_awq_wide(g, st)) return;
   launch_dispatch<true>(to_params(g), g, st);
 }
 

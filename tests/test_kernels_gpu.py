@@ -577,6 +577,43 @@ def test_awq_stream_multitile(ntb, M, sk):
     torch.testing.assert_close(ssp, h.float().pow(2).reshape(M, N // 16, 16).sum(-1), rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("M", [1, 8, 16])
+@pytest.mark.parametrize("N", [2 * 8960, 4096 * 2, 1024])
+def test_awq_wide_decode(M, N):
+    """The wide int4 decode kernel (gemm_awq_wide.hip, ntb = -8: one block per CU owning whole tiles,
+    x and the packed scales staged once per CU) == the dequantised fp32 reference: plain + residual,
+    SiLU pairs, and the RMSNorm hand-off consumer (x = h * gamma, row scale from the producer's
+    per-tile sums of squares); 4-5 tiles per block with idle waves (N = 17920), 2 per block, and
+    fewer tiles than CUs."""
+    torch.manual_seed(400 + M + N)
+    C = ops.native()
+    ws = ops.workspace(torch.device(DEV))
+    K, g = 1536, 128
+    q = torch.randint(0, 16, (N, K), dtype=torch.int32)
+    scales = (torch.rand(K // g, N) * 0.02 + 0.005).bfloat16()
+    zeros = torch.randint(0, 16, (K // g, N)).float().bfloat16()
+    wd = ref.awq_dequant_ref(q, scales, zeros, g).to(DEV)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    res = torch.randn(M, N, device=DEV).bfloat16()
+    awq = {"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV), "group": g}
+    lin = ops.Linear(None, awq=dict(awq))
+    kw = dict(ws=ws, awq_scales=lin.scales, awq_zeros=lin.zeros, group=g, awq_szp=lin.szp)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    C.gemm(x, lin.wp, N, K, out, 0, res=res, ntb=-8, **kw)
+    assert _rel_err(out, ref.linear_ref(x, wd, None, res)) < 2e-2
+    # hand-off consumer: x = hg = bf16(h * gamma) with the producer's per-16-column sums of h^2
+    silu = ops.Linear(None, awq=dict(awq, silu=True))
+    h = torch.randn(M, K, device=DEV).bfloat16()
+    gamma = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+    hg = (h.float() * gamma.float()).bfloat16()
+    ssp = h.float().pow(2).reshape(M, K // 16, 16).sum(-1).contiguous()
+    ys = torch.empty(M, N // 2, device=DEV, dtype=torch.bfloat16)
+    C.gemm(hg, silu.wp, N, K, ys, 2, eps=1e-6, ntb=-8, ssp_in=ssp,
+           **dict(kw, awq_scales=silu.scales, awq_zeros=silu.zeros, awq_szp=silu.szp))
+    xn, _ = ref.rmsnorm_ref(h, gamma, 1e-6)
+    assert _rel_err(ys, ref.silu_mul_linear_ref(xn, wd[: N // 2], wd[N // 2:])) < 2e-2
+
+
 @pytest.mark.parametrize("M", [40, 256])
 def test_awq_prefill_dequant_path(M):
     """Long AWQ steps: int4 -> bf16 fragment-packed scratch (gamma folded) + the bf16 prefill /

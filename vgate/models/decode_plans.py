@@ -24,6 +24,11 @@ PLANS: dict[tuple[int, int, str, str], tuple[int, int, int]] = {
     # k-quads) instead of the K-split awq_gemm_kernel, down_proj in 8 K slices of 4 waves
     (2048, 1536, "qkv", "awq"): (4, 1, 1),
     (1536, 8960, "plain", "awq"): (4, 8, 1),
+    # o_proj on awq_stream_kernel too (1246.5 vs 1257.2 us), gate_up on the wide int4 kernel (one block
+    # per CU owning 4-5 whole tiles, x and scales staged once per CU: 1255.3 vs 1279.1 us;
+    # profiles/r3_awq_decode_sweep.log)
+    (1536, 1536, "plain", "awq"): (4, 1, 1),
+    (17920, 1536, "silu", "awq"): (0, 0, -8),
 }
 
 
