@@ -161,6 +161,8 @@ void launch_awq_gemm(const GemmArgs& g, hipStream_t st) {
   if (g.M <= 0) return;
   // decode on the wide int4 kernel (one block per CU owning whole tiles): g.ntb == -8 (a decode plan)
   if (g.ntb == -8 && launch_awq_wide(g, st)) return;
+  // mixed prefill + decode steps (16 < M <= 64) on the int4 medium kernel (path 2)
+  if (g.path == 2 && launch_awq_mid(g, st)) return;
   launch_dispatch<true>(to_params(g), g, st);
 }
 

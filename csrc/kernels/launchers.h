@@ -68,6 +68,9 @@ bool launch_gemm_mid(const GemmArgs& g, hipStream_t st);
 // AWQ W4A16 decode, wide form (gemm_awq_wide.hip: M <= 16, one block per CU owning whole tiles, x and
 // the group scales staged once per CU); returns false for a shape / mode it does not take
 bool launch_awq_wide(const GemmArgs& g, hipStream_t st);
+// AWQ W4A16 medium-M kernel (gemm_awq_wide.hip, 16 < M <= 64): g.waves tiles per block (8: one block
+// per CU owning whole tiles), g.splitk K slices; false for a shape / mode it does not take
+bool launch_awq_mid(const GemmArgs& g, hipStream_t st);
 // AWQ int4 fragments -> bf16 fragment-packed copy (optionally gamma-folded) for the prefill kernel
 void launch_awq_dequant(const void* wq, const uint16_t* scales, const uint16_t* sz, const uint16_t* gamma,
                         void* out, int N, int K, int group, hipStream_t st);

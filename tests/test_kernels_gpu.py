@@ -614,6 +614,60 @@ def test_awq_wide_decode(M, N):
     assert _rel_err(ys, ref.silu_mul_linear_ref(xn, wd[: N // 2], wd[N // 2:])) < 2e-2
 
 
+@pytest.mark.parametrize("M", [17, 40, 64])
+@pytest.mark.parametrize("w,sk", [(0, 0), (8, 0), (4, 3), (2, 6), (1, 12)])
+def test_awq_mid_gemm(M, w, sk):
+    """The int4 medium-M kernel (awq_mid_kernel, path 2: int4 fragments straight to registers, x by
+    m-tile pairs in LDS with the gamma / x^2 / activation-sum pass, wide or K-split + reduce) ==
+    the dequantised fp32 reference: plain + residual, gamma-in-registers RMSNorm + SiLU pairs (the
+    1120-tile gate_up shape), and QKV + bias + RoPE + paged KV write."""
+    torch.manual_seed(500 + M + 3 * w + sk)
+    C = ops.native()
+    ws = ops.workspace(torch.device(DEV))
+    K, g, D, BS, hq, hkv = 1536, 128, 128, 16, 12, 2
+
+    def awq_lin(N, silu=False, layout="plain", bias=None):
+        q = torch.randint(0, 16, (N, K), dtype=torch.int32)
+        scales = (torch.rand(K // g, N) * 0.02 + 0.005).bfloat16()
+        zeros = torch.randint(0, 16, (K // g, N)).float().bfloat16()
+        lin = ops.Linear(None, bias=bias, awq={"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV),
+                                               "group": g, "silu": silu, "layout": layout})
+        return lin, ref.awq_dequant_ref(q, scales, zeros, g).to(DEV)
+
+    def kw(lin):
+        return dict(ws=ws, awq_scales=lin.scales, awq_zeros=lin.zeros, group=g, awq_szp=lin.szp, path=2, waves=w,
+                    splitk=sk)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    lin, wd = awq_lin(1536)
+    res = torch.randn(M, 1536, device=DEV).bfloat16()
+    out = res.clone()
+    C.gemm(x, lin.wp, 1536, K, out, 0, res=out, **kw(lin))
+    assert _rel_err(out, ref.linear_ref(x, wd, None, res)) < 2e-2
+    nw = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+    xn, _ = ref.rmsnorm_ref(x, nw, 1e-6)
+    gu, wgu = awq_lin(2 * 8960, silu=True)
+    ys = torch.empty(M, 8960, device=DEV, dtype=torch.bfloat16)
+    C.gemm(x, gu.wp, 2 * 8960, K, ys, 2, norm_w=nw, eps=1e-6, **kw(gu))
+    assert _rel_err(ys, ref.silu_mul_linear_ref(xn, wgu[:8960], wgu[8960:])) < 2e-2
+    N = (hq + 2 * hkv) * D
+    b = (torch.randn(N, device=DEV) * 0.1).bfloat16()
+    lq, wq = awq_lin(N, layout="qkv", bias=b)
+    pos = torch.randint(0, 4096, (M,), dtype=torch.int32, device=DEV)
+    nblk = (M + BS - 1) // BS + 8
+    slots = torch.randperm(nblk * BS, device=DEV)[:M].int()
+    cs = ref.rope_cos_sin(4096, D, 1e6, device=DEV)
+    kc = torch.zeros(nblk, hkv, BS, D, device=DEV).bfloat16()
+    vc = torch.zeros_like(kc)
+    qo = torch.empty(M, hq * D, dtype=torch.bfloat16, device=DEV)
+    C.gemm(x, lq.wp, N, K, qo, 3, bias=b, norm_w=nw, eps=1e-6, positions=pos, slots=slots, cos_sin=cs, k_cache=kc,
+           v_cache=vc, hq=hq, hkv=hkv, **kw(lq))
+    qkv = ref.linear_ref(xn, wq, b)
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    ref.rope_kv_ref(qkv, pos, slots, cs, kc2, vc2, hq, hkv, D)
+    assert _rel_err(qo, qkv[:, : hq * D]) < 2e-2
+    assert _rel_err(kc, kc2) < 2e-2 and _rel_err(vc, vc2) < 2e-2
+
+
 @pytest.mark.parametrize("M", [40, 256])
 def test_awq_prefill_dequant_path(M):
     """Long AWQ steps: int4 -> bf16 fragment-packed scratch (gamma folded) + the bf16 prefill /

@@ -343,7 +343,11 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
         return _linear_library(x, lin, out, residual, norm, qkv)
     C = native()
     epi = 3 if qkv is not None else (2 if silu else (1 if out_f32 else 0))
-    if lin.kind == "awq" and M >= AWQ_DEQUANT_MIN_M and row_idx is None and waves == 0 and splitk == 0:
+    awq_mid = (lin.kind == "awq" and AWQ_MID and 16 < M <= 64 and row_idx is None and waves == 0 and splitk == 0
+               and path == 0 and lin.group == 128 and getattr(lin, "szp", None) is not None)
+    if awq_mid:
+        path = 2  # int4 medium kernel (csrc/kernels/gemm_awq_wide.hip awq_mid_kernel): no bf16 scratch
+    elif lin.kind == "awq" and M >= AWQ_DEQUANT_MIN_M and row_idx is None and waves == 0 and splitk == 0:
         return _linear_awq_dequant(x, lin, out, residual, norm, qkv, epi, M)
     ntb = 0
     if M <= 16 and waves == 0 and splitk == 0:
@@ -379,6 +383,9 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
 LIBRARY_MIN_M = int(os.environ.get("VGATE_PREFILL_BLAS_MIN_M", "128"))
 # AWQ steps with at least this many rows run dequant-to-scratch + the bf16 prefill / tile kernels
 AWQ_DEQUANT_MIN_M = int(os.environ.get("VGATE_AWQ_DEQUANT_MIN_M", "32"))
+# AWQ steps of 16 < M <= 64 rows (mixed prefill + decode) on the int4 medium kernel instead of the
+# dequantise-to-scratch path (VGATE_AWQ_MID=0: the scratch path, A/B)
+AWQ_MID = os.environ.get("VGATE_AWQ_MID", "1") != "0"
 _AWQ_SCRATCH: dict = {}
 
 
