@@ -207,7 +207,7 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
     snap = eng.backend.stats() if hasattr(eng.backend, "stats") else {}
     # timed-region forensics (p99): eager (graph-miss) steps and captures INSIDE the timed region
     snap = dict(snap)
-    for k in ("graph_misses_eager", "graph_captures", "steps", "graph_hits"):
+    for k in ("graph_misses_eager", "graph_captures", "steps", "graph_hits", "idle_ms", "prefill_steps"):
         if k in snap and k in snap0:
             snap[f"timed_{k}"] = snap[k] - snap0[k]
     server.should_exit = True
@@ -346,6 +346,11 @@ def main():
             "boot_s": round(max(r["boot_s"] for r in allr), 1),
             "max_s": round(max(lat), 4) if lat else 0.0,
             "timed_engine_steps": allr[0]["engine"].get("timed_steps"),
+            # the engine thread idle (nothing queued, no step in flight) and the steps that carried
+            # prompt tokens, over the timed region: at concurrency c the requests run in waves of c
+            # that start together, so every wave boundary waits for the next c requests' HTTP path
+            "timed_engine_idle_ms": allr[0]["engine"].get("timed_idle_ms"),
+            "timed_prefill_steps": allr[0]["engine"].get("timed_prefill_steps"),
             "timed_eager_steps": allr[0]["engine"].get("timed_graph_misses_eager"),
             "timed_graph_captures": allr[0]["engine"].get("timed_graph_captures"),
             "max_gpu_step_ms": allr[0]["engine"].get("max_gpu_step_ms"),

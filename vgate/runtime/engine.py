@@ -67,6 +67,14 @@ class EngineConfig:
     # graphs instead of running eagerly (eager steps were the p99 tail: profiles/r2_bench*.log)
     warmup_max_tokens: int = 512
     warmup_max_seqs: int = 16
+    # Admission window of an IDLE engine (no sequence running, no step in flight): the first request
+    # to arrive waits until no further request has arrived for `idle_batch_gap_ms` (at most
+    # `idle_batch_window_ms` in all, or until max_num_seqs are queued), so requests that arrive
+    # together — a closed-loop client's next wave — are prefilled in ONE step instead of one step per
+    # arrival (each extra prompt step costs ~2 ms on the decode weights; bench.py
+    # timed_prefill_steps). A running engine never waits: new requests join the next step.
+    idle_batch_window_ms: float = float(os.environ.get("VGATE_IDLE_BATCH_WINDOW_MS", "3.0"))
+    idle_batch_gap_ms: float = float(os.environ.get("VGATE_IDLE_BATCH_GAP_MS", "0.6"))
     # GPU: time the prefill GEMM decompositions per layer shape and token bucket >= 128 at start-up
     # (ops.tune_prefill) instead of relying on the launcher's heuristic alone
     prefill_autotune: bool = os.environ.get("VGATE_PREFILL_AUTOTUNE", "1") != "0"
@@ -98,6 +106,8 @@ class EngineStats:
     max_cycle_ms: float = 0.0  # slowest schedule -> launch -> collect cycle and its (T, S) bucket
     max_cycle_bucket: tuple = (0, 0)
     batch_sizes: collections.Counter = field(default_factory=collections.Counter)
+    idle_s: float = 0.0        # engine thread waiting for work (no step in flight, nothing queued)
+    prefill_steps: int = 0     # steps that carried prompt tokens (mixed or prefill-only)
 
 
 class LLMEngine:
@@ -272,6 +282,28 @@ class LLMEngine:
                 seq.aborted = True
                 self._finish(seq, "abort", notify_sched=False)
 
+    def _coalesce_arrivals(self) -> None:
+        """Called with the condition held: when the engine has nothing running and requests just
+        arrived, give the rest of an arriving burst ``idle_batch_gap_ms`` (since the latest arrival)
+        to join, up to ``idle_batch_window_ms`` in all (EngineConfig)."""
+        win, gap = self.cfg.idle_batch_window_ms, self.cfg.idle_batch_gap_ms
+        if (win <= 0 or gap <= 0 or not self._inbox or self._inflight is not None or self._calls
+                or self.scheduler.has_work() or self.ring is not None):
+            return
+        t0 = time.perf_counter()
+        t_end = t0 + 1e-3 * win
+        cap = self.cfg.max_num_seqs
+        n = len(self._inbox)
+        while self._running and n < cap:
+            now = time.perf_counter()
+            if now >= t_end:
+                break
+            self._cv.wait(timeout=min(1e-3 * gap, t_end - now))
+            if len(self._inbox) == n:
+                break  # nobody arrived within the gap
+            n = len(self._inbox)
+        self.stats.idle_s += time.perf_counter() - t0
+
     def _idle(self) -> bool:
         return (not self._inbox and not self._aborts and not self.scheduler.has_work() and self._inflight is None
                 and not self._calls)
@@ -300,11 +332,14 @@ class LLMEngine:
                 while self._running and self._idle() and not self.runner.pending_captures:
                     if self.ring is not None:  # an idle TP group must not look dead to its followers
                         self.ring.heartbeat()
+                    t_idle = time.perf_counter()
                     self._cv.wait(timeout=0.5)
+                    self.stats.idle_s += time.perf_counter() - t_idle
                 if self._idle():
                     continue  # idle with captures pending: back to the capture check
                 if not self._running:
                     break
+                self._coalesce_arrivals()
                 self._drain_inbox()
             if self._calls:
                 self._run_calls()
@@ -452,6 +487,7 @@ class LLMEngine:
             st.max_cycle_ms = cyc
             st.max_cycle_bucket = (batch.num_tokens, len(batch.items))
         st.prefill_tokens += batch.num_prefill_tokens
+        st.prefill_steps += batch.num_prefill_tokens > 0
         st.decode_tokens += batch.num_decode
         st.batch_sizes[len(batch.items)] += 1
         self.last_step_wall = time.monotonic()
@@ -652,6 +688,7 @@ class LLMEngine:
             "avg_cycle_ms": round(1e3 * st.cycle_time_s / max(1, st.steps), 3),
             "avg_gpu_ms": round(self.runner.gpu_ms / max(1, self.runner.gpu_steps), 3),
             "avg_host_ms": round(self.runner.host_ms / max(1, st.steps), 3),
+            "idle_ms": round(1e3 * st.idle_s, 3), "prefill_steps": st.prefill_steps,
             "graphs_captured": len(self.runner.graphs), "graph_hits": self.runner.graph_hits,
             "graph_misses_eager": self.runner.graph_misses,
             "pending_captures": len(self.runner.pending_captures),
