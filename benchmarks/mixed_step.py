@@ -60,6 +60,8 @@ def main():
     ap.add_argument("--prompts", default="16,32,48,64,128")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--quantization", default=None)
+    ap.add_argument("--burst", type=int, default=0, help="instead: time ONE step prefilling this many prompts "
+                    "of --prompts[0] tokens together (a closed-loop wave's arrival), beside the decode rows")
     ap.add_argument("--medium", default="tuned", choices=["tuned", "mid", "default", "wide"],
                     help="medium-bucket GEMM plans (16 < M < 128): the start-up tuner's, the medium-M kernel "
                          "(its heuristic decomposition) everywhere, or the default path everywhere")
@@ -92,7 +94,20 @@ def main():
     for k in list(eng.runner.graphs):
         del eng.runner.graphs[k]
     key, us = time_graph(eng, a.iters)
-    print(json.dumps({"case": "decode", "rows": a.batch - 1, "bucket": key, "step_us": round(us, 1)}), flush=True)
+    if us is not None:
+        print(json.dumps({"case": "decode", "rows": a.batch - 1, "bucket": key, "step_us": round(us, 1)}), flush=True)
+    if a.burst:
+        P = int(a.prompts.split(",")[0])
+        for n in range(a.burst):
+            ids = [300 + (n * 97 + j * 13) % 5000 for j in range(P)]
+            eng.add_request(f"b{n}", prompt_ids=ids, params=SamplingParams(temperature=0.7, top_p=0.9, max_tokens=1))
+        eng._drain_inbox()
+        for k in list(eng.runner.graphs):
+            del eng.runner.graphs[k]
+        key, us = time_graph(eng, a.iters)
+        print(json.dumps({"case": "burst", "prompts": a.burst, "prompt_len": P, "decode_rows": a.batch - 1,
+                          "bucket": key, "step_us": None if us is None else round(us, 1)}), flush=True)
+        return
     for n, P in enumerate(int(x) for x in a.prompts.split(",")):
         ids = [200 + (n * 71 + j * 13) % 5000 for j in range(P)]
         eng.add_request(f"p{n}", prompt_ids=ids, params=SamplingParams(temperature=0.7, top_p=0.9, max_tokens=1))
