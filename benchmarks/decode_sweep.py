@@ -38,12 +38,12 @@ CANDIDATES = {
 # int4 (AWQ) layers: ntb >= 1 routes qkv / o_proj to awq_stream_kernel (packed scales, XP-packed
 # activations) instead of the K-split awq_gemm_kernel; ntb -2 forces the latter
 CANDIDATES_AWQ = {
-    "qkv": [(0, 0, 0), (0, 0, -8), (4, 1, 1), (6, 1, 1), (8, 1, 1), (2, 1, 1), (3, 1, 1), (12, 1, 1), (2, 2, 1),
+    "qkv": [(0, 0, 0), (4, 1, -9), (2, 1, -9), (1, 1, -9), (4, 2, -9), (2, 2, -9), (0, 0, -8), (4, 1, 1), (6, 1, 1), (8, 1, 1), (2, 1, 1), (3, 1, 1), (12, 1, 1), (2, 2, 1),
             (4, 2, 1)],
-    "o": [(0, 0, 0), (0, 0, -8), (4, 1, 1), (6, 1, 1), (8, 1, 1), (2, 1, 1), (3, 1, 1), (2, 2, 1), (4, 2, 1)],
+    "o": [(0, 0, 0), (4, 1, -9), (2, 1, -9), (1, 1, -9), (4, 2, -9), (2, 2, -9), (0, 0, -8), (4, 1, 1), (6, 1, 1), (8, 1, 1), (2, 1, 1), (3, 1, 1), (2, 2, 1), (4, 2, 1)],
     "gate_up": [(0, 0, 0), (0, 0, -8), (0, 0, 1), (0, 0, 4), (2, 1, 2), (4, 1, 2), (1, 1, 2), (0, 2, 2), (3, 1, 1),
                 (2, 1, 1)],
-    "down": [(0, 0, 0), (0, 2, 1), (0, 8, 1), (6, 4, 1), (2, 8, 1), (4, 8, 1), (4, 4, 1), (2, 4, 1), (8, 2, 1),
+    "down": [(0, 0, 0), (4, 5, -9), (4, 10, -9), (2, 5, -9), (2, 10, -9), (1, 5, -9), (0, 2, 1), (0, 8, 1), (6, 4, 1), (2, 8, 1), (4, 8, 1), (4, 4, 1), (2, 4, 1), (8, 2, 1),
              (0, 5, 1), (0, 7, 1)],
     "lm_head": [(0, 0, 0)],
 }

@@ -264,6 +264,15 @@ __global__ __launch_bounds__(512) void awq_mid_kernel(GemmParams p, int wide) { 
     if constexpr (NORM == 1)
       for (int kq = 0; kq < nkq; ++kq) ssr[mt] += ssp[(kq * MT + mt) * 16 + r16];  // fixed k-quad order
   }
+  if constexpr (NORM == 3) {  // the producer's hand-off: x = h * gamma, rows' sums of squares in ssp_in
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      float ss = prenorm_ss(p, mt * 16 + r16, lane >> 4);
+      ss += xor16(ss);
+      ss += xor32(ss);
+      acc[mt] *= rsqrtf(ss / (float)p.K + p.eps);  // a per-row constant: exact on each K slice's partial
+    }
+  }
   if (S > 1) {
     float* part = p.slabs + (size_t)z * p.M * p.N;
     float* ssq = p.slabs + (size_t)S * p.M * p.N + (size_t)z * p.M;
@@ -341,7 +350,8 @@ static bool launch_awq_mid_epi(const GemmParams& p, int force_w, int force_s, si
     else if (nkq <= 12) VG_AM(MT_, 12); \
     else VG_AM(MT_, 16);                \
   } while (0)
-  if (MT <= 2) VG_AMQ(2);
+  if (MT == 1) VG_AMQ(1);
+  else if (MT == 2) VG_AMQ(2);
   else if (MT == 3) VG_AMQ(3);
   else VG_AMQ(4);
 #undef VG_AMQ
@@ -351,8 +361,9 @@ static bool launch_awq_mid_epi(const GemmParams& p, int force_w, int force_s, si
 }
 
 bool launch_awq_mid(const GemmArgs& g, hipStream_t st) {
-  if (g.M <= 16 || g.M > 64 || g.awq_szp == nullptr || g.group != 128 || g.N % 16 != 0 || g.K % 128 != 0 ||
-      g.rownorm || g.ssp_in != nullptr || g.row_idx != nullptr)
+  // (decode batches too, M <= 16, when a decode plan asks for it: the hand-off consumer mode included)
+  if (g.M <= 0 || g.M > 64 || g.awq_szp == nullptr || g.group != 128 || g.N % 16 != 0 || g.K % 128 != 0 ||
+      g.rownorm || (g.ssp_in != nullptr && g.norm_w != nullptr) || g.row_idx != nullptr)
     return false;
   GemmParams p{};
   p.x = g.x; p.lda = g.lda; p.M = g.M; p.row_idx = nullptr;
@@ -366,9 +377,12 @@ bool launch_awq_mid(const GemmArgs& g, hipStream_t st) {
   p.k_cache = g.k_cache; p.v_cache = g.v_cache; p.hq = g.hq; p.hkv = g.hkv; p.bs = g.bs;
   p.szp = g.awq_szp; p.group = g.group;
   p.dbg_ts = g.dbg_ts;
-  const bool gam = g.norm_w != nullptr;
-#define VG_AMD(E) \
-  return gam ? launch_awq_mid_epi<E, 1>(p, g.waves, g.splitk, g.slab_bytes, st) : launch_awq_mid_epi<E, 0>(p, g.waves, g.splitk, g.slab_bytes, st)
+  p.hg = g.hg; p.hg_gamma = g.hg_gamma; p.ssp_out = g.ssp_out; p.ssp_in = g.ssp_in; p.ssn = g.ssn;
+  const bool gam = g.norm_w != nullptr, pre = g.ssp_in != nullptr;
+#define VG_AMD(E)                                                                  \
+  return gam ? launch_awq_mid_epi<E, 1>(p, g.waves, g.splitk, g.slab_bytes, st)    \
+       : pre ? launch_awq_mid_epi<E, 3>(p, g.waves, g.splitk, g.slab_bytes, st)    \
+             : launch_awq_mid_epi<E, 0>(p, g.waves, g.splitk, g.slab_bytes, st)
   switch (g.epi) {
     case EPI_SILU: VG_AMD(EPI_SILU);
     case EPI_QKV: VG_AMD(EPI_QKV);

@@ -668,6 +668,55 @@ def test_awq_mid_gemm(M, w, sk):
     assert _rel_err(kc, kc2) < 2e-2 and _rel_err(vc, vc2) < 2e-2
 
 
+@pytest.mark.parametrize("M", [1, 8, 16])
+@pytest.mark.parametrize("w,sk", [(4, 1), (2, 3), (1, 5)])
+def test_awq_mid_gemm_decode_modes(M, w, sk):
+    """The int4 medium kernel at decode M (a decode plan's ops.AWQ_MID_DECODE): the RMSNorm hand-off
+    consumer (x = h * gamma, row scale from the producer's per-tile sums, applied to each K slice's
+    partial) and producer (residual GEMM writing hg / per-tile sums of h^2), plain + residual over
+    a long K — against the dequantised fp32 reference."""
+    torch.manual_seed(600 + M + 7 * w + sk)
+    C = ops.native()
+    ws = ops.workspace(torch.device(DEV))
+    g = 128
+
+    def awq_lin(N, K, silu=False):
+        q = torch.randint(0, 16, (N, K), dtype=torch.int32)
+        scales = (torch.rand(K // g, N) * 0.02 + 0.005).bfloat16()
+        zeros = torch.randint(0, 16, (K // g, N)).float().bfloat16()
+        lin = ops.Linear(None, awq={"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV), "group": g,
+                                    "silu": silu})
+        return lin, ref.awq_dequant_ref(q, scales, zeros, g).to(DEV)
+
+    def kw(lin):
+        return dict(ws=ws, awq_scales=lin.scales, awq_zeros=lin.zeros, group=g, awq_szp=lin.szp, path=2, waves=w,
+                    splitk=sk)
+    K = 1536
+    h = torch.randn(M, K, device=DEV).bfloat16()
+    gamma = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+    hg = (h.float() * gamma.float()).bfloat16()
+    ssp = h.float().pow(2).reshape(M, K // 16, 16).sum(-1).contiguous()
+    gu, wgu = awq_lin(2 * 1024, K, silu=True)
+    ys = torch.empty(M, 1024, device=DEV, dtype=torch.bfloat16)
+    C.gemm(hg, gu.wp, 2 * 1024, K, ys, 2, eps=1e-6, ssp_in=ssp, **kw(gu))
+    xn, _ = ref.rmsnorm_ref(h, gamma, 1e-6)
+    assert _rel_err(ys, ref.silu_mul_linear_ref(xn, wgu[:1024], wgu[1024:])) < 2e-2
+    # producer: down_proj class (K = 5 x 1024), residual + hand-off of the next RMSNorm
+    K2, N = 5120, 1536
+    lin, wd = awq_lin(N, K2)
+    x = torch.randn(M, K2, device=DEV).bfloat16()
+    res = torch.randn(M, N, device=DEV).bfloat16()
+    out = res.clone()
+    g2 = (torch.rand(N, device=DEV) + 0.5).bfloat16()
+    hg2 = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ssp2 = torch.empty(M, N // 16, dtype=torch.float32, device=DEV)
+    C.gemm(x, lin.wp, N, K2, out, 0, res=out, hg_out=hg2, hg_gamma=g2, ssp_out=ssp2, **kw(lin))
+    want = ref.linear_ref(x, wd, None, res)
+    assert _rel_err(out, want) < 2e-2
+    assert torch.equal(hg2, (out.float() * g2.float()).bfloat16())
+    torch.testing.assert_close(ssp2, out.float().pow(2).reshape(M, N // 16, 16).sum(-1), rtol=1e-5, atol=1e-4)
+
+
 @pytest.mark.parametrize("M", [40, 256])
 def test_awq_prefill_dequant_path(M):
     """Long AWQ steps: int4 -> bf16 fragment-packed scratch (gamma folded) + the bf16 prefill /

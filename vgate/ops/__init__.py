@@ -354,6 +354,8 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
         waves, splitk, ntb = lin.dec_waves, lin.dec_splitk, lin.dec_ntb
         if ntb == WIDE_DECODE and lin.kind == "dense":  # the wide medium kernel (gemm_mid.hip) at decode M
             waves, splitk, ntb, path = 8, 0, 0, 2
+        elif ntb == AWQ_MID_DECODE and lin.kind == "awq":  # the int4 medium kernel at decode M (waves, K slices)
+            ntb, path = 0, 2
     elif M > 16 and waves == 0 and splitk == 0 and path == 0 and lin.prefill_plan and lin.kind == "dense":  # (AWQ: below)
         pk = _plan_kw(lin.prefill_plan.get(_plan_bucket(lin.prefill_plan, M)), M)
         ntb, splitk, path, waves = pk.get("ntb", 0), pk.get("splitk", 0), pk.get("path", 0), pk.get("waves", 0)
@@ -660,6 +662,7 @@ PREFILL_CANDIDATES = [(0, 0), (64, 0), (128, 0), (128, 2), (128, 4), (256, 0), (
 # MID_BASE - W (W tiles = waves per block) and K slices (0 = its heuristic)
 MID_BASE = -10
 WIDE_DECODE = -8  # Linear.dec_ntb: decode steps (M <= 16) on the wide medium kernel
+AWQ_MID_DECODE = -9  # Linear.dec_ntb of an AWQ layer: decode steps on the int4 medium kernel
 MID_CANDIDATES = [(MID_BASE - w, s) for w in (4, 2) for s in (0, 2, 3, 4, 6, 8, 10, 12, 16)] + [(MID_BASE - 8, 0)]
 _FLUSH: dict = {}
 
