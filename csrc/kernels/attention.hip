@@ -566,8 +566,11 @@ __global__ __launch_bounds__(64 * NW) void attn_flash_kernel(AttnArgs a, int laz
   const int G = a.Hq / a.Hkv;
   const int QG = NW / G;
   const int QPB = 16 * CT * QG;
-  const int h = blockIdx.y;
-  const int tile = blockIdx.x;
+  // grid (Hkv x halves, tiles): the KV heads (and a split range's two halves) of one tile are
+  // adjacent in dispatch order, so the tile list's longest-first order holds across every head
+  const int zs = gridDim.x / a.Hkv;
+  const int h = blockIdx.x / zs;
+  const int tile = blockIdx.y;
   const int s = a.tile_seq[tile];
   if (s < 0) return;
   const int q0 = a.tile_q0[tile];
@@ -581,6 +584,14 @@ __global__ __launch_bounds__(64 * NW) void attn_flash_kernel(AttnArgs a, int laz
   const int kv_end = ctx - qlen + qhi;       // the block's causal bound (exclusive)
   const int nch = (kv_end + FL_KV - 1) / FL_KV;
   const int nfull = max(0, ctx - qlen + q0 + 1) / FL_KV;  // chunks below every query's bound
+  // K split (two halves per KV head, launch_attention): a range of >= 4 chunks runs as two halves of whole
+  // chunks, [0, nch/2) on z = 0 and [nch/2, nch) on z = 1, met in the epilogue; the causal
+  // triangle's long tail then costs half a range per block. Block-uniform, before any barrier.
+  const int z = blockIdx.x % zs;
+  const bool split = !SWP && zs > 1 && nch >= 4;
+  if (z > 0 && !split) return;
+  const int c0 = split && z == 1 ? nch / 2 : 0;
+  const int c1 = split && z == 0 ? nch / 2 : nch;
   const int col = lane & 15, g4 = lane >> 4;
   // Q fragments (B operand of S^T = K Q^T): CT column tiles x 4 k-slices
   uint4 qf[CT][4];
@@ -636,7 +647,7 @@ __global__ __launch_bounds__(64 * NW) void attn_flash_kernel(AttnArgs a, int laz
   }
   auto issue = [&](int c) {
     const uint32_t stage = lds_addr_of(smem) + (uint32_t)((c % FL_NST) * FL_STAGE);
-    const int cc = min(c, nch - 1);
+    const int cc = min(c, c1 - 1);
     int pg[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) pg[j] = __builtin_amdgcn_readfirstlane(s_bt[min(4 * cc + j, npg - 1)]);  // past the bound: the last page
@@ -739,13 +750,13 @@ __global__ __launch_bounds__(64 * NW) void attn_flash_kernel(AttnArgs a, int laz
     }
   };
   if constexpr (!SWP) {
-    if (nch > 0) {
+    if (c1 > c0) {
 #pragma unroll
-      for (int c = 0; c < FL_NST - 1; ++c) issue(c);
+      for (int c = 0; c < FL_NST - 1; ++c) issue(c0 + c);
     }
-    __builtin_amdgcn_s_waitcnt(vm_imm((FL_NST - 2) * P));  // chunk 0 landed (this wave's pieces)
+    __builtin_amdgcn_s_waitcnt(vm_imm((FL_NST - 2) * P));  // chunk c0 landed (this wave's pieces)
     __builtin_amdgcn_s_barrier();                          // everyone's
-    for (int c = 0; c < nch; ++c) {
+    for (int c = c0; c < c1; ++c) {
       issue(c + FL_NST - 1);  // into the stage every wave finished reading last iteration
       f32x4 st[4][CT];
       bf16x8 pb[CT][2];
@@ -783,6 +794,103 @@ __global__ __launch_bounds__(64 * NW) void attn_flash_kernel(AttnArgs a, int laz
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the look-ahead DMAs drained before the block exits
+  if (split) {
+    // The two halves meet per wave. Each rounds its partial to bf16 normalised by its own sum
+    // (o / l) with (m, l) in fp32 and takes the wave's ticket; the first arriver publishes that
+    // (16-B sc1 stores, drain, ready flag) and exits, the second waits for the flag (the first
+    // never waits, so it always gets there), re-arms both words and merges the two ROUNDED
+    // partials in fixed half order: the result does not depend on which half came first. Slot:
+    // the leader's rank over the step (every earlier sequence holds ceil(qlen / QPB) leaders),
+    // KV head, wave; the host sized fl_ws for (tiles 16 / QPB + S + 1) Hkv NW <= 32768 slots.
+    int before = 0;
+    for (int i = lane; i < s; i += 64) {
+      const int ql = a.query_start[i + 1] - a.query_start[i];
+      before += (ql + QPB - 1) / QPB;
+    }
+#pragma unroll
+    for (int sh = 32; sh > 0; sh >>= 1) before += __shfl_xor(before, sh);
+    const uint32_t wslot = (uint32_t)(((before + q0 / QPB) * a.Hkv + h) * NW + wid);
+    uint32_t* ticket = a.fl_tickets + wslot;
+    uint32_t* ready = a.fl_tickets + 32768 + wslot;
+    float ll[CT];
+    uint4 pw[CT][4];  // this half's o / l, bf16, mt pairs
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      ll[ct] = l[ct];
+      ll[ct] += xor16(ll[ct]);
+      ll[ct] += xor32(ll[ct]);
+      const float inv = ll[ct] > 0.f ? 1.f / ll[ct] : 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const f32x4 x0 = o[ct][2 * w], x1 = o[ct][2 * w + 1];
+        pw[ct][w] = make_uint4(pack_bf2(x0[0] * inv, x0[1] * inv), pack_bf2(x0[2] * inv, x0[3] * inv),
+                               pack_bf2(x1[0] * inv, x1[1] * inv), pack_bf2(x1[2] * inv, x1[3] * inv));
+      }
+    }
+    constexpr uint32_t PW = CT * 4 + 1;  // 16-B words per lane: the bf16 partial, then (m, l) pairs
+    const uint32_t slot_off = wslot * PW * 1024u + lane * 16u;
+    uint32_t old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __shfl(old, 0);
+    if (old == 0) {
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+          st_sc1_x4(a.fl_ws, slot_off + (uint32_t)(ct * 4 + w) * 1024u, __builtin_bit_cast(f32x4, pw[ct][w]));
+      st_sc1_x4(a.fl_ws, slot_off + CT * 4 * 1024u, f32x4{m[0], ll[0], m[CT - 1], ll[CT - 1]});
+      drain_stores();
+      if (lane == 0) __hip_atomic_store(ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (lane == 0) {
+      uint32_t spins = 0;
+      while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 22)) break;  // bounded: never hang the GPU (the result is then wrong)
+      }
+      __hip_atomic_store(ready, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("" ::: "memory");  // the partial's loads stay behind the flag
+    uint4 qb[CT][4];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+        qb[ct][w] = __builtin_bit_cast(uint4, ld_sc1_x4(a.fl_ws, slot_off + (uint32_t)(ct * 4 + w) * 1024u));
+    const f32x4 mlb = ld_sc1_x4(a.fl_ws, slot_off + CT * 4 * 1024u);
+    auto lo_f = [](uint32_t u) { return __uint_as_float(u << 16); };
+    auto hi_f = [](uint32_t u) { return __uint_as_float(u & 0xffff0000u); };
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const float mo = ct == 0 ? mlb[0] : mlb[2], lo = ct == 0 ? mlb[1] : mlb[3];
+      const float m0 = z == 0 ? m[ct] : mo, m1 = z == 0 ? mo : m[ct];
+      const float l0 = z == 0 ? ll[ct] : lo, l1 = z == 0 ? lo : ll[ct];
+      const float mm = fmaxf(m0, m1);
+      const float mref = mm == -INFINITY ? 0.f : mm;
+      const float a0 = __builtin_amdgcn_exp2f(m0 - mref) * l0, a1 = __builtin_amdgcn_exp2f(m1 - mref) * l1;
+      const float lt = a0 + a1;
+      const float w0 = lt > 0.f ? a0 / lt : 0.f, w1 = lt > 0.f ? a1 / lt : 0.f;
+      const int qi = qw0 + 16 * ct + col;
+      if (qi >= qhi) continue;
+      const size_t orow = (size_t)(qs + qi) * a.out_stride + (size_t)hq * D_;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const uint4 p0 = z == 0 ? pw[ct][w] : qb[ct][w], p1 = z == 0 ? qb[ct][w] : pw[ct][w];
+        const uint32_t u0[4] = {p0.x, p0.y, p0.z, p0.w}, u1[4] = {p1.x, p1.y, p1.z, p1.w};
+#pragma unroll
+        for (int hmt = 0; hmt < 2; ++hmt) {
+          uint2 pk;
+          pk.x = pack_bf2(lo_f(u0[2 * hmt]) * w0 + lo_f(u1[2 * hmt]) * w1, hi_f(u0[2 * hmt]) * w0 + hi_f(u1[2 * hmt]) * w1);
+          pk.y = pack_bf2(lo_f(u0[2 * hmt + 1]) * w0 + lo_f(u1[2 * hmt + 1]) * w1,
+                          hi_f(u0[2 * hmt + 1]) * w0 + hi_f(u1[2 * hmt + 1]) * w1);
+          *reinterpret_cast<uint2*>(a.out + orow + 16 * (2 * w + hmt) + 4 * g4) = pk;
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
     float ll = l[ct];
@@ -848,6 +956,8 @@ static int attn_waves(const AttnArgs& a) {
 int g_flash_prefill = -1;  // -1: VGATE_FLASH_PREFILL (default on); 0 / 1: set_flash_prefill (tests)
 void set_flash_prefill(int on) { g_flash_prefill = on; }
 
+static int cu_count();
+
 void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
   int tiles = a.num_tiles > 0 ? a.num_tiles : 0;
   // prefill tiles on the flash kernel (its own launch; a decode-only graph bucket carries no tile
@@ -862,7 +972,18 @@ void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
     static const int swp = [] { const char* e = getenv("VGATE_FLASH_SWP"); return e ? atoi(e) : 0; }();
     const size_t lds = (size_t)(nst == 2 ? 2 : 4) * FL_STAGE + (size_t)a.max_blocks * 4;
     const size_t lds4 = (size_t)4 * FL_STAGE + (size_t)a.max_blocks * 4;
-    const dim3 grid(tiles, a.Hkv, 1), block(64 * fc.nw);
+    // K split of the long causal ranges (two halves per KV head, adjacent in grid.x) when the workspace holds every wave's partial
+    int zs = 1;
+    if (!swp && f.fl_ws != nullptr && f.fl_tickets != nullptr) {
+      const int qpb = 16 * fc.ct * (fc.nw / (a.Hq / a.Hkv));
+      const size_t leaders = (size_t)tiles * 16 / qpb + (size_t)a.S + 1;
+      const size_t slots = leaders * a.Hkv * fc.nw;
+      // only while the step's blocks do not fill the chip twice over (more blocks than that
+      // balance the causal triangle themselves; CT = 2 blocks hold a CU alone, CT = 1 two)
+      const bool few = (size_t)tiles * 16 / qpb * a.Hkv * fc.ct <= (size_t)2 * cu_count();
+      if (few && slots <= 32768 && slots * (fc.ct * 4 + 1) * 1024 <= f.fl_ws_bytes) zs = 2;
+    }
+    const dim3 grid(a.Hkv * zs, tiles, 1), block(64 * fc.nw);
 #define VG_FL(CT_, NW_)                                                                                      \
     do {                                                                                                     \
       if (swp) hipLaunchKernelGGL((attn_flash_kernel<CT_, NW_, 4, true>), grid, block, lds4, st, f, lazy);     \

@@ -165,6 +165,12 @@ struct AttnArgs {
   // profiling only: phase timestamps (s_memtime) of block (0,0,0) wave 0, or null
   unsigned long long* dbg_ts;
   unsigned long long* tl;  // launch timeline slot (set by the launcher), or null
+  // flash prefill K split (attention.hip attn_flash_kernel, two blocks per KV head): the two halves of a long
+  // causal range meet through bf16 partials + fp32 (m, l) in fl_ws and a zeroed, self-resetting
+  // ticket + ready word per (leader, KV head, wave) (fl_tickets: 65536 words); null -> no split
+  float* fl_ws = nullptr;
+  size_t fl_ws_bytes = 0;
+  uint32_t* fl_tickets = nullptr;
 };
 void launch_attn_decode(const AttnArgs& a, hipStream_t st);
 void launch_attn_prefill(const AttnArgs& a, hipStream_t st);

@@ -289,11 +289,23 @@ void attn_decode(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const
   vgate::launch_attn_decode(a, cur_stream());
 }
 
+// the flash prefill K split's workspace: the GEMM workspace (ops.workspace), 65536 zeroed
+// self-resetting tickets, then fp32 slabs; a flash launch never overlaps a GEMM on the stream
+static void set_flash_ws(vgate::AttnArgs& a, const c10::optional<Tensor>& flash_ws) {
+  if (!flash_ws.has_value() || !flash_ws->defined()) return;
+  CHECK_DEV(*flash_ws); CHECK_DT(*flash_ws, torch::kInt32);
+  TORCH_CHECK(flash_ws->numel() > 65536, "attention: flash_ws is the GEMM workspace");
+  a.fl_tickets = reinterpret_cast<uint32_t*>(flash_ws->data_ptr());
+  a.fl_ws = reinterpret_cast<float*>(flash_ws->data_ptr()) + 65536;
+  a.fl_ws_bytes = (size_t)(flash_ws->numel() - 65536) * 4;
+}
+
 void attn_prefill(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const Tensor& v_cache,
                   const Tensor& block_tables, const Tensor& context_lens,
                   const Tensor& query_start, const Tensor& tile_seq, const Tensor& tile_q0,
-                  Tensor& out, int64_t Hq, int64_t Hkv, double scale) {
+                  Tensor& out, int64_t Hq, int64_t Hkv, double scale, const c10::optional<Tensor>& flash_ws) {
   auto a = attn_common(q, q_stride, k_cache, v_cache, block_tables, context_lens, out, Hq, Hkv, scale);
+  set_flash_ws(a, flash_ws);
   CHECK_DT(query_start, torch::kInt32); CHECK_DT(tile_seq, torch::kInt32); CHECK_DT(tile_q0, torch::kInt32);
   a.query_start = reinterpret_cast<const int32_t*>(query_start.data_ptr());
   a.tile_seq = reinterpret_cast<const int32_t*>(tile_seq.data_ptr());
@@ -307,8 +319,10 @@ void attention(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const T
                const Tensor& block_tables, const Tensor& context_lens, const Tensor& query_start,
                const Tensor& tile_seq, const Tensor& tile_q0, Tensor& out, Tensor& part_o, Tensor& part_ml,
                int64_t Hq, int64_t Hkv, int64_t part_size, double scale, int64_t out_stride,
-               const c10::optional<Tensor>& tickets, const c10::optional<Tensor>& dbg_ts) {
+               const c10::optional<Tensor>& tickets, const c10::optional<Tensor>& dbg_ts,
+               const c10::optional<Tensor>& flash_ws) {
   auto a = attn_common(q, q_stride, k_cache, v_cache, block_tables, context_lens, out, Hq, Hkv, scale);
+  set_flash_ws(a, flash_ws);
   if (out_stride > 0) a.out_stride = (int)out_stride;
   CHECK_DT(query_start, torch::kInt32); CHECK_DT(tile_seq, torch::kInt32); CHECK_DT(tile_q0, torch::kInt32);
   CHECK_DT(part_o, torch::kFloat32); CHECK_DT(part_ml, torch::kFloat32);
@@ -583,7 +597,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),
         py::arg("part_o"), py::arg("part_ml"), py::arg("Hq"), py::arg("Hkv"), py::arg("part_size"), py::arg("scale"),
-        py::arg("out_stride") = 0, py::arg("tickets") = py::none(), py::arg("dbg_ts") = py::none());
+        py::arg("out_stride") = 0, py::arg("tickets") = py::none(), py::arg("dbg_ts") = py::none(),
+        py::arg("flash_ws") = py::none());
   m.def("attention_o", &attention_o, "decode attention + o_proj GEMM (+residual) as one launch; false = not fused",
         py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),
@@ -601,7 +616,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("gamma") = py::none());
   m.def("silu_mul", &silu_mul, "out = silu(y[:, :I]) * y[:, I:] (library gate_up epilogue)");
   m.def("attn_decode", &attn_decode, "paged split-K decode attention");
-  m.def("attn_prefill", &attn_prefill, "paged varlen causal prefill attention");
+  m.def("attn_prefill", &attn_prefill, "paged varlen causal prefill attention",
+        py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
+        py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),
+        py::arg("Hq"), py::arg("Hkv"), py::arg("scale"), py::arg("flash_ws") = py::none());
   m.def("sample", &sample, "temperature/top-k/top-p sampling (segmented Gumbel-max + exact rejection)",
         py::arg("logits"), py::arg("temperature"), py::arg("top_p"), py::arg("top_k"), py::arg("seeds"),
         py::arg("offsets"), py::arg("out"), py::arg("out_logprob") = py::none(), py::arg("ws") = py::none());

@@ -1500,5 +1500,16 @@ def test_flash_prefill_matches_tile_kernel_and_reference(Hq, Hkv):
         out = torch.zeros(T, Hq * D, device=DEV).bfloat16()
         ops.attention(qkv, stride, kc, vc, bt, cl, qs, ts, tq, out, po, pml, Hq, Hkv, 512, scale)
         assert _rel_err(out.view(T, Hq, D), r) < 2e-2
+        # the K split (ranges of >= 4 chunks as two halves met through the workspace, ctx 300 / 456
+        # here) is deterministic and matches the unsplit kernel
+        assert ops.FLASH_SPLIT
+        out2 = torch.zeros_like(out)
+        ops.attention(qkv, stride, kc, vc, bt, cl, qs, ts, tq, out2, po, pml, Hq, Hkv, 512, scale)
+        assert torch.equal(out, out2)
+        ops.FLASH_SPLIT = False
+        out3 = torch.zeros_like(out)
+        ops.attention(qkv, stride, kc, vc, bt, cl, qs, ts, tq, out3, po, pml, Hq, Hkv, 512, scale)
+        assert _rel_err(out, out3) < 1e-2
     finally:
+        ops.FLASH_SPLIT = True
         C.set_flash_prefill(-1)

@@ -463,6 +463,11 @@ def _linear_library(x, lin: Linear, out, residual, norm, qkv):
     return out
 
 
+# flash prefill: long causal ranges run as two K halves met through fp32 partials in the GEMM
+# workspace (csrc/kernels/attention.hip attn_flash_kernel, two blocks per KV head); VGATE_FLASH_SPLIT=0 turns it off
+FLASH_SPLIT = os.environ.get("VGATE_FLASH_SPLIT", "1") != "0"
+
+
 def attention(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start, tile_seq, tile_q0, out,
               part_o, part_ml, Hq: int, Hkv: int, part_size: int, scale: float, tickets=None):
     """Unified paged attention for a mixed step (decode rows + prefill tiles, one launch).
@@ -471,7 +476,8 @@ def attention(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_s
     if tickets is None:
         tickets = attn_tickets(q.device)
     native().attention(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start, tile_seq, tile_q0,
-                       out, part_o, part_ml, Hq, Hkv, part_size, scale, 0, tickets)
+                       out, part_o, part_ml, Hq, Hkv, part_size, scale, 0, tickets,
+                       flash_ws=workspace(q.device) if FLASH_SPLIT else None)
     return out
 
 
@@ -627,7 +633,8 @@ def attention_prefill(q, q_stride, k_cache, v_cache, block_tables, context_lens,
         out.view(T, Hq, D).copy_(o)
         return out
     native().attn_prefill(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start,
-                          tile_seq, tile_q0, out, Hq, Hkv, scale)
+                          tile_seq, tile_q0, out, Hq, Hkv, scale,
+                          flash_ws=workspace(q.device) if FLASH_SPLIT else None)
     return out
 
 
