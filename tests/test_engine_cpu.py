@@ -192,3 +192,18 @@ def test_tile_order_and_decode_only_buckets():
         T, S = r.bucket_for(nt, ns)
         assert T >= nt and S >= ns
         assert (T > S) if nt > ns else True, (nt, ns, T, S)
+    # several prompt chunks in one step: one longest-first order of every sequence's leaders
+    # (causal range = cached context + the leader's first query), then the idle tiles
+    lead = r.tile_lead
+    qlens, ctxs = [40, 1, 100], [40, 9, 300]
+    qs = np.array([0] + list(np.cumsum(qlens)), dtype=np.int32)
+    cl = np.array(ctxs, dtype=np.int32)
+    ts, tq = ops.prefill_tiles([q if q > 1 else 0 for q in qlens], lead)
+    ts, tq = np.array(ts, dtype=np.int32), np.array(tq, dtype=np.int32)
+    before = sorted(zip(ts.tolist(), tq.tolist()))
+    r._order_tiles(ts, tq, len(ts), qs, cl)
+    assert sorted(zip(ts.tolist(), tq.tolist())) == before
+    nl = int((tq % lead == 0).sum())
+    assert all(int(t) % lead == 0 for t in tq[:nl]) and all(int(t) % lead for t in tq[nl:])
+    rng = [int(cl[s] - qlens[s] + q) for s, q in zip(ts[:nl], tq[:nl])]
+    assert rng == sorted(rng, reverse=True)

@@ -182,7 +182,7 @@ def _timeout_worker(rank, port, path, q, go):
 
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-                          MASTER_PORT=str(port), VGATE_TP_TIMEOUT_S="60", VGATE_AR_SPIN_LIMIT="20000")
+                          MASTER_PORT=str(port), VGATE_TP_TIMEOUT_S="60", VGATE_AR_SPIN_LIMIT="200000")
         import torch.distributed as dist
 
         from vgate.runtime.engine import LLMEngine

@@ -173,6 +173,7 @@ class ModelRunner:
         bt = m.bt_host
         t = 0
         ntile = 0
+        npre = 0
         samples = []
         qs[0] = 0
         for s, (seq, n) in enumerate(batch.items):
@@ -208,6 +209,7 @@ class ModelRunner:
                     tseq[ntile: ntile + k] = s
                     tq0[ntile: ntile + k] = order
                 ntile += k
+                npre += 1
             sp = seq.params
             temp[s] = 0.0 if sp.greedy else sp.temperature
             topp[s] = sp.top_p
@@ -229,9 +231,23 @@ class ModelRunner:
         tile_cap = self.meta.tile_cap(T, S)
         if ntile > tile_cap:
             raise RuntimeError("prefill tile overflow")
+        if npre > 1:
+            self._order_tiles(tseq, tq0, ntile, qs, cl)
         tseq[ntile:tile_cap] = -1
         self._n_tok, self._n_seq = t, ns
         return samples
+
+    def _order_tiles(self, tseq, tq0, ntile, qs, cl) -> None:
+        """One longest-first tile order over the whole step (several prompt chunks): the flash
+        kernel dispatches tiles in list order (csrc/kernels/attention.hip attn_flash_kernel, grid
+        (KV heads x halves, tiles)), so every sequence's working blocks (lead-query group
+        leaders) go first by causal range, then the tiles that exit at once."""
+        ts, tq = tseq[:ntile].copy(), tq0[:ntile].copy()
+        kv = cl[ts] - (qs[ts + 1] - qs[ts]) + tq  # context before the tile's first query
+        key = np.where(tq % self.tile_lead == 0, kv, -1)
+        o = np.argsort(-key, kind="stable")
+        tseq[:ntile] = ts[o]
+        tq0[:ntile] = tq[o]
 
     # ----------------------------------------------------------------- forward
     def _forward_sample(self, view):
