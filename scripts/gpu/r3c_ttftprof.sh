@@ -8,3 +8,5 @@ grep '^{' gpurun_out/r3c_ttftprof.log
 f=$(find /tmp/ttftprof -name '*kernel_stats.csv' | head -1)
 cp "$f" gpurun_out/r3c_ttftprof_kernel_stats.csv
 head -25 "$f" | cut -c1-220
+VGATE_FLASH_CT=2 timeout -k 10 300 python -u benchmarks/attn_prefill_bench.py --lens 1024,2048,4096,8192 > gpurun_out/r3c_flash_ct2split.log 2>&1 || { tail -30 gpurun_out/r3c_flash_ct2split.log; exit 1; }
+echo "CT=2 + split"; grep '^{' gpurun_out/r3c_flash_ct2split.log | grep qwen | cut -c1-200
