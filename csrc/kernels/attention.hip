@@ -584,14 +584,16 @@ __global__ __launch_bounds__(64 * NW) void attn_flash_kernel(AttnArgs a, int laz
   const int kv_end = ctx - qlen + qhi;       // the block's causal bound (exclusive)
   const int nch = (kv_end + FL_KV - 1) / FL_KV;
   const int nfull = max(0, ctx - qlen + q0 + 1) / FL_KV;  // chunks below every query's bound
-  // K split (two halves per KV head, launch_attention): a range of >= 4 chunks runs as two halves of whole
-  // chunks, [0, nch/2) on z = 0 and [nch/2, nch) on z = 1, met in the epilogue; the causal
-  // triangle's long tail then costs half a range per block. Block-uniform, before any barrier.
+  // K split (zs parts per KV head, launch_attention): a range of nch chunks runs as nsp =
+  // min(zs, nch / 2) parts of whole chunks (>= 2 each), part z on [nch z / nsp, nch (z+1) / nsp),
+  // met in the epilogue; the causal triangle's long tail then costs 1 / nsp of a range per block.
+  // Parts past nsp exit at once. Block-uniform, before any barrier.
   const int z = blockIdx.x % zs;
-  const bool split = !SWP && zs > 1 && nch >= 4;
-  if (z > 0 && !split) return;
-  const int c0 = split && z == 1 ? nch / 2 : 0;
-  const int c1 = split && z == 0 ? nch / 2 : nch;
+  const int nsp = SWP ? 1 : min(zs, nch / 2);
+  const bool split = nsp > 1;
+  if (z >= max(nsp, 1)) return;
+  const int c0 = split ? nch * z / nsp : 0;
+  const int c1 = split ? nch * (z + 1) / nsp : nch;
   const int col = lane & 15, g4 = lane >> 4;
   // Q fragments (B operand of S^T = K Q^T): CT column tiles x 4 k-slices
   uint4 qf[CT][4];
@@ -795,13 +797,14 @@ __global__ __launch_bounds__(64 * NW) void attn_flash_kernel(AttnArgs a, int laz
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the look-ahead DMAs drained before the block exits
   if (split) {
-    // The two halves meet per wave. Each rounds its partial to bf16 normalised by its own sum
-    // (o / l) with (m, l) in fp32 and takes the wave's ticket; the first arriver publishes that
-    // (16-B sc1 stores, drain, ready flag) and exits, the second waits for the flag (the first
-    // never waits, so it always gets there), re-arms both words and merges the two ROUNDED
-    // partials in fixed half order: the result does not depend on which half came first. Slot:
-    // the leader's rank over the step (every earlier sequence holds ceil(qlen / QPB) leaders),
-    // KV head, wave; the host sized fl_ws for (tiles 16 / QPB + S + 1) Hkv NW <= 32768 slots.
+    // The parts meet per wave. Each rounds its partial to bf16 normalised by its own sum (o / l),
+    // (m, l) in fp32, and takes the wave's ticket first: the nsp - 1 early arrivers publish
+    // (16-B sc1 stores, drain, +1 on the ready word) and exit; the last waits for ready = nsp - 1
+    // (the others never wait, so they always get there), re-arms both words and merges every
+    // part's ROUNDED partial in fixed part order: the result does not depend on arrival order.
+    // Slot: the leader's rank over the step (every earlier sequence holds ceil(qlen / QPB)
+    // leaders), KV head, wave; the host sized fl_ws for (tiles 16 / QPB + S + 1) Hkv NW <= 32768
+    // slots of zs parts.
     int before = 0;
     for (int i = lane; i < s; i += 64) {
       const int ql = a.query_start[i + 1] - a.query_start[i];
@@ -813,7 +816,7 @@ __global__ __launch_bounds__(64 * NW) void attn_flash_kernel(AttnArgs a, int laz
     uint32_t* ticket = a.fl_tickets + wslot;
     uint32_t* ready = a.fl_tickets + 32768 + wslot;
     float ll[CT];
-    uint4 pw[CT][4];  // this half's o / l, bf16, mt pairs
+    uint4 pw[CT][4];  // this part's o / l, bf16, mt pairs
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       ll[ct] = l[ct];
@@ -827,66 +830,86 @@ __global__ __launch_bounds__(64 * NW) void attn_flash_kernel(AttnArgs a, int laz
                                pack_bf2(x1[0] * inv, x1[1] * inv), pack_bf2(x1[2] * inv, x1[3] * inv));
       }
     }
-    constexpr uint32_t PW = CT * 4 + 1;  // 16-B words per lane: the bf16 partial, then (m, l) pairs
-    const uint32_t slot_off = wslot * PW * 1024u + lane * 16u;
+    constexpr uint32_t PW = CT * 4 + 1;  // 16-B words per lane and part: the bf16 partial, then (m, l) pairs
+    const uint32_t lane_off = lane * 16u;
+    auto part_off = [&](int p) { return (wslot * (uint32_t)zs + (uint32_t)p) * PW * 1024u + lane_off; };
     uint32_t old = 0;
     if (lane == 0) old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     old = __shfl(old, 0);
-    if (old == 0) {
+    if (old + 1 < (uint32_t)nsp) {
+      const uint32_t off = part_off(z);
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
         for (int w = 0; w < 4; ++w)
-          st_sc1_x4(a.fl_ws, slot_off + (uint32_t)(ct * 4 + w) * 1024u, __builtin_bit_cast(f32x4, pw[ct][w]));
-      st_sc1_x4(a.fl_ws, slot_off + CT * 4 * 1024u, f32x4{m[0], ll[0], m[CT - 1], ll[CT - 1]});
+          st_sc1_x4(a.fl_ws, off + (uint32_t)(ct * 4 + w) * 1024u, __builtin_bit_cast(f32x4, pw[ct][w]));
+      st_sc1_x4(a.fl_ws, off + CT * 4 * 1024u, f32x4{m[0], ll[0], m[CT - 1], ll[CT - 1]});
       drain_stores();
-      if (lane == 0) __hip_atomic_store(ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) __hip_atomic_fetch_add(ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
     if (lane == 0) {
       uint32_t spins = 0;
-      while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 < (uint32_t)nsp) {
         __builtin_amdgcn_s_sleep(1);
         if (++spins > (1u << 22)) break;  // bounded: never hang the GPU (the result is then wrong)
       }
       __hip_atomic_store(ready, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    asm volatile("" ::: "memory");  // the partial's loads stay behind the flag
-    uint4 qb[CT][4];
+    asm volatile("" ::: "memory");  // the partials' loads stay behind the flag
+    // every part's (m, l) -> weights, then the partials in part order
+    f32x4 ml[4];
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-      for (int w = 0; w < 4; ++w)
-        qb[ct][w] = __builtin_bit_cast(uint4, ld_sc1_x4(a.fl_ws, slot_off + (uint32_t)(ct * 4 + w) * 1024u));
-    const f32x4 mlb = ld_sc1_x4(a.fl_ws, slot_off + CT * 4 * 1024u);
+    for (int p = 0; p < 4; ++p)
+      ml[p] = (p < nsp && p != z) ? ld_sc1_x4(a.fl_ws, part_off(p) + CT * 4 * 1024u)
+                                  : f32x4{m[0], ll[0], m[CT - 1], ll[CT - 1]};
     auto lo_f = [](uint32_t u) { return __uint_as_float(u << 16); };
     auto hi_f = [](uint32_t u) { return __uint_as_float(u & 0xffff0000u); };
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
-      const float mo = ct == 0 ? mlb[0] : mlb[2], lo = ct == 0 ? mlb[1] : mlb[3];
-      const float m0 = z == 0 ? m[ct] : mo, m1 = z == 0 ? mo : m[ct];
-      const float l0 = z == 0 ? ll[ct] : lo, l1 = z == 0 ? lo : ll[ct];
-      const float mm = fmaxf(m0, m1);
+      float mm = -INFINITY;
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        if (p < nsp) mm = fmaxf(mm, ml[p][2 * ct]);
       const float mref = mm == -INFINITY ? 0.f : mm;
-      const float a0 = __builtin_amdgcn_exp2f(m0 - mref) * l0, a1 = __builtin_amdgcn_exp2f(m1 - mref) * l1;
-      const float lt = a0 + a1;
-      const float w0 = lt > 0.f ? a0 / lt : 0.f, w1 = lt > 0.f ? a1 / lt : 0.f;
+      float wt[4], lt = 0.f;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        wt[p] = p < nsp ? __builtin_amdgcn_exp2f(ml[p][2 * ct] - mref) * ml[p][2 * ct + 1] : 0.f;
+        lt += wt[p];
+      }
+      const float inv = lt > 0.f ? 1.f / lt : 0.f;
+      float acc[32];
+#pragma unroll
+      for (int e = 0; e < 32; ++e) acc[e] = 0.f;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        if (p >= nsp) continue;
+        uint4 q4[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+          q4[w] = p == z ? pw[ct][w] : __builtin_bit_cast(uint4, ld_sc1_x4(a.fl_ws, part_off(p) + (uint32_t)(ct * 4 + w) * 1024u));
+        const float wp = wt[p] * inv;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const uint32_t u[4] = {q4[w].x, q4[w].y, q4[w].z, q4[w].w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            acc[8 * w + 2 * k] += lo_f(u[k]) * wp;
+            acc[8 * w + 2 * k + 1] += hi_f(u[k]) * wp;
+          }
+        }
+      }
       const int qi = qw0 + 16 * ct + col;
       if (qi >= qhi) continue;
       const size_t orow = (size_t)(qs + qi) * a.out_stride + (size_t)hq * D_;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const uint4 p0 = z == 0 ? pw[ct][w] : qb[ct][w], p1 = z == 0 ? qb[ct][w] : pw[ct][w];
-        const uint32_t u0[4] = {p0.x, p0.y, p0.z, p0.w}, u1[4] = {p1.x, p1.y, p1.z, p1.w};
-#pragma unroll
-        for (int hmt = 0; hmt < 2; ++hmt) {
-          uint2 pk;
-          pk.x = pack_bf2(lo_f(u0[2 * hmt]) * w0 + lo_f(u1[2 * hmt]) * w1, hi_f(u0[2 * hmt]) * w0 + hi_f(u1[2 * hmt]) * w1);
-          pk.y = pack_bf2(lo_f(u0[2 * hmt + 1]) * w0 + lo_f(u1[2 * hmt + 1]) * w1,
-                          hi_f(u0[2 * hmt + 1]) * w0 + hi_f(u1[2 * hmt + 1]) * w1);
-          *reinterpret_cast<uint2*>(a.out + orow + 16 * (2 * w + hmt) + 4 * g4) = pk;
-        }
+      for (int mt = 0; mt < 8; ++mt) {
+        uint2 pk;
+        pk.x = pack_bf2(acc[4 * mt], acc[4 * mt + 1]);
+        pk.y = pack_bf2(acc[4 * mt + 2], acc[4 * mt + 3]);
+        *reinterpret_cast<uint2*>(a.out + orow + 16 * mt + 4 * g4) = pk;
       }
     }
     return;
@@ -972,16 +995,24 @@ void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
     static const int swp = [] { const char* e = getenv("VGATE_FLASH_SWP"); return e ? atoi(e) : 0; }();
     const size_t lds = (size_t)(nst == 2 ? 2 : 4) * FL_STAGE + (size_t)a.max_blocks * 4;
     const size_t lds4 = (size_t)4 * FL_STAGE + (size_t)a.max_blocks * 4;
-    // K split of the long causal ranges (two halves per KV head, adjacent in grid.x) when the workspace holds every wave's partial
+    // K split of the long causal ranges (zs parts per KV head, adjacent in grid.x) when the
+    // workspace holds every wave's partials: 2 parts while the step's working blocks fill less
+    // than two waves of the chip's block slots (CT = 2 blocks hold a CU alone, CT = 1 two), 4
+    // while 4 parts per block still fit in one wave (profiles/r3_flash_split.log: 4 parts won
+    // only there: Llama-3-70B TP=8 2048 39.8 -> 31.9 us, lost at Qwen 2048 46 -> 50, Llama-8B
+    // 1024 35 -> 45); none once the blocks alone fill two waves (they balance the triangle)
     int zs = 1;
+    static const int max_parts = [] { const char* e = getenv("VGATE_FLASH_PARTS"); const int v = e ? atoi(e) : 4; return v >= 4 ? 4 : (v >= 2 ? 2 : 1); }();
     if (!swp && f.fl_ws != nullptr && f.fl_tickets != nullptr) {
       const int qpb = 16 * fc.ct * (fc.nw / (a.Hq / a.Hkv));
       const size_t leaders = (size_t)tiles * 16 / qpb + (size_t)a.S + 1;
       const size_t slots = leaders * a.Hkv * fc.nw;
-      // only while the step's blocks do not fill the chip twice over (more blocks than that
-      // balance the causal triangle themselves; CT = 2 blocks hold a CU alone, CT = 1 two)
-      const bool few = (size_t)tiles * 16 / qpb * a.Hkv * fc.ct <= (size_t)2 * cu_count();
-      if (few && slots <= 32768 && slots * (fc.ct * 4 + 1) * 1024 <= f.fl_ws_bytes) zs = 2;
+      const size_t blocks = (size_t)tiles * 16 / qpb * a.Hkv;
+      const size_t cap = (size_t)cu_count() * (fc.ct == 2 ? 1 : 2);
+      if (blocks < 2 * cap) zs = 2;
+      if (blocks * 4 <= cap) zs = 4;
+      zs = min(zs, max_parts);
+      if (slots > 32768 || slots * zs * (fc.ct * 4 + 1) * 1024 > f.fl_ws_bytes) zs = 1;
     }
     const dim3 grid(a.Hkv * zs, tiles, 1), block(64 * fc.nw);
 #define VG_FL(CT_, NW_)                                                                                      \
