@@ -326,7 +326,9 @@ def main():
         out = {
             "metric": METRIC.format(model="Qwen2.5-1.5B" if model_name == "Qwen2.5-1.5B-Instruct" else model_name), "value": round(value, 3), "unit": "req/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * wall / args.steps, 2), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": round(value / BASELINE_REQ_S, 3), "dtype": "bf16",
+            "scaling": "weak", "vs_baseline": round(value / BASELINE_REQ_S, 3),
+            # weight precision of the run: int4 weights with bf16 activations for AWQ
+            "dtype": "w4a16" if (args.quantization or "").lower() == "awq" else "bf16",
             "data": f"synthetic unique prompts, random-init weights ({model_name} architecture)",
             "config": {"model": model_name, "quantization": args.quantization or "none",
                        "security_rate_limiter": bool(args.security),

@@ -28,6 +28,46 @@ os.environ.setdefault("VGATE_DRY_RUN", "true")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: requires an AMD MI355X GPU (gfx950) and the native extension")
     config.addinivalue_line("markers", "slow: long-running test")
+    if os.environ.get("PYTHONASYNCIODEBUG"):
+        _install_asyncio_debug_recorder()
+
+
+# ---- asyncio debug pass (tests/test_asyncio_debug.py runs the async suites with
+# PYTHONASYNCIODEBUG=1): every asyncio-logger warning (slow callback > 100 ms, non-threadsafe call,
+# never-retrieved exception) and every "coroutine ... was never awaited" is recorded and fails the run
+ASYNCIO_DEBUG_FINDINGS: list[str] = []
+
+
+def _install_asyncio_debug_recorder() -> None:
+    import logging
+    import warnings
+
+    class _Rec(logging.Handler):
+        def emit(self, record):
+            msg = record.getMessage()
+            if "coro=<test_" in msg:  # a test function's own body blocking its loop: harness, not product
+                return
+            ASYNCIO_DEBUG_FINDINGS.append(f"asyncio {record.levelname}: {msg}")
+
+    lg = logging.getLogger("asyncio")
+    lg.addHandler(_Rec(level=logging.WARNING))
+    lg.setLevel(logging.WARNING)
+    orig = warnings.showwarning
+
+    def show(message, category, filename, lineno, file=None, line=None):
+        if issubclass(category, RuntimeWarning) and "never awaited" in str(message):
+            ASYNCIO_DEBUG_FINDINGS.append(f"{category.__name__}: {message} ({filename}:{lineno})")
+        return orig(message, category, filename, lineno, file, line)
+    warnings.showwarning = show
+    warnings.filterwarnings("always", message=".*was never awaited", category=RuntimeWarning)
+
+
+def pytest_sessionfinish(session, exitstatus):
+    if os.environ.get("PYTHONASYNCIODEBUG") and ASYNCIO_DEBUG_FINDINGS:
+        import gc
+        gc.collect()
+        sys.stderr.write("\nASYNCIO-DEBUG FINDINGS:\n" + "\n".join(ASYNCIO_DEBUG_FINDINGS) + "\n")
+        session.exitstatus = 1
 
 
 @pytest.hookimpl(tryfirst=True)

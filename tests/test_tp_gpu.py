@@ -174,7 +174,7 @@ def test_tp2_two_shot_long_prefill_matches_tp1(tmp_path):
     assert tp_out == ref
 
 
-def _timeout_worker(rank, port, path, q, go):
+def _timeout_worker(rank, port, path, q, go, ring="1"):
     import sys
 
     def say(*a):
@@ -182,7 +182,8 @@ def _timeout_worker(rank, port, path, q, go):
 
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-                          MASTER_PORT=str(port), VGATE_TP_TIMEOUT_S="60", VGATE_AR_SPIN_LIMIT="200000")
+                          MASTER_PORT=str(port), VGATE_TP_TIMEOUT_S="60", VGATE_AR_SPIN_LIMIT="200000",
+                          VGATE_RING_IDS=ring)
         import torch.distributed as dist
 
         from vgate.runtime.engine import LLMEngine
@@ -226,12 +227,14 @@ def _timeout_worker(rank, port, path, q, go):
 
 
 @pytest.mark.timeout(300)
-def test_tp2_peer_stops_custom_allreduce_times_out_and_engine_fails(tmp_path):
+@pytest.mark.parametrize("ring", ["1", "0"])
+def test_tp2_peer_stops_custom_allreduce_times_out_and_engine_fails(tmp_path, ring):
     """Timeout path of the custom all-reduce: rank 1 is frozen (SIGSTOP) after a good generation;
     rank 0's next step waits for it at the first collective, gives up after the spin limit (set
     short here), every later collective of the step skips the wait (sticky error word), the
     step's last graph node hands the word to the host, and the engine fails the step: the request
-    ends with an error and the engine reports unhealthy (its /health then answers 503)."""
+    ends with an error and the engine reports unhealthy (its /health then answers 503).
+    ring "0" (VGATE_RING_IDS=0: no ids-ring node) takes the ar.check() read instead."""
     import signal
 
     path = _ckpt(tmp_path)
@@ -239,7 +242,7 @@ def test_tp2_peer_stops_custom_allreduce_times_out_and_engine_fails(tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     go = ctx.Event()
-    procs = [ctx.Process(target=_timeout_worker, args=(r, port, path, q, go)) for r in range(2)]
+    procs = [ctx.Process(target=_timeout_worker, args=(r, port, path, q, go, ring)) for r in range(2)]
     for p in procs:
         p.start()
     pid1 = None

@@ -31,6 +31,11 @@ from typing import Any, AsyncIterator, Dict, List, Optional, Tuple
 
 import httpx
 
+try:  # imported with the module, not by the first request on the event loop (~0.2 s)
+    import aiohttp as _aiohttp
+except ImportError:  # pragma: no cover - aiohttp is in requirements.txt
+    _aiohttp = None
+
 from vgate.config import ModelConfig, WorkerConfig
 from vgate.logging_config import get_logger
 from vgate.metrics import WORKER_LATENCY, WORKER_REQUESTS, WORKER_RETRIES
@@ -61,8 +66,9 @@ class _AiohttpTransport:
     """Serving-path HTTP client: one aiohttp session (keep-alive pool) per event loop."""
 
     def __init__(self, cfg: WorkerConfig, headers: dict):
-        import aiohttp
-        self._aiohttp = aiohttp
+        if _aiohttp is None:
+            raise RuntimeError("the remote backend needs aiohttp")
+        aiohttp = self._aiohttp = _aiohttp
         # SSE pass-through: no bound on the stream's lifetime (a long generation is legitimate),
         # timeout_seconds bounds the silence between two chunks instead
         self._stream_timeout = aiohttp.ClientTimeout(total=None, connect=cfg.connect_timeout_seconds,

@@ -80,6 +80,10 @@ class WorkerHealthChecker:
         kw = dict(timeout=self.timeout_seconds, headers=self._headers)
         if self._transport is not None:
             kw["transport"] = self._transport
+        else:
+            # the client's TLS context (CA bundle parse, ~0.1 s) is built off the event loop: the
+            # asyncio debug pass flags it as a slow callback otherwise (tests/test_asyncio_debug.py)
+            kw["verify"] = await asyncio.to_thread(httpx.create_ssl_context)
         async with httpx.AsyncClient(**kw) as client:
             try:
                 await self.refresh_members()

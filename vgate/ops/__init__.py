@@ -505,6 +505,61 @@ def attention_o(q, q_stride, k_cache, v_cache, block_tables, context_lens, query
                                      lin.bias, attn_o_sync(q.device)))
 
 
+# fused decode MLP (csrc/kernels/mlp_fused.hip): gate_up -> SiLU -> down_proj (+residual) as one launch
+# for steps of <= 16 rows; VGATE_FUSED_MLP=1 turns it on (being tuned: slower than the two GEMMs so far)
+FUSED_MLP = os.environ.get("VGATE_FUSED_MLP", "0") == "1"
+_MLP_WS: dict = {}
+_EPOCH: dict = {}
+
+
+def mlp_workspace(device, H: int, I: int) -> torch.Tensor:
+    """Per-device int32 workspace of the fused MLP: [4096 n-tile tickets | 4096 words (give-up word at 0)
+    | 16 I words of h granules | fp32 partial slabs for up to 16 slices x 4 pieces per n-tile]. Zeroed
+    once (tickets self-reset); allocate before any graph capture — it never moves afterwards."""
+    key = str(device)
+    need = 8192 + 16 * I + (H // 16) * 16 * 4 * 256
+    t = _MLP_WS.get(key)
+    if t is None or t.numel() < need:
+        t = _MLP_WS[key] = torch.zeros(need, dtype=torch.int32, device=device)
+    return t
+
+
+def mlp_error(device) -> int:
+    """The fused MLP's sticky give-up word (non-zero: a granule poll timed out; the step's output is
+    garbage). Reads the device (a sync): tests / health checks only."""
+    t = _MLP_WS.get(str(device))
+    return int(t[4096].item()) if t is not None else 0
+
+
+def forward_epoch(device) -> torch.Tensor:
+    """Per-device forward counter: the embedding kernel adds 1 per forward and the fused MLP tags its
+    h granules with it (epoch, layer), so a replayed graph never reads the previous forward's h."""
+    key = str(device)
+    t = _EPOCH.get(key)
+    if t is None:
+        t = _EPOCH[key] = torch.zeros(4, dtype=torch.int32, device=device)
+    return t
+
+
+def mlp_decode(x: torch.Tensor, gate_up: "Linear", down: "Linear", out: torch.Tensor, residual, eps: float,
+               layer: int, epoch: torch.Tensor, slices: int = 0, grid: int = 0) -> bool:
+    """``out = [residual +] down(silu(gate(xn)) * up(xn))``, xn = RMSNorm(x) with the gamma folded into
+    ``gate_up`` (Linear.fold_norm), as ONE launch (decode steps, <= 16 rows; out may alias x and
+    residual). Returns False and launches nothing when the layers or the shape do not fit the fused
+    form (AWQ / unfolded gamma / bias / more rows): the caller then runs the two GEMMs."""
+    if not FUSED_MLP or not _gpu(x) or x.shape[0] > 16:
+        return False
+    if gate_up.kind != "dense" or down.kind != "dense" or gate_up.layout != "silu" or gate_up.norm_gamma is None:
+        return False
+    if gate_up.bias is not None or down.bias is not None or gate_up.wp is None or down.wp is None:
+        return False
+    I, H = gate_up.N // 2, gate_up.K
+    if down.K != I or down.N != H:
+        return False
+    return bool(native().mlp_decode(x, gate_up.wp, down.wp, H, I, out, residual, float(eps),
+                                    mlp_workspace(x.device, H, I), epoch, int(layer), slices, grid))
+
+
 _AO_SYNC: dict = {}
 
 
@@ -546,9 +601,10 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor
 
 
 def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None, vstart: int = 0,
-              prev: torch.Tensor | None = None):
+              prev: torch.Tensor | None = None, epoch: torch.Tensor | None = None):
     """Row gather with vocab-shard masking (rows outside this TP rank's shard are zero).
-    ids < 0 name a token the previous step sampled on the device: id = prev[-id - 1]."""
+    ids < 0 name a token the previous step sampled on the device: id = prev[-id - 1].
+    epoch (GPU): the forward counter of :func:`forward_epoch`, bumped by the same launch."""
     if out is None:
         out = torch.empty(ids.numel(), table.shape[1], dtype=table.dtype, device=table.device)
     if not _gpu(table):
@@ -556,7 +612,7 @@ def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None =
             ids = torch.where(ids < 0, prev.to(ids.device)[(-ids - 1).clamp(min=0).long()], ids)
         out.copy_(ref.embedding_ref(ids, table, vstart))
         return out
-    native().embedding(ids, table, out, vstart, prev)
+    native().embedding(ids, table, out, vstart, prev, epoch)
     return out
 
 

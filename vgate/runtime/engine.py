@@ -608,7 +608,9 @@ class LLMEngine:
         ar = self.tp.custom_ar
         if ar is None:
             return
-        if self.runner.gpu and self.runner.ar_base:
+        # the ring words are written only by the ids_to_host node (VGATE_RING_IDS=1, the default);
+        # with the ring off the error word is read by ar.check() below
+        if self.runner.gpu and self.runner.ar_base and getattr(self.runner, "ring_ids", False):
             err, secs, calls = self.runner.collective_words()
             if calls and len(self._ar_ms) < 65536:
                 self._ar_ms.append(1e3 * secs)
