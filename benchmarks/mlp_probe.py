@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--slices", type=int, default=0)
     a = ap.parse_args()
+    ops.FUSED_MLP = True
     dev = torch.device("cuda:0")
     H, I, M = a.H, a.I, a.M
     g = torch.Generator(device=dev).manual_seed(0)

@@ -850,12 +850,19 @@ __global__ __launch_bounds__(64 * NW) void attn_flash_kernel(AttnArgs a, int laz
     }
     if (lane == 0) {
       uint32_t spins = 0;
+      bool late = false;
       while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 < (uint32_t)nsp) {
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 22)) break;  // bounded: never hang the GPU (the result is then wrong)
+        if (++spins > (1u << 22)) { late = true; break; }  // bounded: never hang the GPU
       }
-      __hip_atomic_store(ready, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (late) {
+        // the result is wrong and a late part may still add to `ready`: leave the words as they are and
+        // raise the sticky fault word, which the step's last node hands to the host (engine fails)
+        if (a.fault != nullptr) atomicOr(a.fault, 2u);
+      } else {
+        __hip_atomic_store(ready, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     asm volatile("" ::: "memory");  // the partials' loads stay behind the flag
     // every part's (m, l) -> weights, then the partials in part order

@@ -255,19 +255,22 @@ __global__ __launch_bounds__(256) void copy16_kernel(const uint4* __restrict__ s
 // after the graph (the graph-end -> next-dispatch boundary was ~9 us of the gap between steps).
 __global__ __launch_bounds__(64) void ids_to_host_kernel(const int32_t* __restrict__ ids, int32_t* __restrict__ ring,
                                                          const int32_t* __restrict__ slot, int stride, int n,
-                                                         const uint32_t* __restrict__ ar) {
+                                                         const uint32_t* __restrict__ ar,
+                                                         const uint32_t* __restrict__ fault) {
   const int s = *slot;
   for (int i = threadIdx.x; i < n; i += 64) ring[(size_t)s * stride + i] = ids[i];
   if (ar != nullptr && threadIdx.x < 3)  // custom all-reduce {error, ticks, calls}: sticky / running words
     ring[(size_t)s * stride + stride - 4 + threadIdx.x] =
         (int32_t)__hip_atomic_load(ar + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (fault != nullptr && threadIdx.x == 3)  // in-launch hand-off give-ups (flash K split, fused MLP): sticky
+    ring[(size_t)s * stride + stride - 1] = (int32_t)__hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __threadfence_system();
 }
 
 void launch_ids_to_host(const int32_t* ids, int32_t* ring, const int32_t* slot, int stride, int n, hipStream_t st,
-                        const uint32_t* ar) {
-  if (n <= 0 && ar == nullptr) return;
-  hipLaunchKernelGGL(ids_to_host_kernel, dim3(1), dim3(64), 0, st, ids, ring, slot, stride, n, ar);
+                        const uint32_t* ar, const uint32_t* fault) {
+  if (n <= 0 && ar == nullptr && fault == nullptr) return;
+  hipLaunchKernelGGL(ids_to_host_kernel, dim3(1), dim3(64), 0, st, ids, ring, slot, stride, n, ar, fault);
 }
 
 void launch_copy16(const void* src, void* dst, size_t bytes, bool to_host, hipStream_t st) {

@@ -143,9 +143,10 @@ void set_flash_prefill(int on);  // prefill tiles on the flash kernel: 1 on, 0 o
 void launch_copy16(const void* src, void* dst, size_t bytes, bool to_host, hipStream_t st);
 // ids[0, n) -> ring[*slot * stride + i] (ring: device-mapped pinned host memory); with `ar` (the
 // own custom all-reduce signal area's error word, or null) also its {error, ticks, calls} words ->
-// ring[*slot * stride + stride - 4 + {0, 1, 2}] (the TP collective health / time, no host sync)
+// ring[*slot * stride + stride - 4 + {0, 1, 2}] (the TP collective health / time, no host sync); with
+// `fault` (ops.fault_word: the sticky give-up word of the in-launch hand-offs) also -> stride - 1
 void launch_ids_to_host(const int32_t* ids, int32_t* ring, const int32_t* slot, int stride, int n, hipStream_t st,
-                        const uint32_t* ar = nullptr);
+                        const uint32_t* ar = nullptr, const uint32_t* fault = nullptr);
 
 // NeoX RoPE on q,k inside the fused qkv buffer + paged KV-cache write.
 // qkv: [T, (Hq + 2*Hkv) * D]; cos_sin: [max_pos, D] f32 (cos | sin halves)
@@ -194,6 +195,9 @@ struct AttnArgs {
   float* fl_ws = nullptr;
   size_t fl_ws_bytes = 0;
   uint32_t* fl_tickets = nullptr;
+  // sticky kernel-fault word (bit 1: a flash K-split waiter gave up), copied to the host each step by
+  // launch_ids_to_host; null = none
+  uint32_t* fault = nullptr;
 };
 void launch_attn_decode(const AttnArgs& a, hipStream_t st);
 void launch_attn_prefill(const AttnArgs& a, hipStream_t st);

@@ -202,7 +202,7 @@ void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vsta
 // Returns false (nothing launched) when the shape does not fit the fused work split.
 bool mlp_decode(const Tensor& x, const Tensor& wgu, const Tensor& wd, int64_t H, int64_t I, Tensor& out,
                 const c10::optional<Tensor>& res, double eps, Tensor& ws, const Tensor& epoch, int64_t layer,
-                int64_t slices, int64_t grid, const c10::optional<Tensor>& dbg) {
+                int64_t slices, int64_t grid, const c10::optional<Tensor>& dbg, const c10::optional<Tensor>& fault) {
   CHECK_DEV(x); CHECK_DEV(wgu); CHECK_DEV(wd); CHECK_DEV(out); CHECK_DEV(ws); CHECK_DEV(epoch);
   CHECK_DT(x, torch::kBFloat16); CHECK_DT(out, torch::kBFloat16); CHECK_DT(wgu, torch::kBFloat16);
   CHECK_DT(wd, torch::kBFloat16); CHECK_DT(ws, torch::kInt32); CHECK_DT(epoch, torch::kInt32);
@@ -225,7 +225,8 @@ bool mlp_decode(const Tensor& x, const Tensor& wgu, const Tensor& wd, int64_t H,
   int32_t* w32 = reinterpret_cast<int32_t*>(ws.data_ptr());
   g.tickets = reinterpret_cast<uint32_t*>(w32);
   g.max_tickets = 4096;
-  g.err = reinterpret_cast<uint32_t*>(w32 + 4096);
+  uint32_t* fw = reinterpret_cast<uint32_t*>(opt_ptr<int32_t>(fault, torch::kInt32, "fault"));
+  g.err = fw != nullptr ? fw : reinterpret_cast<uint32_t*>(w32 + 4096);
   g.hbuf = w32 + 8192;
   g.slabs = reinterpret_cast<float*>(w32 + fixed);
   g.slab_bytes = (size_t)(ws.numel() - fixed) * 4;
@@ -332,7 +333,9 @@ void attn_decode(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const
 
 // the flash prefill K split's workspace: the GEMM workspace (ops.workspace), 65536 zeroed
 // self-resetting tickets, then fp32 slabs; a flash launch never overlaps a GEMM on the stream
-static void set_flash_ws(vgate::AttnArgs& a, const c10::optional<Tensor>& flash_ws) {
+static void set_flash_ws(vgate::AttnArgs& a, const c10::optional<Tensor>& flash_ws,
+                         const c10::optional<Tensor>& fault = c10::nullopt) {
+  a.fault = reinterpret_cast<uint32_t*>(opt_ptr<int32_t>(fault, torch::kInt32, "fault"));
   if (!flash_ws.has_value() || !flash_ws->defined()) return;
   CHECK_DEV(*flash_ws); CHECK_DT(*flash_ws, torch::kInt32);
   TORCH_CHECK(flash_ws->numel() > 65536, "attention: flash_ws is the GEMM workspace");
@@ -344,9 +347,10 @@ static void set_flash_ws(vgate::AttnArgs& a, const c10::optional<Tensor>& flash_
 void attn_prefill(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const Tensor& v_cache,
                   const Tensor& block_tables, const Tensor& context_lens,
                   const Tensor& query_start, const Tensor& tile_seq, const Tensor& tile_q0,
-                  Tensor& out, int64_t Hq, int64_t Hkv, double scale, const c10::optional<Tensor>& flash_ws) {
+                  Tensor& out, int64_t Hq, int64_t Hkv, double scale, const c10::optional<Tensor>& flash_ws,
+                  const c10::optional<Tensor>& fault) {
   auto a = attn_common(q, q_stride, k_cache, v_cache, block_tables, context_lens, out, Hq, Hkv, scale);
-  set_flash_ws(a, flash_ws);
+  set_flash_ws(a, flash_ws, fault);
   CHECK_DT(query_start, torch::kInt32); CHECK_DT(tile_seq, torch::kInt32); CHECK_DT(tile_q0, torch::kInt32);
   a.query_start = reinterpret_cast<const int32_t*>(query_start.data_ptr());
   a.tile_seq = reinterpret_cast<const int32_t*>(tile_seq.data_ptr());
@@ -361,9 +365,9 @@ void attention(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const T
                const Tensor& tile_seq, const Tensor& tile_q0, Tensor& out, Tensor& part_o, Tensor& part_ml,
                int64_t Hq, int64_t Hkv, int64_t part_size, double scale, int64_t out_stride,
                const c10::optional<Tensor>& tickets, const c10::optional<Tensor>& dbg_ts,
-               const c10::optional<Tensor>& flash_ws) {
+               const c10::optional<Tensor>& flash_ws, const c10::optional<Tensor>& fault) {
   auto a = attn_common(q, q_stride, k_cache, v_cache, block_tables, context_lens, out, Hq, Hkv, scale);
-  set_flash_ws(a, flash_ws);
+  set_flash_ws(a, flash_ws, fault);
   if (out_stride > 0) a.out_stride = (int)out_stride;
   CHECK_DT(query_start, torch::kInt32); CHECK_DT(tile_seq, torch::kInt32); CHECK_DT(tile_q0, torch::kInt32);
   CHECK_DT(part_o, torch::kFloat32); CHECK_DT(part_ml, torch::kFloat32);
@@ -511,17 +515,21 @@ void kernel_copy(Tensor& dst, const Tensor& src, int64_t nbytes) {
   vgate::launch_copy16(device_view(src), device_view(dst), (size_t)n, !dst.is_cuda(), cur_stream());
 }
 
-void ids_to_host(const Tensor& ids, Tensor& ring, const Tensor& slot, int64_t n, int64_t ar_base) {
+void ids_to_host(const Tensor& ids, Tensor& ring, const Tensor& slot, int64_t n, int64_t ar_base,
+                 const c10::optional<Tensor>& fault) {
   CHECK_DEV(ids); CHECK_DEV(slot);
   CHECK_DT(ids, torch::kInt32); CHECK_DT(ring, torch::kInt32); CHECK_DT(slot, torch::kInt32);
   TORCH_CHECK(ring.dim() == 2 && ring.is_contiguous() && !ring.is_cuda(), "ids_to_host: ring = pinned int32 [slots, stride]");
   TORCH_CHECK(n >= 0 && n <= ids.numel() && n <= ring.size(1), "ids_to_host: n exceeds ids or a ring slot");
-  TORCH_CHECK(ar_base == 0 || n <= ring.size(1) - 4, "ids_to_host: the all-reduce words need the slot's last 4 ints");
+  const uint32_t* fw = reinterpret_cast<const uint32_t*>(opt_ptr<int32_t>(fault, torch::kInt32, "fault"));
+  TORCH_CHECK((ar_base == 0 && fw == nullptr) || n <= ring.size(1) - 4,
+              "ids_to_host: the all-reduce / fault words need the slot's last 4 ints");
   const uint32_t* ar = ar_base ? reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(ar_base) + vgate::ar_error_offset())
                                : nullptr;
   c10::DeviceGuard guard(ids.device());
   vgate::launch_ids_to_host(reinterpret_cast<const int32_t*>(ids.data_ptr()), reinterpret_cast<int32_t*>(device_view(ring)),
-                            reinterpret_cast<const int32_t*>(slot.data_ptr()), (int)ring.size(1), (int)n, cur_stream(), ar);
+                            reinterpret_cast<const int32_t*>(slot.data_ptr()), (int)ring.size(1), (int)n, cur_stream(), ar,
+                            fw);
 }
 
 void prefetch(const Tensor& t, int64_t blocks) {
@@ -639,7 +647,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),
         py::arg("part_o"), py::arg("part_ml"), py::arg("Hq"), py::arg("Hkv"), py::arg("part_size"), py::arg("scale"),
         py::arg("out_stride") = 0, py::arg("tickets") = py::none(), py::arg("dbg_ts") = py::none(),
-        py::arg("flash_ws") = py::none());
+        py::arg("flash_ws") = py::none(), py::arg("fault") = py::none());
   m.def("attention_o", &attention_o, "decode attention + o_proj GEMM (+residual) as one launch; false = not fused",
         py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),
@@ -652,7 +660,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("mlp_decode", &mlp_decode, "fused decode MLP: out = [res +] down(silu(gate) * up)(RMSNorm rows), one launch; "
         "false = shape not fused", py::arg("x"), py::arg("wgu"), py::arg("wd"), py::arg("H"), py::arg("I"),
         py::arg("out"), py::arg("res") = py::none(), py::arg("eps"), py::arg("ws"), py::arg("epoch"),
-        py::arg("layer"), py::arg("slices") = 0, py::arg("grid") = 0, py::arg("dbg") = py::none());
+        py::arg("layer"), py::arg("slices") = 0, py::arg("grid") = 0, py::arg("dbg") = py::none(),
+        py::arg("fault") = py::none());
   m.def("rmsnorm", &rmsnorm, "RMSNorm with optional fused residual add");
   m.def("rope_kv", &rope_kv, "NeoX RoPE + paged KV-cache write (rotated q in place or into q_out)",
         py::arg("qkv"), py::arg("positions"), py::arg("slots"), py::arg("cos_sin"), py::arg("k_cache"),
@@ -665,7 +674,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_prefill", &attn_prefill, "paged varlen causal prefill attention",
         py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),
-        py::arg("Hq"), py::arg("Hkv"), py::arg("scale"), py::arg("flash_ws") = py::none());
+        py::arg("Hq"), py::arg("Hkv"), py::arg("scale"), py::arg("flash_ws") = py::none(),
+        py::arg("fault") = py::none());
   m.def("sample", &sample, "temperature/top-k/top-p sampling (segmented Gumbel-max + exact rejection)",
         py::arg("logits"), py::arg("temperature"), py::arg("top_p"), py::arg("top_k"), py::arg("seeds"),
         py::arg("offsets"), py::arg("out"), py::arg("out_logprob") = py::none(), py::arg("ws") = py::none());
@@ -682,7 +692,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_dec_bal", &vgate::set_dec_bal, "balanced decode GEMM: 1 on, 0 off, -1 environment (VGATE_DEC_BAL)");
   m.def("set_dec_u", &vgate::set_dec_u, "decode GEMM register group: 0 auto, -1 round-2 rule, 6/8/10/12 forced, -100 environment");
   m.def("ids_to_host", &ids_to_host, "sampled ids -> slot *slot of a pinned host ring (graph-capturable, device-read slot)",
-        py::arg("ids"), py::arg("ring"), py::arg("slot"), py::arg("n"), py::arg("ar_base") = 0);
+        py::arg("ids"), py::arg("ring"), py::arg("slot"), py::arg("n"), py::arg("ar_base") = 0,
+        py::arg("fault") = py::none());
   m.def("prefetch", &prefetch, "read a tensor once with the default cache policy (MALL warm-up)",
         py::arg("t"), py::arg("blocks") = 256);
   m.def("ar_alloc", &ar_alloc, "uncached device allocation for the custom all-reduce (zeroed)");

@@ -122,3 +122,34 @@ async def test_sigterm_drains_then_hands_over_to_the_server_handler():
         restore()
         signal.signal(signal.SIGTERM, old)
         worker_api.reset_drain()
+
+
+async def test_stream_counts_from_acceptance_and_releases_a_body_that_never_ran():
+    """An accepted stream counts for the drain from the endpoint's return, before the server first
+    iterates its body (a drain in that window finished early), and is released exactly
+    once: at the body's end, or — when the body never runs — when the response is dropped."""
+    import gc
+
+    from vgate.worker_api import StreamRequest
+    cfg = VGateConfig(role="worker")
+    eng = VGateEngine(model_config=cfg.model, worker_config=cfg.worker, backend=DryRunBackend(), dry_run=True)
+    worker_api.reset_drain()
+    prev = worker_api.get_engine()
+    worker_api.set_engine(eng)
+    try:
+        resp = await worker_api.internal_generate_stream(StreamRequest(prompt="a b c"), request=None)
+        assert worker_api.inflight() == 1
+        chunks = [c async for c in resp.body_iterator]
+        assert chunks[-1] == "data: [DONE]\n\n"
+        assert worker_api.inflight() == 0
+        dropped = await worker_api.internal_generate_stream(StreamRequest(prompt="x"), request=None)
+        assert worker_api.inflight() == 1
+        del dropped
+        gc.collect()
+        assert worker_api.inflight() == 0
+    finally:
+        if prev is not None:
+            worker_api.set_engine(prev)
+        else:
+            worker_api._engine = None
+        worker_api.reset_drain()

@@ -207,3 +207,30 @@ def test_tile_order_and_decode_only_buckets():
     assert all(int(t) % lead == 0 for t in tq[:nl]) and all(int(t) % lead for t in tq[nl:])
     rng = [int(cl[s] - qlens[s] + q) for s, q in zip(ts[:nl], tq[:nl])]
     assert rng == sorted(rng, reverse=True)
+
+
+def test_idle_admission_window_only_waits_for_an_expected_wave():
+    """The idle admission window coalesces a returning closed-loop wave into one prefill step, but a
+    lone request reaching a quiet engine starts at once (no added time to first token)."""
+    import time
+
+    eng = make_engine(idle_batch_window_ms=50.0, idle_batch_gap_ms=20.0, idle_batch_recent_ms=1000.0)
+    sp = SamplingParams(temperature=0.0, max_tokens=2, ignore_eos=True)
+    eng.add_request("lone", params=sp, prompt_ids=[5, 6, 7])
+    with eng._cv:
+        t0 = time.perf_counter()
+        eng._coalesce_arrivals()
+        assert time.perf_counter() - t0 < 0.01  # quiet engine: no wait for a burst
+    eng.run_until_idle()
+    # two requests finished just now: the next arrival waits one gap for the rest of its wave
+    eng._finish_times.extend([time.perf_counter()] * 2)
+    eng.add_request("wave0", params=sp, prompt_ids=[5, 6, 8])
+    eng._running = True  # (the window only waits inside a running engine loop)
+    try:
+        with eng._cv:
+            t0 = time.perf_counter()
+            eng._coalesce_arrivals()
+            assert time.perf_counter() - t0 >= 0.015
+    finally:
+        eng._running = False
+    eng.run_until_idle()

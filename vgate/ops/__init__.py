@@ -477,7 +477,7 @@ def attention(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_s
         tickets = attn_tickets(q.device)
     native().attention(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start, tile_seq, tile_q0,
                        out, part_o, part_ml, Hq, Hkv, part_size, scale, 0, tickets,
-                       flash_ws=workspace(q.device) if FLASH_SPLIT else None)
+                       flash_ws=workspace(q.device) if FLASH_SPLIT else None, fault=fault_word(q.device))
     return out
 
 
@@ -524,11 +524,27 @@ def mlp_workspace(device, H: int, I: int) -> torch.Tensor:
     return t
 
 
+_FAULT: dict = {}
+
+
+def fault_word(device) -> torch.Tensor:
+    """Per-device sticky fault word of the in-launch hand-offs (bit 0: a fused-MLP granule poll gave
+    up, bit 1: a flash K-split waiter gave up). Kernels only OR bits in; the step graph's last node
+    copies it to the host ring (ModelRunner.kernel_fault), and a non-zero word fails the engine."""
+    key = str(device)
+    t = _FAULT.get(key)
+    if t is None:
+        t = _FAULT[key] = torch.zeros(4, dtype=torch.int32, device=device)
+    return t
+
+
 def mlp_error(device) -> int:
     """The fused MLP's sticky give-up word (non-zero: a granule poll timed out; the step's output is
     garbage). Reads the device (a sync): tests / health checks only."""
     t = _MLP_WS.get(str(device))
-    return int(t[4096].item()) if t is not None else 0
+    own = int(t[4096].item()) if t is not None else 0
+    f = _FAULT.get(str(device))
+    return own | (int(f[0].item()) & 1 if f is not None else 0)
 
 
 def forward_epoch(device) -> torch.Tensor:
@@ -557,7 +573,8 @@ def mlp_decode(x: torch.Tensor, gate_up: "Linear", down: "Linear", out: torch.Te
     if down.K != I or down.N != H:
         return False
     return bool(native().mlp_decode(x, gate_up.wp, down.wp, H, I, out, residual, float(eps),
-                                    mlp_workspace(x.device, H, I), epoch, int(layer), slices, grid))
+                                    mlp_workspace(x.device, H, I), epoch, int(layer), slices, grid,
+                                    fault=fault_word(x.device)))
 
 
 _AO_SYNC: dict = {}
@@ -690,7 +707,7 @@ def attention_prefill(q, q_stride, k_cache, v_cache, block_tables, context_lens,
         return out
     native().attn_prefill(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start,
                           tile_seq, tile_q0, out, Hq, Hkv, scale,
-                          flash_ws=workspace(q.device) if FLASH_SPLIT else None)
+                          flash_ws=workspace(q.device) if FLASH_SPLIT else None, fault=fault_word(q.device))
     return out
 
 
@@ -844,6 +861,9 @@ def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = 0.05
             plan[M] = best if times[best] < (1.0 - margin) * times[(0, 0)] else (0, 0)
         plans[key] = plan
         lin.prefill_plan = plan
+    # the cache-flush buffer of the cold timer (512 MiB) is start-up scratch: give it back
+    _FLUSH.pop(str(dev), None)
+    torch.cuda.empty_cache()
     return plans
 
 
@@ -891,6 +911,7 @@ def softmax_scale(head_dim: int) -> float:
 
 __all__ = [
     "native", "native_available", "pack_weight", "unpack_weight", "interleave_gate_up", "pack_awq",
-    "Linear", "linear", "attention", "attention_o", "workspace", "row_permutation", "reserve_awq_scratch", "pack_awq_sz", "rmsnorm", "embedding", "rope_kv", "attention_decode", "attention_prefill",
+    "Linear", "linear", "attention", "attention_o", "workspace", "fault_word", "mlp_decode", "mlp_workspace",
+    "forward_epoch", "mlp_error", "row_permutation", "reserve_awq_scratch", "pack_awq_sz", "rmsnorm", "embedding", "rope_kv", "attention_decode", "attention_prefill",
     "prefill_tiles", "sample", "softmax_scale", "ref", "host_device_copy", "tune_prefill", "apply_prefill_plans",
 ]

@@ -75,6 +75,11 @@ class EngineConfig:
     # timed_prefill_steps). A running engine never waits: new requests join the next step.
     idle_batch_window_ms: float = float(os.environ.get("VGATE_IDLE_BATCH_WINDOW_MS", "3.0"))
     idle_batch_gap_ms: float = float(os.environ.get("VGATE_IDLE_BATCH_GAP_MS", "0.6"))
+    # ...but only when a burst is expected: at least 2 requests finished within the last
+    # `idle_batch_recent_ms` (a closed-loop client's wave comes back right after the previous wave
+    # ended). A request reaching an engine that has been quiet longer (an interactive request) is
+    # prefilled at once, with no added time to first token (round-3 ADVICE).
+    idle_batch_recent_ms: float = float(os.environ.get("VGATE_IDLE_BATCH_RECENT_MS", "20"))
     # GPU: time the prefill GEMM decompositions per layer shape and token bucket >= 128 at start-up
     # (ops.tune_prefill) instead of relying on the launcher's heuristic alone
     prefill_autotune: bool = os.environ.get("VGATE_PREFILL_AUTOTUNE", "1") != "0"
@@ -185,6 +190,7 @@ class LLMEngine:
         if self.tp.size > 1 and not self.tp.simulated:
             self._init_ring()
         self._inflight = None  # (batch, handle) of the launched, not yet post-processed step
+        self._finish_times: collections.deque = collections.deque(maxlen=64)  # idle admission window
         self._calls: collections.deque = collections.deque()  # (fn, future) run on the engine thread
         self.last_error: str | None = None
         self.last_step_wall = time.monotonic()
@@ -200,6 +206,7 @@ class LLMEngine:
         if cfg.num_kv_blocks:
             n = cfg.num_kv_blocks
         elif self.device.type == "cuda":
+            ops.workspace(self.device)  # the 256 MiB GEMM workspace is allocated before the free memory is read
             free, total = torch.cuda.mem_get_info(self.device)
             reserve = 4 * 2**30 + cfg.max_num_seqs * self.arch.vocab_size * 12
             budget = cfg.gpu_memory_utilization * total - (total - free) - reserve
@@ -290,6 +297,9 @@ class LLMEngine:
         if (win <= 0 or gap <= 0 or not self._inbox or self._inflight is not None or self._calls
                 or self.scheduler.has_work() or self.ring is not None):
             return
+        recent = time.perf_counter() - 1e-3 * self.cfg.idle_batch_recent_ms
+        if sum(1 for t in self._finish_times if t >= recent) < 2 and len(self._inbox) < 2:
+            return  # no wave is coming back: a lone request starts now
         t0 = time.perf_counter()
         t_end = t0 + 1e-3 * win
         cap = self.cfg.max_num_seqs
@@ -548,6 +558,7 @@ class LLMEngine:
             seq.status = SeqStatus.FINISHED
             seq.finish_reason = reason
         seq.finish_time = time.perf_counter()
+        self._finish_times.append(seq.finish_time)
         if seq.pending:  # abort / error with samples still in flight: drop the placeholders
             seq.output_ids = [t for t in seq.output_ids if t != PENDING]
             seq.pending.clear()
@@ -605,6 +616,10 @@ class LLMEngine:
         sticky error word (and the collective time counters) into the pinned ids ring
         (ModelRunner.collective_words), so the check is a host memory read (ROUND-2 ADVICE: the
         blocking hipMemcpy of ``ar.check()`` serialised rank 0 with its in-flight step)."""
+        fault = self.runner.kernel_fault() if self.runner.gpu else 0
+        if fault:
+            raise RuntimeError(f"an in-launch kernel hand-off gave up waiting (fault word {fault:#x}); "
+                               "the step's results are invalid")
         ar = self.tp.custom_ar
         if ar is None:
             return

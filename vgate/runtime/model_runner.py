@@ -107,6 +107,7 @@ class ModelRunner:
             ar = getattr(getattr(model, "tp", None), "custom_ar", None)
             self.ar_base = int(ar.own) if ar is not None and getattr(ar, "own", None) else 0
             self._ar_last = (0, 0)  # (ticks, calls) at the last read
+            self.fault = ops.fault_word(self.device)  # in-launch hand-off give-ups, read via the ring
             self._last_collected: int | None = None
             self._launches = 0
             # VGATE_RING_IDS=0: copy the ids after the graph instead (A/B experiments)
@@ -255,7 +256,8 @@ class ModelRunner:
         ops.sample(logits, view.temperature, view.top_p, view.top_k, view.seeds, view.offsets,
                    out=self.out_tokens[: view.S])
         if self.gpu and self.ring_ids:  # last node of the step graph: sampled ids -> pinned ring slot
-            ops.native().ids_to_host(self.out_tokens, self.out_ring, view.ring_slot, view.S, self.ar_base)
+            ops.native().ids_to_host(self.out_tokens, self.out_ring, view.ring_slot, view.S, self.ar_base,
+                                     fault=self.fault)
         return logits
 
     def _capture(self, T: int, S: int):
@@ -368,6 +370,15 @@ class ModelRunner:
         self._uncollected[h.k] = False
         self._last_collected = h.k
         return toks
+
+    def kernel_fault(self, k: int | None = None) -> int:
+        """The sticky fault word of the in-launch hand-offs (ops.fault_word) as the step graph's last
+        node copied it into ring slot ``k`` (default: the last collected step); 0 = healthy. No sync."""
+        if not self.gpu or not self.ring_ids:
+            return 0
+        if k is None:
+            k = self._last_collected if self._last_collected is not None else self._k ^ 1
+        return int(self.out_ring[k][-1])
 
     def collective_words(self, k: int | None = None) -> tuple[int, float, int]:
         """(error, seconds, calls) of the custom all-reduce since the previous call, from the words

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import asyncio
 import json
+import weakref
 from typing import Optional
 
 from fastapi import APIRouter, HTTPException, Request
@@ -169,8 +170,21 @@ async def internal_generate_stream(body: StreamRequest, request: Request):
     sp_in = body.sampling_params
     sp = backend.create_sampling_params(temperature=sp_in.temperature, top_p=sp_in.top_p, max_tokens=sp_in.max_tokens)
 
+    # the stream counts from ACCEPTANCE (here, before the response object exists) to its last byte:
+    # a drain that starts between this point and the server's first iteration of the body still
+    # waits for it. Released once, by the body's finally or — when the body never starts (client
+    # gone, response dropped) — by the generator object's finaliser.
+    _Accepted().__enter__()
+    released = [False]
+
+    def release():
+        global _inflight
+        if not released[0]:
+            released[0] = True
+            _inflight -= 1
+
     async def gen():
-        with _Accepted():  # the stream counts until its last byte
+        try:
             try:
                 async for piece in backend.stream_generate(body.prompt, sp):
                     yield f"data: {json.dumps(piece)}\n\n"
@@ -180,5 +194,9 @@ async def internal_generate_stream(body: StreamRequest, request: Request):
                 INFERENCE_ERRORS.labels(error_type=type(e).__name__).inc()
                 yield f"data: {json.dumps({'error': {'message': str(e), 'type': type(e).__name__}})}\n\n"
             yield "data: [DONE]\n\n"
+        finally:
+            release()
 
-    return StreamingResponse(gen(), media_type="text/event-stream")
+    body_gen = gen()
+    weakref.finalize(body_gen, release)
+    return StreamingResponse(body_gen, media_type="text/event-stream")
