@@ -39,7 +39,6 @@ def main():
     ap.add_argument("--mixed", type=int, default=0, help="time a MIXED step: one prompt of this many tokens "
                     "beside the decode rows (benchmarks/mixed_step.py)")
     ap.add_argument("--wide-gate-up", action="store_true", help="medium buckets: the wide medium kernel for gate_up")
-    ap.add_argument("--o-tiles", type=int, default=96, help="o_proj column tiles of a fused attn_o launch (N / 16)")
     a = ap.parse_args()
     eng = LLMEngine(EngineConfig(model=a.model, device="cuda:0", max_model_len=2048, max_num_seqs=a.max_seqs,
                                  max_num_batched_tokens=2048, num_kv_blocks=a.kv_blocks or None, warmup=False,
@@ -63,18 +62,6 @@ def main():
     summary, live, cap, t = measure(eng)
     summary.update(batch=a.batch, ctx=a.ctx)
     print(json.dumps(summary), flush=True)
-    # fused attention + o_proj launches: the two block roles' timings (blocks [0, nb - o_tiles)
-    # are attention, the rest o_proj column tiles), relative to the launch's first block start
-    for name, off, nb in cap:
-        if name != "attn_o":
-            continue
-        blk = t[off // 2: off // 2 + nb]
-        t0 = blk[:, 0].min()
-        nA = nb - a.o_tiles
-        f = lambda v: [round(float(x) / TICKS_PER_US, 2) for x in (v.min(), v.float().median(), v.max())]  # noqa: E731
-        print(json.dumps({"attn_o_roles": {"attn_end_min_med_max": f(blk[:nA, 1] - t0),
-                                           "o_start_min_med_max": f(blk[nA:, 0] - t0),
-                                           "o_end_min_med_max": f(blk[nA:, 1] - t0)}}))
     for x in live[:14]:
         print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in x.items() if k not in ("t0", "t1")}))
     if a.json:

@@ -168,7 +168,7 @@ __device__ __forceinline__ void load_k_regs(uint4 (&kf)[8], const bf16_t* kb0, c
 __host__ __device__ constexpr int dec_ml_off(int nw) { return nw * CHUNK * D_ * 2; }
 
 // Output stores. SC1: write-through (device-coherent) stores, for a consumer that reads the
-// result inside the same launch (attn_o_kernel: the o_proj blocks load it with sc1 loads)
+// result inside the same launch (a consumer in the same launch loads it with sc1 loads)
 template <bool SC1>
 __device__ __forceinline__ void out_store16(bf16_t* base, size_t elem, uint4 v) {
   if constexpr (SC1) {
@@ -943,15 +943,14 @@ __global__ __launch_bounds__(64 * NW) void attn_flash_kernel(AttnArgs a, int laz
 // flash configuration for a head group of G (ct = 0: not supported): waves NW = 8 when G | 8
 // (G query groups of 8 / G), 6 for G = 3, 6; two 16-query column tiles per wave for G <= 4
 // (Llama: 64-query blocks), one above (16-query blocks keep >= one block per CU at 2k tokens for
-// the 1-2 KV-head layouts; VGATE_FLASH_CT=2 forces two)
+// the 1-2 KV-head layouts; two there were slower at every length, profiles/r3_flash_split.log)
 struct FlashCfg { int ct, nw; };
 static FlashCfg flash_cfg(const AttnArgs& a) {
   if (a.D != D_ || a.BS != BS_ || a.Hkv <= 0 || a.Hq % a.Hkv) return {0, 0};
   const int G = a.Hq / a.Hkv;
   const int nw = 8 % G == 0 ? 8 : (6 % G == 0 ? 6 : 0);
   if (nw == 0) return {0, 0};
-  static const int force = [] { const char* e = getenv("VGATE_FLASH_CT"); return e ? atoi(e) : 0; }();
-  const int ct = G <= 4 ? 2 : (force == 2 ? 2 : 1);
+  const int ct = G <= 4 ? 2 : 1;
   return {ct, nw};
 }
 
@@ -996,12 +995,10 @@ void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
   if (fc.ct > 0) {
     AttnArgs f = a;
     f.tl = tl_take("attn_flash", tiles * a.Hkv);
-    // experiments: VGATE_FLASH_NST (ring stages 2 / 3 / 4), VGATE_FLASH_LAZY (0: rescale every chunk)
-    static const int nst = [] { const char* e = getenv("VGATE_FLASH_NST"); const int v = e ? atoi(e) : 2; return v <= 2 ? 2 : 4; }();
-    static const int lazy = [] { const char* e = getenv("VGATE_FLASH_LAZY"); return e ? atoi(e) : 1; }();
-    static const int swp = [] { const char* e = getenv("VGATE_FLASH_SWP"); return e ? atoi(e) : 0; }();
-    const size_t lds = (size_t)(nst == 2 ? 2 : 4) * FL_STAGE + (size_t)a.max_blocks * 4;
-    const size_t lds4 = (size_t)4 * FL_STAGE + (size_t)a.max_blocks * 4;
+    // a 2-stage K/V ring with the lazy rescale (4 stages and eager rescale measured no faster:
+    // profiles/r3_flash_split.log)
+    constexpr int lazy = 1;
+    const size_t lds = (size_t)2 * FL_STAGE + (size_t)a.max_blocks * 4;
     // K split of the long causal ranges (zs parts per KV head, adjacent in grid.x) when the
     // workspace holds every wave's partials: 2 parts while the step's working blocks fill less
     // than two waves of the chip's block slots (CT = 2 blocks hold a CU alone, CT = 1 two), 4
@@ -1009,8 +1006,7 @@ void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
     // only there: Llama-3-70B TP=8 2048 39.8 -> 31.9 us, lost at Qwen 2048 46 -> 50, Llama-8B
     // 1024 35 -> 45); none once the blocks alone fill two waves (they balance the triangle)
     int zs = 1;
-    static const int max_parts = [] { const char* e = getenv("VGATE_FLASH_PARTS"); const int v = e ? atoi(e) : 4; return v >= 4 ? 4 : (v >= 2 ? 2 : 1); }();
-    if (!swp && f.fl_ws != nullptr && f.fl_tickets != nullptr) {
+    if (f.fl_ws != nullptr && f.fl_tickets != nullptr) {
       const int qpb = 16 * fc.ct * (fc.nw / (a.Hq / a.Hkv));
       const size_t leaders = (size_t)tiles * 16 / qpb + (size_t)a.S + 1;
       const size_t slots = leaders * a.Hkv * fc.nw;
@@ -1018,16 +1014,10 @@ void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
       const size_t cap = (size_t)cu_count() * (fc.ct == 2 ? 1 : 2);
       if (blocks < 2 * cap) zs = 2;
       if (blocks * 4 <= cap) zs = 4;
-      zs = min(zs, max_parts);
       if (slots > 32768 || slots * zs * (fc.ct * 4 + 1) * 1024 > f.fl_ws_bytes) zs = 1;
     }
     const dim3 grid(a.Hkv * zs, tiles, 1), block(64 * fc.nw);
-#define VG_FL(CT_, NW_)                                                                                      \
-    do {                                                                                                     \
-      if (swp) hipLaunchKernelGGL((attn_flash_kernel<CT_, NW_, 4, true>), grid, block, lds4, st, f, lazy);     \
-      else if (nst == 2) hipLaunchKernelGGL((attn_flash_kernel<CT_, NW_, 2, false>), grid, block, lds, st, f, lazy); \
-      else hipLaunchKernelGGL((attn_flash_kernel<CT_, NW_, 4, false>), grid, block, lds, st, f, lazy);         \
-    } while (0)
+#define VG_FL(CT_, NW_) hipLaunchKernelGGL((attn_flash_kernel<CT_, NW_, 2, false>), grid, block, lds, st, f, lazy)
     if (fc.nw == 8) {
       if (fc.ct == 2) VG_FL(2, 8); else VG_FL(1, 8);
     } else {
@@ -1053,93 +1043,6 @@ void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
   }
 }
 
-// ------------------------------------------------- attention + o_proj in one launch ----
-// A decode step's o_proj streams 4.7-33 MB of weights that do not depend on the attention
-// output, yet as its own launch it starts only after the attention grid has drained (a kernel
-// boundary) and then pays its first HBM round trip. attn_o_kernel runs both as block roles of
-// ONE grid: blocks [0, nA) are the attention blocks of launch_attention (decode partitions +
-// prefill tiles, KV-head major), blocks [nA, nA + nO) are o_proj column tiles. An o_proj block
-// loads its whole weight k-range into registers and prefetches its residual words at launch —
-// overlapped with attention — then waits for the attention blocks' arrivals and finishes with
-// one round trip for the activations.
-//
-// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1 table):
-// every attention output byte is stored write-through (sc1, 16 / 8 B), each attention block's
-// waves drain their stores (vmcnt(0)) and meet at a barrier, then one lane adds 1 to
-// sync[0] (agent-scope atomic); one lane of each o_proj block polls sync[0] with sc1 loads
-// (s_sleep between polls, bounded), the block meets at a barrier and loads the activations
-// with sc1 loads only. The last o_proj block to finish (sync[32] ticket) zeroes both words,
-// so the counters are ready for the next launch (graph replays included). Producers never
-// wait on consumers and the host launches the fused form only when the whole grid is
-// co-resident (occupancy x CUs), so no dispatch order is assumed.
-constexpr int AO_SYNC_STRIDE = 32;  // sync words on separate 128-B lines
-
-template <int KMAX>
-__device__ __forceinline__ void oproj_tile(const GemmParams& p, int tile, uint32_t* sync, uint32_t nA, uint32_t nO,
-                                           char* smem) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int KT = p.K >> 5;
-  const int kbeg = (KT * wid) / nw, kend = (KT * (wid + 1)) / nw;  // host: kend - kbeg <= KMAX
-  const int r16 = lane & 15;
-  // 1) the wave's whole weight range in flight at launch (clamped duplicates past kend)
-  const uint4* wb = p.wp + (size_t)tile * KT * 64 + lane;
-  uint4 w[KMAX];
-#pragma unroll
-  for (int u = 0; u < KMAX; ++u) w[u] = ld_nt16(wb + (size_t)min(kbeg + u, kend - 1) * 64);
-  EpiPre<1> pre;
-  if (wid == 0) epi_pre_a<1, EPI_BF16>(p, pre, r16, tile, 4 * (lane >> 4));
-  // 2) wait for every attention block
-  if (threadIdx.x == 0) {
-    uint32_t spins = 0;
-    while (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nA) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 20)) break;  // bounded: never hang the GPU (the result is then wrong)
-    }
-  }
-  __syncthreads();
-  // 3) activations: rows r16 < M of this wave's k-range, device-coherent loads
-  const bool xok = r16 < p.M;
-  const uint32_t xoff = (uint32_t)(((size_t)r16 * p.lda + 8 * (lane >> 4)) * 2);
-  uint4 xa[KMAX];
-#pragma unroll
-  for (int u = 0; u < KMAX; ++u) {
-    const f32x4 v = ld_sc1_x4(reinterpret_cast<const float*>(p.x), xoff + (uint32_t)(min(kbeg + u, kend - 1) * 64));
-    xa[u] = (xok && kbeg + u < kend) ? __builtin_bit_cast(uint4, v) : make_uint4(0, 0, 0, 0);
-  }
-  f32x4 acc[1][1] = {{f32x4{0.f, 0.f, 0.f, 0.f}}};
-#pragma unroll
-  for (int u = 0; u < KMAX; ++u) acc[0][0] = mfma16(as_bf16x8(w[u]), as_bf16x8(xa[u]), acc[0][0]);
-  const float ssr[1] = {0.f};
-  gemm_finish<1, 1, EPI_BF16, 0, true>(p, acc, ssr, smem, 0, tile, pre);
-  // 4) the last o_proj block re-arms the counters for the next launch
-  if (threadIdx.x == 0) {
-    const uint32_t d = __hip_atomic_fetch_add(sync + AO_SYNC_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (d == nO - 1) {
-      __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(sync + AO_SYNC_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-template <int KMAX>
-__global__ __launch_bounds__(512) void attn_o_kernel(AttnArgs a, int dec_seqs, int dec_blocks, int nx, GemmParams p,
-                                                     uint32_t* sync, int nO) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  TLScope tl_scope(a.tl);
-  const int nA = nx * a.Hkv;
-  const int b = blockIdx.x;
-  if (b < nA) {
-    const int bx = b % nx, h = b / nx;
-    if (bx < dec_blocks) decode_block<true>(a, bx % dec_seqs, h, bx / dec_seqs, smem);
-    else prefill_body<true>(a, bx - dec_blocks, h, smem);
-    drain_stores();  // this wave's write-through output stores are device-visible
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  oproj_tile<KMAX>(p, b - nA, sync, (uint32_t)nA, (uint32_t)nO, smem);
-}
-
 static int cu_count() {
   static const int n = [] {
     int dev = 0, v = 0;
@@ -1148,45 +1051,6 @@ static int cu_count() {
     return v > 0 ? v : 1;
   }();
   return n;
-}
-
-template <int KMAX>
-static int ao_resident(int threads, size_t lds) {  // co-resident blocks of the fused grid (fixed launch shape)
-  static const int cap = [threads, lds] {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_o_kernel<KMAX>, threads, lds) != hipSuccess) return 0;
-    return n * cu_count();
-  }();
-  return cap;
-}
-
-bool launch_attention_o(const AttnArgs& a, int dec_seqs, const GemmArgs& g, uint32_t* sync, hipStream_t st) {
-  const int G = a.Hq / a.Hkv;
-  const int tiles = a.num_tiles > 0 ? a.num_tiles : 0;
-  const int dec_blocks = dec_seqs > 0 ? dec_seqs * a.num_parts : 0;
-  const int nx = dec_blocks + tiles;
-  if (sync == nullptr || g.M <= 0 || g.M > 16 || nx <= 0 || G > 8 || g.K % 32 != 0 || g.N % 16 != 0) return false;
-  if (dec_seqs > 0 && a.num_parts > 1 && a.tickets == nullptr) return false;  // needs the in-launch merge
-  if (g.epi != EPI_BF16 || g.row_idx != nullptr || g.norm_w != nullptr || g.rownorm) return false;
-  constexpr int NW = 8;
-  const int KT = g.K / 32;
-  const int per = (KT + NW - 1) / NW;
-  if (per > 16) return false;
-  const int nA = nx * a.Hkv, nO = g.N / 16;
-  const size_t lds = (size_t)(attn_lds_bytes(NW) > red_bytes<1, 1>(NW) + ssq_bytes<1>(NW) + 16
-                                  ? attn_lds_bytes(NW) : red_bytes<1, 1>(NW) + ssq_bytes<1>(NW) + 16);
-  const int cap = per <= 8 ? ao_resident<8>(64 * NW, lds) : ao_resident<16>(64 * NW, lds);
-  if (nA + nO > cap) return false;
-  GemmParams p{};
-  p.x = g.x; p.lda = g.lda; p.M = g.M; p.wp = reinterpret_cast<const uint4*>(g.wp); p.N = g.N; p.K = g.K;
-  p.bias = g.bias; p.res = g.res; p.ldr = g.ldr; p.out = g.out; p.ldo = g.ldo; p.splitk = 1;
-  AttnArgs b = a;
-  b.tl = tl_take("attn_o", nA + nO);
-  if (per <= 8)
-    hipLaunchKernelGGL(attn_o_kernel<8>, dim3(nA + nO), dim3(64 * NW), lds, st, b, dec_seqs, dec_blocks, nx, p, sync, nO);
-  else
-    hipLaunchKernelGGL(attn_o_kernel<16>, dim3(nA + nO), dim3(64 * NW), lds, st, b, dec_seqs, dec_blocks, nx, p, sync, nO);
-  return true;
 }
 
 void launch_attn_decode(const AttnArgs& a, hipStream_t st) {

@@ -45,16 +45,8 @@
 
 namespace vgate {
 
-int g_tail_split = -1;  // -1: VGATE_TAIL_SPLIT (default on); 0 / 1: set_tail_split (tests)
-void set_tail_split(int on) { g_tail_split = on; }
-int g_dec_u = -100;  // -100: VGATE_DEC_U; else the forced decode register group size (tests, A/B)
+int g_dec_u = -100;  // -100: the launcher's rule; else the forced decode register group size (tests)
 void set_dec_u(int u) { g_dec_u = u; }
-int g_dec_bal = -1;
-int g_awq_lds = -1;
-int g_dec_rot = -1;
-void set_dec_rot(int on) { g_dec_rot = on; }
-void set_awq_lds(int on) { g_awq_lds = on; }
-void set_dec_bal(int on) { g_dec_bal = on; }
 
 VG_EXTERN_EPI(EPI_BF16)
 VG_EXTERN_EPI(EPI_F32)
@@ -132,12 +124,6 @@ static GemmParams to_params(const GemmArgs& g) {
   p.k_cache = g.k_cache; p.v_cache = g.v_cache; p.hq = g.hq; p.hkv = g.hkv; p.bs = g.bs;
   p.scales = g.scales; p.zeros = g.zeros; p.group = g.group; p.szp = g.awq_szp;
   p.dbg_ts = g.dbg_ts;
-  // profiling only (benchmarks, never in a serving config): VGATE_GEMM_PROBE=1 skips the decode
-  // kernels' activation loads (garbage results) to price them against the weight stream
-  static const int probe = [] { const char* e = getenv("VGATE_GEMM_PROBE"); return e ? atoi(e) : 0; }();
-  p.probe = probe;
-  static const int rot = [] { const char* e = getenv("VGATE_DEC_ROT"); return e ? atoi(e) : 0; }();
-  p.rot = g_dec_rot >= 0 ? g_dec_rot : rot;
   p.hg = g.hg; p.hg_gamma = g.hg_gamma; p.ssp_out = g.ssp_out; p.ssp_in = g.ssp_in; p.ssn = g.ssn;
   return p;
 }

@@ -47,12 +47,11 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
   TLScope tl_scope(p.dbg_ts);
   const int KT = p.K >> 5;
   const SplitPos sp = split_pos(p);
-  const int nt0 = (p.tail_full > 0 ? sp.tile : (int)blockIdx.x) * NTB;
+  const int nt0 = (int)blockIdx.x * NTB;
   const int m_base = blockIdx.y * 16 * MB;
-  // this block's k-slice, then this wave's contiguous range inside it (p.rot: range index rotated
-  // by the block index, so the launch's blocks spread their activation requests over the slice)
+  // this block's k-slice, then this wave's contiguous range inside it
   const int s0 = (KT * sp.slice) / sp.nsl, s1 = (KT * (sp.slice + 1)) / sp.nsl;
-  const int wr = p.rot ? (wid + (int)blockIdx.x) % nw : wid;
+  const int wr = wid;
   int kbeg = s0 + ((s1 - s0) * wr) / nw;
   int kend = s0 + ((s1 - s0) * (wr + 1)) / nw;
   if constexpr (XP > 1) {  // waves take whole packs of XP k-steps (K % (32 * XP) == 0 on host)
@@ -97,8 +96,8 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
     for (int u = 0; u < U; u += XP)  // packed: slot u holds the raw load for k-steps u..u+XP-1
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb)
-        a[u][mb] = (xok[mb] && !(p.probe & 1)) ? *reinterpret_cast<const uint4*>(xrow[mb] + min(k0 + u, kend - XP) * 32)
-                                               : make_uint4(0, 0, 0, 0);
+        a[u][mb] = xok[mb] ? *reinterpret_cast<const uint4*>(xrow[mb] + min(k0 + u, kend - XP) * 32)
+                           : make_uint4(0, 0, 0, 0);
   };
   auto unpack_grp = [&](uint4 (&a)[U][MB]) {
     if constexpr (XP > 1) {
@@ -154,9 +153,8 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
       mma_grp(b, a, kt);
     }
   } else if (ngrp > 0) {
-    // group g of the wave starts at k-step gk(g); p.rot rotates the group order by the block index
-    const int gr = p.rot ? (int)(blockIdx.x % (unsigned)ngrp) : 0;
-    auto gk = [&](int g) { const int q = g + gr; return kbeg + (q < ngrp ? q : q - ngrp) * U; };
+    // group g of the wave starts at k-step gk(g)
+    auto gk = [&](int g) { return kbeg + g * U; };
     uint4 b0[U][NTB], a0[U][MB], b1[U][NTB], a1[U][MB];
     load_grp(b0, a0, gk(0));
     if (epi_thr) epi_pre_b<NTB, EPI>(p, pre, nt0, 4 * (lane >> 4));  // dependent on phase A only
@@ -172,165 +170,6 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
   }
   if (epi_thr && !pre_b) epi_pre_b<NTB, EPI>(p, pre, nt0, 4 * (lane >> 4));
   gemm_finish<MB, NTB, EPI, NORM, MB == 1>(p, acc, ssr, smem, m_base, nt0, pre);
-}
-
-// ---- balanced decode GEMM: every CU streams the same bytes (wide N, M <= 16) ----
-// A one-tile-per-block grid of q * ncu + r tiles (gate_up: 1120 = 4 x 256 + 96) leaves r CUs with
-// one tile more than the rest, and the launch lasts as long as those CUs (block durations 8.3 ->
-// 12.4 us, profiles/r3_head0_timeline.log). Here the grid is ONE block per CU (LDS-pinned): block b
-// owns full tiles [q b, q b + q), WPT waves per tile splitting its K, and P = r S / ncu PIECES of the
-// r tail tiles, each tail tile cut into S k-slices (gate_up: S = 8, 3 pieces of 6 k-steps per CU),
-// so every CU moves q tiles + r / ncu of a tile. The pieces run on P extra waves that start with the
-// launch and own nothing else: piece -> sc1 slab -> drain -> ticket, and the piece whose ticket comes
-// last sums the S slabs in piece order and runs the epilogue — all while the full tiles still stream,
-// so the cross-CU combine is off the launch's critical path (a combine at the END costs ~3 us:
-// splitk-seam, MI355X_MICROARCH.md). Fixed summation orders: bit-reproducible.
-template <int U, int EPI, int NORM, int XP>
-__device__ __forceinline__ void bal_stream(const GemmParams& p, const uint4* wbase, int kbeg, int kend, f32x4& acc,
-                                           float& ssr, const bf16_t* xrow, bool xok, int r16) {
-  constexpr int R = 16 / XP;
-  auto load_grp = [&](uint4 (&b)[U], uint4 (&a)[U], int k0) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) b[u] = ld_nt16(wbase + (size_t)min(k0 + u, kend - 1) * 64);
-#pragma unroll
-    for (int u = 0; u < U; u += XP)
-      a[u] = (xok && !(p.probe & 1)) ? *reinterpret_cast<const uint4*>(xrow + min(k0 + u, kend - XP) * 32)
-                                     : make_uint4(0, 0, 0, 0);
-  };
-  auto mma_grp = [&](const uint4 (&b)[U], uint4 (&a)[U], int k0) {
-    if constexpr (XP > 1) {
-      const uint32_t lom = r16 < R ? ~0u : 0u;
-#pragma unroll
-      for (int u = 0; u < U; u += XP) {
-        const uint4 v = a[u];
-        const uint4 v1 = row_ror<R>(v);
-        a[u] = and_mask(v, lom);
-        a[u + 1] = and_mask(v1, lom);
-        if constexpr (XP == 4) {
-          const uint4 v2 = row_ror<2 * R>(v), v3 = row_ror<3 * R>(v);
-          a[u + 2] = and_mask(v2, lom);
-          a[u + 3] = and_mask(v3, lom);
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (k0 + u >= kend) a[u] = make_uint4(0, 0, 0, 0);
-    if constexpr (NORM == 2) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) a[u] = norm_frag<2>(a[u], nullptr, 0, ssr);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) acc = mfma16(as_bf16x8(b[u]), as_bf16x8(a[u]), acc);
-  };
-  const int ngrp = (kend - kbeg + U - 1) / U;
-  if (ngrp <= 0) return;
-  int kt = kbeg;
-  uint4 b0[U], a0[U], b1[U], a1[U];
-  load_grp(b0, a0, kt);
-  int g = 0;
-  for (; g + 2 <= ngrp; g += 2) {
-    load_grp(b1, a1, kt + U);
-    mma_grp(b0, a0, kt);
-    if (g + 2 < ngrp) load_grp(b0, a0, kt + 2 * U);
-    mma_grp(b1, a1, kt + U);
-    kt += 2 * U;
-  }
-  if (g < ngrp) mma_grp(b0, a0, kt);
-}
-
-// BalArgs packed into GemmParams' spare fields by the launcher: q = full tiles per block, S = slices
-// per tail tile, P = pieces per block, WPT = waves per full tile (blockDim = 64 (q WPT + P))
-template <int U, int EPI, int NORM, int XP>
-__global__ __launch_bounds__(768) void gemm_bal_kernel(GemmParams p, int q, int S, int P, int WPT) {
-  static_assert(NORM == 0 || NORM == 2, "balanced decode GEMM: no norm, or the folded-gamma row scale");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  TLScope tl_scope(p.dbg_ts);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int KT = p.K >> 5;
-  const int ncu = gridDim.x, b = blockIdx.x;
-  const int r16 = lane & 15, m = r16;
-  const int mrow = XP > 1 ? r16 % (16 / XP) : r16;
-  const bool xok = mrow < p.M;
-  const bf16_t* xrow = p.x + (size_t)row_of(p, mrow) * p.lda + 8 * (lane >> 4) + (XP > 1 ? (r16 / (16 / XP)) * 32 : 0);
-  const int nfull = q * WPT;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  float ssr = 0.f;
-  f32x4* red = reinterpret_cast<f32x4*>(smem);                       // [nfull][64]
-  float* ssq = reinterpret_cast<float*>(smem + (size_t)nfull * 1024);  // [nfull][16]
-  if (wid >= nfull) {
-    // ---- a piece of a tail tile: k-slice (piece % S) of tail tile q ncu + piece / S ----
-    const int piece = P * b + (wid - nfull);
-    const int tt = q * ncu + piece / S, slice = piece % S;
-    const int kl = KT / S;
-    const uint4* wbase = p.wp + (size_t)tt * KT * 64 + lane;
-    bal_stream<U, EPI, NORM, XP>(p, wbase, slice * kl, slice * kl + kl, acc, ssr, xrow, xok, r16);
-    float ss = ssr;
-    if constexpr (NORM) {
-      ss += xor16(ss);
-      ss += xor32(ss);
-    }
-    // slab [tail tile][slice]: 64 lanes x 16 B partial tile + 16 row sums of squares
-    constexpr int SLAB = 64 * 4 + 16;  // floats
-    const int tidx = tt - q * ncu;
-    float* slab = p.slabs + ((size_t)tidx * S + slice) * SLAB;
-    st_sc1_x4(p.slabs, (uint32_t)(((size_t)tidx * S + slice) * SLAB * 4 + lane * 16), acc);
-    if (NORM && lane < 16) st_sc1(slab + 256 + lane, ss);
-    drain_stores();
-    uint32_t old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add(p.counters + tidx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    old = __builtin_amdgcn_readfirstlane(old);
-    if (old != (uint32_t)(S - 1)) return;
-    if (lane == 0) __hip_atomic_store(p.counters + tidx, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // last arriver: all S slabs in slice order (every load issued before the first add)
-    const uint32_t base = (uint32_t)((size_t)tidx * S * SLAB * 4);
-    f32x4 r[SK_MAX];
-#pragma unroll
-    for (int z = 0; z < SK_MAX; ++z) r[z] = ld_sc1_x4(p.slabs, base + (uint32_t)(min(z, S - 1) * SLAB * 4 + lane * 16));
-    float sv[SK_MAX];
-    if constexpr (NORM) {
-#pragma unroll
-      for (int z = 0; z < SK_MAX; ++z) sv[z] = ld_sc1(p.slabs + (size_t)tidx * S * SLAB + min(z, S - 1) * SLAB + 256 + m);
-    }
-    f32x4 v[1] = {r[0]};
-    float ss_row = NORM ? sv[0] : 0.f;
-#pragma unroll
-    for (int z = 1; z < SK_MAX; ++z)
-      if (z < S) {
-        v[0] += r[z];
-        if constexpr (NORM) ss_row += sv[z];
-      }
-    if constexpr (NORM) v[0] *= rsqrtf(ss_row / (float)p.K + p.eps);
-    epilogue<1, EPI, false>(p, v, m, tt, 4 * (lane >> 4), EpiPre<1>{}, m < p.M);
-    return;
-  }
-  // ---- a k-range of a full tile ----
-  const int tile = q * b + wid / WPT, part = wid % WPT;
-  const int kr = KT / WPT;
-  const uint4* wbase = p.wp + (size_t)tile * KT * 64 + lane;
-  bal_stream<U, EPI, NORM, XP>(p, wbase, part * kr, part * kr + kr, acc, ssr, xrow, xok, r16);
-  red[wid * 64 + lane] = acc;
-  if constexpr (NORM) {
-    float ss = ssr;
-    ss += xor16(ss);
-    ss += xor32(ss);
-    if (lane < 16) ssq[wid * 16 + lane] = ss;
-  }
-  // the tile's WPT waves meet (LDS only: the piece waves never join, so a named barrier is not
-  // needed — every full-tile wave passes this point once, the piece waves have exited or never wait)
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  if (part != 0) return;
-  const int w0 = wid;
-  f32x4 v[1] = {red[w0 * 64 + lane]};
-  float ss_row = NORM ? ssq[w0 * 16 + m] : 0.f;
-  for (int w = 1; w < WPT; ++w) {
-    v[0] += red[(w0 + w) * 64 + lane];
-    if constexpr (NORM) ss_row += ssq[(w0 + w) * 16 + m];
-  }
-  if constexpr (NORM) v[0] *= rsqrtf(ss_row / (float)p.K + p.eps);
-  epilogue<1, EPI, false>(p, v, m, tile, 4 * (lane >> 4), EpiPre<1>{}, m < p.M);
 }
 
 // ---- AWQ W4A16 ----
@@ -699,8 +538,8 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
   TLScope tl_scope(p.dbg_ts);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int KQ = p.K >> 7;
-  const SplitPos sp = split_pos(p);  // (tail split: the last tiles run as K halves)
-  const int nt0 = (p.tail_full > 0 ? sp.tile : (int)blockIdx.x) * NTB;
+  const SplitPos sp = split_pos(p);
+  const int nt0 = (int)blockIdx.x * NTB;
   const int s0 = (KQ * sp.slice) / sp.nsl, s1 = (KQ * (sp.slice + 1)) / sp.nsl;
   const int qbeg = s0 + ((s1 - s0) * wid) / nw;
   const int qend = s0 + ((s1 - s0) * (wid + 1)) / nw;
@@ -728,12 +567,11 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
 #pragma unroll
       for (int j = 0; j < NTB; ++j) {
         w[u][j] = ld_nt16(wbase + ((size_t)j * KQ + kq) * 64);
-        sz[u][j] = (p.probe & 2) ? make_uint4(0x3c003c00u, 0x3c003c00u, 0, 0) : szbase[((size_t)j * KQ + kq) * 4];
+        sz[u][j] = szbase[((size_t)j * KQ + kq) * 4];
       }
 #pragma unroll
       for (int v = 0; v < XL; ++v)
-        xa[u][v] = (xok && !(p.probe & 1)) ? *reinterpret_cast<const uint4*>(xrow + (kq * 4 + v * XP) * 32)
-                                           : make_uint4(0, 0, 0, 0);
+        xa[u][v] = xok ? *reinterpret_cast<const uint4*>(xrow + (kq * 4 + v * XP) * 32) : make_uint4(0, 0, 0, 0);
       if constexpr (NORM == 1) {
 #pragma unroll
         for (int v = 0; v < XL; ++v) ga[u][v] = *reinterpret_cast<const uint4*>(grow + (kq * 4 + v * XP) * 32);
@@ -843,123 +681,6 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
     if (g < ngrp) mma_grp(wa, sa, xa, gaa, kq);
   }
   gemm_finish<1, NTB, EPI, NORM, false>(p, acc, ssr, smem, 0, nt0, EpiPre<NTB>{});
-}
-
-// ---- AWQ W4A16 decode, activation slice shared through LDS (M <= 16) ----
-// At decode batch sizes the activations of a k-quad outweigh its int4 weights (8 rows x 128 k bf16
-// = 2 KiB vs a 1 KiB int4 fragment), so the one-tile-per-block kernels above move 2-3x more bytes
-// of activations and scales through each CU than weight bytes from HBM (awq_stream gate_up spans
-// 9.3 us for 13.8 MB; with its activation and scale loads switched off 6.6 us,
-// profiles/r2_awq_load_probe.log). Here a block owns T adjacent column tiles and one K slice:
-//   * a LOADER wave (the last one) DMAs the slice of x into LDS in MFMA B-fragment order
-//     (global_load_lds_dwordx4: 1 KiB per k-step, no VGPRs), waits for it and arrives at the
-//     block barrier;
-//   * each of the T tile waves issues its WHOLE int4 k-slice and packed group scales (every
-//     weight byte of the launch requested in the first microsecond), joins the barrier without
-//     waiting for them (raw s_barrier: loads stay in flight), then reads x fragments from LDS;
-//   * the raw-nibble identity sum_k x (v - z) s = s sum_k x (128 + v) - (128 s + s z) X gives the
-//     group scale per k-quad after four MFMAs (X = the k-quad's activation sum, from the LDS
-//     fragments); the producer's RMSNorm hand-off (NORM 3) or none (NORM 0);
-//   * S K-slices of a tile meet by slab + ticket (last arriver sums them in slice order).
-// One x slice per block instead of one per tile; T x the activation reuse.
-template <int Q, int EPI, int NORM>
-__global__ __launch_bounds__(576) void awq_lds_kernel(GemmParams p, int T, int S) {
-  static_assert(NORM == 0 || NORM == 3, "awq_lds_kernel: no norm, or the producer's RMSNorm hand-off");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  TLScope tl_scope(p.dbg_ts);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int KQ = p.K >> 7;
-  const int ngroups = (p.N >> 4) / T;
-  const int slice = blockIdx.x / ngroups, grp = blockIdx.x % ngroups;
-  const int q0 = (KQ * slice) / S, q1 = (KQ * (slice + 1)) / S, nq = q1 - q0;
-  const int r16 = lane & 15;
-  uint4* xs = reinterpret_cast<uint4*>(smem);  // [4 nq][64] B fragments of the slice
-  if (wid == T) {
-    // loader: rows >= M repeat row M - 1 (their output columns are never stored)
-    const bf16_t* xr = p.x + (size_t)row_of(p, r16) * p.lda + 8 * (lane >> 4) + (size_t)q0 * 128;
-    // pieces in a block-rotated order: the launch's loaders do not all hit the same x lines at once
-    const int np = 4 * nq, r0 = (int)(blockIdx.x % (unsigned)np);
-    for (int i = 0; i < np; ++i) {
-      const int t = i + r0 < np ? i + r0 : i + r0 - np;
-      glds16(xr + t * 32, __builtin_amdgcn_readfirstlane(lds_addr_of(xs + t * 64)));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    return;
-  }
-  const int nt = grp * T + wid;
-  const uint4* wb = p.wp + (size_t)nt * KQ * 64 + lane;
-  const uint4* sb = reinterpret_cast<const uint4*>(p.szp) + (size_t)nt * KQ * 4 + (lane >> 4);
-  uint4 w[Q], sz[Q];
-#pragma unroll
-  for (int g = 0; g < Q; ++g) {
-    const int kq = q0 + min(g, nq - 1);  // clamped past the slice: issued unconditionally, never consumed
-    w[g] = ld_nt16(wb + (size_t)kq * 64);
-    sz[g] = sb[(size_t)kq * 4];
-  }
-  float ss = 0.f;
-  if constexpr (NORM == 3) {
-    ss = prenorm_ss(p, r16, lane >> 4);
-    ss += xor16(ss);
-    ss += xor32(ss);
-  }
-  asm volatile("s_barrier" ::: "memory");  // x slice in LDS; the weight loads stay in flight
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int g = 0; g < Q; ++g) {
-    if (g < nq) {  // wave-uniform
-      uint4 b[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) b[u] = xs[(g * 4 + u) * 64 + lane];
-      float X = 0.f;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float f[8];
-        unpack8(b[u], f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) X += f[j];
-      }
-      X += xor16(X);
-      X += xor32(X);
-      f32x4 pr = {0.f, 0.f, 0.f, 0.f};
-      pr = mfma16(raw8(w[g].x), as_bf16x8(b[0]), pr);
-      pr = mfma16(raw8(w[g].y), as_bf16x8(b[1]), pr);
-      pr = mfma16(raw8(w[g].z), as_bf16x8(b[2]), pr);
-      pr = mfma16(raw8(w[g].w), as_bf16x8(b[3]), pr);
-      const uint4 q = sz[g];
-      const float s4[4] = {bf_lo(q.x), bf_hi(q.x), bf_lo(q.y), bf_hi(q.y)};
-      const float z4[4] = {bf_lo(q.z), bf_hi(q.z), bf_lo(q.w), bf_hi(q.w)};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] = fmaf(s4[i], pr[i], fmaf(-fmaf(128.f, s4[i], z4[i]), X, acc[i]));
-    }
-  }
-  // lane holds D[n = 4 (l >> 4) + i][m = l & 15]; the RMSNorm row scale is linear: per slice
-  if constexpr (NORM == 3) acc *= rsqrtf(ss / (float)p.K + p.eps);
-  const int m = r16, nsub = 4 * (lane >> 4);
-  if (S == 1) {
-    f32x4 v[1] = {acc};
-    epilogue<1, EPI, false>(p, v, m, nt, nsub, EpiPre<1>{}, m < p.M);
-    return;
-  }
-  constexpr int SLAB = 64 * 4;  // floats per (tile, slice)
-  const uint32_t off = (uint32_t)(((size_t)nt * S + slice) * SLAB * 4);
-  st_sc1_x4(p.slabs, off + (uint32_t)lane * 16u, acc);
-  drain_stores();
-  uint32_t old = 0;
-  if (lane == 0) old = __hip_atomic_fetch_add(p.counters + nt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  old = __builtin_amdgcn_readfirstlane(old);
-  if (old != (uint32_t)(S - 1)) return;
-  if (lane == 0) __hip_atomic_store(p.counters + nt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t base = (uint32_t)((size_t)nt * S * SLAB * 4);
-  constexpr int SMAX = 16;
-  f32x4 r[SMAX];
-#pragma unroll
-  for (int z = 0; z < SMAX; ++z) r[z] = ld_sc1_x4(p.slabs, base + (uint32_t)(min(z, S - 1) * SLAB * 4 + lane * 16));
-  f32x4 v[1] = {r[0]};
-#pragma unroll
-  for (int z = 1; z < SMAX; ++z)
-    if (z < S) v[0] += r[z];
-  epilogue<1, EPI, false>(p, v, m, nt, nsub, EpiPre<1>{}, m < p.M);
 }
 
 // ---- prefill / medium-M tile GEMM (M > 16, bf16 weights) ----
@@ -1103,10 +824,7 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(GemmParams p) {
 // ------------------------------------------------------------------ host side
 struct Plan { int waves, splitk; };
 
-extern int g_tail_split;  // gemm.hip: -1 = VGATE_TAIL_SPLIT; 0 / 1: set_tail_split (tests)
-extern int g_dec_u;       // gemm.hip: -100 = VGATE_DEC_U; else the forced decode register group size
-extern int g_dec_bal;     // gemm.hip: -1 = VGATE_DEC_BAL; 0 / 1: the balanced decode GEMM off / on
-extern int g_awq_lds;     // gemm.hip: -1 = VGATE_AWQ_LDS (default off); 0 / 1: awq_lds_kernel off / on
+extern int g_dec_u;       // gemm.hip: -100 = the launcher's rule; else the forced decode register group size (tests)
 
 inline int cu_count_gemm() {
   static const int n = [] {
@@ -1158,57 +876,6 @@ static void launch_dec_u(int u, dim3 grid, dim3 block, size_t lds, hipStream_t s
   hipLaunchKernelGGL((gemm_kernel<MB, NTB, U, EPI, NORM, true, XP>), grid, block, lds, st, p);
 }
 
-// Balanced decode GEMM (gemm_bal_kernel) when the shape fits it: wide N (>= one tile per CU), the
-// tail tiles cut into S | KT slices whose pieces spread evenly over the CUs, <= 12 waves per block
-// (the pipelined stream needs ~160 VGPRs: 3 waves per SIMD; at 16 waves it spilled and ran 2x slower).
-// Returns false (caller launches the one-tile-per-block kernel) otherwise, or when switched off
-// (set_dec_bal / VGATE_DEC_BAL=0).
-template <int EPI, int NORM>
-static bool launch_bal(GemmParams p, const GemmArgs& g, hipStream_t st) {
-  if constexpr (!(EPI == EPI_SILU || EPI == EPI_BF16 || EPI == EPI_F32) || !(NORM == 0 || NORM == 2)) {
-    return false;
-  } else {
-    static const int env_bal = [] { const char* e = getenv("VGATE_DEC_BAL"); return e ? atoi(e) : 0; }();
-    if ((g_dec_bal >= 0 ? g_dec_bal : env_bal) == 0) return false;
-    if (g.M > 16 || g.waves > 0 || g.splitk > 0 || g.ntb > 0 || g.row_idx != nullptr || g.slabs == nullptr) return false;
-    const int ncu = cu_count_gemm();
-    const int ntiles = g.N / 16, KT = g.K / 32;
-    const int q = ntiles / ncu, r = ntiles % ncu;
-    if (q < 1) return false;
-    const int xp = g.M <= 4 && KT % 4 == 0 ? 4 : (g.M <= 8 && KT % 2 == 0 ? 2 : 1);
-    int S = 0;
-    if (r == 0) {
-      S = 1;
-    } else {
-      for (int c : {2, 4, 8})
-        if (c <= SK_MAX && (r * c) % ncu == 0 && KT % c == 0 && (KT / c) % xp == 0) { S = c; break; }
-    }
-    if (S == 0) return false;
-    const int P = r == 0 ? 0 : r * S / ncu;
-    int WPT = 0;
-    for (int c : {4, 3, 2, 1})
-      if (KT % c == 0 && (KT / c) % xp == 0 && q * c + P <= 12) { WPT = c; break; }
-    if (WPT == 0) return false;
-    constexpr int SLAB = 64 * 4 + 16;
-    if ((size_t)r * S * SLAB * 4 > g.slab_bytes || r > g.max_counters) return false;
-    const int nw = q * WPT + P;
-    // >= 80 KiB of LDS: one block per CU, so the per-CU byte count is what the grid says
-    const size_t lds = std::max<size_t>((size_t)q * WPT * (1024 + 64), 80 * 1024 + 16);
-    if (p.dbg_ts == nullptr) p.dbg_ts = tl_take(EPI == EPI_SILU ? "gemm_bal_gate_up" : "gemm_bal", ncu);
-    p.splitk = 1;
-    p.tail_full = 0;
-    const int kr = KT / WPT, kl = r ? KT / S : 0;
-    auto slots = [&](int u) { return q * WPT * ((kr + u - 1) / u * u) + P * ((kl + u - 1) / u * u); };
-    const bool u6 = xp != 4 && slots(6) < slots(8);
-#define VG_BAL(UU, XP_) hipLaunchKernelGGL((gemm_bal_kernel<UU, EPI, NORM, XP_>), dim3(ncu), dim3(64 * nw), lds, st, p, q, S, P, WPT)
-    if (xp == 4) VG_BAL(8, 4);
-    else if (xp == 2) { if (u6) VG_BAL(6, 2); else VG_BAL(8, 2); }
-    else { if (u6) VG_BAL(6, 1); else VG_BAL(8, 1); }
-#undef VG_BAL
-    return true;
-  }
-}
-
 template <int MB, int NTB, int EPI, int NORM, bool AWQ>
 static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
   const int ntiles = g.N / 16;
@@ -1217,32 +884,12 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
   const int ksteps = AWQ ? g.K / 128 : g.K / 32;
   Plan pl = plan(nblk, mchunks, ksteps, MB, NTB, g.waves, g.splitk);
   if (AWQ && pl.waves > 8) pl.waves = 8;  // awq_gemm_kernel: __launch_bounds__(512)
-  // Tail split (decode, wide N): q * ncu + r one-tile blocks put q + 1 tiles on r CUs and q on the
-  // rest, and the launch lasts as long as the q + 1 CUs; cutting the r tail tiles into K halves
-  // (combined by gemm_finish's last-arriver slab hand-off) leaves every CU q tiles + at most one
-  // half (gate_up: 1120 tiles = 4 x 256 + 96). VGATE_TAIL_SPLIT=0/1 (sweeps)
-  static const int tail_env = [] { const char* e = getenv("VGATE_TAIL_SPLIT"); return e ? atoi(e) : 1; }();
-  const int tail_mode = g_tail_split >= 0 ? g_tail_split : tail_env;
-  const int ncu = cu_count_gemm();
-  int grid_x = nblk;
-  p.tail_full = 0;
-  if (!AWQ && MB == 1 && tail_mode != 0 && pl.splitk == 1 && mchunks == 1 && g.waves <= 0 && g.splitk <= 0 &&
-      nblk > ncu && nblk % ncu != 0 && nblk % ncu <= ncu / 2) {
-    const int tail = nblk % ncu;
-    const size_t need = (size_t)(nblk + tail) * 2 * (NTB * 64 * 16 + (NORM ? 16 * 4 : 0));
-    if (g.slabs != nullptr && need <= g.slab_bytes && nblk <= g.max_counters) {
-      p.tail_full = nblk - tail;
-      grid_x = nblk + tail;
-      pl.splitk = 2;  // slab stride: at most 2 slices per tile
-    }
-  }
   const size_t need_slab = (size_t)nblk * mchunks * pl.splitk * (MB * NTB * 64 * 16 + (NORM ? 16 * MB * 4 : 0));
-  if (p.tail_full == 0 && pl.splitk > 1 &&
-      (g.slabs == nullptr || need_slab > g.slab_bytes || nblk * mchunks > g.max_counters))
+  if (pl.splitk > 1 && (g.slabs == nullptr || need_slab > g.slab_bytes || nblk * mchunks > g.max_counters))
     pl.splitk = 1;  // workspace too small: fall back to one slice (still correct)
   p.splitk = pl.splitk;
   const size_t lds = red_bytes<MB, NTB>(pl.waves) + ssq_bytes<MB>(pl.waves) + 16;
-  dim3 grid(grid_x, mchunks, p.tail_full > 0 ? 1 : pl.splitk), block(64 * pl.waves);
+  dim3 grid(nblk, mchunks, pl.splitk), block(64 * pl.waves);
   if (p.dbg_ts == nullptr)
     p.dbg_ts = tl_take(AWQ ? "awq_gemm" : (EPI == EPI_QKV ? "gemm_qkv" : EPI == EPI_SILU ? "gemm_gate_up"
                                             : EPI == EPI_F32 ? "gemm_f32" : "gemm"), (int)(grid.x * grid.y * grid.z));
@@ -1255,9 +902,6 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
     else hipLaunchKernelGGL((awq_gemm_kernel<MB, NTB, EPI, NORM>), grid, block, lds, st, p);
   }
   else if constexpr (MB == 1) {
-    if constexpr (NTB == 1) {
-      if (p.tail_full == 0 && pl.splitk == 1 && launch_bal<EPI, NORM>(p, g, st)) return;
-    }
     constexpr int U = NTB == 1 ? 8 : 4;
     const int KT = g.K / 32;
     // One-tile blocks: the register group size U is chosen per launch so that a wave's whole
@@ -1269,13 +913,10 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
     // default: the round-2 rule (-1). The all-in-two-groups rule (0) was measured SLOWER in-engine:
     // gate_up at 2 x 12 needs more VGPRs, its 1120 blocks no longer fit in one round (span 12.7 ->
     // 13.4 us), and down_proj at 2 x 10 took 9.4 vs 8.8 us (profiles/r3_dec_u_negative.log)
-    static const int env_u = [] { const char* e = getenv("VGATE_DEC_U"); return e ? atoi(e) : -1; }();
-    const int force_u = g_dec_u != -100 ? g_dec_u : env_u;
-    // (tail split: the full tiles' and the halves' per-wave ranges both count)
-    const int kpw = (KT / (p.tail_full > 0 ? 1 : pl.splitk) + pl.waves - 1) / pl.waves;
-    const int kph = p.tail_full > 0 ? (KT / 2 + pl.waves - 1) / pl.waves : 0;
+    const int force_u = g_dec_u != -100 ? g_dec_u : -1;
+    const int kpw = (KT / pl.splitk + pl.waves - 1) / pl.waves;
     const int xp = g.M <= 4 && KT % 4 == 0 ? 4 : (g.M <= 8 && KT % 2 == 0 ? 2 : 1);
-    auto slots = [&](int u) { return (kpw + u - 1) / u * u + (kph + u - 1) / u * u; };
+    auto slots = [&](int u) { return (kpw + u - 1) / u * u; };
     int u = 8;
     if (NTB == 1) {
       if (force_u > 0) {
@@ -1286,8 +927,8 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
         int best = 0;
         for (int c : {6, 8, 10, 12}) {
           if (c % xp) continue;
-          const bool two = 2 * c >= kpw && (kph == 0 || 2 * c >= kph);
-          const bool best_two = best > 0 && 2 * best >= kpw && (kph == 0 || 2 * best >= kph);
+          const bool two = 2 * c >= kpw;
+          const bool best_two = best > 0 && 2 * best >= kpw;
           if (best == 0 || (two && !best_two) || (two == best_two && slots(c) < slots(best))) best = c;
         }
         u = best > 0 ? best : 8;
@@ -1386,29 +1027,10 @@ static bool launch_awq_stream(GemmParams p, const GemmArgs& g, hipStream_t st) {
   if (!one && ntb > 1) return false;
   const size_t need_slab = (size_t)nblk * sk * (ntb * 64 * 16 + (NORM ? 16 * 4 : 0));
   if (sk > 1 && (g.slabs == nullptr || need_slab > g.slab_bytes || nblk > g.max_counters)) return false;
-  // tail split as in launch_one (gate_up at 2 tiles per block: 560 = 2 x 256 + 48 blocks)
-  p.tail_full = 0;
-  int grid_x = nblk;
-  {
-    static const int tail_env = [] { const char* e = getenv("VGATE_TAIL_SPLIT"); return e ? atoi(e) : 1; }();
-    const int ncu = cu_count_gemm();
-    const int tail = nblk % ncu;
-    const size_t need = (size_t)(nblk + tail) * 2 * (ntb * 64 * 16 + (NORM ? 16 * 4 : 0));
-    if ((g_tail_split >= 0 ? g_tail_split : tail_env) != 0 && sk == 1 && g.waves <= 0 && g.splitk <= 0 && nblk > ncu &&
-        tail != 0 && tail <= ncu / 2 && g.slabs != nullptr && need <= g.slab_bytes && nblk <= g.max_counters) {
-      p.tail_full = nblk - tail;
-      grid_x = nblk + tail;
-      sk = 2;  // slab stride
-    }
-  }
   p.splitk = sk;
-  {
-    static const int probe = [] { const char* e = getenv("VGATE_AWQ_PROBE"); return e ? atoi(e) : 0; }();
-    p.probe = probe;
-  }
   const size_t lds = (size_t)w * ntb * 64 * 16 * (w > 1) + ssq_bytes<1>(w) + 16;
-  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_stream", p.tail_full > 0 ? grid_x : nblk * sk);
-  const dim3 grid(grid_x, 1, p.tail_full > 0 ? 1 : sk);
+  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_stream", nblk * sk);
+  const dim3 grid(nblk, 1, sk);
   const bool small = (qslice + w - 1) / w <= 3;
   if constexpr (EPI == EPI_QKV) {
     launch_awq_stream_ntb<EPI, NORM, 1>(p, grid, w, one, small, lds, st, g.M);
@@ -1420,63 +1042,11 @@ static bool launch_awq_stream(GemmParams p, const GemmArgs& g, hipStream_t st) {
   return true;
 }
 
-// AWQ decode with the LDS-shared activation slice (awq_lds_kernel) when it applies: M <= 16, group
-// 128 with the packed scales, no RMSNorm or the producer's hand-off (NORM 0 / 3). Picks T tiles
-// per block and S K-slices (<= 16 k-quads each) for the largest grid that stays within one block
-// per CU. Off by default (measured: 1.49 vs 1.34 ms decode step on Qwen-1.5B AWQ, profiles/
-// r3_rot_awq_lds_negative.log); set_awq_lds(1) / VGATE_AWQ_LDS=1 switches it on (tests, A/B).
-template <int EPI, int NORM>
-static bool launch_awq_lds(GemmParams p, const GemmArgs& g, hipStream_t st) {
-  if constexpr (!(NORM == 0 || NORM == 3)) {
-    return false;
-  } else {
-    static const int env = [] { const char* e = getenv("VGATE_AWQ_LDS"); return e ? atoi(e) : 0; }();
-    if ((g_awq_lds >= 0 ? g_awq_lds : env) == 0) return false;
-    if (g.M > 16 || g.group != 128 || g.awq_szp == nullptr || g.waves > 0 || g.splitk > 0 || g.ntb != 0 ||
-        g.row_idx != nullptr || g.K % 128 != 0)
-      return false;
-    const int ncu = cu_count_gemm();
-    const int ntiles = g.N / 16, KQ = g.K / 128;
-    int bestS = 0, bestT = 0, bestB = 0;
-    for (int S = 1; S <= 16 && S <= KQ; ++S) {
-      if ((KQ + S - 1) / S > 16) continue;
-      for (int T = 1; T <= 8; ++T) {
-        if (ntiles % T) continue;
-        const int blocks = S * (ntiles / T);
-        if (blocks > ncu) continue;
-        if (blocks > bestB) { bestB = blocks; bestS = S; bestT = T; }
-      }
-      if (bestB >= ncu * 7 / 8) break;  // the smallest S that nearly fills the chip
-    }
-    if (bestB == 0) return false;
-    const int S = bestS, T = bestT;
-    if (S > 1) {
-      const size_t need = (size_t)ntiles * S * 64 * 16;
-      if (g.slabs == nullptr || need > g.slab_bytes || ntiles > g.max_counters) return false;
-    }
-    p.splitk = S;
-    const int nqmax = (KQ + S - 1) / S;
-    const size_t lds = (size_t)nqmax * 4 * 1024;
-    if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_lds", bestB);
-    const dim3 grid(bestB), block(64 * (T + 1));
-#define VG_AL(QQ) hipLaunchKernelGGL((awq_lds_kernel<QQ, EPI, NORM>), grid, block, lds, st, p, T, S)
-    if (nqmax <= 4) VG_AL(4);
-    else if (nqmax <= 6) VG_AL(6);
-    else if (nqmax <= 8) VG_AL(8);
-    else if (nqmax <= 10) VG_AL(10);
-    else if (nqmax <= 12) VG_AL(12);
-    else VG_AL(16);
-#undef VG_AL
-    return true;
-  }
-}
-
 template <int NTB, int EPI, int NORM, bool AWQ>
 static void launch_m(GemmParams p, const GemmArgs& g, hipStream_t st) {
   if constexpr (AWQ) {
     // g.ntb: -1 forces the LDS-staged kernel, -2 the K-split awq_gemm_kernel (sweeps / tests)
     if constexpr (NORM != 2) {  // (the gamma-folded row-scale mode has no int4 form)
-      if (g.ntb == 0 && launch_awq_lds<EPI, NORM>(p, g, st)) return;
       if (g.ntb != -2 && launch_awq_stream<EPI, NORM>(p, g, st)) return;
       if (g.ntb != -2 && launch_awq_dec<NTB, EPI, NORM>(p, g, st)) return;
     }

@@ -23,22 +23,12 @@ struct GemmParams {
   bf16_t* k_cache; bf16_t* v_cache; int hq; int hkv; int bs;
   const bf16_t* scales; const bf16_t* zeros; int group;
   const bf16_t* szp;  // AWQ decode: fragment-packed (scale, scale * zero) [N/16][K/128][4][8]
-  int probe;          // profiling only (benchmarks/awq_sweep.py): 1 = skip activation loads, 2 = skip scale loads
   // RMSNorm hand-off for the int4 consumers (decode, TP = 1). Producer (EPI_BF16 residual GEMMs:
   // o_proj, down_proj): hg = bf16(h * gamma) of the output rows h it stores, and per-(row, 16-column
   // tile) sums of squares of h -> ssp_out [M][N/16]. Consumer (NORM == 3): x = hg (gamma already
   // applied), row scale rsqrt(sum of ssp_in[m][0..ssn) / K + eps) — no gamma loads, no x^2 pass.
   bf16_t* hg; const bf16_t* hg_gamma; float* ssp_out; const float* ssp_in; int ssn;
   unsigned long long* dbg_ts;  // per-block [start, end] realtime stamps (profiling), or null
-  // tail split (decode, one m-chunk): blocks [0, tail_full) own one column tile each over the full K;
-  // the remaining tiles are cut into 2 K halves (blocks tail_full + 2 j + {0, 1} -> tile tail_full + j),
-  // so a grid of q * 256 + r tiles runs as q whole tiles + r / 128 halves per CU instead of q or q + 1
-  // whole tiles. 0 = off (grid = (tiles, m-chunks, splitk)).
-  int tail_full;
-  // decode kernels: rotate which wave of a block takes which k-range (and, inside a wave's range,
-  // the order of its register groups) by the block index, so the blocks of a launch do not all
-  // request the same activation lines at the same instant (VGATE_DEC_ROT, A/B)
-  int rot;
 };
 
 // (column-tile block, K slice, slices) of this block: the grid decomposition of gemm_finish's hand-off
@@ -46,12 +36,6 @@ struct SplitPos {
   int tile, slice, nsl;
 };
 __device__ __forceinline__ SplitPos split_pos(const GemmParams& p) {
-  if (p.tail_full > 0) {
-    const int b = blockIdx.x;
-    if (b < p.tail_full) return SplitPos{b, 0, 1};
-    const int j = b - p.tail_full;
-    return SplitPos{p.tail_full + (j >> 1), j & 1, 2};
-  }
   return SplitPos{(int)(blockIdx.y * gridDim.x + blockIdx.x), (int)blockIdx.z, p.splitk};
 }
 

@@ -628,12 +628,9 @@ static void launch_prefill2_one(const GemmParams& p, int nz, hipStream_t st) {
 
 template <int EPI, int NORM, int NTB, int BM = 256, int BN = 128, int WM = 4, int WN = 2, int NS = 3>
 static void launch_prefill2_cfg(const GemmParams& p, int nz, hipStream_t st) {
-  // measured (profiles/r2_prefill_gemm_sched.log): MFMAs at raised priority +5-7 % on the 256 x 256
-  // tile, neutral on 256 x 128; the split DMA issue neutral to negative
-  static const int sched = [] { const char* e = getenv("VGATE_PREFILL_SCHED"); return e ? atoi(e) : 1; }();
-  if (sched == 1) launch_prefill2_one<EPI, NORM, NTB, BM, BN, WM, WN, NS, 1>(p, nz, st);
-  else if (sched == 2) launch_prefill2_one<EPI, NORM, NTB, BM, BN, WM, WN, NS, 2>(p, nz, st);
-  else launch_prefill2_one<EPI, NORM, NTB, BM, BN, WM, WN, NS, 0>(p, nz, st);
+  // MFMAs at raised priority (schedule 1): +5-7 % on the 256 x 256 tile, neutral on 256 x 128; the
+  // split DMA issue was neutral to negative (profiles/r2_prefill_gemm_sched.log)
+  launch_prefill2_one<EPI, NORM, NTB, BM, BN, WM, WN, NS, 1>(p, nz, st);
 }
 
 template <int EPI, int NORM, int NTB, int BN = 256>
@@ -700,21 +697,18 @@ static bool launch_prefill_epi(const GemmParams& p, int force_bn, int force_sk, 
   // 256 x 256 when its grid covers ~3/4 of the chip, else v2 (256 x 128, 3-deep ring)
   // when its grid still covers the chip without split-K (profiles/r2_prefill_gemm_sched.log: the
   // 256-square tile +20-35 % at >= 192 blocks, up to -30 % at 128)
-  static const int v2_mode = [] { const char* e = getenv("VGATE_PREFILL_V2"); return e ? atoi(e) : 1; }();
   const int blocks_v3 = ((p.M + 255) / 256) * (p.N % 256 == 0 ? p.N / 256 : 0);
   const int blocks_v2 = ((p.M + 255) / 256) * (p.N % 128 == 0 ? p.N / 128 : 0);
-  if (v2_mode != 0 && force_bn == 0 && force_sk == 0 && blocks_v3 >= 180) {
+  if (force_bn == 0 && force_sk == 0 && blocks_v3 >= 180) {
     // the 4-phase 256 x 256 kernel (v4: +7-22 % over the same tile with one barrier per K-tile,
-    // profiles/r2_prefill_gemm_v4.log); VGATE_PREFILL_V2=3 keeps the one-barrier tile
-    if (v2_mode == 3) launch_prefill2_cfg<EPI, NORM, NTB, 256, 256, 4, 2, 2>(p, 1, st);
-    else launch_prefill4_cfg<EPI, NORM, NTB>(p, 1, st);
+    // profiles/r2_prefill_gemm_v4.log)
+    launch_prefill4_cfg<EPI, NORM, NTB>(p, 1, st);
     return true;
   }
-  if (v2_mode != 0 && force_bn == 0 && force_sk == 0 && blocks_v2 >= 192) {
+  if (force_bn == 0 && force_sk == 0 && blocks_v2 >= 192) {
     // the 4-phase kernel on 256 x 128 (+0-8 % over the 3-deep-ring v2 at 192-256 blocks,
-    // profiles/r2_prefill_gemm_v4.log); VGATE_PREFILL_V2=3 keeps v2
-    if (v2_mode == 3) launch_prefill2_cfg<EPI, NORM, NTB>(p, 1, st);
-    else launch_prefill4_cfg<EPI, NORM, NTB, 128>(p, 1, st);
+    // profiles/r2_prefill_gemm_v4.log)
+    launch_prefill4_cfg<EPI, NORM, NTB, 128>(p, 1, st);
     return true;
   }
   if (force_bn == 256) {  // forced (tests / sweeps), split-K as chosen above

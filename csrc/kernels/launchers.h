@@ -134,12 +134,8 @@ bool launch_mlp_decode(const MlpDecodeArgs& g, hipStream_t st);
 // Default-policy read sweep of [p, p + bytes) over `blocks` workgroups (MALL warm-up).
 void launch_prefetch(const void* p, size_t bytes, int blocks, hipStream_t st);
 // bytes % 16 == 0; src / dst device pointers (pinned host memory: its device-mapped address)
-void set_tail_split(int on);
-void set_dec_u(int u);
-void set_dec_bal(int on);
-void set_awq_lds(int on);
-void set_dec_rot(int on);
-void set_flash_prefill(int on);  // prefill tiles on the flash kernel: 1 on, 0 off (16-query tiles), -1 env  // decode GEMM: rotate wave k-ranges / group order by block (1), not (0), env (-1)  // AWQ decode with the LDS-shared activation slice: 1 on, 0 off, -1 VGATE_AWQ_LDS  // balanced decode GEMM (gemm_bal_kernel): 1 on, 0 off, -1 VGATE_DEC_BAL  // decode GEMM register group: 0 auto, -1 round-2 rule, 6/8/10/12 forced, -100 env  // decode GEMM tail split on / off (-1: VGATE_TAIL_SPLIT env, default on)
+void set_dec_u(int u);  // decode GEMM register group: -100 the launcher's rule, 6 / 8 / 10 / 12 forced (tests)
+void set_flash_prefill(int on);  // prefill tiles on the flash kernel: 1 on, 0 off (16-query tiles), -1 env
 void launch_copy16(const void* src, void* dst, size_t bytes, bool to_host, hipStream_t st);
 // ids[0, n) -> ring[*slot * stride + i] (ring: device-mapped pinned host memory); with `ar` (the
 // own custom all-reduce signal area's error word, or null) also its {error, ticks, calls} words ->
@@ -205,10 +201,6 @@ void launch_attn_prefill(const AttnArgs& a, hipStream_t st);
 // with a single query token do work) + prefill tiles (tile_seq < 0 = padding).
 void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st);
 
-// Decode attention + the o_proj GEMM (EPI_BF16, optional residual, M <= 16) as block roles of
-// one launch (attention.hip attn_o_kernel). sync: >= 64 zeroed, self-resetting uint32 words.
-// Returns false (nothing launched) when the shapes / grid do not fit the fused form.
-bool launch_attention_o(const AttnArgs& a, int dec_seqs, const GemmArgs& g, uint32_t* sync, hipStream_t st);
 
 struct SampleArgs {
   const float* logits;  // [B, V] f32, row stride ldl

@@ -376,11 +376,7 @@ void set_sample_nseg(int n) { g_sample_nseg = n; }
 
 int sample_segments(int B, int V) {
   const int V4 = V >> 2;
-  static const int env_force = [] {
-    const char* e = getenv("VGATE_SAMPLE_NSEG");  // experiments only (bounded below)
-    return e ? atoi(e) : 0;
-  }();
-  const int force = g_sample_nseg > 0 ? g_sample_nseg : env_force;
+  const int force = g_sample_nseg;
   int nseg = SAMPLE_MAX_BLOCKS / (B > 0 ? B : 1);
   if (force > 0 && force < nseg) nseg = force;
   if (nseg > SAMPLE_THREADS) nseg = SAMPLE_THREADS;  // the merge loads one partial per thread
@@ -397,22 +393,16 @@ void launch_sample(const SampleArgs& s, hipStream_t st) {
   int nseg = sample_segments(s.B, s.V);
   if (s.parts == nullptr || s.sync == nullptr) nseg = 1;
   SampleArgs a = s;
-  static const bool meet_only = getenv("VGATE_SAMPLE_MEET") != nullptr;  // experiments: the in-launch kernel
-  if (nseg > 1 && s.state != nullptr && s.tickets != nullptr && g_sample_round_launches >= 0 && !meet_only) {
+  if (nseg > 1 && s.state != nullptr && s.tickets != nullptr && g_sample_round_launches >= 0) {
     // pass 0 and the first rejection rounds as launches (last-arriver merges, no meetings),
     // then the in-launch rounds for rows still pending
-    // pass block width (experiments): 512 / 1024 threads measured no faster than 256 — a pass is
-    // bound by its memory round trips, not the sweep's Philox + log work (profiles/r2_sampler_nseg_sweep.log)
-    static const int nt = [] { const char* e = getenv("VGATE_SAMPLE_THREADS"); return e ? atoi(e) : 256; }();
+    // pass block width 256: 512 / 1024 threads measured no faster — a pass is bound by its memory
+    // round trips, not the sweep's Philox + log work (profiles/r2_sampler_nseg_sweep.log)
     a.tl = tl_take("sample_pass0", nseg * s.B);
-    if (nt == 256) hipLaunchKernelGGL(sample_pass0_kernel<256>, dim3(nseg, s.B), dim3(256), 0, st, a);
-    else if (nt == 512) hipLaunchKernelGGL(sample_pass0_kernel<512>, dim3(nseg, s.B), dim3(512), 0, st, a);
-    else hipLaunchKernelGGL(sample_pass0_kernel<1024>, dim3(nseg, s.B), dim3(1024), 0, st, a);
+    hipLaunchKernelGGL(sample_pass0_kernel<256>, dim3(nseg, s.B), dim3(256), 0, st, a);
     for (int r = 1; r <= g_sample_round_launches; ++r) {
       a.tl = tl_take("sample_round", nseg * s.B);
-      if (nt == 256) hipLaunchKernelGGL(sample_round_kernel<256>, dim3(nseg, s.B), dim3(256), 0, st, a, (uint32_t)r);
-      else if (nt == 512) hipLaunchKernelGGL(sample_round_kernel<512>, dim3(nseg, s.B), dim3(512), 0, st, a, (uint32_t)r);
-      else hipLaunchKernelGGL(sample_round_kernel<1024>, dim3(nseg, s.B), dim3(1024), 0, st, a, (uint32_t)r);
+      hipLaunchKernelGGL(sample_round_kernel<256>, dim3(nseg, s.B), dim3(256), 0, st, a, (uint32_t)r);
     }
     a.tl = tl_take("sample_resume", nseg * s.B);
     hipLaunchKernelGGL(sample_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, a,

@@ -398,53 +398,6 @@ void attention(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const T
   vgate::launch_attention(a, a.S, cur_stream());
 }
 
-// attention(...) + resid = o_proj(attn) [+ resid] as ONE launch when the fused form fits
-// (decode-sized steps, see attention.hip attn_o_kernel); returns false and launches nothing
-// otherwise (the caller runs the two ops). sync: zeroed int32 [>= 64], self-resetting.
-bool attention_o(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const Tensor& v_cache,
-                 const Tensor& block_tables, const Tensor& context_lens, const Tensor& query_start,
-                 const Tensor& tile_seq, const Tensor& tile_q0, Tensor& out, Tensor& part_o, Tensor& part_ml,
-                 int64_t Hq, int64_t Hkv, int64_t part_size, double scale, const Tensor& tickets,
-                 const Tensor& wp, int64_t N, int64_t K, Tensor& y, const c10::optional<Tensor>& res,
-                 const c10::optional<Tensor>& bias, const Tensor& sync) {
-  auto a = attn_common(q, q_stride, k_cache, v_cache, block_tables, context_lens, out, Hq, Hkv, scale);
-  CHECK_DT(query_start, torch::kInt32); CHECK_DT(tile_seq, torch::kInt32); CHECK_DT(tile_q0, torch::kInt32);
-  CHECK_DT(part_o, torch::kFloat32); CHECK_DT(part_ml, torch::kFloat32);
-  TORCH_CHECK(part_size % 32 == 0 && part_size <= 1024, "attention_o: part_size must be a multiple of 32, <= 1024");
-  TORCH_CHECK(query_start.numel() >= a.S + 1, "attention_o: query_start needs S+1 entries");
-  a.query_start = reinterpret_cast<const int32_t*>(query_start.data_ptr());
-  a.tile_seq = reinterpret_cast<const int32_t*>(tile_seq.data_ptr());
-  a.tile_q0 = reinterpret_cast<const int32_t*>(tile_q0.data_ptr());
-  a.num_tiles = (int)tile_seq.numel();
-  a.num_parts = (int)part_o.size(2);
-  a.part_size = (int)part_size;
-  TORCH_CHECK((int64_t)a.num_parts * part_size >= block_tables.size(1) * 16,
-              "attention_o: partitions do not cover max context");
-  TORCH_CHECK(part_o.size(0) >= a.S && part_o.size(1) == Hq, "attention_o: part_o shape");
-  a.part_o = reinterpret_cast<float*>(part_o.data_ptr());
-  a.part_ml = reinterpret_cast<float*>(part_ml.data_ptr());
-  CHECK_DEV(tickets); CHECK_DT(tickets, torch::kInt32);
-  TORCH_CHECK(tickets.numel() >= (int64_t)a.S * Hkv, "attention_o: tickets need S*Hkv zeroed int32");
-  a.tickets = reinterpret_cast<uint32_t*>(tickets.data_ptr());
-  CHECK_DEV(wp); CHECK_DT(wp, torch::kBFloat16); CHECK_DEV(y); CHECK_DT(y, torch::kBFloat16); CHECK_LASTDIM(y);
-  TORCH_CHECK(wp.numel() == N * K && K == Hq * 128, "attention_o: o_proj weight must be [N, Hq*128] packed");
-  CHECK_DEV(sync); CHECK_DT(sync, torch::kInt32);
-  TORCH_CHECK(sync.numel() >= 64, "attention_o: sync needs 64 zeroed int32");
-  const int64_t T = out.size(0);
-  TORCH_CHECK(y.dim() == 2 && y.size(0) >= T && y.size(1) >= N, "attention_o: y shape");
-  vgate::GemmArgs g{};
-  g.x = bf16p(out); g.lda = a.out_stride; g.M = (int)T;
-  g.wp = wp.data_ptr(); g.N = (int)N; g.K = (int)K;
-  g.bias = opt_bf16(bias);
-  g.res = opt_bf16(res);
-  g.ldr = g.res ? (int)res->stride(0) : 0;
-  if (g.res) TORCH_CHECK(res->size(0) >= T && res->size(1) >= N, "attention_o: residual shape");
-  g.out = y.data_ptr(); g.ldo = (int)y.stride(0);
-  g.epi = 0;
-  c10::DeviceGuard guard(q.device());
-  return vgate::launch_attention_o(a, a.S, g, reinterpret_cast<uint32_t*>(sync.data_ptr()), cur_stream());
-}
-
 void sample(const Tensor& logits, const c10::optional<Tensor>& temperature,
             const c10::optional<Tensor>& top_p, const c10::optional<Tensor>& top_k,
             const c10::optional<Tensor>& seeds, const c10::optional<Tensor>& offsets, Tensor& out,
@@ -648,12 +601,6 @@ PYBIND11_MODULE(_C, m) {
         py::arg("part_o"), py::arg("part_ml"), py::arg("Hq"), py::arg("Hkv"), py::arg("part_size"), py::arg("scale"),
         py::arg("out_stride") = 0, py::arg("tickets") = py::none(), py::arg("dbg_ts") = py::none(),
         py::arg("flash_ws") = py::none(), py::arg("fault") = py::none());
-  m.def("attention_o", &attention_o, "decode attention + o_proj GEMM (+residual) as one launch; false = not fused",
-        py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
-        py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),
-        py::arg("part_o"), py::arg("part_ml"), py::arg("Hq"), py::arg("Hkv"), py::arg("part_size"), py::arg("scale"),
-        py::arg("tickets"), py::arg("wp"), py::arg("N"), py::arg("K"), py::arg("y"), py::arg("res") = py::none(),
-        py::arg("bias") = py::none(), py::arg("sync"));
   m.def("embedding", &embedding, "vocab-sharded embedding gather (negative ids: previous step's samples)",
         py::arg("ids"), py::arg("table"), py::arg("out"), py::arg("vstart") = 0, py::arg("prev") = py::none(),
         py::arg("epoch") = py::none());
@@ -685,11 +632,7 @@ PYBIND11_MODULE(_C, m) {
         "rejection rounds the sampler runs as their own launches before the in-launch fallback (experiments)");
   m.def("kernel_copy", &kernel_copy, "pinned host <-> device copy by a kernel on the current stream (no SDMA)",
         py::arg("dst"), py::arg("src"), py::arg("nbytes"));
-  m.def("set_tail_split", &vgate::set_tail_split, "decode GEMM tail split: 1 on, 0 off, -1 environment (tests / sweeps)");
   m.def("set_flash_prefill", &vgate::set_flash_prefill, "flash prefill attention: 1 on, 0 off, -1 environment");
-  m.def("set_dec_rot", &vgate::set_dec_rot, "decode GEMM k-range rotation by block: 1 on, 0 off, -1 environment");
-  m.def("set_awq_lds", &vgate::set_awq_lds, "AWQ decode, LDS-shared activation slice: 1 on, 0 off, -1 environment");
-  m.def("set_dec_bal", &vgate::set_dec_bal, "balanced decode GEMM: 1 on, 0 off, -1 environment (VGATE_DEC_BAL)");
   m.def("set_dec_u", &vgate::set_dec_u, "decode GEMM register group: 0 auto, -1 round-2 rule, 6/8/10/12 forced, -100 environment");
   m.def("ids_to_host", &ids_to_host, "sampled ids -> slot *slot of a pinned host ring (graph-capturable, device-read slot)",
         py::arg("ids"), py::arg("ring"), py::arg("slot"), py::arg("n"), py::arg("ar_base") = 0,

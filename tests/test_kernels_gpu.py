@@ -668,55 +668,6 @@ def test_awq_mid_gemm(M, w, sk):
     assert _rel_err(kc, kc2) < 2e-2 and _rel_err(vc, vc2) < 2e-2
 
 
-@pytest.mark.parametrize("M", [1, 8, 16])
-@pytest.mark.parametrize("w,sk", [(4, 1), (2, 3), (1, 5)])
-def test_awq_mid_gemm_decode_modes(M, w, sk):
-    """The int4 medium kernel at decode M (a decode plan's ops.AWQ_MID_DECODE): the RMSNorm hand-off
-    consumer (x = h * gamma, row scale from the producer's per-tile sums, applied to each K slice's
-    partial) and producer (residual GEMM writing hg / per-tile sums of h^2), plain + residual over
-    a long K — against the dequantised fp32 reference."""
-    torch.manual_seed(600 + M + 7 * w + sk)
-    C = ops.native()
-    ws = ops.workspace(torch.device(DEV))
-    g = 128
-
-    def awq_lin(N, K, silu=False):
-        q = torch.randint(0, 16, (N, K), dtype=torch.int32)
-        scales = (torch.rand(K // g, N) * 0.02 + 0.005).bfloat16()
-        zeros = torch.randint(0, 16, (K // g, N)).float().bfloat16()
-        lin = ops.Linear(None, awq={"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV), "group": g,
-                                    "silu": silu})
-        return lin, ref.awq_dequant_ref(q, scales, zeros, g).to(DEV)
-
-    def kw(lin):
-        return dict(ws=ws, awq_scales=lin.scales, awq_zeros=lin.zeros, group=g, awq_szp=lin.szp, path=2, waves=w,
-                    splitk=sk)
-    K = 1536
-    h = torch.randn(M, K, device=DEV).bfloat16()
-    gamma = (torch.rand(K, device=DEV) + 0.5).bfloat16()
-    hg = (h.float() * gamma.float()).bfloat16()
-    ssp = h.float().pow(2).reshape(M, K // 16, 16).sum(-1).contiguous()
-    gu, wgu = awq_lin(2 * 1024, K, silu=True)
-    ys = torch.empty(M, 1024, device=DEV, dtype=torch.bfloat16)
-    C.gemm(hg, gu.wp, 2 * 1024, K, ys, 2, eps=1e-6, ssp_in=ssp, **kw(gu))
-    xn, _ = ref.rmsnorm_ref(h, gamma, 1e-6)
-    assert _rel_err(ys, ref.silu_mul_linear_ref(xn, wgu[:1024], wgu[1024:])) < 2e-2
-    # producer: down_proj class (K = 5 x 1024), residual + hand-off of the next RMSNorm
-    K2, N = 5120, 1536
-    lin, wd = awq_lin(N, K2)
-    x = torch.randn(M, K2, device=DEV).bfloat16()
-    res = torch.randn(M, N, device=DEV).bfloat16()
-    out = res.clone()
-    g2 = (torch.rand(N, device=DEV) + 0.5).bfloat16()
-    hg2 = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-    ssp2 = torch.empty(M, N // 16, dtype=torch.float32, device=DEV)
-    C.gemm(x, lin.wp, N, K2, out, 0, res=out, hg_out=hg2, hg_gamma=g2, ssp_out=ssp2, **kw(lin))
-    want = ref.linear_ref(x, wd, None, res)
-    assert _rel_err(out, want) < 2e-2
-    assert torch.equal(hg2, (out.float() * g2.float()).bfloat16())
-    torch.testing.assert_close(ssp2, out.float().pow(2).reshape(M, N // 16, 16).sum(-1), rtol=1e-5, atol=1e-4)
-
-
 @pytest.mark.parametrize("M", [40, 256])
 def test_awq_prefill_dequant_path(M):
     """Long AWQ steps: int4 -> bf16 fragment-packed scratch (gamma folded) + the bf16 prefill /
@@ -771,62 +722,6 @@ def test_unified_attention_mixed_batch(Hq, Hkv):
         out = torch.zeros(T, Hq * D, device=DEV).bfloat16()
         ops.attention(q, Hq * D, kc, vc, bt, cl, qs, ts, tq, out, po, pml, Hq, Hkv, part, scale)
         assert _rel_err(out.view(T, Hq, D), r) < 2e-2
-
-
-@pytest.mark.parametrize("Hq,Hkv,N", [(12, 2, 1536), (32, 8, 1024), (8, 1, 2048), (64, 8, 512)])
-@pytest.mark.parametrize("qlens,ctxs", [([1] * 8, [40, 1, 700, 33, 1500, 64, 2, 129]),
-                                        ([1, 1, 3, 1, 5], [100, 513, 20, 9, 37]), ([1], [5])])
-@pytest.mark.parametrize("residual,bias", [(True, False), (False, True)])
-def test_attention_o_fused(Hq, Hkv, N, qlens, ctxs, residual, bias):
-    """attention + o_proj (+residual / bias) as one launch == the two-launch path == fp32
-    references; repeated launches exercise the self-resetting arrival counters."""
-    torch.manual_seed(21)
-    D, BS = 128, 16
-    S = len(qlens)
-    maxb = 128
-    nblk = S * maxb + 4
-    kc, vc = _make_cache(nblk, Hkv, seed=5)
-    bt = (torch.randperm(nblk)[: S * maxb]).reshape(S, maxb).int().to(DEV)
-    qs = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32, device=DEV)
-    T = int(qs[-1])
-    cl = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
-    q = torch.randn(T, Hq * D, device=DEV).bfloat16()
-    ts, tq = ops.prefill_tiles([ql if ql > 1 else 0 for ql in qlens])
-    ts = torch.tensor(ts + [-1], dtype=torch.int32, device=DEV)
-    tq = torch.tensor(tq + [0], dtype=torch.int32, device=DEV)
-    K = Hq * D
-    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
-    b = torch.randn(N, device=DEV).bfloat16() if bias else None
-    lin = ops.Linear(w, bias=b)
-    resid0 = torch.randn(T, N, device=DEV).bfloat16()
-    scale = 1 / math.sqrt(D)
-    part = 512
-    P = (maxb * BS + part - 1) // part
-    po = torch.empty(S, Hq, P, D, device=DEV)
-    pml = torch.empty(S, Hq, P, 2, device=DEV)
-    a_ref = ref.attention_ref(q.view(T, Hq, D), kc, vc, bt, cl, qs.cpu(), Hq, Hkv, scale).reshape(T, K)
-    # two-launch path
-    out2 = torch.zeros(T, K, device=DEV).bfloat16()
-    y2 = resid0.clone()
-    ops.attention(q, K, kc, vc, bt, cl, qs, ts, tq, out2, po, pml, Hq, Hkv, part, scale)
-    ops.linear(out2, lin, out=y2, residual=y2 if residual else None)
-    for _ in range(3):
-        out = torch.zeros(T, K, device=DEV).bfloat16()
-        y = resid0.clone()
-        fused = ops.attention_o(q, K, kc, vc, bt, cl, qs, ts, tq, out, po, pml, Hq, Hkv, part, scale, lin, y,
-                                residual=residual, force=True)
-        if not fused:  # grid larger than the co-resident capacity: the caller's two launches run
-            # (decode grids of 8 KV heads x 8 sequences x 4 partitions, or K = 8192 deeper than
-            # one register group per wave)
-            assert Hkv == 8, "the Qwen-shaped decode steps must take the fused form"
-            return
-        assert _rel_err(out, a_ref) < 2e-2
-        # the fused grid runs attention with 8 waves per block (merge order differs from 6 waves)
-        assert _rel_err(out, out2) < 5e-3
-        y_ref = ref.linear_ref(out, w, b, resid0 if residual else None)
-        assert _rel_err(y, y_ref) < 1e-2
-        assert _rel_err(y, y2) < 5e-3
-    assert int(ops.attn_o_sync(DEV).abs().sum()) == 0  # counters re-armed
 
 
 @pytest.mark.parametrize("T", [5, 40])
@@ -1245,39 +1140,6 @@ def test_tune_prefill_plans_match_heuristic_results():
             assert _rel_err(y, y0) < 1e-2, (lin.layout, M)
 
 
-@pytest.mark.parametrize("M", [1, 8, 16])
-def test_decode_gemm_tail_split(M):
-    """Decode GEMMs over more column tiles than CUs (q * CUs + r, r <= CUs / 2) cut the r tail tiles
-    into K halves combined by the last-arriver slab hand-off: == the one-slice grid within split-K
-    rounding for residual, SiLU (folded-norm row scale) and the row-gathered f32 LM-head form."""
-    C = ops.native()
-    torch.manual_seed(500 + M)
-    K = 1536
-    ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    N = 16 * (4 * ncu + 96)  # 4 tiles per CU + a 96-tile tail
-    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
-    x = torch.randn(M, K, device=DEV).bfloat16()
-    res = torch.randn(M, N, device=DEV).bfloat16()
-    nw = (torch.rand(K, device=DEV) + 0.5).bfloat16()
-    xn, _ = ref.rmsnorm_ref(x, nw, 1e-6)
-    cases = [("plain", dict(residual=res), ref.linear_ref(x, w, None, res)),
-             ("silu", dict(norm=(nw, 1e-6)), ref.silu_mul_linear_ref(xn, w[: N // 2], w[N // 2:])),
-             ("f32", dict(out_f32=True, norm=(nw, 1e-6)), ref.linear_ref(xn, w, out_f32=True))]
-    try:
-        for kind, kw, want in cases:
-            lin = ops.Linear(w, kind="silu" if kind == "silu" else "plain")
-            if kind == "silu":
-                lin.fold_norm(nw)
-            outs = []
-            for on in (1, 0):
-                C.set_tail_split(on)
-                outs.append(ops.linear(x, lin, **kw))
-            assert _rel_err(outs[0], want) < 2e-2, kind
-            assert _rel_err(outs[0], outs[1]) < 1e-2, kind
-    finally:
-        ops._configure(C)  # back to the process default (VGATE_TAIL_SPLIT)
-
-
 @pytest.mark.parametrize("M", [3, 8, 12])
 def test_decode_gemm_register_groups_bit_identical(M):
     """The decode GEMM's register group size (k-steps per in-flight group: auto, the round-2
@@ -1315,144 +1177,6 @@ def test_decode_gemm_register_groups_bit_identical(M):
             assert _rel_err(outs[0].float().cpu(), r.float()) < 1e-2, (N, K, kind)
     finally:
         C.set_dec_u(-100)
-
-
-@pytest.mark.parametrize("M", [5, 8, 12, 16])
-def test_balanced_decode_gemm(M):
-    """Balanced decode GEMM (one block per CU: q full tiles + pieces of the tail tiles, combined by
-    the last piece): SiLU with folded RMSNorm on the Qwen2.5-1.5B gate_up shape (1120 tiles), a
-    residual GEMM with 608 tiles and an f32-output one — against the fp32 reference, run-to-run
-    bit-identical, and close to the one-tile-per-block kernel."""
-    C = ops.native()
-    torch.manual_seed(90 + M)
-    ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    try:
-        for N, K, kind in ((17920, 1536, "silu"), ((2 * ncu + 96) * 16, 1536, "plain"),
-                           ((4 * ncu + 64) * 16, 2048, "f32")):
-            x = torch.randn(M, K, device=DEV).bfloat16()
-            w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
-            g = (torch.rand(K, device=DEV) + 0.5).bfloat16()
-            lin = ops.Linear(w, kind="silu") if kind == "silu" else ops.Linear(w)
-            res = torch.randn(M, N, device=DEV).bfloat16()
-
-            def run():
-                if kind == "silu":
-                    return ops.linear(x, lin, norm=(g, 1e-6))
-                if kind == "f32":
-                    return ops.linear(x, lin, out_f32=True)
-                y = res.clone()
-                ops.linear(x, lin, out=y, residual=y)
-                return y
-            if kind == "silu":
-                lin.fold_norm(g)
-            C.set_dec_bal(0)
-            y0 = run()
-            C.set_dec_bal(1)
-            y1, y2 = run(), run()
-            assert torch.equal(y1, y2), (N, K, kind)
-            if kind == "silu":
-                xn, _ = ref.rmsnorm_ref(x.cpu(), g.cpu(), 1e-6)
-                r = ref.silu_mul_linear_ref(xn, w.cpu()[: N // 2], w.cpu()[N // 2:])
-            elif kind == "f32":
-                r = ref.linear_ref(x.cpu(), w.cpu(), out_f32=True)
-            else:
-                r = ref.linear_ref(x.cpu(), w.cpu(), None, res.cpu())
-            assert _rel_err(y1.float().cpu(), r.float()) < 1e-2, (N, K, kind)
-            assert _rel_err(y1.float(), y0.float()) < 1e-2, (N, K, kind)
-    finally:
-        C.set_dec_bal(-1)
-
-
-@pytest.mark.parametrize("M", [1, 5, 8, 16])
-def test_awq_lds_kernel(M):
-    """AWQ decode with the LDS-shared activation slice (awq_lds_kernel: a loader wave DMAs x into
-    LDS, T tile waves stream their int4 k-slices; K-slices combined by slab + ticket) on the
-    Qwen2.5-1.5B shapes: plain + residual (down_proj: 8960-deep K, split over slices), SiLU
-    (gate_up), with and without the RMSNorm hand-off == the dequantised fp32 reference and the
-    awq_stream kernel; deterministic run to run."""
-    C = ops.native()
-    torch.manual_seed(120 + M)
-    g = 128
-    try:
-        for N, K, layout in ((17920, 1536, "silu"), (1536, 8960, "plain"), (1536, 1536, "plain")):
-            q = torch.randint(0, 16, (N, K), dtype=torch.int32)
-            sc = (torch.rand(K // g, N) * 0.01 + 0.002).bfloat16()
-            zz = torch.randint(0, 16, (K // g, N)).float().bfloat16()
-            wd = ref.awq_dequant_ref(q, sc, zz, g).to(DEV)
-            lin = ops.Linear(None, kind="awq", awq={"qint": q, "scales": sc.to(DEV), "zeros": zz.to(DEV), "group": g,
-                                                    "layout": layout})
-            x = torch.randn(M, K, device=DEV).bfloat16()
-            res = torch.randn(M, N, device=DEV).bfloat16()
-            outs = {}
-            for on in (1, 0):
-                C.set_awq_lds(on)
-                if layout == "silu":
-                    y = ops.linear(x, lin)
-                    y2 = ops.linear(x, lin)
-                else:
-                    y = res.clone()
-                    ops.linear(x, lin, out=y, residual=y)
-                    y2 = res.clone()
-                    ops.linear(x, lin, out=y2, residual=y2)
-                assert torch.equal(y, y2), (N, K, on)
-                outs[on] = y
-            want = (ref.silu_mul_linear_ref(x, wd[: N // 2], wd[N // 2:]) if layout == "silu"
-                    else ref.linear_ref(x, wd, None, res))
-            assert _rel_err(outs[1], want) < 2e-2, (N, K, _rel_err(outs[1], want))
-            assert _rel_err(outs[1], outs[0]) < 1e-2, (N, K)
-            # RMSNorm hand-off consumer (x = h * gamma, row scale from the producer's sums)
-            if K == 1536:
-                gamma = (torch.rand(K, device=DEV) + 0.5).bfloat16()
-                hg = (x.float() * gamma.float()).bfloat16()
-                ssp = x.float().pow(2).reshape(M, K // 16, 16).sum(-1)
-                o_n = torch.empty(M, lin.out_features, dtype=torch.bfloat16, device=DEV)
-                o_h = torch.empty_like(o_n)
-                C.set_awq_lds(0)
-                ops.linear(x, lin, out=o_n, norm=(gamma, 1e-6))
-                C.set_awq_lds(1)
-                ops.linear(hg, lin, out=o_h, prenorm=(ssp, 1e-6))
-                assert _rel_err(o_h, o_n) < 1e-2, (N, K, _rel_err(o_h, o_n))
-    finally:
-        C.set_awq_lds(-1)
-
-
-@pytest.mark.parametrize("M", [3, 8, 12])
-def test_decode_gemm_block_rotation(M):
-    """Decode GEMM with the k-range / group order rotated by block (set_dec_rot): same product
-    (fp32 reference), deterministic run to run, close to the unrotated kernel."""
-    C = ops.native()
-    torch.manual_seed(150 + M)
-    try:
-        for N, K, kind, waves, splitk in ((1536, 8960, "plain", 8, 2), (17920, 1536, "silu", 2, 1),
-                                          (2048, 1536, "plain", 8, 1)):
-            x = torch.randn(M, K, device=DEV).bfloat16()
-            w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
-            g = (torch.rand(K, device=DEV) + 0.5).bfloat16()
-            lin = ops.Linear(w, kind=kind) if kind == "silu" else ops.Linear(w)
-            if kind == "silu":
-                lin.fold_norm(g)
-            res = torch.randn(M, N // (2 if kind == "silu" else 1), device=DEV).bfloat16()
-
-            def run():
-                if kind == "silu":
-                    return ops.linear(x, lin, norm=(g, 1e-6), waves=waves, splitk=splitk)
-                y = res.clone()
-                ops.linear(x, lin, out=y, residual=y, waves=waves, splitk=splitk)
-                return y
-            C.set_dec_rot(0)
-            y0 = run()
-            C.set_dec_rot(1)
-            y1, y2 = run(), run()
-            assert torch.equal(y1, y2)
-            assert _rel_err(y1.float(), y0.float()) < 1e-2, (N, K, kind)
-            if kind == "silu":
-                xn, _ = ref.rmsnorm_ref(x.cpu(), g.cpu(), 1e-6)
-                r = ref.silu_mul_linear_ref(xn, w.cpu()[: N // 2], w.cpu()[N // 2:])
-            else:
-                r = ref.linear_ref(x.cpu(), w.cpu(), None, res.cpu())
-            assert _rel_err(y1.float().cpu(), r.float()) < 1e-2, (N, K, kind)
-    finally:
-        C.set_dec_rot(-1)
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (12, 2), (8, 1), (16, 16)])

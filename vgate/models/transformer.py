@@ -241,17 +241,9 @@ class DecoderModel:
                 ops.linear(hg, L.qkv, out=q, prenorm=(ssp, eps), qkv=qkv_args)
             else:
                 ops.linear(resid, L.qkv, out=q, norm=(L.in_norm, eps), qkv=qkv_args)
-            # attention and o_proj (+ residual) as one launch when VGATE_FUSE_ATTN_O=1 (decode-sized
-            # steps; measured slower, off by default: ops.attention_o); otherwise two launches
-            if not hand and ops.attention_o(q, sh.hq * D, kc, vc, sv.block_tables, sv.context_lens, sv.query_start, sv.tile_seq,
-                               sv.tile_q0, attn, part_o, part_ml, sh.hq, sh.hkv, part_size, self.scale, L.o, resid,
-                               residual=first):
-                if tp.size > 1:
-                    tp.all_reduce(resid)
-            else:
-                ops.attention(q, sh.hq * D, kc, vc, sv.block_tables, sv.context_lens, sv.query_start, sv.tile_seq,
-                              sv.tile_q0, attn, part_o, part_ml, sh.hq, sh.hkv, part_size, self.scale)
-                self._row_parallel(attn, L.o, resid, first, norm_out=(hg, ssp, L.post_norm) if hand else None)
+            ops.attention(q, sh.hq * D, kc, vc, sv.block_tables, sv.context_lens, sv.query_start, sv.tile_seq,
+                          sv.tile_q0, attn, part_o, part_ml, sh.hq, sh.hkv, part_size, self.scale)
+            self._row_parallel(attn, L.o, resid, first, norm_out=(hg, ssp, L.post_norm) if hand else None)
             if not hand and T <= 16 and ops.mlp_decode(resid, L.gate_up, L.down, resid, resid if first else None,
                                                       eps, li, self.epoch):
                 if tp.size > 1:

@@ -47,12 +47,7 @@ def native():
 
 
 def _configure(mod) -> None:
-    """Runtime knobs of the extension that default from the environment on the Python side.
-    VGATE_TAIL_SPLIT: decode GEMMs over q * CUs + r column tiles run the r tail tiles as K halves
-    (csrc/kernels/gemm.hip launch_one / launch_awq_stream; measured slower, off by default:
-    profiles/r2_tail_split_negative.log)."""
-    if hasattr(mod, "set_tail_split"):
-        mod.set_tail_split(int(os.environ.get("VGATE_TAIL_SPLIT", "0")))
+    """Runtime knobs of the extension that default from the environment on the Python side."""
     # VGATE_SAMPLE_ROUND_LAUNCHES: top-k / top-p rejection rounds run as their own launches before
     # the in-launch fallback (csrc/kernels/sampling.hip launch_sample). 1: the bench A/B measured
     # 93.1 / 93.2 req/s at 1 vs 92.3 / 93.0 at 2 and 92.4 at 3, sampler_probe 31.1 vs 32.5 us
@@ -351,11 +346,7 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
         return _linear_awq_dequant(x, lin, out, residual, norm, qkv, epi, M)
     ntb = 0
     if M <= 16 and waves == 0 and splitk == 0:
-        waves, splitk, ntb = lin.dec_waves, lin.dec_splitk, lin.dec_ntb
-        if ntb == WIDE_DECODE and lin.kind == "dense":  # the wide medium kernel (gemm_mid.hip) at decode M
-            waves, splitk, ntb, path = 8, 0, 0, 2
-        elif ntb == AWQ_MID_DECODE and lin.kind == "awq":  # the int4 medium kernel at decode M (waves, K slices)
-            ntb, path = 0, 2
+        waves, splitk, ntb = lin.dec_waves, lin.dec_splitk, lin.dec_ntb  # (AWQ ntb -8: the wide int4 kernel)
     elif M > 16 and waves == 0 and splitk == 0 and path == 0 and lin.prefill_plan and lin.kind == "dense":  # (AWQ: below)
         pk = _plan_kw(lin.prefill_plan.get(_plan_bucket(lin.prefill_plan, M)), M)
         ntb, splitk, path, waves = pk.get("ntb", 0), pk.get("splitk", 0), pk.get("path", 0), pk.get("waves", 0)
@@ -481,30 +472,6 @@ def attention(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_s
     return out
 
 
-def attention_o(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start, tile_seq, tile_q0, out,
-                part_o, part_ml, Hq: int, Hkv: int, part_size: int, scale: float, lin: "Linear", y: torch.Tensor,
-                residual: bool, force: bool = False) -> bool:
-    """attention(...) then ``y = out @ W_o^T (+ y if residual)`` as ONE launch (decode-sized steps):
-    the o_proj blocks stream their weights while the attention blocks run and take the attention
-    output over an in-launch hand-off (csrc/kernels/attention.hip attn_o_kernel). Returns False
-    and launches nothing when the fused form does not apply (GPU only; the caller then runs
-    :func:`attention` and :func:`linear`).
-
-    Off by default (VGATE_FUSE_ATTN_O=1 or ``force`` enables it): measured on the MI355X, the
-    fused launch is SLOWER than the two launches (Qwen2.5-1.5B decode, batch 8: 13.5 vs 11.8 us
-    per layer, profiles/r2_attn_o_fusion_negative.log) — the o_proj weight burst delays the
-    latency-bound attention blocks by 2-3 us and the flag hand-off plus the activation round trip
-    after the last attention block (~4 us) costs as much as the kernel boundary it replaces."""
-    if not _gpu(q) or lin.kind != "dense" or lin.wp is None or out.shape[0] > 16:
-        return False
-    if not force and os.environ.get("VGATE_FUSE_ATTN_O", "0") != "1":
-        return False
-    return bool(native().attention_o(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start, tile_seq,
-                                     tile_q0, out, part_o, part_ml, Hq, Hkv, part_size, scale,
-                                     attn_tickets(q.device), lin.wp, lin.N, lin.K, y, y if residual else None,
-                                     lin.bias, attn_o_sync(q.device)))
-
-
 # fused decode MLP (csrc/kernels/mlp_fused.hip): gate_up -> SiLU -> down_proj (+residual) as one launch
 # for steps of <= 16 rows; VGATE_FUSED_MLP=1 turns it on (being tuned: slower than the two GEMMs so far)
 FUSED_MLP = os.environ.get("VGATE_FUSED_MLP", "0") == "1"
@@ -575,18 +542,6 @@ def mlp_decode(x: torch.Tensor, gate_up: "Linear", down: "Linear", out: torch.Te
     return bool(native().mlp_decode(x, gate_up.wp, down.wp, H, I, out, residual, float(eps),
                                     mlp_workspace(x.device, H, I), epoch, int(layer), slices, grid,
                                     fault=fault_word(x.device)))
-
-
-_AO_SYNC: dict = {}
-
-
-def attn_o_sync(device) -> torch.Tensor:
-    """Self-resetting arrival counters of the fused attention + o_proj launch (zeroed once)."""
-    key = str(device)
-    t = _AO_SYNC.get(key)
-    if t is None:
-        t = _AO_SYNC[key] = torch.zeros(64, dtype=torch.int32, device=device)
-    return t
 
 
 _TICKETS: dict = {}
@@ -741,8 +696,6 @@ PREFILL_CANDIDATES = [(0, 0), (64, 0), (128, 0), (128, 2), (128, 4), (256, 0), (
 # medium-M kernel (csrc/kernels/gemm_mid.hip, 16 < M <= 64) candidates, encoded as tile code
 # MID_BASE - W (W tiles = waves per block) and K slices (0 = its heuristic)
 MID_BASE = -10
-WIDE_DECODE = -8  # Linear.dec_ntb: decode steps (M <= 16) on the wide medium kernel
-AWQ_MID_DECODE = -9  # Linear.dec_ntb of an AWQ layer: decode steps on the int4 medium kernel
 MID_CANDIDATES = [(MID_BASE - w, s) for w in (4, 2) for s in (0, 2, 3, 4, 6, 8, 10, 12, 16)] + [(MID_BASE - 8, 0)]
 _FLUSH: dict = {}
 
@@ -911,7 +864,7 @@ def softmax_scale(head_dim: int) -> float:
 
 __all__ = [
     "native", "native_available", "pack_weight", "unpack_weight", "interleave_gate_up", "pack_awq",
-    "Linear", "linear", "attention", "attention_o", "workspace", "fault_word", "mlp_decode", "mlp_workspace",
+    "Linear", "linear", "attention", "workspace", "fault_word", "mlp_decode", "mlp_workspace",
     "forward_epoch", "mlp_error", "row_permutation", "reserve_awq_scratch", "pack_awq_sz", "rmsnorm", "embedding", "rope_kv", "attention_decode", "attention_prefill",
     "prefill_tiles", "sample", "softmax_scale", "ref", "host_device_copy", "tune_prefill", "apply_prefill_plans",
 ]
