@@ -21,7 +21,7 @@ import torch  # noqa: E402
 
 from vgate import ops  # noqa: E402
 
-PHASES = ["start", "x_staged", "gate_up_done", "h_stored", "h_polled", "down_done", "ticket", "end"]
+PHASES = ["start", "x_staged", "gate_up_done_all_waves", "h_stored", "h_polled", "down_done", "ticket", "end"]
 
 
 def main():
@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--I", type=int, default=8960)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--slices", type=int, default=0)
+    ap.add_argument("--b-early", type=int, default=0)
     a = ap.parse_args()
     ops.FUSED_MLP = True
     dev = torch.device("cuda:0")
@@ -52,7 +53,7 @@ def main():
     def fused():
         epoch.add_(1)
         for li, (gu, dn, _) in enumerate(layers):
-            assert ops.mlp_decode(x, gu, dn, x, x, 1e-6, li, epoch, slices=a.slices)
+            assert ops.mlp_decode(x, gu, dn, x, x, 1e-6, li, epoch, slices=a.slices, b_early=a.b_early)
 
     def unfused():
         for gu, dn, gamma in layers:
@@ -83,7 +84,7 @@ def main():
     for li, (gu, dn, _) in enumerate(layers):
         kw = {"dbg": dbg} if li == a.layers // 2 else {}
         ops.native().mlp_decode(x, gu.wp, dn.wp, H, I, x, x, 1e-6, ops.mlp_workspace(dev, H, I), epoch, li,
-                                a.slices, 0, **kw)
+                                a.slices, 0, b_early=a.b_early, **kw)
     torch.cuda.synchronize()
     st = dbg.view(G, 8).cpu().double()
     t0 = st[:, 0].min()

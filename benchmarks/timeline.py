@@ -39,6 +39,10 @@ def main():
     ap.add_argument("--mixed", type=int, default=0, help="time a MIXED step: one prompt of this many tokens "
                     "beside the decode rows (benchmarks/mixed_step.py)")
     ap.add_argument("--wide-gate-up", action="store_true", help="medium buckets: the wide medium kernel for gate_up")
+    ap.add_argument("--replays", type=int, default=0,
+                    help="after the measured step, replay its graph N times back to back (no host sync between) "
+                         "and report the last replay too: a hole that only the first replay shows is the host's "
+                         "graph launch, not the GPU")
     a = ap.parse_args()
     eng = LLMEngine(EngineConfig(model=a.model, device="cuda:0", max_model_len=2048, max_num_seqs=a.max_seqs,
                                  max_num_batched_tokens=2048, num_kv_blocks=a.kv_blocks or None, warmup=False,
@@ -59,8 +63,8 @@ def main():
         eng.add_request("mixed", prompt_ids=[200 + (j * 13) % 5000 for j in range(a.mixed)],
                         params=SamplingParams(temperature=0.7, top_p=0.9, max_tokens=1))
         eng._drain_inbox()
-    summary, live, cap, t = measure(eng)
-    summary.update(batch=a.batch, ctx=a.ctx)
+    summary, live, cap, t = measure(eng, a.replays)
+    summary.update(batch=a.batch, ctx=a.ctx, replays=a.replays)
     print(json.dumps(summary), flush=True)
     for x in live[:14]:
         print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in x.items() if k not in ("t0", "t1")}))
@@ -68,9 +72,10 @@ def main():
         Path(a.json).write_text(json.dumps({"summary": summary, "launches": live}, indent=1))
 
 
-def measure(eng):
+def measure(eng, replays: int = 0):
     """Re-capture the engine's decode bucket(s) with timeline slots, run one step, and return
-    (summary, launches in start order, captured launch entries, raw stamps)."""
+    (summary, launches in start order, captured launch entries, raw stamps). replays > 0: then
+    replay the newest graph that many times back to back and keep the last replay's stamps."""
     C = ops.native()
     r = eng.runner
     torch.cuda.synchronize()
@@ -85,6 +90,11 @@ def measure(eng):
     for _ in range(3):
         eng.step()
     torch.cuda.synchronize()
+    if replays > 0:
+        g = r.graphs[max(r.graphs.keys())]
+        for _ in range(replays):
+            g.replay()
+        torch.cuda.synchronize()
     t = buf[:used].view(-1, 2).cpu()
     # the capture runs the forward twice (eager warm-up, then capture): keep the captured half
     n = len(ents)

@@ -128,6 +128,7 @@ struct MlpDecodeArgs {
   int slices;                 // h slices (0: 8)
   int grid;                   // workgroups (0: the CU count; all must be resident at once)
   unsigned long long* dbg = nullptr;  // profiling: [grid][8] phase stamps (s_memrealtime), or null
+  int b_early = 0;            // 1: issue the down weights right behind the first gate_up groups (A/B)
 };
 bool launch_mlp_decode(const MlpDecodeArgs& g, hipStream_t st);
 

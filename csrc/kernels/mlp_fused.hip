@@ -89,7 +89,7 @@ struct Split {
   }
 };
 
-template <int W, int UA, int NGA, int NB, int XPW, int HPW>
+template <int W, int UA, int NGA, int NB, int XPW, int HPW, bool BEARLY, bool XWAIT>
 __global__ __launch_bounds__(64 * W) void mlp_decode_kernel(MlpParams a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   TLScope tl_scope(a.tl);
@@ -166,9 +166,26 @@ __global__ __launch_bounds__(64 * W) void mlp_decode_kernel(MlpParams a) {
     }
   };
 
+  // residual words of the n-tile this wave would finalise (read only by an n-tile's last arriver;
+  // loaded now so the combine at the end waits for nothing but the slabs)
+  const int LB0 = pb1 - pb0;
+  const int uA0 = pb0 / KS2, nfin = LB0 > 0 ? (pb1 - 1) / KS2 - uA0 + 1 : 0;
+  uint2 resw;
+  {  // (unconditional buffer load: zeros past the range, no branch around a load)
+    const __amdgpu_buffer_rsrc_t rr = rsrc_of(a.res != nullptr ? a.res : a.x);
+    const uint32_t off = (uint32_t)(((size_t)mrow * a.ldr + (uA0 + w) * 16 + 4 * g4) * 2);
+    const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rr, (a.res != nullptr && w < nfin) ? off : OOB_OFF, 0, 0);
+    const uint32_t v2 = __builtin_amdgcn_raw_buffer_load_b32(rr, (a.res != nullptr && w < nfin) ? off + 4 : OOB_OFF, 0, 0);
+    resw = make_uint2(v, v2);
+  }
+  // XWAIT: the x rows land before any weight load is issued — a CU's loads return at the rate of
+  // its whole burst, in any issue order (MI355X_MICROARCH.md, prologue HBM burst): x issued ahead of
+  // 192 KB of weight groups still arrived ~5.5 us late and held back the first MFMA and every refill
+  if constexpr (XWAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   uint4 b0[UA], b1[UA];
   loadA(b0, p0);
   if constexpr (NGA > 1) loadA(b1, p0 + UA);
+  if constexpr (BEARLY) loadB();  // down weights right behind the first gate_up groups
 
   float ss = 0.f;
 #pragma unroll
@@ -205,14 +222,14 @@ __global__ __launch_bounds__(64 * W) void mlp_decode_kernel(MlpParams a) {
     uint4 (&buf)[UA] = (g & 1) ? b1 : b0;
     mmaA(buf, p0 + g * UA);
     if (g + 2 < NGA) loadA(buf, p0 + (g + 2) * UA);
-    else if (g == (NGA >= 2 ? NGA - 2 : 0)) loadB();
+    else if (!BEARLY && g == (NGA >= 2 ? NGA - 2 : 0)) loadB();
   }
 
-  if (w == 0) MLP_STAMP(2);
   // ---- phase A epilogue: partial tiles meet in LDS (wave order), row scale, SiLU, h granules ----
   red[(w * 2) * 64 + lane] = acc0;
   red[(w * 2 + 1) * 64 + lane] = acc1;
   lds_barrier();
+  if (w == 0) MLP_STAMP(2);  // (every wave's gate_up range done)
   if (w < tl1 - tl0) {
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     for (int ww = 0; ww < W; ++ww) {
@@ -342,7 +359,7 @@ __global__ __launch_bounds__(64 * W) void mlp_decode_kernel(MlpParams a) {
     const int n = u * 16 + 4 * g4;
     float o[4] = {y[0], y[1], y[2], y[3]};
     if (a.res != nullptr) {
-      const uint2 rw = *reinterpret_cast<const uint2*>(a.res + (size_t)r16 * a.ldr + n);
+      const uint2 rw = resw;  // (prefetched at the start: this wave's n-tile u = uA0 + w)
       const float rr[4] = {__uint_as_float(rw.x << 16), __uint_as_float(rw.x & 0xffff0000u),
                            __uint_as_float(rw.y << 16), __uint_as_float(rw.y & 0xffff0000u)};
 #pragma unroll
@@ -445,10 +462,13 @@ bool launch_mlp_decode(const MlpDecodeArgs& g, hipStream_t st) {
   p.epoch = g.epoch; p.layer = g.layer; p.S = S;
   p.tl = tl_take("mlp_fused", G);
   p.dbg = g.dbg;
-#define VG_MLP(NG) hipLaunchKernelGGL((mlp_decode_kernel<W, UA, NG, NB, XPW, HPW>), dim3(G), dim3(64 * W), lds, st, p)
-  if (nga <= 2) VG_MLP(2);
-  else if (nga <= 4) VG_MLP(4);
-  else VG_MLP(8);
+#define VG_MLP(NG, BE, XW) hipLaunchKernelGGL((mlp_decode_kernel<W, UA, NG, NB, XPW, HPW, BE, XW>), dim3(G), dim3(64 * W), lds, st, p)
+#define VG_MLP_NG(BE, XW) do { if (nga <= 2) VG_MLP(2, BE, XW); else if (nga <= 4) VG_MLP(4, BE, XW); else VG_MLP(8, BE, XW); } while (0)
+  // b_early bit 0: down weights right behind the first gate_up groups; bit 1: do NOT wait for x first
+  const bool be = (g.b_early & 1) != 0, xw = (g.b_early & 2) == 0;
+  if (be) { if (xw) VG_MLP_NG(true, true); else VG_MLP_NG(true, false); }
+  else { if (xw) VG_MLP_NG(false, true); else VG_MLP_NG(false, false); }
+#undef VG_MLP_NG
 #undef VG_MLP
   return true;
 }

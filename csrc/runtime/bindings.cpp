@@ -202,7 +202,8 @@ void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vsta
 // Returns false (nothing launched) when the shape does not fit the fused work split.
 bool mlp_decode(const Tensor& x, const Tensor& wgu, const Tensor& wd, int64_t H, int64_t I, Tensor& out,
                 const c10::optional<Tensor>& res, double eps, Tensor& ws, const Tensor& epoch, int64_t layer,
-                int64_t slices, int64_t grid, const c10::optional<Tensor>& dbg, const c10::optional<Tensor>& fault) {
+                int64_t slices, int64_t grid, const c10::optional<Tensor>& dbg, const c10::optional<Tensor>& fault,
+                int64_t b_early) {
   CHECK_DEV(x); CHECK_DEV(wgu); CHECK_DEV(wd); CHECK_DEV(out); CHECK_DEV(ws); CHECK_DEV(epoch);
   CHECK_DT(x, torch::kBFloat16); CHECK_DT(out, torch::kBFloat16); CHECK_DT(wgu, torch::kBFloat16);
   CHECK_DT(wd, torch::kBFloat16); CHECK_DT(ws, torch::kInt32); CHECK_DT(epoch, torch::kInt32);
@@ -233,6 +234,7 @@ bool mlp_decode(const Tensor& x, const Tensor& wgu, const Tensor& wd, int64_t H,
   g.epoch = reinterpret_cast<const uint32_t*>(epoch.data_ptr());
   g.layer = (int)layer; g.slices = (int)slices; g.grid = (int)grid;
   g.dbg = reinterpret_cast<unsigned long long*>(opt_ptr<int64_t>(dbg, torch::kInt64, "dbg"));
+  g.b_early = (int)b_early;
   if (M == 0) return true;
   c10::DeviceGuard guard(x.device());
   return vgate::launch_mlp_decode(g, cur_stream());
@@ -608,7 +610,7 @@ PYBIND11_MODULE(_C, m) {
         "false = shape not fused", py::arg("x"), py::arg("wgu"), py::arg("wd"), py::arg("H"), py::arg("I"),
         py::arg("out"), py::arg("res") = py::none(), py::arg("eps"), py::arg("ws"), py::arg("epoch"),
         py::arg("layer"), py::arg("slices") = 0, py::arg("grid") = 0, py::arg("dbg") = py::none(),
-        py::arg("fault") = py::none());
+        py::arg("fault") = py::none(), py::arg("b_early") = 0);
   m.def("rmsnorm", &rmsnorm, "RMSNorm with optional fused residual add");
   m.def("rope_kv", &rope_kv, "NeoX RoPE + paged KV-cache write (rotated q in place or into q_out)",
         py::arg("qkv"), py::arg("positions"), py::arg("slots"), py::arg("cos_sin"), py::arg("k_cache"),

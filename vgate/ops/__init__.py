@@ -525,7 +525,7 @@ def forward_epoch(device) -> torch.Tensor:
 
 
 def mlp_decode(x: torch.Tensor, gate_up: "Linear", down: "Linear", out: torch.Tensor, residual, eps: float,
-               layer: int, epoch: torch.Tensor, slices: int = 0, grid: int = 0) -> bool:
+               layer: int, epoch: torch.Tensor, slices: int = 0, grid: int = 0, b_early: int = 0) -> bool:
     """``out = [residual +] down(silu(gate(xn)) * up(xn))``, xn = RMSNorm(x) with the gamma folded into
     ``gate_up`` (Linear.fold_norm), as ONE launch (decode steps, <= 16 rows; out may alias x and
     residual). Returns False and launches nothing when the layers or the shape do not fit the fused
@@ -541,7 +541,7 @@ def mlp_decode(x: torch.Tensor, gate_up: "Linear", down: "Linear", out: torch.Te
         return False
     return bool(native().mlp_decode(x, gate_up.wp, down.wp, H, I, out, residual, float(eps),
                                     mlp_workspace(x.device, H, I), epoch, int(layer), slices, grid,
-                                    fault=fault_word(x.device)))
+                                    fault=fault_word(x.device), b_early=b_early))
 
 
 _TICKETS: dict = {}
