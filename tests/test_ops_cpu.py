@@ -128,3 +128,16 @@ def test_host_device_copy_cpu_fallback():
     dst = torch.zeros(64, dtype=torch.int32)
     ops.host_device_copy(dst, src, 40)
     assert torch.equal(dst[:10], src[:10]) and int(dst[10:].abs().sum()) == 0
+
+
+def test_plan_cache_round_trip(tmp_path):
+    """Persisted start-up GEMM plans: stored per key, other keys kept, tuples restored."""
+    from vgate import ops
+    path = str(tmp_path / "sub" / "plans.json")
+    plans = {(2048, 1536): {128: (128, 0), 48: (-1, -1)}, (17920, 1536): {512: (768, 2)}}
+    assert ops.load_plan_cache(path, "k1") is None
+    ops.save_plan_cache(path, "k1", plans)
+    ops.save_plan_cache(path, "k2", {(1, 2): {3: (4, 5)}})
+    assert ops.load_plan_cache(path, "k1") == plans
+    assert ops.load_plan_cache(path, "k2") == {(1, 2): {3: (4, 5)}}
+    assert ops.load_plan_cache(path, "nope") is None

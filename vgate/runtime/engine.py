@@ -83,6 +83,9 @@ class EngineConfig:
     # GPU: time the prefill GEMM decompositions per layer shape and token bucket >= 128 at start-up
     # (ops.tune_prefill) instead of relying on the launcher's heuristic alone
     prefill_autotune: bool = os.environ.get("VGATE_PREFILL_AUTOTUNE", "1") != "0"
+    # measured plans persist per (device, native build, shapes) in this JSON file ("" = off): a restart
+    # skips the start-up measurement (ops.tune_prefill_cached)
+    plan_cache: str = os.environ.get("VGATE_PLAN_CACHE", "~/.cache/vgate/gemm_plans.json")
     arch_overrides: dict | None = None
 
     def resolve_device(self) -> torch.device:
@@ -148,6 +151,7 @@ class LLMEngine:
                                   cfg.max_model_len, cfg.block_size, eager, part,
                                   cfg.graph_token_buckets)
         self.prefill_plans: dict = {}
+        self.plans_from_cache = False
         if self.device.type == "cuda" and cfg.prefill_autotune:
             t1 = time.perf_counter()
             # prefill buckets (>= 128 rows) and the medium buckets of mixed prefill + decode steps
@@ -156,13 +160,16 @@ class LLMEngine:
             if self.tp.size > 1:
                 # rank 0 measures, every rank applies the same plans (per-rank timing noise would
                 # otherwise give TP ranks different tile / K-split choices, and N x the start-up cost)
-                plans = ops.tune_prefill(lins, ms) if self.tp.is_first else None
+                plans = ops.tune_prefill_cached(lins, ms, cfg.plan_cache)[0] if self.tp.is_first else None
                 self.prefill_plans = self.tp.broadcast_object(plans)
                 ops.apply_prefill_plans(lins, self.prefill_plans)
+                cached = False
             else:
-                self.prefill_plans = ops.tune_prefill(lins, ms)
-            log.info("prefill GEMM plans for %d shapes x %d buckets in %.2fs: %s", len(self.prefill_plans), len(ms),
-                     time.perf_counter() - t1, {f"{n}x{k}": p for (n, k), p in self.prefill_plans.items()})
+                self.prefill_plans, cached = ops.tune_prefill_cached(lins, ms, cfg.plan_cache)
+            self.plans_from_cache = cached
+            log.info("prefill GEMM plans for %d shapes x %d buckets in %.2fs%s: %s", len(self.prefill_plans), len(ms),
+                     time.perf_counter() - t1, " (plan cache)" if cached else "",
+                     {f"{n}x{k}": p for (n, k), p in self.prefill_plans.items()})
         if gloo_tp and not eager:
             cap = self.tp.custom_bytes()
             H, vloc = self.arch.hidden_size, self.model.shard.vocab
