@@ -21,7 +21,8 @@ import torch  # noqa: E402
 
 from vgate import ops  # noqa: E402
 
-PHASES = ["start", "x_staged", "gate_up_done_all_waves", "h_stored", "h_polled", "down_done", "ticket", "end"]
+PHASES = ["start", "setup_done", "x_issued", "x_landed", "x_staged", "gate_up_done_all_waves", "h_stored", "h_polled",
+          "down_done", "ticket", "end"]
 
 
 def main():
@@ -79,14 +80,14 @@ def main():
 
     # phase stamps of one fused launch (the middle layer, cold weights: the previous layers evict it)
     G = 256
-    dbg = torch.zeros(G * 8, dtype=torch.int64, device=dev)
+    dbg = torch.zeros(G * 16, dtype=torch.int64, device=dev)
     epoch.add_(1)
     for li, (gu, dn, _) in enumerate(layers):
         kw = {"dbg": dbg} if li == a.layers // 2 else {}
         ops.native().mlp_decode(x, gu.wp, dn.wp, H, I, x, x, 1e-6, ops.mlp_workspace(dev, H, I), epoch, li,
                                 a.slices, 0, b_early=a.b_early, **kw)
     torch.cuda.synchronize()
-    st = dbg.view(G, 8).cpu().double()
+    st = dbg.view(G, 16).cpu().double()
     t0 = st[:, 0].min()
     out = {}
     for i, ph in enumerate(PHASES):

@@ -95,7 +95,7 @@ __global__ __launch_bounds__(64 * W) void mlp_decode_kernel(MlpParams a) {
   TLScope tl_scope(a.tl);
 #define MLP_STAMP(i)                                                                          \
   do {                                                                                        \
-    if (a.dbg != nullptr && lane == 0) a.dbg[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    if (a.dbg != nullptr && lane == 0) a.dbg[blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
   // the wave index through readfirstlane: every range / branch below derived from it is then a
   // scalar (SCC) branch — as threadIdx.x >> 6 the compiler treats them as divergent, masks EXEC around
@@ -135,11 +135,13 @@ __global__ __launch_bounds__(64 * W) void mlp_decode_kernel(MlpParams a) {
   const int mrow = r16 < a.M ? r16 : a.M - 1;  // padded rows duplicate a real row (never stored)
   const uint32_t xoff = (uint32_t)(((size_t)mrow * a.ldx + 8 * g4) * 2);
   uint4 xv[XPW];
+  if (w == 0) MLP_STAMP(1);
 #pragma unroll
   for (int i = 0; i < XPW; ++i) {
     const int kk = w + i * W;
     xv[i] = bld<0>(rx, kk < KT1 ? xoff + (uint32_t)kk * 64u : OOB_OFF);
   }
+  if (w == 0) MLP_STAMP(2);
 
   // ---- phase A weight stream: this wave's contiguous (tile, k-step) range, NGA groups of UA ----
   const int p0 = (PA * w) / W, p1 = (PA * (w + 1)) / W;
@@ -181,7 +183,10 @@ __global__ __launch_bounds__(64 * W) void mlp_decode_kernel(MlpParams a) {
   // XWAIT: the x rows land before any weight load is issued — a CU's loads return at the rate of
   // its whole burst, in any issue order (MI355X_MICROARCH.md, prologue HBM burst): x issued ahead of
   // 192 KB of weight groups still arrived ~5.5 us late and held back the first MFMA and every refill
-  if constexpr (XWAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (XWAIT) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (w == 0) MLP_STAMP(3);
+  }
   uint4 b0[UA], b1[UA];
   loadA(b0, p0);
   if constexpr (NGA > 1) loadA(b1, p0 + UA);
@@ -201,7 +206,7 @@ __global__ __launch_bounds__(64 * W) void mlp_decode_kernel(MlpParams a) {
   ss += xor32(ss);
   if (lane < 16) ssw[w * 16 + lane] = ss;
   lds_barrier();
-  if (w == 0) MLP_STAMP(1);
+  if (w == 0) MLP_STAMP(4);
 
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   auto mmaA = [&](const uint4 (&v)[UA], int q0) {
@@ -229,7 +234,7 @@ __global__ __launch_bounds__(64 * W) void mlp_decode_kernel(MlpParams a) {
   red[(w * 2) * 64 + lane] = acc0;
   red[(w * 2 + 1) * 64 + lane] = acc1;
   lds_barrier();
-  if (w == 0) MLP_STAMP(2);  // (every wave's gate_up range done)
+  if (w == 0) MLP_STAMP(5);  // (every wave's gate_up range done)
   if (w < tl1 - tl0) {
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     for (int ww = 0; ww < W; ++ww) {
@@ -251,7 +256,7 @@ __global__ __launch_bounds__(64 * W) void mlp_decode_kernel(MlpParams a) {
       st_sc1_x4(a.hbuf, off, as_f4(gv));
     }
   }
-  if (w == 0) MLP_STAMP(3);
+  if (w == 0) MLP_STAMP(6);
 
   // ---- phase B: stage the slice's h (poll the granules) -> LDS fragments ----
   uint4* hf = xf;  // x fragments are dead (every wave passed the barrier above)
@@ -298,7 +303,7 @@ __global__ __launch_bounds__(64 * W) void mlp_decode_kernel(MlpParams a) {
     }
   }
   lds_barrier();
-  if (w == 0) MLP_STAMP(4);
+  if (w == 0) MLP_STAMP(7);
 
   // ---- phase B MFMAs: weights in registers, h from LDS ----
   f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
@@ -314,7 +319,7 @@ __global__ __launch_bounds__(64 * W) void mlp_decode_kernel(MlpParams a) {
   red[(w * 2) * 64 + lane] = c0;
   red[(w * 2 + 1) * 64 + lane] = c1;
   lds_barrier();
-  if (w == 0) MLP_STAMP(5);
+  if (w == 0) MLP_STAMP(8);
   if (LB <= 0) return;
   const int uA = pb0 / KS2, uZ = (pb1 - 1) / KS2;
   if (w > uZ - uA) return;
@@ -335,7 +340,7 @@ __global__ __launch_bounds__(64 * W) void mlp_decode_kernel(MlpParams a) {
   if (lane == 0) old = __hip_atomic_fetch_add(a.tickets + u, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   old = __builtin_amdgcn_readfirstlane(old);
   const uint32_t total = (uint32_t)(S * npc);
-  if (w == 0) MLP_STAMP(6);
+  if (w == 0) MLP_STAMP(9);
   if (old != total - 1) return;
   if (lane == 0) __hip_atomic_store(a.tickets + u, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // last arriver: every (slice, piece) slab in fixed order; all loads issued before the adds
@@ -370,7 +375,7 @@ __global__ __launch_bounds__(64 * W) void mlp_decode_kernel(MlpParams a) {
     pk.y = pack_bf2(o[2], o[3]);
     *reinterpret_cast<uint2*>(a.out + (size_t)r16 * a.ldo + n) = pk;
   }
-  MLP_STAMP(7);
+  MLP_STAMP(10);
 #undef MLP_STAMP
 }
 
