@@ -3,7 +3,8 @@
 packed-weight prefill kernels vs the launcher's choice, hipBLASLt as the oracle.
 
 tile codes (GemmArgs.ntb on the prefill path): 0 launcher, 64 / 128 = v1 128 x 64 / 128 x 128,
-256 = v2 256 x 128 (3-deep ring), 512 = v2 256 x 256, 768 = v4 256 x 128, 1024 = v4 256 x 256.
+256 = v2 256 x 128 (3-deep ring), 512 = v2 256 x 256, 768 = v4 256 x 128, 1024 = v4 256 x 256,
+1280 / 1281 = v2 128 x 128 on a 4-deep ring (4 / 8 waves), 640 / 641 = v2 128 x 64 (4 / 8 waves).
 
     python benchmarks/prefill_tile_sweep.py [--ms 384,512] [--model qwen]
 """

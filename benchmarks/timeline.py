@@ -47,6 +47,7 @@ def main():
     eng = LLMEngine(EngineConfig(model=a.model, device="cuda:0", max_model_len=2048, max_num_seqs=a.max_seqs,
                                  max_num_batched_tokens=2048, num_kv_blocks=a.kv_blocks or None, warmup=False,
                                  quantization=a.quantization))
+    eng.runner.defer_capture = False  # capture each bucket on first sight: the measured step replays a graph
     for i in range(a.batch):
         ids = [100 + (i * 131 + j * 17) % 5000 for j in range(a.ctx)]
         eng.add_request(f"r{i}", prompt_ids=ids,

@@ -85,11 +85,9 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int32_t* __restric
                                                          const int32_t* __restrict__ prev,
                                                          const bf16_t* __restrict__ table,
                                                          bf16_t* __restrict__ out, int H,
-                                                         int vstart, int vrows, unsigned long long* tl,
-                                                         uint32_t* epoch) {
+                                                         int vstart, int vrows, unsigned long long* tl) {
   TLScope tl_scope(tl);
   const int t = blockIdx.x;
-  if (epoch != nullptr && t == 0 && threadIdx.x == 0) *epoch += 1u;  // read by the NEXT launches only
   int tok = ids[t];
   if (tok < 0 && prev != nullptr) tok = prev[-tok - 1];
   const int id = tok - vstart;
@@ -100,10 +98,10 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int32_t* __restric
 }
 
 void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int T, int H,
-                      int vstart, int vrows, hipStream_t st, const int32_t* prev, uint32_t* epoch) {
+                      int vstart, int vrows, hipStream_t st, const int32_t* prev) {
   if (T <= 0) return;
   hipLaunchKernelGGL(embedding_kernel, dim3(T), dim3(256), 0, st, ids, prev, table, out, H, vstart, vrows,
-                     tl_take("embedding", T), epoch);
+                     tl_take("embedding", T));
 }
 
 // One workgroup per token. Work items:

@@ -731,6 +731,19 @@ static bool launch_prefill_epi(const GemmParams& p, int force_bn, int force_sk, 
     launch_prefill4_cfg<EPI, NORM, NTB, 128>(p, nz, st);
     return true;
   }
+  // mid-M (128 < M <= 512) tuner candidates: the 128-row tiles on a 4-deep ring, one block per CU
+  // (the 2-deep ring above waits vmcnt(0) per K-tile and relies on a second resident block)
+  if (force_bn == 1280 || force_bn == 1281) {
+    if (p.N % 128 != 0) return false;
+    if (force_bn == 1280) launch_prefill2_cfg<EPI, NORM, NTB, 128, 128, 2, 2, 4>(p, nz, st);
+    else launch_prefill2_cfg<EPI, NORM, NTB, 128, 128, 2, 4, 4>(p, nz, st);
+    return true;
+  }
+  if (force_bn == 640 || force_bn == 641) {
+    if (force_bn == 640) launch_prefill2_cfg<EPI, NORM, NTB, 128, 64, 2, 2, 4>(p, nz, st);
+    else launch_prefill2_cfg<EPI, NORM, NTB, 128, 64, 4, 2, 4>(p, nz, st);
+    return true;
+  }
   if (wide) launch_prefill_cfg<128, 128, EPI, NORM, NTB>(p, nz, st);
   else launch_prefill_cfg<128, 64, EPI, NORM, NTB>(p, nz, st);
   return true;

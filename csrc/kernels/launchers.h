@@ -105,32 +105,8 @@ void launch_rmsnorm(const uint16_t* x, int ldx, uint16_t* res, int ldres, const 
                     uint16_t* y, int ldy, int M, int H, float eps, hipStream_t st);
 
 // Embedding gather with vocab-shard masking (TP): rows outside [vstart, vstart+vrows) -> 0.
-// epoch (optional): the per-forward counter of the in-launch hand-offs (mlp_fused.hip), +1 per call.
 void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int T, int H,
-                      int vstart, int vrows, hipStream_t st, const int32_t* prev = nullptr,
-                      uint32_t* epoch = nullptr);
-
-// Fused decode MLP (mlp_fused.hip): out = [res +] down(silu(gate(x s)) * up(x s)), s = RMSNorm row
-// scale (gamma folded into wgu), M <= 16 rows, one launch. wgu: SiLU-layout fragment-packed
-// [2I/16][H/32][64][8] bf16; wd: [H/16][I/32][64][8]. Returns false (nothing launched) when the shape
-// does not fit the work split; the caller then runs the two GEMMs.
-struct MlpDecodeArgs {
-  const uint16_t* x; int ldx; int M;
-  const void* wgu; const void* wd; int H; int I;
-  uint16_t* out; int ldo; const uint16_t* res; int ldr;
-  float eps;
-  void* hbuf;                 // >= 64 * I bytes: the h granules
-  float* slabs; size_t slab_bytes;
-  uint32_t* tickets; int max_tickets;  // zeroed once, self-resetting
-  uint32_t* err;              // sticky give-up word
-  const uint32_t* epoch;      // per-forward counter (launch_embedding)
-  int layer;                  // < 127, distinct per layer of one forward
-  int slices;                 // h slices (0: 8)
-  int grid;                   // workgroups (0: the CU count; all must be resident at once)
-  unsigned long long* dbg = nullptr;  // profiling: [grid][8] phase stamps (s_memrealtime), or null
-  int b_early = 0;            // 1: issue the down weights right behind the first gate_up groups (A/B)
-};
-bool launch_mlp_decode(const MlpDecodeArgs& g, hipStream_t st);
+                      int vstart, int vrows, hipStream_t st, const int32_t* prev = nullptr);
 
 // Default-policy read sweep of [p, p + bytes) over `blocks` workgroups (MALL warm-up).
 void launch_prefetch(const void* p, size_t bytes, int blocks, hipStream_t st);

@@ -184,7 +184,7 @@ void rmsnorm(const Tensor& x, const c10::optional<Tensor>& res, const Tensor& w,
 }
 
 void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart,
-               const c10::optional<Tensor>& prev, const c10::optional<Tensor>& epoch) {
+               const c10::optional<Tensor>& prev) {
   CHECK_DEV(ids); CHECK_DEV(table); CHECK_DEV(out);
   CHECK_DT(ids, torch::kInt32); CHECK_DT(table, torch::kBFloat16); CHECK_DT(out, torch::kBFloat16);
   TORCH_CHECK(table.is_contiguous() && out.is_contiguous(), "embedding: contiguous");
@@ -193,51 +193,7 @@ void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vsta
   c10::DeviceGuard guard(ids.device());
   vgate::launch_embedding(reinterpret_cast<const int32_t*>(ids.data_ptr()), bf16p(table),
                           bf16p_mut(out), (int)T, (int)H, (int)vstart, (int)table.size(0),
-                          cur_stream(), opt_ptr<const int32_t>(prev, torch::kInt32, "prev"),
-                          reinterpret_cast<uint32_t*>(opt_ptr<int32_t>(epoch, torch::kInt32, "epoch")));
-}
-
-// Fused decode MLP (csrc/kernels/mlp_fused.hip). ws = int32 [4096 tickets | 4096 (err at 0) | 16 I
-// h-granule words | slabs]; epoch = int32 [>= 1] bumped once per forward by the embedding kernel.
-// Returns false (nothing launched) when the shape does not fit the fused work split.
-bool mlp_decode(const Tensor& x, const Tensor& wgu, const Tensor& wd, int64_t H, int64_t I, Tensor& out,
-                const c10::optional<Tensor>& res, double eps, Tensor& ws, const Tensor& epoch, int64_t layer,
-                int64_t slices, int64_t grid, const c10::optional<Tensor>& dbg, const c10::optional<Tensor>& fault,
-                int64_t b_early) {
-  CHECK_DEV(x); CHECK_DEV(wgu); CHECK_DEV(wd); CHECK_DEV(out); CHECK_DEV(ws); CHECK_DEV(epoch);
-  CHECK_DT(x, torch::kBFloat16); CHECK_DT(out, torch::kBFloat16); CHECK_DT(wgu, torch::kBFloat16);
-  CHECK_DT(wd, torch::kBFloat16); CHECK_DT(ws, torch::kInt32); CHECK_DT(epoch, torch::kInt32);
-  CHECK_LASTDIM(x); CHECK_LASTDIM(out);
-  TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && x.size(1) >= H && out.size(1) >= H, "mlp_decode: x / out [M, >= H]");
-  TORCH_CHECK(wgu.numel() == 2 * I * H && wd.numel() == H * I, "mlp_decode: packed weight sizes");
-  TORCH_CHECK(layer >= 0 && layer < 127, "mlp_decode: layer index must be in [0, 127)");
-  const int64_t M = x.size(0);
-  TORCH_CHECK(out.size(0) >= M, "mlp_decode: out rows");
-  const int64_t fixed = 8192 + 16 * I;
-  TORCH_CHECK(ws.is_contiguous() && ws.numel() > fixed, "mlp_decode: workspace too small");
-  vgate::MlpDecodeArgs g{};
-  g.x = bf16p(x); g.ldx = (int)x.stride(0); g.M = (int)M;
-  g.wgu = wgu.data_ptr(); g.wd = wd.data_ptr(); g.H = (int)H; g.I = (int)I;
-  g.out = bf16p_mut(out); g.ldo = (int)out.stride(0);
-  g.res = opt_bf16(res);
-  g.ldr = g.res ? (int)res->stride(0) : 0;
-  if (g.res) TORCH_CHECK(res->size(0) >= M && res->size(1) >= H && res->stride(1) == 1, "mlp_decode: residual shape");
-  g.eps = (float)eps;
-  int32_t* w32 = reinterpret_cast<int32_t*>(ws.data_ptr());
-  g.tickets = reinterpret_cast<uint32_t*>(w32);
-  g.max_tickets = 4096;
-  uint32_t* fw = reinterpret_cast<uint32_t*>(opt_ptr<int32_t>(fault, torch::kInt32, "fault"));
-  g.err = fw != nullptr ? fw : reinterpret_cast<uint32_t*>(w32 + 4096);
-  g.hbuf = w32 + 8192;
-  g.slabs = reinterpret_cast<float*>(w32 + fixed);
-  g.slab_bytes = (size_t)(ws.numel() - fixed) * 4;
-  g.epoch = reinterpret_cast<const uint32_t*>(epoch.data_ptr());
-  g.layer = (int)layer; g.slices = (int)slices; g.grid = (int)grid;
-  g.dbg = reinterpret_cast<unsigned long long*>(opt_ptr<int64_t>(dbg, torch::kInt64, "dbg"));
-  g.b_early = (int)b_early;
-  if (M == 0) return true;
-  c10::DeviceGuard guard(x.device());
-  return vgate::launch_mlp_decode(g, cur_stream());
+                          cur_stream(), opt_ptr<const int32_t>(prev, torch::kInt32, "prev"));
 }
 
 void rope_kv(Tensor& qkv, const Tensor& positions, const c10::optional<Tensor>& slots,
@@ -604,13 +560,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("out_stride") = 0, py::arg("tickets") = py::none(), py::arg("dbg_ts") = py::none(),
         py::arg("flash_ws") = py::none(), py::arg("fault") = py::none());
   m.def("embedding", &embedding, "vocab-sharded embedding gather (negative ids: previous step's samples)",
-        py::arg("ids"), py::arg("table"), py::arg("out"), py::arg("vstart") = 0, py::arg("prev") = py::none(),
-        py::arg("epoch") = py::none());
-  m.def("mlp_decode", &mlp_decode, "fused decode MLP: out = [res +] down(silu(gate) * up)(RMSNorm rows), one launch; "
-        "false = shape not fused", py::arg("x"), py::arg("wgu"), py::arg("wd"), py::arg("H"), py::arg("I"),
-        py::arg("out"), py::arg("res") = py::none(), py::arg("eps"), py::arg("ws"), py::arg("epoch"),
-        py::arg("layer"), py::arg("slices") = 0, py::arg("grid") = 0, py::arg("dbg") = py::none(),
-        py::arg("fault") = py::none(), py::arg("b_early") = 0);
+        py::arg("ids"), py::arg("table"), py::arg("out"), py::arg("vstart") = 0, py::arg("prev") = py::none());
   m.def("rmsnorm", &rmsnorm, "RMSNorm with optional fused residual add");
   m.def("rope_kv", &rope_kv, "NeoX RoPE + paged KV-cache write (rotated q in place or into q_out)",
         py::arg("qkv"), py::arg("positions"), py::arg("slots"), py::arg("cos_sin"), py::arg("k_cache"),

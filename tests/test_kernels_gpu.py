@@ -959,7 +959,8 @@ def test_awq_library_prefill_path(layout):
 
 @pytest.mark.parametrize("M", [128, 200, 1024, 4096])
 @pytest.mark.parametrize("bn,sk", [(0, 0), (64, 0), (128, 0), (64, 3), (256, 0), (256, 2), (512, 0), (512, 2),
-                                   (1024, 0), (1024, 3), (768, 0), (768, 2)])
+                                   (1024, 0), (1024, 3), (768, 0), (768, 2), (1280, 0), (1281, 2), (640, 3),
+                                   (641, 0)])
 def test_prefill_lds_gemm_all_epilogues(M, bn, sk):
     """The LDS-tiled MFMA prefill kernel (gemm_prefill.hip, path=1) on the decode kernels'
     fragment-packed weights, against the fp32 references: plain + in-place residual,

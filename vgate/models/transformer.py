@@ -110,14 +110,6 @@ class DecoderModel:
         self.tp_overlap_min_tokens = int(os.environ.get("VGATE_TP_OVERLAP_MIN_TOKENS", "256"))
         self.comm_stream = (torch.cuda.Stream(self.device)
                             if self.device.type == "cuda" and self.tp.size > 1 else None)
-        # decode steps (<= 16 rows): gate_up -> SiLU -> down_proj as ONE launch (ops.mlp_decode), its h
-        # hand-off tagged with a per-forward epoch the embedding kernel bumps; workspace sized here,
-        # before any graph capture
-        self.epoch = None
-        if self.device.type == "cuda":
-            self.epoch = ops.forward_epoch(self.device)
-            if ops.FUSED_MLP and self.layers and self.layers[0].gate_up.kind == "dense":
-                ops.mlp_workspace(self.device, arch.hidden_size, self.shard.inter)
 
     def _keep_library_copies(self) -> bool:
         """Plain weight copies for hipBLASLt prefill GEMMs (ops.linear, M >= 128) — a comparison
@@ -213,7 +205,7 @@ class DecoderModel:
         dev = self.device
         # RMSNorms are folded into the consuming GEMMs (deferred row scale), so a layer is
         # qkv GEMM -> attention -> o GEMM (+residual) -> gate_up GEMM -> down GEMM (+residual).
-        resid = ops.embedding(sv.ids, self.embed, vstart=sh.vocab0, prev=sv.prev_tokens, epoch=self.epoch)
+        resid = ops.embedding(sv.ids, self.embed, vstart=sh.vocab0, prev=sv.prev_tokens)
         if tp.size > 1:
             tp.all_reduce(resid)
         q = torch.empty(T, sh.hq * D, dtype=torch.bfloat16, device=dev)
@@ -244,11 +236,6 @@ class DecoderModel:
             ops.attention(q, sh.hq * D, kc, vc, sv.block_tables, sv.context_lens, sv.query_start, sv.tile_seq,
                           sv.tile_q0, attn, part_o, part_ml, sh.hq, sh.hkv, part_size, self.scale)
             self._row_parallel(attn, L.o, resid, first, norm_out=(hg, ssp, L.post_norm) if hand else None)
-            if not hand and T <= 16 and ops.mlp_decode(resid, L.gate_up, L.down, resid, resid if first else None,
-                                                      eps, li, self.epoch):
-                if tp.size > 1:
-                    tp.all_reduce(resid)
-                continue
             if hand:
                 ops.linear(hg, L.gate_up, out=mlp, prenorm=(ssp, eps))
             else:

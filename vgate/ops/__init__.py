@@ -472,76 +472,18 @@ def attention(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_s
     return out
 
 
-# fused decode MLP (csrc/kernels/mlp_fused.hip): gate_up -> SiLU -> down_proj (+residual) as one launch
-# for steps of <= 16 rows; VGATE_FUSED_MLP=1 turns it on (being tuned: slower than the two GEMMs so far)
-FUSED_MLP = os.environ.get("VGATE_FUSED_MLP", "0") == "1"
-_MLP_WS: dict = {}
-_EPOCH: dict = {}
-
-
-def mlp_workspace(device, H: int, I: int) -> torch.Tensor:
-    """Per-device int32 workspace of the fused MLP: [4096 n-tile tickets | 4096 words (give-up word at 0)
-    | 16 I words of h granules | fp32 partial slabs for up to 16 slices x 4 pieces per n-tile]. Zeroed
-    once (tickets self-reset); allocate before any graph capture — it never moves afterwards."""
-    key = str(device)
-    need = 8192 + 16 * I + (H // 16) * 16 * 4 * 256
-    t = _MLP_WS.get(key)
-    if t is None or t.numel() < need:
-        t = _MLP_WS[key] = torch.zeros(need, dtype=torch.int32, device=device)
-    return t
-
-
 _FAULT: dict = {}
 
 
 def fault_word(device) -> torch.Tensor:
-    """Per-device sticky fault word of the in-launch hand-offs (bit 0: a fused-MLP granule poll gave
-    up, bit 1: a flash K-split waiter gave up). Kernels only OR bits in; the step graph's last node
+    """Per-device sticky fault word of the in-launch hand-offs (bit 1: a flash K-split waiter gave
+    up; bit 0 is reserved). Kernels only OR bits in; the step graph's last node
     copies it to the host ring (ModelRunner.kernel_fault), and a non-zero word fails the engine."""
     key = str(device)
     t = _FAULT.get(key)
     if t is None:
         t = _FAULT[key] = torch.zeros(4, dtype=torch.int32, device=device)
     return t
-
-
-def mlp_error(device) -> int:
-    """The fused MLP's sticky give-up word (non-zero: a granule poll timed out; the step's output is
-    garbage). Reads the device (a sync): tests / health checks only."""
-    t = _MLP_WS.get(str(device))
-    own = int(t[4096].item()) if t is not None else 0
-    f = _FAULT.get(str(device))
-    return own | (int(f[0].item()) & 1 if f is not None else 0)
-
-
-def forward_epoch(device) -> torch.Tensor:
-    """Per-device forward counter: the embedding kernel adds 1 per forward and the fused MLP tags its
-    h granules with it (epoch, layer), so a replayed graph never reads the previous forward's h."""
-    key = str(device)
-    t = _EPOCH.get(key)
-    if t is None:
-        t = _EPOCH[key] = torch.zeros(4, dtype=torch.int32, device=device)
-    return t
-
-
-def mlp_decode(x: torch.Tensor, gate_up: "Linear", down: "Linear", out: torch.Tensor, residual, eps: float,
-               layer: int, epoch: torch.Tensor, slices: int = 0, grid: int = 0, b_early: int = 0) -> bool:
-    """``out = [residual +] down(silu(gate(xn)) * up(xn))``, xn = RMSNorm(x) with the gamma folded into
-    ``gate_up`` (Linear.fold_norm), as ONE launch (decode steps, <= 16 rows; out may alias x and
-    residual). Returns False and launches nothing when the layers or the shape do not fit the fused
-    form (AWQ / unfolded gamma / bias / more rows): the caller then runs the two GEMMs."""
-    if not FUSED_MLP or not _gpu(x) or x.shape[0] > 16:
-        return False
-    if gate_up.kind != "dense" or down.kind != "dense" or gate_up.layout != "silu" or gate_up.norm_gamma is None:
-        return False
-    if gate_up.bias is not None or down.bias is not None or gate_up.wp is None or down.wp is None:
-        return False
-    I, H = gate_up.N // 2, gate_up.K
-    if down.K != I or down.N != H:
-        return False
-    return bool(native().mlp_decode(x, gate_up.wp, down.wp, H, I, out, residual, float(eps),
-                                    mlp_workspace(x.device, H, I), epoch, int(layer), slices, grid,
-                                    fault=fault_word(x.device), b_early=b_early))
 
 
 _TICKETS: dict = {}
@@ -573,10 +515,9 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor
 
 
 def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None, vstart: int = 0,
-              prev: torch.Tensor | None = None, epoch: torch.Tensor | None = None):
+              prev: torch.Tensor | None = None):
     """Row gather with vocab-shard masking (rows outside this TP rank's shard are zero).
-    ids < 0 name a token the previous step sampled on the device: id = prev[-id - 1].
-    epoch (GPU): the forward counter of :func:`forward_epoch`, bumped by the same launch."""
+    ids < 0 name a token the previous step sampled on the device: id = prev[-id - 1]."""
     if out is None:
         out = torch.empty(ids.numel(), table.shape[1], dtype=table.dtype, device=table.device)
     if not _gpu(table):
@@ -584,7 +525,7 @@ def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None =
             ids = torch.where(ids < 0, prev.to(ids.device)[(-ids - 1).clamp(min=0).long()], ids)
         out.copy_(ref.embedding_ref(ids, table, vstart))
         return out
-    native().embedding(ids, table, out, vstart, prev, epoch)
+    native().embedding(ids, table, out, vstart, prev)
     return out
 
 
@@ -693,6 +634,9 @@ def _plan_bucket(plan: dict, M: int):
 PREFILL_CANDIDATES = [(0, 0), (64, 0), (128, 0), (128, 2), (128, 4), (256, 0), (256, 4), (256, 6), (768, 0),
                       (768, 2), (768, 3), (768, 4), (768, 6), (1024, 0), (1024, 2), (1024, 3), (1024, 4),
                       (1024, 6)]
+# 128-row tiles on a 4-deep ring, one block per CU (128 x 128 / 128 x 64, 4 or 8 waves): timed for
+# 64 < M <= 1024 only, where the grid of the 2-deep-ring tile is one or two partial rounds
+PREFILL_RING_CANDIDATES = [(t, s) for t in (1280, 1281, 640, 641) for s in (0, 2, 3)]
 # medium-M kernel (csrc/kernels/gemm_mid.hip, 16 < M <= 64) candidates, encoded as tile code
 # MID_BASE - W (W tiles = waves per block) and K slices (0 = its heuristic)
 MID_BASE = -10
@@ -783,7 +727,8 @@ def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = 0.05
             out = torch.empty(M, lin.N, dtype=torch.bfloat16, device=dev)
             times = {}
             cold = _cold_timer(dev) if M < 128 else None
-            for bn, sk in PREFILL_CANDIDATES + (MID_CANDIDATES if 16 < M <= 64 else []):
+            extra = MID_CANDIDATES if 16 < M <= 64 else PREFILL_RING_CANDIDATES if 64 < M <= 1024 else []
+            for bn, sk in PREFILL_CANDIDATES + extra:
                 def run():
                     C.gemm(x, wp, lin.N, lin.K, out, 0, ws=ws, **_plan_kw((bn, sk), M))
                 try:
@@ -830,7 +775,7 @@ def _plan_cache_key(lins: list, ms: list[int]) -> str:
     st = os.stat(so) if so and os.path.exists(so) else None
     shapes = sorted({(lin.N, lin.K, lin.kind) for lin in lins if getattr(lin, "wp", None) is not None})
     blob = json_dumps([props.name, props.multi_processor_count, st.st_size if st else 0,
-                       int(st.st_mtime) if st else 0, shapes, sorted(ms), PREFILL_CANDIDATES, MID_CANDIDATES])
+                       int(st.st_mtime) if st else 0, shapes, sorted(ms), PREFILL_CANDIDATES, PREFILL_RING_CANDIDATES, MID_CANDIDATES])
     return hashlib.sha1(blob.encode()).hexdigest()
 
 
@@ -933,7 +878,7 @@ def softmax_scale(head_dim: int) -> float:
 
 __all__ = [
     "native", "native_available", "pack_weight", "unpack_weight", "interleave_gate_up", "pack_awq",
-    "Linear", "linear", "attention", "workspace", "fault_word", "mlp_decode", "mlp_workspace",
-    "forward_epoch", "mlp_error", "row_permutation", "reserve_awq_scratch", "pack_awq_sz", "rmsnorm", "embedding", "rope_kv", "attention_decode", "attention_prefill",
+    "Linear", "linear", "attention", "workspace", "fault_word",
+    "row_permutation", "reserve_awq_scratch", "pack_awq_sz", "rmsnorm", "embedding", "rope_kv", "attention_decode", "attention_prefill",
     "prefill_tiles", "sample", "softmax_scale", "ref", "host_device_copy", "tune_prefill", "apply_prefill_plans",
 ]
