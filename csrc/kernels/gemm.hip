@@ -135,6 +135,8 @@ void launch_gemm(const GemmArgs& g, hipStream_t st) {
   // mixed prefill + decode steps (16 < M <= 64): the medium-M kernel when the start-up tuner
   // measured it faster (path 2, gemm_mid.hip); it declines shapes / modes it does not take
   if (g.path == 2 && launch_gemm_mid(g, st)) return;
+  // decode rows on the stream-K kernel (path 3: a decode plan / forced), else the tile-per-block kernels
+  if (g.path == 3 && launch_gemm_sk(g, st)) return;
   if (g.path == 1 || (g.path == 0 && g.M >= 128 && g.waves == 0 && g.splitk == 0)) {
     GemmArgs h = g;
     if (g.path == 0) h.ntb = 0;

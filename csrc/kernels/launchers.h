@@ -57,8 +57,16 @@ struct GemmArgs {
   float* ssp_out = nullptr;
   const float* ssp_in = nullptr;
   int ssn = 0;
+  // stream-K decode kernel (path 3, gemm_streamk.hip): zeroed publisher-slot workspace and the
+  // sticky fault word (bit 2: a partial poll gave up)
+  void* sk_pub = nullptr;
+  size_t sk_bytes = 0;
+  uint32_t* fault = nullptr;
 };
 void launch_gemm(const GemmArgs& g, hipStream_t st);
+// stream-K decode GEMM (gemm_streamk.hip): M <= 16 dense rows, one equal share of the packed weight
+// stream per CU; returns false (nothing launched) for a shape / mode it does not take
+bool launch_gemm_sk(const GemmArgs& g, hipStream_t st);
 // LDS-tiled prefill GEMM (gemm_prefill.hip) for long steps; returns false for a shape / mode it
 // does not take (caller falls back). g.ntb: forced tile width (0 heuristic, 64, 128).
 bool launch_gemm_prefill(const GemmArgs& g, hipStream_t st);

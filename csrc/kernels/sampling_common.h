@@ -1,6 +1,5 @@
-// Sampling math shared by the sampler (sampling.hip) and the LM-head GEMM epilogue that
-// produces per-tile sampling partials (gemm_epilogue.h): Philox4x32-10 uniforms, the
-// (max, Z, argmax, Gumbel key) accumulator and its merges.
+// Sampling math of the sampler (sampling.hip): Philox4x32-10 uniforms, the (max, Z, argmax,
+// Gumbel key) accumulator and its merges.
 #pragma once
 #include "common.h"
 

@@ -57,7 +57,8 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
           bool rownorm, const c10::optional<Tensor>& dbg_ts, int64_t ntb, int64_t path,
           const c10::optional<Tensor>& awq_szp, const c10::optional<Tensor>& hg_out,
           const c10::optional<Tensor>& hg_gamma, const c10::optional<Tensor>& ssp_out,
-          const c10::optional<Tensor>& ssp_in) {
+          const c10::optional<Tensor>& ssp_in, const c10::optional<Tensor>& sk_ws,
+          const c10::optional<Tensor>& fault) {
   CHECK_DEV(x); CHECK_DEV(wp); CHECK_DEV(out);
   CHECK_DT(x, torch::kBFloat16);
   CHECK_LASTDIM(x); CHECK_LASTDIM(out);
@@ -142,6 +143,13 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
     g.ssp_in = reinterpret_cast<const float*>(ssp_in->data_ptr());
     g.ssn = (int)(K / 16);
   }
+  if (sk_ws.has_value() && sk_ws->defined()) {
+    CHECK_DEV(*sk_ws); CHECK_DT(*sk_ws, torch::kInt32);
+    TORCH_CHECK(sk_ws->is_contiguous(), "sk_ws: contiguous");
+    g.sk_pub = sk_ws->data_ptr();
+    g.sk_bytes = (size_t)sk_ws->numel() * 4;
+  }
+  g.fault = reinterpret_cast<uint32_t*>(opt_ptr<int32_t>(fault, torch::kInt32, "fault"));
   c10::DeviceGuard guard(x.device());
   if (awq) vgate::launch_awq_gemm(g, cur_stream());
   else vgate::launch_gemm(g, cur_stream());
@@ -552,7 +560,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("awq_scales") = py::none(), py::arg("awq_zeros") = py::none(), py::arg("group") = 128,
         py::arg("rownorm") = false, py::arg("dbg_ts") = py::none(), py::arg("ntb") = 0, py::arg("path") = 0,
         py::arg("awq_szp") = py::none(), py::arg("hg_out") = py::none(), py::arg("hg_gamma") = py::none(),
-        py::arg("ssp_out") = py::none(), py::arg("ssp_in") = py::none());
+        py::arg("ssp_out") = py::none(), py::arg("ssp_in") = py::none(), py::arg("sk_ws") = py::none(),
+        py::arg("fault") = py::none());
   m.def("attention", &attention, "unified paged attention: decode (partitions merged in-launch) + varlen prefill tiles",
         py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),

@@ -173,6 +173,7 @@ class Linear:
         # model from the measured per-shape table (vgate/models/decode_plans.py)
         self.dec_waves = 0
         self.dec_splitk = 0
+        self.dec_sk = None  # stream-K decode kernel for this layer: None = STREAMK_DECODE
         self.dec_ntb = 0
         # prefill (M >= 128) tile / K-slice choice per M bucket, measured at engine start-up
         # (tune_prefill); empty = the launcher's heuristic
@@ -345,12 +346,20 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
     elif lin.kind == "awq" and M >= AWQ_DEQUANT_MIN_M and row_idx is None and waves == 0 and splitk == 0:
         return _linear_awq_dequant(x, lin, out, residual, norm, qkv, epi, M)
     ntb = 0
+    sk = False
     if M <= 16 and waves == 0 and splitk == 0:
         waves, splitk, ntb = lin.dec_waves, lin.dec_splitk, lin.dec_ntb  # (AWQ ntb -8: the wide int4 kernel)
+        # stream-K decode kernel (csrc/kernels/gemm_streamk.hip): per-Linear plan, else the module default
+        sk = (lin.kind == "dense" and path == 0 and row_idx is None and norm_out is None
+              and (lin.dec_sk if lin.dec_sk is not None else STREAMK_DECODE))
+        if sk:
+            path = 3
     elif M > 16 and waves == 0 and splitk == 0 and path == 0 and lin.prefill_plan and lin.kind == "dense":  # (AWQ: below)
         pk = _plan_kw(lin.prefill_plan.get(_plan_bucket(lin.prefill_plan, M)), M)
         ntb, splitk, path, waves = pk.get("ntb", 0), pk.get("splitk", 0), pk.get("path", 0), pk.get("waves", 0)
     kw = dict(bias=lin.bias, res=residual, ws=workspace(x.device), waves=waves, splitk=splitk, ntb=ntb, path=path)
+    if sk:
+        kw.update(sk_ws=sk_workspace(x.device), fault=fault_word(x.device))
     if norm is not None:
         if lin.norm_gamma is not None:  # gamma lives in the weights: row scale only
             kw.update(rownorm=True, eps=float(norm[1]))
@@ -870,6 +879,22 @@ def sample_workspace(device) -> torch.Tensor:
         ws = torch.zeros(32768, dtype=torch.int32, device=device)
         _SWS[key] = ws
     return ws
+
+
+# decode GEMMs (<= 16 rows, dense) on the stream-K kernel: one equal share of the packed weight
+# stream per CU (csrc/kernels/gemm_streamk.hip); per-layer override: Linear.dec_sk
+STREAMK_DECODE = os.environ.get("VGATE_STREAMK", "0") == "1"
+_SKWS: dict = {}
+
+
+def sk_workspace(device) -> torch.Tensor:
+    """Zeroed publisher slots of the stream-K decode kernel (the owner clears what it reads, so it
+    stays zero between launches): 64 MiB covers ntiles x (contributors - 1) x 3 KiB of any model."""
+    key = str(device)
+    t = _SKWS.get(key)
+    if t is None:
+        t = _SKWS[key] = torch.zeros(16 * 2**20, dtype=torch.int32, device=device)
+    return t
 
 
 def softmax_scale(head_dim: int) -> float:
