@@ -10,19 +10,20 @@
 //
 // A block's range = [lead | body]: the lead is the tail of a tile that started in an earlier
 // block (a partial), the body is whole tiles plus possibly the head of a tile that continues in
-// later blocks. Waves: WL lead waves split the lead, the rest split the body (every wave one
-// contiguous range, at most two tiles: accumulators A / B). The waves meet in LDS (fixed wave
-// order). Then:
-//   * whole tiles of the body -> the epilogue directly (bias / residual / SiLU*mul / QKV+RoPE+KV,
-//     the decode kernels' epilogue code, deferred RMSNorm row scale from the same x fragments);
-//   * the lead partial -> published to its owner (the block holding the tile's first k-step) as
-//     data-carrying granules: {value, tag} 8-byte pairs in 16-B device-coherent (sc1) stores —
-//     the data is its own flag (cdna_hip_programming.md Guideline 16 R2), no drain, fence or
-//     counter on the publisher;
-//   * the owner, after its own range, polls the granules of the later blocks of its last tile
-//     (one sc1 round trip when they are there: those blocks published as soon as their range was
-//     done), adds them in block order (bit-reproducible), runs the epilogue and clears the slots
-//     for the next launch (kernel boundary in between).
+// later blocks. Every wave takes 1/W of the lead FIRST, then 1/W of the body (at most two body
+// tiles per wave: accumulators A / B, parked in registers at the boundaries). Then:
+//   * the lead partial leaves early: the last wave to finish its lead share (LDS counter) adds
+//     the W partials in wave order and publishes them to the tile's owner (the block holding the
+//     tile's first k-step) as data-carrying granules: {value, tag} 8-byte pairs in 16-B
+//     device-coherent (sc1) stores — the data is its own flag (cdna_hip_programming.md Guideline
+//     16 R2), no drain, fence or counter on the publisher — while the body loads stream on;
+//   * the waves meet in LDS (fixed wave order); whole body tiles -> the epilogue directly (bias /
+//     residual / SiLU*mul / QKV+RoPE+KV, the decode kernels' epilogue code, deferred RMSNorm row
+//     scale from the same x fragments);
+//   * the owner of the last body tile, once its own range is done, polls the later blocks'
+//     granules (published at the start of their ranges: normally there already), adds them in
+//     block order (bit-reproducible), runs the epilogue and clears the slots for the next launch
+//     (kernel boundary in between).
 // Every global load of the stream is issued unconditionally (buffer loads; a slot past the wave's
 // range is an offset beyond the resource: zeros, no memory traffic), so the compiler's vmcnt
 // bookkeeping stays exact (no vmcnt(0) at branch joins). Polls are bounded: a give-up sets bit 2
@@ -61,13 +62,6 @@ __device__ __host__ __forceinline__ int sk_start(int b, int Lp, int G) { return 
 // the block whose range holds pack X: max b with sk_start(b) <= X
 __device__ __host__ __forceinline__ int sk_owner(int X, int Lp, int G) { return ((X + 1) * G + Lp - 1) / Lp - 1; }
 
-// the lead waves of a block: proportional to the lead's share of the range, >= 1 each side
-__device__ __host__ __forceinline__ int sk_lead_waves(int nlead, int nbody, int W) {
-  if (nlead <= 0) return 0;
-  if (nbody <= 0) return W;
-  int wl = (nlead * W + (nlead + nbody) / 2) / (nlead + nbody);
-  return wl < 1 ? 1 : (wl > W - 1 ? W - 1 : wl);
-}
 
 }  // namespace
 
@@ -85,19 +79,26 @@ __global__ __launch_bounds__(64 * W) void gemm_sk_kernel(GemmParams p, SkParams 
   const int t0 = qa / KP;
   const int le = (qa % KP) ? min(qb, (t0 + 1) * KP) : qa;  // lead = [qa, le), body = [le, qb)
   const int nlead = le - qa, nbody = qb - le;
-  const int WL = sk_lead_waves(nlead, nbody, W);
-  const bool lead = w < WL;
-  int ka, kb;
-  if (lead) {
-    ka = qa + (nlead * w) / WL;
-    kb = qa + (nlead * (w + 1)) / WL;
-  } else {
-    const int wb = w - WL, WB = W - WL;
-    ka = le + (nbody * wb) / WB;
-    kb = le + (nbody * (wb + 1)) / WB;
-  }
-  const int tA = ka / KP, kk0 = ka - tA * KP;  // first tile of the wave, pack index inside it
-  const int bnd = (tA + 1) * KP;               // packs >= bnd: the wave's second tile
+  // every wave takes 1/W of the lead, then 1/W of the body: the lead partial is complete after the
+  // first few packs of every wave and leaves early (its owner waits on it at the END of its range)
+  const int la = qa + (nlead * w) / W, nl = qa + (nlead * (w + 1)) / W - la;
+  const int ba = le + (nbody * w) / W, nb = le + (nbody * (w + 1)) / W - ba;
+  const int n = nl + nb;
+  const int lpos0 = la - t0 * KP;           // lead: pack index inside tile t0
+  const int tA = ba / KP, bpos0 = ba - tA * KP;
+  const int bnd = (tA + 1) * KP;            // body packs >= bnd: the wave's second body tile
+
+  // LDS: lead partials [W][64] f32x4 + [W][16] sums + arrival counter | body [W][2] accumulators,
+  // [W][2][16] sums, [W][2] tile ids
+  f32x4* slead = reinterpret_cast<f32x4*>(smem);
+  float* ssl = reinterpret_cast<float*>(smem + W * 64 * 16);
+  int* lcnt = reinterpret_cast<int*>(smem + W * 64 * 16 + W * 16 * 4);
+  char* body = smem + W * 64 * 16 + W * 16 * 4 + 16;
+  f32x4* sacc = reinterpret_cast<f32x4*>(body);
+  float* sss = reinterpret_cast<float*>(body + W * 2 * 64 * 16);
+  int* stile = reinterpret_cast<int*>(body + W * 2 * 64 * 16 + W * 2 * 16 * 4);
+  if (threadIdx.x == 0) *lcnt = 0;
+  __syncthreads();
 
   const __amdgpu_buffer_rsrc_t rW = rsrc_of(p.wp), rX = rsrc_of(p.x);
   const int mrow = XP > 1 ? r16 % R : r16;
@@ -106,9 +107,10 @@ __global__ __launch_bounds__(64 * W) void gemm_sk_kernel(GemmParams p, SkParams 
   auto load = [&](uint4 (&wv)[UA], uint4 (&xv)[UP], int g) {
 #pragma unroll
     for (int u = 0; u < UP; ++u) {
-      const int P = ka + g * UP + u;
-      const bool ok = P < kb;
-      int pos = kk0 + g * UP + u;  // pack index inside its tile (one boundary crossing at most)
+      const int i = g * UP + u;
+      const bool inl = i < nl, ok = i < n;
+      const int P = inl ? la + i : ba + (i - nl);
+      int pos = inl ? lpos0 + i : bpos0 + (i - nl);  // pack index inside its tile (one crossing at most)
       pos = pos >= KP ? pos - KP : pos;
 #pragma unroll
       for (int v = 0; v < XP; ++v)
@@ -116,16 +118,46 @@ __global__ __launch_bounds__(64 * W) void gemm_sk_kernel(GemmParams p, SkParams 
       xv[u] = skld<0>(rX, ok && xok ? xbase + (uint32_t)pos * (uint32_t)(XP * 64) : SK_OOB);
     }
   };
-  // one running accumulator; at the wave's tile boundary (pack bnd) it is parked in accA and
-  // restarted. Packs past the range were loaded as zeros and add nothing: the MFMAs run
-  // unconditionally (a branch around them made the compiler re-issue loads under it and drain vmcnt)
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accA = {0.f, 0.f, 0.f, 0.f}, accB = {0.f, 0.f, 0.f, 0.f};
-  float ss = 0.f, ssA = 0.f, ssB = 0.f;
+  // the lead partial leaves as data-carrying granules to its owner's slot (t0, j - 1): the last of
+  // the W waves to arrive (LDS counter) adds their partials in wave order and publishes
+  auto lead_arrive = [&](const f32x4& a, float sq) {
+    if (nlead <= 0) return;  // block-uniform
+    float q = sq;
+    if constexpr (NORM) {
+      q += xor16(q);
+      q += xor32(q);
+    }
+    slead[w * 64 + lane] = a;
+    if (lane < 16) ssl[w * 16 + lane] = q;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    int last = 0;
+    if (lane == 0) last = __hip_atomic_fetch_add(lcnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == W - 1;
+    last = __builtin_amdgcn_readfirstlane(last);
+    if (!last) return;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    float t = 0.f;
+    for (int ww = 0; ww < W; ++ww) {
+      v += slead[ww * 64 + lane];
+      t += ssl[ww * 16 + r16];
+    }
+    const int j = b - sk_owner(t0 * KP, Lp, G);  // >= 1: the tile started in an earlier block
+    const uint32_t off = (uint32_t)((((size_t)t0 * (s.cmax - 1) + (j - 1)) * 64 + lane) * 3 * 16);
+    skst(s.pub, off, make_uint4(__float_as_uint(v[0]), SK_TAG, __float_as_uint(v[1]), SK_TAG));
+    skst(s.pub, off + 16, make_uint4(__float_as_uint(v[2]), SK_TAG, __float_as_uint(v[3]), SK_TAG));
+    skst(s.pub, off + 32, make_uint4(__float_as_uint(t), SK_TAG, 0u, 0u));
+  };
+  // one running accumulator, parked at the lead -> body switch (pack nl: the lead partial leaves)
+  // and at the body's tile boundary (accA). Packs past the range were loaded as zeros and add
+  // nothing: the MFMAs run unconditionally (a branch around them made the compiler re-issue loads
+  // under it and drain vmcnt).
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accL = {0.f, 0.f, 0.f, 0.f}, accA = {0.f, 0.f, 0.f, 0.f},
+        accB = {0.f, 0.f, 0.f, 0.f};
+  float ss = 0.f, ssL = 0.f, ssA = 0.f, ssB = 0.f;
   const uint32_t lom = r16 < R ? ~0u : 0u;
   auto mma = [&](const uint4 (&wv)[UA], const uint4 (&xv)[UP], int g) {
 #pragma unroll
     for (int u = 0; u < UP; ++u) {
-      const int P = ka + g * UP + u;
+      const int i = g * UP + u;
       uint4 a[XP];
       if constexpr (XP == 1) {
         a[0] = xv[u];
@@ -137,7 +169,13 @@ __global__ __launch_bounds__(64 * W) void gemm_sk_kernel(GemmParams p, SkParams 
           a[3] = and_mask(row_ror<3 * R>(xv[u]), lom);
         }
       }
-      if (P == bnd && P < kb) {  // wave-uniform: register moves only
+      if (i == nl) {  // wave-uniform: the lead share is done (register moves; it leaves at the group's end)
+        accL = acc;
+        acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        ssL = ss;
+        ss = 0.f;
+      }
+      if (i > nl && ba + (i - nl) == bnd && i < n) {  // the body's tile boundary: register moves only
         accA = acc;
         acc = f32x4{0.f, 0.f, 0.f, 0.f};
         ssA = ss;
@@ -171,8 +209,15 @@ __global__ __launch_bounds__(64 * W) void gemm_sk_kernel(GemmParams p, SkParams 
       if (g + 2 < NGA) load(w0, x0, g + 2);
     }
     __builtin_amdgcn_sched_barrier(0);
+    // the group in which the lead share ended (a wave without one arrives after group 0)
+    if (nl < (g + 1) * UP && (nl >= g * UP || g == 0)) lead_arrive(accL, ssL);
   }
-  if (kb > bnd) {
+  if (nl >= NGA * UP) {  // (a lead share filling every register group: parked nowhere yet)
+    lead_arrive(acc, ss);
+    acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    ss = 0.f;
+  }
+  if (ba + nb > bnd && nb > 0) {
     accB = acc;
     ssB = ss;
   } else {
@@ -186,10 +231,7 @@ __global__ __launch_bounds__(64 * W) void gemm_sk_kernel(GemmParams p, SkParams 
     ssB += xor32(ssB);
   }
 
-  // ---- the waves meet in LDS: [W][2] accumulators, row sums, tile ids ----
-  f32x4* sacc = reinterpret_cast<f32x4*>(smem);
-  float* sss = reinterpret_cast<float*>(smem + W * 2 * 64 * 16);
-  int* stile = reinterpret_cast<int*>(smem + W * 2 * 64 * 16 + W * 2 * 16 * 4);
+  // ---- the body waves meet in LDS ----
   sacc[(w * 2) * 64 + lane] = accA;
   sacc[(w * 2 + 1) * 64 + lane] = accB;
   if (lane < 16) {
@@ -197,44 +239,27 @@ __global__ __launch_bounds__(64 * W) void gemm_sk_kernel(GemmParams p, SkParams 
     sss[(w * 2 + 1) * 16 + lane] = ssB;
   }
   if (lane == 0) {
-    stile[w * 2] = ka < kb ? tA : -1;
-    stile[w * 2 + 1] = kb > bnd ? tA + 1 : -1;
+    stile[w * 2] = nb > 0 ? tA : -1;
+    stile[w * 2 + 1] = ba + nb > bnd && nb > 0 ? tA + 1 : -1;
   }
   __syncthreads();
 
-  // tasks: [lead publish] + body tiles, wave w takes tasks w, w + W, ...
-  const int has_lead = nlead > 0 ? 1 : 0;
+  // the body tiles, wave w takes tiles w, w + W, ...: whole tiles -> epilogue; the last one, if it
+  // continues in later blocks, first adds their published lead partials (block order)
   const int tb0 = le / KP, tb1 = nbody > 0 ? (qb - 1) / KP : tb0 - 1;
-  const int ntask = has_lead + (tb1 - tb0 + 1);
-  const size_t slot_words = (size_t)64 * 3;  // uint4 per (tile, publisher) slot
-  for (int task = w; task < ntask; task += W) {
+  for (int t = tb0 + w; t <= tb1; t += W) {
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    float ss = 0.f;
-    if (has_lead && task == 0) {
-      // the lead partial of tile t0: its lead waves' slot A in wave order -> publisher slot j - 1
-      for (int ww = 0; ww < WL; ++ww) {
-        v += sacc[(ww * 2) * 64 + lane];
-        ss += sss[(ww * 2) * 16 + r16];
-      }
-      const int j = b - sk_owner(t0 * KP, Lp, G);  // >= 1
-      const uint32_t off = (uint32_t)((((size_t)t0 * (s.cmax - 1) + (j - 1)) * 64 + lane) * 3 * 16);
-      skst(s.pub, off, make_uint4(__float_as_uint(v[0]), SK_TAG, __float_as_uint(v[1]), SK_TAG));
-      skst(s.pub, off + 16, make_uint4(__float_as_uint(v[2]), SK_TAG, __float_as_uint(v[3]), SK_TAG));
-      skst(s.pub, off + 32, make_uint4(__float_as_uint(ss), SK_TAG, 0u, 0u));
-      continue;
-    }
-    const int t = tb0 + task - has_lead;
-    for (int ww = WL; ww < W; ++ww) {
+    float sq = 0.f;
+    for (int ww = 0; ww < W; ++ww) {
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         if (stile[ww * 2 + k] == t) {
           v += sacc[(ww * 2 + k) * 64 + lane];
-          ss += sss[(ww * 2 + k) * 16 + r16];
+          sq += sss[(ww * 2 + k) * 16 + r16];
         }
       }
     }
     if ((t + 1) * KP > qb) {
-      // owned tile continuing in later blocks: their published partials, in block order
       const int tend = (t + 1) * KP;
       for (int j = 1; j < s.cmax && sk_start(b + j, Lp, G) < tend; ++j) {
         const uint32_t off = (uint32_t)((((size_t)t * (s.cmax - 1) + (j - 1)) * 64 + lane) * 3 * 16);
@@ -253,14 +278,14 @@ __global__ __launch_bounds__(64 * W) void gemm_sk_kernel(GemmParams p, SkParams 
           __builtin_amdgcn_s_sleep(1);
         }
         v += f32x4{__uint_as_float(g0.x), __uint_as_float(g0.z), __uint_as_float(g1.x), __uint_as_float(g1.z)};
-        ss += __uint_as_float(g2.x);
+        sq += __uint_as_float(g2.x);
         const uint4 z = make_uint4(0u, 0u, 0u, 0u);
         skst(s.pub, off, z);
         skst(s.pub, off + 16, z);
         skst(s.pub, off + 32, z);
       }
     }
-    if constexpr (NORM) v *= rsqrtf(ss / (float)p.K + p.eps);
+    if constexpr (NORM) v *= rsqrtf(sq / (float)p.K + p.eps);
     f32x4 vv[1] = {v};
     epilogue<1, EPI, false>(p, vv, r16, t, 4 * g4, EpiPre<1>{}, r16 < p.M);
   }
@@ -289,13 +314,9 @@ SkPlan sk_plan(int ntiles, int KT, int M, int G, int W, int UA) {
     const int t0 = qa / KP;
     const int le = (qa % KP) ? std::min(qb, (t0 + 1) * KP) : qa;
     const int nlead = le - qa, nbody = qb - le;
-    const int WL = sk_lead_waves(nlead, nbody, W);
-    if (WL > 0) maxn = std::max(maxn, (nlead + WL - 1) / WL);
-    if (WL < W) {
-      const int nb = (nbody + (W - WL) - 1) / (W - WL);
-      if (nb > KP) return pl;  // a body wave would cross two tile boundaries
-      maxn = std::max(maxn, nb);
-    }
+    const int nlw = (nlead + W - 1) / W, nbw = (nbody + W - 1) / W;
+    if (nbw > KP) return pl;  // a body share would cross two tile boundaries
+    maxn = std::max(maxn, nlw + nbw);
   }
   // contributors per tile: blocks overlapping [t KP, (t + 1) KP)
   int cmax = 1;
@@ -311,11 +332,21 @@ SkPlan sk_plan(int ntiles, int KT, int M, int G, int W, int UA) {
   return pl;
 }
 
-template <int EPI, int NORM, int XP>
-void sk_launch_xp(const GemmParams& p, const SkParams& s, int nga, int G, hipStream_t st) {
-  constexpr int W = 8, UA = 8;
-  const size_t lds = W * 2 * 64 * 16 + W * 2 * 16 * 4 + W * 2 * 4;
-#define VG_SK(N) hipLaunchKernelGGL((gemm_sk_kernel<W, UA, N, EPI, NORM, XP>), dim3(G), dim3(64 * W), lds, st, p, s)
+// The LDS request pins the blocks per CU: the equal shares only balance the chip if no CU takes
+// two of them while another idles (the dispatcher packs workgroups onto a CU while its registers
+// and LDS allow). 1 per CU: > 80 KiB of the 160 KiB; 2 per CU: > 160 / 3 KiB.
+template <int W, int UA, int EPI, int NORM, int XP>
+void sk_launch_cfg(const GemmParams& p, const SkParams& s, int nga, int G, int per_cu, hipStream_t st) {
+  constexpr size_t need = W * 64 * 16 + W * 16 * 4 + 16 + W * 2 * 64 * 16 + W * 2 * 16 * 4 + W * 2 * 4;
+  const size_t lds = std::max(need, per_cu == 1 ? (size_t)82 * 1024 : (size_t)54 * 1024);
+#define VG_SK(N)                                                                                              \
+  do {                                                                                                        \
+    auto kern = gemm_sk_kernel<W, UA, N, EPI, NORM, XP>;                                                      \
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),                        \
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess; \
+    (void)attr;                                                                                               \
+    hipLaunchKernelGGL(kern, dim3(G), dim3(64 * W), lds, st, p, s);                                           \
+  } while (0)
   if (nga == 1) VG_SK(1);
   else if (nga == 2) VG_SK(2);
   else if (nga == 4) VG_SK(4);
@@ -323,11 +354,20 @@ void sk_launch_xp(const GemmParams& p, const SkParams& s, int nga, int G, hipStr
 #undef VG_SK
 }
 
+// (W, UA): 8 waves x groups of 8 k-steps (default), 4 x 8, 8 x 4 (sweeps: GemmArgs waves / ntb)
+template <int EPI, int NORM, int XP>
+void sk_launch_xp(const GemmParams& p, const SkParams& s, int w, int ua, int nga, int G, int per_cu, hipStream_t st) {
+  if (w == 4) sk_launch_cfg<4, 8, EPI, NORM, XP>(p, s, nga, G, per_cu, st);
+  else if (ua == 4) sk_launch_cfg<8, 4, EPI, NORM, XP>(p, s, nga, G, per_cu, st);
+  else sk_launch_cfg<8, 8, EPI, NORM, XP>(p, s, nga, G, per_cu, st);
+}
+
 template <int EPI, int NORM>
-void sk_launch(const GemmParams& p, const SkParams& s, int xp, int nga, int G, hipStream_t st) {
-  if (xp == 4) sk_launch_xp<EPI, NORM, 4>(p, s, nga, G, st);
-  else if (xp == 2) sk_launch_xp<EPI, NORM, 2>(p, s, nga, G, st);
-  else sk_launch_xp<EPI, NORM, 1>(p, s, nga, G, st);
+void sk_launch(const GemmParams& p, const SkParams& s, int xp, int w, int ua, int nga, int G, int per_cu,
+               hipStream_t st) {
+  if (xp == 4) sk_launch_xp<EPI, NORM, 4>(p, s, w, ua, nga, G, per_cu, st);
+  else if (xp == 2) sk_launch_xp<EPI, NORM, 2>(p, s, w, ua, nga, G, per_cu, st);
+  else sk_launch_xp<EPI, NORM, 1>(p, s, w, ua, nga, G, per_cu, st);
 }
 
 }  // namespace
@@ -338,7 +378,13 @@ bool launch_gemm_sk(const GemmArgs& g, hipStream_t st) {
       g.sk_pub == nullptr || g.K % 32 != 0)
     return false;
   if (g.epi == EPI_QKV && (g.N / 16) % 2 != 0) return false;
-  const int G = cu_count_gemm(), W = 8, UA = 8;
+  const int norm = g.rownorm ? 2 : 0;
+  // instantiated pairs: plain / f32 without a norm, SiLU / QKV with the folded-gamma row scale
+  if ((norm == 2) != (g.epi == EPI_SILU || g.epi == EPI_QKV)) return false;
+  // sweeps: g.waves 4 = 4 waves per block, g.ntb 4 = groups of 4 k-steps, g.splitk 2 = 2 blocks per CU
+  const int W = g.waves == 4 ? 4 : 8, UA = (g.ntb == 4 && W == 8) ? 4 : 8;
+  const int per_cu = g.splitk == 2 ? 2 : 1;
+  const int G = cu_count_gemm() * per_cu;
   const int ntiles = g.N / 16, KT = g.K / 32;
   const SkPlan pl = sk_plan(ntiles, KT, g.M, G, W, UA);
   if (!pl.ok) return false;
@@ -358,17 +404,12 @@ bool launch_gemm_sk(const GemmArgs& g, hipStream_t st) {
                         : g.epi == EPI_F32 ? "gemm_sk_f32" : (g.K > g.N ? "gemm_sk_down" : "gemm_sk_o");
   p.dbg_ts = g.dbg_ts != nullptr ? g.dbg_ts : tl_take(tl_name, G);
   SkParams s{KT, ntiles * KT / pl.XP, pl.cmax, reinterpret_cast<uint4*>(g.sk_pub), g.fault};
-  const int norm = g.rownorm ? 2 : 0;
-#define VG_SKE(E)                                                          \
-  do {                                                                     \
-    if (norm == 2) sk_launch<E, 2>(p, s, pl.XP, pl.NGA, G, st);            \
-    else sk_launch<E, 0>(p, s, pl.XP, pl.NGA, G, st);                      \
-  } while (0)
+#define VG_SKE(E, NORM_) sk_launch<E, NORM_>(p, s, pl.XP, W, UA, pl.NGA, G, per_cu, st)
   switch (g.epi) {
-    case EPI_SILU: VG_SKE(EPI_SILU); break;
-    case EPI_QKV: VG_SKE(EPI_QKV); break;
-    case EPI_F32: VG_SKE(EPI_F32); break;
-    default: VG_SKE(EPI_BF16);
+    case EPI_SILU: VG_SKE(EPI_SILU, 2); break;
+    case EPI_QKV: VG_SKE(EPI_QKV, 2); break;
+    case EPI_F32: VG_SKE(EPI_F32, 0); break;
+    default: VG_SKE(EPI_BF16, 0);
   }
 #undef VG_SKE
   return true;

@@ -29,17 +29,48 @@
 
 namespace vgate {
 
+// Lane exchange on the VALU (no LDS round trip per step, unlike __shfl_xor's ds_bpermute): DPP
+// quad permutes for partners 1 and 2, row rotations by 4 and 8 (after the quad steps every lane of
+// a quad holds the quad's merge, so rotations complete the 16-lane row), permlane swaps for 16 / 32.
+template <int K>
+__device__ __forceinline__ uint32_t lane_x(uint32_t v) {
+  if constexpr (K == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+  else if constexpr (K == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);  // [2,3,0,1]
+  else if constexpr (K == 4) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, false);  // row_ror:4
+  else if constexpr (K == 8) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  else if constexpr (K == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (threadIdx.x & 16) ? r[0] : r[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (threadIdx.x & 32) ? r[0] : r[1];
+  }
+}
+template <int K>
+__device__ __forceinline__ void acc_step(Acc& a, float c) {
+  const float om = __uint_as_float(lane_x<K>(__float_as_uint(a.mx)));
+  const float oz = __uint_as_float(lane_x<K>(__float_as_uint(a.z)));
+  const int oi = (int)lane_x<K>((uint32_t)a.amx);
+  const float ok = __uint_as_float(lane_x<K>(__float_as_uint(a.gk)));
+  const int ogi = (int)lane_x<K>((uint32_t)a.gi);
+  const float ocnt = __uint_as_float(lane_x<K>(__float_as_uint(a.cnt)));
+  const float oq = __uint_as_float(lane_x<K>(__float_as_uint(a.q)));
+  merge_mz(a.mx, a.z, a.amx, om, oz, oi, c);
+  merge_g(a.gk, a.gi, ok, ogi);
+  a.cnt += ocnt;
+  a.q += oq;
+}
+
 // Block-wide reduction of an Acc into LDS slot `out` (thread 0 holds the result).
 __device__ __forceinline__ void block_reduce_acc(Acc& a, float c, Acc* red) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   __syncthreads();  // `red` may still be read by thread 0 from a previous reduction
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    merge_mz(a.mx, a.z, a.amx, __shfl_xor(a.mx, o, 64), __shfl_xor(a.z, o, 64), __shfl_xor(a.amx, o, 64), c);
-    merge_g(a.gk, a.gi, __shfl_xor(a.gk, o, 64), __shfl_xor(a.gi, o, 64));
-    a.cnt += __shfl_xor(a.cnt, o, 64);
-    a.q += __shfl_xor(a.q, o, 64);
-  }
+  acc_step<1>(a, c);
+  acc_step<2>(a, c);
+  acc_step<4>(a, c);
+  acc_step<8>(a, c);
+  acc_step<16>(a, c);
+  acc_step<32>(a, c);
   if (lane == 0) red[wid] = a;
   __syncthreads();
   if (threadIdx.x == 0) {

@@ -173,7 +173,7 @@ class Linear:
         # model from the measured per-shape table (vgate/models/decode_plans.py)
         self.dec_waves = 0
         self.dec_splitk = 0
-        self.dec_sk = None  # stream-K decode kernel for this layer: None = STREAMK_DECODE
+        self.dec_sk = None  # stream-K decode kernel: None = STREAMK_DECODE, bool, or (waves, blocks/CU, group)
         self.dec_ntb = 0
         # prefill (M >= 128) tile / K-slice choice per M bucket, measured at engine start-up
         # (tune_prefill); empty = the launcher's heuristic
@@ -352,8 +352,9 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
         # stream-K decode kernel (csrc/kernels/gemm_streamk.hip): per-Linear plan, else the module default
         sk = (lin.kind == "dense" and path == 0 and row_idx is None and norm_out is None
               and (lin.dec_sk if lin.dec_sk is not None else STREAMK_DECODE))
-        if sk:
+        if sk:  # (W, blocks per CU, k-steps per register group) of the plan, 0 = the kernel's default
             path = 3
+            waves, splitk, ntb = lin.dec_sk if isinstance(lin.dec_sk, tuple) else (0, 0, 0)
     elif M > 16 and waves == 0 and splitk == 0 and path == 0 and lin.prefill_plan and lin.kind == "dense":  # (AWQ: below)
         pk = _plan_kw(lin.prefill_plan.get(_plan_bucket(lin.prefill_plan, M)), M)
         ntb, splitk, path, waves = pk.get("ntb", 0), pk.get("splitk", 0), pk.get("path", 0), pk.get("waves", 0)
