@@ -48,7 +48,15 @@ def layer_kinds(live):
     nxt = None
     for x in live:
         n = x["kernel"]
-        if n.startswith("gemm_qkv"):
+        if n.startswith("gemm_sk_"):  # stream-K launches carry their role in the name
+            k = {"gemm_sk_qkv": "qkv", "gemm_sk_gate_up": "gate_up", "gemm_sk_f32": "lm_head"}.get(n)
+            if k is None:
+                k, nxt = (nxt or "?"), None
+            elif k == "qkv":
+                nxt = "o"
+            elif k == "gate_up":
+                nxt = "down"
+        elif n.startswith("gemm_qkv"):
             k, nxt = "qkv", "o"
         elif n.startswith("attention") or n.startswith("attn"):
             k = "attention"

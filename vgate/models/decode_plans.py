@@ -8,17 +8,28 @@ their current plan (benchmarks/decode_sweep.py for TP = 1 models, benchmarks/tp_
 --sweep for one TP rank's shapes). A shape missing here measured best on the heuristic.
 
 Key: (N, K, layout, weight kind) of the packed weight; layout "qkv" / "silu" / "plain".
+Value: (waves, K slices, column tiles per block) of the tile-per-block kernels, or
+("sk", waves, blocks per CU, k-steps per register group) for the stream-K kernel
+(csrc/kernels/gemm_streamk.hip: one equal share of the weight stream per CU), which wins on the
+large matrices where the tile count leaves CUs uneven (benchmarks/sk_probe.py,
+profiles/r4_streamk_probe.log).
 """
 from __future__ import annotations
 
-PLANS: dict[tuple[int, int, str, str], tuple[int, int, int]] = {
+PLANS: dict[tuple[int, int, str, str], tuple] = {
     # Llama-3-70B TP = 8, one rank, batch 8, ctx 128 (profiles/r3_tp8_rank_sweep.log):
-    # per-rank step 5027 -> 4859 us with all five applied
+    # per-rank step 5027 -> 4859 us with the round-3 five applied
     (1280, 8192, "qkv", "dense"): (8, 3, 0),     # 80 tiles x 256 k-steps: 240 blocks (heuristic 8 x 2: +33 us)
     (8192, 1024, "plain", "dense"): (2, 1, 1),   # o_proj
-    (7168, 8192, "silu", "dense"): (4, 1, 0),    # gate_up: 448 one-tile blocks at 4 waves (heuristic 8: +118 us)
-    (8192, 3584, "plain", "dense"): (8, 1, 2),   # down_proj
+    # gate_up / down_proj on stream-K, 4 waves, one block per CU (r4 probe: 23.5 vs 26.2 us and 12.8 vs
+    # 13.5 us per launch; round 3: 448 one-tile blocks at 4 waves, down (8, 1, 2))
+    (7168, 8192, "silu", "dense"): ("sk", 4, 1, 8),
+    (8192, 3584, "plain", "dense"): ("sk", 4, 1, 8),
     (16032, 8192, "plain", "dense"): (8, 1, 1),  # LM head shard
+    # Llama-3-8B, batch 8 (r4 probe): qkv 13.6 vs 15.1, gate_up 39.0 vs 41.3, down 21.1 vs 21.9 us
+    (6144, 4096, "qkv", "dense"): ("sk", 8, 1, 4),
+    (28672, 4096, "silu", "dense"): ("sk", 4, 1, 8),
+    (4096, 14336, "plain", "dense"): ("sk", 4, 1, 8),
     # Qwen2.5-1.5B AWQ int4, batch 8, ctx 100 (profiles/r3_awq_decode_sweep.log, whole-step replays;
     # baseline 1287.8 us): qkv on awq_stream_kernel (packed scales, XP-packed activations, 4 waves x 3
     # k-quads) instead of the K-split awq_gemm_kernel, down_proj in 8 K slices of 4 waves
@@ -39,6 +50,9 @@ def apply(model) -> int:
     for lin in lins:
         p = PLANS.get((lin.N, lin.K, lin.layout, lin.kind))
         if p is not None:
-            lin.dec_waves, lin.dec_splitk, lin.dec_ntb = p
+            if p[0] == "sk":
+                lin.dec_sk = tuple(p[1:])
+            else:
+                lin.dec_waves, lin.dec_splitk, lin.dec_ntb = p
             n += 1
     return n
