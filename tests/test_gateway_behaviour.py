@@ -450,7 +450,9 @@ async def test_dryrun_capacity_bounds_concurrent_generations(monkeypatch):
     monkeypatch.setattr(base, "_DRYRUN_MAX_CONCURRENCY", 0)
     t0 = time.perf_counter()
     await asyncio.gather(*(be.agenerate(f"q{i}", {"max_tokens": 1}) for i in range(4)))
-    assert time.perf_counter() - t0 < 0.08  # without the capacity knob calls do not queue
+    # without the capacity knob calls do not queue: one ~40 ms round fewer (relative, so a loaded
+    # host or the asyncio debug pass does not flake it)
+    assert time.perf_counter() - t0 < took - 0.02
 
 
 # ------------------------------------------------------------------------- cache log

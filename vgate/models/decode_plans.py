@@ -21,15 +21,15 @@ PLANS: dict[tuple[int, int, str, str], tuple] = {
     # per-rank step 5027 -> 4859 us with the round-3 five applied
     (1280, 8192, "qkv", "dense"): (8, 3, 0),     # 80 tiles x 256 k-steps: 240 blocks (heuristic 8 x 2: +33 us)
     (8192, 1024, "plain", "dense"): (2, 1, 1),   # o_proj
-    # gate_up / down_proj on stream-K, 4 waves, one block per CU (r4 probe: 23.5 vs 26.2 us and 12.8 vs
-    # 13.5 us per launch; round 3: 448 one-tile blocks at 4 waves, down (8, 1, 2))
-    (7168, 8192, "silu", "dense"): ("sk", 4, 1, 8),
+    (7168, 8192, "silu", "dense"): (4, 1, 0),    # gate_up: 448 one-tile blocks at 4 waves (heuristic 8: +118 us)
+    # down_proj on stream-K, 4 waves, one block per CU (r4 probe: 12.8 vs 13.5 us per launch; round 3: (8, 1, 2))
     (8192, 3584, "plain", "dense"): ("sk", 4, 1, 8),
     (16032, 8192, "plain", "dense"): (8, 1, 1),  # LM head shard
-    # Llama-3-8B, batch 8 (r4 probe): qkv 13.6 vs 15.1, gate_up 39.0 vs 41.3, down 21.1 vs 21.9 us
+    # Llama-3-8B, batch 8 (r4 probe, profiles/r4_streamk_probe.log): qkv on stream-K (13.6 vs 15.1 us per
+    # launch); gate_up and down_proj on 4-wave tile blocks (39.0 vs 41.3, 21.1 vs 21.9 us)
     (6144, 4096, "qkv", "dense"): ("sk", 8, 1, 4),
-    (28672, 4096, "silu", "dense"): ("sk", 4, 1, 8),
-    (4096, 14336, "plain", "dense"): ("sk", 4, 1, 8),
+    (28672, 4096, "silu", "dense"): (4, 1, 0),
+    (4096, 14336, "plain", "dense"): (4, 1, 1),
     # Qwen2.5-1.5B AWQ int4, batch 8, ctx 100 (profiles/r3_awq_decode_sweep.log, whole-step replays;
     # baseline 1287.8 us): qkv on awq_stream_kernel (packed scales, XP-packed activations, 4 waves x 3
     # k-quads) instead of the K-split awq_gemm_kernel, down_proj in 8 K slices of 4 waves

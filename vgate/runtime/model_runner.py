@@ -33,8 +33,10 @@ from vgate.utils.profiling import range_
 
 log = logging.getLogger("vgate.engine")
 
-DEFAULT_T_BUCKETS = [1, 2, 4, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256, 384, 512, 768, 1024, 1536, 2048,
-                     3072, 4096, 6144, 8192, 12288, 16384]
+# (320 / 448 / 640: a wave of 8 ~50-token prompts lands on 384-448 tokens; padded to 512 its prefill
+# GEMMs did 14-33 % more work, profiles/r4_prefill_ring_tiles.log)
+DEFAULT_T_BUCKETS = [1, 2, 4, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256, 320, 384, 448, 512, 640, 768, 1024, 1536,
+                     2048, 3072, 4096, 6144, 8192, 12288, 16384]
 DEFAULT_S_BUCKETS = [1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024]
 
 
