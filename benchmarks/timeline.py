@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--mixed", type=int, default=0, help="time a MIXED step: one prompt of this many tokens "
                     "beside the decode rows (benchmarks/mixed_step.py)")
     ap.add_argument("--wide-gate-up", action="store_true", help="medium buckets: the wide medium kernel for gate_up")
+    ap.add_argument("--prefill", action="store_true", help="time the PREFILL step of the batch (its prompts as one "
+                    "multi-prompt step) instead of a decode step")
     ap.add_argument("--replays", type=int, default=0,
                     help="after the measured step, replay its graph N times back to back (no host sync between) "
                          "and report the last replay too: a hole that only the first replay shows is the host's "
@@ -53,7 +55,7 @@ def main():
         eng.add_request(f"r{i}", prompt_ids=ids,
                         params=SamplingParams(temperature=0.7, top_p=0.9, max_tokens=400, ignore_eos=True))
     eng._drain_inbox()
-    for _ in range(4):  # prefill + a few decode steps (graphs of the decode bucket captured)
+    for _ in range(0 if a.prefill else 4):  # prefill + a few decode steps (graphs of the decode bucket captured)
         eng.step()
     if a.wide_gate_up:
         for L in eng.model.layers:
