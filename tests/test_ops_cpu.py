@@ -141,3 +141,25 @@ def test_plan_cache_round_trip(tmp_path):
     assert ops.load_plan_cache(path, "k1") == plans
     assert ops.load_plan_cache(path, "k2") == {(1, 2): {3: (4, 5)}}
     assert ops.load_plan_cache(path, "nope") is None
+
+
+def test_decode_plans_apply_tile_and_streamk_entries():
+    """decode_plans.apply sets tile-kernel plans on (waves, K slices, tiles) and stream-K plans on
+    ("sk", waves, blocks per CU, group) entries, by (N, K, layout, kind)."""
+    from types import SimpleNamespace
+    from vgate.models import decode_plans
+
+    def lin(N, K, layout="plain", kind="dense"):
+        return SimpleNamespace(N=N, K=K, layout=layout, kind=kind, dec_waves=0, dec_splitk=0, dec_ntb=0, dec_sk=None)
+    L = SimpleNamespace(qkv=lin(6144, 4096, "qkv"), o=lin(4096, 4096), gate_up=lin(28672, 4096, "silu"),
+                        down=lin(4096, 14336))
+    model = SimpleNamespace(layers=[L], lm_head=lin(128256, 4096))
+    n = decode_plans.apply(model)
+    assert n == 3
+    assert L.qkv.dec_sk == (8, 1, 4) and L.qkv.dec_waves == 0
+    assert (L.gate_up.dec_waves, L.gate_up.dec_splitk, L.gate_up.dec_ntb) == (4, 1, 0) and L.gate_up.dec_sk is None
+    assert (L.down.dec_waves, L.down.dec_splitk, L.down.dec_ntb) == (4, 1, 1)
+    assert L.o.dec_sk is None and L.o.dec_waves == 0
+    for key, val in decode_plans.PLANS.items():
+        assert len(key) == 4 and key[2] in ("qkv", "silu", "plain") and key[3] in ("dense", "awq")
+        assert (val[0] == "sk" and len(val) == 4) or (len(val) == 3 and all(isinstance(v, int) for v in val))
