@@ -661,15 +661,23 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
   };
   int kq = qbeg;
   const int ngrp = (qend - qbeg + U - 1) / U;
+  // epilogue operands of wave 0's (row, 4 columns) item at launch, as gemm_kernel does: the
+  // residual / bias words and the QKV position -> cos/sin chain leave with the weight stream
+  // instead of adding one or two dependent round trips after the reduction
+  EpiPre<NTB> pre;
+  const bool epi_thr = threadIdx.x < 64;
+  if (epi_thr) epi_pre_a<NTB, EPI>(p, pre, r16, nt0, 4 * (lane >> 4));
   if constexpr (!PP) {
     // ONE group covering the wave's whole k-range (host-checked: <= U k-quads): every load of
     // the wave in flight at once, one memory round trip per block
     uint4 wa[U][NTB], sa[U][NTB], xa[U][XL], gaa[U][GL];
     load_grp(wa, sa, xa, gaa, kq);
+    if (epi_thr) epi_pre_b<NTB, EPI>(p, pre, nt0, 4 * (lane >> 4));
     mma_grp(wa, sa, xa, gaa, kq);
   } else if (ngrp > 0) {
     uint4 wa[U][NTB], sa[U][NTB], xa[U][XL], gaa[U][GL], wb[U][NTB], sb[U][NTB], xb[U][XL], gab[U][GL];
     load_grp(wa, sa, xa, gaa, kq);
+    if (epi_thr) epi_pre_b<NTB, EPI>(p, pre, nt0, 4 * (lane >> 4));
     int g = 0;
     for (; g + 2 <= ngrp; g += 2) {
       load_grp(wb, sb, xb, gab, kq + U);
@@ -680,7 +688,10 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
     }
     if (g < ngrp) mma_grp(wa, sa, xa, gaa, kq);
   }
-  gemm_finish<1, NTB, EPI, NORM, false>(p, acc, ssr, smem, 0, nt0, EpiPre<NTB>{});
+  if constexpr (PP) {
+    if (ngrp <= 0 && epi_thr) epi_pre_b<NTB, EPI>(p, pre, nt0, 4 * (lane >> 4));
+  }
+  gemm_finish<1, NTB, EPI, NORM, true>(p, acc, ssr, smem, 0, nt0, pre);
 }
 
 // ---- prefill / medium-M tile GEMM (M > 16, bf16 weights) ----

@@ -99,6 +99,12 @@ __global__ __launch_bounds__(64 * W) void gemm_sk_kernel(GemmParams p, SkParams 
   int* stile = reinterpret_cast<int*>(body + W * 2 * 64 * 16 + W * 2 * 16 * 4);
   if (threadIdx.x == 0) *lcnt = 0;
   __syncthreads();
+  // epilogue operands of this wave's first body tile (tiles tb0 + w, tb0 + w + W, ...), loaded at
+  // launch beside the weight stream: residual / bias words, the QKV position -> cos/sin chain
+  const int tb0 = le / KP, tb1 = nbody > 0 ? (qb - 1) / KP : tb0 - 1;
+  const int tpre = tb0 + w;
+  EpiPre<1> pre;
+  if (tpre <= tb1) epi_pre_a<1, EPI>(p, pre, r16, tpre, 4 * g4);
 
   const __amdgpu_buffer_rsrc_t rW = rsrc_of(p.wp), rX = rsrc_of(p.x);
   const int mrow = XP > 1 ? r16 % R : r16;
@@ -198,6 +204,7 @@ __global__ __launch_bounds__(64 * W) void gemm_sk_kernel(GemmParams p, SkParams 
   uint4 w0[UA], w1[UA], x0[UP], x1[UP];
   load(w0, x0, 0);
   if constexpr (NGA > 1) load(w1, x1, 1);
+  if (tpre <= tb1) epi_pre_b<1, EPI>(p, pre, tpre, 4 * g4);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int g = 0; g < NGA; ++g) {
@@ -246,7 +253,6 @@ __global__ __launch_bounds__(64 * W) void gemm_sk_kernel(GemmParams p, SkParams 
 
   // the body tiles, wave w takes tiles w, w + W, ...: whole tiles -> epilogue; the last one, if it
   // continues in later blocks, first adds their published lead partials (block order)
-  const int tb0 = le / KP, tb1 = nbody > 0 ? (qb - 1) / KP : tb0 - 1;
   for (int t = tb0 + w; t <= tb1; t += W) {
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     float sq = 0.f;
@@ -287,7 +293,8 @@ __global__ __launch_bounds__(64 * W) void gemm_sk_kernel(GemmParams p, SkParams 
     }
     if constexpr (NORM) v *= rsqrtf(sq / (float)p.K + p.eps);
     f32x4 vv[1] = {v};
-    epilogue<1, EPI, false>(p, vv, r16, t, 4 * g4, EpiPre<1>{}, r16 < p.M);
+    if (t == tpre) epilogue<1, EPI, true>(p, vv, r16, t, 4 * g4, pre, r16 < p.M);
+    else epilogue<1, EPI, false>(p, vv, r16, t, 4 * g4, EpiPre<1>{}, r16 < p.M);
   }
 }
 
