@@ -22,6 +22,7 @@
 // RNG: Philox4x32-10 keyed by the per-row seed, counter (float4 index, offset, round),
 // so results are reproducible for a given (seed, offset) and independent of NSEG.
 // Merges read the segments' partials in a fixed order: bit-reproducible.
+#include <algorithm>
 #include <cstdlib>
 
 #include "launchers.h"
@@ -416,6 +417,9 @@ int sample_segments(int B, int V) {
   return nseg < 1 ? 1 : nseg;
 }
 
+int g_sample_resume_div = 1;  // resume-kernel blocks per row = nseg / div (A/B: set_sample_resume_div)
+void set_sample_resume_div(int d) { g_sample_resume_div = d < 1 ? 1 : d; }
+
 int g_sample_round_launches = 2;  // rejection rounds as their own launches before the in-launch fallback
 void set_sample_round_launches(int n) { g_sample_round_launches = n < -1 ? -1 : n; }  // -1: meetings only
 
@@ -435,8 +439,11 @@ void launch_sample(const SampleArgs& s, hipStream_t st) {
       a.tl = tl_take("sample_round", nseg * s.B);
       hipLaunchKernelGGL(sample_round_kernel<256>, dim3(nseg, s.B), dim3(256), 0, st, a, (uint32_t)r);
     }
-    a.tl = tl_take("sample_resume", nseg * s.B);
-    hipLaunchKernelGGL(sample_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, a,
+    // rows still pending continue with in-launch meetings on fewer blocks per row (a meeting's
+    // cost grows with its arrivals; the Philox counters follow the float4 index, not the split)
+    const int nres = std::max(1, nseg / std::max(1, g_sample_resume_div));
+    a.tl = tl_take("sample_resume", nres * s.B);
+    hipLaunchKernelGGL(sample_kernel, dim3(nres, s.B), dim3(SAMPLE_THREADS), 0, st, a,
                        (uint32_t)(g_sample_round_launches + 1));
     return;
   }

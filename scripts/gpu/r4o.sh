@@ -21,3 +21,25 @@ for m in qwen llama8b; do
   timeout -k 10 300 python -u benchmarks/sk_probe.py --model $m > gpurun_out/r4o_probe_$m.log 2>&1 || { tail -30 gpurun_out/r4o_probe_$m.log; exit 1; }
   grep '^{' gpurun_out/r4o_probe_$m.log
 done
+timeout -k 10 300 python -u benchmarks/timeline.py --prefill --batch 8 --ctx 50 > gpurun_out/r4o_tl_prefill.log 2>&1 || { tail -30 gpurun_out/r4o_tl_prefill.log; exit 1; }
+python - <<'PY'
+import json
+for l in open("gpurun_out/r4o_tl_prefill.log"):
+    if l.startswith('{"kv_blocks'):
+        d = json.loads(l)
+        print("prefill step", d["step_us"], d["launches"], d["sum_gap_us"])
+        for k, v in list(d["per_kernel"].items())[:8]:
+            print("  ", k, v["n"], v["avg_span_us"], v["avg_gap_after_us"])
+PY
+for dv in 1 4; do
+VGATE_SAMPLE_RESUME_DIV=$dv timeout -k 10 300 python -u benchmarks/timeline.py --batch 8 --ctx 100 > gpurun_out/r4o_tl_div$dv.log 2>&1 || { tail -30 gpurun_out/r4o_tl_div$dv.log; exit 1; }
+python - <<PY
+import json
+for l in open("gpurun_out/r4o_tl_div$dv.log"):
+    if l.startswith('{"kv_blocks'):
+        d = json.loads(l)
+        print("div $dv step", d["step_us"])
+        for k, v in d["per_kernel"].items():
+            if "sample" in k: print("  ", k, v["avg_span_us"], v["dur_med"], v["dur_max"])
+PY
+done
