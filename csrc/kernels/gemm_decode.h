@@ -138,8 +138,9 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
         for (int mb = 0; mb < MB; ++mb) acc[mb][j] = mfma16(as_bf16x8(b[u][j]), as_bf16x8(a[u][mb]), acc[mb][j]);
   };
   // epilogue operands of this thread's (row, 4 columns) item (decode: wave 0 runs the epilogue)
-  EpiPre<NTB> pre;
-  const bool epi_thr = MB == 1 && threadIdx.x < 64;
+  EpiPre<NTB> pre;  // (two tiles' words: blocks of 4 tiles load theirs in the epilogue)
+  constexpr bool PREF = MB == 1 && NTB <= 2;
+  const bool epi_thr = PREF && threadIdx.x < 64;
   if (epi_thr) epi_pre_a<NTB, EPI>(p, pre, m_base + r16, nt0, 4 * (lane >> 4));
   bool pre_b = false;
   // Whole groups of U k-steps, the last one possibly partial: no serial tail, so a wave
@@ -169,7 +170,7 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
     if (g < ngrp) mma_grp(b0, a0, gk(g));
   }
   if (epi_thr && !pre_b) epi_pre_b<NTB, EPI>(p, pre, nt0, 4 * (lane >> 4));
-  gemm_finish<MB, NTB, EPI, NORM, MB == 1>(p, acc, ssr, smem, m_base, nt0, pre);
+  gemm_finish<MB, NTB, EPI, NORM, PREF>(p, acc, ssr, smem, m_base, nt0, pre);
 }
 
 // ---- AWQ W4A16 ----
@@ -664,8 +665,10 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
   // epilogue operands of wave 0's (row, 4 columns) item at launch, as gemm_kernel does: the
   // residual / bias words and the QKV position -> cos/sin chain leave with the weight stream
   // instead of adding one or two dependent round trips after the reduction
+  // (EpiPre holds two tiles' words: blocks of 4 tiles load theirs in the epilogue)
+  constexpr bool PREF = NTB <= 2;
   EpiPre<NTB> pre;
-  const bool epi_thr = threadIdx.x < 64;
+  const bool epi_thr = PREF && threadIdx.x < 64;
   if (epi_thr) epi_pre_a<NTB, EPI>(p, pre, r16, nt0, 4 * (lane >> 4));
   if constexpr (!PP) {
     // ONE group covering the wave's whole k-range (host-checked: <= U k-quads): every load of
@@ -691,7 +694,7 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
   if constexpr (PP) {
     if (ngrp <= 0 && epi_thr) epi_pre_b<NTB, EPI>(p, pre, nt0, 4 * (lane >> 4));
   }
-  gemm_finish<1, NTB, EPI, NORM, true>(p, acc, ssr, smem, 0, nt0, pre);
+  gemm_finish<1, NTB, EPI, NORM, PREF>(p, acc, ssr, smem, 0, nt0, pre);
 }
 
 // ---- prefill / medium-M tile GEMM (M > 16, bf16 weights) ----
