@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256, 2) void gemm_prefill_kernel(GemmParams p) {
 #pragma unroll
         for (int a = 0; a < NT; ++a) {
           const int n = (nt_blk + wn * NT + a) * 16 + 4 * (lane >> 4);
-          *reinterpret_cast<f32x4*>(part + (size_t)m * p.N + n) = acc[a][b];
+          __builtin_nontemporal_store(acc[a][b], reinterpret_cast<f32x4*>(part + (size_t)m * p.N + n));
         }
       }
     }
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_prefill2_kernel(GemmPara
 #pragma unroll
         for (int a = 0; a < NT; ++a) {
           const int n = (nt_blk + wn * NT + a) * 16 + 4 * (lane >> 4);
-          *reinterpret_cast<f32x4*>(part + (size_t)m * p.N + n) = acc[a][b];
+          __builtin_nontemporal_store(acc[a][b], reinterpret_cast<f32x4*>(part + (size_t)m * p.N + n));
         }
       }
     }
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(512, 1) void gemm_prefill4_kernel(GemmParams p) {
 #pragma unroll
         for (int a = 0; a < NWN; ++a) {
           const int n = (nt_blk + wr * NWN + a) * 16 + 4 * (lane >> 4);
-          *reinterpret_cast<f32x4*>(part + (size_t)m * p.N + n) = acc[a][b];
+          __builtin_nontemporal_store(acc[a][b], reinterpret_cast<f32x4*>(part + (size_t)m * p.N + n));
         }
       }
     }
@@ -669,6 +669,8 @@ static void launch_prefill_cfg(const GemmParams& p, int nz, hipStream_t st) {
   }
 }
 
+// Split-K partials leave with non-temporal stores: dirty fp32 slabs in L2 are written back at the
+// kernel boundary and held the next launch back 2-4 us (prefill-step timeline, r4).
 // Tile shape: 128 x 128 when that grid covers the chip, else 128 x 64 (narrow N: o_proj,
 // down, 70B/TP shards). A grid still under ~200 blocks is split along K (>= 4 stages of 64 per
 // slice, <= 8 slices, partials within the workspace) and combined by prefill_reduce_kernel.
