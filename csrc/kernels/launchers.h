@@ -212,7 +212,6 @@ void launch_sample(const SampleArgs& s, hipStream_t st);
 int sample_segments(int B, int V);
 void set_sample_nseg(int n);  // cap on segments per row (0 = B*NSEG <= 1024 bound only)
 void set_sample_round_launches(int n);  // rejection rounds run as launches (0 = pass 0 only)
-void set_sample_resume_div(int d);      // resume-kernel blocks per row = segments / d
 
 // Custom one-shot all-reduce over IPC-mapped peer buffers (xGMI).
 struct AllReduceArgs {

@@ -417,9 +417,6 @@ int sample_segments(int B, int V) {
   return nseg < 1 ? 1 : nseg;
 }
 
-int g_sample_resume_div = 1;  // resume-kernel blocks per row = nseg / div (A/B: set_sample_resume_div)
-void set_sample_resume_div(int d) { g_sample_resume_div = d < 1 ? 1 : d; }
-
 int g_sample_round_launches = 2;  // rejection rounds as their own launches before the in-launch fallback
 void set_sample_round_launches(int n) { g_sample_round_launches = n < -1 ? -1 : n; }  // -1: meetings only
 
@@ -439,11 +436,8 @@ void launch_sample(const SampleArgs& s, hipStream_t st) {
       a.tl = tl_take("sample_round", nseg * s.B);
       hipLaunchKernelGGL(sample_round_kernel<256>, dim3(nseg, s.B), dim3(256), 0, st, a, (uint32_t)r);
     }
-    // rows still pending continue with in-launch meetings on fewer blocks per row (a meeting's
-    // cost grows with its arrivals; the Philox counters follow the float4 index, not the split)
-    const int nres = std::max(1, nseg / std::max(1, g_sample_resume_div));
-    a.tl = tl_take("sample_resume", nres * s.B);
-    hipLaunchKernelGGL(sample_kernel, dim3(nres, s.B), dim3(SAMPLE_THREADS), 0, st, a,
+    a.tl = tl_take("sample_resume", nseg * s.B);
+    hipLaunchKernelGGL(sample_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, a,
                        (uint32_t)(g_sample_round_launches + 1));
     return;
   }

@@ -589,7 +589,6 @@ PYBIND11_MODULE(_C, m) {
         py::arg("offsets"), py::arg("out"), py::arg("out_logprob") = py::none(), py::arg("ws") = py::none());
   m.def("sample_segments", &vgate::sample_segments, "blocks per row the sampler uses for (B, V)");
   m.def("set_sample_nseg", &vgate::set_sample_nseg, "cap the sampler's segments per row (experiments)");
-  m.def("set_sample_resume_div", &vgate::set_sample_resume_div, "resume-kernel blocks per row = segments / d (A/B)");
   m.def("set_sample_round_launches", &vgate::set_sample_round_launches,
         "rejection rounds the sampler runs as their own launches before the in-launch fallback (experiments)");
   m.def("kernel_copy", &kernel_copy, "pinned host <-> device copy by a kernel on the current stream (no SDMA)",

@@ -54,8 +54,6 @@ def _configure(mod) -> None:
     # (profiles/r2_sampler_round_launches.log)
     if hasattr(mod, "set_sample_round_launches"):
         mod.set_sample_round_launches(int(os.environ.get("VGATE_SAMPLE_ROUND_LAUNCHES", "1")))
-    if hasattr(mod, "set_sample_resume_div"):
-        mod.set_sample_resume_div(int(os.environ.get("VGATE_SAMPLE_RESUME_DIV", "1")))
 
 
 def native_available() -> bool:
@@ -738,11 +736,9 @@ def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = 0.05
             x = torch.rand(M, lin.K, device=dev, generator=g).bfloat16()
             out = torch.empty(M, lin.N, dtype=torch.bfloat16, device=dev)
             times = {}
-            # cold weights (Infinity Cache flushed before each launch) up to 1024 rows: in a step every
-            # layer's weights arrive from HBM, and back-to-back timing kept 55 MB of gate_up resident and
-            # picked the 256 x 256 tile at M = 448 that ran 57 us in the graph
-            # (profiles/r4_prefill_step_timeline.log)
-            cold = _cold_timer(dev) if M <= 1024 else None
+            # (cold-weight timing for M >= 128 too was measured: it picked slower down_proj plans at
+            # M = 448 and the same gate_up tile, profiles/r4_prefill_step_timeline.log)
+            cold = _cold_timer(dev) if M < 128 else None
             extra = MID_CANDIDATES if 16 < M <= 64 else PREFILL_RING_CANDIDATES if 64 < M <= 1024 else []
             for bn, sk in PREFILL_CANDIDATES + extra:
                 def run():
