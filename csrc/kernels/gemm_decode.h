@@ -557,7 +557,9 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
 #pragma unroll
   for (int j = 0; j < NTB; ++j) acc[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // NORM 3: the producer's sums of squares of row r16 (wave 0 of slice 0 carries them into gemm_finish)
-  float ssr[1] = {(NORM == 3 && wid == 0 && sp.slice == 0) ? prenorm_ss(p, r16, lane >> 4) : 0.f};
+  // (NORM 3: the producer's sums of squares are read after the stream, by wave 0 of slice 0, so
+  // their loads never hold back the first weight group)
+  float ssr[1] = {0.f};
   constexpr int XL = 4 / XP;  // activation loads per k-quad
   const uint32_t lom = r16 < R ? ~0u : 0u;
   constexpr int GL = NORM == 1 ? XL : 1;
@@ -693,6 +695,9 @@ __global__ __launch_bounds__(512) void awq_stream_kernel(GemmParams p) {
   }
   if constexpr (PP) {
     if (ngrp <= 0 && epi_thr) epi_pre_b<NTB, EPI>(p, pre, nt0, 4 * (lane >> 4));
+  }
+  if constexpr (NORM == 3) {
+    if (wid == 0 && sp.slice == 0) ssr[0] = prenorm_ss(p, r16, lane >> 4);
   }
   gemm_finish<1, NTB, EPI, NORM, PREF>(p, acc, ssr, smem, 0, nt0, pre);
 }

@@ -181,13 +181,15 @@ __device__ __forceinline__ float prenorm_ss(const GemmParams& p, int m, int quar
   if (m >= p.M) return 0.f;
   const float* s = p.ssp_in + (size_t)m * p.ssn;
   const int q0 = (p.ssn * quarter) >> 2, q1 = (p.ssn * (quarter + 1)) >> 2;
+  // every load of a 32-value chunk in flight together: one round trip per chunk (24 values per lane
+  // at K = 1536; 8-value steps cost three dependent round trips there)
   float acc = 0.f;
-  for (int t0 = q0; t0 < q1; t0 += 8) {
-    float r[8];
+  for (int t0 = q0; t0 < q1; t0 += 32) {
+    float r[32];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) r[u] = s[min(t0 + u, q1 - 1)];
+    for (int u = 0; u < 32; ++u) r[u] = s[min(t0 + u, q1 - 1)];
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+    for (int u = 0; u < 32; ++u)
       if (t0 + u < q1) acc += r[u];
   }
   return acc;
