@@ -17,3 +17,19 @@ for l in open("gpurun_out/r4q_tl_rl$rl.log"):
             if "sample" in k: print("  ", k, v["n"], v["avg_span_us"], v["dur_med"], v["dur_max"])
 PY
 done
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "awq" -x -q --timeout 120 --timeout-method thread > gpurun_out/r4q_awq_tests.log 2>&1 || { echo AWQ_TEST_FAIL; tail -40 gpurun_out/r4q_awq_tests.log; exit 1; }
+tail -1 gpurun_out/r4q_awq_tests.log
+timeout -k 10 300 python -u benchmarks/timeline.py --batch 8 --ctx 100 --quantization awq > gpurun_out/r4q_tl_awq.log 2>&1 || { tail -30 gpurun_out/r4q_tl_awq.log; exit 1; }
+python - <<'PY'
+import json
+for l in open("gpurun_out/r4q_tl_awq.log"):
+    if l.startswith('{"kv_blocks'):
+        d = json.loads(l)
+        print("awq step", d["step_us"])
+        for k, v in list(d["per_kernel"].items())[:5]:
+            print("  ", k, v["n"], v["avg_span_us"], v["dur_med"], v["dur_max"])
+PY
+timeout -k 10 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 --quantization awq > gpurun_out/r4q_awq_bench.log 2>&1 || { tail -30 gpurun_out/r4q_awq_bench.log; exit 1; }
+tail -1 gpurun_out/r4q_awq_bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('awq (no security)', {k: d.get(k) for k in ('value','p50_s','p99_s','engine_avg_gpu_ms','dtype')})"
+timeout -k 10 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r4q_bf16_bench.log 2>&1 || { tail -30 gpurun_out/r4q_bf16_bench.log; exit 1; }
+tail -1 gpurun_out/r4q_bf16_bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('bf16 same box', {k: d.get(k) for k in ('value','p50_s','p99_s','engine_avg_gpu_ms')})"
