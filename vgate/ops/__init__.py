@@ -53,7 +53,10 @@ def _configure(mod) -> None:
     # 93.1 / 93.2 req/s at 1 vs 92.3 / 93.0 at 2 and 92.4 at 3, sampler_probe 31.1 vs 32.5 us
     # (profiles/r2_sampler_round_launches.log)
     if hasattr(mod, "set_sample_round_launches"):
-        mod.set_sample_round_launches(int(os.environ.get("VGATE_SAMPLE_ROUND_LAUNCHES", "1")))
+        # 0: pass 0, then every rejection round in the resume kernel's in-launch meetings — two sampler
+        # launches; the step time is the same as with one round launch (1266.1 vs 1269.9-1271.2 us,
+        # profiles/r4_sampler_round_launches.log)
+        mod.set_sample_round_launches(int(os.environ.get("VGATE_SAMPLE_ROUND_LAUNCHES", "0")))
 
 
 def native_available() -> bool:
