@@ -120,6 +120,7 @@ static GemmParams to_params(const GemmArgs& g) {
   p.bias = g.bias; p.res = g.res; p.ldr = g.ldr;
   p.out = g.out; p.ldo = g.ldo;
   p.slabs = g.slabs; p.counters = g.counters;
+  p.gran = nullptr; p.fault = g.fault;  // (granule split-K: set by the decode launchers when it fits)
   p.positions = g.positions; p.slots = g.slots; p.cos_sin = g.cos_sin;
   p.k_cache = g.k_cache; p.v_cache = g.v_cache; p.hq = g.hq; p.hkv = g.hkv; p.bs = g.bs;
   p.scales = g.scales; p.zeros = g.zeros; p.group = g.group; p.szp = g.awq_szp;

@@ -19,6 +19,10 @@ struct GemmParams {
   const bf16_t* bias; const bf16_t* res; int ldr;
   void* out; int ldo;
   int splitk; float* slabs; uint32_t* counters;
+  // decode split-K (MB = 1) by data-carrying granules instead of slabs + ticket: slices below the last
+  // publish {value, tag} pairs, the last slice's block (dispatched after every other slice: z-major
+  // order) collects, adds in slice order and clears; zeroed once (ops.sk_workspace), or null
+  uint4* gran; uint32_t* fault;
   const int32_t* positions; const int32_t* slots; const float* cos_sin;
   bf16_t* k_cache; bf16_t* v_cache; int hq; int hkv; int bs;
   const bf16_t* scales; const bf16_t* zeros; int group;
@@ -352,6 +356,89 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
   }
   const SplitPos sp = split_pos(p);
   const int tile = sp.tile;
+  if constexpr (MB == 1) {
+    if (sp.nsl > 1 && p.gran != nullptr) {
+      // wave 0, lane l: the block's partial of (row l & 15, 4 columns) per tile + the slice's row sum
+      // of squares. Granule slot (tile, z < nsl - 1): [NTB][64][2] uint4 values + [64] uint4 sums.
+      if (threadIdx.x >= 64) return;
+      const int l = threadIdx.x;
+      f32x4 v[NTB];
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) {
+        if (nw > 1) {
+          f32x4 t = {0.f, 0.f, 0.f, 0.f};
+          for (int w = 0; w < nw; ++w) t += red4[w * SLOTS + j * 64 + l];
+          v[j] = t;
+        } else {
+          v[j] = acc[0][j];
+        }
+      }
+      float ss = 0.f;
+      if constexpr (NORM) {
+        for (int w = 0; w < nw; ++w) ss += ssqw[w * 16 + (l & 15)];
+      }
+      constexpr int GW = (2 * NTB + 1) * 64;  // uint4 per slot
+      constexpr uint32_t TAG = 1u;
+      const size_t slot0 = (size_t)tile * (p.splitk - 1);
+      if (sp.slice < sp.nsl - 1) {
+        const uint32_t off = (uint32_t)(((slot0 + sp.slice) * GW) * 16);
+#pragma unroll
+        for (int j = 0; j < NTB; ++j) {
+          st_sc1_x4(reinterpret_cast<float*>(p.gran), off + (uint32_t)((j * 64 + l) * 2) * 16u,
+                    __builtin_bit_cast(f32x4, make_uint4(__float_as_uint(v[j][0]), TAG, __float_as_uint(v[j][1]), TAG)));
+          st_sc1_x4(reinterpret_cast<float*>(p.gran), off + (uint32_t)((j * 64 + l) * 2 + 1) * 16u,
+                    __builtin_bit_cast(f32x4, make_uint4(__float_as_uint(v[j][2]), TAG, __float_as_uint(v[j][3]), TAG)));
+        }
+        st_sc1_x4(reinterpret_cast<float*>(p.gran), off + (uint32_t)(NTB * 128 + l) * 16u,
+                  __builtin_bit_cast(f32x4, make_uint4(__float_as_uint(ss), TAG, 0u, 0u)));
+        return;
+      }
+      // the last slice: every other slice's granules, in slice order (bit-reproducible)
+      for (int z = 0; z < sp.nsl - 1; ++z) {
+        const uint32_t off = (uint32_t)(((slot0 + z) * GW) * 16);
+        uint4 g[NTB][2], gs;
+        int spins = 0;
+        while (true) {
+          bool ok = true;
+#pragma unroll
+          for (int j = 0; j < NTB; ++j)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              g[j][h] = __builtin_bit_cast(uint4, ld_sc1_x4(reinterpret_cast<const float*>(p.gran),
+                                                             off + (uint32_t)((j * 64 + l) * 2 + h) * 16u));
+              ok = ok && g[j][h].y == TAG && g[j][h].w == TAG;
+            }
+          gs = __builtin_bit_cast(uint4, ld_sc1_x4(reinterpret_cast<const float*>(p.gran), off + (uint32_t)(NTB * 128 + l) * 16u));
+          ok = ok && gs.y == TAG;
+          if (__all(ok)) break;
+          if (++spins > (1 << 20)) {  // bounded: the step fails loudly (fault word), never hangs
+            if (l == 0 && p.fault != nullptr) atomicOr(p.fault, 8u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int j = 0; j < NTB; ++j)
+          v[j] += f32x4{__uint_as_float(g[j][0].x), __uint_as_float(g[j][0].z), __uint_as_float(g[j][1].x),
+                        __uint_as_float(g[j][1].z)};
+        ss += __uint_as_float(gs.x);
+        const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < NTB; ++j) {
+          st_sc1_x4(reinterpret_cast<float*>(p.gran), off + (uint32_t)((j * 64 + l) * 2) * 16u, zero);
+          st_sc1_x4(reinterpret_cast<float*>(p.gran), off + (uint32_t)((j * 64 + l) * 2 + 1) * 16u, zero);
+        }
+        st_sc1_x4(reinterpret_cast<float*>(p.gran), off + (uint32_t)(NTB * 128 + l) * 16u, zero);
+      }
+      if constexpr (NORM) {  // (ssqw rows are already folded over the row's four lanes)
+        const float sc = rsqrtf(ss / (float)p.K + p.eps);
+#pragma unroll
+        for (int j = 0; j < NTB; ++j) v[j] *= sc;
+      }
+      epilogue<NTB, EPI, PRE>(p, v, m_base + (l & 15), nt0, 4 * (l >> 4), pre, m_base + (l & 15) < p.M);
+      return;
+    }
+  }
   if (sp.nsl > 1) {
     // 1) this slice's partial tile -> fp32 slab [tile][slice][SLOTS]; under NORM also the
     //    slice's per-row partial sum of squares -> [tile][slice][16*MB] after all slabs

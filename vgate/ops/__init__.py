@@ -362,7 +362,7 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
         pk = _plan_kw(lin.prefill_plan.get(_plan_bucket(lin.prefill_plan, M)), M)
         ntb, splitk, path, waves = pk.get("ntb", 0), pk.get("splitk", 0), pk.get("path", 0), pk.get("waves", 0)
     kw = dict(bias=lin.bias, res=residual, ws=workspace(x.device), waves=waves, splitk=splitk, ntb=ntb, path=path)
-    if sk:
+    if M <= 16:  # stream-K slots / the decode split-K granules (zeroed, self-clearing) and the fault word
         kw.update(sk_ws=sk_workspace(x.device), fault=fault_word(x.device))
     if norm is not None:
         if lin.norm_gamma is not None:  # gamma lives in the weights: row scale only
