@@ -910,7 +910,7 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
   // decode, two slices: combined through granules (gemm_finish; down_proj 8.43 -> 8.22 us span). More
   // slices keep the slab + ticket combine, which issues every slice's loads at once (the granule
   // owner polls the slices one after another: int4 down_proj at 8 slices 8.6 -> 9.7 us)
-  if constexpr (MB == 1) {
+  if constexpr (MB == 1 && NTB == 1) {
     const size_t need_g = (size_t)nblk * (2 * NTB + 1) * 64 * 16;
     if (pl.splitk == 2 && g.sk_pub != nullptr && need_g <= g.sk_bytes) p.gran = reinterpret_cast<uint4*>(g.sk_pub);
   }
@@ -1054,7 +1054,7 @@ static bool launch_awq_stream(GemmParams p, const GemmArgs& g, hipStream_t st) {
   const size_t need_slab = (size_t)nblk * sk * (ntb * 64 * 16 + (NORM ? 16 * 4 : 0));
   if (sk > 1 && (g.slabs == nullptr || need_slab > g.slab_bytes || nblk > g.max_counters)) return false;
   p.splitk = sk;
-  if (sk == 2 && g.sk_pub != nullptr && (size_t)nblk * (2 * ntb + 1) * 64 * 16 <= g.sk_bytes)
+  if (sk == 2 && ntb == 1 && g.sk_pub != nullptr && (size_t)nblk * (2 * ntb + 1) * 64 * 16 <= g.sk_bytes)
     p.gran = reinterpret_cast<uint4*>(g.sk_pub);
   const size_t lds = (size_t)w * ntb * 64 * 16 * (w > 1) + ssq_bytes<1>(w) + 16;
   if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_stream", nblk * sk);

@@ -356,7 +356,8 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
   }
   const SplitPos sp = split_pos(p);
   const int tile = sp.tile;
-  if constexpr (MB == 1) {
+  if constexpr (MB == 1 && NTB == 1) {  // (one-tile decode blocks: the path's registers would cost the
+                                         // multi-tile LM-head blocks their occupancy)
     if (sp.nsl > 1 && p.gran != nullptr) {
       // wave 0, lane l: the block's partial of (row l & 15, 4 columns) per tile + the slice's row sum
       // of squares. Granule slot (tile, z < nsl - 1): [NTB][64][2] uint4 values + [64] uint4 sums.
