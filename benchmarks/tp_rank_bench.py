@@ -83,6 +83,9 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--sweep", action="store_true", help="in-context decode decomposition table per projection")
     ap.add_argument("--kinds", default="qkv,o,gate_up,down,lm_head")
+    ap.add_argument("--fused-ar", action="store_true",
+                    help="o_proj / down_proj all-reduce in their epilogue against a one-rank loopback region "
+                         "(prices the fused exchange's in-kernel cost; no peers)")
     a = ap.parse_args()
     if a.sweep:  # the sweep's (0, 0, 0) row is the launcher heuristic, not the measured table
         import os
@@ -91,6 +94,10 @@ def main():
     from timeline import measure
 
     tp = TPGroup(rank=a.rank, size=a.tp, simulated=True)
+    if a.fused_ar:
+        from vgate.parallel.custom_allreduce import LoopbackFused
+
+        tp.custom_ar = LoopbackFused(torch.device("cuda:0"))
     eng = LLMEngine(EngineConfig(model=a.model, device="cuda:0", max_model_len=2048, max_num_seqs=64,
                                  max_num_batched_tokens=2048, num_kv_blocks=1024, warmup=False,
                                  tensor_parallel_size=a.tp, prefill_autotune=False), tp=tp)
@@ -112,7 +119,9 @@ def main():
         eng.step()
     base = time_step(eng, a.iters)
     print(json.dumps({"per_rank_step_us": round(base, 1), "batch": a.batch, "ctx": a.ctx,
-                      "note": "compute only; collectives stubbed"}), flush=True)
+                      "note": ("o / down all-reduce fused in the epilogue against a loopback region (no peers); "
+                               "embedding all-reduce and logits all-gather stubbed") if a.fused_ar
+                      else "compute only; collectives stubbed"}), flush=True)
     summary, live, _, _ = measure(eng)
     kinds = layer_kinds(live)
     agg = {}

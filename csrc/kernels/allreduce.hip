@@ -287,6 +287,7 @@ __global__ __launch_bounds__(AR_THREADS) void ar_all_gather_kernel(const uint4* 
 }
 
 int64_t ar_error_offset() { return (int64_t)offsetof(ArSignal, error); }
+uint32_t ar_spin() { return ar_spin_limit(); }
 int64_t ar_blocks_used() { return ar_blocks(); }
 static_assert(offsetof(ArSignal, ticks) == offsetof(ArSignal, error) + 4 && offsetof(ArSignal, calls) == offsetof(ArSignal, error) + 8,
               "ids_to_host copies {error, ticks, calls} as consecutive words");

@@ -126,11 +126,22 @@ static GemmParams to_params(const GemmArgs& g) {
   p.scales = g.scales; p.zeros = g.zeros; p.group = g.group; p.szp = g.awq_szp;
   p.dbg_ts = g.dbg_ts;
   p.hg = g.hg; p.hg_gamma = g.hg_gamma; p.ssp_out = g.ssp_out; p.ssp_in = g.ssp_in; p.ssn = g.ssn;
+  p.ar = ArFused{};
+  if (g.ar_world > 0) {
+    for (int r = 0; r < 8; ++r) p.ar.base[r] = g.ar_fused[r];
+    p.ar.err = g.ar_err; p.ar.rank = g.ar_rank; p.ar.world = g.ar_world; p.ar.spin = ar_spin();
+  }
   return p;
 }
 
 void launch_gemm(const GemmArgs& g, hipStream_t st) {
   if (g.M <= 0) return;
+  // TP row-parallel decode GEMM with the all-reduce in the epilogue: the tile-per-block decode kernels
+  // (one wave finishes a whole 16-row tile: epilogue_ar's lane layout); the binding checked the shape
+  if (g.ar_world > 0) {
+    launch_dispatch<false>(to_params(g), g, st);
+    return;
+  }
   // long steps (prefill chunks): the LDS-tiled MFMA kernel (gemm_prefill.hip) on the same packed
   // weights; it declines shapes / modes it does not take
   // mixed prefill + decode steps (16 < M <= 64): the medium-M kernel when the start-up tuner
@@ -148,6 +159,12 @@ void launch_gemm(const GemmArgs& g, hipStream_t st) {
 
 void launch_awq_gemm(const GemmArgs& g, hipStream_t st) {
   if (g.M <= 0) return;
+  if (g.ar_world > 0) {  // fused all-reduce: the K-split int4 kernel (gemm_finish -> epilogue_ar)
+    GemmArgs h = g;
+    h.ntb = -2;
+    launch_dispatch<true>(to_params(h), h, st);
+    return;
+  }
   // decode on the wide int4 kernel (one block per CU owning whole tiles): g.ntb == -8 (a decode plan)
   if (g.ntb == -8 && launch_awq_wide(g, st)) return;
   // mixed prefill + decode steps (16 < M <= 64) on the int4 medium kernel (path 2)

@@ -12,6 +12,14 @@ namespace vgate {
 enum GemmEpi : int { EPI_BF16 = 0, EPI_F32 = 1, EPI_SILU = 2, EPI_QKV = 3 };
 constexpr int SK_MAX = 8;  // split-K slices per tile (the combine issues all slices' loads at once)
 
+// TP row-parallel decode GEMM: the all-reduce runs in the epilogue (epilogue_ar) when world >= 1
+struct ArFused {
+  char* base[8];   // every rank's fused region (launchers.h AR_FUSED_*), own one included
+  uint32_t* err;   // own sticky all-reduce error word (allreduce.hip ArSignal::error)
+  int rank, world;
+  uint32_t spin;   // polls before a wait gives up
+};
+
 struct GemmParams {
   const bf16_t* x; int lda; int M; const int32_t* row_idx;
   const uint4* wp; int N; int K;
@@ -33,6 +41,7 @@ struct GemmParams {
   // applied), row scale rsqrt(sum of ssp_in[m][0..ssn) / K + eps) — no gamma loads, no x^2 pass.
   bf16_t* hg; const bf16_t* hg_gamma; float* ssp_out; const float* ssp_in; int ssn;
   unsigned long long* dbg_ts;  // per-block [start, end] realtime stamps (profiling), or null
+  ArFused ar;                  // world 0: no fused all-reduce
 };
 
 // (column-tile block, K slice, slices) of this block: the grid decomposition of gemm_finish's hand-off
@@ -199,6 +208,103 @@ __device__ __forceinline__ float prenorm_ss(const GemmParams& p, int m, int quar
   return acc;
 }
 
+// ---- TP row-parallel decode GEMM (o_proj / down_proj): the all-reduce inside the epilogue ----
+// Under tensor parallelism every rank's GEMM yields a partial sum of the output. Instead of storing
+// it and launching the custom all-reduce (allreduce.hip: copy-in, signal, reduce, a launch and a
+// copy per collective), the wave that finishes output tile t (M <= 16 rows x 16 columns, lane ->
+// (row m, 4 columns)) publishes its fp32 partial into its own IPC-shared buffer, raises tile t's
+// arrival word at every peer, waits for every peer's arrival on tile t, sums the peers' partials
+// in rank order (bit-identical on every rank, so the replicated residual stream stays identical)
+// and stores bf16(sum) + residual. Per-tile epochs (the owner's own arrival word in its own
+// region: only it writes that slot), parity buffers by epoch, bounded waits on the all-reduce's
+// sticky error word: the one-shot kernel's safety argument, per tile (a peer re-uses a parity
+// buffer of tile t only after my next arrival on t, which follows my reads). Every lane of the
+// wave calls in (wave-wide poll). Decode launchers only (gemm.hip routes ar_world >= 1 there).
+template <int NTB, bool have>
+__device__ __forceinline__ void epilogue_ar(const GemmParams& p, const f32x4 (&v)[NTB], int m, int nt0, int nsub,
+                                            const EpiPre<NTB> e, bool valid) {
+  const ArFused& a = p.ar;
+  const int lane = threadIdx.x & 63;
+  const int piece = (m & 15) | ((nsub >> 2) << 4);  // this lane's 16-B piece of a tile slot
+  char* const mine = a.base[a.rank];
+  uint32_t* const my_flags = reinterpret_cast<uint32_t*>(mine);
+  uint32_t ep[NTB];
+  f32x4 o[NTB];
+#pragma unroll
+  for (int j = 0; j < NTB; ++j) {
+    const int t = nt0 + j;
+    ep[j] = __hip_atomic_load(&my_flags[t * 8 + a.rank], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
+    o[j] = v[j];
+    if (p.bias) {
+      uint2 b;
+      if constexpr (have) b = j == 0 ? e.b0 : e.b1;
+      else b = *reinterpret_cast<const uint2*>(p.bias + t * 16 + nsub);
+      o[j][0] += bf_lo(b.x); o[j][1] += bf_hi(b.x);
+      o[j][2] += bf_lo(b.y); o[j][3] += bf_hi(b.y);
+    }
+    *reinterpret_cast<f32x4*>(mine + AR_FUSED_FLAG_BYTES + (int64_t)(ep[j] & 1) * AR_FUSED_DATA +
+                              ((int64_t)t * 64 + piece) * 16) = o[j];
+  }
+  __threadfence_system();
+  if (lane < a.world) {  // arrive at every peer (own region included: that word is my epoch)
+    uint32_t* pf = reinterpret_cast<uint32_t*>(a.base[lane]);
+#pragma unroll
+    for (int j = 0; j < NTB; ++j)
+      __hip_atomic_store(&pf[(nt0 + j) * 8 + a.rank], ep[j], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
+    uint32_t spins = 0;
+    while (true) {
+      bool ok = true;
+      if (lane < a.world) {
+#pragma unroll
+        for (int j = 0; j < NTB; ++j)
+          ok = ok && (int32_t)(__hip_atomic_load(&my_flags[(nt0 + j) * 8 + lane], __ATOMIC_ACQUIRE,
+                                                 __HIP_MEMORY_SCOPE_SYSTEM) - ep[j]) >= 0;
+      }
+      if (__all(ok)) break;
+      if (++spins > a.spin) {  // a peer never arrived: sticky error, the host fails the step
+        if (lane == 0) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NTB; ++j) {
+    const int t = nt0 + j;
+    const int64_t off = AR_FUSED_FLAG_BYTES + (int64_t)(ep[j] & 1) * AR_FUSED_DATA + ((int64_t)t * 64 + piece) * 16;
+    // every peer's piece in flight before the first is summed; slots past world re-read rank 0
+    f32x4 r[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int src = q < a.world ? q : 0;
+      r[q] = src == a.rank ? o[j]
+                           : __builtin_bit_cast(f32x4, ld_nt16(reinterpret_cast<const uint4*>(a.base[src] + off)));
+    }
+    f32x4 s = r[0];
+#pragma unroll
+    for (int q = 1; q < 8; ++q)
+      if (q < a.world) s += r[q];
+    if (!valid) continue;
+    const int n = t * 16 + nsub;
+    float y[4] = {s[0], s[1], s[2], s[3]};
+    if (p.res) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) y[i] = bf2f(f2bf(y[i]));  // torch: all_reduce(x@W).bf16() + res
+      uint2 rr;
+      if constexpr (have) rr = j == 0 ? e.r0 : e.r1;
+      else rr = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldr + n);
+      y[0] += bf_lo(rr.x); y[1] += bf_hi(rr.x);
+      y[2] += bf_lo(rr.y); y[3] += bf_hi(rr.y);
+    }
+    uint2 pk;
+    pk.x = pack_bf2(y[0], y[1]);
+    pk.y = pack_bf2(y[2], y[3]);
+    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + n) = pk;
+  }
+}
+
 // ---- epilogue for one (row m, 4 columns) group; v[j] are the NTB reduced tiles ----
 // `e` = operands prefetched at launch (decode kernel) when `have`, else loaded here.
 // `have` is a compile-time choice: a runtime select between a prefetched register value
@@ -209,6 +315,10 @@ template <int NTB, int EPI, bool have>
 __device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[NTB], int m, int nt0, int nsub,
                                          const EpiPre<NTB> e, bool valid) {
   if constexpr (EPI == EPI_BF16) {
+    if (p.ar.world > 0) {  // every lane calls in: wave-wide arrival poll
+      epilogue_ar<NTB, have>(p, v, m, nt0, nsub, e, valid);
+      return;
+    }
     if (p.hg != nullptr) {  // every lane calls in: the tile's sum of squares is a cross-lane fold
       epilogue_norm_out<NTB, have>(p, v, m, nt0, nsub, e, valid);
       return;

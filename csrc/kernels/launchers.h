@@ -62,6 +62,12 @@ struct GemmArgs {
   void* sk_pub = nullptr;
   size_t sk_bytes = 0;
   uint32_t* fault = nullptr;
+  // TP row-parallel decode GEMM with the all-reduce in its epilogue (ar_world >= 1; gemm_epilogue.h
+  // epilogue_ar): every rank's fused region (IPC-mapped, AR_FUSED_BYTES) and the own sticky error word
+  char* ar_fused[8] = {};
+  uint32_t* ar_err = nullptr;
+  int ar_rank = 0;
+  int ar_world = 0;
 };
 void launch_gemm(const GemmArgs& g, hipStream_t st);
 // stream-K decode GEMM (gemm_streamk.hip): M <= 16 dense rows, one equal share of the packed weight
@@ -87,6 +93,14 @@ void launch_awq_dequant(const void* wq, const uint16_t* scales, const uint16_t* 
 // bases[p]: rank p's IPC-mapped allocation = [AR_SIGNAL_BYTES signal area][2 x max_bytes data];
 // bf16 in/out (may alias), nbytes % 16 == 0, nbytes <= max_bytes
 constexpr int64_t AR_SIGNAL_BYTES = 65536;
+// fused row-parallel GEMM + all-reduce (gemm_epilogue.h epilogue_ar): a region after the two data
+// buffers = arrival words [AR_FUSED_TILES][8] u32, then two parity buffers of one fp32 16 x 16 tile
+// (1 KiB) per 16-column output tile
+constexpr int AR_FUSED_TILES = 1024;
+constexpr int64_t AR_FUSED_FLAG_BYTES = (int64_t)AR_FUSED_TILES * 8 * 4;
+constexpr int64_t AR_FUSED_DATA = (int64_t)AR_FUSED_TILES * 1024;
+constexpr int64_t AR_FUSED_BYTES = AR_FUSED_FLAG_BYTES + 2 * AR_FUSED_DATA;
+uint32_t ar_spin();  // the wait bound of every all-reduce kind (VGATE_AR_SPIN_LIMIT)
 void launch_custom_allreduce(const void* in, void* out, int64_t nbytes, char* const* bases, int rank, int world,
                              int64_t max_bytes, hipStream_t st, int two_shot = 0);
 // all-gather over the same buffers: out = [rank 0's in | rank 1's in | ...] (nbytes each)

@@ -58,7 +58,8 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
           const c10::optional<Tensor>& awq_szp, const c10::optional<Tensor>& hg_out,
           const c10::optional<Tensor>& hg_gamma, const c10::optional<Tensor>& ssp_out,
           const c10::optional<Tensor>& ssp_in, const c10::optional<Tensor>& sk_ws,
-          const c10::optional<Tensor>& fault) {
+          const c10::optional<Tensor>& fault, const std::vector<int64_t>& ar_bases, int64_t ar_rank,
+          int64_t ar_fused_off) {
   CHECK_DEV(x); CHECK_DEV(wp); CHECK_DEV(out);
   CHECK_DT(x, torch::kBFloat16);
   CHECK_LASTDIM(x); CHECK_LASTDIM(out);
@@ -150,6 +151,18 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
     g.sk_bytes = (size_t)sk_ws->numel() * 4;
   }
   g.fault = reinterpret_cast<uint32_t*>(opt_ptr<int32_t>(fault, torch::kInt32, "fault"));
+  if (!ar_bases.empty()) {
+    // TP row-parallel decode GEMM + all-reduce in the epilogue (vgate/parallel/custom_allreduce.py)
+    const int world = (int)ar_bases.size();
+    TORCH_CHECK(world <= 8 && ar_rank >= 0 && ar_rank < world, "gemm ar: world 1..8, rank in range");
+    TORCH_CHECK(epi == 0 && M <= 16 && !g.hg && N / 16 <= vgate::AR_FUSED_TILES,
+                "gemm ar: bf16 epilogue, M <= 16, no norm hand-off, N <= 16 * AR_FUSED_TILES");
+    TORCH_CHECK(ar_fused_off >= vgate::AR_SIGNAL_BYTES, "gemm ar: fused region offset");
+    for (int r = 0; r < world; ++r) g.ar_fused[r] = reinterpret_cast<char*>(ar_bases[r]) + ar_fused_off;
+    g.ar_err = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ar_bases[ar_rank]) + vgate::ar_error_offset());
+    g.ar_rank = (int)ar_rank;
+    g.ar_world = world;
+  }
   c10::DeviceGuard guard(x.device());
   if (awq) vgate::launch_awq_gemm(g, cur_stream());
   else vgate::launch_gemm(g, cur_stream());
@@ -561,7 +574,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("rownorm") = false, py::arg("dbg_ts") = py::none(), py::arg("ntb") = 0, py::arg("path") = 0,
         py::arg("awq_szp") = py::none(), py::arg("hg_out") = py::none(), py::arg("hg_gamma") = py::none(),
         py::arg("ssp_out") = py::none(), py::arg("ssp_in") = py::none(), py::arg("sk_ws") = py::none(),
-        py::arg("fault") = py::none());
+        py::arg("fault") = py::none(), py::arg("ar_bases") = std::vector<int64_t>{}, py::arg("ar_rank") = 0,
+        py::arg("ar_fused_off") = 0);
   m.def("attention", &attention, "unified paged attention: decode (partitions merged in-launch) + varlen prefill tiles",
         py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),
@@ -606,6 +620,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("ar_open", &ar_open, "map a peer's ar_alloc buffer (hipIpcOpenMemHandle)");
   m.def("ar_close", &ar_close);
   m.def("ar_error", &ar_error, "read-and-clear the wait-timeout word of the own signal area");
+  m.def("ar_fused_bytes", [] { return vgate::AR_FUSED_BYTES; },
+        "bytes of the fused row-parallel GEMM + all-reduce region (after the two data buffers)");
   m.def("ar_blocks", &vgate::ar_blocks_used, "workgroups per custom all-reduce call (VGATE_AR_BLOCKS)");
   m.def("custom_allreduce", &custom_allreduce, "one-shot bf16 all-reduce over IPC-mapped peer buffers",
         py::arg("inp"), py::arg("out"), py::arg("bases"), py::arg("rank"), py::arg("max_bytes"),

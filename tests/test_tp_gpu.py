@@ -91,10 +91,12 @@ def _worker(rank, world, port, path, q, eager=False, env=None, tokens=320, promp
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("eager", [False, True])
-def test_tp2_on_gpu_matches_tp1(tmp_path, eager):
+@pytest.mark.parametrize("eager,fused", [(False, "1"), (True, "1"), (False, "0")])
+def test_tp2_on_gpu_matches_tp1(tmp_path, eager, fused):
     """graph == eager == TP=1: with every decode collective on the IPC kernels (all-reduce and the
-    logits all-gather) a gloo TP group replays captured hipGraphs for the buckets they cover."""
+    logits all-gather) a gloo TP group replays captured hipGraphs for the buckets they cover.
+    fused "1" (default): the decode o_proj / down_proj all-reduce inside their GEMM epilogue
+    (gemm_epilogue.h epilogue_ar); "0": the GEMM stores its partial, the one-shot kernel reduces."""
     from vgate.models.weights import save_checkpoint
     from vgate.runtime.engine import EngineConfig, LLMEngine
 
@@ -111,7 +113,8 @@ def test_tp2_on_gpu_matches_tp1(tmp_path, eager):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, path, q, eager)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, path, q, eager, {"VGATE_TP_FUSED_AR": fused}))
+             for r in range(2)]
     for p in procs:
         p.start()
     try:

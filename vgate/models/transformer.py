@@ -163,6 +163,13 @@ class DecoderModel:
         tp = self.tp
         T = x.shape[0]
         nch = self.tp_overlap_chunks if tp.size > 1 and T >= self.tp_overlap_min_tokens else 1
+        car = tp.custom_ar if tp.size > 1 else None
+        if nch <= 1 and car is not None and norm_out is None and resid.is_cuda and car.fuses(lin, x, resid):
+            # decode rows: the all-reduce runs in the GEMM's epilogue (every rank sums the ranks'
+            # fp32 partials in rank order, then adds the residual): one launch, no copy-in
+            ops.linear(x, lin, out=resid, residual=resid, ar=car)
+            car.calls += 1
+            return
         if nch <= 1:
             ops.linear(x, lin, out=resid, residual=resid if first else None, norm_out=norm_out)
             if tp.size > 1:

@@ -301,8 +301,13 @@ def workspace(device) -> torch.Tensor:
 def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
            residual: torch.Tensor | None = None, out_f32: bool = False, waves: int = 0, splitk: int = 0,
            norm: tuple | None = None, row_idx: torch.Tensor | None = None, qkv: dict | None = None,
-           path: int = 0, norm_out: tuple | None = None, prenorm: tuple | None = None) -> torch.Tensor:
+           path: int = 0, norm_out: tuple | None = None, prenorm: tuple | None = None,
+           ar=None) -> torch.Tensor:
     """out = epilogue(prologue(x) @ W^T).
+
+    ar (GPU, <= 16 rows, bf16 epilogue): a :class:`vgate.parallel.custom_allreduce.CustomAllReduce`;
+    the TP row-parallel GEMM then all-reduces in its epilogue: out = bf16(sum over ranks of
+    x @ W^T [+ bias]) + residual, one launch and no copy-in (gemm_epilogue.h epilogue_ar).
 
     RMSNorm hand-off to the int4 decode kernels (GPU, <= 16 rows, TP = 1; gemm_epilogue.h):
     norm_out=(hg, ssp, gamma) on a residual GEMM also writes hg = out * gamma and per-16-column
@@ -353,7 +358,7 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
     if M <= 16 and waves == 0 and splitk == 0:
         waves, splitk, ntb = lin.dec_waves, lin.dec_splitk, lin.dec_ntb  # (AWQ ntb -8: the wide int4 kernel)
         # stream-K decode kernel (csrc/kernels/gemm_streamk.hip): per-Linear plan, else the module default
-        sk = (lin.kind == "dense" and path == 0 and row_idx is None and norm_out is None
+        sk = (lin.kind == "dense" and path == 0 and row_idx is None and norm_out is None and ar is None
               and (lin.dec_sk if lin.dec_sk is not None else STREAMK_DECODE))
         if sk:  # (W, blocks per CU, k-steps per register group) of the plan, 0 = the kernel's default
             path = 3
@@ -382,6 +387,10 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
         kw.update(hg_out=norm_out[0], ssp_out=norm_out[1], hg_gamma=norm_out[2])
     if prenorm is not None:
         kw.update(ssp_in=prenorm[0], eps=float(prenorm[1]))
+    if ar is not None:
+        if M > 16 or epi != 0:
+            raise ValueError("fused all-reduce: decode rows (<= 16) and the bf16 epilogue only")
+        kw.update(ar_bases=ar.bases, ar_rank=ar.rank, ar_fused_off=ar.fused_off)
     C.gemm(x, lin.wp, lin.N, lin.K, out, epi, **kw)
     return out
 

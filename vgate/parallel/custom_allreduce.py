@@ -19,6 +19,7 @@ is the MI355X-native data plane the TP engine needs.
 from __future__ import annotations
 
 import logging
+import os
 
 import torch
 import torch.distributed as dist
@@ -27,6 +28,10 @@ log = logging.getLogger("vgate.parallel")
 
 SIGNAL_BYTES = 65536  # csrc/kernels/launchers.h AR_SIGNAL_BYTES
 MAX_RANKS = 8
+FUSED_TILES = 1024  # launchers.h AR_FUSED_TILES: output columns <= 16 * 1024 for the fused GEMM + all-reduce
+# VGATE_TP_FUSED_AR=0: decode row-parallel GEMMs store their partial and run the separate all-reduce
+# kernel (A/B); default: the all-reduce runs inside the GEMM's epilogue (gemm_epilogue.h epilogue_ar)
+FUSED = os.environ.get("VGATE_TP_FUSED_AR", "1") != "0"
 
 
 class CustomAllReduce:
@@ -45,7 +50,9 @@ class CustomAllReduce:
         mine = None
         try:
             with torch.cuda.device(device):
-                self.own = self.C.ar_alloc(SIGNAL_BYTES + 2 * self.max_bytes)
+                # + the fused row-parallel GEMM region (arrival words + two parity tile buffers)
+                self.fused_off = SIGNAL_BYTES + 2 * self.max_bytes
+                self.own = self.C.ar_alloc(self.fused_off + int(self.C.ar_fused_bytes()))
                 mine = bytes(self.C.ar_ipc_handle(self.own).numpy().tobytes())
         except Exception as e:  # noqa: BLE001 - reported through the gather, so no rank waits
             log.warning("custom all-reduce allocation failed: %s: %s", type(e).__name__, e)
@@ -74,7 +81,6 @@ class CustomAllReduce:
         self.calls = 0
         # VGATE_AR_TWO_SHOT: 1 forces the two-shot kernel for every all-reduce, -1 the one-shot one,
         # 0 (default) picks by size (tests force two-shot at TP = 2, where it is never picked)
-        import os
         self.force = int(os.environ.get("VGATE_AR_TWO_SHOT", "0"))
 
     def should_use(self, t: torch.Tensor) -> bool:
@@ -89,6 +95,12 @@ class CustomAllReduce:
         self.C.custom_allreduce(t, out, self.bases, self.rank, self.max_bytes, two_shot or self.force)
         self.calls += 1
         return out
+
+    def fuses(self, lin, x: torch.Tensor, out: torch.Tensor) -> bool:
+        """Whether the row-parallel GEMM ``out = x @ lin^T`` can all-reduce in its epilogue
+        (decode rows, bf16 output of at most AR_FUSED_TILES 16-column tiles on this device)."""
+        return (FUSED and x.shape[0] <= 16 and out.dtype == torch.bfloat16 and out.device == self.device
+                and lin.N // 16 <= FUSED_TILES)
 
     def should_gather(self, t: torch.Tensor) -> bool:
         nbytes = t.numel() * t.element_size()
@@ -114,6 +126,42 @@ class CustomAllReduce:
             self.C.ar_close(ptr)
         self.C.ar_free(self.own)
         self.own, self._opened = None, []
+
+
+class LoopbackFused:
+    """A one-rank fused all-reduce region (world 1: every tile exchanges with itself). It prices
+    the fused epilogue — partial store, arrival word, poll, re-read — on one GPU without peers
+    (``benchmarks/tp_rank_bench.py --fused-ar``, the kernel tests); the standalone collectives
+    stay no-ops (``should_use`` / ``should_gather`` are False)."""
+
+    def __init__(self, device: torch.device):
+        from vgate import ops
+
+        self.C = ops.native()
+        self.rank, self.world, self.device, self.max_bytes = 0, 1, device, 0
+        self.fused_off = SIGNAL_BYTES
+        with torch.cuda.device(device):
+            self.own = self.C.ar_alloc(SIGNAL_BYTES + int(self.C.ar_fused_bytes()))
+        self.bases = [self.own]
+        self.calls = 0
+
+    fuses = CustomAllReduce.fuses
+
+    def should_use(self, t: torch.Tensor) -> bool:
+        return False
+
+    def should_gather(self, t: torch.Tensor) -> bool:
+        return False
+
+    def check(self) -> None:
+        if self.C.ar_error(self.own):
+            raise RuntimeError("custom all-reduce: a peer did not arrive within the spin limit")
+
+    def close(self) -> None:
+        if self.own is not None:
+            torch.cuda.synchronize(self.device)
+            self.C.ar_free(self.own)
+            self.own = None
 
 
 def maybe_create(group, rank: int, world: int, device: torch.device, max_bytes: int = 8 << 20):
