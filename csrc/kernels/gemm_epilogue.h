@@ -223,6 +223,12 @@ __device__ __forceinline__ float prenorm_ss(const GemmParams& p, int m, int quar
 template <int NTB, bool have>
 __device__ __forceinline__ void epilogue_ar(const GemmParams& p, const f32x4 (&v)[NTB], int m, int nt0, int nsub,
                                             const EpiPre<NTB> e, bool valid) {
+  // The regions are uncached device memory (hipDeviceMallocUncached, mapped by the peers): no L2
+  // holds their lines, so the hand-off needs ORDER, not cache maintenance — a system-scope release
+  // / acquire would write back / drop the whole L2 (buffer_wbl2 / buffer_inv) once per tile and
+  // cost the launch its weights. Partial -> sc0 sc1 vector stores, s_waitcnt vmcnt(0), relaxed
+  // arrival word; relaxed polls; sc0 sc1 vector loads of the peers' partials after the poll.
+  constexpr int SYS = 17;  // cache policy sc0 | sc1: system-coherent, bypasses every cache level
   const ArFused& a = p.ar;
   const int lane = threadIdx.x & 63;
   const int piece = (m & 15) | ((nsub >> 2) << 4);  // this lane's 16-B piece of a tile slot
@@ -233,7 +239,8 @@ __device__ __forceinline__ void epilogue_ar(const GemmParams& p, const f32x4 (&v
 #pragma unroll
   for (int j = 0; j < NTB; ++j) {
     const int t = nt0 + j;
-    ep[j] = __hip_atomic_load(&my_flags[t * 8 + a.rank], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
+    ep[j] = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(&my_flags[t * 8 + a.rank], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u);
     o[j] = v[j];
     if (p.bias) {
       uint2 b;
@@ -242,15 +249,15 @@ __device__ __forceinline__ void epilogue_ar(const GemmParams& p, const f32x4 (&v
       o[j][0] += bf_lo(b.x); o[j][1] += bf_hi(b.x);
       o[j][2] += bf_lo(b.y); o[j][3] += bf_hi(b.y);
     }
-    *reinterpret_cast<f32x4*>(mine + AR_FUSED_FLAG_BYTES + (int64_t)(ep[j] & 1) * AR_FUSED_DATA +
-                              ((int64_t)t * 64 + piece) * 16) = o[j];
+    const char* slot = mine + AR_FUSED_FLAG_BYTES + (int64_t)(ep[j] & 1) * AR_FUSED_DATA + (int64_t)t * 1024;
+    __builtin_amdgcn_raw_buffer_store_b128(o[j], rsrc_of(slot), (uint32_t)piece * 16u, 0, SYS);
   }
-  __threadfence_system();
+  drain_stores();
   if (lane < a.world) {  // arrive at every peer (own region included: that word is my epoch)
     uint32_t* pf = reinterpret_cast<uint32_t*>(a.base[lane]);
 #pragma unroll
     for (int j = 0; j < NTB; ++j)
-      __hip_atomic_store(&pf[(nt0 + j) * 8 + a.rank], ep[j], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&pf[(nt0 + j) * 8 + a.rank], ep[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
     uint32_t spins = 0;
@@ -259,7 +266,7 @@ __device__ __forceinline__ void epilogue_ar(const GemmParams& p, const f32x4 (&v
       if (lane < a.world) {
 #pragma unroll
         for (int j = 0; j < NTB; ++j)
-          ok = ok && (int32_t)(__hip_atomic_load(&my_flags[(nt0 + j) * 8 + lane], __ATOMIC_ACQUIRE,
+          ok = ok && (int32_t)(__hip_atomic_load(&my_flags[(nt0 + j) * 8 + lane], __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_SYSTEM) - ep[j]) >= 0;
       }
       if (__all(ok)) break;
@@ -270,17 +277,18 @@ __device__ __forceinline__ void epilogue_ar(const GemmParams& p, const f32x4 (&v
       __builtin_amdgcn_s_sleep(1);
     }
   }
+  asm volatile("" ::: "memory");  // the partial loads stay behind the poll
 #pragma unroll
   for (int j = 0; j < NTB; ++j) {
     const int t = nt0 + j;
-    const int64_t off = AR_FUSED_FLAG_BYTES + (int64_t)(ep[j] & 1) * AR_FUSED_DATA + ((int64_t)t * 64 + piece) * 16;
+    const int64_t off = AR_FUSED_FLAG_BYTES + (int64_t)(ep[j] & 1) * AR_FUSED_DATA + (int64_t)t * 1024;
     // every peer's piece in flight before the first is summed; slots past world re-read rank 0
     f32x4 r[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int src = q < a.world ? q : 0;
       r[q] = src == a.rank ? o[j]
-                           : __builtin_bit_cast(f32x4, ld_nt16(reinterpret_cast<const uint4*>(a.base[src] + off)));
+                           : __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(a.base[src] + off), (uint32_t)piece * 16u, 0, SYS);
     }
     f32x4 s = r[0];
 #pragma unroll
