@@ -155,12 +155,7 @@ class LLMEngine:
         if self.device.type == "cuda" and cfg.prefill_autotune:
             t1 = time.perf_counter()
             # prefill buckets (>= 128 rows) and the medium buckets of mixed prefill + decode steps
-            ms = [t for t in self.runner.t_buckets if t > 16]
-            # + the long-prompt chunk sizes (eager steps past the graph buckets): tuned plans at 2048 rows
-            # took Llama-3-8B's per-layer prefill GEMMs 860 -> 802 us and Qwen2.5-1.5B's 345 -> 261 us
-            # (profiles/r4_prefill_chunk_buckets.log)
-            top = max(ms) if ms else 0
-            ms += [m for m in (1024, 2048, 4096, 8192) if top < m <= cfg.max_num_batched_tokens]
+            ms = [t for t in self.runner.t_buckets if t > 16]  # (t_buckets end at max_num_batched_tokens)
             lins = [lin for L in self.model.layers for lin in (L.qkv, L.o, L.gate_up, L.down)]
             if self.tp.size > 1:
                 # rank 0 measures, every rank applies the same plans (per-rank timing noise would
