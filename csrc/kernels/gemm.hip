@@ -52,6 +52,7 @@ VG_EXTERN_EPI(EPI_BF16)
 VG_EXTERN_EPI(EPI_F32)
 VG_EXTERN_EPI(EPI_SILU)
 VG_EXTERN_EPI(EPI_QKV)
+VG_EXTERN_EPI(EPI_BF16_AR)
 
 // ---- AWQ prefill operand: int4 fragments -> bf16 fragments (same fragment order) ----
 // Long AWQ steps run the LDS-tiled bf16 prefill kernel (gemm_prefill.hip) on a per-call scratch
@@ -139,7 +140,7 @@ void launch_gemm(const GemmArgs& g, hipStream_t st) {
   // TP row-parallel decode GEMM with the all-reduce in the epilogue: the tile-per-block decode kernels
   // (one wave finishes a whole 16-row tile: epilogue_ar's lane layout); the binding checked the shape
   if (g.ar_world > 0) {
-    launch_dispatch<false>(to_params(g), g, st);
+    dispatch_epi<EPI_BF16_AR, false>(to_params(g), g, st);
     return;
   }
   // long steps (prefill chunks): the LDS-tiled MFMA kernel (gemm_prefill.hip) on the same packed
@@ -162,7 +163,7 @@ void launch_awq_gemm(const GemmArgs& g, hipStream_t st) {
   if (g.ar_world > 0) {  // fused all-reduce: the K-split int4 kernel (gemm_finish -> epilogue_ar)
     GemmArgs h = g;
     h.ntb = -2;
-    launch_dispatch<true>(to_params(h), h, st);
+    dispatch_epi<EPI_BF16_AR, true>(to_params(h), h, st);
     return;
   }
   // decode on the wide int4 kernel (one block per CU owning whole tiles): g.ntb == -8 (a decode plan)

@@ -1109,6 +1109,14 @@ void dispatch_epi(GemmParams p, const GemmArgs& g, hipStream_t st) {
   const int norm = g.norm_w != nullptr ? 1 : (g.rownorm ? 2 : (g.ssp_in != nullptr ? 3 : 0));
   const int ntiles = g.N / 16;
   const bool pair = ntiles % 2 == 0 && ntiles >= 1024;
+  if constexpr (EPI == EPI_BF16_AR) {  // TP all-reduce in the epilogue: decode rows, no norm (gemm.hip)
+    if constexpr (!AWQ) {
+      if (g.ntb == 4 && ntiles % 4 == 0) { launch_one<1, 4, EPI, 0, AWQ>(p, g, st); return; }
+    }
+    if (g.ntb == 2 || (g.ntb == 0 && pair)) launch_one<1, 2, EPI, 0, AWQ>(p, g, st);
+    else launch_one<1, 1, EPI, 0, AWQ>(p, g, st);
+    return;
+  }
 #define VG_NORM(NTB_)                                                           \
   do {                                                                          \
     if (norm == 1) launch_m<NTB_, EPI, 1, AWQ>(p, g, st);                       \

@@ -9,7 +9,9 @@
 
 namespace vgate {
 
-enum GemmEpi : int { EPI_BF16 = 0, EPI_F32 = 1, EPI_SILU = 2, EPI_QKV = 3 };
+// EPI_BF16_AR: EPI_BF16 with the TP all-reduce in the epilogue (epilogue_ar); its own instantiations
+// (gemm_epi_bf16ar.hip), so the TP = 1 kernels carry none of its code or registers
+enum GemmEpi : int { EPI_BF16 = 0, EPI_F32 = 1, EPI_SILU = 2, EPI_QKV = 3, EPI_BF16_AR = 4 };
 constexpr int SK_MAX = 8;  // split-K slices per tile (the combine issues all slices' loads at once)
 
 // TP row-parallel decode GEMM: the all-reduce runs in the epilogue (epilogue_ar) when world >= 1
@@ -115,13 +117,13 @@ __device__ __forceinline__ void epi_pre_a(const GemmParams& p, EpiPre<NTB>& e, i
     e.pos = p.positions[m];
     e.slot = p.slots[m];
     e.b0 = p.bias ? *reinterpret_cast<const uint2*>(p.bias + qkv_col(nt0, nsub)) : make_uint2(0, 0);
-  } else if constexpr (EPI == EPI_BF16 || EPI == EPI_F32) {
+  } else if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_AR || EPI == EPI_F32) {
 #pragma unroll
     for (int j = 0; j < NTB; ++j) {
       const int n = (nt0 + j) * 16 + nsub;
       const uint2 b = p.bias ? *reinterpret_cast<const uint2*>(p.bias + n) : make_uint2(0, 0);
       uint2 r = make_uint2(0, 0);
-      if constexpr (EPI == EPI_BF16) r = p.res ? *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldr + n) : r;
+      if constexpr (EPI != EPI_F32) r = p.res ? *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldr + n) : r;
       if (j == 0) { e.b0 = b; e.r0 = r; } else { e.b1 = b; e.r1 = r; }
     }
   }
@@ -219,7 +221,8 @@ __device__ __forceinline__ float prenorm_ss(const GemmParams& p, int m, int quar
 // region: only it writes that slot), parity buffers by epoch, bounded waits on the all-reduce's
 // sticky error word: the one-shot kernel's safety argument, per tile (a peer re-uses a parity
 // buffer of tile t only after my next arrival on t, which follows my reads). Every lane of the
-// wave calls in (wave-wide poll). Decode launchers only (gemm.hip routes ar_world >= 1 there).
+// wave calls in (wave-wide poll). Decode launchers only (gemm.hip routes ar_world >= 1 to the
+// EPI_BF16_AR instantiations of the one-wave-per-tile decode kernels).
 template <int NTB, bool have>
 __device__ __forceinline__ void epilogue_ar(const GemmParams& p, const f32x4 (&v)[NTB], int m, int nt0, int nsub,
                                             const EpiPre<NTB> e, bool valid) {
@@ -322,11 +325,11 @@ __device__ __forceinline__ void epilogue_ar(const GemmParams& p, const f32x4 (&v
 template <int NTB, int EPI, bool have>
 __device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[NTB], int m, int nt0, int nsub,
                                          const EpiPre<NTB> e, bool valid) {
+  if constexpr (EPI == EPI_BF16_AR) {  // every lane calls in: wave-wide arrival poll
+    epilogue_ar<NTB, have>(p, v, m, nt0, nsub, e, valid);
+    return;
+  }
   if constexpr (EPI == EPI_BF16) {
-    if (p.ar.world > 0) {  // every lane calls in: wave-wide arrival poll
-      epilogue_ar<NTB, have>(p, v, m, nt0, nsub, e, valid);
-      return;
-    }
     if (p.hg != nullptr) {  // every lane calls in: the tile's sum of squares is a cross-lane fold
       epilogue_norm_out<NTB, have>(p, v, m, nt0, nsub, e, valid);
       return;
