@@ -221,8 +221,16 @@ struct SampleArgs {
   // zero-initialised, self-resetting arrival tickets [B]; null -> in-launch meetings only
   struct RowState* state = nullptr;
   uint32_t* tickets = nullptr;
+  // single-launch mode (sampling.hip sample_gran_kernel): tagged partial granules [B][2][nseg][2] uint4,
+  // per-row epochs [B] and exit tickets [B] (zero-initialised, self-advancing / self-resetting), and
+  // the sticky fault word (bit 16: a row meeting gave up); null -> the pass kernels
+  void* gran = nullptr;
+  uint32_t* epoch = nullptr;
+  uint32_t* done = nullptr;
+  uint32_t* fault = nullptr;
 };
 void launch_sample(const SampleArgs& s, hipStream_t st);
+void set_sample_single(int on);  // 1 (default): the single-launch granule sampler when its workspace is given
 int sample_segments(int B, int V);
 void set_sample_nseg(int n);  // cap on segments per row (0 = B*NSEG <= 1024 bound only)
 void set_sample_round_launches(int n);  // rejection rounds run as launches (0 = pass 0 only)

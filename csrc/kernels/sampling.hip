@@ -403,6 +403,134 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a, ui
   }
 }
 
+// ---- single launch: tagged granules instead of tickets / counters ----
+// The pass kernels' meetings cost a launch boundary per pass, the in-launch ones a serialised
+// atomic per arriving block (~0.5 us each, 32 per row). Here every block of a row publishes its
+// pass partial as two 16-B granules {.., tag} (device-coherent sc1 stores, one transaction each),
+// and EVERY block of the row gathers all of the row's granules itself (lane s polls segment s
+// until both tags carry this pass's tag), merges them in the same fixed lane order and takes the
+// same accept / reject decision — no counter, no merger block, one memory round trip after the
+// last partial lands. Tags = (row epoch << 6) | pass: the epoch advances once per launch (the
+// row's last block to leave, told by its exit ticket), so a granule of an earlier launch never
+// matches; granules alternate two buffers by pass parity (a block reaches pass g + 2, rewriting
+// parity g, only after every block of the row published g + 1, i.e. finished reading g).
+// Every wait is bounded: a give-up sets fault bit 16 (the engine fails the step) and the row
+// falls back to its argmax. B x nseg <= 256 blocks: all co-resident.
+__device__ __forceinline__ void gran_publish(uint4* g, const Acc& a, int mode, uint32_t tag) {
+  // mode 0 (pass 0): {mx, z, amx} + {gk, gi}; mode 1 (rounds): {cnt, q, gk} + {gi}
+  const f32x4 g0 = mode == 0 ? f32x4{a.mx, a.z, __int_as_float(a.amx), __uint_as_float(tag)}
+                             : f32x4{a.cnt, a.q, a.gk, __uint_as_float(tag)};
+  const f32x4 g1 = mode == 0 ? f32x4{a.gk, __int_as_float(a.gi), 0.f, __uint_as_float(tag)}
+                             : f32x4{__int_as_float(a.gi), 0.f, 0.f, __uint_as_float(tag)};
+  st_sc1_x4(reinterpret_cast<float*>(g), 0u, g0);
+  st_sc1_x4(reinterpret_cast<float*>(g), 16u, g1);
+}
+
+// wave 0: gather the nseg granule pairs of (row, parity) and merge them in lane order; lane 0 ends
+// with the merge. Returns false if a wait gave up.
+__device__ __forceinline__ bool gran_gather(const uint4* gbase, int nseg, int mode, uint32_t tag, float c, Acc& out,
+                                            uint32_t* fault) {
+  const int lane = threadIdx.x & 63;
+  Acc a = acc_init();
+  bool ok = true;
+  if (lane < nseg) {
+    const float* gp = reinterpret_cast<const float*>(gbase + 2 * lane);
+    f32x4 g0, g1;
+    uint32_t spins = 0;
+    while (true) {
+      g0 = ld_sc1_x4(gp, 0u);
+      g1 = ld_sc1_x4(gp, 16u);
+      if (__float_as_uint(g0[3]) == tag && __float_as_uint(g1[3]) == tag) break;
+      if (++spins > (1u << 22)) { ok = false; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (ok) {
+      if (mode == 0) {
+        a.mx = g0[0]; a.z = g0[1]; a.amx = __float_as_int(g0[2]); a.gk = g1[0]; a.gi = __float_as_int(g1[1]);
+      } else {
+        a.cnt = g0[0]; a.q = g0[1]; a.gk = g0[2]; a.gi = __float_as_int(g1[0]);
+      }
+    }
+  }
+  const bool all_ok = __all(ok);
+  if (!all_ok && lane == 0 && fault != nullptr) atomicOr(fault, 16u);
+  acc_step<1>(a, c);
+  acc_step<2>(a, c);
+  acc_step<4>(a, c);
+  acc_step<8>(a, c);
+  acc_step<16>(a, c);
+  acc_step<32>(a, c);
+  out = a;
+  return all_ok;
+}
+
+__global__ __launch_bounds__(SAMPLE_THREADS) void sample_gran_kernel(SampleArgs a) {
+  TLScope tl_scope(a.tl);
+  __shared__ Acc red[SAMPLE_THREADS / 64];
+  __shared__ Acc merged;
+  __shared__ int s_ok;
+  const int seg = blockIdx.x, nseg = gridDim.x, row = blockIdx.y, tid = threadIdx.x;
+  const int V4 = a.V >> 2;
+  const int v_lo = (int)(((long long)V4 * seg) / nseg), v_hi = (int)(((long long)V4 * (seg + 1)) / nseg);
+  const float* x = a.logits + (size_t)row * a.ldl;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  const RowParams rp = row_params(a, row);
+  const float c = rp.c;
+  const uint32_t ep = __builtin_amdgcn_readfirstlane(__float_as_uint(ld_sc1(reinterpret_cast<const float*>(a.epoch + row))));
+  uint4* rowg = reinterpret_cast<uint4*>(a.gran) + (size_t)row * 2 * nseg * 2;  // [parity][nseg][2]
+  // one pass: sweep, block merge, publish, gather every segment's granules, share the row merge
+  auto pass = [&](int mode, float xj, float rmx, uint32_t round, uint32_t gen) -> bool {
+    Acc acc = acc_init();
+    sweep_range(x4, v_lo, v_hi, mode, xj, rmx, round, rp, acc);
+    block_reduce_acc(acc, c, red);
+    const uint32_t tag = (ep << 6) | gen;
+    uint4* pg = rowg + (size_t)(gen & 1) * nseg * 2;
+    if (tid == 0) {
+      gran_publish(pg + 2 * seg, acc, mode, tag);
+    }
+    if (tid < 64) {
+      Acc r;
+      const bool ok = gran_gather(pg, nseg, mode, tag, c, r, a.fault);
+      if (tid == 0) {
+        merged = r;
+        s_ok = ok;
+      }
+    }
+    __syncthreads();
+    return s_ok != 0;
+  };
+  uint32_t gen = 1;
+  bool ok = pass(0, 0.f, 0.f, 0u, gen);
+  const float mx = merged.mx, z = merged.z;
+  int chosen = merged.amx, j = merged.gi;
+  if (ok && !rp.greedy) {
+    if (rp.use_k || rp.use_p) {
+      const float pmass = rp.topp * z;
+      for (uint32_t round = 1; round <= 60 && j >= 0; ++round) {
+        ok = pass(1, x[j], mx, round, ++gen);
+        if (!ok) { j = -1; break; }
+        const bool ok_k = !rp.use_k || merged.cnt < (float)rp.topk;
+        const bool ok_p = !rp.use_p || merged.q < pmass;
+        if (ok_k && ok_p) break;
+        j = merged.gi;  // next candidate, drawn from {x > x_j}
+      }
+    }
+    if (j >= 0) chosen = j;
+  }
+  if (tid == 0) {
+    if (seg == 0) finish_row(a, row, chosen, mx, z, c);
+    // the row's last block to leave advances the epoch (every block read it at its start)
+    const uint32_t d = __hip_atomic_fetch_add(a.done + row, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == (uint32_t)nseg - 1) {
+      __hip_atomic_store(a.done + row, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      st_sc1(reinterpret_cast<float*>(a.epoch + row), __uint_as_float((ep + 1u) & 0x03ffffffu));
+    }
+  }
+}
+
+int g_sample_single = 1;
+void set_sample_single(int on) { g_sample_single = on; }
+
 int g_sample_nseg = 64;  // segments per row cap (set_sample_nseg; measured: benchmarks/sampler_stress.py)
 void set_sample_nseg(int n) { g_sample_nseg = n; }
 
@@ -425,6 +553,11 @@ void launch_sample(const SampleArgs& s, hipStream_t st) {
   int nseg = sample_segments(s.B, s.V);
   if (s.parts == nullptr || s.sync == nullptr) nseg = 1;
   SampleArgs a = s;
+  if (nseg > 1 && nseg <= 64 && g_sample_single && s.gran != nullptr && s.epoch != nullptr && s.done != nullptr) {
+    a.tl = tl_take("sample_gran", nseg * s.B);
+    hipLaunchKernelGGL(sample_gran_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, a);
+    return;
+  }
   if (nseg > 1 && s.state != nullptr && s.tickets != nullptr && g_sample_round_launches >= 0) {
     // pass 0 and the first rejection rounds as launches (last-arriver merges, no meetings),
     // then the in-launch rounds for rows still pending

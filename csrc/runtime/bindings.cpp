@@ -380,7 +380,8 @@ void attention(const Tensor& q, int64_t q_stride, const Tensor& k_cache, const T
 void sample(const Tensor& logits, const c10::optional<Tensor>& temperature,
             const c10::optional<Tensor>& top_p, const c10::optional<Tensor>& top_k,
             const c10::optional<Tensor>& seeds, const c10::optional<Tensor>& offsets, Tensor& out,
-            const c10::optional<Tensor>& out_logprob, const c10::optional<Tensor>& ws) {
+            const c10::optional<Tensor>& out_logprob, const c10::optional<Tensor>& ws,
+            const c10::optional<Tensor>& fault) {
   CHECK_DEV(logits); CHECK_DEV(out);
   CHECK_DT(logits, torch::kFloat32); CHECK_DT(out, torch::kInt32);
   CHECK_LASTDIM(logits);
@@ -416,8 +417,16 @@ void sample(const Tensor& logits, const c10::optional<Tensor>& temperature,
         s.state = reinterpret_cast<vgate::RowState*>(reinterpret_cast<int32_t*>(ws->data_ptr()) + 20480);
         s.tickets = reinterpret_cast<uint32_t*>(ws->data_ptr()) + 22528;
       }
+      // [24576, 28672): single-launch granules [B][2][nseg][2] x 16 B (B * nseg <= 256); [28672, 28928)
+      // per-row epochs; [28928, 29184) per-row exit tickets
+      if (ws->numel() >= 29184 && s.B <= 256) {
+        s.gran = reinterpret_cast<int32_t*>(ws->data_ptr()) + 24576;
+        s.epoch = reinterpret_cast<uint32_t*>(ws->data_ptr()) + 28672;
+        s.done = reinterpret_cast<uint32_t*>(ws->data_ptr()) + 28928;
+      }
     }
   }
+  s.fault = reinterpret_cast<uint32_t*>(opt_ptr<int32_t>(fault, torch::kInt32, "fault"));
   c10::DeviceGuard guard(logits.device());
   vgate::launch_sample(s, cur_stream());
 }
@@ -600,7 +609,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("fault") = py::none());
   m.def("sample", &sample, "temperature/top-k/top-p sampling (segmented Gumbel-max + exact rejection)",
         py::arg("logits"), py::arg("temperature"), py::arg("top_p"), py::arg("top_k"), py::arg("seeds"),
-        py::arg("offsets"), py::arg("out"), py::arg("out_logprob") = py::none(), py::arg("ws") = py::none());
+        py::arg("offsets"), py::arg("out"), py::arg("out_logprob") = py::none(), py::arg("ws") = py::none(),
+        py::arg("fault") = py::none());
+  m.def("set_sample_single", &vgate::set_sample_single,
+        "1: the single-launch granule sampler (default), 0: the pass kernels (A/B)");
   m.def("sample_segments", &vgate::sample_segments, "blocks per row the sampler uses for (B, V)");
   m.def("set_sample_nseg", &vgate::set_sample_nseg, "cap the sampler's segments per row (experiments)");
   m.def("set_sample_round_launches", &vgate::set_sample_round_launches,

@@ -4,6 +4,7 @@ Run on an MI355X: ``python -m pytest tests -m gpu``. Shapes include the real
 Qwen2.5-1.5B / Llama-3 projection sizes.
 """
 import math
+import os
 
 import pytest
 import torch
@@ -345,6 +346,53 @@ def test_sample_top_p_frequent_rejection(B):
     assert counts[allowed].sum().item() == n, "sampled outside the nucleus"
     emp = counts.double() / n
     assert (emp[allowed] - q[allowed]).abs().max().item() < 0.03, (emp[allowed], q[allowed])
+
+
+@pytest.mark.parametrize("B", [1, 8, 16])
+def test_sample_single_launch_matches_pass_kernels(B):
+    """The single-launch granule sampler (every block gathers its row's tagged partials itself) draws
+    exactly what the pass kernels draw — same Gumbel noise, same acceptance tests — over many
+    consecutive launches (the per-row epoch advances each launch, so stale granules never match),
+    for greedy / temperature / top-p / top-k rows, and under hipGraph replay."""
+    torch.manual_seed(40 + B)
+    V = 151936
+    C = ops.native()
+    L = (torch.randn(B, V, device=DEV) * 0.8).contiguous()
+    t = torch.full((B,), 0.7, device=DEV)
+    t[0] = 0.0  # a greedy row
+    tp = torch.full((B,), 0.9, device=DEV)
+    tk = torch.full((B,), -1, dtype=torch.int32, device=DEV)
+    if B > 2:
+        tk[2] = 50
+        tp[1] = 1.0  # plain temperature row
+    seeds = torch.arange(B, device=DEV, dtype=torch.int64) * 7 + 3
+    try:
+        for off in range(120):
+            offs = torch.full((B,), off, dtype=torch.int64, device=DEV)
+            C.set_sample_single(1)
+            a = ops.sample(L, t, top_p=tp, top_k=tk, seeds=seeds, offsets=offs)
+            C.set_sample_single(0)
+            b = ops.sample(L, t, top_p=tp, top_k=tk, seeds=seeds, offsets=offs)
+            assert torch.equal(a, b), off
+        C.set_sample_single(1)
+        offs = torch.full((B,), 7, dtype=torch.int64, device=DEV)
+        out = torch.empty(B, dtype=torch.int32, device=DEV)
+        want = ops.sample(L, t, top_p=tp, top_k=tk, seeds=seeds, offsets=offs).clone()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                ops.sample(L, t, top_p=tp, top_k=tk, seeds=seeds, offsets=offs, out=out)
+        torch.cuda.current_stream().wait_stream(s)
+        for _ in range(70):  # > 64 replays: the epoch keeps the tags apart
+            out.fill_(-1)
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(out, want)
+        assert int(ops.fault_word(DEV)[0].item()) & 16 == 0, "a sampler row meeting gave up"
+    finally:
+        C.set_sample_single(int(os.environ.get("VGATE_SAMPLE_SINGLE", "1")))
 
 
 def test_sample_logprob():

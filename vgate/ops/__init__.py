@@ -57,6 +57,9 @@ def _configure(mod) -> None:
         # launches; the step time is the same as with one round launch (1266.1 vs 1269.9-1271.2 us,
         # profiles/r4_sampler_round_launches.log)
         mod.set_sample_round_launches(int(os.environ.get("VGATE_SAMPLE_ROUND_LAUNCHES", "0")))
+    if hasattr(mod, "set_sample_single"):
+        # VGATE_SAMPLE_SINGLE=0: the pass kernels above instead of the single-launch granule sampler
+        mod.set_sample_single(int(os.environ.get("VGATE_SAMPLE_SINGLE", "1")))
 
 
 def native_available() -> bool:
@@ -499,7 +502,8 @@ _FAULT: dict = {}
 
 def fault_word(device) -> torch.Tensor:
     """Per-device sticky fault word of the in-launch hand-offs (bit 1: a flash K-split waiter gave
-    up; bit 0 is reserved). Kernels only OR bits in; the step graph's last node
+    up, 4: a stream-K partial poll, 8: a split-K granule poll, 16: a sampler row meeting; bit 0 is
+    reserved). Kernels only OR bits in; the step graph's last node
     copies it to the host ring (ModelRunner.kernel_fault), and a non-zero word fails the engine."""
     key = str(device)
     t = _FAULT.get(key)
@@ -638,7 +642,8 @@ def sample(logits, temperature=None, top_p=None, top_k=None, seeds=None, offsets
     if not _gpu(logits):
         out.copy_(ref.sample_ref(logits, temperature, top_p, top_k, generators))
         return out
-    native().sample(logits, temperature, top_p, top_k, seeds, offsets, out, out_logprob, sample_workspace(logits.device))
+    native().sample(logits, temperature, top_p, top_k, seeds, offsets, out, out_logprob, sample_workspace(logits.device),
+                    fault_word(logits.device))
     return out
 
 
