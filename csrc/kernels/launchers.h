@@ -221,12 +221,11 @@ struct SampleArgs {
   // zero-initialised, self-resetting arrival tickets [B]; null -> in-launch meetings only
   struct RowState* state = nullptr;
   uint32_t* tickets = nullptr;
-  // single-launch mode (sampling.hip sample_gran_kernel): tagged partial granules [B][2][nseg][2] uint4,
-  // per-row epochs [B] and exit tickets [B] (zero-initialised, self-advancing / self-resetting), and
-  // the sticky fault word (bit 16: a row meeting gave up); null -> the pass kernels
+  // single-launch mode (sampling.hip sample_gran_kernel): tagged partial granules [B][2][nseg][2] uint4
+  // and per-row epochs [B] (zero-initialised, self-advancing), and the sticky fault word (bit 16: a row
+  // meeting gave up); null -> the pass kernels
   void* gran = nullptr;
   uint32_t* epoch = nullptr;
-  uint32_t* done = nullptr;
   uint32_t* fault = nullptr;
 };
 void launch_sample(const SampleArgs& s, hipStream_t st);

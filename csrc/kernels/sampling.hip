@@ -410,10 +410,10 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a, ui
 // and EVERY block of the row gathers all of the row's granules itself (lane s polls segment s
 // until both tags carry this pass's tag), merges them in the same fixed lane order and takes the
 // same accept / reject decision — no counter, no merger block, one memory round trip after the
-// last partial lands. Tags = (row epoch << 6) | pass: the epoch advances once per launch (the
-// row's last block to leave, told by its exit ticket), so a granule of an earlier launch never
-// matches; granules alternate two buffers by pass parity (a block reaches pass g + 2, rewriting
-// parity g, only after every block of the row published g + 1, i.e. finished reading g).
+// last partial lands. Tags = (row epoch << 6) | pass: the epoch advances once per launch (one store
+// by the row's segment 0 at its exit, see the end of the kernel), so a granule of an earlier launch
+// never matches; granules alternate two buffers by pass parity (a block reaches pass g + 2,
+// rewriting parity g, only after every block of the row published g + 1, i.e. finished reading g).
 // Every wait is bounded: a give-up sets fault bit 16 (the engine fails the step) and the row
 // falls back to its argmax. B x nseg <= 256 blocks: all co-resident.
 __device__ __forceinline__ void gran_publish(uint4* g, const Acc& a, int mode, uint32_t tag) {
@@ -464,9 +464,10 @@ __device__ __forceinline__ bool gran_gather(const uint4* gbase, int nseg, int mo
   return all_ok;
 }
 
-__global__ __launch_bounds__(SAMPLE_THREADS) void sample_gran_kernel(SampleArgs a) {
+template <int NT>
+__global__ __launch_bounds__(NT) void sample_gran_kernel(SampleArgs a) {
   TLScope tl_scope(a.tl);
-  __shared__ Acc red[SAMPLE_THREADS / 64];
+  __shared__ Acc red[NT / 64];
   __shared__ Acc merged;
   __shared__ int s_ok;
   const int seg = blockIdx.x, nseg = gridDim.x, row = blockIdx.y, tid = threadIdx.x;
@@ -517,14 +518,12 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_gran_kernel(SampleArgs 
     }
     if (j >= 0) chosen = j;
   }
-  if (tid == 0) {
-    if (seg == 0) finish_row(a, row, chosen, mx, z, c);
-    // the row's last block to leave advances the epoch (every block read it at its start)
-    const uint32_t d = __hip_atomic_fetch_add(a.done + row, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (d == (uint32_t)nseg - 1) {
-      __hip_atomic_store(a.done + row, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      st_sc1(reinterpret_cast<float*>(a.epoch + row), __uint_as_float((ep + 1u) & 0x03ffffffu));
-    }
+  if (tid == 0 && seg == 0) {
+    finish_row(a, row, chosen, mx, z, c);
+    // advance the row's epoch for the next launch: one store by segment 0, no exit ticket (32 device-scope
+    // atomics or same-word stores per row serialise at the memory side). Safe: no block gets here before
+    // it gathered pass 1 from EVERY block of its row, i.e. after every block read the epoch
+    st_sc1(reinterpret_cast<float*>(a.epoch + row), __uint_as_float((ep + 1u) & 0x03ffffffu));
   }
 }
 
@@ -553,9 +552,10 @@ void launch_sample(const SampleArgs& s, hipStream_t st) {
   int nseg = sample_segments(s.B, s.V);
   if (s.parts == nullptr || s.sync == nullptr) nseg = 1;
   SampleArgs a = s;
-  if (nseg > 1 && nseg <= 64 && g_sample_single && s.gran != nullptr && s.epoch != nullptr && s.done != nullptr) {
+  if (nseg > 1 && nseg <= 64 && g_sample_single && s.gran != nullptr && s.epoch != nullptr) {
     a.tl = tl_take("sample_gran", nseg * s.B);
-    hipLaunchKernelGGL(sample_gran_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, a);
+    // 256 threads per block: 512 / 1024 measured no faster / slower (profiles/r4_sampler_single_launch.log)
+    hipLaunchKernelGGL(sample_gran_kernel<256>, dim3(nseg, s.B), dim3(256), 0, st, a);
     return;
   }
   if (nseg > 1 && s.state != nullptr && s.tickets != nullptr && g_sample_round_launches >= 0) {

@@ -418,11 +418,10 @@ void sample(const Tensor& logits, const c10::optional<Tensor>& temperature,
         s.tickets = reinterpret_cast<uint32_t*>(ws->data_ptr()) + 22528;
       }
       // [24576, 28672): single-launch granules [B][2][nseg][2] x 16 B (B * nseg <= 256); [28672, 28928)
-      // per-row epochs; [28928, 29184) per-row exit tickets
-      if (ws->numel() >= 29184 && s.B <= 256) {
+      // per-row epochs
+      if (ws->numel() >= 28928 && s.B <= 256) {
         s.gran = reinterpret_cast<int32_t*>(ws->data_ptr()) + 24576;
         s.epoch = reinterpret_cast<uint32_t*>(ws->data_ptr()) + 28672;
-        s.done = reinterpret_cast<uint32_t*>(ws->data_ptr()) + 28928;
       }
     }
   }
