@@ -138,7 +138,12 @@ def main():
             r["weight_MB"] = round(nb / 1e6, 2)
             r["TB_per_s"] = round(nb / (span / n) / 1e6, 2)
         rows[k] = r
+    # on a real TP node each step adds its collectives as launches: the embedding all-reduce and the
+    # logits all-gather, plus one all-reduce per row-parallel GEMM unless it runs in the GEMM's epilogue
+    # (decode rows, VGATE_TP_FUSED_AR: gemm_epilogue.h epilogue_ar)
+    nl = len(m.layers)
     print(json.dumps({"timeline_step_us": summary["step_us"], "launches": summary["launches"],
+                      "collective_launches_per_real_step": {"fused_all_reduce": 2, "separate_all_reduce": 2 + 2 * nl},
                       "sum_gap_us": summary["sum_gap_us"], "per_kind": rows}), flush=True)
     if not a.sweep:
         return
