@@ -406,8 +406,10 @@ def test_sample_logprob():
 
 # ---------------------------------------------------------------- fused GEMM v2
 @pytest.mark.parametrize("M,N,K", [(8, 1536, 1536), (8, 1536, 8960), (40, 2048, 1536), (200, 512, 1024)])
-@pytest.mark.parametrize("splitk", [1, 4, 8])
+@pytest.mark.parametrize("splitk", [1, 2, 3, 4, 8])
 def test_gemm_splitk_residual_inplace(M, N, K, splitk):
+    """In-launch split-K: 2-4 slices of a decode tile meet through tagged granules (polled together
+    by the last slice), more through fp32 slabs + a ticket; repeated launches re-use both."""
     torch.manual_seed(10)
     x = torch.randn(M, K, device=DEV).bfloat16()
     w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
