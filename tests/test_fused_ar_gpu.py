@@ -43,7 +43,7 @@ def _dense(N, K, seed):
     return w, ops.Linear(w)
 
 
-@pytest.mark.parametrize("M", [1, 8, 16])
+@pytest.mark.parametrize("M", [1, 16])
 @pytest.mark.parametrize("N,K,waves,splitk,ntb", [
     (1024, 2048, 0, 0, 0),     # launcher heuristic
     (8192, 1024, 2, 1, 1),     # Llama-3-70B TP = 8 o_proj plan

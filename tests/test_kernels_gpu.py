@@ -351,7 +351,7 @@ def test_sample_top_p_frequent_rejection(B):
 @pytest.mark.parametrize("B", [1, 8, 16])
 def test_sample_single_launch_matches_pass_kernels(B):
     """The single-launch granule sampler (every block gathers its row's tagged partials itself) draws
-    exactly what the pass kernels draw — same Gumbel noise, same acceptance tests — over many
+    exactly what the pass kernels draw — same Gumbel noise, same acceptance tests — over 80
     consecutive launches (the per-row epoch advances each launch, so stale granules never match),
     for greedy / temperature / top-p / top-k rows, and under hipGraph replay."""
     torch.manual_seed(40 + B)
@@ -367,7 +367,7 @@ def test_sample_single_launch_matches_pass_kernels(B):
         tp[1] = 1.0  # plain temperature row
     seeds = torch.arange(B, device=DEV, dtype=torch.int64) * 7 + 3
     try:
-        for off in range(120):
+        for off in range(80):
             offs = torch.full((B,), off, dtype=torch.int64, device=DEV)
             C.set_sample_single(1)
             a = ops.sample(L, t, top_p=tp, top_k=tk, seeds=seeds, offsets=offs)
@@ -406,10 +406,10 @@ def test_sample_logprob():
 
 # ---------------------------------------------------------------- fused GEMM v2
 @pytest.mark.parametrize("M,N,K", [(8, 1536, 1536), (8, 1536, 8960), (40, 2048, 1536), (200, 512, 1024)])
-@pytest.mark.parametrize("splitk", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("splitk", [1, 3, 8])
 def test_gemm_splitk_residual_inplace(M, N, K, splitk):
-    """In-launch split-K: 2-4 slices of a decode tile meet through tagged granules (polled together
-    by the last slice), more through fp32 slabs + a ticket; repeated launches re-use both."""
+    """In-launch split-K through fp32 slabs + a ticket (the two-slice granule combine: the decode
+    plans / test_gemm_norm_splitk); repeated launches re-use the self-resetting tickets."""
     torch.manual_seed(10)
     x = torch.randn(M, K, device=DEV).bfloat16()
     w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
