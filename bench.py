@@ -4,7 +4,8 @@ prompts) at fixed client concurrency — the reference's published metric
 (6.47 req/s, p50 1.19 s, p99 1.53 s at concurrency 8, max_tokens 64).
 
 Every rank is one GPU running a full V-Gate stack (gateway + native engine) as a
-DP serving replica behind a real uvicorn HTTP server on 127.0.0.1; a closed-loop
+DP serving replica behind a real HTTP/1.1 server on 127.0.0.1 (vgate.api.server by
+default, ``--server uvicorn`` for uvicorn/h11); a closed-loop
 client in the same process keeps ``--concurrency`` requests in flight against it
 through the full path (HTTP -> security -> cache/dedup/admission -> engine ->
 JSON). One "step" = ``--requests-per-step`` requests (40 = the reference run).
@@ -19,7 +20,6 @@ from __future__ import annotations
 
 import argparse
 import asyncio
-import contextlib
 import json
 import os
 import subprocess
@@ -50,37 +50,58 @@ def pct(xs, p):
 
 
 async def run_load(port: int, n: int, concurrency: int, max_tokens: int, rank: int, start_idx: int,
-                   model: str = "Qwen/Qwen2.5-1.5B-Instruct", api_key: str | None = None):
-    import aiohttp
+                   model: str = "Qwen/Qwen2.5-1.5B-Instruct", api_key: str | None = None, client: str = "lean"):
+    """Closed loop: ``concurrency`` requests in flight, ``n`` in all (reference bench_load.py:160-212).
+    ``client`` "lean" = vgate.utils.http1 keep-alive pool (the default: the load generator shares
+    this process's event loop with the server, so its own per-request cost would be charged to
+    the server), "aiohttp" = the reference's client library."""
     lat, starts, fails, tokens = [], [], 0, 0
     sem = asyncio.Semaphore(concurrency)
-    url = f"http://127.0.0.1:{port}/v1/chat/completions"
-    conn = aiohttp.TCPConnector(limit=concurrency * 2)
-    timeout = aiohttp.ClientTimeout(total=300)
+    path = "/v1/chat/completions"
     headers = {"Authorization": f"Bearer {api_key}"} if api_key else None
-    async with aiohttp.ClientSession(connector=conn, timeout=timeout, headers=headers) as s:
-        async def one(i):
-            nonlocal fails, tokens
-            async with sem:
-                body = {"model": model,
-                        "messages": [{"role": "user", "content": make_prompt(rank, start_idx + i)}],
-                        "max_tokens": max_tokens}
-                t0 = time.perf_counter()
-                try:
-                    async with s.post(url, json=body) as r:
-                        data = await r.json()
-                        if r.status != 200:
-                            fails += 1
-                        else:
-                            tokens += data["usage"]["completion_tokens"]
-                except Exception:  # noqa: BLE001
-                    fails += 1
-                lat.append(time.perf_counter() - t0)
-                starts.append(t0 - t_run)
 
+    def body_of(i):
+        return {"model": model, "messages": [{"role": "user", "content": make_prompt(rank, start_idx + i)}],
+                "max_tokens": max_tokens}
+
+    if client == "aiohttp":
+        import aiohttp
+        conn = aiohttp.TCPConnector(limit=concurrency * 2)
+        session = aiohttp.ClientSession(connector=conn, timeout=aiohttp.ClientTimeout(total=300), headers=headers)
+
+        async def post(body):
+            async with session.post(f"http://127.0.0.1:{port}{path}", json=body) as r:
+                return r.status, await r.json()
+    else:
+        from vgate.utils.http1 import Http1Pool
+        session = Http1Pool("127.0.0.1", port, headers=headers)
+
+        async def post(body):
+            status, _, data = await session.request("POST", path, json.dumps(body).encode())
+            return status, json.loads(data)
+
+    async def one(i):
+        nonlocal fails, tokens
+        async with sem:
+            body = body_of(i)
+            t0 = time.perf_counter()
+            try:
+                status, data = await post(body)
+                if status != 200:
+                    fails += 1
+                else:
+                    tokens += data["usage"]["completion_tokens"]
+            except Exception:  # noqa: BLE001
+                fails += 1
+            lat.append(time.perf_counter() - t0)
+            starts.append(t0 - t_run)
+
+    try:
         t_run = t0 = time.perf_counter()
         await asyncio.gather(*(one(i) for i in range(n)))
         wall = time.perf_counter() - t0
+    finally:
+        await session.close()
     return lat, fails, tokens, wall, starts
 
 
@@ -99,9 +120,8 @@ def engine_model_cfg(args, rank: int, local: int) -> dict:
 
 async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=None, group=None):
     import torch
-    import uvicorn
-
     from vgate.api.app import create_app
+    from vgate.api.server import make_server
     from vgate.config import VGateConfig
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -119,11 +139,9 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
     )
     app = create_app(cfg)
     port = args.port + local
-    server = uvicorn.Server(uvicorn.Config(app, host="127.0.0.1", port=port, log_level="warning",
-                                           access_log=False, lifespan="on"))
     # the in-process server is stopped by this script, never by a signal: leave the process's
     # handlers alone (a profiler's native SIGINT/SIGTERM handler is not restorable from Python)
-    server.capture_signals = contextlib.nullcontext
+    server = make_server(app, "127.0.0.1", port, args.server)
     srv_task = asyncio.create_task(server.serve())
     t_boot = time.perf_counter()
     while not server.started:
@@ -147,12 +165,13 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
 
     async def load(n, start_idx):
         if client is None:  # default: the load loop shares this process's event loop / GIL
-            return await run_load(port, n, args.concurrency, args.max_tokens, rank, start_idx, args.model, key)
+            return await run_load(port, n, args.concurrency, args.max_tokens, rank, start_idx, args.model, key,
+                                  args.client)
         # the load generator is its own process (as the reference's bench_load.py against a
         # running server): one command line in, one result line out; the server keeps serving
         # on this event loop while the reply is awaited off-loop
         cmd = {"port": port, "n": n, "concurrency": args.concurrency, "max_tokens": args.max_tokens,
-               "rank": rank, "start_idx": start_idx, "model": args.model, "api_key": key}
+               "rank": rank, "start_idx": start_idx, "model": args.model, "api_key": key, "client": args.client}
         client.stdin.write(json.dumps(cmd) + "\n")
         client.stdin.flush()
         line = await asyncio.get_running_loop().run_in_executor(None, client.stdout.readline)
@@ -207,9 +226,13 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
     snap = eng.backend.stats() if hasattr(eng.backend, "stats") else {}
     # timed-region forensics (p99): eager (graph-miss) steps and captures INSIDE the timed region
     snap = dict(snap)
-    for k in ("graph_misses_eager", "graph_captures", "steps", "graph_hits", "idle_ms", "prefill_steps"):
+    for k in ("graph_misses_eager", "graph_captures", "steps", "graph_hits", "idle_ms", "prefill_steps", "waves",
+              "wave_requests"):
         if k in snap and k in snap0:
             snap[f"timed_{k}"] = snap[k] - snap0[k]
+    if "wave_sum_ms" in snap and "wave_sum_ms" in snap0:
+        nw = max(1, snap.get("timed_waves", 0))
+        snap["wave_breakdown_ms"] = [round((a - b) / nw, 3) for a, b in zip(snap["wave_sum_ms"], snap0["wave_sum_ms"])]
     server.should_exit = True
     await srv_task
     slow = sorted(zip(lat, starts), reverse=True)[:8]
@@ -236,7 +259,8 @@ def client_loop():
     for line in sys.stdin:
         c = json.loads(line)
         lat, fails, tokens, wall, starts = asyncio.run(run_load(c["port"], c["n"], c["concurrency"], c["max_tokens"],
-                                                        c["rank"], c["start_idx"], c["model"], c["api_key"]))
+                                                        c["rank"], c["start_idx"], c["model"], c["api_key"],
+                                                        c.get("client", "lean")))
         sys.stdout.write(json.dumps({"lat": lat, "fails": fails, "tokens": tokens, "wall": wall, "starts": starts}) + "\n")
         sys.stdout.flush()
 
@@ -262,6 +286,10 @@ def main():
                     help="run the load loop in a separate client process (default: in the server process; "
                          "measured slower on the 1-GPU box: 68 vs 81 req/s, profiles/r1_bench_client_modes.log)")
     ap.add_argument("--client-proc", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--server", default="vgate", choices=["vgate", "uvicorn"],
+                    help="HTTP server: vgate.api.server (default) or uvicorn (h11)")
+    ap.add_argument("--client", default="lean", choices=["lean", "aiohttp"],
+                    help="load-generator HTTP client: vgate.utils.http1 (default) or aiohttp")
     ap.add_argument("--switch-interval-us", type=float,
                     default=float(os.environ.get("VGATE_SWITCH_INTERVAL_US", "0")),
                     help="sys.setswitchinterval for the server process (0 = Python default 5 ms)")
@@ -332,7 +360,8 @@ def main():
             "data": f"synthetic unique prompts, random-init weights ({model_name} architecture)",
             "config": {"model": model_name, "quantization": args.quantization or "none",
                        "security_rate_limiter": bool(args.security),
-                       "load_client": "separate process" if args.client_process else "in-process",
+                       "load_client": ("separate process" if args.client_process else "in-process") + f" ({args.client})",
+                       "http_server": args.server,
                        "engine_core": "separate process" if args.engine_process else "in-process", "global_batch": args.concurrency * dp,
                        "seq_len": args.max_tokens,
                        "parallelism": f"dp{dp}" if args.tp == 1 else f"dp{dp}xtp{args.tp}",
@@ -353,6 +382,11 @@ def main():
             # that start together, so every wave boundary waits for the next c requests' HTTP path
             "timed_engine_idle_ms": allr[0]["engine"].get("timed_idle_ms"),
             "timed_prefill_steps": allr[0]["engine"].get("timed_prefill_steps"),
+            # per idle -> busy transition: [idle start -> first arrival, first -> last arrival of the
+            # wave, last arrival -> step start] in ms, and the requests per transition
+            "wave_breakdown_ms": allr[0]["engine"].get("wave_breakdown_ms"),
+            "timed_waves": allr[0]["engine"].get("timed_waves"),
+            "timed_wave_requests": allr[0]["engine"].get("timed_wave_requests"),
             "timed_eager_steps": allr[0]["engine"].get("timed_graph_misses_eager"),
             "timed_graph_captures": allr[0]["engine"].get("timed_graph_captures"),
             "max_gpu_step_ms": allr[0]["engine"].get("max_gpu_step_ms"),

@@ -14,7 +14,6 @@ from __future__ import annotations
 
 import argparse
 import asyncio
-import contextlib
 import cProfile
 import json
 import os
@@ -31,9 +30,8 @@ import bench  # noqa: E402
 
 
 async def main_async(a):
-    import uvicorn
-
     from vgate.api.app import create_app
+    from vgate.api.server import make_server
     from vgate.config import VGateConfig
 
     cfg = VGateConfig(role="gateway", batch={"max_batch_size": a.concurrency}, cache={"enabled": True, "maxsize": 1000},
@@ -42,27 +40,27 @@ async def main_async(a):
                                 "api_keys": [{"key": bench.BENCH_KEY, "name": "bench", "rate_limit": 10_000_000}],
                                 "rate_limiting": {"enabled": True, "window_seconds": 60}})
     app = create_app(cfg)
-    server = uvicorn.Server(uvicorn.Config(app, host="127.0.0.1", port=a.port, log_level="warning", access_log=False,
-                                           lifespan="on"))
-    server.capture_signals = contextlib.nullcontext
+    server = make_server(app, "127.0.0.1", a.port, a.server)
     task = asyncio.create_task(server.serve())
     while not server.started:
         await asyncio.sleep(0.05)
     key = bench.BENCH_KEY if a.security else None
     bench.t_run = time.perf_counter()
-    await bench.run_load(a.port, 200, a.concurrency, 64, 0, 0, api_key=key)  # warm-up
+    await bench.run_load(a.port, 200, a.concurrency, 64, 0, 0, api_key=key, client=a.client)  # warm-up
     prof = cProfile.Profile() if a.profile else None
     bench.t_run = time.perf_counter()
     t0 = time.perf_counter()
     if prof:
         prof.enable()
-    lat, fails, _, _ = (await bench.run_load(a.port, a.requests, a.concurrency, 64, 0, 10_000_000, api_key=key))[:4]
+    lat, fails, _, _ = (await bench.run_load(a.port, a.requests, a.concurrency, 64, 0, 10_000_000, api_key=key,
+                                                client=a.client))[:4]
     if prof:
         prof.disable()
     wall = time.perf_counter() - t0
     server.should_exit = True
     await task
     print(json.dumps({"requests": a.requests, "concurrency": a.concurrency, "security": bool(a.security),
+                      "server": a.server, "client": a.client,
                       "req_per_s": round(a.requests / wall, 1), "us_per_request": round(1e6 * wall / a.requests, 1),
                       "p50_ms": round(1e3 * bench.pct(lat, 50), 3), "fails": fails}), flush=True)
     if prof:
@@ -76,6 +74,8 @@ def main():
     ap.add_argument("--concurrency", type=int, default=8)
     ap.add_argument("--port", type=int, default=18300)
     ap.add_argument("--security", action="store_true")
+    ap.add_argument("--server", default="vgate", choices=["vgate", "uvicorn"])
+    ap.add_argument("--client", default="lean", choices=["lean", "aiohttp"])
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--top", type=int, default=35)
     a = ap.parse_args()

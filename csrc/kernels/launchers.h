@@ -213,26 +213,23 @@ struct SampleArgs {
   const int64_t* offsets;    // [B] per-row philox offset (e.g. generated-token count)
   int32_t* out;              // [B]
   float* out_logprob;        // [B] or null
-  // segmented (multi-block per row) mode; null -> one block per row
-  float* parts;              // [B * nseg][8] partials (B * nseg <= 256)
-  uint32_t* sync;            // [2 * B] zero-initialised, self-resetting row counters
   unsigned long long* tl;    // launch timeline slot (set by the launcher), or null
-  // pass-kernel mode (sampling.hip sample_pass0_kernel): per-row state [B][8 words] and
-  // zero-initialised, self-resetting arrival tickets [B]; null -> in-launch meetings only
-  struct RowState* state = nullptr;
-  uint32_t* tickets = nullptr;
-  // single-launch mode (sampling.hip sample_gran_kernel): tagged partial granules [B][2][nseg][2] uint4
-  // and per-row epochs [B] (zero-initialised, self-advancing), and the sticky fault word (bit 16: a row
-  // meeting gave up); null -> the pass kernels
+  // segmented mode (sampling.hip sample_gran_kernel, B <= SAMPLE_GRAN_ROWS): tagged partial granules,
+  // a fixed region of SAMPLE_GRAN_ROW uint4 per row, and per-row epochs [B] (zero-initialised,
+  // self-advancing); null -> one block per row. fault: sticky word (bit 16: a row's wait gave up)
   void* gran = nullptr;
   uint32_t* epoch = nullptr;
   uint32_t* fault = nullptr;
 };
+// sampler workspace (int32 words): [0, SAMPLE_WS_GRAN) per-row epochs, then the granule regions
+constexpr int SAMPLE_GRAN_SEGS = 64;                        // max segments per row
+constexpr int SAMPLE_GRAN_ROWS = 128;                       // rows of the segmented mode (nseg >= 2)
+constexpr int SAMPLE_GRAN_ROW = 2 * SAMPLE_GRAN_SEGS * 2;   // uint4 per row: [parity][segment][2]
+constexpr int SAMPLE_WS_GRAN = 256;                         // int32 offset of the granules (16-B aligned)
+constexpr int SAMPLE_WS_WORDS = SAMPLE_WS_GRAN + SAMPLE_GRAN_ROWS * SAMPLE_GRAN_ROW * 4;
 void launch_sample(const SampleArgs& s, hipStream_t st);
-void set_sample_single(int on);  // 1 (default): the single-launch granule sampler when its workspace is given
 int sample_segments(int B, int V);
-void set_sample_nseg(int n);  // cap on segments per row (0 = B*NSEG <= 1024 bound only)
-void set_sample_round_launches(int n);  // rejection rounds run as launches (0 = pass 0 only)
+void set_sample_nseg(int n);  // cap on segments per row, 1..SAMPLE_GRAN_SEGS (1 = one block per row)
 
 // Custom one-shot all-reduce over IPC-mapped peer buffers (xGMI).
 struct AllReduceArgs {

@@ -3,10 +3,9 @@
 //
 // Parallel layout: each row is split into NSEG segments, one 256-thread block per
 // (segment, row), so a batch-8 step spreads its 8 x 600 KB of logits over 256 CUs
-// instead of 8. The blocks of a row meet at a per-row arrival counter after each
-// pass (sc1 partial stores -> drain -> counter; sc1 loads; NSEG is chosen on the host so that
-// B * NSEG <= 256 blocks, all co-resident, and every spin has a give-up bound).
-// With NSEG == 1 (large batches) a row is one block and the "meeting" is a barrier.
+// instead of 8. After each pass the blocks of a row exchange tagged partials (sample_gran_kernel:
+// NSEG is chosen on the host so that B * NSEG <= 256 blocks, all co-resident, and every wait has a
+// give-up bound). With NSEG == 1 (large batches) a row is one block (sample_row_kernel).
 //
 // Exact sampling, no sort, no histogram atomics:
 //   pass 0: per segment (max, Z = sum e^{(x-max)/T}, argmax) and the Gumbel-max draw
@@ -86,34 +85,6 @@ __device__ __forceinline__ void block_reduce_acc(Acc& a, float c, Acc* red) {
   }
 }
 
-// Per-row meeting point of the NSEG blocks after pass `gen` (1-based).
-// Returns false if the wait gave up (caller falls back to the argmax).
-// Arrive with one agent-scope atomic add; poll the counter with relaxed sc1 loads (s_sleep
-// between polls: a read-modify-write poll from every block of a row queues behind the
-// arrivals at the memory-side atomic unit and was 4x slower at 1024 blocks); every partial is
-// stored and loaded sc1, so no cache-wide acquire is needed. The partials live in two
-// buffers by pass parity (see parts_even / parts_odd): without that, a fast block's NEXT-pass
-// partial could overwrite one a slow block was still merging, the blocks of a row then took
-// different accept / reject decisions and the ones left waiting spun to the give-up bound
-// (the 60-470 ms sampler launches of profiles/r2_bench1_kernels.txt).
-__device__ __forceinline__ bool row_meet(uint32_t* ctr, uint32_t target, int* ok_flag) {
-  drain_stores();  // this block's sc1 partial stores are device-visible before it arrives
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-    int ok = 1;
-    uint32_t spins = 0;
-    while (v < target) {
-      __builtin_amdgcn_s_sleep(1);
-      v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (++spins > (1u << 22)) { ok = 0; break; }  // bounded: never hang the GPU
-    }
-    *ok_flag = ok;
-  }
-  __syncthreads();
-  return *ok_flag != 0;
-}
-
 // Per-row sampling parameters (row-uniform).
 struct RowParams {
   float T, c, cn, topp;
@@ -186,200 +157,39 @@ __device__ __forceinline__ void sweep_range(const float4* x4, int v_lo, int v_hi
   }
 }
 
-// ---- pass kernels: a kernel boundary instead of an in-launch meeting ----
-// The segmented kernel's meetings (every block of a row arrives, then polls until the last
-// one has) cost ~0.5 us per arriving block (sampler_probe: 18 us greedy / 35 us top-p at 32
-// segments, 143 us at 128). Here a pass is its own launch: each block publishes its partial
-// (sc1 stores, drained) and takes one arrival ticket; the LAST block of the row — told by the
-// value its atomic returned, nobody waits — merges the partials in fixed segment order and
-// decides. The decision travels to the next launch in a per-row state word (kernel boundary).
-//   sample_pass0_kernel: pass 0; greedy / plain-temperature rows are final here, top-k / top-p
-//                        rows leave their Gumbel candidate pending;
-//   sample_round_kernel: acceptance test of the pending candidate (one rejection round);
-//   sample_kernel(resume): rows still pending after the round launches continue with the
-//                        in-launch rounds (rare).
-struct RowState {
-  float mx, z;  // pass-0 row max and Z
-  int amx;      // pass-0 argmax (fallback)
-  int j;        // pending candidate
-  int status;   // 1 = pending acceptance of j, 0 = out[row] written
-  int pad[3];
-};
-
-// publish this block's merged Acc (thread 0 holds it) and take the row's ticket; returns true in
-// the row's last-arriving block, whose thread 0 then holds the fixed-order merge of all segments
-__device__ __forceinline__ bool publish_last(Acc& acc, SamplePart* parts, uint32_t* ticket, int seg, int nseg, float c,
-                                             Acc* red, int* flag) {
-  if (threadIdx.x == 0) {
-    float* w = reinterpret_cast<float*>(parts + seg);
-    st_sc1(w + 0, acc.mx); st_sc1(w + 1, acc.z); st_sc1(w + 2, __int_as_float(acc.amx));
-    st_sc1(w + 3, acc.gk); st_sc1(w + 4, __int_as_float(acc.gi)); st_sc1(w + 5, acc.cnt);
-    st_sc1(w + 6, acc.q);
-    drain_stores();
-    const uint32_t old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == (uint32_t)(nseg - 1);
-    if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = last;
-  }
-  __syncthreads();
-  if (!*flag) return false;
-  Acc r = acc_init();
-  if (threadIdx.x < nseg) {
-    const float* w = reinterpret_cast<const float*>(parts + threadIdx.x);
-    r = Acc{ld_sc1(w + 0), ld_sc1(w + 1), __float_as_int(ld_sc1(w + 2)), ld_sc1(w + 3),
-            __float_as_int(ld_sc1(w + 4)), ld_sc1(w + 5), ld_sc1(w + 6)};
-  }
-  block_reduce_acc(r, c, red);
-  if (threadIdx.x == 0) acc = r;
-  return true;
-}
-
 __device__ __forceinline__ void finish_row(const SampleArgs& a, int row, int chosen, float mx, float z, float c) {
   a.out[row] = chosen;
   if (a.out_logprob) a.out_logprob[row] = ((a.logits[(size_t)row * a.ldl + chosen] - mx) * c - log2f(z)) / LOG2E_S;
 }
 
-template <int NT>
-__global__ __launch_bounds__(NT) void sample_pass0_kernel(SampleArgs a) {
-  TLScope tl_scope(a.tl);
-  __shared__ Acc red[NT / 64];
-  __shared__ int flag;
-  const int seg = blockIdx.x, nseg = gridDim.x, row = blockIdx.y;
-  const int V4 = a.V >> 2;
-  const int v_lo = (int)(((long long)V4 * seg) / nseg), v_hi = (int)(((long long)V4 * (seg + 1)) / nseg);
-  const RowParams rp = row_params(a, row);
-  Acc acc = acc_init();
-  sweep_range(reinterpret_cast<const float4*>(a.logits + (size_t)row * a.ldl), v_lo, v_hi, 0, 0.f, 0.f, 0u, rp, acc);
-  block_reduce_acc(acc, rp.c, red);
-  SamplePart* parts = reinterpret_cast<SamplePart*>(a.parts) + (size_t)row * nseg;
-  if (!publish_last(acc, parts, a.tickets + row, seg, nseg, rp.c, red, &flag)) return;
-  if (threadIdx.x == 0) {
-    RowState& st = a.state[row];
-    st.mx = acc.mx; st.z = acc.z; st.amx = acc.amx;
-    if (!rp.greedy && (rp.use_k || rp.use_p) && acc.gi >= 0) {
-      st.j = acc.gi;
-      st.status = 1;
-    } else {
-      st.status = 0;
-      finish_row(a, row, rp.greedy || acc.gi < 0 ? acc.amx : acc.gi, acc.mx, acc.z, rp.c);
-    }
-  }
-}
-
-template <int NT>
-__global__ __launch_bounds__(NT) void sample_round_kernel(SampleArgs a, uint32_t round) {
-  TLScope tl_scope(a.tl);
-  __shared__ Acc red[NT / 64];
-  __shared__ int flag;
-  const int seg = blockIdx.x, nseg = gridDim.x, row = blockIdx.y;
-  const RowState st = a.state[row];
-  if (st.status != 1) return;  // row-uniform
-  const int V4 = a.V >> 2;
-  const int v_lo = (int)(((long long)V4 * seg) / nseg), v_hi = (int)(((long long)V4 * (seg + 1)) / nseg);
-  const RowParams rp = row_params(a, row);
-  const float* x = a.logits + (size_t)row * a.ldl;
-  const float xj = x[st.j];
-  Acc acc = acc_init();
-  sweep_range(reinterpret_cast<const float4*>(x), v_lo, v_hi, 1, xj, st.mx, round, rp, acc);
-  block_reduce_acc(acc, rp.c, red);
-  SamplePart* parts = reinterpret_cast<SamplePart*>(a.parts) + (size_t)row * nseg;
-  if (!publish_last(acc, parts, a.tickets + row, seg, nseg, rp.c, red, &flag)) return;
-  if (threadIdx.x == 0) {
-    RowState& s = a.state[row];
-    const bool ok_k = !rp.use_k || acc.cnt < (float)rp.topk;
-    const bool ok_p = !rp.use_p || acc.q < rp.topp * st.z;
-    if (ok_k && ok_p) {
-      s.status = 0;
-      finish_row(a, row, st.j, st.mx, st.z, rp.c);
-    } else if (acc.gi < 0) {
-      s.status = 0;
-      finish_row(a, row, st.amx, st.mx, st.z, rp.c);
-    } else {
-      s.j = acc.gi;  // next candidate, drawn from {x > x_j}
-    }
-  }
-}
-
-// resume > 0: only rows the pass kernels left pending (state), from rejection round `resume` on
-__global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a, uint32_t resume) {
+// ---- one block per row (NSEG == 1: batches above SAMPLE_MAX_BLOCKS / 2 rows, or no workspace) ----
+// Every pass sweeps the whole row and ends at a block barrier; same passes, noise and acceptance
+// tests as the segmented kernel below.
+__global__ __launch_bounds__(SAMPLE_THREADS) void sample_row_kernel(SampleArgs a) {
   TLScope tl_scope(a.tl);
   __shared__ Acc red[SAMPLE_THREADS / 64];
   __shared__ Acc merged;
-  __shared__ int ok_flag;
-  const int seg = blockIdx.x, nseg = gridDim.x;
-  const int row = blockIdx.y;
+  const int row = blockIdx.y, tid = threadIdx.x;
   const int V4 = a.V >> 2;  // host guarantees V % 4 == 0 and 16-B aligned rows
-  const int v_lo = (int)(((long long)V4 * seg) / nseg), v_hi = (int)(((long long)V4 * (seg + 1)) / nseg);
   const float* x = a.logits + (size_t)row * a.ldl;
   const float4* x4 = reinterpret_cast<const float4*>(x);
-  const int tid = threadIdx.x;
-  RowState st{};
-  if (resume > 0) {
-    st = a.state[row];
-    if (st.status != 1) return;  // row-uniform: decided by the pass kernels
-  }
   const RowParams rp = row_params(a, row);
   const float c = rp.c;
-  // two partial buffers by pass parity: a block that has passed meet g may already publish
-  // pass g+1 while a slower block of its row is still reading pass g's partials; it cannot
-  // reach pass g+2 before every block has arrived at meet g+1, i.e. finished reading g
-  SamplePart* parts_even = reinterpret_cast<SamplePart*>(a.parts) + (size_t)row * nseg;
-  SamplePart* parts_odd = parts_even + (size_t)SAMPLE_MAX_BLOCKS;
-  uint32_t* ctr = a.sync ? a.sync + row : nullptr;
-
-  // publish this block's partial and merge all segments of the row (fixed order)
-  auto exchange = [&](Acc& acc, uint32_t gen) -> bool {
+  auto pass = [&](int mode, float xj, float rmx, uint32_t round) {
+    Acc acc = acc_init();
+    sweep_range(x4, 0, V4, mode, xj, rmx, round, rp, acc);
     block_reduce_acc(acc, c, red);
-    bool ok = true;
-    if (nseg > 1) {
-      if (tid == 0) {  // device-coherent (sc1) stores: read by the row's other blocks in-launch
-        SamplePart* parts = (gen & 1) ? parts_odd : parts_even;
-        float* w = reinterpret_cast<float*>(parts + seg);
-        st_sc1(w + 0, acc.mx); st_sc1(w + 1, acc.z); st_sc1(w + 2, __int_as_float(acc.amx));
-        st_sc1(w + 3, acc.gk); st_sc1(w + 4, __int_as_float(acc.gi)); st_sc1(w + 5, acc.cnt);
-        st_sc1(w + 6, acc.q);
-      }
-      ok = row_meet(ctr, gen * (uint32_t)nseg, &ok_flag);
-      if (ok) {  // all partials loaded at once (one per thread), then a fixed-shape tree
-        Acc r = acc_init();
-        if (tid < nseg) {
-          const SamplePart* parts = (gen & 1) ? parts_odd : parts_even;
-          const float* w = reinterpret_cast<const float*>(parts + tid);
-          r = Acc{ld_sc1(w + 0), ld_sc1(w + 1), __float_as_int(ld_sc1(w + 2)), ld_sc1(w + 3),
-                  __float_as_int(ld_sc1(w + 4)), ld_sc1(w + 5), ld_sc1(w + 6)};
-        }
-        block_reduce_acc(r, c, red);
-        if (tid == 0) acc = r;
-      }
-    }
-    __syncthreads();
     if (tid == 0) merged = acc;
     __syncthreads();
-    return ok;
   };
-
-  float mx, z;
-  int chosen, j;
-  uint32_t gen = 0, round0 = 1;
-  bool ok = true;
-  if (resume == 0) {
-    Acc acc = acc_init();
-    sweep_range(x4, v_lo, v_hi, 0, 0.f, 0.f, 0u, rp, acc);
-    ok = exchange(acc, ++gen);
-    mx = merged.mx; z = merged.z; chosen = merged.amx; j = merged.gi;
-  } else {
-    mx = st.mx; z = st.z; chosen = st.amx; j = st.j;
-    round0 = resume;
-  }
-  if (ok && !rp.greedy) {
+  pass(0, 0.f, 0.f, 0u);
+  const float mx = merged.mx, z = merged.z;
+  int chosen = merged.amx, j = merged.gi;
+  if (!rp.greedy) {
     if (rp.use_k || rp.use_p) {
       const float pmass = rp.topp * z;
-      for (uint32_t round = round0; round <= 64 && j >= 0; ++round) {
-        const float xj = x[j];
-        Acc acc = acc_init();
-        sweep_range(x4, v_lo, v_hi, 1, xj, mx, round, rp, acc);
-        ok = exchange(acc, ++gen);
-        if (!ok) { j = -1; break; }
+      for (uint32_t round = 1; round <= SAMPLE_MAX_ROUNDS && j >= 0; ++round) {
+        pass(1, x[j], mx, round);
         const bool ok_k = !rp.use_k || merged.cnt < (float)rp.topk;
         const bool ok_p = !rp.use_p || merged.q < pmass;
         if (ok_k && ok_p) break;
@@ -388,19 +198,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a, ui
     }
     if (j >= 0) chosen = j;
   }
-  if (seg == 0 && tid == 0) {
-    finish_row(a, row, chosen, mx, z, c);
-    if (resume > 0) a.state[row].status = 0;
-  }
-  // self-reset for the next launch: the last block of the row to leave zeroes the counters
-  if (nseg > 1 && gen > 0 && tid == 0) {
-    uint32_t* done = a.sync + a.B;
-    const uint32_t d = __hip_atomic_fetch_add(done + row, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (d == (uint32_t)nseg - 1) {
-      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(done + row, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  if (tid == 0) finish_row(a, row, chosen, mx, z, c);
 }
 
 // ---- single launch: tagged granules instead of tickets / counters ----
@@ -414,6 +212,10 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a, ui
 // by the row's segment 0 at its exit, see the end of the kernel), so a granule of an earlier launch
 // never matches; granules alternate two buffers by pass parity (a block reaches pass g + 2,
 // rewriting parity g, only after every block of the row published g + 1, i.e. finished reading g).
+// Each row owns a FIXED granule region of SAMPLE_GRAN_SEGS segments whatever the launch's (B, nseg):
+// a slot is only ever written by its own row, under that row's monotonic epoch. (A layout that moved
+// with nseg let row r read row r' < r's leftovers from a launch of another batch size whose tag
+// happened to equal r's current one — round-4 ADVICE.)
 // Every wait is bounded: a give-up sets fault bit 16 (the engine fails the step) and the row
 // falls back to its argmax. B x nseg <= 256 blocks: all co-resident.
 __device__ __forceinline__ void gran_publish(uint4* g, const Acc& a, int mode, uint32_t tag) {
@@ -478,14 +280,14 @@ __global__ __launch_bounds__(NT) void sample_gran_kernel(SampleArgs a) {
   const RowParams rp = row_params(a, row);
   const float c = rp.c;
   const uint32_t ep = __builtin_amdgcn_readfirstlane(__float_as_uint(ld_sc1(reinterpret_cast<const float*>(a.epoch + row))));
-  uint4* rowg = reinterpret_cast<uint4*>(a.gran) + (size_t)row * 2 * nseg * 2;  // [parity][nseg][2]
+  uint4* rowg = reinterpret_cast<uint4*>(a.gran) + (size_t)row * SAMPLE_GRAN_ROW;  // [parity][SEGS][2]
   // one pass: sweep, block merge, publish, gather every segment's granules, share the row merge
   auto pass = [&](int mode, float xj, float rmx, uint32_t round, uint32_t gen) -> bool {
     Acc acc = acc_init();
     sweep_range(x4, v_lo, v_hi, mode, xj, rmx, round, rp, acc);
     block_reduce_acc(acc, c, red);
     const uint32_t tag = (ep << 6) | gen;
-    uint4* pg = rowg + (size_t)(gen & 1) * nseg * 2;
+    uint4* pg = rowg + (size_t)(gen & 1) * SAMPLE_GRAN_SEGS * 2;
     if (tid == 0) {
       gran_publish(pg + 2 * seg, acc, mode, tag);
     }
@@ -507,7 +309,7 @@ __global__ __launch_bounds__(NT) void sample_gran_kernel(SampleArgs a) {
   if (ok && !rp.greedy) {
     if (rp.use_k || rp.use_p) {
       const float pmass = rp.topp * z;
-      for (uint32_t round = 1; round <= 60 && j >= 0; ++round) {
+      for (uint32_t round = 1; round <= SAMPLE_MAX_ROUNDS && j >= 0; ++round) {
         ok = pass(1, x[j], mx, round, ++gen);
         if (!ok) { j = -1; break; }
         const bool ok_k = !rp.use_k || merged.cnt < (float)rp.topk;
@@ -527,55 +329,30 @@ __global__ __launch_bounds__(NT) void sample_gran_kernel(SampleArgs a) {
   }
 }
 
-int g_sample_single = 1;
-void set_sample_single(int on) { g_sample_single = on; }
-
-int g_sample_nseg = 64;  // segments per row cap (set_sample_nseg; measured: benchmarks/sampler_stress.py)
-void set_sample_nseg(int n) { g_sample_nseg = n; }
+int g_sample_nseg = SAMPLE_GRAN_SEGS;  // segments per row cap (set_sample_nseg; benchmarks/sampler_stress.py)
+void set_sample_nseg(int n) { g_sample_nseg = n < 1 ? 1 : (n > SAMPLE_GRAN_SEGS ? SAMPLE_GRAN_SEGS : n); }
 
 int sample_segments(int B, int V) {
   const int V4 = V >> 2;
-  const int force = g_sample_nseg;
   int nseg = SAMPLE_MAX_BLOCKS / (B > 0 ? B : 1);
-  if (force > 0 && force < nseg) nseg = force;
-  if (nseg > SAMPLE_THREADS) nseg = SAMPLE_THREADS;  // the merge loads one partial per thread
+  if (nseg > g_sample_nseg) nseg = g_sample_nseg;
   const int cap = V4 / 256;  // >= 1024 logits per segment
   if (nseg > cap) nseg = cap;
   return nseg < 1 ? 1 : nseg;
 }
 
-int g_sample_round_launches = 2;  // rejection rounds as their own launches before the in-launch fallback
-void set_sample_round_launches(int n) { g_sample_round_launches = n < -1 ? -1 : n; }  // -1: meetings only
-
 void launch_sample(const SampleArgs& s, hipStream_t st) {
   if (s.B <= 0) return;
-  int nseg = sample_segments(s.B, s.V);
-  if (s.parts == nullptr || s.sync == nullptr) nseg = 1;
+  const int nseg = sample_segments(s.B, s.V);
   SampleArgs a = s;
-  if (nseg > 1 && nseg <= 64 && g_sample_single && s.gran != nullptr && s.epoch != nullptr) {
+  if (nseg > 1 && s.gran != nullptr && s.epoch != nullptr && s.B <= SAMPLE_GRAN_ROWS) {
     a.tl = tl_take("sample_gran", nseg * s.B);
     // 256 threads per block: 512 / 1024 measured no faster / slower (profiles/r4_sampler_single_launch.log)
     hipLaunchKernelGGL(sample_gran_kernel<256>, dim3(nseg, s.B), dim3(256), 0, st, a);
     return;
   }
-  if (nseg > 1 && s.state != nullptr && s.tickets != nullptr && g_sample_round_launches >= 0) {
-    // pass 0 and the first rejection rounds as launches (last-arriver merges, no meetings),
-    // then the in-launch rounds for rows still pending
-    // pass block width 256: 512 / 1024 threads measured no faster — a pass is bound by its memory
-    // round trips, not the sweep's Philox + log work (profiles/r2_sampler_nseg_sweep.log)
-    a.tl = tl_take("sample_pass0", nseg * s.B);
-    hipLaunchKernelGGL(sample_pass0_kernel<256>, dim3(nseg, s.B), dim3(256), 0, st, a);
-    for (int r = 1; r <= g_sample_round_launches; ++r) {
-      a.tl = tl_take("sample_round", nseg * s.B);
-      hipLaunchKernelGGL(sample_round_kernel<256>, dim3(nseg, s.B), dim3(256), 0, st, a, (uint32_t)r);
-    }
-    a.tl = tl_take("sample_resume", nseg * s.B);
-    hipLaunchKernelGGL(sample_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, a,
-                       (uint32_t)(g_sample_round_launches + 1));
-    return;
-  }
-  a.tl = tl_take("sample", nseg * s.B);
-  hipLaunchKernelGGL(sample_kernel, dim3(nseg, s.B), dim3(SAMPLE_THREADS), 0, st, a, 0u);
+  a.tl = tl_take("sample", s.B);
+  hipLaunchKernelGGL(sample_row_kernel, dim3(1, s.B), dim3(SAMPLE_THREADS), 0, st, a);
 }
 
 }  // namespace vgate

@@ -36,17 +36,8 @@ constexpr int SAMPLE_THREADS = 256;
 // nseg 16 / 32 / 64 / 128 -> 38.7 / 35.2 / 55.8 / 143 us for 8 rows at top-p 0.9,
 // profiles/r2_sampler_nseg_sweep.log)
 constexpr int SAMPLE_MAX_BLOCKS = 256;
+constexpr int SAMPLE_MAX_ROUNDS = 60;  // rejection rounds before the row keeps its last candidate / argmax
 constexpr float LOG2E_S = 1.4426950408889634f;
-
-// Per-(row, segment) partial, 8 words.
-struct SamplePart {
-  float mx, z;      // segment max and sum e^{(x - mx) c}
-  int amx;          // segment argmax (lowest index on ties)
-  float gk;         // best Gumbel key
-  int gi;           // its index (-1 = none)
-  float cnt, q;     // acceptance statistics for the current candidate
-  int pad;
-};
 
 struct Acc {  // POD (lives in LDS too); start from acc_init()
   float mx, z;

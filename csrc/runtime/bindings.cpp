@@ -406,23 +406,12 @@ void sample(const Tensor& logits, const c10::optional<Tensor>& temperature,
   s.out = reinterpret_cast<int32_t*>(out.data_ptr());
   s.out_logprob = const_cast<float*>(static_cast<const float*>(fp(out_logprob, torch::kFloat32)));
   if (ws.has_value() && ws->defined()) {
-    // [0, 512): row counters (2 per row, B <= 256 in segmented mode); [512, ...): partials
-    // (8 words per block, B * nseg <= 256 blocks (1024 allowed), two buffers by pass parity)
-    // [20480, 22528): per-row pass state (8 words, B <= 256); [22528, 22784): pass tickets
-    TORCH_CHECK(ws->scalar_type() == torch::kInt32 && ws->is_cuda() && ws->numel() >= 16896, "sample: ws must be int32[>=16896]");
-    if (vgate::sample_segments(s.B, s.V) > 1) {
-      s.sync = reinterpret_cast<uint32_t*>(ws->data_ptr());
-      s.parts = reinterpret_cast<float*>(ws->data_ptr()) + 512;
-      if (ws->numel() >= 22784 && s.B <= 256) {
-        s.state = reinterpret_cast<vgate::RowState*>(reinterpret_cast<int32_t*>(ws->data_ptr()) + 20480);
-        s.tickets = reinterpret_cast<uint32_t*>(ws->data_ptr()) + 22528;
-      }
-      // [24576, 28672): single-launch granules [B][2][nseg][2] x 16 B (B * nseg <= 256); [28672, 28928)
-      // per-row epochs
-      if (ws->numel() >= 28928 && s.B <= 256) {
-        s.gran = reinterpret_cast<int32_t*>(ws->data_ptr()) + 24576;
-        s.epoch = reinterpret_cast<uint32_t*>(ws->data_ptr()) + 28672;
-      }
+    // per-row epochs, then one fixed granule region per row (launchers.h SAMPLE_WS_*)
+    TORCH_CHECK(ws->scalar_type() == torch::kInt32 && ws->is_cuda() && ws->numel() >= vgate::SAMPLE_WS_WORDS,
+                "sample: ws must be int32[>=", vgate::SAMPLE_WS_WORDS, "]");
+    if (s.B <= vgate::SAMPLE_GRAN_ROWS) {
+      s.epoch = reinterpret_cast<uint32_t*>(ws->data_ptr());
+      s.gran = reinterpret_cast<int32_t*>(ws->data_ptr()) + vgate::SAMPLE_WS_GRAN;
     }
   }
   s.fault = reinterpret_cast<uint32_t*>(opt_ptr<int32_t>(fault, torch::kInt32, "fault"));
@@ -610,12 +599,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("logits"), py::arg("temperature"), py::arg("top_p"), py::arg("top_k"), py::arg("seeds"),
         py::arg("offsets"), py::arg("out"), py::arg("out_logprob") = py::none(), py::arg("ws") = py::none(),
         py::arg("fault") = py::none());
-  m.def("set_sample_single", &vgate::set_sample_single,
-        "1: the single-launch granule sampler (default), 0: the pass kernels (A/B)");
   m.def("sample_segments", &vgate::sample_segments, "blocks per row the sampler uses for (B, V)");
-  m.def("set_sample_nseg", &vgate::set_sample_nseg, "cap the sampler's segments per row (experiments)");
-  m.def("set_sample_round_launches", &vgate::set_sample_round_launches,
-        "rejection rounds the sampler runs as their own launches before the in-launch fallback (experiments)");
+  m.def("set_sample_nseg", &vgate::set_sample_nseg, "cap the sampler's segments per row (1 = one block per row)");
+  m.attr("SAMPLE_WS_WORDS") = vgate::SAMPLE_WS_WORDS;
   m.def("kernel_copy", &kernel_copy, "pinned host <-> device copy by a kernel on the current stream (no SDMA)",
         py::arg("dst"), py::arg("src"), py::arg("nbytes"));
   m.def("set_flash_prefill", &vgate::set_flash_prefill, "flash prefill attention: 1 on, 0 off, -1 environment");

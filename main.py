@@ -19,8 +19,6 @@ app = create_app(config)
 
 
 def main() -> None:
-    import uvicorn
-
     tp = config.model.tensor_parallel_size
     rank = int(os.environ.get("RANK", "0"))
     if tp > 1 and rank % tp != 0:
@@ -28,8 +26,13 @@ def main() -> None:
         from vgate.backends.native import NativeBackend
         NativeBackend().load_model(config.model)
         return
-    uvicorn.run(app, host=config.server.host, port=config.server.port, log_level="warning",
-                access_log=False)
+    if config.server.http == "uvicorn":
+        import uvicorn
+        uvicorn.run(app, host=config.server.host, port=config.server.port, log_level="warning",
+                    access_log=False)
+        return
+    from vgate.api.server import run
+    run(app, host=config.server.host, port=config.server.port)
 
 
 if __name__ == "__main__":

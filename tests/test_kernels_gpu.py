@@ -348,51 +348,60 @@ def test_sample_top_p_frequent_rejection(B):
     assert (emp[allowed] - q[allowed]).abs().max().item() < 0.03, (emp[allowed], q[allowed])
 
 
-@pytest.mark.parametrize("B", [1, 8, 16])
-def test_sample_single_launch_matches_pass_kernels(B):
-    """The single-launch granule sampler (every block gathers its row's tagged partials itself) draws
-    exactly what the pass kernels draw — same Gumbel noise, same acceptance tests — over 80
-    consecutive launches (the per-row epoch advances each launch, so stale granules never match),
-    for greedy / temperature / top-p / top-k rows, and under hipGraph replay."""
-    torch.manual_seed(40 + B)
+def test_sample_segmented_matches_row_kernel_across_batch_sizes():
+    """The segmented sampler (every block gathers its row's tagged partials itself) draws what the
+    one-block-per-row kernel draws — same Gumbel noise, same acceptance tests — while the batch size
+    ALTERNATES between launches (8 -> 4 -> 16 -> 8 ...: the rows' granule layout must not move with
+    nseg, round-4 ADVICE: rows of a smaller batch wrote into a larger batch's row regions and a row
+    whose epoch had not moved matched them), for greedy / temperature / top-p / top-k rows, then under
+    hipGraph replay (> 64 replays: the per-row epoch keeps the tags apart)."""
+    torch.manual_seed(40)
     V = 151936
     C = ops.native()
-    L = (torch.randn(B, V, device=DEV) * 0.8).contiguous()
-    t = torch.full((B,), 0.7, device=DEV)
+    L = (torch.randn(16, V, device=DEV) * 0.8).contiguous()
+    t = torch.full((16,), 0.7, device=DEV)
     t[0] = 0.0  # a greedy row
-    tp = torch.full((B,), 0.9, device=DEV)
-    tk = torch.full((B,), -1, dtype=torch.int32, device=DEV)
-    if B > 2:
-        tk[2] = 50
-        tp[1] = 1.0  # plain temperature row
-    seeds = torch.arange(B, device=DEV, dtype=torch.int64) * 7 + 3
+    tp = torch.full((16,), 0.9, device=DEV)
+    tk = torch.full((16,), -1, dtype=torch.int32, device=DEV)
+    tk[2] = 50
+    tk[5] = 20
+    tp[5] = 0.5
+    tp[1] = 1.0  # plain temperature row
+    seeds = torch.arange(16, device=DEV, dtype=torch.int64) * 7 + 3
     try:
-        for off in range(80):
+        for off in range(90):
+            B = (8, 4, 16, 8, 2, 16)[off % 6]
             offs = torch.full((B,), off, dtype=torch.int64, device=DEV)
-            C.set_sample_single(1)
-            a = ops.sample(L, t, top_p=tp, top_k=tk, seeds=seeds, offsets=offs)
-            C.set_sample_single(0)
-            b = ops.sample(L, t, top_p=tp, top_k=tk, seeds=seeds, offsets=offs)
-            assert torch.equal(a, b), off
-        C.set_sample_single(1)
+            args = (L[:B], t[:B])
+            kw = dict(top_p=tp[:B], top_k=tk[:B], seeds=seeds[:B], offsets=offs)
+            assert C.sample_segments(B, V) > 1
+            a = ops.sample(*args, **kw).clone()
+            C.set_sample_nseg(1)
+            b = ops.sample(*args, **kw)
+            C.set_sample_nseg(64)
+            assert torch.equal(a, b), (off, B, a, b)
+        B = 8
         offs = torch.full((B,), 7, dtype=torch.int64, device=DEV)
         out = torch.empty(B, dtype=torch.int32, device=DEV)
-        want = ops.sample(L, t, top_p=tp, top_k=tk, seeds=seeds, offsets=offs).clone()
+        kw = dict(top_p=tp[:B], top_k=tk[:B], seeds=seeds[:B], offsets=offs)
+        want = ops.sample(L[:B], t[:B], **kw).clone()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s):
-                ops.sample(L, t, top_p=tp, top_k=tk, seeds=seeds, offsets=offs, out=out)
+                ops.sample(L[:B], t[:B], out=out, **kw)
         torch.cuda.current_stream().wait_stream(s)
-        for _ in range(70):  # > 64 replays: the epoch keeps the tags apart
+        for i in range(70):
             out.fill_(-1)
             g.replay()
+            if i % 10 == 5:  # other batch sizes between replays
+                ops.sample(L[:4], t[:4], top_p=tp[:4], top_k=tk[:4], seeds=seeds[:4], offsets=offs[:4])
             torch.cuda.synchronize()
             assert torch.equal(out, want)
-        assert int(ops.fault_word(DEV)[0].item()) & 16 == 0, "a sampler row meeting gave up"
+        assert int(ops.fault_word(DEV)[0].item()) & 16 == 0, "a sampler row wait gave up"
     finally:
-        C.set_sample_single(int(os.environ.get("VGATE_SAMPLE_SINGLE", "1")))
+        C.set_sample_nseg(64)
 
 
 def test_sample_logprob():

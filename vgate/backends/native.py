@@ -18,6 +18,7 @@ import itertools
 import os
 import threading
 import time
+import weakref
 from typing import Any, AsyncIterator, Dict, List
 
 from vgate.config import ModelConfig
@@ -109,6 +110,7 @@ class NativeBackend:
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
         rid = f"n{next(_req_ids)}"
+        done = _completions(loop)
 
         def cb(kind, seq, payload):
             if kind == "token":
@@ -117,7 +119,7 @@ class NativeBackend:
                 res = RuntimeError(f"engine error: {payload}")
             else:
                 res = self._result(seq)
-            loop.call_soon_threadsafe(_resolve, fut, res)
+            done.push(fut, res)
 
         self.engine.add_request(rid, prompt, self._params(sampling_params), cb)
         try:
@@ -206,6 +208,45 @@ class NativeBackend:
         if self.engine is not None:
             self.engine.stop()
             self.engine.shutdown_followers()
+
+
+class _LoopCompletions:
+    """Results handed from the engine thread to one event loop, one wake-up per burst.
+
+    A wave of requests finishes inside one engine step; ``call_soon_threadsafe`` per request
+    writes the loop's self-pipe and schedules a handle each time. Here the first result of a
+    burst schedules one flush and later ones only append, so the loop wakes once per step."""
+
+    def __init__(self, loop: asyncio.AbstractEventLoop):
+        self.loop = loop
+        self.items: list = []
+        self.lock = threading.Lock()
+
+    def push(self, fut: asyncio.Future, res) -> None:
+        with self.lock:
+            first = not self.items
+            self.items.append((fut, res))
+        if first:
+            try:
+                self.loop.call_soon_threadsafe(self._flush)
+            except RuntimeError:  # loop closed (shutdown): nobody is waiting any more
+                pass
+
+    def _flush(self) -> None:
+        with self.lock:
+            items, self.items = self.items, []
+        for fut, res in items:
+            _resolve(fut, res)
+
+
+_loop_completions: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def _completions(loop: asyncio.AbstractEventLoop) -> _LoopCompletions:
+    c = _loop_completions.get(loop)
+    if c is None:
+        c = _loop_completions[loop] = _LoopCompletions(loop)
+    return c
 
 
 def _resolve(fut: asyncio.Future, res):

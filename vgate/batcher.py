@@ -21,6 +21,7 @@ the tracing context re-attached. Results also carry ``prompt_tokens`` and
 from __future__ import annotations
 
 import asyncio
+import contextlib
 import contextvars
 import functools
 import time
@@ -33,10 +34,11 @@ from vgate.logging_config import get_logger
 from vgate.metrics import (ABANDONED_INFERENCES, BATCH_PROCESSING_TIME, BATCH_QUEUE_TIME, BATCH_SIZE,
                            DEDUP_RATIO, DEDUPLICATED_REQUESTS, INFERENCE_ERRORS, INFLIGHT_INFERENCES,
                            PENDING_REQUESTS, TOKENS_GENERATED, TOTAL_BATCHES, TPOT, TTFT, UNIQUE_PROMPTS_PER_BATCH)
-from vgate.tracing import get_current_trace_id, get_tracer
+from vgate.tracing import _NOOP, get_current_trace_id, get_tracer, is_tracing_enabled
 
 logger = get_logger("vgate.batcher")
 tracer = get_tracer(__name__)
+_NO_SPAN = contextlib.nullcontext(_NOOP)  # reusable: yields the no-op span
 
 
 @dataclass
@@ -58,7 +60,6 @@ class RequestBatcher:
         self.max_concurrent_inferences = 1 if self._serialize_inference else self.max_batch_size
         self._semaphore = asyncio.Semaphore(self.max_concurrent_inferences)
         self._inflight: Dict[str, _Inflight] = {}
-        self._lock = asyncio.Lock()
         self._running = False
         self.total_requests = 0
         self.total_batches = 0
@@ -82,8 +83,7 @@ class RequestBatcher:
 
     async def stop(self):
         self._running = False
-        async with self._lock:
-            pending = [e.task for e in self._inflight.values() if e.task is not None]
+        pending = [e.task for e in self._inflight.values() if e.task is not None]
         if pending:
             await asyncio.gather(*pending, return_exceptions=True)
         logger.info("Batcher stopped")
@@ -91,28 +91,30 @@ class RequestBatcher:
     # ------------------------------------------------------------------ submit
     async def submit(self, prompt: str, max_tokens: Optional[int] = None, temperature: Optional[float] = None,
                      top_p: Optional[float] = None, timeout: Optional[float] = None) -> Dict[str, Any]:
-        with tracer.start_as_current_span("batcher.submit") as span:
+        # no span objects at all while tracing is off (the serving default): this runs once per request
+        cm = tracer.start_as_current_span("batcher.submit") if is_tracing_enabled() else _NO_SPAN
+        with cm as span:
             cfg = get_config()
             max_tokens = cfg.inference.max_tokens if max_tokens is None else max_tokens
             temperature = cfg.inference.temperature if temperature is None else temperature
             top_p = cfg.inference.top_p if top_p is None else top_p
             span.set_attribute("prompt_length", len(prompt))
             key = ResultCache.make_key(prompt, temperature, top_p, max_tokens)
-            cached = await self.cache.get(key)
+            cached = self.cache.get_nowait(key)
             if cached:
                 span.set_attribute("cache_hit", True)
                 return cached
             span.set_attribute("cache_hit", False)
             self.total_requests += 1
-            async with self._lock:
-                entry = self._inflight.get(key)
-                coalesced = entry is not None
-                if entry is None:
-                    entry = _Inflight()
-                    self._inflight[key] = entry
-                    entry.task = asyncio.create_task(self._execute(entry, key, prompt, temperature, top_p, max_tokens))
-                    entry.task.add_done_callback(functools.partial(self._retire, key))
-                entry.waiters += 1
+            # no await between the lookup and the registration: atomic on the event loop
+            entry = self._inflight.get(key)
+            coalesced = entry is not None
+            if entry is None:
+                entry = _Inflight()
+                self._inflight[key] = entry
+                entry.task = asyncio.create_task(self._execute(entry, key, prompt, temperature, top_p, max_tokens))
+                entry.task.add_done_callback(functools.partial(self._retire, key))
+            entry.waiters += 1
             span.set_attribute("deduplicated", coalesced)
             if coalesced:
                 self.total_deduplicated += 1
@@ -123,15 +125,13 @@ class RequestBatcher:
                     return await asyncio.wait_for(asyncio.shield(entry.task), timeout=timeout)
                 return await asyncio.shield(entry.task)
             finally:
-                await self._release_waiter(entry, key)
+                self._release_waiter(entry, key)
 
-    async def _release_waiter(self, entry: _Inflight, key: str) -> None:
-        async with self._lock:
-            entry.waiters -= 1
-            if entry.waiters > 0 or entry.started or entry.task.done():
-                return
-            abandoned = entry.task
-        abandoned.cancel()
+    def _release_waiter(self, entry: _Inflight, key: str) -> None:
+        entry.waiters -= 1
+        if entry.waiters > 0 or entry.started or entry.task.done():
+            return
+        entry.task.cancel()
         ABANDONED_INFERENCES.inc()
         logger.info("Cancelled abandoned request before admission", extra={"extra_data": {"cache_key": key[:8]}})
 
@@ -165,7 +165,7 @@ class RequestBatcher:
             if waiting:
                 self._waiting -= 1
                 PENDING_REQUESTS.set(self._waiting)
-        await self.cache.put(key, result)
+        self.cache.put_nowait(key, result)
         return result
 
     # --------------------------------------------------------------- inference
@@ -175,7 +175,8 @@ class RequestBatcher:
         t0 = time.perf_counter()
         try:
             if hasattr(backend, "agenerate"):
-                with tracer.start_as_current_span("batcher.inference") as span:
+                cm = tracer.start_as_current_span("batcher.inference") if is_tracing_enabled() else _NO_SPAN
+                with cm as span:
                     span.set_attribute("num_prompts", 1)
                     sp = backend.create_sampling_params(temperature=temperature, top_p=top_p, max_tokens=max_tokens)
                     br = await backend.agenerate(prompt, sp)

@@ -34,6 +34,9 @@ class _Section(BaseModel):
 class ServerConfig(_Section):
     host: str = "0.0.0.0"
     port: int = 8000
+    # HTTP front end of ``python main.py``: "vgate" (vgate.api.server, lean HTTP/1.1) or
+    # "uvicorn" (h11). ``uvicorn main:app`` works either way: the app is plain ASGI.
+    http: str = "vgate"
 
 
 class WorkerDiscoveryConfig(_Section):

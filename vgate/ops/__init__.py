@@ -47,19 +47,8 @@ def native():
 
 
 def _configure(mod) -> None:
-    """Runtime knobs of the extension that default from the environment on the Python side."""
-    # VGATE_SAMPLE_ROUND_LAUNCHES: top-k / top-p rejection rounds run as their own launches before
-    # the in-launch fallback (csrc/kernels/sampling.hip launch_sample). 1: the bench A/B measured
-    # 93.1 / 93.2 req/s at 1 vs 92.3 / 93.0 at 2 and 92.4 at 3, sampler_probe 31.1 vs 32.5 us
-    # (profiles/r2_sampler_round_launches.log)
-    if hasattr(mod, "set_sample_round_launches"):
-        # 0: pass 0, then every rejection round in the resume kernel's in-launch meetings — two sampler
-        # launches; the step time is the same as with one round launch (1266.1 vs 1269.9-1271.2 us,
-        # profiles/r4_sampler_round_launches.log)
-        mod.set_sample_round_launches(int(os.environ.get("VGATE_SAMPLE_ROUND_LAUNCHES", "0")))
-    if hasattr(mod, "set_sample_single"):
-        # VGATE_SAMPLE_SINGLE=0: the pass kernels above instead of the single-launch granule sampler
-        mod.set_sample_single(int(os.environ.get("VGATE_SAMPLE_SINGLE", "1")))
+    """Runtime knobs of the extension that default from the environment on the Python side (none
+    left: the sampler's pass-kernel and round-launch variants were deleted in round 5)."""
 
 
 def native_available() -> bool:
@@ -892,11 +881,12 @@ _SWS: dict = {}
 
 
 def sample_workspace(device) -> torch.Tensor:
-    """Zeroed row counters + partials of the segmented sampler (self-resetting, per device)."""
+    """Per-row epochs + fixed per-row granule regions of the segmented sampler (zeroed once, per
+    device; launchers.h SAMPLE_WS_*)."""
     key = str(device)
     ws = _SWS.get(key)
     if ws is None:
-        ws = torch.zeros(32768, dtype=torch.int32, device=device)
+        ws = torch.zeros(int(native().SAMPLE_WS_WORDS), dtype=torch.int32, device=device)
         _SWS[key] = ws
     return ws
 

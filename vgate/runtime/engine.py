@@ -116,6 +116,12 @@ class EngineStats:
     batch_sizes: collections.Counter = field(default_factory=collections.Counter)
     idle_s: float = 0.0        # engine thread waiting for work (no step in flight, nothing queued)
     prefill_steps: int = 0     # steps that carried prompt tokens (mixed or prefill-only)
+    # idle -> busy transitions (engine._wave_account): sums of the three boundary phases
+    waves: int = 0
+    wave_first_s: float = 0.0
+    wave_spread_s: float = 0.0
+    wave_tail_s: float = 0.0
+    wave_size: int = 0
 
 
 class LLMEngine:
@@ -305,11 +311,16 @@ class LLMEngine:
                 or self.scheduler.has_work() or self.ring is not None):
             return
         recent = time.perf_counter() - 1e-3 * self.cfg.idle_batch_recent_ms
-        if sum(1 for t in self._finish_times if t >= recent) < 2 and len(self._inbox) < 2:
+        came_back = sum(1 for t in self._finish_times if t >= recent)
+        if came_back < 2 and len(self._inbox) < 2:
             return  # no wave is coming back: a lone request starts now
         t0 = time.perf_counter()
         t_end = t0 + 1e-3 * win
         cap = self.cfg.max_num_seqs
+        # a closed-loop client sends one new request per finished one: once as many have arrived as
+        # just finished, the wave is complete and the prefill starts without waiting out the gap
+        if came_back >= 2:
+            cap = min(cap, came_back)
         n = len(self._inbox)
         while self._running and n < cap:
             now = time.perf_counter()
@@ -320,6 +331,19 @@ class LLMEngine:
                 break  # nobody arrived within the gap
             n = len(self._inbox)
         self.stats.idle_s += time.perf_counter() - t0
+
+    def _wave_account(self, t_idle0: float) -> None:
+        """Break an idle -> busy transition into (idle start -> first arrival), (first -> last
+        arrival of the batch), (last arrival -> step start): the wave-boundary forensics of
+        bench.py (``wave_breakdown_ms``)."""
+        arr = [s.arrival for s in self._inbox]
+        now = time.perf_counter()
+        st = self.stats
+        st.waves += 1
+        st.wave_first_s += max(0.0, min(arr) - t_idle0)
+        st.wave_spread_s += max(arr) - min(arr)
+        st.wave_tail_s += now - max(arr)
+        st.wave_size += len(arr)
 
     def _idle(self) -> bool:
         return (not self._inbox and not self._aborts and not self.scheduler.has_work() and self._inflight is None
@@ -346,10 +370,13 @@ class LLMEngine:
                         self.runner.defer_capture_failed = True
                         self.runner.pending_captures.clear()
             with self._cv:
+                t_idle0 = None
                 while self._running and self._idle() and not self.runner.pending_captures:
                     if self.ring is not None:  # an idle TP group must not look dead to its followers
                         self.ring.heartbeat()
                     t_idle = time.perf_counter()
+                    if t_idle0 is None:
+                        t_idle0 = t_idle
                     self._cv.wait(timeout=0.5)
                     self.stats.idle_s += time.perf_counter() - t_idle
                 if self._idle():
@@ -357,6 +384,8 @@ class LLMEngine:
                 if not self._running:
                     break
                 self._coalesce_arrivals()
+                if t_idle0 is not None and self._inbox:
+                    self._wave_account(t_idle0)
                 self._drain_inbox()
             if self._calls:
                 self._run_calls()
@@ -725,4 +754,6 @@ class LLMEngine:
             "max_cycle_tokens_seqs": list(st.max_cycle_bucket),
             "preemptions": self.scheduler.num_preemptions, "prefix_cache_hits": int(getattr(self.kvm.alloc, "hits", 0)),
             "healthy": self.healthy,
+            "waves": st.waves, "wave_sum_ms": [round(1e3 * st.wave_first_s, 3), round(1e3 * st.wave_spread_s, 3),
+                                                round(1e3 * st.wave_tail_s, 3)], "wave_requests": st.wave_size,
         }

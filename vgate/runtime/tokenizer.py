@@ -35,6 +35,10 @@ class SyntheticTokenizer:
         self._special = {bos_token_id, *self.eos_token_ids}
         self._lo = self.OFFSET + 256
         self._table: dict[int, bytes] = {}
+        # hot-path caches (encode runs on the serving event loop, decode on the engine thread at
+        # every finished request): the ids of each pre-tokenised word, and the bytes of each id
+        self._word_ids: dict[bytes, tuple] = {}
+        self._bytes: list = [None] * max(0, vocab_size)
 
     def _pieces(self, data: bytes):
         for m in _PRETOK.finditer(data):
@@ -42,18 +46,33 @@ class SyntheticTokenizer:
             for i in range(0, len(p), 6):
                 yield p[i: i + 6]
 
-    def encode(self, text: str, add_bos: bool = False) -> list[int]:
-        ids = [self.bos_token_id] if add_bos else []
+    def _encode_word(self, word: bytes) -> tuple:
+        ids = []
         span = self.vocab_size - self._lo
-        for p in self._pieces(text.encode("utf-8")):
+        for i in range(0, len(word), 6):
+            p = word[i: i + 6]
             if len(p) > 1 and span > 0:
                 t = self._lo + zlib.crc32(p) % span
                 if t not in self._special:
                     prev = self._table.setdefault(t, p)
                     if prev == p:
+                        if t < len(self._bytes):
+                            self._bytes[t] = p  # the learned piece replaces a pseudo-word
                         ids.append(t)
                         continue
             ids.extend(self.OFFSET + b for b in p)
+        return tuple(ids)
+
+    def encode(self, text: str, add_bos: bool = False) -> list[int]:
+        ids = [self.bos_token_id] if add_bos else []
+        cache = self._word_ids
+        for word in _PRETOK.findall(text.encode("utf-8")):
+            w = cache.get(word)
+            if w is None:
+                w = self._encode_word(word)
+                if len(cache) < 1 << 20:
+                    cache[word] = w
+            ids.extend(w)
         return ids
 
     def _piece(self, t: int) -> bytes:
@@ -70,11 +89,20 @@ class SyntheticTokenizer:
             w += _SYLL[(h >> 12) & 15]
         return (" " + w).encode()
 
+    def _piece_cached(self, t: int) -> bytes:
+        b = self._bytes
+        if 0 <= t < len(b):
+            v = b[t]
+            if v is None:
+                v = b[t] = self._piece(t)
+            return v
+        return self._piece(t)
+
     def decode(self, ids: list[int]) -> str:
-        return b"".join(self._piece(t) for t in ids).decode("utf-8", errors="replace")
+        return self.decode_bytes(ids).decode("utf-8", errors="replace")
 
     def decode_bytes(self, ids: list[int]) -> bytes:
-        return b"".join(self._piece(t) for t in ids)
+        return b"".join(map(self._piece_cached, ids))
 
 
 class HFTokenizer:

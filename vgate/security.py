@@ -15,6 +15,7 @@ deque windows instead of list rebuilds.
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import time
 from collections import defaultdict, deque
@@ -22,10 +23,11 @@ from typing import Optional
 
 from vgate.config import APIKeyConfig, SecurityConfig
 from vgate.logging_config import get_logger
-from vgate.tracing import get_tracer
+from vgate.tracing import _NOOP, get_tracer, is_tracing_enabled
 
 logger = get_logger("vgate.security")
 tracer = get_tracer(__name__)
+_NO_SPAN = contextlib.nullcontext(_NOOP)
 
 
 class RateLimiter:
@@ -66,6 +68,10 @@ class RateLimiter:
     def get_usage(self, key: str) -> dict:
         q = self._cleanup(key, time.monotonic())
         return {"current_requests": len(q), "window_seconds": self.window_seconds}
+
+
+_HDR_NAMES = {k: k.lower().encode() for k in ("X-RateLimit-Limit", "X-RateLimit-Remaining", "X-RateLimit-Reset",
+                                               "Retry-After")}
 
 
 def parse_bearer(value: Optional[str]) -> Optional[str]:
@@ -118,7 +124,7 @@ class SecurityMiddleware:
         if path in self.exempt:
             await self.app(scope, receive, send)
             return
-        with tracer.start_as_current_span("security.check") as span:
+        with (tracer.start_as_current_span("security.check") if is_tracing_enabled() else _NO_SPAN) as span:
             span.set_attribute("http.path", path)
             key = parse_bearer(_header(scope, b"authorization"))
             if not key:
@@ -143,7 +149,7 @@ class SecurityMiddleware:
         if not headers:
             await self.app(scope, receive, send)
             return
-        extra = [(k.lower().encode(), v.encode()) for k, v in headers.items()]
+        extra = [(_HDR_NAMES.get(k) or k.lower().encode(), v.encode()) for k, v in headers.items()]
 
         async def send_with_headers(msg):
             if msg["type"] == "http.response.start":
