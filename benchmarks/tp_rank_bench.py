@@ -88,8 +88,8 @@ def main():
                          "(prices the fused exchange's in-kernel cost; no peers)")
     a = ap.parse_args()
     if a.sweep:  # the sweep's (0, 0, 0) row is the launcher heuristic, not the measured table
-        import os
-        os.environ["VGATE_DECODE_PLANS"] = "0"
+        from vgate.models import transformer
+        transformer.APPLY_DECODE_PLANS = False
     from decode_sweep import set_plan, time_step
     from timeline import measure
 
@@ -140,7 +140,7 @@ def main():
         rows[k] = r
     # on a real TP node each step adds its collectives as launches: the embedding all-reduce and the
     # logits all-gather, plus one all-reduce per row-parallel GEMM unless it runs in the GEMM's epilogue
-    # (decode rows, VGATE_TP_FUSED_AR: gemm_epilogue.h epilogue_ar)
+    # (decode rows, model.tp_fused_allreduce: gemm_epilogue.h epilogue_ar)
     nl = len(m.layers)
     print(json.dumps({"timeline_step_us": summary["step_us"], "launches": summary["launches"],
                       "collective_launches_per_real_step": {"fused_all_reduce": 2, "separate_all_reduce": 2 + 2 * nl},

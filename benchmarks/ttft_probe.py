@@ -1,13 +1,11 @@
 """Time to first token for long prompts (engine-level, one request at a time, after a
 warm-up request of the same length so the step's hipGraph bucket is captured): prefill
-throughput of the attention + GEMM kernels. Run with VGATE_PREFILL_BLAS=0/1 to compare the
-fused tile kernels against the hipBLASLt library path for the projections.
+throughput of the attention + GEMM kernels.
 
     python benchmarks/ttft_probe.py --model Qwen/Qwen2.5-1.5B-Instruct --lens 512 2048 4096
 """
 import argparse
 import json
-import os
 import sys
 import threading
 import time
@@ -51,8 +49,7 @@ def main():
         time.sleep(0.5)  # idle: deferred captures
         ts = [one(eng, f"r{L}-{i}", [t + i + 1 for t in ids]) for i in range(3)]
         print(json.dumps({"model": a.model.split("/")[-1], "prompt_len": L, "chunk": a.chunk,
-                          "prefill_blas": os.environ.get("VGATE_PREFILL_BLAS", "auto"), "quantization": a.quantization,
-                          "library_prefill": eng.model.library_prefill,
+                          "quantization": a.quantization,
                           "ttft_ms": round(1e3 * min(ts), 2), "prefill_tok_s": round(L / min(ts))}), flush=True)
     eng.stop()
 

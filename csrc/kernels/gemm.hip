@@ -149,7 +149,15 @@ void launch_gemm(const GemmArgs& g, hipStream_t st) {
   // measured it faster (path 2, gemm_mid.hip); it declines shapes / modes it does not take
   if (g.path == 2 && launch_gemm_mid(g, st)) return;
   // decode rows on the stream-K kernel (path 3: a decode plan / forced), else the tile-per-block kernels
-  if (g.path == 3 && launch_gemm_sk(g, st)) return;
+  if (g.path == 3) {
+    if (launch_gemm_sk(g, st)) return;
+    // declined (shape / mode / occupancy): a stream-K plan's (waves, blocks per CU, k-group) fields
+    // mean nothing to the tile kernels — fall back on the launcher's own heuristic
+    GemmArgs h = g;
+    h.path = 0; h.waves = 0; h.splitk = 0; h.ntb = 0;
+    launch_dispatch<false>(to_params(h), h, st);
+    return;
+  }
   if (g.path == 1 || (g.path == 0 && g.M >= 128 && g.waves == 0 && g.splitk == 0)) {
     GemmArgs h = g;
     if (g.path == 0) h.ntb = 0;

@@ -342,8 +342,24 @@ SkPlan sk_plan(int ntiles, int KT, int M, int G, int W, int UA) {
 // The LDS request pins the blocks per CU: the equal shares only balance the chip if no CU takes
 // two of them while another idles (the dispatcher packs workgroups onto a CU while its registers
 // and LDS allow). 1 per CU: > 80 KiB of the 160 KiB; 2 per CU: > 160 / 3 KiB.
+//
+// The owners of a tile wait for granules of blocks dispatched after them, so all G blocks must be
+// resident at once: the launcher asks the runtime how many blocks of this kernel fit per CU at this
+// LDS request (VGPRs included) and declines the launch when G do not (the caller then runs the tile
+// kernels). It cannot see CUs held by kernels of OTHER streams: this path assumes the engine's decode
+// step owns the device (no concurrent compute stream), which the engine guarantees; the waits are
+// bounded all the same (fault bit 4) so a violation fails the step instead of hanging the GPU.
+template <typename K>
+bool sk_fits(K kern, int threads, size_t lds, int G) {
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(kern), threads, lds) !=
+      hipSuccess)
+    return false;
+  return (long long)per * cu_count_gemm() >= G;
+}
+
 template <int W, int UA, int EPI, int NORM, int XP>
-void sk_launch_cfg(const GemmParams& p, const SkParams& s, int nga, int G, int per_cu, hipStream_t st) {
+bool sk_launch_cfg(const GemmParams& p, const SkParams& s, int nga, int G, int per_cu, hipStream_t st) {
   constexpr size_t need = W * 64 * 16 + W * 16 * 4 + 16 + W * 2 * 64 * 16 + W * 2 * 16 * 4 + W * 2 * 4;
   const size_t lds = std::max(need, per_cu == 1 ? (size_t)82 * 1024 : (size_t)54 * 1024);
 #define VG_SK(N)                                                                                              \
@@ -352,6 +368,9 @@ void sk_launch_cfg(const GemmParams& p, const SkParams& s, int nga, int G, int p
     static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),                        \
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess; \
     (void)attr;                                                                                               \
+    static int fits[3] = {-1, -1, -1}; /* per blocks-per-CU setting (lds and G follow from it) */            \
+    if (fits[per_cu] < 0) fits[per_cu] = sk_fits(kern, 64 * W, lds, G) ? 1 : 0;                               \
+    if (!fits[per_cu]) return false;                                                                          \
     hipLaunchKernelGGL(kern, dim3(G), dim3(64 * W), lds, st, p, s);                                           \
   } while (0)
   if (nga == 1) VG_SK(1);
@@ -359,22 +378,23 @@ void sk_launch_cfg(const GemmParams& p, const SkParams& s, int nga, int G, int p
   else if (nga == 4) VG_SK(4);
   else VG_SK(8);
 #undef VG_SK
+  return true;
 }
 
 // (W, UA): 8 waves x groups of 8 k-steps (default), 4 x 8, 8 x 4 (sweeps: GemmArgs waves / ntb)
 template <int EPI, int NORM, int XP>
-void sk_launch_xp(const GemmParams& p, const SkParams& s, int w, int ua, int nga, int G, int per_cu, hipStream_t st) {
-  if (w == 4) sk_launch_cfg<4, 8, EPI, NORM, XP>(p, s, nga, G, per_cu, st);
-  else if (ua == 4) sk_launch_cfg<8, 4, EPI, NORM, XP>(p, s, nga, G, per_cu, st);
-  else sk_launch_cfg<8, 8, EPI, NORM, XP>(p, s, nga, G, per_cu, st);
+bool sk_launch_xp(const GemmParams& p, const SkParams& s, int w, int ua, int nga, int G, int per_cu, hipStream_t st) {
+  if (w == 4) return sk_launch_cfg<4, 8, EPI, NORM, XP>(p, s, nga, G, per_cu, st);
+  if (ua == 4) return sk_launch_cfg<8, 4, EPI, NORM, XP>(p, s, nga, G, per_cu, st);
+  return sk_launch_cfg<8, 8, EPI, NORM, XP>(p, s, nga, G, per_cu, st);
 }
 
 template <int EPI, int NORM>
-void sk_launch(const GemmParams& p, const SkParams& s, int xp, int w, int ua, int nga, int G, int per_cu,
+bool sk_launch(const GemmParams& p, const SkParams& s, int xp, int w, int ua, int nga, int G, int per_cu,
                hipStream_t st) {
-  if (xp == 4) sk_launch_xp<EPI, NORM, 4>(p, s, w, ua, nga, G, per_cu, st);
-  else if (xp == 2) sk_launch_xp<EPI, NORM, 2>(p, s, w, ua, nga, G, per_cu, st);
-  else sk_launch_xp<EPI, NORM, 1>(p, s, w, ua, nga, G, per_cu, st);
+  if (xp == 4) return sk_launch_xp<EPI, NORM, 4>(p, s, w, ua, nga, G, per_cu, st);
+  if (xp == 2) return sk_launch_xp<EPI, NORM, 2>(p, s, w, ua, nga, G, per_cu, st);
+  return sk_launch_xp<EPI, NORM, 1>(p, s, w, ua, nga, G, per_cu, st);
 }
 
 }  // namespace
@@ -413,13 +433,12 @@ bool launch_gemm_sk(const GemmArgs& g, hipStream_t st) {
   SkParams s{KT, ntiles * KT / pl.XP, pl.cmax, reinterpret_cast<uint4*>(g.sk_pub), g.fault};
 #define VG_SKE(E, NORM_) sk_launch<E, NORM_>(p, s, pl.XP, W, UA, pl.NGA, G, per_cu, st)
   switch (g.epi) {
-    case EPI_SILU: VG_SKE(EPI_SILU, 2); break;
-    case EPI_QKV: VG_SKE(EPI_QKV, 2); break;
-    case EPI_F32: VG_SKE(EPI_F32, 0); break;
-    default: VG_SKE(EPI_BF16, 0);
+    case EPI_SILU: return VG_SKE(EPI_SILU, 2);
+    case EPI_QKV: return VG_SKE(EPI_QKV, 2);
+    case EPI_F32: return VG_SKE(EPI_F32, 0);
+    default: return VG_SKE(EPI_BF16, 0);
   }
 #undef VG_SKE
-  return true;
 }
 
 }  // namespace vgate

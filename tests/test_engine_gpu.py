@@ -152,18 +152,13 @@ def test_awq_engine_generates():
     assert eng.model.weight_bytes() < _engine().model.weight_bytes()
 
 
-@pytest.mark.parametrize("library", [False, True])
-def test_long_prompt_prefill_matches_reference(library, monkeypatch):
+def test_long_prompt_prefill_matches_reference():
     """A 300-token prompt is prefilled in steps of >= 128 tokens, which take the hand-written
-    LDS-tiled MFMA prefill kernel on the packed weights (default: no second weight copy) or,
-    with VGATE_PREFILL_BLAS=1, the hipBLASLt comparison path; greedy tokens are still the
-    (near-)argmax of the dense fp32 model, teacher-forced, and equal the eager engine's."""
-    from vgate import ops
-    monkeypatch.setenv("VGATE_PREFILL_BLAS", "1" if library else "0")
+    LDS-tiled MFMA prefill kernel on the packed weights; greedy tokens are the (near-)argmax of the
+    dense fp32 model, teacher-forced, and equal the eager engine's."""
     long_prompt = [3 + (j * 29) % 500 for j in range(300)]
     sp = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
     eng = _engine()
-    assert eng.model.library_prefill == library and ops.LIBRARY_MIN_M <= 256
     g = _run(eng, [("long", long_prompt, sp)])["long"].output_ids
     e = _run(_engine(enforce_eager=True), [("long", long_prompt, sp)])["long"].output_ids
     assert g == e

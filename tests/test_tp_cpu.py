@@ -25,9 +25,10 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _cfg(path, tp):
+def _cfg(path, tp, timeout=120.0):
     return EngineConfig(model=path, device="cpu", tensor_parallel_size=tp, max_model_len=256, max_num_seqs=8,
-                        max_num_batched_tokens=64, num_kv_blocks=128, warmup=False, seed=0)
+                        max_num_batched_tokens=64, num_kv_blocks=128, warmup=False, seed=0,
+                        tp_timeout_seconds=timeout)
 
 
 def _generate(eng):
@@ -49,7 +50,8 @@ def _worker(rank, world, port, path, q, overlap_min=None, embed_ids=None):
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                           MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         if overlap_min is not None:  # row-chunked row-parallel GEMMs + per-chunk all-reduce
-            os.environ.update(VGATE_TP_OVERLAP_MIN_TOKENS=str(overlap_min), VGATE_TP_OVERLAP_CHUNKS="3")
+            from vgate.models import transformer
+            transformer.TP_OVERLAP_MIN_TOKENS, transformer.TP_OVERLAP_CHUNKS = overlap_min, 3
         torch.set_num_threads(1)
         eng = LLMEngine(_cfg(path, world))
         assert eng.tp.size == world and eng.tp.rank == rank
@@ -155,9 +157,9 @@ def test_tp_group_routes_small_allreduce_to_custom_ar():
 
 def _failing_worker(rank, world, port, path, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port), VGATE_TP_TIMEOUT_S="20")
+                      MASTER_PORT=str(port))
     torch.set_num_threads(1)
-    eng = LLMEngine(_cfg(path, world))
+    eng = LLMEngine(_cfg(path, world, timeout=20))
     if rank == 1:
         def boom(*a, **k):
             raise RuntimeError("injected follower fault")
@@ -196,9 +198,9 @@ def test_tp_follower_fault_tears_down_group(tmp_path):
 def _idle_worker(rank, world, port, path, q, idle_s):
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
-                          MASTER_PORT=str(port), VGATE_TP_TIMEOUT_S="2")
+                          MASTER_PORT=str(port))
         torch.set_num_threads(1)
-        eng = LLMEngine(_cfg(path, world))
+        eng = LLMEngine(_cfg(path, world, timeout=2))
         if rank != 0:
             eng.follower_loop()  # os._exit(1) if it sees no heartbeat for 2 s
             q.put(("ok", None))
@@ -228,7 +230,7 @@ def _idle_worker(rank, world, port, path, q, idle_s):
 @pytest.mark.timeout(300)
 def test_tp_group_survives_idle_longer_than_timeout(tmp_path):
     """ROUND-2 ADVICE (high): rank 0 must stamp the step-ring heartbeat while its serving loop
-    idles, else every follower's ring wait times out after VGATE_TP_TIMEOUT_S and the group
+    idles, else every follower's ring wait times out after tp_timeout_seconds and the group
     tears itself down. Idle 5 s at a 2 s timeout, then serve: every request completes."""
     ref_eng = LLMEngine(EngineConfig(model="tiny", device="cpu", max_model_len=256, max_num_seqs=8,
                                      max_num_batched_tokens=64, num_kv_blocks=128, warmup=False, seed=0))

@@ -33,12 +33,12 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _cfg(path, tp, eager=False, tokens=320):
+def _cfg(path, tp, eager=False, tokens=320, **opts):
     from vgate.runtime.engine import EngineConfig
 
     return EngineConfig(model=path, device="cuda:0", tensor_parallel_size=tp, max_model_len=1024, max_num_seqs=8,
                         max_num_batched_tokens=tokens, num_kv_blocks=256, warmup=False, seed=0,
-                        enforce_eager=eager)
+                        enforce_eager=eager, tp_timeout_seconds=60.0, **opts)
 
 
 def _generate(eng, prompts=None):
@@ -63,17 +63,17 @@ def _generate(eng, prompts=None):
 LONG = {"long600": [7 + (j * 13) % 450 for j in range(600)], "short": [9, 8, 7, 6, 5]}
 
 
-def _worker(rank, world, port, path, q, eager=False, env=None, tokens=320, prompts=None):
+def _worker(rank, world, port, path, q, eager=False, env=None, tokens=320, prompts=None, opts=None):
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-                          MASTER_PORT=str(port), VGATE_TP_TIMEOUT_S="60", **(env or {}))
+                          MASTER_PORT=str(port), **(env or {}))
         import torch.distributed as dist
 
         from vgate.runtime.engine import LLMEngine
 
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        eng = LLMEngine(_cfg(path, world, eager, tokens))
+        eng = LLMEngine(_cfg(path, world, eager, tokens, **(opts or {})))
         assert eng.tp.size == world and eng.tp.rank == rank and eng.tp.backend == "gloo"
         eng.runner.defer_capture = False
         assert eng.model.num_heads_local * world == eng.arch.num_heads
@@ -91,12 +91,12 @@ def _worker(rank, world, port, path, q, eager=False, env=None, tokens=320, promp
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("eager,fused", [(False, "1"), (True, "1"), (False, "0")])
+@pytest.mark.parametrize("eager,fused", [(False, True), (True, True), (False, False)])
 def test_tp2_on_gpu_matches_tp1(tmp_path, eager, fused):
     """graph == eager == TP=1: with every decode collective on the IPC kernels (all-reduce and the
     logits all-gather) a gloo TP group replays captured hipGraphs for the buckets they cover.
-    fused "1" (default): the decode o_proj / down_proj all-reduce inside their GEMM epilogue
-    (gemm_epilogue.h epilogue_ar); "0": the GEMM stores its partial, the one-shot kernel reduces."""
+    fused (default): the decode o_proj / down_proj all-reduce inside their GEMM epilogue
+    (gemm_epilogue.h epilogue_ar); not fused: the GEMM stores its partial, the one-shot kernel reduces."""
     from vgate.models.weights import save_checkpoint
     from vgate.runtime.engine import EngineConfig, LLMEngine
 
@@ -113,7 +113,8 @@ def test_tp2_on_gpu_matches_tp1(tmp_path, eager, fused):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, path, q, eager, {"VGATE_TP_FUSED_AR": fused}))
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, path, q, eager, None, 320, None,
+                                                           {"tp_fused_allreduce": fused}))
              for r in range(2)]
     for p in procs:
         p.start()
@@ -177,7 +178,7 @@ def test_tp2_two_shot_long_prefill_matches_tp1(tmp_path):
     assert tp_out == ref
 
 
-def _timeout_worker(rank, port, path, q, go, ring="1"):
+def _timeout_worker(rank, port, path, q, go):
     import sys
 
     def say(*a):
@@ -185,8 +186,7 @@ def _timeout_worker(rank, port, path, q, go, ring="1"):
 
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-                          MASTER_PORT=str(port), VGATE_TP_TIMEOUT_S="60", VGATE_AR_SPIN_LIMIT="200000",
-                          VGATE_RING_IDS=ring)
+                          MASTER_PORT=str(port), VGATE_AR_SPIN_LIMIT="200000")
         import torch.distributed as dist
 
         from vgate.runtime.engine import LLMEngine
@@ -230,14 +230,12 @@ def _timeout_worker(rank, port, path, q, go, ring="1"):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("ring", ["1", "0"])
-def test_tp2_peer_stops_custom_allreduce_times_out_and_engine_fails(tmp_path, ring):
+def test_tp2_peer_stops_custom_allreduce_times_out_and_engine_fails(tmp_path):
     """Timeout path of the custom all-reduce: rank 1 is frozen (SIGSTOP) after a good generation;
     rank 0's next step waits for it at the first collective, gives up after the spin limit (set
     short here), every later collective of the step skips the wait (sticky error word), the
     step's last graph node hands the word to the host, and the engine fails the step: the request
-    ends with an error and the engine reports unhealthy (its /health then answers 503).
-    ring "0" (VGATE_RING_IDS=0: no ids-ring node) takes the ar.check() read instead."""
+    ends with an error and the engine reports unhealthy (its /health then answers 503)."""
     import signal
 
     path = _ckpt(tmp_path)
@@ -245,7 +243,7 @@ def test_tp2_peer_stops_custom_allreduce_times_out_and_engine_fails(tmp_path, ri
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     go = ctx.Event()
-    procs = [ctx.Process(target=_timeout_worker, args=(r, port, path, q, go, ring)) for r in range(2)]
+    procs = [ctx.Process(target=_timeout_worker, args=(r, port, path, q, go)) for r in range(2)]
     for p in procs:
         p.start()
     pid1 = None

@@ -43,7 +43,12 @@ def engine_config_from(model_config: ModelConfig):
         seed=model_config.seed, block_size=model_config.kv_block_size,
         part_size=model_config.attention_partition_size,
         graph_token_buckets=model_config.hip_graph_token_buckets,
-        warmup_max_tokens=model_config.graph_warmup_max_tokens, warmup_max_seqs=model_config.graph_warmup_max_seqs)
+        warmup_max_tokens=model_config.graph_warmup_max_tokens, warmup_max_seqs=model_config.graph_warmup_max_seqs,
+        idle_batch_window_ms=model_config.idle_batch_window_ms, idle_batch_gap_ms=model_config.idle_batch_gap_ms,
+        idle_batch_recent_ms=model_config.idle_batch_recent_ms, prefill_autotune=model_config.prefill_autotune,
+        plan_cache=model_config.plan_cache or "", tp_timeout_seconds=model_config.tp_timeout_seconds,
+        tp_custom_allreduce=model_config.tp_custom_allreduce, tp_fused_allreduce=model_config.tp_fused_allreduce,
+        tp_collective_self_check=model_config.tp_collective_self_check)
 
 
 def freeze_heap() -> None:

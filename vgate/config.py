@@ -118,6 +118,24 @@ class ModelConfig(_Section):
     # <= graph_warmup_max_seqs (others are captured the first time the engine is idle)
     graph_warmup_max_tokens: int = 512
     graph_warmup_max_seqs: int = 16
+    # admission window of an IDLE engine: a closed-loop client's next wave is prefilled in one step
+    # (the first arrival waits up to idle_batch_gap_ms for the next, idle_batch_window_ms in all, and
+    # only when >= 2 requests finished within idle_batch_recent_ms; vgate/runtime/engine.py)
+    idle_batch_window_ms: float = 3.0
+    idle_batch_gap_ms: float = 0.6
+    idle_batch_recent_ms: float = 20.0
+    # start-up timing of the prefill GEMM decompositions per shape and token bucket, and the JSON file
+    # the measured plans persist in per (device, native build, shapes) ("" / null = no file)
+    prefill_autotune: bool = True
+    plan_cache: Optional[str] = "~/.cache/vgate/gemm_plans.json"
+    # tensor parallel (tensor_parallel_size > 1): collective / step-ring timeout, the custom IPC
+    # all-reduce kernels (false: RCCL for every collective), the all-reduce fused into the decode
+    # row-parallel GEMM epilogue, and the start-up self-check of the custom collectives against
+    # torch.distributed (a mismatch turns the custom paths off group-wide)
+    tp_timeout_seconds: float = 120.0
+    tp_custom_allreduce: bool = True
+    tp_fused_allreduce: bool = True
+    tp_collective_self_check: bool = True
 
     @field_validator("engine_type")
     @classmethod

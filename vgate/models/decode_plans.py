@@ -22,7 +22,11 @@ PLANS: dict[tuple[int, int, str, str], tuple] = {
     (1280, 8192, "qkv", "dense"): (8, 3, 0),     # 80 tiles x 256 k-steps: 240 blocks (heuristic 8 x 2: +33 us)
     (8192, 1024, "plain", "dense"): (2, 1, 1),   # o_proj
     (7168, 8192, "silu", "dense"): (4, 1, 0),    # gate_up: 448 one-tile blocks at 4 waves (heuristic 8: +118 us)
-    # down_proj on stream-K, 4 waves, one block per CU (r4 probe: 12.8 vs 13.5 us per launch; round 3: (8, 1, 2))
+    # down_proj on stream-K, 4 waves, one block per CU (r4 probe: 12.8 vs 13.5 us per launch; round 3: (8, 1, 2)).
+    # NOTE: a rank with the fused row-parallel all-reduce (the TP default) runs its row-parallel GEMMs
+    # on the tile kernels with the all-reduce epilogue, so this entry is unused there (measured with
+    # collectives stubbed, benchmarks/tp_rank_bench.py); a declined stream-K launch falls back on the
+    # launcher's heuristic, not on these fields (csrc/kernels/gemm.hip launch_gemm)
     (8192, 3584, "plain", "dense"): ("sk", 4, 1, 8),
     (16032, 8192, "plain", "dense"): (8, 1, 1),  # LM head shard
     # Llama-3-8B, batch 8 (r4 probe, profiles/r4_streamk_probe.log): qkv on stream-K (13.6 vs 15.1 us per

@@ -21,7 +21,6 @@ with no extra kernel.
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 
 import torch
@@ -29,6 +28,14 @@ import torch
 from vgate import ops
 from vgate.models.config import ModelArch
 from vgate.parallel.comm import TPGroup
+
+# the measured per-shape decode decompositions (vgate/models/decode_plans.py) at model construction;
+# the decode sweeps turn this off to time the launcher's heuristic
+APPLY_DECODE_PLANS = True
+# TP comm / compute overlap of long steps: row-parallel GEMMs of >= TP_OVERLAP_MIN_TOKENS rows run in
+# TP_OVERLAP_CHUNKS row chunks, chunk i's all-reduce on a side stream under chunk i+1's GEMM
+TP_OVERLAP_CHUNKS = 4
+TP_OVERLAP_MIN_TOKENS = 256
 
 
 @dataclass
@@ -90,15 +97,14 @@ class DecoderModel:
         else:
             from vgate.models.weights import random_init
             random_init(self, seed)
-        self.library_prefill = self._keep_library_copies()
-        if self.device.type == "cuda" and self.quant == "awq" and not self.library_prefill:
+        if self.device.type == "cuda" and self.quant == "awq":
             # long AWQ steps: int4 -> bf16 dequant of one matrix at a time into a shared scratch
             # (ops.linear), sized once here so graph capture never allocates
             lins = [lin for L in self.layers for lin in (L.qkv, L.o, L.gate_up, L.down)]
             ops.reserve_awq_scratch(self.device, max(lin.N * lin.K for lin in lins if lin.kind == "awq"))
-        if self.device.type == "cuda" and os.environ.get("VGATE_FOLD_NORM", "1") != "0":
+        if self.device.type == "cuda":
             self.fold_norms()
-        if os.environ.get("VGATE_DECODE_PLANS", "1") != "0":  # measured decode decompositions per shape
+        if APPLY_DECODE_PLANS:  # measured decode decompositions per shape
             from vgate.models import decode_plans
             decode_plans.apply(self)
         table_len = max(max_model_len, 16) + 1
@@ -106,26 +112,10 @@ class DecoderModel:
                                             device=self.device)
         # TP comm/compute overlap for long steps (prefill): row-parallel GEMMs run in row
         # chunks and chunk i's all-reduce runs on a side stream while chunk i+1's GEMM runs
-        self.tp_overlap_chunks = int(os.environ.get("VGATE_TP_OVERLAP_CHUNKS", "4"))
-        self.tp_overlap_min_tokens = int(os.environ.get("VGATE_TP_OVERLAP_MIN_TOKENS", "256"))
+        self.tp_overlap_chunks = TP_OVERLAP_CHUNKS
+        self.tp_overlap_min_tokens = TP_OVERLAP_MIN_TOKENS
         self.comm_stream = (torch.cuda.Stream(self.device)
                             if self.device.type == "cuda" and self.tp.size > 1 else None)
-
-    def _keep_library_copies(self) -> bool:
-        """Plain weight copies for hipBLASLt prefill GEMMs (ops.linear, M >= 128) — a comparison
-        mode only for bf16 weights: by default their long steps run the hand-written LDS-tiled
-        MFMA kernel (csrc/kernels/gemm_prefill.hip) on the packed weights, no second copy kept.
-        AWQ int4 layers keep no copy either: a long step dequantises one matrix at a time into a
-        shared scratch and runs the same prefill kernel (ops.linear). VGATE_PREFILL_BLAS: "0"
-        (default) = none, "awq" = copies for AWQ layers only, "1" = every layer."""
-        mode = os.environ.get("VGATE_PREFILL_BLAS", "0")
-        if self.device.type != "cuda" or mode == "0" or (mode == "awq" and self.quant != "awq"):
-            return False
-        lins = [lin for L in self.layers for lin in (L.qkv, L.o, L.gate_up, L.down)]
-        extra = sum(lin.N * lin.K * 2 for lin in lins)
-        if mode not in ("1", "awq") and extra > 0.1 * torch.cuda.get_device_properties(self.device).total_memory:
-            return False
-        return all([lin.keep_library_copy() for lin in lins])
 
     def fold_norms(self) -> int:
         """Fold every RMSNorm weight into the packed matrix of the GEMM that consumes it
@@ -226,8 +216,7 @@ class DecoderModel:
         # int4 decode steps: the residual GEMMs (o_proj, down_proj) hand the NEXT RMSNorm over —
         # h * gamma plus per-tile sums of h^2 — so the int4 qkv / gate_up kernels read normed rows
         # (no gamma loads, no x^2 pass; ops.linear norm_out / prenorm)
-        hand = (self.quant == "awq" and tp.size == 1 and T <= 16
-                and os.environ.get("VGATE_AWQ_NORM_HANDOFF", "1") != "0")
+        hand = self.quant == "awq" and tp.size == 1 and T <= 16
         if hand:
             hg = torch.empty(T, a.hidden_size, dtype=torch.bfloat16, device=dev)
             ssp = torch.empty(T, a.hidden_size // 16, dtype=torch.float32, device=dev)

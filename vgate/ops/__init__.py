@@ -163,12 +163,11 @@ class Linear:
         self.kind = "awq" if awq is not None else "dense"
         self.bias = bias
         self.norm_gamma = None  # RMSNorm weight folded into the packed copy (see fold_norm)
-        self.wl = None  # optional plain [N, K] copy for library (hipBLASLt) prefill GEMMs
         # decode-GEMM decomposition for M <= 16 steps (0 = the launcher's heuristic): set by the
         # model from the measured per-shape table (vgate/models/decode_plans.py)
         self.dec_waves = 0
         self.dec_splitk = 0
-        self.dec_sk = None  # stream-K decode kernel: None = STREAMK_DECODE, bool, or (waves, blocks/CU, group)
+        self.dec_sk = None  # stream-K decode kernel: None = STREAMK_DECODE, or (waves, blocks/CU, group)
         self.dec_ntb = 0
         # prefill (M >= 128) tile / K-slice choice per M bucket, measured at engine start-up
         # (tune_prefill); empty = the launcher's heuristic
@@ -213,24 +212,7 @@ class Linear:
             return False
         g = gamma.to(self.wp.device, torch.float32).reshape(1, self.K // 32, 4, 1, 8)
         self.wp.copy_((self.wp.float() * g).to(torch.bfloat16))
-        if self.wl is not None:
-            self.wl.copy_((self.wl.float() * gamma.to(self.wl.device, torch.float32)[None]).to(torch.bfloat16))
         self.norm_gamma = gamma.detach().clone()
-        return True
-
-    def keep_library_copy(self) -> bool:
-        """Keep a plain [N, K] bf16 copy (original row order) for long prefill steps, which
-        go to hipBLASLt + separate epilogues: at M >= 128 the library MFMA GEMM is 1.3-3x
-        faster than the fragment-packed decode/tile kernels (benchmarks/prefill_blas_probe.py,
-        profiles/r1_prefill_blas_probe.log). Call before fold_norm. GPU weights only; AWQ
-        weights are dequantized once (the W4A16 kernels have no M > 16 tile path: prefill of
-        an AWQ model was 4.6x slower than bf16, profiles/r1_ttft_awq.log)."""
-        if self.wp is None or self.norm_gamma is not None:
-            return False
-        if self.kind == "awq":
-            self.wl = self._awq_dense().contiguous()
-            return True
-        self.wl = self.dense_weight().contiguous()
         return True
 
     def _awq_dense(self) -> torch.Tensor:
@@ -266,7 +248,7 @@ class Linear:
         return w
 
     def nbytes(self) -> int:
-        """Bytes a decode step streams (the library copy is prefill-only)."""
+        """Bytes a decode step streams."""
         if self.kind == "awq" and self.w is None:
             n = self.wp.numel() * 4 + self.scales.numel() * 4  # int4 + (s, s*z) bf16 per group
             return n + (self.szp.numel() * 2 if getattr(self, "szp", None) is not None else 0)
@@ -334,12 +316,9 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
         else:
             out.copy_(ref.linear_ref(xx, wd, lin.bias, residual, out_f32))
         return out
-    if (lin.wl is not None and M >= (LIBRARY_MIN_M_AWQ if lin.kind == "awq" else LIBRARY_MIN_M) and row_idx is None
-            and not out_f32):
-        return _linear_library(x, lin, out, residual, norm, qkv)
     C = native()
     epi = 3 if qkv is not None else (2 if silu else (1 if out_f32 else 0))
-    awq_mid = (lin.kind == "awq" and AWQ_MID and 16 < M <= 64 and row_idx is None and waves == 0 and splitk == 0
+    awq_mid = (lin.kind == "awq" and 16 < M <= 64 and row_idx is None and waves == 0 and splitk == 0
                and path == 0 and lin.group == 128 and getattr(lin, "szp", None) is not None)
     if awq_mid:
         path = 2  # int4 medium kernel (csrc/kernels/gemm_awq_wide.hip awq_mid_kernel): no bf16 scratch
@@ -387,12 +366,9 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
     return out
 
 
-LIBRARY_MIN_M = int(os.environ.get("VGATE_PREFILL_BLAS_MIN_M", "128"))
-# AWQ steps with at least this many rows run dequant-to-scratch + the bf16 prefill / tile kernels
-AWQ_DEQUANT_MIN_M = int(os.environ.get("VGATE_AWQ_DEQUANT_MIN_M", "32"))
-# AWQ steps of 16 < M <= 64 rows (mixed prefill + decode) on the int4 medium kernel instead of the
-# dequantise-to-scratch path (VGATE_AWQ_MID=0: the scratch path, A/B)
-AWQ_MID = os.environ.get("VGATE_AWQ_MID", "1") != "0"
+# AWQ steps of 16 < M <= 64 rows (mixed prefill + decode) run the int4 medium kernel; longer ones
+# (M >= AWQ_DEQUANT_MIN_M not taken by it) dequantise to scratch + the bf16 prefill / tile kernels
+AWQ_DEQUANT_MIN_M = 32
 _AWQ_SCRATCH: dict = {}
 
 
@@ -422,55 +398,11 @@ def _linear_awq_dequant(x, lin: "Linear", out, residual, norm, qkv, epi, M):
         kw.update(_plan_kw(lin.prefill_plan.get(_plan_bucket(lin.prefill_plan, M)), M))
     C.gemm(x, scratch, lin.N, lin.K, out, epi, **kw)
     return out
-# the W4A16 kernels are decode kernels (no tile path above M = 16): hand AWQ steps to the
-# library copy earlier
-LIBRARY_MIN_M_AWQ = int(os.environ.get("VGATE_PREFILL_BLAS_MIN_M_AWQ", "32"))
-_ONES: dict = {}
-
-
-def _linear_library(x, lin: Linear, out, residual, norm, qkv):
-    """Long-step (prefill) path of :func:`linear`: RMSNorm kernel -> hipBLASLt GEMM on the
-    plain weight copy, then bias / residual adds, and SiLU*mul or RoPE + KV write (+ q
-    placement) as one epilogue kernel each. Same math as the fused kernels up to where the
-    bf16 roundings fall."""
-    xx = x
-    if norm is not None:
-        if lin.norm_gamma is not None:  # gamma is folded into wl: unit-weight RMSNorm
-            key = (str(x.device), lin.K)
-            ones = _ONES.get(key)
-            if ones is None:
-                ones = _ONES[key] = torch.ones(lin.K, dtype=torch.bfloat16, device=x.device)
-            xx = rmsnorm(x[:, :lin.K], ones, float(norm[1]))
-        else:
-            xx = rmsnorm(x[:, :lin.K], norm[0], float(norm[1]))
-    elif x.shape[1] != lin.K:
-        xx = x[:, :lin.K]
-    wt = lin.wl.t()
-    C = native()
-    if lin.layout == "silu":
-        y = torch.mm(xx, wt)
-        C.silu_mul(y, out)  # one fused epilogue kernel
-        return out
-    # plain GEMM + separate adds: hipBLASLt's beta = 1 / bias-epilogue variants (addmm) made
-    # an eagerly-run step differ bitwise from its captured replay (algorithm choice), which
-    # the deferred-capture engine must not see (tests/test_engine_gpu.py)
-    y = torch.mm(xx, wt)
-    if lin.bias is not None:
-        y += lin.bias
-    if qkv is not None:
-        C.rope_kv(y, qkv["positions"], qkv["slots"], qkv["cos_sin"], qkv["k_cache"], qkv["v_cache"],
-                  qkv["hq"], qkv["hkv"], 128, out)  # rotated q written straight into out
-        return out
-    if residual is not None:
-        torch.add(y, residual, out=out)
-    else:
-        out.copy_(y)
-    return out
 
 
 # flash prefill: long causal ranges run as two K halves met through fp32 partials in the GEMM
-# workspace (csrc/kernels/attention.hip attn_flash_kernel, two blocks per KV head); VGATE_FLASH_SPLIT=0 turns it off
-FLASH_SPLIT = os.environ.get("VGATE_FLASH_SPLIT", "1") != "0"
+# workspace (csrc/kernels/attention.hip attn_flash_kernel, two blocks per KV head); tests turn it off
+FLASH_SPLIT = True
 
 
 def attention(q, q_stride, k_cache, v_cache, block_tables, context_lens, query_start, tile_seq, tile_q0, out,
@@ -701,7 +633,13 @@ def _plan_kw(cfg, M: int) -> dict:
 MEDIUM_DEFAULT = (-1, -1)  # medium-M plan entry: keep the default (decode / tile kernel) path
 
 
-def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = 0.05) -> dict:
+# bump whenever the MEANING of a stored plan changes on the Python side (the _plan_kw encoding of a
+# (tile, K slices) code, MID_BASE, the tuner margin): a cached plan set is keyed on this too
+PLAN_FORMAT = 2
+TUNE_MARGIN = 0.05
+
+
+def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = TUNE_MARGIN) -> dict:
     """Start-up measurement of the prefill GEMM decomposition per (N, K) shape and M bucket.
 
     The launcher's tile / K-split heuristic misses by up to 1.8x at mid M, where the grid of
@@ -785,15 +723,17 @@ def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = 0.05
 
 def _plan_cache_key(lins: list, ms: list[int]) -> str:
     """What a stored plan set was measured for: the device, the native build (size + mtime of the
-    extension) and every (N, K) shape x M bucket x candidate list — any change re-measures."""
+    extension), the plan encoding (PLAN_FORMAT, TUNE_MARGIN) and every (N, K) shape x M bucket x
+    candidate list — any change re-measures."""
     import hashlib
     dev = lins[0].wp.device
     props = torch.cuda.get_device_properties(dev)
     so = getattr(native(), "__file__", "") or ""
     st = os.stat(so) if so and os.path.exists(so) else None
     shapes = sorted({(lin.N, lin.K, lin.kind) for lin in lins if getattr(lin, "wp", None) is not None})
-    blob = json_dumps([props.name, props.multi_processor_count, st.st_size if st else 0,
-                       int(st.st_mtime) if st else 0, shapes, sorted(ms), PREFILL_CANDIDATES, PREFILL_RING_CANDIDATES, MID_CANDIDATES])
+    blob = json_dumps([PLAN_FORMAT, TUNE_MARGIN, props.name, props.multi_processor_count, st.st_size if st else 0,
+                       int(st.st_mtime) if st else 0, shapes, sorted(ms), PREFILL_CANDIDATES, PREFILL_RING_CANDIDATES,
+                       MID_CANDIDATES])
     return hashlib.sha1(blob.encode()).hexdigest()
 
 
@@ -861,15 +801,12 @@ def apply_prefill_plans(lins: list, plans: dict) -> None:
             lin.prefill_plan = dict(plan)
 
 
-KERNEL_COPY = os.environ.get("VGATE_KERNEL_COPY", "1") != "0"
-
-
 def host_device_copy(dst: torch.Tensor, src: torch.Tensor, nbytes: int) -> None:
     """Copy the first ``nbytes`` between a pinned host tensor and a device tensor on the current
     stream. GPU: a kernel on the compute queue (csrc/kernels/elementwise.hip copy16_kernel), so the
     step loop's metadata upload and sampled-id download take no SDMA engine hand-off; both tensors
-    must hold ``nbytes`` rounded up to 16. ``VGATE_KERNEL_COPY=0``: hipMemcpyAsync."""
-    if KERNEL_COPY and (dst.is_cuda or src.is_cuda) and native_available():
+    must hold ``nbytes`` rounded up to 16 (without the extension: a non-blocking tensor copy)."""
+    if (dst.is_cuda or src.is_cuda) and native_available():
         native().kernel_copy(dst, src, int(nbytes))
         return
     d8 = dst.view(torch.uint8) if dst.dtype != torch.uint8 else dst
@@ -891,9 +828,10 @@ def sample_workspace(device) -> torch.Tensor:
     return ws
 
 
-# decode GEMMs (<= 16 rows, dense) on the stream-K kernel: one equal share of the packed weight
-# stream per CU (csrc/kernels/gemm_streamk.hip); per-layer override: Linear.dec_sk
-STREAMK_DECODE = os.environ.get("VGATE_STREAMK", "0") == "1"
+# every dense decode GEMM (<= 16 rows) on the stream-K kernel: one equal share of the packed weight
+# stream per CU (csrc/kernels/gemm_streamk.hip); off by default — the measured per-shape plans
+# (Linear.dec_sk, vgate/models/decode_plans.py) pick it where it wins; tests turn it on
+STREAMK_DECODE = False
 _SKWS: dict = {}
 
 

@@ -5,7 +5,7 @@ only two collectives per transformer layer (after the row-parallel o_proj and
 down_proj) plus one all-reduce after the vocab-parallel embedding and one
 all-gather of the vocab-sharded logits — the Megatron layout of SURVEY.md §2.3.1.
 
-All-reduces up to ``VGATE_CUSTOM_AR_MAX_BYTES`` (8 MiB) go to the custom xGMI kernels
+All-reduces up to ``CUSTOM_AR_MAX_BYTES`` (8 MiB) go to the custom xGMI kernels
 (:mod:`vgate.parallel.custom_allreduce`: one-shot to 512 KiB, two-shot above) and the
 logits all-gather to its IPC all-gather, when they are available (all ranks on one node
 with peer access); larger messages, and every collective of a CPU (gloo) group, go
@@ -97,12 +97,19 @@ def normalize_backend(name: str) -> str:
     return "gloo" if "gloo" in name else name
 
 
-def init_tp(tp_size: int, backend: str | None = None) -> TPGroup:
+CUSTOM_AR_MAX_BYTES = 8 << 20
+
+
+def init_tp(tp_size: int, backend: str | None = None, timeout_s: float = 120.0, custom_allreduce: bool = True,
+            fused_allreduce: bool = True) -> TPGroup:
     """Initialise (or return) the TP group from torchrun-style env vars.
 
     With tp_size == 1 no process group is created. With tp_size > 1 the caller
     must have launched ``tp_size`` processes (torchrun) with RANK/WORLD_SIZE/
-    MASTER_ADDR/MASTER_PORT set; LOCAL_RANK selects the GPU.
+    MASTER_ADDR/MASTER_PORT set; LOCAL_RANK selects the GPU. ``timeout_s`` bounds every
+    collective of a new process group (a dead peer fails the group instead of torch's 10 min);
+    ``custom_allreduce`` / ``fused_allreduce``: the IPC kernels and the GEMM-epilogue all-reduce
+    (model.tp_custom_allreduce / model.tp_fused_allreduce).
     """
     global _TP
     if _TP is not None and _TP.size == tp_size:
@@ -121,9 +128,7 @@ def init_tp(tp_size: int, backend: str | None = None) -> TPGroup:
         from datetime import timedelta
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        # a hung collective (dead peer) fails after VGATE_TP_TIMEOUT_S instead of torch's 10 min
-        dist.init_process_group(backend=backend,
-                                timeout=timedelta(seconds=float(os.environ.get("VGATE_TP_TIMEOUT_S", "120"))))
+        dist.init_process_group(backend=backend, timeout=timedelta(seconds=float(timeout_s)))
     world = dist.get_world_size()
     rank = dist.get_rank()
     if world % tp_size:
@@ -137,12 +142,12 @@ def init_tp(tp_size: int, backend: str | None = None) -> TPGroup:
             grp = g
     _TP = TPGroup(rank=rank % tp_size, size=tp_size, group=grp, backend=normalize_backend(backend))
     # the one-shot kernel maps peer buffers over IPC; the group only exchanges the handles
-    if torch.cuda.is_available() and os.environ.get("VGATE_CUSTOM_AR", "1") != "0":
+    if torch.cuda.is_available() and custom_allreduce:
         from vgate.parallel.custom_allreduce import maybe_create
 
         dev = torch.device("cuda", torch.cuda.current_device())
-        _TP.custom_ar = maybe_create(grp, _TP.rank, tp_size, dev,
-                                     max_bytes=int(os.environ.get("VGATE_CUSTOM_AR_MAX_BYTES", str(8 << 20))))
+        _TP.custom_ar = maybe_create(grp, _TP.rank, tp_size, dev, max_bytes=CUSTOM_AR_MAX_BYTES,
+                                     fused=fused_allreduce)
     return _TP
 
 

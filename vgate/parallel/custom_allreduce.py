@@ -29,9 +29,6 @@ log = logging.getLogger("vgate.parallel")
 SIGNAL_BYTES = 65536  # csrc/kernels/launchers.h AR_SIGNAL_BYTES
 MAX_RANKS = 8
 FUSED_TILES = 1024  # launchers.h AR_FUSED_TILES: output columns <= 16 * 1024 for the fused GEMM + all-reduce
-# VGATE_TP_FUSED_AR=0: decode row-parallel GEMMs store their partial and run the separate all-reduce
-# kernel (A/B); default: the all-reduce runs inside the GEMM's epilogue (gemm_epilogue.h epilogue_ar)
-FUSED = os.environ.get("VGATE_TP_FUSED_AR", "1") != "0"
 
 
 class CustomAllReduce:
@@ -45,6 +42,7 @@ class CustomAllReduce:
             raise ValueError(f"custom all-reduce supports 2..{MAX_RANKS} ranks, got {world}")
         self.C = ops.native()
         self.rank, self.world, self.device = rank, world, device
+        self.fused = True
         self.max_bytes = int(max_bytes)
         self.own, self.bases, self._opened = None, [], []
         mine = None
@@ -99,7 +97,7 @@ class CustomAllReduce:
     def fuses(self, lin, x: torch.Tensor, out: torch.Tensor) -> bool:
         """Whether the row-parallel GEMM ``out = x @ lin^T`` can all-reduce in its epilogue
         (decode rows, bf16 output of at most AR_FUSED_TILES 16-column tiles on this device)."""
-        return (FUSED and x.shape[0] <= 16 and out.dtype == torch.bfloat16 and out.device == self.device
+        return (self.fused and x.shape[0] <= 16 and out.dtype == torch.bfloat16 and out.device == self.device
                 and lin.N // 16 <= FUSED_TILES)
 
     def should_gather(self, t: torch.Tensor) -> bool:
@@ -164,7 +162,8 @@ class LoopbackFused:
             self.own = None
 
 
-def maybe_create(group, rank: int, world: int, device: torch.device, max_bytes: int = 8 << 20):
+def maybe_create(group, rank: int, world: int, device: torch.device, max_bytes: int = 8 << 20,
+                 fused: bool = True):
     """The custom all-reduce when every rank of ``group`` is a GPU of this node with peer
     access, else None (callers fall back to RCCL)."""
     if world < 2 or world > MAX_RANKS or device.type != "cuda":
@@ -179,7 +178,12 @@ def maybe_create(group, rank: int, world: int, device: torch.device, max_bytes: 
         log.info("custom all-reduce disabled: no peer access between all ranks")
         return None
     try:
-        return CustomAllReduce(group, rank, world, device, max_bytes)
+        ar = CustomAllReduce(group, rank, world, device, max_bytes)
+        # model.tp_fused_allreduce=false: decode row-parallel GEMMs store their partial and the
+        # separate all-reduce kernel reduces it; default: the all-reduce runs inside the GEMM's
+        # epilogue (gemm_epilogue.h epilogue_ar)
+        ar.fused = fused
+        return ar
     except Exception as e:  # noqa: BLE001 - fall back to RCCL, loudly
         log.warning("custom all-reduce unavailable (%s: %s); using RCCL for every all-reduce", type(e).__name__, e)
         return None

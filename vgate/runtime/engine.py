@@ -73,19 +73,27 @@ class EngineConfig:
     # together — a closed-loop client's next wave — are prefilled in ONE step instead of one step per
     # arrival (each extra prompt step costs ~2 ms on the decode weights; bench.py
     # timed_prefill_steps). A running engine never waits: new requests join the next step.
-    idle_batch_window_ms: float = float(os.environ.get("VGATE_IDLE_BATCH_WINDOW_MS", "3.0"))
-    idle_batch_gap_ms: float = float(os.environ.get("VGATE_IDLE_BATCH_GAP_MS", "0.6"))
+    idle_batch_window_ms: float = 3.0
+    idle_batch_gap_ms: float = 0.6
     # ...but only when a burst is expected: at least 2 requests finished within the last
     # `idle_batch_recent_ms` (a closed-loop client's wave comes back right after the previous wave
     # ended). A request reaching an engine that has been quiet longer (an interactive request) is
     # prefilled at once, with no added time to first token (round-3 ADVICE).
-    idle_batch_recent_ms: float = float(os.environ.get("VGATE_IDLE_BATCH_RECENT_MS", "20"))
+    idle_batch_recent_ms: float = 20.0
     # GPU: time the prefill GEMM decompositions per layer shape and token bucket >= 128 at start-up
     # (ops.tune_prefill) instead of relying on the launcher's heuristic alone
-    prefill_autotune: bool = os.environ.get("VGATE_PREFILL_AUTOTUNE", "1") != "0"
+    prefill_autotune: bool = True
     # measured plans persist per (device, native build, shapes) in this JSON file ("" = off): a restart
     # skips the start-up measurement (ops.tune_prefill_cached)
-    plan_cache: str = os.environ.get("VGATE_PLAN_CACHE", "~/.cache/vgate/gemm_plans.json")
+    plan_cache: str = "~/.cache/vgate/gemm_plans.json"
+    # tensor parallel: collective timeout of the process group and the TP step ring, the custom IPC
+    # all-reduce / all-gather kernels (else RCCL for everything), the all-reduce fused into the
+    # decode row-parallel GEMM epilogue, and the start-up self-check of the custom collectives
+    # against torch.distributed (a mismatch turns the custom paths off group-wide)
+    tp_timeout_seconds: float = 120.0
+    tp_custom_allreduce: bool = True
+    tp_fused_allreduce: bool = True
+    tp_collective_self_check: bool = True
     arch_overrides: dict | None = None
 
     def resolve_device(self) -> torch.device:
@@ -130,7 +138,9 @@ class LLMEngine:
         self.device = cfg.resolve_device()
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
-        self.tp = tp or (init_tp(cfg.tensor_parallel_size) if cfg.tensor_parallel_size > 1 else TPGroup())
+        self.tp = tp or (init_tp(cfg.tensor_parallel_size, timeout_s=cfg.tp_timeout_seconds,
+                                 custom_allreduce=cfg.tp_custom_allreduce, fused_allreduce=cfg.tp_fused_allreduce)
+                         if cfg.tensor_parallel_size > 1 else TPGroup())
         weights = cfg.weights_path
         if weights is None and os.path.isdir(os.path.expanduser(cfg.model)):
             weights = os.path.expanduser(cfg.model)
@@ -627,7 +637,7 @@ class LLMEngine:
         name = None
         if self.tp.is_first:
             name = f"/vgate_ring_{os.getpid()}_{id(self) & 0xffffff:x}"
-            self.ring = C.StepRing(name, True, slots=int(os.environ.get("VGATE_TP_RING_SLOTS", "8")),
+            self.ring = C.StepRing(name, True, slots=8,
                                    slot_bytes=self.runner.meta.nbytes, followers=self.tp.size - 1)
         name = self.tp.broadcast_object(name)
         if not self.tp.is_first:
@@ -641,7 +651,7 @@ class LLMEngine:
         """Rank 0: ship the step plan now in the runner's host metadata buffer to the followers."""
         m = self.runner.meta
         n = m.used_bytes(ns) if mode != self.RING_CAPTURE else m.used_bytes(0)
-        timeout = float(os.environ.get("VGATE_TP_TIMEOUT_S", "120"))
+        timeout = float(self.cfg.tp_timeout_seconds)
         if not self.ring.publish(T, S, ns, nt, mode, m.host, n, timeout):
             raise RuntimeError(f"TP step ring: a follower made no progress for {timeout:.0f}s")
 
@@ -659,9 +669,9 @@ class LLMEngine:
         ar = self.tp.custom_ar
         if ar is None:
             return
-        # the ring words are written only by the ids_to_host node (VGATE_RING_IDS=1, the default);
-        # with the ring off the error word is read by ar.check() below
-        if self.runner.gpu and self.runner.ar_base and getattr(self.runner, "ring_ids", False):
+        # the step graph's ids_to_host node copies the all-reduce's words into the ring slot; a CPU
+        # group (gloo, no ring words) reads the error word through ar.check() below
+        if self.runner.gpu and self.runner.ar_base:
             err, secs, calls = self.runner.collective_words()
             if calls and len(self._ar_ms) < 65536:
                 self._ar_ms.append(1e3 * secs)
@@ -691,7 +701,7 @@ class LLMEngine:
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
         f = self.tp.rank - 1
-        timeout = float(os.environ.get("VGATE_TP_TIMEOUT_S", "120"))
+        timeout = float(self.cfg.tp_timeout_seconds)
         while True:
             buf = r.follower_host_buffer()
             T, S, ns, nt, mode, _ = self.ring.wait(f, buf, timeout)

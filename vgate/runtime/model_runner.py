@@ -19,7 +19,6 @@ from __future__ import annotations
 
 import bisect
 import logging
-import os
 import time
 from dataclasses import dataclass
 
@@ -38,21 +37,6 @@ log = logging.getLogger("vgate.engine")
 DEFAULT_T_BUCKETS = [1, 2, 4, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256, 320, 384, 448, 512, 640, 768, 1024, 1536,
                      2048, 3072, 4096, 6144, 8192, 12288, 16384]
 DEFAULT_S_BUCKETS = [1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024]
-
-
-class _GraphRing:
-    """Identical captures of one bucket; each replay() launches the next one in turn."""
-
-    __slots__ = ("execs", "i")
-
-    def __init__(self, execs):
-        self.execs = execs
-        self.i = 0
-
-    def replay(self) -> None:
-        g = self.execs[self.i]
-        self.i = (self.i + 1) % len(self.execs)
-        g.replay()
 
 
 @dataclass
@@ -112,13 +96,10 @@ class ModelRunner:
             self.fault = ops.fault_word(self.device)  # in-launch hand-off give-ups, read via the ring
             self._last_collected: int | None = None
             self._launches = 0
-            # VGATE_RING_IDS=0: copy the ids after the graph instead (A/B experiments)
-            self.ring_ids = os.environ.get("VGATE_RING_IDS", "1") != "0"
             self.stream = torch.cuda.Stream(self.device)
-            # per-step device time from timing events (VGATE_STEP_TIMING=0: plain completion events)
-            self.step_timing = os.environ.get("VGATE_STEP_TIMING", "1") != "0"
-            self.started = [torch.cuda.Event(enable_timing=self.step_timing) for _ in range(2)]
-            self.dones = [torch.cuda.Event(enable_timing=self.step_timing) for _ in range(2)]
+            # per-step device time from timing events (every 8th step is timed)
+            self.started = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            self.dones = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             self.meta_copied = [torch.cuda.Event() for _ in range(2)]  # TP followers (they never collect)
             self._meta_pending = [False, False]
             self._uncollected = [False, False]  # launch() of buffer k whose step is not collected yet
@@ -127,11 +108,6 @@ class ModelRunner:
         self.graph_hits = 0
         self.graph_misses = 0
         self.defer_capture = True  # miss -> eager step now, capture at the next idle point
-        # execs per bucket, replayed round-robin. In isolation back-to-back launches of ONE
-        # hipGraphExec leave ~0.1 ms between them and alternating two identical execs ~0.015 ms
-        # (benchmarks/graph_relaunch_probe.py), but the engine's step loop (event records +
-        # a D2H copy between replays) shows no difference (88.9 req/s either way): default 1
-        self.graph_copies = max(1, int(os.environ.get("VGATE_GRAPH_COPIES", "1")))
         self.pending_captures: dict[tuple[int, int], int] = {}
         self.defer_capture_failed = False  # a deferred capture raised: stop queueing more
         self.capture_seconds = 0.0
@@ -257,7 +233,7 @@ class ModelRunner:
         logits = self.model.forward(view, self.kv, self.part_size)
         ops.sample(logits, view.temperature, view.top_p, view.top_k, view.seeds, view.offsets,
                    out=self.out_tokens[: view.S])
-        if self.gpu and self.ring_ids:  # last node of the step graph: sampled ids -> pinned ring slot
+        if self.gpu:  # last node of the step graph: sampled ids (+ fault / collective words) -> pinned ring slot
             ops.native().ids_to_host(self.out_tokens, self.out_ring, view.ring_slot, view.S, self.ar_base,
                                      fault=self.fault)
         return logits
@@ -278,17 +254,14 @@ class ModelRunner:
         torch.cuda.synchronize()
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
-        execs = []
-        for _ in range(self.graph_copies):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.pool, stream=s):
-                self._forward_sample(view)
-            execs.append(g)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self.pool, stream=s):
+            self._forward_sample(view)
         torch.cuda.synchronize()
         self.captures += 1
         self.capture_seconds += time.perf_counter() - t0
         log.debug("captured hipGraph T=%d S=%d in %.1f ms", T, S, 1e3 * (time.perf_counter() - t0))
-        return execs[0] if len(execs) == 1 else _GraphRing(execs)
+        return g
 
     @torch.inference_mode()
     def execute(self, batch: ScheduledBatch) -> tuple[list[int], list[bool]]:
@@ -320,7 +293,7 @@ class ModelRunner:
         if self.on_plan is not None:
             self.on_plan(T, S, ns, nt, 0)
         # device time of every 8th step (an event record is a marker packet in the queue)
-        timed = self.step_timing and self._launches % 8 == 0
+        timed = self._launches % 8 == 0
         self._launches += 1
         if timed:
             self.started[k].record()
@@ -349,8 +322,6 @@ class ModelRunner:
             view = self.meta.view(T, S)
             view.num_tokens, view.num_seqs = nt, ns
             self._forward_sample(view)
-        if not self.ring_ids:
-            ops.host_device_copy(self.out_hosts[k], self.out_tokens, 4 * ns)
         self.dones[k].record()
         self.host_ms += 1e3 * (time.perf_counter() - t_host)
         return StepHandle(k, ns, samples, None, t_host, (T, S), eager, timed)
@@ -376,7 +347,7 @@ class ModelRunner:
     def kernel_fault(self, k: int | None = None) -> int:
         """The sticky fault word of the in-launch hand-offs (ops.fault_word) as the step graph's last
         node copied it into ring slot ``k`` (default: the last collected step); 0 = healthy. No sync."""
-        if not self.gpu or not self.ring_ids:
+        if not self.gpu:
             return 0
         if k is None:
             k = self._last_collected if self._last_collected is not None else self._k ^ 1

@@ -16,7 +16,6 @@ from __future__ import annotations
 
 import contextlib
 import contextvars
-import os
 import random
 import threading
 import time
@@ -230,6 +229,3 @@ def attach_traceparent(value: str | None):
     finally:
         _current.reset(tok)
 
-
-if os.getenv("VGATE_TRACING_DEBUG"):
-    _enabled = True
