@@ -9,6 +9,7 @@ bench.py against the dry-run backend with zero simulated latency, so the measure
 request IS the host path, and optionally profiles it (cProfile, top functions by own time).
 
     VGATE_DRY_RUN=true python benchmarks/http_overhead.py [--requests 2000] [--profile]
+    python benchmarks/http_overhead.py --waves    # the wave-boundary gap itself (see main_waves)
 """
 from __future__ import annotations
 
@@ -68,6 +69,69 @@ async def main_async(a):
         st.sort_stats("tottime").print_stats(a.top)
 
 
+class _WaveBackend:
+    """Dry-run backend that answers every request after the same fixed delay: a closed-loop client at
+    concurrency c then runs in waves of c, exactly like the headline load on the engine."""
+    supports_concurrent_calls = True
+    supports_streaming = False
+
+    def __init__(self, delay_s: float):
+        self.delay = delay_s
+        self.arr: list = []
+        self.fin: list = []
+
+    def create_sampling_params(self, temperature, top_p, max_tokens):
+        return {"temperature": temperature, "top_p": top_p, "max_tokens": max_tokens}
+
+    async def agenerate(self, prompt, sp):
+        self.arr.append(time.perf_counter())
+        await asyncio.sleep(self.delay)
+        self.fin.append(time.perf_counter())
+        return {"text": "x" * 256, "num_tokens": sp["max_tokens"], "prompt_tokens": 30, "finish_reason": "length",
+                "metrics": {}}
+
+    def shutdown(self):
+        pass
+
+
+async def main_waves(a):
+    """Wave-boundary gap: from the last response of wave k leaving the backend to the first (and the
+    last) request of wave k+1 reaching it — the engine's idle time per wave in bench.py
+    (timed_engine_idle_ms / timed_waves), without a GPU."""
+    from vgate.api.app import create_app
+    from vgate.api.server import make_server
+    from vgate.config import VGateConfig
+    from vgate.engine import VGateEngine
+
+    cfg = VGateConfig(role="gateway", batch={"max_batch_size": a.concurrency}, cache={"enabled": True, "maxsize": 1000},
+                      logging={"level": "WARNING", "json_format": True})
+    be = _WaveBackend(0.02)
+    eng = VGateEngine(model_config=cfg.model, worker_config=cfg.worker, backend=be, dry_run=True)
+    app = create_app(cfg, engine=eng)
+    server = make_server(app, "127.0.0.1", a.port, a.server)
+    task = asyncio.create_task(server.serve())
+    while not server.started:
+        await asyncio.sleep(0.05)
+    bench.t_run = time.perf_counter()
+    c = a.concurrency
+    await bench.run_load(a.port, 10 * c, c, 64, 0, 0, client=a.client)
+    be.arr.clear()
+    be.fin.clear()
+    nw = max(10, a.requests // c)
+    await bench.run_load(a.port, nw * c, c, 64, 0, 10_000_000, client=a.client)
+    server.should_exit = True
+    await task
+    first, last = [], []
+    for w in range(1, nw):
+        arr = sorted(be.arr[w * c:(w + 1) * c])
+        fin = sorted(be.fin[(w - 1) * c:w * c])
+        first.append(arr[0] - fin[-1])
+        last.append(arr[-1] - fin[-1])
+    print(json.dumps({"waves": nw, "concurrency": c, "server": a.server, "client": a.client,
+                      "gap_first_arrival_ms_p50": round(1e3 * bench.pct(first, 50), 3),
+                      "gap_last_arrival_ms_p50": round(1e3 * bench.pct(last, 50), 3)}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--requests", type=int, default=2000)
@@ -78,8 +142,9 @@ def main():
     ap.add_argument("--client", default="lean", choices=["lean", "aiohttp"])
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--top", type=int, default=35)
+    ap.add_argument("--waves", action="store_true", help="measure the wave-boundary gap instead")
     a = ap.parse_args()
-    asyncio.run(main_async(a))
+    asyncio.run(main_waves(a) if a.waves else main_async(a))
 
 
 if __name__ == "__main__":

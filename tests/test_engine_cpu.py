@@ -234,3 +234,17 @@ def test_idle_admission_window_only_waits_for_an_expected_wave():
     finally:
         eng._running = False
     eng.run_until_idle()
+    # the whole wave is back (as many arrivals as recent finishes): the step starts without the gap
+    eng._finish_times.clear()
+    eng._finish_times.extend([time.perf_counter()] * 2)
+    eng.add_request("wave1a", params=sp, prompt_ids=[5, 6, 9])
+    eng.add_request("wave1b", params=sp, prompt_ids=[5, 6, 10])
+    eng._running = True
+    try:
+        with eng._cv:
+            t0 = time.perf_counter()
+            eng._coalesce_arrivals()
+            assert time.perf_counter() - t0 < 0.01
+    finally:
+        eng._running = False
+    eng.run_until_idle()

@@ -63,10 +63,13 @@ def _generate(eng, prompts=None):
 LONG = {"long600": [7 + (j * 13) % 450 for j in range(600)], "short": [9, 8, 7, 6, 5]}
 
 
-def _worker(rank, world, port, path, q, eager=False, env=None, tokens=320, prompts=None, opts=None):
+def _worker(rank, world, port, path, q, eager=False, env=None, tokens=320, prompts=None, opts=None, inject=False):
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                           MASTER_PORT=str(port), **(env or {}))
+        if inject:  # the start-up self-check of the last rank sees a corrupted all-reduce result
+            from vgate.parallel import custom_allreduce
+            custom_allreduce._INJECT_SELF_CHECK_FAULT = True
         import torch.distributed as dist
 
         from vgate.runtime.engine import LLMEngine
@@ -77,6 +80,10 @@ def _worker(rank, world, port, path, q, eager=False, env=None, tokens=320, promp
         assert eng.tp.size == world and eng.tp.rank == rank and eng.tp.backend == "gloo"
         eng.runner.defer_capture = False
         assert eng.model.num_heads_local * world == eng.arch.num_heads
+        if inject:
+            assert eng.tp.custom_ar is None and eng.tp_self_check.startswith("failed"), eng.tp_self_check
+        else:
+            assert eng.tp_self_check == "passed", eng.tp_self_check
         if rank == 0:
             out = _generate(eng, prompts)
             used_ar = eng.tp.custom_ar is not None and eng.tp.custom_ar.calls > 0
@@ -131,6 +138,32 @@ def test_tp2_on_gpu_matches_tp1(tmp_path, eager, fused):
     assert used_ar, "the custom all-reduce was not used between the two ranks"
     assert tp_out == ref
     assert (graphs > 0) == (not eager), graphs
+
+
+@pytest.mark.timeout(300)
+def test_tp2_collective_self_check_failure_falls_back_to_tp1_tokens(tmp_path):
+    """Start-up self-check: one rank's check sees a wrong custom all-reduce result (test hook); the
+    verdict is agreed over the group, EVERY rank drops the custom IPC collectives (RCCL / gloo for
+    everything, eager steps on this gloo group) and the generation still equals TP = 1."""
+    path = _ckpt(tmp_path)
+    ref_eng = __import__("vgate.runtime.engine", fromlist=["LLMEngine"]).LLMEngine(_cfg(path, 1, True))
+    ref = _generate(ref_eng)
+    del ref_eng
+    torch.cuda.synchronize()
+    port = _free_port()
+    _, q, procs = _spawn(2, _worker, lambda r, q: (r, 2, port, path, q, False, None, 320, None, None, True))
+    try:
+        results = [q.get(timeout=240) for _ in procs]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    errs = [r[1] for r in results if r[0] == "err"]
+    assert not errs, errs[0]
+    tp_out, used_ar, graphs = next(r[1] for r in results if r[1] is not None)
+    assert not used_ar
+    assert tp_out == ref
 
 
 def _ckpt(tmp_path):

@@ -622,6 +622,7 @@ async def _engine_metrics_loop(st: AppState, period: float = 1.0):
             if callable(h):
                 M.ENGINE_HEALTHY.set(1 if h() else 0)
             M.ENGINE_GRAPH_HIT_RATIO.set(s.get("graph_hit_ratio", 0.0))
+            M.ENGINE_TP_CUSTOM_COLLECTIVES.set(s.get("tp_custom_collectives", 0))
             drain_ar = getattr(getattr(b, "engine", None), "drain_allreduce_times", None)
             if callable(drain_ar):
                 for ms in drain_ar():

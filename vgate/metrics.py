@@ -103,6 +103,9 @@ ENGINE_EAGER_STEPS = _metric(Counter, "vgate_engine_eager_steps_total",
                              "Steps run without a captured hipGraph (first sight of a token/sequence bucket)")
 ENGINE_GRAPH_HIT_RATIO = _metric(Gauge, "vgate_engine_hipgraph_hit_ratio", "hipGraph replays / all steps (lifetime)")
 ENGINE_HEALTHY = _metric(Gauge, "vgate_engine_healthy", "1 while the engine passes its fault and watchdog checks")
+ENGINE_TP_CUSTOM_COLLECTIVES = _metric(Gauge, "vgate_engine_tp_custom_collectives",
+                                       "1 while the TP group runs its custom IPC collectives (0: RCCL only, e.g. "
+                                       "after a failed start-up self-check)")
 ENGINE_ALLREDUCE_SECONDS = _metric(Histogram, "vgate_engine_allreduce_seconds",
                                    "Tensor-parallel all-reduce time per decode step (probed on the engine's own "
                                    "comm path: every layer's two collectives at the decode message size)",

@@ -29,6 +29,7 @@ log = logging.getLogger("vgate.parallel")
 SIGNAL_BYTES = 65536  # csrc/kernels/launchers.h AR_SIGNAL_BYTES
 MAX_RANKS = 8
 FUSED_TILES = 1024  # launchers.h AR_FUSED_TILES: output columns <= 16 * 1024 for the fused GEMM + all-reduce
+_INJECT_SELF_CHECK_FAULT = False  # tests: the last rank's self-check sees a wrong all-reduce result
 
 
 class CustomAllReduce:
@@ -115,6 +116,71 @@ class CustomAllReduce:
         """Raise if a wait timed out since the last check (a peer never arrived)."""
         if self.C.ar_error(self.own):
             raise RuntimeError("custom all-reduce: a peer did not arrive within the spin limit")
+
+    def self_check(self, group, backend: str, hidden: int, row_lin=None) -> tuple[bool, list[str]]:
+        """Start-up cross-check of every custom path against ``torch.distributed`` on ``group``
+        (RCCL on a node; every rank calls it at the same point, before any graph capture).
+
+        Cases: the one-shot kernel at decode sizes (1 / 8 / 16 rows x ``hidden``), the two-shot kernel
+        at chunk sizes (256 / 512 rows, within ``max_bytes``), the IPC all-gather of a logits-shaped
+        fp32 block, and — when ``row_lin`` (a row-parallel Linear of the model) is given and the
+        fused epilogue is on — the GEMM with the all-reduce in its epilogue against the same GEMM's
+        partial reduced by torch.distributed. Sums are compared within bf16 rounding; a wait that
+        gave up (the sticky error word) fails the check too. Returns (ok on EVERY rank, per-case
+        failure notes of this rank); the verdict is agreed over the group, so all ranks take the
+        same decision (the engine then drops the custom paths group-wide)."""
+        dev = self.device
+        notes: list[str] = []
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(4242 + 7919 * self.rank)
+
+        def ref_sum(t: torch.Tensor) -> torch.Tensor:
+            r = t.float() if backend == "nccl" else t.float().cpu()
+            dist.all_reduce(r, group=group)
+            return r.to(dev)
+
+        def close(a: torch.Tensor, b: torch.Tensor, what: str) -> None:
+            a, b = a.float(), b.float()
+            scale = float(b.abs().max()) + 1e-6
+            err = float((a - b).abs().max()) / scale
+            if not torch.isfinite(a).all() or err > 2e-2:
+                notes.append(f"{what}: max rel err {err:.3g}")
+
+        def rnd(*shape, dtype=torch.bfloat16):
+            return torch.randn(*shape, generator=gen, device=dev).to(dtype)
+
+        with torch.cuda.device(dev):
+            for rows, form in ((1, -1), (8, -1), (16, -1), (256, 1), (512, 1)):
+                if rows * hidden * 2 > self.max_bytes:
+                    continue
+                t = rnd(rows, hidden)
+                want = ref_sum(t)
+                got = self.all_reduce(t.clone(), two_shot=form)
+                if _INJECT_SELF_CHECK_FAULT and self.rank == self.world - 1:
+                    got[0, :8] += 64.0  # test hook: as if a peer's slice had been read stale
+                close(got, want, f"{'one' if form < 0 else 'two'}-shot all-reduce {rows}x{hidden}")
+            g = rnd(8, 1024, dtype=torch.float32)
+            if self.should_gather(g):
+                got = self.all_gather(g)
+                want = [torch.empty_like(g if backend == "nccl" else g.cpu()) for _ in range(self.world)]
+                dist.all_gather(want, g if backend == "nccl" else g.cpu(), group=group)
+                close(got, torch.stack([w.to(dev) for w in want]), "all-gather 8x1024 f32")
+            if row_lin is not None and self.fused and getattr(row_lin, "wp", None) is not None:
+                from vgate import ops
+                x = rnd(8, row_lin.K)
+                out = torch.zeros(8, row_lin.N, dtype=torch.bfloat16, device=dev)
+                if self.fuses(row_lin, x, out):
+                    part = ops.linear(x, row_lin)
+                    want = ref_sum(part)
+                    ops.linear(x, row_lin, out=out, ar=self)
+                    close(out, want, f"fused GEMM epilogue all-reduce 8x{row_lin.N}")
+            torch.cuda.synchronize(dev)
+            if self.C.ar_error(self.own):
+                notes.append("a wait gave up (error word set)")
+        verdicts = [None] * self.world
+        dist.all_gather_object(verdicts, notes, group=group)
+        bad = [(r, v) for r, v in enumerate(verdicts) if v]
+        return not bad, [f"rank {r}: {'; '.join(v)}" for r, v in bad]
 
     def close(self) -> None:
         if self.own is None:

@@ -152,6 +152,9 @@ class LLMEngine:
             torch.cuda.synchronize()
         self.load_seconds = time.perf_counter() - t0
         self.num_blocks = self._size_kv()
+        self.tp_self_check = "n/a"
+        if self.tp.custom_ar is not None and cfg.tp_collective_self_check and not self.tp.simulated:
+            self._collective_self_check()
         self.kv_caches = allocate_kv_tensors(self.arch.num_layers, self.num_blocks, self.model.num_kv_heads_local,
                                              self.arch.head_dim, self.device, block_size=cfg.block_size)
         self.kvm = KVCacheManager(self.num_blocks, cfg.block_size, cfg.enable_prefix_caching)
@@ -245,6 +248,26 @@ class LLMEngine:
         if n < (1 if cfg.num_kv_blocks else 16):
             raise RuntimeError(f"not enough memory for the KV cache ({n} blocks)")
         return n
+
+    def _collective_self_check(self) -> None:
+        """Every rank, before the first graph capture: the custom collectives (one-shot, two-shot,
+        all-gather, the fused GEMM-epilogue all-reduce) against torch.distributed on the group. The
+        verdict is agreed over the group; on a mismatch or a give-up every rank drops the custom
+        paths (RCCL for every collective from then on), logs it and reports it (/stats
+        tp_self_check, gauge vgate_engine_tp_custom_collectives)."""
+        car = self.tp.custom_ar
+        t0 = time.perf_counter()
+        ok, notes = car.self_check(self.tp.group, self.tp.backend, self.arch.hidden_size, self.model.layers[0].o)
+        if ok:
+            self.tp_self_check = "passed"
+            log.info("TP collective self-check passed in %.2fs (custom all-reduce / all-gather == %s)",
+                     time.perf_counter() - t0, self.tp.backend)
+            return
+        self.tp_self_check = "failed: " + " | ".join(notes)
+        log.error("TP collective self-check FAILED (%s); the custom IPC collectives are disabled on every rank "
+                  "of the group, all collectives go through %s", "; ".join(notes), self.tp.backend)
+        car.close()
+        self.tp.custom_ar = None
 
     # --------------------------------------------------------------- lifecycle
     def start(self) -> None:
@@ -764,6 +787,7 @@ class LLMEngine:
             "max_cycle_tokens_seqs": list(st.max_cycle_bucket),
             "preemptions": self.scheduler.num_preemptions, "prefix_cache_hits": int(getattr(self.kvm.alloc, "hits", 0)),
             "healthy": self.healthy,
+            "tp_custom_collectives": int(self.tp.custom_ar is not None), "tp_self_check": self.tp_self_check,
             "waves": st.waves, "wave_sum_ms": [round(1e3 * st.wave_first_s, 3), round(1e3 * st.wave_spread_s, 3),
                                                 round(1e3 * st.wave_tail_s, 3)], "wave_requests": st.wave_size,
         }
