@@ -15,7 +15,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 import torch  # noqa: E402
 
-from benchmarks.mall_probe import timeline_graph  # noqa: E402
+from benchmarks.tlgraph import timeline_graph  # noqa: E402
 
 
 def block_stats(C, fn):

@@ -20,7 +20,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 import torch  # noqa: E402
 
-from benchmarks.mall_probe import timeline_graph  # noqa: E402
+from benchmarks.tlgraph import timeline_graph  # noqa: E402
 from vgate import ops  # noqa: E402
 
 SHAPES = {"down": (1536, 8960), "o_proj": (1536, 1536), "lm_head": (151936, 1536)}

@@ -2,7 +2,7 @@
 device? Times the host-side cost of back-to-back replays of one ~1 ms graph vs
 alternating two identical graphs (MI355X, torch.cuda.CUDAGraph = hipGraphExec).
 
-    python benchmarks/graph_relaunch_probe.py
+    python benchmarks/probes/graph_relaunch_probe.py
 """
 import json
 import time

@@ -9,57 +9,25 @@ of weight copies (every launch cold in L2 and MALL) in three forms:
 Block spans come from the launch timeline (TLScope): the GEMM span with and without the
 sweep in front is the MALL-hit speed-up; the sweep span is its cost when it cannot be hidden.
 
-    python benchmarks/mall_probe.py
+    python benchmarks/probes/mall_probe.py
 """
 from __future__ import annotations
 
 import json
 import math
 import sys
-from collections import defaultdict
 from pathlib import Path
 
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 import torch  # noqa: E402
 
 from vgate import ops  # noqa: E402
+from tlgraph import timeline_graph  # noqa: E402
 
 SHAPES = [("qkv", 2048, 1536, "plain", 0), ("o_proj", 1536, 1536, "plain", 0), ("gate_up", 17920, 1536, "silu", 2),
           ("down", 1536, 8960, "plain", 0)]
-
-
-def timeline_graph(C, fns, reps=3):
-    """Capture fns() in a graph with timeline slots, replay, return {name: [spans_us]}."""
-    buf = torch.zeros(1 << 20, dtype=torch.int64, device="cuda")
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        fns()
-    torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    C.timeline_start(buf)
-    with torch.cuda.graph(g, stream=s):
-        fns()
-    used = C.timeline_stop()
-    ents = C.timeline_entries()
-    spans = defaultdict(list)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    wall = []
-    for _ in range(reps):
-        buf.zero_()
-        e0.record()
-        g.replay()
-        e1.record()
-        torch.cuda.synchronize()
-        wall.append(e0.elapsed_time(e1) * 1e3)
-    t = buf[:used].view(-1, 2).cpu()
-    for name, off, nb in ents:
-        blk = t[off // 2: off // 2 + nb]
-        ok = blk[:, 0] > 0
-        if ok.any():
-            spans[name].append((int(blk[ok, 1].max()) - int(blk[ok, 0].min())) / 100.0)
-    return spans, min(wall)
 
 
 def main():

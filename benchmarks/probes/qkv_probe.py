@@ -4,7 +4,7 @@ Block spans (launch timeline) of the decode QKV projection with its fusions swit
 at a time: plain GEMM, + deferred RMSNorm row scale, + bias, + RoPE / paged KV-cache write
 epilogue, all of them (the engine's form). Weights cycle through > 600 MB of copies.
 
-    python benchmarks/qkv_probe.py
+    python benchmarks/probes/qkv_probe.py
 """
 from __future__ import annotations
 
@@ -13,11 +13,11 @@ import math
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 
 import torch  # noqa: E402
 
-from benchmarks.mall_probe import timeline_graph  # noqa: E402
+from benchmarks.tlgraph import timeline_graph  # noqa: E402
 from vgate import ops  # noqa: E402
 
 

@@ -5,7 +5,7 @@ weights, as in a decode step), replayed back to back; per-launch time = graph ti
 launch boundaries included, as in the engine). Stream-K variants: (waves, blocks per CU,
 k-steps per register group).
 
-    python benchmarks/sk_probe.py [--model qwen] [--m 8]
+    python benchmarks/probes/sk_probe.py [--model qwen] [--m 8]
 """
 from __future__ import annotations
 
@@ -15,7 +15,7 @@ import math
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 
 import torch  # noqa: E402
 

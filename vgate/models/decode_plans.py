@@ -11,7 +11,7 @@ Key: (N, K, layout, weight kind) of the packed weight; layout "qkv" / "silu" / "
 Value: (waves, K slices, column tiles per block) of the tile-per-block kernels, or
 ("sk", waves, blocks per CU, k-steps per register group) for the stream-K kernel
 (csrc/kernels/gemm_streamk.hip: one equal share of the weight stream per CU), which wins on the
-large matrices where the tile count leaves CUs uneven (benchmarks/sk_probe.py,
+large matrices where the tile count leaves CUs uneven (benchmarks/probes/sk_probe.py,
 profiles/r4_streamk_probe.log).
 """
 from __future__ import annotations
