@@ -78,7 +78,9 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
     const int m = m_base + mb * 16 + (XP > 1 ? r16 % R : r16);
     xok[mb] = m < p.M;
     xrow[mb] = p.x + (size_t)row_of(p, m) * p.lda + 8 * (lane >> 4) + (XP > 1 ? (r16 / R) * 32 : 0);
-    ssr[mb] = 0.f;
+    // NORM 3: the producer's per-tile sums of squares of row (lane & 15), issued with the first
+    // weight group and used only in gemm_finish (wave 0 of slice 0 carries them)
+    ssr[mb] = (NORM == 3 && wid == 0 && sp.slice == 0) ? prenorm_ss(p, m_base + mb * 16 + r16, lane >> 4) : 0.f;
   }
   const bf16_t* nw_ptr = p.norm_w ? p.norm_w + 8 * (lane >> 4) : nullptr;
 
@@ -124,7 +126,7 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
       if (k0 + u >= kend)
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb) a[u][mb] = make_uint4(0, 0, 0, 0);
-    if constexpr (NORM) {
+    if constexpr (NORM == 1 || NORM == 2) {
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -1072,6 +1074,10 @@ static bool launch_awq_stream(GemmParams p, const GemmArgs& g, hipStream_t st) {
 
 template <int NTB, int EPI, int NORM, bool AWQ>
 static void launch_m(GemmParams p, const GemmArgs& g, hipStream_t st) {
+  if constexpr (!AWQ && NORM == 3) {  // bf16 consumer of the RMSNorm hand-off: decode rows only (binding)
+    launch_one<1, NTB, EPI, 3, false>(p, g, st);
+    return;
+  }
   if constexpr (AWQ) {
     // g.ntb: -1 forces the LDS-staged kernel, -2 the K-split awq_gemm_kernel (sweeps / tests)
     if constexpr (NORM != 2) {  // (the gamma-folded row-scale mode has no int4 form)
@@ -1121,7 +1127,7 @@ void dispatch_epi(GemmParams p, const GemmArgs& g, hipStream_t st) {
   do {                                                                          \
     if (norm == 1) launch_m<NTB_, EPI, 1, AWQ>(p, g, st);                       \
     else if (norm == 2 && !AWQ) launch_m<NTB_, EPI, 2, AWQ>(p, g, st);          \
-    else if (norm == 3 && AWQ) launch_m<NTB_, EPI, 3, AWQ>(p, g, st);           \
+    else if (norm == 3) launch_m<NTB_, EPI, 3, AWQ>(p, g, st);                  \
     else launch_m<NTB_, EPI, 0, AWQ>(p, g, st);                                 \
   } while (0)
   if constexpr (EPI == EPI_SILU) {  // self-contained 16-column tiles (8 gate + 8 up); g.ntb 2 / 4: tiles per block (sweeps)

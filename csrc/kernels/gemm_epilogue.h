@@ -40,7 +40,8 @@ struct GemmParams {
   // RMSNorm hand-off for the int4 consumers (decode, TP = 1). Producer (EPI_BF16 residual GEMMs:
   // o_proj, down_proj): hg = bf16(h * gamma) of the output rows h it stores, and per-(row, 16-column
   // tile) sums of squares of h -> ssp_out [M][N/16]. Consumer (NORM == 3): x = hg (gamma already
-  // applied), row scale rsqrt(sum of ssp_in[m][0..ssn) / K + eps) — no gamma loads, no x^2 pass.
+  // applied; int4) or x = h with gamma folded into the bf16 weights (hg null), row scale
+  // rsqrt(sum of ssp_in[m][0..ssn) / K + eps) — no gamma loads, no x^2 pass.
   bf16_t* hg; const bf16_t* hg_gamma; float* ssp_out; const float* ssp_in; int ssn;
   unsigned long long* dbg_ts;  // per-block [start, end] realtime stamps (profiling), or null
   ArFused ar;                  // world 0: no fused all-reduce
@@ -142,9 +143,9 @@ __device__ __forceinline__ void epi_pre_b(const GemmParams& p, EpiPre<NTB>& e, i
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-// EPI_BF16 with the RMSNorm hand-off (p.hg): out = bf16(bf16(acc) + bias + res) as the plain
-// epilogue, plus hg = bf16(out * gamma) and the tile's sum of out^2 (lane groups folded, group 0
-// stores ssp_out[m][tile]).
+// EPI_BF16 with the RMSNorm hand-off (p.ssp_out): out = bf16(bf16(acc) + bias + res) as the plain
+// epilogue, plus the tile's sum of out^2 (lane groups folded, group 0 stores ssp_out[m][tile]) and,
+// for int4 consumers (p.hg), hg = bf16(out * gamma).
 template <int NTB, bool have>
 __device__ __forceinline__ void epilogue_norm_out(const GemmParams& p, const f32x4 (&v)[NTB], int m, int nt0, int nsub,
                                                   const EpiPre<NTB> e, bool valid) {
@@ -175,12 +176,14 @@ __device__ __forceinline__ void epilogue_norm_out(const GemmParams& p, const f32
       pk.y = pack_bf2(o[2], o[3]);
       *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + n) = pk;
       const float h4[4] = {bf_lo(pk.x), bf_hi(pk.x), bf_lo(pk.y), bf_hi(pk.y)};  // the stored values
-      const uint2 g = *reinterpret_cast<const uint2*>(p.hg_gamma + n);
-      const float g4[4] = {bf_lo(g.x), bf_hi(g.x), bf_lo(g.y), bf_hi(g.y)};
-      uint2 hk;
-      hk.x = pack_bf2(h4[0] * g4[0], h4[1] * g4[1]);
-      hk.y = pack_bf2(h4[2] * g4[2], h4[3] * g4[3]);
-      *reinterpret_cast<uint2*>(p.hg + (size_t)m * p.ldo + n) = hk;
+      if (p.hg != nullptr) {  // int4 consumers read h * gamma; bf16 ones fold gamma into W (ss only)
+        const uint2 g = *reinterpret_cast<const uint2*>(p.hg_gamma + n);
+        const float g4[4] = {bf_lo(g.x), bf_hi(g.x), bf_lo(g.y), bf_hi(g.y)};
+        uint2 hk;
+        hk.x = pack_bf2(h4[0] * g4[0], h4[1] * g4[1]);
+        hk.y = pack_bf2(h4[2] * g4[2], h4[3] * g4[3]);
+        *reinterpret_cast<uint2*>(p.hg + (size_t)m * p.ldo + n) = hk;
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) s2 += h4[i] * h4[i];
     }
@@ -196,9 +199,24 @@ __device__ __forceinline__ float prenorm_ss(const GemmParams& p, int m, int quar
   if (m >= p.M) return 0.f;
   const float* s = p.ssp_in + (size_t)m * p.ssn;
   const int q0 = (p.ssn * quarter) >> 2, q1 = (p.ssn * (quarter + 1)) >> 2;
-  // every load of a 32-value chunk in flight together: one round trip per chunk (24 values per lane
-  // at K = 1536; 8-value steps cost three dependent round trips there)
   float acc = 0.f;
+  if ((p.ssn & 15) == 0) {
+    // 16-B loads (a quarter is a multiple of 4 values, 16-B aligned): at K = 1536 six per lane,
+    // all in flight together
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(s + q0);
+    const int n4 = (q1 - q0) >> 2;
+    for (int t0 = 0; t0 < n4; t0 += 8) {
+      f32x4 r[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) r[u] = s4[min(t0 + u, n4 - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (t0 + u < n4) acc += (r[u][0] + r[u][1]) + (r[u][2] + r[u][3]);
+    }
+    return acc;
+  }
+  // every load of a 32-value chunk in flight together: one round trip per chunk (8-value steps
+  // cost three dependent round trips at K = 1536)
   for (int t0 = q0; t0 < q1; t0 += 32) {
     float r[32];
 #pragma unroll
@@ -330,7 +348,7 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[N
     return;
   }
   if constexpr (EPI == EPI_BF16) {
-    if (p.hg != nullptr) {  // every lane calls in: the tile's sum of squares is a cross-lane fold
+    if (p.ssp_out != nullptr) {  // every lane calls in: the tile's sum of squares is a cross-lane fold
       epilogue_norm_out<NTB, have>(p, v, m, nt0, nsub, e, valid);
       return;
     }

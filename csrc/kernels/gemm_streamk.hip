@@ -401,7 +401,7 @@ bool sk_launch(const GemmParams& p, const SkParams& s, int xp, int w, int ua, in
 
 bool launch_gemm_sk(const GemmArgs& g, hipStream_t st) {
   if (g.M <= 0) return true;
-  if (g.M > 16 || g.row_idx != nullptr || g.norm_w != nullptr || g.hg != nullptr || g.ssp_in != nullptr ||
+  if (g.M > 16 || g.row_idx != nullptr || g.norm_w != nullptr || g.ssp_out != nullptr || g.ssp_in != nullptr ||
       g.sk_pub == nullptr || g.K % 32 != 0)
     return false;
   if (g.epi == EPI_QKV && (g.N / 16) % 2 != 0) return false;

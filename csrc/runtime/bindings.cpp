@@ -125,22 +125,29 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
     TORCH_CHECK(group == 128 && awq_szp->numel() == N / 16 * (K / 128) * 32, "awq_szp: [N/16][K/128][4][8], group 128");
     g.awq_szp = reinterpret_cast<const uint16_t*>(awq_szp->data_ptr());
   }
-  if (hg_out.has_value() && hg_out->defined()) {
-    // producer of the int4 consumers' RMSNorm hand-off: decode rows, bf16 residual epilogue
-    TORCH_CHECK(epi == 0 && M <= 16 && hg_gamma.has_value() && ssp_out.has_value(), "hg_out: epi 0, M <= 16, gamma, ssp_out");
-    CHECK_DEV(*hg_out); CHECK_DT(*hg_out, torch::kBFloat16); CHECK_LASTDIM(*hg_out);
-    TORCH_CHECK(hg_out->stride(0) == out.stride(0) && hg_out->size(0) >= M && hg_out->size(1) >= N, "hg_out: like out");
-    TORCH_CHECK(hg_gamma->numel() == N, "hg_gamma: N elements");
+  if (ssp_out.has_value() && ssp_out->defined()) {
+    // producer of the next RMSNorm's hand-off: decode rows, bf16 residual epilogue. It stores the
+    // per-(row, 16-column tile) sums of squares of its output; for int4 consumers also hg = out * gamma
+    TORCH_CHECK(epi == 0 && M <= 16, "ssp_out: epi 0, M <= 16");
     CHECK_DEV(*ssp_out); CHECK_DT(*ssp_out, torch::kFloat32);
     TORCH_CHECK(ssp_out->numel() >= M * (N / 16), "ssp_out: [M][N/16]");
-    g.hg = reinterpret_cast<uint16_t*>(hg_out->data_ptr());
-    g.hg_gamma = opt_bf16(hg_gamma);
     g.ssp_out = reinterpret_cast<float*>(ssp_out->data_ptr());
+    if (hg_out.has_value() && hg_out->defined()) {
+      CHECK_DEV(*hg_out); CHECK_DT(*hg_out, torch::kBFloat16); CHECK_LASTDIM(*hg_out);
+      TORCH_CHECK(hg_out->stride(0) == out.stride(0) && hg_out->size(0) >= M && hg_out->size(1) >= N, "hg_out: like out");
+      TORCH_CHECK(hg_gamma.has_value() && hg_gamma->numel() == N, "hg_gamma: N elements");
+      g.hg = reinterpret_cast<uint16_t*>(hg_out->data_ptr());
+      g.hg_gamma = opt_bf16(hg_gamma);
+    }
+  } else {
+    TORCH_CHECK(!(hg_out.has_value() && hg_out->defined()), "hg_out needs ssp_out");
   }
   if (ssp_in.has_value() && ssp_in->defined()) {
-    TORCH_CHECK(awq && M <= 16 && !g.norm_w && !rownorm, "ssp_in: int4 decode consumers without another norm mode");
+    // consumer: int4 (x = h * gamma) or bf16 with gamma folded into the packed weights (x = h)
+    TORCH_CHECK(M <= 16 && !g.norm_w && !rownorm, "ssp_in: decode consumers without another norm mode");
     CHECK_DEV(*ssp_in); CHECK_DT(*ssp_in, torch::kFloat32);
-    TORCH_CHECK(ssp_in->numel() >= M * (K / 16), "ssp_in: [M][K/16]");
+    TORCH_CHECK(ssp_in->numel() >= M * (K / 16) && (reinterpret_cast<uintptr_t>(ssp_in->data_ptr()) % 16) == 0,
+                "ssp_in: [M][K/16], 16-B aligned");
     g.ssp_in = reinterpret_cast<const float*>(ssp_in->data_ptr());
     g.ssn = (int)(K / 16);
   }
@@ -155,7 +162,7 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
     // TP row-parallel decode GEMM + all-reduce in the epilogue (vgate/parallel/custom_allreduce.py)
     const int world = (int)ar_bases.size();
     TORCH_CHECK(world <= 8 && ar_rank >= 0 && ar_rank < world, "gemm ar: world 1..8, rank in range");
-    TORCH_CHECK(epi == 0 && M <= 16 && !g.hg && N / 16 <= vgate::AR_FUSED_TILES,
+    TORCH_CHECK(epi == 0 && M <= 16 && !g.ssp_out && N / 16 <= vgate::AR_FUSED_TILES,
                 "gemm ar: bf16 epilogue, M <= 16, no norm hand-off, N <= 16 * AR_FUSED_TILES");
     TORCH_CHECK(ar_fused_off >= vgate::AR_SIGNAL_BYTES, "gemm ar: fused region offset");
     for (int r = 0; r < world; ++r) g.ar_fused[r] = reinterpret_cast<char*>(ar_bases[r]) + ar_fused_off;

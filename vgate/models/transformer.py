@@ -216,28 +216,39 @@ class DecoderModel:
         # int4 decode steps: the residual GEMMs (o_proj, down_proj) hand the NEXT RMSNorm over —
         # h * gamma plus per-tile sums of h^2 — so the int4 qkv / gate_up kernels read normed rows
         # (no gamma loads, no x^2 pass; ops.linear norm_out / prenorm)
-        hand = self.quant == "awq" and tp.size == 1 and T <= 16
+        # decode steps (TP = 1): the residual GEMMs (o_proj, down_proj) hand the NEXT RMSNorm over — the
+        # per-(row, 16-column tile) sums of h^2 of the rows they store — so the consumer (qkv, gate_up)
+        # applies the row scale from them: no x^2 pass beside its weight stream (ops.linear norm_out /
+        # prenorm). int4 consumers also get hg = h * gamma (their weights carry no gamma); bf16 consumers
+        # read h itself (gamma folded into the packed weights), except on a stream-K plan (no hand-off there)
+        hand = tp.size == 1 and T <= 16 and dev.type == "cuda"
+        awq = self.quant == "awq"
         if hand:
-            hg = torch.empty(T, a.hidden_size, dtype=torch.bfloat16, device=dev)
+            hg = torch.empty(T, a.hidden_size, dtype=torch.bfloat16, device=dev) if awq else None
             ssp = torch.empty(T, a.hidden_size // 16, dtype=torch.float32, device=dev)
         nl = len(self.layers)
+
+        def takes(lin) -> bool:  # a consumer of the hand-off
+            return hand and (awq or (lin.norm_gamma is not None and not lin.dec_sk))
+
         for li, L in enumerate(self.layers):
             kc, vc = kv_caches[li]
             qkv_args = dict(positions=sv.positions, slots=sv.slots, cos_sin=self.cos_sin, k_cache=kc, v_cache=vc,
                             hq=sh.hq, hkv=sh.hkv)
-            if hand and li > 0:
-                ops.linear(hg, L.qkv, out=q, prenorm=(ssp, eps), qkv=qkv_args)
+            if li > 0 and takes(L.qkv):
+                ops.linear(hg if awq else resid, L.qkv, out=q, prenorm=(ssp, eps), qkv=qkv_args)
             else:
                 ops.linear(resid, L.qkv, out=q, norm=(L.in_norm, eps), qkv=qkv_args)
             ops.attention(q, sh.hq * D, kc, vc, sv.block_tables, sv.context_lens, sv.query_start, sv.tile_seq,
                           sv.tile_q0, attn, part_o, part_ml, sh.hq, sh.hkv, part_size, self.scale)
-            self._row_parallel(attn, L.o, resid, first, norm_out=(hg, ssp, L.post_norm) if hand else None)
-            if hand:
-                ops.linear(hg, L.gate_up, out=mlp, prenorm=(ssp, eps))
+            gu = takes(L.gate_up)
+            self._row_parallel(attn, L.o, resid, first, norm_out=(hg, ssp, L.post_norm) if gu else None)
+            if gu:
+                ops.linear(hg if awq else resid, L.gate_up, out=mlp, prenorm=(ssp, eps))
             else:
                 ops.linear(resid, L.gate_up, out=mlp, norm=(L.post_norm, eps))
-            nxt = (hg, ssp, self.layers[li + 1].in_norm) if hand and li + 1 < nl else None
-            self._row_parallel(mlp, L.down, resid, first, norm_out=nxt)
+            nq = li + 1 < nl and takes(self.layers[li + 1].qkv)
+            self._row_parallel(mlp, L.down, resid, first, norm_out=(hg, ssp, self.layers[li + 1].in_norm) if nq else None)
         if return_hidden:
             return resid
         logits = ops.linear(resid, self.lm_head, out_f32=True, norm=(self.final_norm, eps), row_idx=sv.sample_idx)
