@@ -216,10 +216,19 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
             gcs["n2"] += info.get("generation") == 2
             gcs["max_ms"] = max(gcs["max_ms"], 1e3 * (time.perf_counter() - gcs["t"]))
     gc.callbacks.append(gc_cb)
+    prof = None
+    if args.profile_loop:  # the serving event loop's own work in the timed region (this thread only)
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     mon = asyncio.create_task(lag_monitor(t0))
     lat, fails, tokens, _, starts = await load(per_step * args.steps, 0)
     mon.cancel()
+    if prof is not None:
+        prof.disable()
+        import pstats
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(40)
     gc.callbacks.remove(gc_cb)
     barrier()
     wall = time.perf_counter() - t0
@@ -286,6 +295,8 @@ def main():
                     help="run the load loop in a separate client process (default: in the server process; "
                          "measured slower on the 1-GPU box: 68 vs 81 req/s, profiles/r1_bench_client_modes.log)")
     ap.add_argument("--client-proc", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--profile-loop", action="store_true",
+                    help="cProfile the serving event loop over the timed region (stats to stderr; slows it)")
     ap.add_argument("--server", default="vgate", choices=["vgate", "uvicorn"],
                     help="HTTP server: vgate.api.server (default) or uvicorn (h11)")
     ap.add_argument("--client", default="lean", choices=["lean", "aiohttp"],

@@ -59,8 +59,10 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> Path:
     rt_hdrs = sorted((CSRC / "runtime").glob("*.h"))
     jobs_list = []
     common = ["-O3", "-std=c++17", "-fPIC"]
+    want = []  # this tree's objects: a stale object of a deleted / renamed source is never linked
     for src in sorted((CSRC / "kernels").glob("*.hip")):
         obj = BUILD / (src.stem + ".o")
+        want.append(obj)
         if force or _newer(src, obj, kernel_hdrs):
             cmd = [HIPCC, f"--offload-arch={ARCH}", *common, "-munsafe-fp-atomics",
                    "-Wno-unused-result", "-c", str(src), "-o", str(obj)]
@@ -73,6 +75,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> Path:
     ]
     for src in sorted((CSRC / "runtime").glob("*.cpp")):
         obj = BUILD / (src.stem + ".o")
+        want.append(obj)
         if force or _newer(src, obj, kernel_hdrs + rt_hdrs):
             jobs_list.append(["g++", *common, *host_flags, "-c", str(src), "-o", str(obj)])
     if jobs_list:
@@ -80,7 +83,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> Path:
             print(f"[vgate.build] compiling {len(jobs_list)} translation unit(s) for {ARCH}", flush=True)
         with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
             list(ex.map(_run, jobs_list))
-    objs = sorted(BUILD.glob("*.o"))
+    objs = sorted(want)
     out = ext_path()
     if force or jobs_list or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
         link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(out),

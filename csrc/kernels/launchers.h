@@ -82,6 +82,9 @@ bool launch_gemm_mid(const GemmArgs& g, hipStream_t st);
 // AWQ W4A16 decode, wide form (gemm_awq_wide.hip: M <= 16, one block per CU owning whole tiles, x and
 // the group scales staged once per CU); returns false for a shape / mode it does not take
 bool launch_awq_wide(const GemmArgs& g, hipStream_t st);
+// AWQ W4A16 decode, register-stationary activations (gemm_awq_kx.hip: M <= 16, group 128, packed
+// scales; WIDE one block per CU / TILE one tile per block + K slices). False: shape / mode not taken.
+bool launch_awq_kx(const GemmArgs& g, hipStream_t st);
 // AWQ W4A16 medium-M kernel (gemm_awq_wide.hip, 16 < M <= 64): g.waves tiles per block (8: one block
 // per CU owning whole tiles), g.splitk K slices; false for a shape / mode it does not take
 bool launch_awq_mid(const GemmArgs& g, hipStream_t st);

@@ -673,6 +673,62 @@ def test_awq_wide_decode(M, N):
     assert _rel_err(ys, ref.silu_mul_linear_ref(xn, wd[: N // 2], wd[N // 2:])) < 2e-2
 
 
+@pytest.mark.parametrize("M", [1, 5, 8, 13, 16])
+@pytest.mark.parametrize("N,K,w,sk", [(2 * 8960, 1536, 0, 0), (4096 * 2, 1536, 0, 0), (2 * 8960, 1536, 8, 0),
+                                      (1536, 8960, 0, 0), (1536, 1536, 0, 0), (1536, 1536, 6, 2),
+                                      (1024, 2048, 4, 3), (2048, 1536, 16, 1)])
+def test_awq_kx_decode(M, N, K, w, sk):
+    """The register-stationary int4 decode kernel (gemm_awq_kx.hip; ntb = -12 forces it with the given
+    waves / K slices, 0 = its own choice) == the dequantised fp32 reference: WIDE blocks (one per CU,
+    4-5 or 2 tiles each) and TILE blocks (one tile, 1-3 K slices: granules / slabs), XP = 2 (M <= 8)
+    and XP = 1; plain + residual, RMSNorm gamma in registers + SiLU pairs, the hand-off consumer
+    (x = h * gamma, row scale from the producer's per-tile sums) and the hand-off producer (hg, sums)."""
+    torch.manual_seed(700 + M + N // 64 + K // 128 + w + sk)
+    C = ops.native()
+    ws = ops.workspace(torch.device(DEV))
+    g = 128
+    q = torch.randint(0, 16, (N, K), dtype=torch.int32)
+    scales = (torch.rand(K // g, N) * 0.02 + 0.005).bfloat16()
+    zeros = torch.randint(0, 16, (K // g, N)).float().bfloat16()
+    wd = ref.awq_dequant_ref(q, scales, zeros, g).to(DEV)
+    awq = {"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV), "group": g}
+    lin = ops.Linear(None, awq=dict(awq))
+    kw = dict(ws=ws, awq_scales=lin.scales, awq_zeros=lin.zeros, group=g, awq_szp=lin.szp, ntb=-12, waves=w,
+              splitk=sk)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    res = torch.randn(M, N, device=DEV).bfloat16()
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    C.gemm(x, lin.wp, N, K, out, 0, res=res, **kw)
+    want = ref.linear_ref(x, wd, None, res)
+    assert _rel_err(out, want) < 2e-2
+    # hand-off producer: h = x W^T + res, hg = bf16(h * gamma), per-16-column sums of h^2
+    gamma_n = (torch.rand(N, device=DEV) + 0.5).bfloat16()
+    h = res.clone()
+    hg = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ssp_n = torch.empty(M, N // 16, dtype=torch.float32, device=DEV)
+    C.gemm(x, lin.wp, N, K, h, 0, res=h, hg_out=hg, hg_gamma=gamma_n, ssp_out=ssp_n, **kw)
+    assert torch.equal(h, out)
+    assert torch.equal(hg, (h.float() * gamma_n.float()).bfloat16())
+    torch.testing.assert_close(ssp_n, h.float().pow(2).reshape(M, N // 16, 16).sum(-1), rtol=1e-5, atol=1e-4)
+    # RMSNorm gamma in registers + SiLU pairs, and the hand-off consumer of the same rows
+    silu = ops.Linear(None, awq=dict(awq, silu=True))
+    skw = dict(kw, awq_scales=silu.scales, awq_zeros=silu.zeros, awq_szp=silu.szp)
+    hx = torch.randn(M, K, device=DEV).bfloat16()
+    gamma = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+    xn, _ = ref.rmsnorm_ref(hx, gamma, 1e-6)
+    want_s = ref.silu_mul_linear_ref(xn, wd[: N // 2], wd[N // 2:])
+    ys = torch.empty(M, N // 2, device=DEV, dtype=torch.bfloat16)
+    C.gemm(hx, silu.wp, N, K, ys, 2, norm_w=gamma, eps=1e-6, **skw)
+    assert _rel_err(ys, want_s) < 2e-2
+    if K // 16 <= 128:  # the producer's sums in the prefetched form (and the plain one past it)
+        hgx = (hx.float() * gamma.float()).bfloat16()
+        ssp = hx.float().pow(2).reshape(M, K // 16, 16).sum(-1).contiguous()
+        yh = torch.empty_like(ys)
+        C.gemm(hgx, silu.wp, N, K, yh, 2, eps=1e-6, ssp_in=ssp, **skw)
+        assert _rel_err(yh, want_s) < 2e-2
+        assert _rel_err(yh, ys) < 1e-2
+
+
 @pytest.mark.parametrize("M", [17, 40, 64])
 @pytest.mark.parametrize("w,sk", [(0, 0), (8, 0), (4, 3), (2, 6), (1, 12)])
 def test_awq_mid_gemm(M, w, sk):

@@ -34,16 +34,9 @@ PLANS: dict[tuple[int, int, str, str], tuple] = {
     (6144, 4096, "qkv", "dense"): ("sk", 8, 1, 4),
     (28672, 4096, "silu", "dense"): (4, 1, 0),
     (4096, 14336, "plain", "dense"): (4, 1, 1),
-    # Qwen2.5-1.5B AWQ int4, batch 8, ctx 100 (profiles/r3_awq_decode_sweep.log, whole-step replays;
-    # baseline 1287.8 us): qkv on awq_stream_kernel (packed scales, XP-packed activations, 4 waves x 3
-    # k-quads) instead of the K-split awq_gemm_kernel, down_proj in 8 K slices of 4 waves
-    (2048, 1536, "qkv", "awq"): (4, 1, 1),
-    (1536, 8960, "plain", "awq"): (4, 8, 1),
-    # o_proj on awq_stream_kernel too (1246.5 vs 1257.2 us), gate_up on the wide int4 kernel (one block
-    # per CU owning 4-5 whole tiles, x and scales staged once per CU: 1255.3 vs 1279.1 us;
+    # Qwen2.5-1.5B AWQ int4: no entries — every int4 decode GEMM runs the register-stationary kernel
+    # (csrc/kernels/gemm_awq_kx.hip) on its own grid rule (round 3's awq_stream / wide plans:
     # profiles/r3_awq_decode_sweep.log)
-    (1536, 1536, "plain", "awq"): (4, 1, 1),
-    (17920, 1536, "silu", "awq"): (0, 0, -8),
 }
 
 
