@@ -1,8 +1,9 @@
-"""AWQ W4A16 decode GEMM sweep on the MI355X (Qwen2.5-1.5B shapes, M = 8, group 128):
-split-K of the LDS-shared-activation kernel (awq_dec_kernel) and the K-split kernel
-(waves forced), block spans from the launch timeline, weights cycled through > 600 MB.
+"""AWQ W4A16 decode GEMM sweep on the MI355X (Qwen2.5-1.5B shapes, M = 8, group 128): the
+register-stationary kernel (csrc/kernels/gemm_awq_kx.hip, ntb = -12) over (waves, K slices) per
+shape against its own grid rule (0, 0, 0) and the older int4 kernels; block spans from the launch
+timeline, weights cycled through > 400 MB (cold), the decode split-K granule workspace as in-engine.
 
-    python benchmarks/awq_sweep.py
+    python benchmarks/awq_sweep.py            (AWQ_SWEEP_CFGS="w:sk:ntb,..." / AWQ_SWEEP_SHAPES=down,...)
 """
 from __future__ import annotations
 
@@ -63,6 +64,7 @@ def main():
     only = os.environ.get("AWQ_SWEEP_SHAPES")
     dev = torch.device("cuda")
     ws = ops.workspace(dev)
+    skw = dict(sk_ws=ops.sk_workspace(dev), fault=ops.fault_word(dev))
     for name, N, K, layout in SHAPES:
         if only and name not in only.split(","):
             continue
@@ -77,26 +79,34 @@ def main():
         epi = 2 if layout == "silu" else 0
         out = torch.empty(M, N // 2 if epi == 2 else N, device=dev, dtype=torch.bfloat16)
         rows = []
-        # ntb: 0 = launcher's choice (awq_stream_kernel), -1 = LDS-staged awq_dec_kernel,
-        # -2 = K-split awq_gemm_kernel, 1 / 2 / 4 = awq_stream_kernel with that many tiles per block
-        cfgs = [(0, 0, 0), (2, 0, 0), (4, 0, 0), (8, 0, 0), (0, 2, 0), (0, 4, 0), (0, 0, -1), (4, 0, -2),
-                (0, 0, 1), (0, 0, 2), (0, 0, 4), (8, 0, 4), (0, 2, 2), (0, 2, 4), (0, 4, 4)]
+        # ntb: 0 = launcher's choice (register-stationary kernel), -12 / -13 / -14 = that kernel with 1 / 2 / 4
+        # tiles per GROUP block and the forced (waves, slices), -2 = K-split awq_gemm_kernel
+        cfgs = {"qkv": [(0, 0, 0), (8, 1, -12)],
+                "o_proj": [(0, 0, 0), (8, 1, -12)],
+                "gate_up": [(0, 0, 0), (4, 0, -2)],
+                "down": [(0, 0, 0), (16, 1, -12), (12, 1, -12), (8, 4, -13), (8, 3, -13), (16, 2, -13), (16, 1, -13),
+                         (14, 1, -12)]}[name]
         if os.environ.get("AWQ_SWEEP_CFGS"):
             cfgs = [tuple(int(v) for v in c.split(":")) for c in os.environ["AWQ_SWEEP_CFGS"].split(",")]
-        for waves, sk, ntb in cfgs:
+        ssp = (x.float().pow(2).reshape(M, K // 16, 16).sum(-1)).contiguous()
+        if name in ("qkv", "gate_up"):
+            cfgs = cfgs + [(w_, s_, n_, "norm3") for (w_, s_, n_) in cfgs[:1]]
+        for cfg in cfgs:
+            waves, sk, ntb = cfg[:3]
+            nkw = dict(ssp_in=ssp, eps=1e-6) if len(cfg) > 3 else {}
             def fns():
                 for i in range(12):
                     L = lins[i % ncopy]
                     C.gemm(x, L.wp, N, K, out, epi, res=None if epi else res, ws=ws, waves=waves, splitk=sk,
-                           awq_scales=L.scales, awq_zeros=L.zeros, group=g, awq_szp=L.szp, ntb=ntb)
+                           awq_scales=L.scales, awq_zeros=L.zeros, group=g, awq_szp=L.szp, ntb=ntb, **skw, **nkw)
             spans, wall = timeline_graph(C, fns)
             vals = [v for vs in spans.values() for v in vs]
             w_us = wall / 12
             L0 = lins[0]
             bs = block_stats(C, lambda: C.gemm(x, L0.wp, N, K, out, epi, res=None if epi else res, ws=ws, waves=waves,
                                                splitk=sk, awq_scales=L0.scales, awq_zeros=L0.zeros, group=g,
-                                               awq_szp=L0.szp, ntb=ntb))
-            rows.append({"waves": waves, "splitk": sk, "ntb": ntb, "span_us": round(sum(vals[1:]) / (len(vals) - 1), 2),
+                                               awq_szp=L0.szp, ntb=ntb, **skw, **nkw))
+            rows.append({"waves": waves, "splitk": sk, "ntb": ntb, "norm": 3 if nkw else 0, "span_us": round(sum(vals[1:]) / (len(vals) - 1), 2),
                          "wall_us": round(w_us, 2), "eff_TBps": round(lins[0].nbytes() / w_us / 1e6, 2), "blocks": bs})
         print(json.dumps({"shape": name, "N": N, "K": K, "rows": rows}), flush=True)
 

@@ -35,16 +35,13 @@ CANDIDATES = {
              (2, 8, 1), (1, 8, 1), (4, 5, 1), (8, 6, 1), (2, 6, 1)],
     "lm_head": [(0, 0, 0), (8, 1, 2), (4, 1, 2), (2, 1, 2), (1, 1, 2), (4, 1, 4), (2, 1, 1), (4, 1, 1)],
 }
-# int4 (AWQ) layers: ntb >= 1 routes qkv / o_proj to awq_stream_kernel (packed scales, XP-packed
-# activations) instead of the K-split awq_gemm_kernel; ntb -2 forces the latter
+# int4 (AWQ) layers: the register-stationary kernel (csrc/kernels/gemm_awq_kx.hip); ntb -12 / -13 / -14
+# force 1 / 2 / 4 tiles per GROUP block with the given (waves, K slices), -2 the K-split awq_gemm_kernel
 CANDIDATES_AWQ = {
-    "qkv": [(0, 0, 0), (4, 1, -9), (2, 1, -9), (1, 1, -9), (4, 2, -9), (2, 2, -9), (0, 0, -8), (4, 1, 1), (6, 1, 1), (8, 1, 1), (2, 1, 1), (3, 1, 1), (12, 1, 1), (2, 2, 1),
-            (4, 2, 1)],
-    "o": [(0, 0, 0), (4, 1, -9), (2, 1, -9), (1, 1, -9), (4, 2, -9), (2, 2, -9), (0, 0, -8), (4, 1, 1), (6, 1, 1), (8, 1, 1), (2, 1, 1), (3, 1, 1), (2, 2, 1), (4, 2, 1)],
-    "gate_up": [(0, 0, 0), (0, 0, -8), (0, 0, 1), (0, 0, 4), (2, 1, 2), (4, 1, 2), (1, 1, 2), (0, 2, 2), (3, 1, 1),
-                (2, 1, 1)],
-    "down": [(0, 0, 0), (4, 5, -9), (4, 10, -9), (2, 5, -9), (2, 10, -9), (1, 5, -9), (0, 2, 1), (0, 8, 1), (6, 4, 1), (2, 8, 1), (4, 8, 1), (4, 4, 1), (2, 4, 1), (8, 2, 1),
-             (0, 5, 1), (0, 7, 1)],
+    "qkv": [(0, 0, 0), (8, 1, -12), (16, 1, -12), (6, 2, -12), (4, 0, -2)],
+    "o": [(0, 0, 0), (8, 1, -12), (16, 1, -12), (6, 2, -12), (12, 1, -13), (4, 0, -2)],
+    "gate_up": [(0, 0, 0), (8, 0, -12), (16, 0, -12), (6, 0, -12)],
+    "down": [(0, 0, 0), (8, 4, -13), (8, 3, -13), (16, 2, -12), (12, 3, -12), (8, 8, -14), (4, 0, -2)],
     "lm_head": [(0, 0, 0)],
 }
 

@@ -175,10 +175,8 @@ void launch_awq_gemm(const GemmArgs& g, hipStream_t st) {
     return;
   }
   // decode (M <= 16) on the register-stationary int4 kernel: the launcher's choice (no forced waves /
-  // tiles per block), or g.ntb == -12 with the forced waves / slices
-  if (g.path == 0 && ((g.ntb == 0 && g.waves == 0) || g.ntb == -12) && launch_awq_kx(g, st)) return;
-  // the wide int4 kernel (one block per CU owning whole tiles, one wave per tile): g.ntb == -8
-  if (g.ntb == -8 && launch_awq_wide(g, st)) return;
+  // tiles per block), or g.ntb = -12 / -13 / -14 (1 / 2 / 4 tiles per block) with the forced waves / slices
+  if (g.path == 0 && ((g.ntb == 0 && g.waves == 0) || (g.ntb <= -12 && g.ntb >= -14)) && launch_awq_kx(g, st)) return;
   // mixed prefill + decode steps (16 < M <= 64) on the int4 medium kernel (path 2)
   if (g.path == 2 && launch_awq_mid(g, st)) return;
   launch_dispatch<true>(to_params(g), g, st);

@@ -6,8 +6,9 @@
 // bytes that are not weights. And once the bytes are in, the nibble -> bf16 unpack (MFMA A operand)
 // and the group scale cost ~45 VALU instructions per (tile, k-quad) — for Qwen2.5-1.5B gate_up
 // (1120 tiles x 12 k-quads over 256 CUs) ~0.9 us of VALU time per SIMD, as long as a third of the
-// HBM stream. The earlier int4 kernels serialised that work behind the stream (one wave per tile:
-// awq_wide 9.85 us) or behind LDS staging of x (benchmarks/probes/awq_wide_anatomy.hip).
+// HBM stream. The round-2..4 int4 kernels serialised that work behind the stream (one wave per tile:
+// 9.85 us for gate_up) or behind LDS staging of x (benchmarks/probes/awq_wide_anatomy.hip keeps a copy
+// of that design; profiles/r5_awq_wide_anatomy_and_kx_probe.log).
 //
 // Here the waves of a block split K and every wave keeps ITS activation fragments in registers
 // (XP-packed: one 16-B load covers XP k-steps of M <= 16 / XP real rows) while it streams the int4
@@ -23,9 +24,11 @@
 // Two grid forms:
 //   WIDE  (N >= one tile per CU, gate_up): one block per CU owning whole tiles [t0, t0 + ntb),
 //         ntb <= TMAX; the waves' partials meet in LDS and wave j finishes tile t0 + j.
-//   TILE  (narrow N: qkv, o_proj, down_proj): one tile per block, gridDim.z K slices; the waves'
-//         partials, the slices (granules / slabs) and the epilogue are gemm_finish's, with the
-//         epilogue operands (residual, bias, RoPE position / cos-sin) prefetched at launch.
+//   GROUP (narrow N: qkv, o_proj, down_proj): TMAX = 1, 2 or 4 adjacent tiles per block, gridDim.z
+//         K slices; the waves' partials, the slices (granules / slabs) and the epilogue are
+//         gemm_finish's, with the epilogue operands (residual, bias, RoPE position / cos-sin) of
+//         1-2 tile blocks prefetched at launch. More tiles per block = fewer activation bytes per
+//         weight byte (deep K: down_proj), one tile = the shortest block (qkv / o_proj).
 // NORM: 0 none; 1 RMSNorm gamma in registers (x * gamma in bf16, raw x^2 summed; layer 0 of the
 // hand-off chain); 3 the producer's hand-off (x = h * gamma, row sums of squares in ssp_in).
 #include "gemm_decode.h"
@@ -33,22 +36,19 @@
 namespace vgate {
 
 // bf16 (128 + v) of the 8 nibbles of one dword (ops.pack_awq order: element j of k-step u at bits
-// 16 (j & 1) + 4 (j >> 1)): 3 shifts + 4 v_and_or_b32 (the compiler emits and + or: 11 VALU). The
-// results feed MFMA A operands, and the hazard recognizer does not see through inline asm: the block
-// ends with the 2 wait states a VALU-written VGPR needs before an MFMA reads it.
-__device__ __forceinline__ bf16x8 kx_raw8(uint32_t q, uint32_t m, uint32_t o) {
-  uint32_t r0, r1, r2, r3;
-  asm("v_lshrrev_b32 %1, 4, %4\n\t"
-      "v_lshrrev_b32 %2, 8, %4\n\t"
-      "v_lshrrev_b32 %3, 12, %4\n\t"
-      "v_and_or_b32 %0, %4, %5, %6\n\t"
-      "v_and_or_b32 %1, %1, %5, %6\n\t"
-      "v_and_or_b32 %2, %2, %5, %6\n\t"
-      "v_and_or_b32 %3, %3, %5, %6\n\t"
-      "s_nop 1"
-      : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3)
-      : "v"(q), "v"(m), "v"(o));
-  return as_bf16x8(make_uint4(r0, r1, r2, r3));
+// 16 (j & 1) + 4 (j >> 1), i.e. output dword i holds the low (i even) / high (i odd) nibbles of bytes
+// i/2 and i/2 + 2). The nibbles are isolated into bytes (lo = q & 0x0F0F0F0F, hi = (q >> 4) & ...)
+// and each output dword is one v_perm_b32 of two of those bytes with two 0x43 bytes: 7 VALU per 8
+// values, all compiler-visible (an inline-asm v_and_or_b32 form needed three register moves per
+// dword to build the MFMA operand tuple plus a manual MFMA hazard wait).
+__device__ __forceinline__ bf16x8 kx_raw8(uint32_t q, uint32_t c43) {
+  const uint32_t lo = q & 0x0F0F0F0Fu, hi = (q >> 4) & 0x0F0F0F0Fu;
+  uint4 r;
+  r.x = __builtin_amdgcn_perm(c43, lo, 0x04020400u);  // [lo.b0, 0x43, lo.b2, 0x43]
+  r.y = __builtin_amdgcn_perm(c43, hi, 0x04020400u);
+  r.z = __builtin_amdgcn_perm(c43, lo, 0x04030401u);  // [lo.b1, 0x43, lo.b3, 0x43]
+  r.w = __builtin_amdgcn_perm(c43, hi, 0x04030401u);
+  return as_bf16x8(r);
 }
 
 typedef __bf16 kx_bf2 __attribute__((ext_vector_type(2)));
@@ -62,41 +62,20 @@ __device__ __forceinline__ float kx_sum8(uint4 v, float acc) {  // acc + the 8 b
   return acc;
 }
 
-constexpr int KX_SSL = 8;  // NORM 3 prefetch: f32x4 loads per lane (ssn <= 128, ssn % 16 == 0)
-
-// the producer's per-tile sums of squares of row m, this lane's quarter, loaded at launch (NORM 3)
-struct KxSs {
-  f32x4 r[KX_SSL];
-  int n4;  // 0: prenorm_ss after the stream (ssn not in the prefetch form)
-};
-__device__ __forceinline__ void kx_ss_issue(const GemmParams& p, KxSs& s, int m, int quarter) {
-  s.n4 = (p.ssn & 15) == 0 && p.ssn <= 16 * KX_SSL && m < p.M ? p.ssn >> 4 : 0;
-  const f32x4* src = reinterpret_cast<const f32x4*>(p.ssp_in + (size_t)(m < p.M ? m : 0) * p.ssn + quarter * (p.ssn >> 2));
-#pragma unroll
-  for (int u = 0; u < KX_SSL; ++u)
-    if (u < s.n4) s.r[u] = src[u];
-}
-__device__ __forceinline__ float kx_ss_sum(const GemmParams& p, const KxSs& s, int m, int quarter) {
-  if (s.n4 == 0) return prenorm_ss(p, m, quarter);
-  float acc = 0.f;
-#pragma unroll
-  for (int u = 0; u < KX_SSL; ++u)
-    if (u < s.n4) acc += (s.r[u][0] + s.r[u][1]) + (s.r[u][2] + s.r[u][3]);
-  return acc;
-}
-
 // XP: k-steps per activation load (2: M <= 8, 1: M <= 16); KQW: k-quads per wave (host: >= the
-// wave's range); TMAX: tiles per block (WIDE) or 1 (TILE). Registers of loads in flight per lane:
-// kx_regs; up to 64 the block may hold 16 waves (128 VGPRs each), else 8.
+// wave's range); TMAX: tiles per block (WIDE: at most, GROUP: exactly). Registers of loads in flight per lane:
+// kx_regs (+ the NORM 3 prefetch); up to 80 the block may hold 16 waves (128 VGPRs each), else 8.
 template <int XP, int KQW, int TMAX, int NORM>
-__host__ __device__ constexpr int kx_regs() { return 4 * KQW * ((4 / XP) * (NORM == 1 ? 2 : 1) + 2 * TMAX); }
+__host__ __device__ constexpr int kx_regs() {
+  return 4 * KQW * ((4 / XP) * (NORM == 1 ? 2 : 1) + 2 * TMAX) + (NORM == 3 ? 4 * SS_PRE : 0);
+}
 template <int XP, int KQW, int TMAX, int NORM>
-__host__ __device__ constexpr int kx_max_threads() { return kx_regs<XP, KQW, TMAX, NORM>() <= 64 ? 1024 : 512; }
+__host__ __device__ constexpr int kx_max_threads() { return kx_regs<XP, KQW, TMAX, NORM>() <= 80 ? 1024 : 512; }
 
 template <int XP, int KQW, int TMAX, int EPI, int NORM, bool WIDE>
 __global__ __launch_bounds__((kx_max_threads<XP, KQW, TMAX, NORM>())) void awq_kx_kernel(GemmParams p) {
-  static_assert(WIDE || TMAX == 1, "TILE form: one tile per block");
-  static_assert(!WIDE || EPI != EPI_QKV, "QKV tiles finish through gemm_finish (prefetched RoPE operands)");
+  static_assert(EPI != EPI_QKV || (!WIDE && TMAX == 1), "QKV: one-tile GROUP blocks (prefetched RoPE operands)");
+  constexpr bool PRE = !WIDE && TMAX <= 2;  // GROUP blocks of 1-2 tiles: epilogue operands at launch
   constexpr int R = 16 / XP;   // real rows one load covers
   constexpr int XL = 4 / XP;   // activation loads per k-quad
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -112,56 +91,61 @@ __global__ __launch_bounds__((kx_max_threads<XP, KQW, TMAX, NORM>())) void awq_k
     s0 = 0;
     s1 = KQ;
   } else {
-    t0 = blockIdx.x;
-    ntb = 1;
+    t0 = blockIdx.x * TMAX;
+    ntb = TMAX;
     s0 = (KQ * (int)blockIdx.z) / p.splitk;
     s1 = (KQ * ((int)blockIdx.z + 1)) / p.splitk;
   }
   const int q0 = s0 + ((s1 - s0) * wid) / nw;
   const int nq = s0 + ((s1 - s0) * (wid + 1)) / nw - q0;  // <= KQW (host-checked), may be 0
   // NORM 3: the row's sums of squares, issued first (consumed after the stream without waiting on it)
-  KxSs ssv;
-  ssv.n4 = 0;
-  const bool ss_wave = WIDE ? wid < ntb : (wid == 0 && blockIdx.z == 0);
+  SsPre ssv;
+  ssv.n4 = NORM == 3 ? ss_pre_n4(p) : 0;
+  const bool ss_wave = WIDE ? wid < ntb : (wid == 0 && blockIdx.z == 0);  // wave-uniform
   if constexpr (NORM == 3) {
-    if (ss_wave) kx_ss_issue(p, ssv, r16, grp);
+    if (ss_wave && ssv.n4 > 0) ss_pre_issue(p, ssv, r16, grp);
   }
-  // TILE form: the epilogue operands of wave 0's (row, 4 columns) item at launch
-  EpiPre<1> pre;
-  const bool epi_thr = !WIDE && threadIdx.x < 64;
-  if (epi_thr) epi_pre_a<1, EPI>(p, pre, r16, t0, 4 * grp);
-  // activations: lane (r16, grp) loads row r16 % R of k-step r16 / R (+ XP v) of each load
+  // GROUP form: the epilogue operands of wave 0's (row, 4 columns) items at launch
+  EpiPre<TMAX> pre;
+  // wave 0 runs the epilogue. Its operand loads sit under a wave-uniform branch (a lane test would be
+  // an exec-masked one), except QKV's: the RoPE cos/sin loads depend on the position load and go out
+  // after the weight stream, and a branch there would leave every later wait at vmcnt(0) — so every
+  // wave issues them (a few L2-resident words) and only wave 0's are used
+  const bool epi_thr = PRE && (EPI == EPI_QKV || wid == 0);
+  if (epi_thr) epi_pre_a<TMAX, EPI>(p, pre, r16, t0, 4 * grp);
+  // activations: lane (r16, grp) loads row r16 % R of k-step r16 / R (+ XP v) of each load. Rows
+  // past M re-read row M - 1 (row_of clamps) and lanes r16 >= R of a rebuilt fragment keep another
+  // k-step's values: both only feed output rows that are never stored (no masks, no exec-masked loads)
   const int mrow = r16 % R;
-  const bool xok = mrow < p.M;
-  const bf16_t* xrow = p.x + (size_t)row_of(p, mrow) * p.lda + 8 * grp + (XP > 1 ? (r16 / R) * 32 : 0);
+  const bf16_t* xrow = p.x + (size_t)row_of_e<EPI>(p, mrow) * p.lda + 8 * grp + (XP > 1 ? (r16 / R) * 32 : 0);
   const bf16_t* grow = NORM == 1 ? p.norm_w + 8 * grp + (XP > 1 ? (r16 / R) * 32 : 0) : nullptr;
   const uint4* wbase = p.wp + (size_t)t0 * KQ * 64 + lane;
   const uint4* szbase = reinterpret_cast<const uint4*>(p.szp) + (size_t)t0 * KQ * 4 + grp;
   constexpr int GL = NORM == 1 ? XL : 1;
   uint4 xa[KQW][XL], ga[KQW][GL], w[KQW][TMAX], sz[KQW][TMAX];
+  // every load unconditional (clamped re-reads past the wave's range are never consumed): a load
+  // under a branch leaves the paths with different outstanding counts, and the compiler's waits
+  // after the join then cover loads issued later (the weight stream) as well
 #pragma unroll
   for (int q = 0; q < KQW; ++q) {
-    const int kq = q0 + min(q, max(nq - 1, 0));
-    if (q < nq) {  // wave-uniform
+    const int kq = min(q0 + min(q, max(nq - 1, 0)), KQ - 1);
 #pragma unroll
-      for (int v = 0; v < XL; ++v)
-        xa[q][v] = xok ? *reinterpret_cast<const uint4*>(xrow + (size_t)(kq * 4 + v * XP) * 32) : make_uint4(0, 0, 0, 0);
-      if constexpr (NORM == 1) {
+    for (int v = 0; v < XL; ++v)
+      xa[q][v] = *reinterpret_cast<const uint4*>(xrow + (size_t)(kq * 4 + v * XP) * 32);
+    if constexpr (NORM == 1) {
 #pragma unroll
-        for (int v = 0; v < XL; ++v) ga[q][v] = *reinterpret_cast<const uint4*>(grow + (size_t)(kq * 4 + v * XP) * 32);
-      }
+      for (int v = 0; v < XL; ++v) ga[q][v] = *reinterpret_cast<const uint4*>(grow + (size_t)(kq * 4 + v * XP) * 32);
+    }
 #pragma unroll
-      for (int j = 0; j < TMAX; ++j) {
-        const size_t u = (size_t)min(j, ntb - 1) * KQ + kq;
-        w[q][j] = ld_nt16(wbase + u * 64);
-        sz[q][j] = szbase[u * 4];
-      }
+    for (int j = 0; j < TMAX; ++j) {
+      const size_t u = (size_t)min(j, ntb - 1) * KQ + kq;
+      w[q][j] = ld_nt16(wbase + u * 64);
+      sz[q][j] = szbase[u * 4];
     }
   }
   asm volatile("" ::: "memory");  // every load of the wave is in flight before the first MFMA
-  if (epi_thr) epi_pre_b<1, EPI>(p, pre, t0, 4 * grp);
-  const uint32_t lom = r16 < R ? ~0u : 0u;
-  const uint32_t nib_m = 0x000F000Fu, nib_o = 0x43004300u;
+  if (epi_thr) epi_pre_b<TMAX, EPI>(p, pre, t0, 4 * grp);
+  const uint32_t c43 = 0x43434343u;
   f32x4 acc[TMAX];
 #pragma unroll
   for (int j = 0; j < TMAX; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -169,18 +153,19 @@ __global__ __launch_bounds__((kx_max_threads<XP, KQW, TMAX, NORM>())) void awq_k
 #pragma unroll
   for (int q = 0; q < KQW; ++q) {
     if (q >= nq) break;  // wave-uniform
-    // the 4 B fragments of a k-quad from its XP-packed loads (lane r16 < R <- row r16 of each k-step)
+    // the 4 B fragments of a k-quad from its XP-packed loads (lane r16 < R <- row r16 of each k-step;
+    // lanes r16 >= R: don't-care rows)
     auto unpack = [&](const uint4 (&src)[XL], uint4 (&b)[4]) {
 #pragma unroll
       for (int v = 0; v < XL; ++v) {
         if constexpr (XP == 1) {
           b[v] = src[v];
         } else {
-          b[v * XP] = and_mask(src[v], lom);
-          b[v * XP + 1] = and_mask(row_ror<R>(src[v]), lom);
+          b[v * XP] = src[v];
+          b[v * XP + 1] = row_ror<R>(src[v]);
           if constexpr (XP == 4) {
-            b[v * XP + 2] = and_mask(row_ror<2 * R>(src[v]), lom);
-            b[v * XP + 3] = and_mask(row_ror<3 * R>(src[v]), lom);
+            b[v * XP + 2] = row_ror<2 * R>(src[v]);
+            b[v * XP + 3] = row_ror<3 * R>(src[v]);
           }
         }
       }
@@ -221,10 +206,10 @@ __global__ __launch_bounds__((kx_max_threads<XP, KQW, TMAX, NORM>())) void awq_k
     for (int j = 0; j < TMAX; ++j) {
       if (j < ntb) {
         f32x4 pr = {0.f, 0.f, 0.f, 0.f};
-        pr = mfma16(kx_raw8(w[q][j].x, nib_m, nib_o), as_bf16x8(b[0]), pr);
-        pr = mfma16(kx_raw8(w[q][j].y, nib_m, nib_o), as_bf16x8(b[1]), pr);
-        pr = mfma16(kx_raw8(w[q][j].z, nib_m, nib_o), as_bf16x8(b[2]), pr);
-        pr = mfma16(kx_raw8(w[q][j].w, nib_m, nib_o), as_bf16x8(b[3]), pr);
+        pr = mfma16(kx_raw8(w[q][j].x, c43), as_bf16x8(b[0]), pr);
+        pr = mfma16(kx_raw8(w[q][j].y, c43), as_bf16x8(b[1]), pr);
+        pr = mfma16(kx_raw8(w[q][j].z, c43), as_bf16x8(b[2]), pr);
+        pr = mfma16(kx_raw8(w[q][j].w, c43), as_bf16x8(b[3]), pr);
         const uint4 s = sz[q][j];
         const float s4[4] = {bf_lo(s.x), bf_hi(s.x), bf_lo(s.y), bf_hi(s.y)};
         const float z4[4] = {bf_lo(s.z), bf_hi(s.z), bf_lo(s.w), bf_hi(s.w)};
@@ -234,13 +219,15 @@ __global__ __launch_bounds__((kx_max_threads<XP, KQW, TMAX, NORM>())) void awq_k
     }
   }
   if constexpr (!WIDE) {
-    f32x4 a1[1][1] = {{acc[0]}};
+    f32x4 a1[1][TMAX];
+#pragma unroll
+    for (int j = 0; j < TMAX; ++j) a1[0][j] = acc[j];
     float sr[1] = {0.f};
     if constexpr (NORM == 1) sr[0] = ssr;
     if constexpr (NORM == 3) {
-      if (ss_wave) sr[0] = kx_ss_sum(p, ssv, r16, grp);
+      if (ss_wave) sr[0] = ss_pre_sum(p, ssv, r16, grp);
     }
-    gemm_finish<1, 1, EPI, NORM, true>(p, a1, sr, smem, 0, t0, pre);
+    gemm_finish<1, TMAX, EPI, NORM, PRE>(p, a1, sr, smem, 0, t0, pre);
   } else {
     // the waves' partials of every tile (rows < M only) and, NORM 1, their x^2 rows -> LDS
     f32x4* red = reinterpret_cast<f32x4*>(smem);                      // [nw][TMAX][64]
@@ -265,7 +252,7 @@ __global__ __launch_bounds__((kx_max_threads<XP, KQW, TMAX, NORM>())) void awq_k
       v[0] *= rsqrtf(ss / (float)p.K + p.eps);
     }
     if constexpr (NORM == 3) {
-      float ss = kx_ss_sum(p, ssv, r16, grp);
+      float ss = ss_pre_sum(p, ssv, r16, grp);
       ss += xor16(ss);
       ss += xor32(ss);
       v[0] *= rsqrtf(ss / (float)p.K + p.eps);
@@ -287,7 +274,7 @@ static int kx_cus() {
 template <int XP, int KQW, int TMAX, int EPI, int NORM, bool WIDE>
 static bool kx_go(const GemmParams& p, dim3 grid, int nw, hipStream_t st) {
   if (64 * nw > kx_max_threads<XP, KQW, TMAX, NORM>()) return false;
-  const size_t lds = WIDE ? (size_t)nw * TMAX * 1024 + (size_t)nw * 16 * 4 : red_bytes<1, 1>(nw) + ssq_bytes<1>(nw) + 16;
+  const size_t lds = WIDE ? (size_t)nw * TMAX * 1024 + (size_t)nw * 16 * 4 : red_bytes<1, TMAX>(nw) + ssq_bytes<1>(nw) + 16;
   if (lds > 160 * 1024) return false;
   auto kern = awq_kx_kernel<XP, KQW, TMAX, EPI, NORM, WIDE>;
   if (lds > 64 * 1024) {
@@ -300,56 +287,85 @@ static bool kx_go(const GemmParams& p, dim3 grid, int nw, hipStream_t st) {
 }
 
 // Grid choice. WIDE when N has at least one tile per CU (and no slices are forced): one block per CU,
-// min(16, K / 128) waves. Otherwise TILE: one tile per block, K slices while the grid still fits the
-// CUs and every slice keeps >= 16 k-quads (down_proj: 96 tiles x 2 slices of 35), min(16, slice)
-// waves. g.waves / g.splitk force the wave / slice counts (sweeps, tests).
-template <int XP, int EPI, int NORM>
-static bool kx_launch_xp(GemmParams p, const GemmArgs& g, hipStream_t st) {
+// min(16, K / 128) waves. Otherwise GROUP: TB tiles per block (g.ntb -12 / -13 / -14 force 1 / 2 / 4;
+// default 1), K slices while the grid still fits the CUs and every slice keeps >= 16 k-quads
+// (down_proj: 96 tiles x 2 slices of 35), min(16, slice) waves. g.waves / g.splitk force the wave /
+// slice counts (sweeps, tests).
+template <int XP, int TB, int EPI, int NORM>
+static bool kx_group(GemmParams p, const GemmArgs& g, hipStream_t st) {
   const int ntiles = g.N / 16, KQ = g.K / 128, ncu = kx_cus();
-  if constexpr (EPI != EPI_QKV) {
-    if (ntiles >= ncu && g.splitk <= 1) {
-    const int nb = ncu, tneed = (ntiles + nb - 1) / nb;
-    const int nw = g.waves > 0 ? g.waves : std::min(16, KQ);
-    if (nw > 16) return false;
-    const int kqw = (KQ + nw - 1) / nw;
-    if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_kx_wide", nb);
-    p.splitk = 1;
-    const dim3 grid(nb);
-    if (tneed <= 2 && kqw == 1) return kx_go<XP, 1, 2, EPI, NORM, true>(p, grid, nw, st);
-    if (tneed <= 5 && kqw == 1) return kx_go<XP, 1, 5, EPI, NORM, true>(p, grid, nw, st);
-    if (tneed <= 5 && kqw == 2) return kx_go<XP, 2, 5, EPI, NORM, true>(p, grid, nw, st);
-    if (tneed <= 8 && kqw == 1) return kx_go<XP, 1, 8, EPI, NORM, true>(p, grid, nw, st);
-    return false;
-    }
-  }
+  if (ntiles % TB) return false;
+  const int groups = ntiles / TB;
   int S = g.splitk > 0 ? g.splitk : 1;
   if (g.splitk <= 0)
-    while (ntiles * (S + 1) <= ncu && KQ / (S + 1) >= 16) ++S;
+    while (groups * (S + 1) <= ncu && KQ / (S + 1) >= 16) ++S;
   if (S > SK_MAX || S > KQ) return false;
   const int kqs = (KQ + S - 1) / S;
   int nw = g.waves > 0 ? g.waves : std::min(16, kqs);
   int kqw = (kqs + nw - 1) / nw;
-  if (kqw > 4 && g.waves <= 0) {  // the 6-deep form holds 8 waves at most
+  if (kqw > 5 && g.waves <= 0) {  // the 6-deep form holds 8 waves at most
     nw = std::min(8, kqs);
     kqw = (kqs + nw - 1) / nw;
   }
   if (nw > 16 || kqw > 6) return false;
   p.splitk = S;
   if (S > 1) {
-    const size_t need_slab = (size_t)ntiles * S * (64 * 16 + (NORM ? 16 * 4 : 0));
-    const size_t need_g = (size_t)ntiles * 3 * 64 * 16;
-    if (S == 2 && g.sk_pub != nullptr && need_g <= g.sk_bytes) p.gran = reinterpret_cast<uint4*>(g.sk_pub);
-    else if (g.slabs == nullptr || need_slab > g.slab_bytes || ntiles > g.max_counters) return false;
+    const size_t need_slab = (size_t)groups * S * (TB * 64 * 16 + (NORM ? 16 * 4 : 0));
+    const size_t need_g = (size_t)groups * 3 * 64 * 16;
+    if (TB == 1 && S == 2 && g.sk_pub != nullptr && need_g <= g.sk_bytes) p.gran = reinterpret_cast<uint4*>(g.sk_pub);
+    else if (g.slabs == nullptr || need_slab > g.slab_bytes || groups > g.max_counters) return false;
   }
-  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_kx", ntiles * S);
-  const dim3 grid(ntiles, 1, S);
-  switch (kqw) {
-    case 1: return kx_go<XP, 1, 1, EPI, NORM, false>(p, grid, nw, st);
-    case 2: return kx_go<XP, 2, 1, EPI, NORM, false>(p, grid, nw, st);
-    case 3: return kx_go<XP, 3, 1, EPI, NORM, false>(p, grid, nw, st);
-    case 4: return kx_go<XP, 4, 1, EPI, NORM, false>(p, grid, nw, st);
-    default: return kx_go<XP, 6, 1, EPI, NORM, false>(p, grid, nw, st);
+  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_kx", groups * S);
+  const dim3 grid(groups, 1, S);
+  if constexpr (TB == 1) {
+    switch (kqw) {
+      case 1: return kx_go<XP, 1, 1, EPI, NORM, false>(p, grid, nw, st);
+      case 2: return kx_go<XP, 2, 1, EPI, NORM, false>(p, grid, nw, st);
+      case 3: return kx_go<XP, 3, 1, EPI, NORM, false>(p, grid, nw, st);
+      case 4: return kx_go<XP, 4, 1, EPI, NORM, false>(p, grid, nw, st);
+      case 5: return kx_go<XP, 5, 1, EPI, NORM, false>(p, grid, nw, st);
+      default: return kx_go<XP, 6, 1, EPI, NORM, false>(p, grid, nw, st);
+    }
+  } else if constexpr (TB == 2) {
+    switch (kqw) {
+      case 1: return kx_go<XP, 1, 2, EPI, NORM, false>(p, grid, nw, st);
+      case 2: return kx_go<XP, 2, 2, EPI, NORM, false>(p, grid, nw, st);
+      case 3: return kx_go<XP, 3, 2, EPI, NORM, false>(p, grid, nw, st);
+      default: return false;
+    }
+  } else {
+    switch (kqw) {
+      case 1: return kx_go<XP, 1, 4, EPI, NORM, false>(p, grid, nw, st);
+      case 2: return kx_go<XP, 2, 4, EPI, NORM, false>(p, grid, nw, st);
+      default: return false;
+    }
   }
+}
+
+template <int XP, int EPI, int NORM>
+static bool kx_launch_xp(GemmParams p, const GemmArgs& g, hipStream_t st) {
+  const int ntiles = g.N / 16, KQ = g.K / 128, ncu = kx_cus();
+  if constexpr (EPI != EPI_QKV) {
+    if (ntiles >= ncu && g.splitk <= 1 && g.ntb != -13 && g.ntb != -14) {
+      const int nb = ncu, tneed = (ntiles + nb - 1) / nb;
+      const int nw = g.waves > 0 ? g.waves : std::min(16, KQ);
+      if (nw > 16) return false;
+      const int kqw = (KQ + nw - 1) / nw;
+      if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_kx_wide", nb);
+      p.splitk = 1;
+      const dim3 grid(nb);
+      if (tneed <= 2 && kqw == 1) return kx_go<XP, 1, 2, EPI, NORM, true>(p, grid, nw, st);
+      if (tneed <= 5 && kqw == 1) return kx_go<XP, 1, 5, EPI, NORM, true>(p, grid, nw, st);
+      if (tneed <= 5 && kqw == 2) return kx_go<XP, 2, 5, EPI, NORM, true>(p, grid, nw, st);
+      if (tneed <= 8 && kqw == 1) return kx_go<XP, 1, 8, EPI, NORM, true>(p, grid, nw, st);
+      return false;
+    }
+    if constexpr (NORM == 0) {  // multi-tile GROUP blocks: the plain / residual (+ hand-off producer) GEMMs
+      if (g.ntb == -13) return kx_group<XP, 2, EPI, NORM>(p, g, st);
+      if (g.ntb == -14) return kx_group<XP, 4, EPI, NORM>(p, g, st);
+    }
+  }
+  return kx_group<XP, 1, EPI, NORM>(p, g, st);
 }
 
 template <int EPI, int NORM>

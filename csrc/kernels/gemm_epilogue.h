@@ -59,6 +59,14 @@ __device__ __forceinline__ int row_of(const GemmParams& p, int m) {
   m = m < p.M ? m : p.M - 1;  // clamp: duplicated rows are computed but never stored
   return p.row_idx ? p.row_idx[m] : m;
 }
+// Row gathers serve the LM head only (f32 logits of the sampled rows): every other epilogue reads
+// rows in place, and its kernels carry no conditional row-index load (a load under a branch that
+// joins before the weight stream costs the stream a wait on it, see gemm_kernel)
+template <int EPI>
+__device__ __forceinline__ int row_of_e(const GemmParams& p, int m) {
+  if constexpr (EPI == EPI_F32) return row_of(p, m);
+  return m < p.M ? m : p.M - 1;
+}
 
 // LDS carve (one dynamic array; Guideline 17): [reduce | ssq[nw][16*MB] | flag]
 template <int MB, int NTB>
@@ -111,30 +119,42 @@ struct EpiPre {
   int pos, slot;
 };
 
+// The loads are unconditional: a missing bias / residual reads the packed weights instead (always
+// mapped, N x K >= any offset here) and the epilogue's own `if (p.bias)` / `if (p.res)` ignores the
+// words. A load under a branch costs more than the bytes: the compiler's merge copy at the join
+// waits for it there, i.e. before the weight stream is requested.
 template <int NTB, int EPI>
 __device__ __forceinline__ void epi_pre_a(const GemmParams& p, EpiPre<NTB>& e, int m, int nt0, int nsub) {
   m = m < p.M ? m : p.M - 1;
+  const bf16_t* safe = reinterpret_cast<const bf16_t*>(p.wp);
+  const bf16_t* bias = p.bias ? p.bias : safe;
   if constexpr (EPI == EPI_QKV) {
     e.pos = p.positions[m];
     e.slot = p.slots[m];
-    e.b0 = p.bias ? *reinterpret_cast<const uint2*>(p.bias + qkv_col(nt0, nsub)) : make_uint2(0, 0);
+    e.b0 = *reinterpret_cast<const uint2*>(bias + qkv_col(nt0, nsub));
   } else if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_AR || EPI == EPI_F32) {
+    const bf16_t* res = p.res ? p.res + (size_t)m * p.ldr : safe + (size_t)m * p.N;
 #pragma unroll
     for (int j = 0; j < NTB; ++j) {
       const int n = (nt0 + j) * 16 + nsub;
-      const uint2 b = p.bias ? *reinterpret_cast<const uint2*>(p.bias + n) : make_uint2(0, 0);
+      const uint2 b = *reinterpret_cast<const uint2*>(bias + n);
       uint2 r = make_uint2(0, 0);
-      if constexpr (EPI != EPI_F32) r = p.res ? *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldr + n) : r;
+      if constexpr (EPI != EPI_F32) r = *reinterpret_cast<const uint2*>(res + n);
       if (j == 0) { e.b0 = b; e.r0 = r; } else { e.b1 = b; e.r1 = r; }
     }
   }
 }
 
+// (called once the weight stream is issued: the volatile asm with a memory clobber keeps every earlier
+// load above it and is the first reader of the position, so the wait for the position load lands
+// here — left alone, the compiler hoists the address arithmetic and the wait above the weight loads)
 template <int NTB, int EPI>
 __device__ __forceinline__ void epi_pre_b(const GemmParams& p, EpiPre<NTB>& e, int nt0, int nsub) {
   if constexpr (EPI == EPI_QKV) {
     const int d = qkv_rot(nt0, nsub);
-    const float* cs = p.cos_sin + (size_t)e.pos * 128;
+    int pos = e.pos;
+    asm volatile("" : "+v"(pos)::"memory");
+    const float* cs = p.cos_sin + (size_t)pos * 128;
     e.cs = *reinterpret_cast<const float4*>(cs + d);
     e.sn = *reinterpret_cast<const float4*>(cs + 64 + d);
   }
@@ -227,6 +247,42 @@ __device__ __forceinline__ float prenorm_ss(const GemmParams& p, int m, int quar
   }
   return acc;
 }
+
+// NORM 3 consumers: the producer's sums issued at launch, summed after the weight stream (prefetch
+// form: ssn <= 128 = K <= 2048, ssn % 16 == 0; else prenorm_ss after the stream)
+constexpr int SS_PRE = 8;  // f32x4 loads per lane
+
+// The producer's per-tile sums of squares of row m, this lane's quarter, loaded at launch (NORM 3).
+// n4 is wave-uniform and the loads are unconditional inside (rows past M re-read row M - 1, their sum
+// is never used): an exec-masked load makes the compiler wait for it — and for everything issued
+// before it — right where the branch joins, i.e. before the weight stream is even requested.
+struct SsPre {
+  f32x4 r[SS_PRE];
+  int n4;  // 0: prenorm_ss after the stream (ssn not in the prefetch form)
+};
+__device__ __forceinline__ int ss_pre_n4(const GemmParams& p) {
+  return (p.ssn & 15) == 0 && p.ssn <= 16 * SS_PRE ? p.ssn >> 4 : 0;
+}
+__device__ __forceinline__ void ss_pre_issue(const GemmParams& p, SsPre& s, int m, int quarter) {
+  const f32x4* src = reinterpret_cast<const f32x4*>(p.ssp_in + (size_t)min(m, p.M - 1) * p.ssn + quarter * (p.ssn >> 2));
+#pragma unroll
+  for (int u = 0; u < SS_PRE; ++u) s.r[u] = src[min(u, s.n4 - 1)];
+}
+// (call it after the weight stream is issued: the empty volatile asm pins the first use of the loaded
+// registers there — left alone, the compiler hoists this pure-register sum right behind its loads
+// and the wave waits a whole memory round trip before it requests a single weight)
+__device__ __forceinline__ float ss_pre_sum(const GemmParams& p, const SsPre& s, int m, int quarter) {
+  if (s.n4 == 0) return prenorm_ss(p, m, quarter);
+  float acc = 0.f;
+#pragma unroll
+  for (int u = 0; u < SS_PRE; ++u) {
+    f32x4 r = s.r[u];
+    asm volatile("" : "+v"(r));
+    if (u < s.n4) acc += (r[0] + r[1]) + (r[2] + r[3]);
+  }
+  return acc;
+}
+
 
 // ---- TP row-parallel decode GEMM (o_proj / down_proj): the all-reduce inside the epilogue ----
 // Under tensor parallelism every rank's GEMM yields a partial sum of the output. Instead of storing
@@ -385,7 +441,8 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[N
     float4 cs, sn;
     int slot;
     if constexpr (have) {
-      w = e.b0; cs = e.cs; sn = e.sn; slot = e.slot;
+      w = p.bias ? e.b0 : make_uint2(0, 0);  // (epi_pre_a read the weights when there is no bias)
+      cs = e.cs; sn = e.sn; slot = e.slot;
     } else {
       const int mm = m < p.M ? m : p.M - 1;
       w = p.bias ? *reinterpret_cast<const uint2*>(p.bias + qkv_col(nt0, nsub)) : make_uint2(0, 0);

@@ -79,13 +79,10 @@ bool launch_gemm_prefill(const GemmArgs& g, hipStream_t st);
 // medium-M GEMM (gemm_mid.hip, 16 < M <= 64): W = g.waves tiles per block, g.splitk K slices
 // (0 = heuristic); returns false for a shape / mode it does not take (caller falls back)
 bool launch_gemm_mid(const GemmArgs& g, hipStream_t st);
-// AWQ W4A16 decode, wide form (gemm_awq_wide.hip: M <= 16, one block per CU owning whole tiles, x and
-// the group scales staged once per CU); returns false for a shape / mode it does not take
-bool launch_awq_wide(const GemmArgs& g, hipStream_t st);
 // AWQ W4A16 decode, register-stationary activations (gemm_awq_kx.hip: M <= 16, group 128, packed
-// scales; WIDE one block per CU / TILE one tile per block + K slices). False: shape / mode not taken.
+// scales; WIDE one block per CU / GROUP 1-4 tiles per block + K slices). False: shape / mode not taken.
 bool launch_awq_kx(const GemmArgs& g, hipStream_t st);
-// AWQ W4A16 medium-M kernel (gemm_awq_wide.hip, 16 < M <= 64): g.waves tiles per block (8: one block
+// AWQ W4A16 medium-M kernel (gemm_awq_mid.hip, 16 < M <= 64): g.waves tiles per block (8: one block
 // per CU owning whole tiles), g.splitk K slices; false for a shape / mode it does not take
 bool launch_awq_mid(const GemmArgs& g, hipStream_t st);
 // AWQ int4 fragments -> bf16 fragment-packed copy (optionally gamma-folded) for the prefill kernel

@@ -562,13 +562,13 @@ def test_awq_norm_handoff(M, producer):
         assert _rel_err(out_h, out_n) < 1e-2, (layout, _rel_err(out_h, out_n))
 
 
-@pytest.mark.parametrize("kernel", [0, -1, -2, 2, 4])
+@pytest.mark.parametrize("kernel", [0, -2, -12])
 @pytest.mark.parametrize("N,K", [(17920, 1536), (1536, 8960), (2048, 1536)])
 def test_awq_decode_kernels_each(kernel, N, K):
     """Every AWQ decode kernel on the Qwen2.5-1.5B shapes (M = 8, group 128, RMSNorm gamma in
-    registers): 0 = launcher's choice (awq_stream_kernel for wide N / deep K), -1 = LDS-staged
-    awq_dec_kernel, -2 = K-split awq_gemm_kernel, 2 / 4 = awq_stream_kernel with that many tiles
-    per block; == the dequantised fp32 reference."""
+    registers): 0 = launcher's choice (the register-stationary kernel, gemm_awq_kx.hip), -2 = the
+    K-split awq_gemm_kernel (TP / group-64 fallback), -12 = the register-stationary kernel forced;
+    == the dequantised fp32 reference."""
     torch.manual_seed(N + K + kernel)
     M, g = 8, 128
     q = torch.randint(0, 16, (N, K), dtype=torch.int32)
@@ -589,101 +589,20 @@ def test_awq_decode_kernels_each(kernel, N, K):
     assert _rel_err(out, want) < 2e-2
 
 
-@pytest.mark.parametrize("ntb", [1, 2, 4])
-@pytest.mark.parametrize("M", [1, 8, 16])
-@pytest.mark.parametrize("sk", [0, 2])
-def test_awq_stream_multitile(ntb, M, sk):
-    """awq_stream_kernel with NTB tiles per block (one set of activation loads per k-quad for
-    all tiles): plain + residual, SiLU pairs, gamma in registers and the RMSNorm hand-off
-    (hg / per-tile sums of squares written by the epilogue), with and without split-K
-    == the dequantised fp32 reference and the one-tile form."""
-    torch.manual_seed(300 + 10 * ntb + M + sk)
-    C = ops.native()
-    ws = ops.workspace(torch.device(DEV))
-    N, K, g = 4096, 1536, 128
-    q = torch.randint(0, 16, (N, K), dtype=torch.int32)
-    scales = (torch.rand(K // g, N) * 0.02 + 0.005).bfloat16()
-    zeros = torch.randint(0, 16, (K // g, N)).float().bfloat16()
-    wd = ref.awq_dequant_ref(q, scales, zeros, g).to(DEV)
-    x = torch.randn(M, K, device=DEV).bfloat16()
-    res = torch.randn(M, N, device=DEV).bfloat16()
-    awq = {"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV), "group": g}
-    lin = ops.Linear(None, awq=dict(awq))
-    kw = dict(ws=ws, awq_scales=lin.scales, awq_zeros=lin.zeros, group=g, awq_szp=lin.szp, splitk=sk)
-    outs = {}
-    for t in (1, ntb):
-        out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-        C.gemm(x, lin.wp, N, K, out, 0, res=res, ntb=t, **kw)
-        outs[t] = out
-    assert _rel_err(outs[ntb], ref.linear_ref(x, wd, None, res)) < 2e-2
-    assert _rel_err(outs[ntb], outs[1]) < 1e-2  # wave k-split differs with the tile count
-    # RMSNorm gamma in registers + SiLU pairs
-    silu = ops.Linear(None, awq=dict(awq, silu=True))
-    nw = (torch.rand(K, device=DEV) + 0.5).bfloat16()
-    xn, _ = ref.rmsnorm_ref(x, nw, 1e-6)
-    ys = torch.empty(M, N // 2, device=DEV, dtype=torch.bfloat16)
-    C.gemm(x, silu.wp, N, K, ys, 2, norm_w=nw, eps=1e-6, ntb=ntb,
-           **dict(kw, awq_scales=silu.scales, awq_zeros=silu.zeros, awq_szp=silu.szp))
-    assert _rel_err(ys, ref.silu_mul_linear_ref(xn, wd[: N // 2], wd[N // 2:])) < 2e-2
-    # hand-off epilogue: h = x W^T + res, hg = bf16(h * gamma), per-16-column sums of h^2
-    gamma = (torch.rand(N, device=DEV) + 0.5).bfloat16()
-    h = res.clone()
-    hg = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-    ssp = torch.empty(M, N // 16, dtype=torch.float32, device=DEV)
-    C.gemm(x, lin.wp, N, K, h, 0, res=h, ntb=ntb, hg_out=hg, hg_gamma=gamma, ssp_out=ssp, **kw)
-    assert torch.equal(h, outs[ntb])
-    assert torch.equal(hg, (h.float() * gamma.float()).bfloat16())
-    torch.testing.assert_close(ssp, h.float().pow(2).reshape(M, N // 16, 16).sum(-1), rtol=1e-5, atol=1e-4)
-
-
-@pytest.mark.parametrize("M", [1, 8, 16])
-@pytest.mark.parametrize("N", [2 * 8960, 4096 * 2, 1024])
-def test_awq_wide_decode(M, N):
-    """The wide int4 decode kernel (gemm_awq_wide.hip, ntb = -8: one block per CU owning whole tiles,
-    x and the packed scales staged once per CU) == the dequantised fp32 reference: plain + residual,
-    SiLU pairs, and the RMSNorm hand-off consumer (x = h * gamma, row scale from the producer's
-    per-tile sums of squares); 4-5 tiles per block with idle waves (N = 17920), 2 per block, and
-    fewer tiles than CUs."""
-    torch.manual_seed(400 + M + N)
-    C = ops.native()
-    ws = ops.workspace(torch.device(DEV))
-    K, g = 1536, 128
-    q = torch.randint(0, 16, (N, K), dtype=torch.int32)
-    scales = (torch.rand(K // g, N) * 0.02 + 0.005).bfloat16()
-    zeros = torch.randint(0, 16, (K // g, N)).float().bfloat16()
-    wd = ref.awq_dequant_ref(q, scales, zeros, g).to(DEV)
-    x = torch.randn(M, K, device=DEV).bfloat16()
-    res = torch.randn(M, N, device=DEV).bfloat16()
-    awq = {"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV), "group": g}
-    lin = ops.Linear(None, awq=dict(awq))
-    kw = dict(ws=ws, awq_scales=lin.scales, awq_zeros=lin.zeros, group=g, awq_szp=lin.szp)
-    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    C.gemm(x, lin.wp, N, K, out, 0, res=res, ntb=-8, **kw)
-    assert _rel_err(out, ref.linear_ref(x, wd, None, res)) < 2e-2
-    # hand-off consumer: x = hg = bf16(h * gamma) with the producer's per-16-column sums of h^2
-    silu = ops.Linear(None, awq=dict(awq, silu=True))
-    h = torch.randn(M, K, device=DEV).bfloat16()
-    gamma = (torch.rand(K, device=DEV) + 0.5).bfloat16()
-    hg = (h.float() * gamma.float()).bfloat16()
-    ssp = h.float().pow(2).reshape(M, K // 16, 16).sum(-1).contiguous()
-    ys = torch.empty(M, N // 2, device=DEV, dtype=torch.bfloat16)
-    C.gemm(hg, silu.wp, N, K, ys, 2, eps=1e-6, ntb=-8, ssp_in=ssp,
-           **dict(kw, awq_scales=silu.scales, awq_zeros=silu.zeros, awq_szp=silu.szp))
-    xn, _ = ref.rmsnorm_ref(h, gamma, 1e-6)
-    assert _rel_err(ys, ref.silu_mul_linear_ref(xn, wd[: N // 2], wd[N // 2:])) < 2e-2
-
-
 @pytest.mark.parametrize("M", [1, 5, 8, 13, 16])
-@pytest.mark.parametrize("N,K,w,sk", [(2 * 8960, 1536, 0, 0), (4096 * 2, 1536, 0, 0), (2 * 8960, 1536, 8, 0),
-                                      (1536, 8960, 0, 0), (1536, 1536, 0, 0), (1536, 1536, 6, 2),
-                                      (1024, 2048, 4, 3), (2048, 1536, 16, 1)])
-def test_awq_kx_decode(M, N, K, w, sk):
-    """The register-stationary int4 decode kernel (gemm_awq_kx.hip; ntb = -12 forces it with the given
-    waves / K slices, 0 = its own choice) == the dequantised fp32 reference: WIDE blocks (one per CU,
-    4-5 or 2 tiles each) and TILE blocks (one tile, 1-3 K slices: granules / slabs), XP = 2 (M <= 8)
-    and XP = 1; plain + residual, RMSNorm gamma in registers + SiLU pairs, the hand-off consumer
-    (x = h * gamma, row scale from the producer's per-tile sums) and the hand-off producer (hg, sums)."""
-    torch.manual_seed(700 + M + N // 64 + K // 128 + w + sk)
+@pytest.mark.parametrize("N,K,w,sk,tb", [(2 * 8960, 1536, 0, 0, 1), (4096 * 2, 1536, 0, 0, 1), (2 * 8960, 1536, 8, 0, 1),
+                                         (1536, 8960, 0, 0, 1), (1536, 1536, 0, 0, 1), (1536, 1536, 6, 2, 1),
+                                         (1024, 2048, 4, 3, 1), (2048, 1536, 16, 1, 1), (1536, 8960, 12, 4, 2),
+                                         (1536, 8960, 8, 8, 4), (1536, 1536, 6, 1, 2)])
+def test_awq_kx_decode(M, N, K, w, sk, tb):
+    """The register-stationary int4 decode kernel (gemm_awq_kx.hip; ntb = -12 / -13 / -14 forces it with
+    1 / 2 / 4 tiles per GROUP block and the given waves / K slices, 0 = its own choice) == the
+    dequantised fp32 reference: WIDE blocks (one per CU, 4-5 or 2 tiles each) and GROUP blocks (1-4
+    tiles, 1-8 K slices: granules / slabs), XP = 2 (M <= 8) and XP = 1; plain + residual, RMSNorm
+    gamma in registers + SiLU pairs, the hand-off consumer (x = h * gamma, row scale from the
+    producer's per-tile sums) and the hand-off producer (hg, sums). (Multi-tile GROUP blocks take the
+    plain / residual / producer GEMMs; the norm consumers fall back on one-tile blocks.)"""
+    torch.manual_seed(700 + M + N // 64 + K // 128 + w + sk + tb)
     C = ops.native()
     ws = ops.workspace(torch.device(DEV))
     g = 128
@@ -693,8 +612,8 @@ def test_awq_kx_decode(M, N, K, w, sk):
     wd = ref.awq_dequant_ref(q, scales, zeros, g).to(DEV)
     awq = {"qint": q, "scales": scales.to(DEV), "zeros": zeros.to(DEV), "group": g}
     lin = ops.Linear(None, awq=dict(awq))
-    kw = dict(ws=ws, awq_scales=lin.scales, awq_zeros=lin.zeros, group=g, awq_szp=lin.szp, ntb=-12, waves=w,
-              splitk=sk)
+    kw = dict(ws=ws, awq_scales=lin.scales, awq_zeros=lin.zeros, group=g, awq_szp=lin.szp, ntb={1: -12, 2: -13, 4: -14}[tb],
+              waves=w, splitk=sk, sk_ws=ops.sk_workspace(torch.device(DEV)), fault=ops.fault_word(torch.device(DEV)))
     x = torch.randn(M, K, device=DEV).bfloat16()
     res = torch.randn(M, N, device=DEV).bfloat16()
     out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)

@@ -111,7 +111,7 @@ def pack_awq(qint: torch.Tensor) -> torch.Tensor:
 
 
 def pack_awq_sz(scales: torch.Tensor, sz: torch.Tensor) -> torch.Tensor:
-    """Group scales in the AWQ decode kernel's fragment order (csrc/kernels/gemm.hip awq_dec_kernel):
+    """Group scales in the AWQ decode kernels' fragment order (csrc/kernels/gemm_awq_kx.hip, gemm_awq_mid.hip):
     [N/16][K/128][4 lane groups][s(4 cols), s*z(4 cols)] bf16, so the lanes of a 16-lane group load
     their 4 columns' scale AND zero term with ONE 16-B load per (tile, k-quad). Group 128 only."""
     G, N = scales.shape
@@ -321,13 +321,13 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
     awq_mid = (lin.kind == "awq" and 16 < M <= 64 and row_idx is None and waves == 0 and splitk == 0
                and path == 0 and lin.group == 128 and getattr(lin, "szp", None) is not None)
     if awq_mid:
-        path = 2  # int4 medium kernel (csrc/kernels/gemm_awq_wide.hip awq_mid_kernel): no bf16 scratch
+        path = 2  # int4 medium kernel (csrc/kernels/gemm_awq_mid.hip awq_mid_kernel): no bf16 scratch
     elif lin.kind == "awq" and M >= AWQ_DEQUANT_MIN_M and row_idx is None and waves == 0 and splitk == 0:
         return _linear_awq_dequant(x, lin, out, residual, norm, qkv, epi, M)
     ntb = 0
     sk = False
     if M <= 16 and waves == 0 and splitk == 0:
-        waves, splitk, ntb = lin.dec_waves, lin.dec_splitk, lin.dec_ntb  # (AWQ ntb -8: the wide int4 kernel)
+        waves, splitk, ntb = lin.dec_waves, lin.dec_splitk, lin.dec_ntb
         # stream-K decode kernel (csrc/kernels/gemm_streamk.hip): per-Linear plan, else the module default
         sk = (lin.kind == "dense" and path == 0 and row_idx is None and norm_out is None and ar is None
               and (lin.dec_sk if lin.dec_sk is not None else STREAMK_DECODE))
