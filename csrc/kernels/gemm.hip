@@ -148,6 +148,15 @@ void launch_gemm(const GemmArgs& g, hipStream_t st) {
   // mixed prefill + decode steps (16 < M <= 64): the medium-M kernel when the start-up tuner
   // measured it faster (path 2, gemm_mid.hip); it declines shapes / modes it does not take
   if (g.path == 2 && launch_gemm_mid(g, st)) return;
+  // decode rows on the register-stationary kernel (path 4: a decode plan / forced; gemm_kx_bf16.hip)
+  if (g.path == 4) {
+    GemmArgs h = g;
+    if (h.ntb > -12 || h.ntb < -14) h.ntb = 0;
+    if (launch_dense_kx(h, st)) return;
+    h.path = 0; h.waves = 0; h.splitk = 0; h.ntb = 0;
+    launch_dispatch<false>(to_params(h), h, st);
+    return;
+  }
   // decode rows on the stream-K kernel (path 3: a decode plan / forced), else the tile-per-block kernels
   if (g.path == 3) {
     if (launch_gemm_sk(g, st)) return;

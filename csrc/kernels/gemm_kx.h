@@ -1,4 +1,5 @@
-// AWQ W4A16 decode GEMM (M <= 16), register-stationary activations ("kx").
+// Decode GEMM (M <= 16) with register-stationary activations ("kx"): AWQ W4A16 (gemm_kx_q4.hip) and
+// bf16 (gemm_kx_bf16.hip) instantiations of one kernel template.
 //
 // An int4 k-quad of one 16-column tile is 1 KiB of weights, but at M = 8 the k-quad's activations are
 // 2 KiB and its (s, s z) record is fetched as a 1 KiB lane load: a kernel that pairs every weight
@@ -31,6 +32,7 @@
 //         weight byte (deep K: down_proj), one tile = the shortest block (qkv / o_proj).
 // NORM: 0 none; 1 RMSNorm gamma in registers (x * gamma in bf16, raw x^2 summed; layer 0 of the
 // hand-off chain); 3 the producer's hand-off (x = h * gamma, row sums of squares in ssp_in).
+#pragma once
 #include "gemm_decode.h"
 
 namespace vgate {
@@ -62,19 +64,24 @@ __device__ __forceinline__ float kx_sum8(uint4 v, float acc) {  // acc + the 8 b
   return acc;
 }
 
-// XP: k-steps per activation load (2: M <= 8, 1: M <= 16); KQW: k-quads per wave (host: >= the
-// wave's range); TMAX: tiles per block (WIDE: at most, GROUP: exactly). Registers of loads in flight per lane:
-// kx_regs (+ the NORM 3 prefetch); up to 80 the block may hold 16 waves (128 VGPRs each), else 8.
-template <int XP, int KQW, int TMAX, int NORM>
+// Q4: int4 weights + packed scales (else bf16 fragment-packed weights: 4 loads per k-quad and tile, no
+// scales, no dequant — the same grid forms for the dense decode GEMMs). XP: k-steps per activation load
+// (2: M <= 8, 1: M <= 16); KQW: k-quads per wave (host: >= the wave's range); TMAX: tiles per block
+// (WIDE: at most, GROUP: exactly). Registers of loads in flight per lane: kx_regs (+ the NORM 3
+// prefetch); up to 80 the block may hold 16 waves (128 VGPRs each), up to 120 12 waves, else 8.
+template <bool Q4, int XP, int KQW, int TMAX, int NORM>
 __host__ __device__ constexpr int kx_regs() {
-  return 4 * KQW * ((4 / XP) * (NORM == 1 ? 2 : 1) + 2 * TMAX) + (NORM == 3 ? 4 * SS_PRE : 0);
+  return 4 * KQW * ((4 / XP) * (NORM == 1 ? 2 : 1) + (Q4 ? 2 : 4) * TMAX) + (NORM == 3 ? 4 * SS_PRE : 0);
 }
-template <int XP, int KQW, int TMAX, int NORM>
-__host__ __device__ constexpr int kx_max_threads() { return kx_regs<XP, KQW, TMAX, NORM>() <= 80 ? 1024 : 512; }
+template <bool Q4, int XP, int KQW, int TMAX, int NORM>
+__host__ __device__ constexpr int kx_max_threads() {
+  return kx_regs<Q4, XP, KQW, TMAX, NORM>() <= 80 ? 1024 : kx_regs<Q4, XP, KQW, TMAX, NORM>() <= 120 ? 768 : 512;
+}
 
-template <int XP, int KQW, int TMAX, int EPI, int NORM, bool WIDE>
-__global__ __launch_bounds__((kx_max_threads<XP, KQW, TMAX, NORM>())) void awq_kx_kernel(GemmParams p) {
+template <bool Q4, int XP, int KQW, int TMAX, int EPI, int NORM, bool WIDE>
+__global__ __launch_bounds__((kx_max_threads<Q4, XP, KQW, TMAX, NORM>())) void kx_kernel(GemmParams p) {
   static_assert(EPI != EPI_QKV || (!WIDE && TMAX == 1), "QKV: one-tile GROUP blocks (prefetched RoPE operands)");
+  static_assert(Q4 ? NORM != 2 : NORM != 1, "int4: gamma in registers or the hand-off; bf16: gamma folded into W");
   constexpr bool PRE = !WIDE && TMAX <= 2;  // GROUP blocks of 1-2 tiles: epilogue operands at launch
   constexpr int R = 16 / XP;   // real rows one load covers
   constexpr int XL = 4 / XP;   // activation loads per k-quad
@@ -119,10 +126,12 @@ __global__ __launch_bounds__((kx_max_threads<XP, KQW, TMAX, NORM>())) void awq_k
   const int mrow = r16 % R;
   const bf16_t* xrow = p.x + (size_t)row_of_e<EPI>(p, mrow) * p.lda + 8 * grp + (XP > 1 ? (r16 / R) * 32 : 0);
   const bf16_t* grow = NORM == 1 ? p.norm_w + 8 * grp + (XP > 1 ? (r16 / R) * 32 : 0) : nullptr;
-  const uint4* wbase = p.wp + (size_t)t0 * KQ * 64 + lane;
+  constexpr int WL = Q4 ? 1 : 4;  // weight loads per (k-quad, tile)
+  const int KT = KQ * 4;
+  const uint4* wbase = p.wp + (size_t)t0 * (Q4 ? KQ : KT) * 64 + lane;
   const uint4* szbase = reinterpret_cast<const uint4*>(p.szp) + (size_t)t0 * KQ * 4 + grp;
   constexpr int GL = NORM == 1 ? XL : 1;
-  uint4 xa[KQW][XL], ga[KQW][GL], w[KQW][TMAX], sz[KQW][TMAX];
+  uint4 xa[KQW][XL], ga[KQW][GL], w[KQW][TMAX][WL], sz[KQW][TMAX];
   // every load unconditional (clamped re-reads past the wave's range are never consumed): a load
   // under a branch leaves the paths with different outstanding counts, and the compiler's waits
   // after the join then cover loads issued later (the weight stream) as well
@@ -138,9 +147,15 @@ __global__ __launch_bounds__((kx_max_threads<XP, KQW, TMAX, NORM>())) void awq_k
     }
 #pragma unroll
     for (int j = 0; j < TMAX; ++j) {
-      const size_t u = (size_t)min(j, ntb - 1) * KQ + kq;
-      w[q][j] = ld_nt16(wbase + u * 64);
-      sz[q][j] = szbase[u * 4];
+      const size_t tj = (size_t)min(j, ntb - 1);
+      if constexpr (Q4) {
+        const size_t u = tj * KQ + kq;
+        w[q][j][0] = ld_nt16(wbase + u * 64);
+        sz[q][j] = szbase[u * 4];
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) w[q][j][t] = ld_nt16(wbase + (tj * KT + kq * 4 + t) * 64);
+      }
     }
   }
   asm volatile("" ::: "memory");  // every load of the wave is in flight before the first MFMA
@@ -149,7 +164,7 @@ __global__ __launch_bounds__((kx_max_threads<XP, KQW, TMAX, NORM>())) void awq_k
   f32x4 acc[TMAX];
 #pragma unroll
   for (int j = 0; j < TMAX; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float ssr = 0.f;  // NORM 1: this wave's raw x^2 of row r16 (lane quarter)
+  float ssr = 0.f;  // NORM 1 / 2: this wave's raw x^2 of row r16 (lane quarter)
 #pragma unroll
   for (int q = 0; q < KQW; ++q) {
     if (q >= nq) break;  // wave-uniform
@@ -171,7 +186,18 @@ __global__ __launch_bounds__((kx_max_threads<XP, KQW, TMAX, NORM>())) void awq_k
       }
     };
     uint4 src[XL], b[4];
-    if constexpr (NORM == 1) {
+    if constexpr (NORM == 2) {  // bf16, gamma folded into W: the raw rows' sum of squares only
+#pragma unroll
+      for (int v = 0; v < XL; ++v) src[v] = xa[q][v];
+      unpack(src, b);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float f[8];
+        unpack8(b[t], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ssr += f[j] * f[j];
+      }
+    } else if constexpr (NORM == 1) {
       // sum of squares over the RAW activations, unpacked (lane <-> row r16, as gemm_finish folds
       // it); the MFMA operand is bf16(x * gamma), gamma packed like x
       uint4 raw[4];
@@ -196,7 +222,17 @@ __global__ __launch_bounds__((kx_max_threads<XP, KQW, TMAX, NORM>())) void awq_k
 #pragma unroll
       for (int v = 0; v < XL; ++v) src[v] = xa[q][v];
     }
-    unpack(src, b);
+    if constexpr (NORM != 2) unpack(src, b);
+    if constexpr (!Q4) {
+#pragma unroll
+      for (int j = 0; j < TMAX; ++j) {
+        if (j < ntb) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[j] = mfma16(as_bf16x8(w[q][j][t]), as_bf16x8(b[t]), acc[j]);
+        }
+      }
+      continue;
+    }
     float X = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t) X = kx_sum8(b[t], X);
@@ -206,10 +242,10 @@ __global__ __launch_bounds__((kx_max_threads<XP, KQW, TMAX, NORM>())) void awq_k
     for (int j = 0; j < TMAX; ++j) {
       if (j < ntb) {
         f32x4 pr = {0.f, 0.f, 0.f, 0.f};
-        pr = mfma16(kx_raw8(w[q][j].x, c43), as_bf16x8(b[0]), pr);
-        pr = mfma16(kx_raw8(w[q][j].y, c43), as_bf16x8(b[1]), pr);
-        pr = mfma16(kx_raw8(w[q][j].z, c43), as_bf16x8(b[2]), pr);
-        pr = mfma16(kx_raw8(w[q][j].w, c43), as_bf16x8(b[3]), pr);
+        pr = mfma16(kx_raw8(w[q][j][0].x, c43), as_bf16x8(b[0]), pr);
+        pr = mfma16(kx_raw8(w[q][j][0].y, c43), as_bf16x8(b[1]), pr);
+        pr = mfma16(kx_raw8(w[q][j][0].z, c43), as_bf16x8(b[2]), pr);
+        pr = mfma16(kx_raw8(w[q][j][0].w, c43), as_bf16x8(b[3]), pr);
         const uint4 s = sz[q][j];
         const float s4[4] = {bf_lo(s.x), bf_hi(s.x), bf_lo(s.y), bf_hi(s.y)};
         const float z4[4] = {bf_lo(s.z), bf_hi(s.z), bf_lo(s.w), bf_hi(s.w)};
@@ -223,7 +259,7 @@ __global__ __launch_bounds__((kx_max_threads<XP, KQW, TMAX, NORM>())) void awq_k
 #pragma unroll
     for (int j = 0; j < TMAX; ++j) a1[0][j] = acc[j];
     float sr[1] = {0.f};
-    if constexpr (NORM == 1) sr[0] = ssr;
+    if constexpr (NORM == 1 || NORM == 2) sr[0] = ssr;
     if constexpr (NORM == 3) {
       if (ss_wave) sr[0] = ss_pre_sum(p, ssv, r16, grp);
     }
@@ -236,7 +272,7 @@ __global__ __launch_bounds__((kx_max_threads<XP, KQW, TMAX, NORM>())) void awq_k
 #pragma unroll
     for (int j = 0; j < TMAX; ++j)
       if (j < ntb && row_ok) red[(wid * TMAX + j) * 64 + lane] = acc[j];
-    if constexpr (NORM == 1) {
+    if constexpr (NORM == 1 || NORM == 2) {
       ssr += xor16(ssr);
       ssr += xor32(ssr);
       if (lane < 16) ssq[wid * 16 + lane] = ssr;
@@ -246,7 +282,7 @@ __global__ __launch_bounds__((kx_max_threads<XP, KQW, TMAX, NORM>())) void awq_k
     f32x4 v[1] = {{0.f, 0.f, 0.f, 0.f}};
     if (row_ok)
       for (int w2 = 0; w2 < nw; ++w2) v[0] += red[(w2 * TMAX + wid) * 64 + lane];
-    if constexpr (NORM == 1) {
+    if constexpr (NORM == 1 || NORM == 2) {
       float ss = 0.f;
       for (int w2 = 0; w2 < nw; ++w2) ss += ssq[w2 * 16 + r16];
       v[0] *= rsqrtf(ss / (float)p.K + p.eps);
@@ -271,12 +307,12 @@ static int kx_cus() {
   return n;
 }
 
-template <int XP, int KQW, int TMAX, int EPI, int NORM, bool WIDE>
+template <bool Q4, int XP, int KQW, int TMAX, int EPI, int NORM, bool WIDE>
 static bool kx_go(const GemmParams& p, dim3 grid, int nw, hipStream_t st) {
-  if (64 * nw > kx_max_threads<XP, KQW, TMAX, NORM>()) return false;
+  if (64 * nw > kx_max_threads<Q4, XP, KQW, TMAX, NORM>()) return false;
   const size_t lds = WIDE ? (size_t)nw * TMAX * 1024 + (size_t)nw * 16 * 4 : red_bytes<1, TMAX>(nw) + ssq_bytes<1>(nw) + 16;
   if (lds > 160 * 1024) return false;
-  auto kern = awq_kx_kernel<XP, KQW, TMAX, EPI, NORM, WIDE>;
+  auto kern = kx_kernel<Q4, XP, KQW, TMAX, EPI, NORM, WIDE>;
   if (lds > 64 * 1024) {
     static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
@@ -291,7 +327,7 @@ static bool kx_go(const GemmParams& p, dim3 grid, int nw, hipStream_t st) {
 // default 1), K slices while the grid still fits the CUs and every slice keeps >= 16 k-quads
 // (down_proj: 96 tiles x 2 slices of 35), min(16, slice) waves. g.waves / g.splitk force the wave /
 // slice counts (sweeps, tests).
-template <int XP, int TB, int EPI, int NORM>
+template <bool Q4, int XP, int TB, int EPI, int NORM>
 static bool kx_group(GemmParams p, const GemmArgs& g, hipStream_t st) {
   const int ntiles = g.N / 16, KQ = g.K / 128, ncu = kx_cus();
   if (ntiles % TB) return false;
@@ -315,34 +351,34 @@ static bool kx_group(GemmParams p, const GemmArgs& g, hipStream_t st) {
     if (TB == 1 && S == 2 && g.sk_pub != nullptr && need_g <= g.sk_bytes) p.gran = reinterpret_cast<uint4*>(g.sk_pub);
     else if (g.slabs == nullptr || need_slab > g.slab_bytes || groups > g.max_counters) return false;
   }
-  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_kx", groups * S);
+  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take(Q4 ? "awq_kx" : "kx", groups * S);
   const dim3 grid(groups, 1, S);
   if constexpr (TB == 1) {
     switch (kqw) {
-      case 1: return kx_go<XP, 1, 1, EPI, NORM, false>(p, grid, nw, st);
-      case 2: return kx_go<XP, 2, 1, EPI, NORM, false>(p, grid, nw, st);
-      case 3: return kx_go<XP, 3, 1, EPI, NORM, false>(p, grid, nw, st);
-      case 4: return kx_go<XP, 4, 1, EPI, NORM, false>(p, grid, nw, st);
-      case 5: return kx_go<XP, 5, 1, EPI, NORM, false>(p, grid, nw, st);
-      default: return kx_go<XP, 6, 1, EPI, NORM, false>(p, grid, nw, st);
+      case 1: return kx_go<Q4, XP, 1, 1, EPI, NORM, false>(p, grid, nw, st);
+      case 2: return kx_go<Q4, XP, 2, 1, EPI, NORM, false>(p, grid, nw, st);
+      case 3: return kx_go<Q4, XP, 3, 1, EPI, NORM, false>(p, grid, nw, st);
+      case 4: return kx_go<Q4, XP, 4, 1, EPI, NORM, false>(p, grid, nw, st);
+      case 5: return kx_go<Q4, XP, 5, 1, EPI, NORM, false>(p, grid, nw, st);
+      default: return kx_go<Q4, XP, 6, 1, EPI, NORM, false>(p, grid, nw, st);
     }
   } else if constexpr (TB == 2) {
     switch (kqw) {
-      case 1: return kx_go<XP, 1, 2, EPI, NORM, false>(p, grid, nw, st);
-      case 2: return kx_go<XP, 2, 2, EPI, NORM, false>(p, grid, nw, st);
-      case 3: return kx_go<XP, 3, 2, EPI, NORM, false>(p, grid, nw, st);
+      case 1: return kx_go<Q4, XP, 1, 2, EPI, NORM, false>(p, grid, nw, st);
+      case 2: return kx_go<Q4, XP, 2, 2, EPI, NORM, false>(p, grid, nw, st);
+      case 3: return kx_go<Q4, XP, 3, 2, EPI, NORM, false>(p, grid, nw, st);
       default: return false;
     }
   } else {
     switch (kqw) {
-      case 1: return kx_go<XP, 1, 4, EPI, NORM, false>(p, grid, nw, st);
-      case 2: return kx_go<XP, 2, 4, EPI, NORM, false>(p, grid, nw, st);
+      case 1: return kx_go<Q4, XP, 1, 4, EPI, NORM, false>(p, grid, nw, st);
+      case 2: return kx_go<Q4, XP, 2, 4, EPI, NORM, false>(p, grid, nw, st);
       default: return false;
     }
   }
 }
 
-template <int XP, int EPI, int NORM>
+template <bool Q4, int XP, int EPI, int NORM>
 static bool kx_launch_xp(GemmParams p, const GemmArgs& g, hipStream_t st) {
   const int ntiles = g.N / 16, KQ = g.K / 128, ncu = kx_cus();
   if constexpr (EPI != EPI_QKV) {
@@ -351,32 +387,29 @@ static bool kx_launch_xp(GemmParams p, const GemmArgs& g, hipStream_t st) {
       const int nw = g.waves > 0 ? g.waves : std::min(16, KQ);
       if (nw > 16) return false;
       const int kqw = (KQ + nw - 1) / nw;
-      if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("awq_kx_wide", nb);
+      if (p.dbg_ts == nullptr) p.dbg_ts = tl_take(Q4 ? "awq_kx_wide" : "kx_wide", nb);
       p.splitk = 1;
       const dim3 grid(nb);
-      if (tneed <= 2 && kqw == 1) return kx_go<XP, 1, 2, EPI, NORM, true>(p, grid, nw, st);
-      if (tneed <= 5 && kqw == 1) return kx_go<XP, 1, 5, EPI, NORM, true>(p, grid, nw, st);
-      if (tneed <= 5 && kqw == 2) return kx_go<XP, 2, 5, EPI, NORM, true>(p, grid, nw, st);
-      if (tneed <= 8 && kqw == 1) return kx_go<XP, 1, 8, EPI, NORM, true>(p, grid, nw, st);
+      if (tneed <= 2 && kqw == 1) return kx_go<Q4, XP, 1, 2, EPI, NORM, true>(p, grid, nw, st);
+      if (tneed <= 5 && kqw == 1) return kx_go<Q4, XP, 1, 5, EPI, NORM, true>(p, grid, nw, st);
+      if (tneed <= 5 && kqw == 2) return kx_go<Q4, XP, 2, 5, EPI, NORM, true>(p, grid, nw, st);
+      if (tneed <= 8 && kqw == 1) return kx_go<Q4, XP, 1, 8, EPI, NORM, true>(p, grid, nw, st);
       return false;
     }
     if constexpr (NORM == 0) {  // multi-tile GROUP blocks: the plain / residual (+ hand-off producer) GEMMs
-      if (g.ntb == -13) return kx_group<XP, 2, EPI, NORM>(p, g, st);
-      if (g.ntb == -14) return kx_group<XP, 4, EPI, NORM>(p, g, st);
+      if (g.ntb == -13) return kx_group<Q4, XP, 2, EPI, NORM>(p, g, st);
+      if (g.ntb == -14) return kx_group<Q4, XP, 4, EPI, NORM>(p, g, st);
     }
   }
-  return kx_group<XP, 1, EPI, NORM>(p, g, st);
+  return kx_group<Q4, XP, 1, EPI, NORM>(p, g, st);
 }
 
-template <int EPI, int NORM>
+template <bool Q4, int EPI, int NORM>
 static bool kx_launch(const GemmParams& p, const GemmArgs& g, hipStream_t st) {
-  return g.M <= 8 ? kx_launch_xp<2, EPI, NORM>(p, g, st) : kx_launch_xp<1, EPI, NORM>(p, g, st);
+  return g.M <= 8 ? kx_launch_xp<Q4, 2, EPI, NORM>(p, g, st) : kx_launch_xp<Q4, 1, EPI, NORM>(p, g, st);
 }
 
-bool launch_awq_kx(const GemmArgs& g, hipStream_t st) {
-  if (g.M <= 0 || g.M > 16 || g.awq_szp == nullptr || g.group != 128 || g.N % 16 != 0 || g.K % 128 != 0 ||
-      g.rownorm || g.ar_world > 0 || (g.ssp_in != nullptr && g.norm_w != nullptr) || g.epi == EPI_F32)
-    return false;
+static GemmParams kx_params(const GemmArgs& g) {
   GemmParams p{};
   p.x = g.x; p.lda = g.lda; p.M = g.M; p.row_idx = g.row_idx;
   p.wp = reinterpret_cast<const uint4*>(g.wp); p.N = g.N; p.K = g.K;
@@ -390,17 +423,7 @@ bool launch_awq_kx(const GemmArgs& g, hipStream_t st) {
   p.szp = g.awq_szp; p.group = g.group;
   p.dbg_ts = g.dbg_ts;
   p.hg = g.hg; p.hg_gamma = g.hg_gamma; p.ssp_out = g.ssp_out; p.ssp_in = g.ssp_in; p.ssn = g.ssn;
-  const int norm = g.norm_w != nullptr ? 1 : g.ssp_in != nullptr ? 3 : 0;
-#define VG_KX(E)                                            \
-  return norm == 1 ? kx_launch<E, 1>(p, g, st)              \
-       : norm == 3 ? kx_launch<E, 3>(p, g, st)              \
-                   : kx_launch<E, 0>(p, g, st)
-  switch (g.epi) {
-    case EPI_SILU: VG_KX(EPI_SILU);
-    case EPI_QKV: VG_KX(EPI_QKV);
-    default: VG_KX(EPI_BF16);
-  }
-#undef VG_KX
+  return p;
 }
 
 }  // namespace vgate

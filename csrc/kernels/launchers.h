@@ -79,9 +79,11 @@ bool launch_gemm_prefill(const GemmArgs& g, hipStream_t st);
 // medium-M GEMM (gemm_mid.hip, 16 < M <= 64): W = g.waves tiles per block, g.splitk K slices
 // (0 = heuristic); returns false for a shape / mode it does not take (caller falls back)
 bool launch_gemm_mid(const GemmArgs& g, hipStream_t st);
-// AWQ W4A16 decode, register-stationary activations (gemm_awq_kx.hip: M <= 16, group 128, packed
-// scales; WIDE one block per CU / GROUP 1-4 tiles per block + K slices). False: shape / mode not taken.
+// Decode GEMMs with register-stationary activations (gemm_kx.h; M <= 16; WIDE one block per CU / GROUP
+// 1-4 tiles per block + K slices): AWQ W4A16 (group 128, packed scales) and bf16. False: shape / mode
+// not taken (the caller falls back on the other decode kernels).
 bool launch_awq_kx(const GemmArgs& g, hipStream_t st);
+bool launch_dense_kx(const GemmArgs& g, hipStream_t st);
 // AWQ W4A16 medium-M kernel (gemm_awq_mid.hip, 16 < M <= 64): g.waves tiles per block (8: one block
 // per CU owning whole tiles), g.splitk K slices; false for a shape / mode it does not take
 bool launch_awq_mid(const GemmArgs& g, hipStream_t st);

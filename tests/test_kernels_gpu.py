@@ -589,6 +589,51 @@ def test_awq_decode_kernels_each(kernel, N, K):
     assert _rel_err(out, want) < 2e-2
 
 
+@pytest.mark.parametrize("M", [1, 8, 16])
+@pytest.mark.parametrize("N,K,w,sk,tb", [(2 * 8960, 1536, 0, 0, 1), (4096 * 2, 1536, 6, 0, 1), (1536, 8960, 0, 0, 1),
+                                         (1536, 8960, 8, 4, 2), (1536, 1536, 0, 0, 1), (1024, 2048, 8, 8, 4)])
+def test_dense_kx_decode(M, N, K, w, sk, tb):
+    """The register-stationary decode kernel on bf16 weights (path 4; ntb = -12 / -13 / -14 with the
+    given waves / K slices, or its own grid rule) == the fp32 reference and the tile kernels: plain +
+    residual, the hand-off producer (hg-free bf16 form: out + per-tile sums of squares), SiLU pairs with
+    the folded-gamma row scale (NORM 2) and as the hand-off consumer (NORM 3)."""
+    torch.manual_seed(900 + M + N // 64 + K // 128 + w + sk + tb)
+    C = ops.native()
+    dev = torch.device(DEV)
+    kw = dict(ws=ops.workspace(dev), sk_ws=ops.sk_workspace(dev), fault=ops.fault_word(dev), path=4, waves=w,
+              splitk=sk, ntb={1: -12 if (w or sk) else 0, 2: -13, 4: -14}[tb])
+    wt = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    lin = ops.Linear(wt)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    res = torch.randn(M, N, device=DEV).bfloat16()
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    C.gemm(x, lin.wp, N, K, out, 0, res=res, **kw)
+    assert _rel_err(out, ref.linear_ref(x, wt, None, res)) < 1e-2
+    tile = torch.empty_like(out)
+    C.gemm(x, lin.wp, N, K, tile, 0, res=res, ws=kw["ws"])
+    assert _rel_err(out, tile) < 5e-3
+    h = res.clone()
+    ssp_n = torch.empty(M, N // 16, dtype=torch.float32, device=DEV)
+    C.gemm(x, lin.wp, N, K, h, 0, res=h, ssp_out=ssp_n, **kw)
+    assert torch.equal(h, out)
+    torch.testing.assert_close(ssp_n, h.float().pow(2).reshape(M, N // 16, 16).sum(-1), rtol=1e-5, atol=1e-4)
+    # SiLU pairs, RMSNorm gamma folded into W: row scale from x (NORM 2) / from the producer's sums (NORM 3)
+    silu = ops.Linear(wt.clone(), kind="silu")
+    gamma = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+    assert silu.fold_norm(gamma)
+    xn, _ = ref.rmsnorm_ref(x, gamma, 1e-6)
+    want = ref.silu_mul_linear_ref(xn, wt[: N // 2], wt[N // 2:])
+    ys = torch.empty(M, N // 2, device=DEV, dtype=torch.bfloat16)
+    C.gemm(x, silu.wp, N, K, ys, 2, rownorm=True, eps=1e-6, **kw)
+    assert _rel_err(ys, want) < 2e-2
+    if K // 16 <= 128:
+        ssp = x.float().pow(2).reshape(M, K // 16, 16).sum(-1).contiguous()
+        yh = torch.empty_like(ys)
+        C.gemm(x, silu.wp, N, K, yh, 2, eps=1e-6, ssp_in=ssp, **kw)
+        assert _rel_err(yh, want) < 2e-2
+        assert _rel_err(yh, ys) < 1e-2
+
+
 @pytest.mark.parametrize("M", [1, 5, 8, 13, 16])
 @pytest.mark.parametrize("N,K,w,sk,tb", [(2 * 8960, 1536, 0, 0, 1), (4096 * 2, 1536, 0, 0, 1), (2 * 8960, 1536, 8, 0, 1),
                                          (1536, 8960, 0, 0, 1), (1536, 1536, 0, 0, 1), (1536, 1536, 6, 2, 1),

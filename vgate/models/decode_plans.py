@@ -8,7 +8,8 @@ their current plan (benchmarks/decode_sweep.py for TP = 1 models, benchmarks/tp_
 --sweep for one TP rank's shapes). A shape missing here measured best on the heuristic.
 
 Key: (N, K, layout, weight kind) of the packed weight; layout "qkv" / "silu" / "plain".
-Value: (waves, K slices, column tiles per block) of the tile-per-block kernels, or
+Value: (waves, K slices, column tiles per block) of the tile-per-block kernels, ("kx", waves, K
+slices, tiles code) for the register-stationary kernel (path 4; 0 = its own grid rule), or
 ("sk", waves, blocks per CU, k-steps per register group) for the stream-K kernel
 (csrc/kernels/gemm_streamk.hip: one equal share of the weight stream per CU), which wins on the
 large matrices where the tile count leaves CUs uneven (benchmarks/probes/sk_probe.py,
@@ -34,6 +35,11 @@ PLANS: dict[tuple[int, int, str, str], tuple] = {
     (6144, 4096, "qkv", "dense"): ("sk", 8, 1, 4),
     (28672, 4096, "silu", "dense"): (4, 1, 0),
     (4096, 14336, "plain", "dense"): (4, 1, 1),
+    # Qwen2.5-1.5B bf16 gate_up on the register-stationary kernel (one block per CU owning 4-5 whole
+    # tiles, every weight fragment requested at once; csrc/kernels/gemm_kx.h): 10.5 vs 11.9 us per
+    # launch as the hand-off consumer, cold weights (benchmarks/dense_kx_sweep.py,
+    # profiles/r5_dense_kx_sweep.log). qkv / o_proj / down_proj stay on the tile kernels there.
+    (17920, 1536, "silu", "dense"): ("kx", 0, 0, 0),
     # Qwen2.5-1.5B AWQ int4: no entries — every int4 decode GEMM runs the register-stationary kernel
     # (csrc/kernels/gemm_awq_kx.hip) on its own grid rule (round 3's awq_stream / wide plans:
     # profiles/r3_awq_decode_sweep.log)
@@ -49,6 +55,9 @@ def apply(model) -> int:
         if p is not None:
             if p[0] == "sk":
                 lin.dec_sk = tuple(p[1:])
+            elif p[0] == "kx":
+                lin.dec_path = 4
+                lin.dec_waves, lin.dec_splitk, lin.dec_ntb = p[1:]
             else:
                 lin.dec_waves, lin.dec_splitk, lin.dec_ntb = p
             n += 1

@@ -169,6 +169,7 @@ class Linear:
         self.dec_splitk = 0
         self.dec_sk = None  # stream-K decode kernel: None = STREAMK_DECODE, or (waves, blocks/CU, group)
         self.dec_ntb = 0
+        self.dec_path = 0  # 4: the register-stationary decode kernel (csrc/kernels/gemm_kx.h)
         # prefill (M >= 128) tile / K-slice choice per M bucket, measured at engine start-up
         # (tune_prefill); empty = the launcher's heuristic
         self.prefill_plan: dict[int, tuple[int, int]] = {}
@@ -328,6 +329,8 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
     sk = False
     if M <= 16 and waves == 0 and splitk == 0:
         waves, splitk, ntb = lin.dec_waves, lin.dec_splitk, lin.dec_ntb
+        if path == 0 and lin.kind == "dense" and row_idx is None and ar is None:
+            path = getattr(lin, "dec_path", 0)
         # stream-K decode kernel (csrc/kernels/gemm_streamk.hip): per-Linear plan, else the module default
         sk = (lin.kind == "dense" and path == 0 and row_idx is None and norm_out is None and ar is None
               and (lin.dec_sk if lin.dec_sk is not None else STREAMK_DECODE))
