@@ -555,8 +555,11 @@ __device__ __forceinline__ constexpr int vm_imm(int n) {  // s_waitcnt vmcnt(n),
   return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8);
 }
 
+// dec_seqs > 0: the step's decode rows ride in the same launch — grid rows y >= num_tiles are
+// (sequence, partition) decode blocks (part z == 0 of each KV head), so a prefill or mixed step has
+// ONE attention launch (in a prefill-only step those blocks see no single-token sequence and exit)
 template <int CT, int NW, int FL_NST, bool SWP>
-__global__ __launch_bounds__(64 * NW) void attn_flash_kernel(AttnArgs a, int lazy) {
+__global__ __launch_bounds__(64 * NW) void attn_flash_kernel(AttnArgs a, int lazy, int dec_seqs) {
   constexpr int P = (32 + NW - 1) / NW;  // DMA pieces per wave per chunk
   constexpr int FL_LDS = FL_NST * FL_STAGE;
   static_assert((FL_NST - 2) * P < 64, "vmcnt immediate");
@@ -571,6 +574,11 @@ __global__ __launch_bounds__(64 * NW) void attn_flash_kernel(AttnArgs a, int laz
   const int zs = gridDim.x / a.Hkv;
   const int h = blockIdx.x / zs;
   const int tile = blockIdx.y;
+  if (tile >= a.num_tiles) {  // block-uniform: a decode block
+    const int r = tile - a.num_tiles;
+    if (blockIdx.x % zs == 0 && dec_seqs > 0) decode_block(a, r % dec_seqs, h, r / dec_seqs, smem);
+    return;
+  }
   const int s = a.tile_seq[tile];
   if (s < 0) return;
   const int q0 = a.tile_q0[tile];
@@ -994,7 +1002,9 @@ void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
   const FlashCfg fc = tiles > 0 && flash_enabled() ? flash_cfg(a) : FlashCfg{0, 0};
   if (fc.ct > 0) {
     AttnArgs f = a;
-    f.tl = tl_take("attn_flash", tiles * a.Hkv);
+    f.num_tiles = tiles;
+    // the decode rows join this launch (grid rows past the tiles): no second attention launch
+    const int dec_rows = dec_seqs > 0 ? dec_seqs * a.num_parts : 0;
     // a 2-stage K/V ring with the lazy rescale (4 stages and eager rescale measured no faster:
     // profiles/r3_flash_split.log)
     constexpr int lazy = 1;
@@ -1016,15 +1026,22 @@ void launch_attention(const AttnArgs& a, int dec_seqs, hipStream_t st) {
       if (blocks * 4 <= cap) zs = 4;
       if (slots > 32768 || slots * zs * (fc.ct * 4 + 1) * 1024 > f.fl_ws_bytes) zs = 1;
     }
-    const dim3 grid(a.Hkv * zs, tiles, 1), block(64 * fc.nw);
-#define VG_FL(CT_, NW_) hipLaunchKernelGGL((attn_flash_kernel<CT_, NW_, 2, false>), grid, block, lds, st, f, lazy)
+    const dim3 grid(a.Hkv * zs, tiles + dec_rows, 1), block(64 * fc.nw);
+    f.tl = tl_take("attn_flash", (tiles + dec_rows) * a.Hkv * zs);
+    const size_t lds_all = std::max(lds, (size_t)attn_lds_bytes(fc.nw));
+#define VG_FL(CT_, NW_) hipLaunchKernelGGL((attn_flash_kernel<CT_, NW_, 2, false>), grid, block, lds_all, st, f, lazy, dec_seqs)
     if (fc.nw == 8) {
       if (fc.ct == 2) VG_FL(2, 8); else VG_FL(1, 8);
     } else {
       if (fc.ct == 2) VG_FL(2, 6); else VG_FL(1, 6);
     }
 #undef VG_FL
-    tiles = 0;
+    if (dec_seqs > 0 && a.num_parts > 1 && a.tickets == nullptr) {
+      AttnArgs b = a;
+      b.tl = tl_take("attn_reduce", dec_seqs * a.Hq);
+      hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(dec_seqs, a.Hq), dim3(128), 0, st, b);
+    }
+    return;
   }
   const int nw = attn_waves(a);
   const int dec_blocks = dec_seqs > 0 ? dec_seqs * a.num_parts : 0;
