@@ -24,13 +24,14 @@ from vgate import ops  # noqa: E402
 
 SHAPES = [("qkv", 2048, 1536, "plain"), ("o_proj", 1536, 1536, "plain"), ("gate_up", 17920, 1536, "silu"),
           ("down", 1536, 8960, "plain")]
-# (path, waves, splitk, ntb): path 0 = tile kernels (launcher's plan), 4 = register-stationary
+# (path, waves, splitk, ntb): path 0 = tile kernels (launcher's plan / forced waves, slices), 3 = stream-K
+# (waves 4 / 8, blocks per CU 1 / 2 in splitk, k-steps per group 4 / 8 in ntb), 4 = register-stationary
 CFGS = {
     "qkv": [(0, 0, 0, 0), (4, 0, 0, 0), (4, 8, 1, -12), (4, 6, 2, -12), (4, 16, 1, -12)],
     "o_proj": [(0, 0, 0, 0), (4, 0, 0, 0), (4, 8, 1, -12), (4, 6, 2, -12), (4, 12, 1, -13)],
     "gate_up": [(0, 0, 0, 0), (4, 0, 0, 0), (4, 8, 0, -12), (4, 6, 0, -12), (4, 12, 2, -13), (4, 12, 1, -13)],
-    "down": [(0, 0, 0, 0), (4, 0, 0, 0), (4, 16, 2, -12), (4, 8, 4, -13), (4, 16, 4, -13), (4, 8, 8, -14),
-             (4, 12, 3, -12)],
+    "down": [(0, 0, 0, 0), (4, 0, 0, 0), (4, 8, 4, -13), (3, 0, 0, 0), (3, 4, 0, 0), (3, 0, 2, 0), (3, 4, 2, 0),
+             (3, 0, 0, 4), (0, 16, 2, 0), (0, 8, 4, 0), (0, 8, 3, 0), (0, 4, 4, 0), (0, 8, 8, 0)],
 }
 
 
