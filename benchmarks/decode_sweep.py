@@ -53,9 +53,19 @@ def lins(model, kind):
     return [getattr(L, attr) for L in model.layers]
 
 
-def set_plan(model, kind, cfg):  # ntb -8: the wide medium kernel (ops.WIDE_DECODE)
+def set_plan(model, kind, cfg):
+    """cfg: (waves, K slices, tiles code) of the tile kernels, ("kx", waves, slices, tiles code) of the
+    register-stationary kernel (path 4) or ("sk", waves, blocks per CU, group) of stream-K."""
     for lin in lins(model, kind):
-        lin.dec_waves, lin.dec_splitk, lin.dec_ntb = cfg
+        lin.dec_path, lin.dec_sk = 0, False
+        if cfg[0] == "kx":
+            lin.dec_path = 4
+            lin.dec_waves, lin.dec_splitk, lin.dec_ntb = cfg[1:]
+        elif cfg[0] == "sk":
+            lin.dec_sk = tuple(cfg[1:])
+            lin.dec_waves, lin.dec_splitk, lin.dec_ntb = 0, 0, 0
+        else:
+            lin.dec_waves, lin.dec_splitk, lin.dec_ntb = cfg
 
 
 def time_step(eng, iters):

@@ -32,12 +32,17 @@ from vgate.runtime.sampling_params import SamplingParams  # noqa: E402
 
 KINDS = ("qkv", "o", "gate_up", "down")
 # (waves, split-K, tiles per block) candidates for the large-K per-rank shapes (0 = heuristic)
+# ("kx", waves, slices, tiles code): the register-stationary kernel; ("sk", waves, blocks/CU, group): stream-K
 RANK_CANDIDATES = {
-    "qkv": [(0, 0, 0), (8, 1, 0), (8, 2, 0), (8, 3, 0), (8, 4, 0), (8, 6, 0), (8, 8, 0), (4, 4, 0), (4, 8, 0)],
-    "o": [(0, 0, 0), (4, 1, 1), (8, 1, 1), (2, 1, 1), (4, 2, 1), (2, 2, 1), (8, 1, 2), (4, 1, 2)],
-    "gate_up": [(0, 0, 0), (8, 1, 0), (4, 1, 0), (2, 1, 0), (8, 2, 0), (4, 2, 0)],
-    "down": [(0, 0, 0), (8, 1, 1), (4, 1, 1), (8, 2, 1), (4, 2, 1), (8, 4, 1), (8, 1, 2)],
-    "lm_head": [(0, 0, 0), (8, 1, 2), (4, 1, 2), (8, 1, 1), (4, 1, 4)],
+    "qkv": [(0, 0, 0), (8, 3, 0), (8, 4, 0), (4, 4, 0), ("kx", 0, 0, 0), ("kx", 0, 2, 0), ("kx", 0, 4, 0),
+            ("kx", 8, 3, 0), ("kx", 0, 2, -13), ("sk", 8, 1, 4), ("sk", 4, 1, 8), ("sk", 8, 1, 8)],
+    "o": [(0, 0, 0), (2, 1, 1), (4, 1, 1), (8, 1, 1), ("kx", 0, 0, 0), ("kx", 0, 1, 0), ("kx", 0, 1, -13),
+          ("sk", 4, 1, 4)],
+    "gate_up": [(0, 0, 0), (4, 1, 0), (8, 1, 0), ("kx", 0, 2, 0), ("kx", 8, 2, 0), ("kx", 0, 3, 0),
+                ("sk", 4, 1, 8), ("sk", 8, 1, 8)],
+    "down": [(0, 0, 0), ("sk", 4, 1, 8), (8, 1, 1), (4, 1, 1), (8, 2, 1), ("kx", 0, 0, 0), ("kx", 0, 2, 0),
+             ("kx", 0, 2, -13), ("sk", 8, 1, 8)],
+    "lm_head": [(0, 0, 0), (8, 1, 1), (8, 1, 2), (4, 1, 2)],
 }
 
 
@@ -160,7 +165,7 @@ def main():
             res.append((us, cfg))
             print(json.dumps({"kind": kind, "cfg": cfg, "step_us": round(us, 1)}), flush=True)
         us, cfg = min(res)
-        heur = next(u for u, c in res if c == (0, 0, 0))
+        heur = next((u for u, c in res if c == (0, 0, 0)), float("nan"))
         best[kind] = {"cfg": cfg, "step_us": round(us, 1), "heuristic_step_us": round(heur, 1)}
         set_plan(eng.model, kind, cfg)
     print(json.dumps({"best": best, "final_step_us": round(time_step(eng, a.iters), 1)}), flush=True)

@@ -39,7 +39,7 @@ __device__ __forceinline__ uint4 and_mask(uint4 v, uint32_t m) { return make_uin
 // weight stream (measured: benchmarks/stream_probe.hip, +75% time at 96 blocks), so the
 // activation side must be as thin as the batch allows.
 template <int MB, int NTB, int U, int EPI, int NORM, bool PIPE, int XP>
-__global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
+__device__ __forceinline__ void gemm_block(const GemmParams& p) {
   static_assert(XP == 1 || (MB == 1 && PIPE && U % XP == 0), "activation packing is a decode-kernel mode");
   constexpr int R = 16 / XP;  // real rows per packed load
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -187,6 +187,11 @@ __global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
     }
   }
   gemm_finish<MB, NTB, EPI, NORM, PREF>(p, acc, ssr, smem, m_base, nt0, pre);
+}
+
+template <int MB, int NTB, int U, int EPI, int NORM, bool PIPE, int XP>
+__global__ __launch_bounds__(PIPE ? 512 : 1024) void gemm_kernel(GemmParams p) {
+  gemm_block<MB, NTB, U, EPI, NORM, PIPE, XP>(p);
 }
 
 // ---- AWQ W4A16 ----
@@ -488,6 +493,12 @@ inline Plan plan(int nblk, int mchunks, int ksteps, int MB, int NTB, int force_w
   return {w, s};
 }
 
+// Fused QKV projection + decode attention (qkv_attn.hip): the decode QKV launch of a decode-only step
+// with its attention blocks appended (QaSync). False: a (register group, packing, norm mode) it has no
+// instantiation for, or an attention shape it does not take — the caller launches both kernels.
+bool launch_qkv_attn(int u, int xp, int norm, GemmParams p, int nprod, int waves, size_t lds_gemm,
+                     const GemmArgs& g, hipStream_t st);
+
 // decode launch with a runtime-chosen register group size (one-tile blocks; see launch_one)
 template <int MB, int NTB, int U, int EPI, int NORM, int XP>
 static void launch_dec_u(int u, dim3 grid, dim3 block, size_t lds, hipStream_t st, const GemmParams& p) {
@@ -522,10 +533,13 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
   }
   const size_t lds = red_bytes<MB, NTB>(pl.waves) + ssq_bytes<MB>(pl.waves) + 16;
   dim3 grid(nblk, mchunks, pl.splitk), block(64 * pl.waves);
-  if (p.dbg_ts == nullptr)
-    p.dbg_ts = tl_take(AWQ ? "awq_gemm" : (EPI == EPI_QKV ? "gemm_qkv" : EPI == EPI_SILU ? "gemm_gate_up"
-                                            : EPI == EPI_F32 ? "gemm_f32" : "gemm"), (int)(grid.x * grid.y * grid.z));
+  auto take_tl = [&] {
+    if (p.dbg_ts == nullptr)
+      p.dbg_ts = tl_take(AWQ ? "awq_gemm" : (EPI == EPI_QKV ? "gemm_qkv" : EPI == EPI_SILU ? "gemm_gate_up"
+                                              : EPI == EPI_F32 ? "gemm_f32" : "gemm"), (int)(grid.x * grid.y * grid.z));
+  };
   if constexpr (AWQ) {
+    take_tl();
     // chunks of 3 k-quads when every wave's range is exactly 3 (K = 1536 over 4 waves): a chunk of
     // 4 would re-load a clamped fourth k-quad (weights, 4 activation rows, 8 scale / zero words)
     const int KQ = g.K / 128;
@@ -568,10 +582,18 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
       if (u != 6 && u != 8 && u != 10 && u != 12) u = 8;
       if (u % xp) u = 8;
     }
+    if constexpr (EPI == EPI_QKV && NTB == 1) {  // decode-only step: its attention in this launch
+      if (g.fa != nullptr && grid.y == 1 && grid.z == 1 && launch_qkv_attn(u, xp, NORM, p, (int)grid.x, pl.waves, lds, g, st)) {
+        *g.fa_done = true;
+        return;
+      }
+    }
+    take_tl();
     if (xp == 4) launch_dec_u<MB, NTB, U, EPI, NORM, 4>(u, grid, block, lds, st, p);
     else if (xp == 2) launch_dec_u<MB, NTB, U, EPI, NORM, 2>(u, grid, block, lds, st, p);
     else launch_dec_u<MB, NTB, U, EPI, NORM, 1>(u, grid, block, lds, st, p);
   } else {
+    take_tl();
     hipLaunchKernelGGL((gemm_kernel<MB, NTB, MB == 4 ? 2 : 4, EPI, NORM, false, 1>), grid, block, lds, st, p);
   }
 }

@@ -45,6 +45,7 @@ struct GemmParams {
   bf16_t* hg; const bf16_t* hg_gamma; float* ssp_out; const float* ssp_in; int ssn;
   unsigned long long* dbg_ts;  // per-block [start, end] realtime stamps (profiling), or null
   ArFused ar;                  // world 0: no fused all-reduce
+  uint4* qa_gran;              // EPI_QKV: also write q / K / V as tagged granules (qkv_attn.hip), or null
 };
 
 // (column-tile block, K slice, slices) of this block: the grid decomposition of gemm_finish's hand-off
@@ -439,14 +440,15 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[N
     const bool upper = nsub >= 8;      // partner half (d + 64)
     uint2 w;
     float4 cs, sn;
-    int slot;
+    int slot, pos;
     if constexpr (have) {
       w = p.bias ? e.b0 : make_uint2(0, 0);  // (epi_pre_a read the weights when there is no bias)
-      cs = e.cs; sn = e.sn; slot = e.slot;
+      cs = e.cs; sn = e.sn; slot = e.slot; pos = e.pos;
     } else {
       const int mm = m < p.M ? m : p.M - 1;
       w = p.bias ? *reinterpret_cast<const uint2*>(p.bias + qkv_col(nt0, nsub)) : make_uint2(0, 0);
-      const float* cp = p.cos_sin + (size_t)p.positions[mm] * 128;
+      pos = p.positions[mm];
+      const float* cp = p.cos_sin + (size_t)pos * 128;
       cs = *reinterpret_cast<const float4*>(cp + d);
       sn = *reinterpret_cast<const float4*>(cp + 64 + d);
       slot = p.slots[mm];
@@ -467,14 +469,20 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, const f32x4 (&v)[N
     pk.x = pack_bf2(x[0], x[1]);
     pk.y = pack_bf2(x[2], x[3]);
     const int dcol = (upper ? 64 : 0) + d;  // column inside the head
+    bf16_t* dst = nullptr;
     if (head < p.hq) {
-      *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + head * 128 + dcol) = pk;
+      dst = reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + head * 128 + dcol;
     } else if (slot >= 0) {
       const bool is_k = head < p.hq + p.hkv;
       const int kh = is_k ? head - p.hq : head - p.hq - p.hkv;
-      bf16_t* dst = (is_k ? p.k_cache : p.v_cache) +
-                    (((size_t)(slot / p.bs) * p.hkv + kh) * p.bs + (slot % p.bs)) * 128 + dcol;
-      *reinterpret_cast<uint2*>(dst) = pk;
+      dst = (is_k ? p.k_cache : p.v_cache) + (((size_t)(slot / p.bs) * p.hkv + kh) * p.bs + (slot % p.bs)) * 128 + dcol;
+    }
+    if (dst != nullptr) *reinterpret_cast<uint2*>(dst) = pk;
+    if (p.qa_gran != nullptr && slot >= 0) {  // read in this launch by the fused attention blocks
+      const uint32_t pair = (uint32_t)m * (uint32_t)(p.N >> 1) + (uint32_t)((head * 128 + dcol) >> 1);
+      const uint32_t tag = (uint32_t)pos + 1u;
+      st_sc1_x4(reinterpret_cast<float*>(p.qa_gran), pair * 8u,
+                __builtin_bit_cast(f32x4, make_uint4(pk.x, tag, pk.y, tag)));
     }
   } else {
 #pragma unroll

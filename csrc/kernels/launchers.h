@@ -7,6 +7,8 @@
 
 namespace vgate {
 
+struct AttnArgs;
+
 struct GemmArgs {
   const uint16_t* x;  // [M, K] bf16, row stride lda (rows gathered through row_idx if set)
   int lda;
@@ -68,6 +70,12 @@ struct GemmArgs {
   uint32_t* ar_err = nullptr;
   int ar_rank = 0;
   int ar_world = 0;
+  // decode-only step, EPI_QKV: the step's decode attention rides in the same launch when the decode
+  // tile kernel takes the shape (qkv_attn.hip; fa_done set), else the caller launches it after
+  const AttnArgs* fa = nullptr;
+  void* fa_gran = nullptr;      // zeroed granule buffer (QaSync::gran), fa_gran_bytes long
+  size_t fa_gran_bytes = 0;
+  bool* fa_done = nullptr;
 };
 void launch_gemm(const GemmArgs& g, hipStream_t st);
 // stream-K decode GEMM (gemm_streamk.hip): M <= 16 dense rows, one equal share of the packed weight
@@ -195,6 +203,16 @@ struct AttnArgs {
   // sticky kernel-fault word (bit 1: a flash K-split waiter gave up), copied to the host each step by
   // launch_ids_to_host; null = none
   uint32_t* fault = nullptr;
+};
+// In-launch hand-off of the fused QKV projection + decode attention (qkv_attn.hip): the nprod GEMM
+// blocks write q and the new K / V rows also as data-tagged granules {bf16 pair, position + 1} into
+// `gran` ([M][n2 = N / 2] x 8 B, zeroed once: ops.qa_granules); the attention blocks poll them and
+// clear what they read. fault: the sticky fault word (bit 32: a poll gave up).
+struct QaSync {
+  void* gran;
+  int n2;
+  int nprod;
+  uint32_t* fault;
 };
 void launch_attn_decode(const AttnArgs& a, hipStream_t st);
 void launch_attn_prefill(const AttnArgs& a, hipStream_t st);

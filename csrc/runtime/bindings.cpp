@@ -43,6 +43,11 @@ T* opt_ptr(const c10::optional<Tensor>& t, c10::ScalarType dt, const char* name)
   return reinterpret_cast<T*>(t->data_ptr());
 }
 
+vgate::AttnArgs attn_common(const Tensor& q, int64_t q_stride, const Tensor& k_cache,
+                            const Tensor& v_cache, const Tensor& block_tables,
+                            const Tensor& context_lens, Tensor& out, int64_t Hq, int64_t Hkv,
+                            double scale);
+
 // out = epilogue(prologue(x) @ W^T); W fragment-packed [N/16, K/32, 64, 8] bf16, or AWQ
 // int4 [N/16, K/128, 64, 4] int32 with scales/zeros. ws = int32 workspace: [0, 65536)
 // split-K tickets (zeroed once, self-resetting), the rest fp32 slabs.
@@ -59,7 +64,11 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
           const c10::optional<Tensor>& hg_gamma, const c10::optional<Tensor>& ssp_out,
           const c10::optional<Tensor>& ssp_in, const c10::optional<Tensor>& sk_ws,
           const c10::optional<Tensor>& fault, const std::vector<int64_t>& ar_bases, int64_t ar_rank,
-          int64_t ar_fused_off) {
+          int64_t ar_fused_off, const c10::optional<Tensor>& fa_block_tables,
+          const c10::optional<Tensor>& fa_context_lens, const c10::optional<Tensor>& fa_query_start,
+          const c10::optional<Tensor>& fa_out, const c10::optional<Tensor>& fa_part_o,
+          const c10::optional<Tensor>& fa_part_ml, const c10::optional<Tensor>& fa_tickets,
+          const c10::optional<Tensor>& fa_sync, int64_t fa_part_size, double fa_scale) {
   CHECK_DEV(x); CHECK_DEV(wp); CHECK_DEV(out);
   CHECK_DT(x, torch::kBFloat16);
   CHECK_LASTDIM(x); CHECK_LASTDIM(out);
@@ -170,9 +179,46 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
     g.ar_rank = (int)ar_rank;
     g.ar_world = world;
   }
+  // decode-only step: the step's decode attention (q = this projection's output) in the same launch
+  // when the decode tile kernel takes it (qkv_attn.hip), else launched right after the projection
+  vgate::AttnArgs fa{};
+  bool fa_done = false;
+  const bool fused_attn = fa_out.has_value() && fa_out->defined();
+  if (fused_attn) {
+    TORCH_CHECK(epi == 3 && M <= 16, "fused attention: the decode QKV projection (epi 3, M <= 16)");
+    TORCH_CHECK(fa_block_tables.has_value() && fa_context_lens.has_value() && fa_query_start.has_value() &&
+                    fa_part_o.has_value() && fa_part_ml.has_value() && fa_tickets.has_value() && fa_sync.has_value(),
+                "fused attention: block_tables, context_lens, query_start, part_o, part_ml, tickets, sync");
+    Tensor fo = *fa_out;
+    fa = attn_common(out, out.stride(0), *k_cache, *v_cache, *fa_block_tables, *fa_context_lens, fo, hq, hkv,
+                     fa_scale);
+    TORCH_CHECK(fa_part_size % 32 == 0 && fa_part_size <= 1024, "fused attention: part_size");
+    CHECK_DT(*fa_part_o, torch::kFloat32); CHECK_DT(*fa_part_ml, torch::kFloat32);
+    CHECK_DT(*fa_query_start, torch::kInt32);
+    TORCH_CHECK(fa_query_start->numel() >= fa.S + 1, "fused attention: query_start needs S+1 entries");
+    fa.query_start = reinterpret_cast<const int32_t*>(fa_query_start->data_ptr());
+    fa.num_parts = (int)fa_part_o->size(2);
+    fa.part_size = (int)fa_part_size;
+    TORCH_CHECK((int64_t)fa.num_parts * fa_part_size >= fa_block_tables->size(1) * 16,
+                "fused attention: partitions do not cover max context");
+    TORCH_CHECK(fa_part_o->size(0) >= fa.S && fa_part_o->size(1) == hq, "fused attention: part_o shape");
+    fa.part_o = reinterpret_cast<float*>(fa_part_o->data_ptr());
+    fa.part_ml = reinterpret_cast<float*>(fa_part_ml->data_ptr());
+    CHECK_DEV(*fa_tickets); CHECK_DT(*fa_tickets, torch::kInt32);
+    TORCH_CHECK(fa_tickets->numel() >= (int64_t)fa.S * hkv, "fused attention: tickets need S*Hkv zeroed int32");
+    fa.tickets = reinterpret_cast<uint32_t*>(fa_tickets->data_ptr());
+    CHECK_DEV(*fa_sync); CHECK_DT(*fa_sync, torch::kInt32);
+    TORCH_CHECK(fa_sync->is_contiguous(), "fused attention: granule buffer contiguous");
+    fa.fault = g.fault;
+    g.fa = &fa;
+    g.fa_gran = fa_sync->data_ptr();
+    g.fa_gran_bytes = (size_t)fa_sync->numel() * 4;
+    g.fa_done = &fa_done;
+  }
   c10::DeviceGuard guard(x.device());
   if (awq) vgate::launch_awq_gemm(g, cur_stream());
   else vgate::launch_gemm(g, cur_stream());
+  if (fused_attn && !fa_done) vgate::launch_attention(fa, fa.S, cur_stream());
 }
 
 // AWQ int4 packed weight -> bf16 packed weight (same fragment order / row permutation)
@@ -579,7 +625,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("awq_szp") = py::none(), py::arg("hg_out") = py::none(), py::arg("hg_gamma") = py::none(),
         py::arg("ssp_out") = py::none(), py::arg("ssp_in") = py::none(), py::arg("sk_ws") = py::none(),
         py::arg("fault") = py::none(), py::arg("ar_bases") = std::vector<int64_t>{}, py::arg("ar_rank") = 0,
-        py::arg("ar_fused_off") = 0);
+        py::arg("ar_fused_off") = 0, py::arg("fa_block_tables") = py::none(), py::arg("fa_context_lens") = py::none(),
+        py::arg("fa_query_start") = py::none(), py::arg("fa_out") = py::none(), py::arg("fa_part_o") = py::none(),
+        py::arg("fa_part_ml") = py::none(), py::arg("fa_tickets") = py::none(), py::arg("fa_sync") = py::none(),
+        py::arg("fa_part_size") = 512, py::arg("fa_scale") = 1.0);
   m.def("attention", &attention, "unified paged attention: decode (partitions merged in-launch) + varlen prefill tiles",
         py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),

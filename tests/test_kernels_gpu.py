@@ -477,6 +477,73 @@ def test_gemm_qkv_rope_kv_epilogue(hq, hkv):
     assert torch.equal(lin.dense_weight(), w)
 
 
+@pytest.mark.parametrize("hq,hkv", [(12, 2), (8, 1), (32, 8)])
+@pytest.mark.parametrize("S", [1, 5, 8, 16])
+def test_qkv_attention_fused(hq, hkv, S):
+    """Decode-only step: the QKV projection with the decode attention in its launch (qkv_attn.hip)
+    == the two-launch path (q and the K / V cache bit-exact, attention within bf16 rounding of the
+    fp32 reference), contexts of 1 .. 1000 tokens (two partitions, several chunks per wave, the new
+    token first / last in its cache block), and a second launch on reset sync words."""
+    torch.manual_seed(40 + S + hq)
+    H, D, BS, part, maxlen = 1536, 128, 16, 512, 1024
+    nbs = maxlen // BS
+    N = (hq + 2 * hkv) * D
+    ctxs = [100, 1, 33, 257, 700, 512, 513, 31, 64, 65, 1000, 2, 128, 300, 17, 90][:S]
+    nblocks = S * nbs + 3
+    bt = torch.randperm(nblocks)[: S * nbs].view(S, nbs).int().to(DEV)
+    kc = (torch.randn(nblocks, hkv, BS, D, device=DEV) * 0.5).bfloat16()
+    vc = torch.randn(nblocks, hkv, BS, D, device=DEV).bfloat16()
+    cl = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
+    pos = cl - 1
+    slots = (bt[torch.arange(S, device=DEV), (pos // BS).long()] * BS + pos % BS).int()
+    qs = torch.arange(S + 1, dtype=torch.int32, device=DEV)
+    x = torch.randn(S, H, device=DEV).bfloat16()
+    gamma = (torch.rand(H, device=DEV) + 0.5).bfloat16()
+    w = (torch.randn(N, H, device=DEV) / math.sqrt(H)).bfloat16()
+    b = (torch.randn(N, device=DEV) * 0.1).bfloat16()
+    lin = ops.Linear(w, bias=b, layout="qkv")
+    assert lin.fold_norm(gamma)
+    cs = ref.rope_cos_sin(2048, D, 1e6, device=DEV)
+    P = maxlen // part
+    part_o = torch.empty(S, hq, P, D, dtype=torch.float32, device=DEV)
+    part_ml = torch.empty(S, hq, P, 2, dtype=torch.float32, device=DEV)
+    C = ops.native()
+
+    def run(fuse, kcx, vcx):
+        ops.FUSE_QKV_ATTN = fuse
+        q = torch.empty(S, hq * D, dtype=torch.bfloat16, device=DEV)
+        o = torch.zeros(S, hq * D, dtype=torch.bfloat16, device=DEV)
+        ops.linear(x, lin, out=q, norm=(gamma, 1e-6),
+                   qkv=dict(positions=pos, slots=slots, cos_sin=cs, k_cache=kcx, v_cache=vcx, hq=hq, hkv=hkv),
+                   attn=dict(block_tables=bt, context_lens=cl, query_start=qs, out=o, part_o=part_o,
+                             part_ml=part_ml, part_size=part, scale=D ** -0.5))
+        return q, o
+
+    fault0 = int(ops.fault_word(DEV)[0])
+    try:
+        kc1, vc1 = kc.clone(), vc.clone()
+        buf = torch.zeros(1 << 16, dtype=torch.int64, device=DEV)
+        C.timeline_start(buf)
+        q1, o1 = run(True, kc1, vc1)
+        torch.cuda.synchronize()
+        C.timeline_stop()
+        names = [e[0] for e in C.timeline_entries()]
+        q1b, o1b = run(True, kc1, vc1)
+        kc2, vc2 = kc.clone(), vc.clone()
+        q2, o2 = run(False, kc2, vc2)
+        torch.cuda.synchronize()
+    finally:
+        ops.FUSE_QKV_ATTN = True
+    assert (int(ops.fault_word(DEV)[0]) & ~fault0 & 32) == 0, "a fused attention wait gave up"
+    assert torch.equal(q1, q2) and torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
+    assert torch.equal(q1b, q1) and torch.equal(o1b, o1)
+    ro = ref.attention_ref(q2.view(S, hq, D), kc2, vc2, bt, cl, qs, hq, hkv, D ** -0.5).view(S, hq * D)
+    assert _rel_err(o2, ro) < 1e-2
+    assert _rel_err(o1, ro) < 1e-2
+    if (hq, hkv) == (12, 2):  # the Qwen2.5-1.5B decode projection takes the fused launch
+        assert "qkv_attn" in names, names
+
+
 def test_awq_norm_splitk():
     torch.manual_seed(13)
     M, N, K, g = 8, 1536, 1536, 128

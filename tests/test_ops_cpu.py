@@ -162,4 +162,38 @@ def test_decode_plans_apply_tile_and_streamk_entries():
     assert L.o.dec_sk is None and L.o.dec_waves == 0
     for key, val in decode_plans.PLANS.items():
         assert len(key) == 4 and key[2] in ("qkv", "silu", "plain") and key[3] in ("dense", "awq")
-        assert (val[0] == "sk" and len(val) == 4) or (len(val) == 3 and all(isinstance(v, int) for v in val))
+        assert (val[0] in ("sk", "kx") and len(val) == 4) or (len(val) == 3 and all(isinstance(v, int) for v in val))
+    # a register-stationary entry selects decode path 4 with its (waves, slices, tiles code)
+    kxl = lin(17920, 1536, "silu")
+    kxl.dec_path = 0
+    decode_plans.apply(SimpleNamespace(layers=[SimpleNamespace(qkv=lin(1, 1), o=lin(1, 1), gate_up=kxl, down=lin(1, 1))],
+                                       lm_head=lin(1, 1)))
+    assert kxl.dec_path == 4 and (kxl.dec_waves, kxl.dec_splitk, kxl.dec_ntb) == (0, 0, 0)
+
+
+def test_linear_qkv_with_attention_cpu():
+    """ops.linear(qkv=..., attn=...) on the CPU: the projection, RoPE + KV write, then the decode
+    attention over its q (the GPU runs both in one launch, csrc/kernels/qkv_attn.hip)."""
+    torch.manual_seed(3)
+    S, H, D, BS, hq, hkv = 3, 256, 128, 16, 4, 2
+    N = (hq + 2 * hkv) * D
+    lin = ops.Linear((torch.randn(N, H) / H ** 0.5).bfloat16(), layout="qkv")
+    x = torch.randn(S, H).bfloat16()
+    bt = torch.arange(S * 4, dtype=torch.int32).view(S, 4)
+    kc = torch.randn(S * 4, hkv, BS, D).bfloat16()
+    vc = torch.randn(S * 4, hkv, BS, D).bfloat16()
+    cl = torch.tensor([5, 17, 40], dtype=torch.int32)
+    pos = cl - 1
+    slots = (bt[torch.arange(S), (pos // BS).long()] * BS + pos % BS).int()
+    qs = torch.arange(S + 1, dtype=torch.int32)
+    cs = ref.rope_cos_sin(64, D, 1e4)
+    qkv = dict(positions=pos, slots=slots, cos_sin=cs, k_cache=kc, v_cache=vc, hq=hq, hkv=hkv)
+    o = torch.zeros(S, hq * D).bfloat16()
+    part_o = torch.empty(S, hq, 1, D)
+    part_ml = torch.empty(S, hq, 1, 2)
+    q = ops.linear(x, lin, qkv=qkv, attn=dict(block_tables=bt, context_lens=cl, query_start=qs, out=o,
+                                              part_o=part_o, part_ml=part_ml, part_size=64, scale=D ** -0.5))
+    ro = ref.attention_ref(q.view(S, hq, D), kc, vc, bt, cl, qs, hq, hkv, D ** -0.5).view(S, hq * D)
+    assert torch.allclose(o.float(), ro.float(), atol=2e-2, rtol=2e-2)
+    # the new token's K row was written before the attention read it
+    assert torch.count_nonzero(o.float()) > 0

@@ -18,17 +18,14 @@ profiles/r4_streamk_probe.log).
 from __future__ import annotations
 
 PLANS: dict[tuple[int, int, str, str], tuple] = {
-    # Llama-3-70B TP = 8, one rank, batch 8, ctx 128 (profiles/r3_tp8_rank_sweep.log):
-    # per-rank step 5027 -> 4859 us with the round-3 five applied
-    (1280, 8192, "qkv", "dense"): (8, 3, 0),     # 80 tiles x 256 k-steps: 240 blocks (heuristic 8 x 2: +33 us)
-    (8192, 1024, "plain", "dense"): (2, 1, 1),   # o_proj
-    (7168, 8192, "silu", "dense"): (4, 1, 0),    # gate_up: 448 one-tile blocks at 4 waves (heuristic 8: +118 us)
-    # down_proj on stream-K, 4 waves, one block per CU (r4 probe: 12.8 vs 13.5 us per launch; round 3: (8, 1, 2)).
-    # NOTE: a rank with the fused row-parallel all-reduce (the TP default) runs its row-parallel GEMMs
-    # on the tile kernels with the all-reduce epilogue, so this entry is unused there (measured with
-    # collectives stubbed, benchmarks/tp_rank_bench.py); a declined stream-K launch falls back on the
-    # launcher's heuristic, not on these fields (csrc/kernels/gemm.hip launch_gemm)
-    (8192, 3584, "plain", "dense"): ("sk", 4, 1, 8),
+    # Llama-3-70B TP = 8, one rank, batch 8, ctx 128: round-5 in-context sweep with the register-stationary
+    # and stream-K candidates (profiles/r5_tp8_rank_sweep.log; round 3: profiles/r3_tp8_rank_sweep.log)
+    (1280, 8192, "qkv", "dense"): ("kx", 8, 3, 0),  # 80 tiles x 3 K slices, 8 waves (tile kernel 8 x 3: +56 us)
+    (8192, 1024, "plain", "dense"): ("kx", 0, 1, 0),  # o_proj: 512 one-tile blocks (tile kernel 2 x 1: +13 us)
+    (7168, 8192, "silu", "dense"): (4, 1, 0),    # gate_up: 448 one-tile blocks at 4 waves (heuristic 8: +67 us)
+    # down_proj (8192, 3584): the heuristic tile plan (stream-K 4 x 1 x 8, the round-4 entry: +94 us since the
+    # round-5 wait fixes). A rank with the fused row-parallel all-reduce (the TP default) runs o / down on
+    # the tile kernels with the all-reduce epilogue whatever the entry says (vgate/ops linear: path 0 with ar)
     (16032, 8192, "plain", "dense"): (8, 1, 1),  # LM head shard
     # Llama-3-8B, batch 8 (r4 probe, profiles/r4_streamk_probe.log): qkv on stream-K (13.6 vs 15.1 us per
     # launch); gate_up and down_proj on 4-wave tile blocks (39.0 vs 41.3, 21.1 vs 21.9 us)

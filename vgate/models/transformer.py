@@ -231,16 +231,23 @@ class DecoderModel:
         def takes(lin) -> bool:  # a consumer of the hand-off
             return hand and (awq or (lin.norm_gamma is not None and not lin.dec_sk))
 
+        # decode-only steps (T <= S: no prefill tiles, StepMeta.tile_cap): the decode attention rides in
+        # the QKV projection's launch (ops.linear attn=, csrc/kernels/qkv_attn.hip)
+        fuse_attn = T <= S and T <= 16
         for li, L in enumerate(self.layers):
             kc, vc = kv_caches[li]
             qkv_args = dict(positions=sv.positions, slots=sv.slots, cos_sin=self.cos_sin, k_cache=kc, v_cache=vc,
                             hq=sh.hq, hkv=sh.hkv)
+            fa = dict(block_tables=sv.block_tables, context_lens=sv.context_lens, query_start=sv.query_start,
+                      out=attn, part_o=part_o, part_ml=part_ml, part_size=part_size,
+                      scale=self.scale) if fuse_attn else None
             if li > 0 and takes(L.qkv):
-                ops.linear(hg if awq else resid, L.qkv, out=q, prenorm=(ssp, eps), qkv=qkv_args)
+                ops.linear(hg if awq else resid, L.qkv, out=q, prenorm=(ssp, eps), qkv=qkv_args, attn=fa)
             else:
-                ops.linear(resid, L.qkv, out=q, norm=(L.in_norm, eps), qkv=qkv_args)
-            ops.attention(q, sh.hq * D, kc, vc, sv.block_tables, sv.context_lens, sv.query_start, sv.tile_seq,
-                          sv.tile_q0, attn, part_o, part_ml, sh.hq, sh.hkv, part_size, self.scale)
+                ops.linear(resid, L.qkv, out=q, norm=(L.in_norm, eps), qkv=qkv_args, attn=fa)
+            if fa is None:
+                ops.attention(q, sh.hq * D, kc, vc, sv.block_tables, sv.context_lens, sv.query_start, sv.tile_seq,
+                              sv.tile_q0, attn, part_o, part_ml, sh.hq, sh.hkv, part_size, self.scale)
             gu = takes(L.gate_up)
             self._row_parallel(attn, L.o, resid, first, norm_out=(hg, ssp, L.post_norm) if gu else None)
             if gu:

@@ -277,8 +277,13 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
            residual: torch.Tensor | None = None, out_f32: bool = False, waves: int = 0, splitk: int = 0,
            norm: tuple | None = None, row_idx: torch.Tensor | None = None, qkv: dict | None = None,
            path: int = 0, norm_out: tuple | None = None, prenorm: tuple | None = None,
-           ar=None) -> torch.Tensor:
+           ar=None, attn: dict | None = None) -> torch.Tensor:
     """out = epilogue(prologue(x) @ W^T).
+
+    attn (with qkv, decode-only steps): dict(block_tables, context_lens, query_start, out, part_o,
+    part_ml, part_size, scale) — the step's decode attention over q = this projection's output, run
+    in the projection's launch when the decode kernel takes it (csrc/kernels/qkv_attn.hip), else
+    launched right after it; returns q as without it.
 
     ar (GPU, <= 16 rows, bf16 epilogue): a :class:`vgate.parallel.custom_allreduce.CustomAllReduce`;
     the TP row-parallel GEMM then all-reduces in its epilogue: out = bf16(sum over ranks of
@@ -314,6 +319,8 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
             ref.rope_kv_ref(y, qkv["positions"], qkv["slots"], qkv["cos_sin"], qkv["k_cache"], qkv["v_cache"],
                             qkv["hq"], qkv["hkv"], 128)
             out.copy_(y[:, :ncols])
+            if attn is not None:
+                _attn_after(out, qkv, attn)
         else:
             out.copy_(ref.linear_ref(xx, wd, lin.bias, residual, out_f32))
         return out
@@ -365,8 +372,48 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
         if M > 16 or epi != 0:
             raise ValueError("fused all-reduce: decode rows (<= 16) and the bf16 epilogue only")
         kw.update(ar_bases=ar.bases, ar_rank=ar.rank, ar_fused_off=ar.fused_off)
+    if attn is not None:
+        if qkv is None or M > 16:
+            raise ValueError("fused attention: the decode QKV projection (qkv epilogue, <= 16 rows)")
+        if not FUSE_QKV_ATTN:
+            C.gemm(x, lin.wp, lin.N, lin.K, out, epi, **kw)
+            _attn_after(out, qkv, attn)
+            return out
+        kw.update(fa_block_tables=attn["block_tables"], fa_context_lens=attn["context_lens"],
+                  fa_query_start=attn["query_start"], fa_out=attn["out"], fa_part_o=attn["part_o"],
+                  fa_part_ml=attn["part_ml"], fa_tickets=attn_tickets(x.device), fa_sync=qa_sync(x.device),
+                  fa_part_size=int(attn["part_size"]), fa_scale=float(attn["scale"]))
     C.gemm(x, lin.wp, lin.N, lin.K, out, epi, **kw)
     return out
+
+
+# decode-only steps: the decode attention rides in the QKV projection's launch (qkv_attn.hip); tests
+# turn it off to compare against the two-launch path
+FUSE_QKV_ATTN = True
+_QA_SYNC: dict = {}
+
+
+def qa_sync(device) -> torch.Tensor:
+    """Zeroed granule buffer of the fused QKV + attention launch (QaSync: 16 rows x N/2 x 8 B, N <= 32768;
+    the consumers clear what they read)."""
+    key = str(device)
+    t = _QA_SYNC.get(key)
+    if t is None:
+        t = _QA_SYNC[key] = torch.zeros(1 << 20, dtype=torch.int32, device=device)
+    return t
+
+
+def _attn_after(q, qkv, attn):
+    """The two-launch form of ``linear(..., attn=...)``: decode attention over the projection's q."""
+    if not _gpu(q):
+        attention_decode(q, q.stride(0), qkv["k_cache"], qkv["v_cache"], attn["block_tables"], attn["context_lens"],
+                         attn["out"], attn["part_o"], attn["part_ml"], qkv["hq"], qkv["hkv"], int(attn["part_size"]),
+                         float(attn["scale"]), query_start=attn["query_start"])
+        return
+    e = torch.empty(0, dtype=torch.int32, device=q.device)
+    attention(q, q.stride(0), qkv["k_cache"], qkv["v_cache"], attn["block_tables"], attn["context_lens"],
+              attn["query_start"], e, e, attn["out"], attn["part_o"], attn["part_ml"], qkv["hq"], qkv["hkv"],
+              int(attn["part_size"]), float(attn["scale"]))
 
 
 # AWQ steps of 16 < M <= 64 rows (mixed prefill + decode) run the int4 medium kernel; longer ones
