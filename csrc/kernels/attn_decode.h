@@ -280,6 +280,7 @@ __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, in
         ok = qa_get8(*qs, vp, tag, vn) && ok;
       }
       const bool all = __all(ok);
+      if (all && with_q) ATTN_STAMP(6);  // profiling: the query granules are this step's
       if (all || ++spins > (1 << 20)) {  // bounded: the step fails loudly (fault word), never hangs
         if (!all && lane == 0 && qs->fault != nullptr) atomicOr(qs->fault, 32u);
         if (with_q) {
@@ -334,7 +335,16 @@ __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, in
       issue(ka, va, 0);
       poll(true, wid == cnew, ka, va);
       consume(ka, va, 0);
-    } else if (myn > 1) {
+    } else if (myn == 2) {
+      // both chunks in flight before the poll (contexts up to 64 * nw tokens)
+      uint4 ka[8], va[8], kb[8], vb[8];
+      issue(ka, va, 0);
+      issue(kb, vb, 1);
+      if (wid + nw == cnew) poll(true, true, kb, vb);
+      else poll(true, wid == cnew, ka, va);
+      consume(ka, va, 0);
+      consume(kb, vb, 1);
+    } else if (myn > 2) {
       // the new token sits in the context's last chunk: a wave that owns it runs its other chunks
       // through the ping-pong loop and that one after it (the patch's registers stay out of the loop)
       const bool last_new = wid + (myn - 1) * nw == cnew;
@@ -526,6 +536,38 @@ __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, in
     pk.y = pack_bf2(r[2] * iv, r[3] * iv);
     out_store8<SC1>(a.out, (size_t)qbeg * a.out_stride + (size_t)hh * D_ + dd, pk);
   }
+}
+
+// Host side of the fused QKV projection + decode attention launch (qkv_attn.hip, gemm_kx.h): the
+// attention blocks' arguments and the launch's LDS for gx x slices GEMM blocks of `waves` waves;
+// false when the step or shape is not one it takes (the caller launches the two kernels).
+static inline bool qa_setup(GemmParams& p, const GemmArgs& g, int gx, int slices, int waves, size_t lds_gemm,
+                            AttnArgs& a, QaSync& q, size_t& lds) {
+  if (g.fa == nullptr || g.fa_gran == nullptr || g.fa_done == nullptr) return false;
+  if ((size_t)g.M * (size_t)(g.N / 2) * 8 > g.fa_gran_bytes) return false;
+  a = *g.fa;
+  const int G = a.Hq / a.Hkv;
+  // the decode block's merge: G query columns x 16 threads; partitions merged in-launch (tickets)
+  if (waves < 1 || waves > 8 || G * 16 > 64 * waves || a.tickets == nullptr || a.num_tiles > 0) return false;
+  if (a.S * a.num_parts * a.Hkv <= 0) return false;
+  lds = std::max(lds_gemm, (size_t)attn_lds_bytes(waves));
+  if (lds > 160 * 1024) return false;
+  q = QaSync{g.fa_gran, g.N / 2, gx * slices, g.fault};
+  p.qa_gran = reinterpret_cast<uint4*>(g.fa_gran);
+  p.vgx = gx;
+  a.tl = nullptr;
+  return true;
+}
+
+template <typename K>
+static void qa_launch(K kern, const GemmParams& p, const AttnArgs& a, const QaSync& q, int waves, size_t lds,
+                      hipStream_t st) {
+  if (lds > 64 * 1024) {
+    static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    (void)attr;
+  }
+  hipLaunchKernelGGL(kern, dim3(q.nprod + a.S * a.num_parts * a.Hkv), dim3(64 * waves), lds, st, p, a, q);
 }
 
 }  // namespace vgate

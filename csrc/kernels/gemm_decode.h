@@ -48,7 +48,7 @@ __device__ __forceinline__ void gemm_block(const GemmParams& p) {
   TLScope tl_scope(p.dbg_ts);
   const int KT = p.K >> 5;
   const SplitPos sp = split_pos(p);
-  const int nt0 = (int)blockIdx.x * NTB;
+  const int nt0 = blk_x(p) * NTB;
   const int m_base = blockIdx.y * 16 * MB;
   // this block's k-slice, then this wave's contiguous range inside it
   const int s0 = (KT * sp.slice) / sp.nsl, s1 = (KT * (sp.slice + 1)) / sp.nsl;
@@ -496,7 +496,7 @@ inline Plan plan(int nblk, int mchunks, int ksteps, int MB, int NTB, int force_w
 // Fused QKV projection + decode attention (qkv_attn.hip): the decode QKV launch of a decode-only step
 // with its attention blocks appended (QaSync). False: a (register group, packing, norm mode) it has no
 // instantiation for, or an attention shape it does not take — the caller launches both kernels.
-bool launch_qkv_attn(int u, int xp, int norm, GemmParams p, int nprod, int waves, size_t lds_gemm,
+bool launch_qkv_attn(int u, int xp, int norm, GemmParams p, int gx, int slices, int waves, size_t lds_gemm,
                      const GemmArgs& g, hipStream_t st);
 
 // decode launch with a runtime-chosen register group size (one-tile blocks; see launch_one)
@@ -583,7 +583,7 @@ static void launch_one(GemmParams p, const GemmArgs& g, hipStream_t st) {
       if (u % xp) u = 8;
     }
     if constexpr (EPI == EPI_QKV && NTB == 1) {  // decode-only step: its attention in this launch
-      if (g.fa != nullptr && grid.y == 1 && grid.z == 1 && launch_qkv_attn(u, xp, NORM, p, (int)grid.x, pl.waves, lds, g, st)) {
+      if (g.fa != nullptr && grid.y == 1 && launch_qkv_attn(u, xp, NORM, p, (int)grid.x, (int)grid.z, pl.waves, lds, g, st)) {
         *g.fa_done = true;
         return;
       }

@@ -46,14 +46,22 @@ struct GemmParams {
   unsigned long long* dbg_ts;  // per-block [start, end] realtime stamps (profiling), or null
   ArFused ar;                  // world 0: no fused all-reduce
   uint4* qa_gran;              // EPI_QKV: also write q / K / V as tagged granules (qkv_attn.hip), or null
+  int vgx;                     // > 0: a 1-D launch carries the (vgx, 1, slices) grid z-major (qkv_attn.hip)
 };
 
 // (column-tile block, K slice, slices) of this block: the grid decomposition of gemm_finish's hand-off
 struct SplitPos {
   int tile, slice, nsl;
 };
+__device__ __forceinline__ int grid_x(const GemmParams& p) { return p.vgx > 0 ? p.vgx : (int)gridDim.x; }
+__device__ __forceinline__ int blk_x(const GemmParams& p) {
+  return p.vgx > 0 ? (int)blockIdx.x % p.vgx : (int)blockIdx.x;
+}
+__device__ __forceinline__ int blk_z(const GemmParams& p) {
+  return p.vgx > 0 ? (int)blockIdx.x / p.vgx : (int)blockIdx.z;
+}
 __device__ __forceinline__ SplitPos split_pos(const GemmParams& p) {
-  return SplitPos{(int)(blockIdx.y * gridDim.x + blockIdx.x), (int)blockIdx.z, p.splitk};
+  return SplitPos{(int)blockIdx.y * grid_x(p) + blk_x(p), blk_z(p), p.splitk};
 }
 
 __device__ __forceinline__ int row_of(const GemmParams& p, int m) {
@@ -649,7 +657,7 @@ __device__ __forceinline__ void gemm_finish(const GemmParams& p, f32x4 (&acc)[MB
     //    slice's per-row partial sum of squares -> [tile][slice][16*MB] after all slabs
     //    (the row scale is applied to the summed tile: y = rsqrt(sum ss / K + eps) * sum acc)
     const uint32_t slab_off = (uint32_t)(((size_t)tile * p.splitk + sp.slice) * SLOTS * 16);  // bytes
-    float* ssq_all = p.slabs + (size_t)gridDim.x * gridDim.y * p.splitk * SLOTS * 4;
+    float* ssq_all = p.slabs + (size_t)grid_x(p) * gridDim.y * p.splitk * SLOTS * 4;
     if constexpr (NORM) {
       if (threadIdx.x < 16 * MB) {
         float ss = 0.f;

@@ -34,6 +34,7 @@
 // hand-off chain); 3 the producer's hand-off (x = h * gamma, row sums of squares in ssp_in).
 #pragma once
 #include "gemm_decode.h"
+#include "attn_decode.h"
 
 namespace vgate {
 
@@ -79,7 +80,7 @@ __host__ __device__ constexpr int kx_max_threads() {
 }
 
 template <bool Q4, int XP, int KQW, int TMAX, int EPI, int NORM, bool WIDE>
-__global__ __launch_bounds__((kx_max_threads<Q4, XP, KQW, TMAX, NORM>())) void kx_kernel(GemmParams p) {
+__device__ __forceinline__ void kx_block(const GemmParams& p) {
   static_assert(EPI != EPI_QKV || (!WIDE && TMAX == 1), "QKV: one-tile GROUP blocks (prefetched RoPE operands)");
   static_assert(Q4 ? NORM != 2 : NORM != 1, "int4: gamma in registers or the hand-off; bf16: gamma folded into W");
   constexpr bool PRE = !WIDE && TMAX <= 2;  // GROUP blocks of 1-2 tiles: epilogue operands at launch
@@ -93,22 +94,22 @@ __global__ __launch_bounds__((kx_max_threads<Q4, XP, KQW, TMAX, NORM>())) void k
   const int KQ = p.K >> 7, ntiles = p.N >> 4;
   int t0, ntb, s0, s1;
   if constexpr (WIDE) {
-    t0 = (int)(((long long)ntiles * blockIdx.x) / gridDim.x);
-    ntb = (int)(((long long)ntiles * (blockIdx.x + 1)) / gridDim.x) - t0;
+    t0 = (int)(((long long)ntiles * blk_x(p)) / grid_x(p));
+    ntb = (int)(((long long)ntiles * (blk_x(p) + 1)) / grid_x(p)) - t0;
     s0 = 0;
     s1 = KQ;
   } else {
-    t0 = blockIdx.x * TMAX;
+    t0 = blk_x(p) * TMAX;
     ntb = TMAX;
-    s0 = (KQ * (int)blockIdx.z) / p.splitk;
-    s1 = (KQ * ((int)blockIdx.z + 1)) / p.splitk;
+    s0 = (KQ * blk_z(p)) / p.splitk;
+    s1 = (KQ * (blk_z(p) + 1)) / p.splitk;
   }
   const int q0 = s0 + ((s1 - s0) * wid) / nw;
   const int nq = s0 + ((s1 - s0) * (wid + 1)) / nw - q0;  // <= KQW (host-checked), may be 0
   // NORM 3: the row's sums of squares, issued first (consumed after the stream without waiting on it)
   SsPre ssv;
   ssv.n4 = NORM == 3 ? ss_pre_n4(p) : 0;
-  const bool ss_wave = WIDE ? wid < ntb : (wid == 0 && blockIdx.z == 0);  // wave-uniform
+  const bool ss_wave = WIDE ? wid < ntb : (wid == 0 && blk_z(p) == 0);  // wave-uniform
   if constexpr (NORM == 3) {
     if (ss_wave && ssv.n4 > 0) ss_pre_issue(p, ssv, r16, grp);
   }
@@ -297,6 +298,46 @@ __global__ __launch_bounds__((kx_max_threads<Q4, XP, KQW, TMAX, NORM>())) void k
   }
 }
 
+template <bool Q4, int XP, int KQW, int TMAX, int EPI, int NORM, bool WIDE>
+__global__ __launch_bounds__((kx_max_threads<Q4, XP, KQW, TMAX, NORM>())) void kx_kernel(GemmParams p) {
+  kx_block<Q4, XP, KQW, TMAX, EPI, NORM, WIDE>(p);
+}
+
+// The fused QKV projection + decode attention launch on this kernel (design: qkv_attn.hip): GROUP
+// one-tile blocks of <= 8 waves (z-major in the 1-D grid), then the attention blocks
+template <bool Q4, int XP, int KQW, int NORM>
+__global__ __launch_bounds__(512) void kx_qa_kernel(GemmParams p, AttnArgs a, QaSync q) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if ((int)blockIdx.x < q.nprod) {
+    kx_block<Q4, XP, KQW, 1, EPI_QKV, NORM, false>(p);
+    return;
+  }
+  TLScope tl_scope(p.dbg_ts);
+  const int r = (int)blockIdx.x - q.nprod;  // (KV head, partition, sequence), sequence fastest
+  decode_block<false, true>(a, r % a.S, r / (a.S * a.num_parts), (r / a.S) % a.num_parts, smem, &q);
+}
+
+template <bool Q4, int XP, int NORM>
+static bool kx_qa(GemmParams p, const GemmArgs& g, int groups, int S, int kqs, hipStream_t st) {
+  if constexpr (NORM == 0) {
+    return false;
+  } else {
+    const int nw = g.waves > 0 ? g.waves : std::min(8, kqs);
+    const int kqw = (kqs + nw - 1) / nw;
+    if (kqw > 3 || 64 * nw > 512) return false;
+    AttnArgs a;
+    QaSync q;
+    size_t lds;
+    if (!qa_setup(p, g, groups, S, nw, red_bytes<1, 1>(nw) + ssq_bytes<1>(nw) + 16, a, q, lds)) return false;
+    if (p.dbg_ts == nullptr) p.dbg_ts = tl_take(Q4 ? "awq_kx_qa" : "kx_qa", q.nprod + a.S * a.num_parts * a.Hkv);
+    if (kqw == 1) qa_launch(kx_qa_kernel<Q4, XP, 1, NORM>, p, a, q, nw, lds, st);
+    else if (kqw == 2) qa_launch(kx_qa_kernel<Q4, XP, 2, NORM>, p, a, q, nw, lds, st);
+    else qa_launch(kx_qa_kernel<Q4, XP, 3, NORM>, p, a, q, nw, lds, st);
+    *g.fa_done = true;
+    return true;
+  }
+}
+
 static int kx_cus() {
   static const int n = [] {
     int v = 0, dev = 0;
@@ -350,6 +391,9 @@ static bool kx_group(GemmParams p, const GemmArgs& g, hipStream_t st) {
     const size_t need_g = (size_t)groups * 3 * 64 * 16;
     if (TB == 1 && S == 2 && g.sk_pub != nullptr && need_g <= g.sk_bytes) p.gran = reinterpret_cast<uint4*>(g.sk_pub);
     else if (g.slabs == nullptr || need_slab > g.slab_bytes || groups > g.max_counters) return false;
+  }
+  if constexpr (EPI == EPI_QKV && TB == 1) {  // decode-only step: its attention in this launch
+    if (g.fa != nullptr && kx_qa<Q4, XP, NORM>(p, g, groups, S, kqs, st)) return true;
   }
   if (p.dbg_ts == nullptr) p.dbg_ts = tl_take(Q4 ? "awq_kx" : "kx", groups * S);
   const dim3 grid(groups, 1, S);

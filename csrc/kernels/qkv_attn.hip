@@ -40,47 +40,29 @@ __global__ __launch_bounds__(512) void qkv_attn_kernel(GemmParams p, AttnArgs a,
   decode_block<false, true>(a, r % S, r / (S * P), (r / S) % P, smem, &q);
 }
 
-template <int U, int XP, int NORM>
-static void qa_go(const GemmParams& p, const AttnArgs& a, const QaSync& q, int waves, size_t lds, hipStream_t st) {
-  auto kern = qkv_attn_kernel<U, XP, NORM>;
-  if (lds > 64 * 1024) {
-    static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-    (void)attr;
-  }
-  hipLaunchKernelGGL(kern, dim3(q.nprod + a.S * a.num_parts * a.Hkv), dim3(64 * waves), lds, st, p, a, q);
-}
-
 template <int NORM>
 static bool qa_dispatch(int u, int xp, const GemmParams& p, const AttnArgs& a, const QaSync& q, int waves,
                         size_t lds, hipStream_t st) {
-  if (xp == 4 && u == 8) { qa_go<8, 4, NORM>(p, a, q, waves, lds, st); return true; }
-  if (xp == 2 && u == 6) { qa_go<6, 2, NORM>(p, a, q, waves, lds, st); return true; }
-  if (xp == 2 && u == 8) { qa_go<8, 2, NORM>(p, a, q, waves, lds, st); return true; }
-  if (xp == 1 && u == 6) { qa_go<6, 1, NORM>(p, a, q, waves, lds, st); return true; }
-  if (xp == 1 && u == 8) { qa_go<8, 1, NORM>(p, a, q, waves, lds, st); return true; }
+  if (xp == 4 && u == 8) { qa_launch(qkv_attn_kernel<8, 4, NORM>, p, a, q, waves, lds, st); return true; }
+  if (xp == 2 && u == 6) { qa_launch(qkv_attn_kernel<6, 2, NORM>, p, a, q, waves, lds, st); return true; }
+  if (xp == 2 && u == 8) { qa_launch(qkv_attn_kernel<8, 2, NORM>, p, a, q, waves, lds, st); return true; }
+  if (xp == 1 && u == 6) { qa_launch(qkv_attn_kernel<6, 1, NORM>, p, a, q, waves, lds, st); return true; }
+  if (xp == 1 && u == 8) { qa_launch(qkv_attn_kernel<8, 1, NORM>, p, a, q, waves, lds, st); return true; }
   return false;
 }
 
-bool launch_qkv_attn(int u, int xp, int norm, GemmParams p, int nprod, int waves, size_t lds_gemm,
+// gx x slices GEMM blocks (K slices combined in-launch as in the two-launch form: granules / slabs),
+// carried z-major in the 1-D grid (GemmParams::vgx), then the attention blocks
+bool launch_qkv_attn(int u, int xp, int norm, GemmParams p, int gx, int slices, int waves, size_t lds_gemm,
                      const GemmArgs& g, hipStream_t st) {
-  if (g.fa == nullptr || g.fa_gran == nullptr || g.fa_done == nullptr) return false;
-  if ((size_t)g.M * (size_t)(g.N / 2) * 8 > g.fa_gran_bytes) return false;
   if (norm != 2 && norm != 3) return false;  // the decode QKV projections: gamma folded / hand-off
-  AttnArgs a = *g.fa;
-  const int G = a.Hq / a.Hkv;
-  // the decode block's merge: G query columns x 16 threads; partitions merged in-launch (tickets)
-  if (waves < 1 || waves > 8 || G * 16 > 64 * waves || a.tickets == nullptr || a.num_tiles > 0) return false;
-  const int ncons = a.S * a.num_parts * a.Hkv;
-  if (ncons <= 0) return false;
-  const size_t lds = std::max(lds_gemm, (size_t)attn_lds_bytes(waves));
-  if (lds > 160 * 1024) return false;
   const bool inst = (xp == 4 && u == 8) || ((xp == 2 || xp == 1) && (u == 6 || u == 8));
   if (!inst) return false;
-  QaSync q{g.fa_gran, g.N / 2, nprod, g.fault};
-  p.qa_gran = reinterpret_cast<uint4*>(g.fa_gran);
-  a.tl = nullptr;
-  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("qkv_attn", nprod + ncons);
+  AttnArgs a;
+  QaSync q;
+  size_t lds;
+  if (!qa_setup(p, g, gx, slices, waves, lds_gemm, a, q, lds)) return false;
+  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("qkv_attn", q.nprod + a.S * a.num_parts * a.Hkv);
   if (norm == 2) return qa_dispatch<2>(u, xp, p, a, q, waves, lds, st);
   return qa_dispatch<3>(u, xp, p, a, q, waves, lds, st);
 }

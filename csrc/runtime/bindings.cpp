@@ -68,7 +68,8 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
           const c10::optional<Tensor>& fa_context_lens, const c10::optional<Tensor>& fa_query_start,
           const c10::optional<Tensor>& fa_out, const c10::optional<Tensor>& fa_part_o,
           const c10::optional<Tensor>& fa_part_ml, const c10::optional<Tensor>& fa_tickets,
-          const c10::optional<Tensor>& fa_sync, int64_t fa_part_size, double fa_scale) {
+          const c10::optional<Tensor>& fa_sync, int64_t fa_part_size, double fa_scale,
+          const c10::optional<Tensor>& fa_dbg_ts) {
   CHECK_DEV(x); CHECK_DEV(wp); CHECK_DEV(out);
   CHECK_DT(x, torch::kBFloat16);
   CHECK_LASTDIM(x); CHECK_LASTDIM(out);
@@ -210,6 +211,11 @@ void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, 
     CHECK_DEV(*fa_sync); CHECK_DT(*fa_sync, torch::kInt32);
     TORCH_CHECK(fa_sync->is_contiguous(), "fused attention: granule buffer contiguous");
     fa.fault = g.fault;
+    if (fa_dbg_ts.has_value() && fa_dbg_ts->defined()) {  // profiling: attention phase stamps (qa_phases.py)
+      CHECK_DEV(*fa_dbg_ts); CHECK_DT(*fa_dbg_ts, torch::kInt64);
+      TORCH_CHECK(fa_dbg_ts->numel() >= 16, "fused attention: dbg_ts needs 16 int64");
+      fa.dbg_ts = reinterpret_cast<unsigned long long*>(fa_dbg_ts->data_ptr());
+    }
     g.fa = &fa;
     g.fa_gran = fa_sync->data_ptr();
     g.fa_gran_bytes = (size_t)fa_sync->numel() * 4;
@@ -628,7 +634,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("ar_fused_off") = 0, py::arg("fa_block_tables") = py::none(), py::arg("fa_context_lens") = py::none(),
         py::arg("fa_query_start") = py::none(), py::arg("fa_out") = py::none(), py::arg("fa_part_o") = py::none(),
         py::arg("fa_part_ml") = py::none(), py::arg("fa_tickets") = py::none(), py::arg("fa_sync") = py::none(),
-        py::arg("fa_part_size") = 512, py::arg("fa_scale") = 1.0);
+        py::arg("fa_part_size") = 512, py::arg("fa_scale") = 1.0, py::arg("fa_dbg_ts") = py::none());
   m.def("attention", &attention, "unified paged attention: decode (partitions merged in-launch) + varlen prefill tiles",
         py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),

@@ -382,7 +382,7 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
         kw.update(fa_block_tables=attn["block_tables"], fa_context_lens=attn["context_lens"],
                   fa_query_start=attn["query_start"], fa_out=attn["out"], fa_part_o=attn["part_o"],
                   fa_part_ml=attn["part_ml"], fa_tickets=attn_tickets(x.device), fa_sync=qa_sync(x.device),
-                  fa_part_size=int(attn["part_size"]), fa_scale=float(attn["scale"]))
+                  fa_part_size=int(attn["part_size"]), fa_scale=float(attn["scale"]), fa_dbg_ts=attn.get("dbg_ts"))
     C.gemm(x, lin.wp, lin.N, lin.K, out, epi, **kw)
     return out
 

@@ -208,6 +208,7 @@ class LoopbackFused:
             self.own = self.C.ar_alloc(SIGNAL_BYTES + int(self.C.ar_fused_bytes()))
         self.bases = [self.own]
         self.calls = 0
+        self.fused = True  # (CustomAllReduce.fuses reads it: the self-check can turn a real group's off)
 
     fuses = CustomAllReduce.fuses
 
