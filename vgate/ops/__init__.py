@@ -17,6 +17,14 @@ _C = None
 _C_ERR: Exception | None = None
 
 
+def _dev_key(device) -> str:
+    """Key of the per-device buffers below: "cuda" and "cuda:<current>" name the same device."""
+    d = torch.device(device)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return str(d)
+
+
 def native():
     """Return the compiled extension module, building it in-tree if needed."""
     global _C, _C_ERR
@@ -264,7 +272,7 @@ def workspace(device) -> torch.Tensor:
     """Per-device GEMM workspace: 64k split-K tickets (zeroed once) + fp32 slabs (256 MiB on a GPU:
     a K-split prefill GEMM needs slices x M x N x 4 bytes — with 32 MiB the 4-way split of Llama-3-8B
     down_proj at M = 1024 silently fell back to one slice on 64 tiles; 32 MiB on the CPU)."""
-    key = str(device)
+    key = _dev_key(device)
     ws = _WS.get(key)
     if ws is None:
         slab_words = (64 if torch.device(device).type == "cuda" else 8) * 2**20
@@ -283,7 +291,9 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
     attn (with qkv, decode-only steps): dict(block_tables, context_lens, query_start, out, part_o,
     part_ml, part_size, scale) — the step's decode attention over q = this projection's output, run
     in the projection's launch when the decode kernel takes it (csrc/kernels/qkv_attn.hip), else
-    launched right after it; returns q as without it.
+    launched right after it; returns q as without it. With attn["oproj"] = dict(lin, out, residual,
+    ssp_out) and attn["layer"] (TP = 1, bf16) the layer's o_proj joins the launch as a third role
+    when it can; attn["fused"] tells the caller what ran (1: attention, 2: o_proj too).
 
     ar (GPU, <= 16 rows, bf16 epilogue): a :class:`vgate.parallel.custom_allreduce.CustomAllReduce`;
     the TP row-parallel GEMM then all-reduces in its epilogue: out = bf16(sum over ranks of
@@ -375,6 +385,7 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
     if attn is not None:
         if qkv is None or M > 16:
             raise ValueError("fused attention: the decode QKV projection (qkv epilogue, <= 16 rows)")
+        attn["fused"] = 0
         if not FUSE_QKV_ATTN:
             C.gemm(x, lin.wp, lin.N, lin.K, out, epi, **kw)
             _attn_after(out, qkv, attn)
@@ -383,20 +394,39 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
                   fa_query_start=attn["query_start"], fa_out=attn["out"], fa_part_o=attn["part_o"],
                   fa_part_ml=attn["part_ml"], fa_tickets=attn_tickets(x.device), fa_sync=qa_sync(x.device),
                   fa_part_size=int(attn["part_size"]), fa_scale=float(attn["scale"]), fa_dbg_ts=attn.get("dbg_ts"))
+        op = attn.get("oproj")
+        if op is not None and FUSE_OPROJ and op["lin"].kind == "dense":
+            ol = op["lin"]
+            kw.update(o_wp=ol.wp, o_N=ol.N, o_out=op["out"], o_res=op.get("residual"), o_bias=ol.bias,
+                      o_ssp_out=op.get("ssp_out"), step_tag=step_tag(x.device), layer=int(attn.get("layer", 0)))
+        attn["fused"] = int(C.gemm(x, lin.wp, lin.N, lin.K, out, epi, **kw))
+        return out
     C.gemm(x, lin.wp, lin.N, lin.K, out, epi, **kw)
     return out
 
 
-# decode-only steps: the decode attention rides in the QKV projection's launch (qkv_attn.hip); tests
-# turn it off to compare against the two-launch path
+# decode-only steps: the decode attention rides in the QKV projection's launch (qkv_attn.hip), and at
+# TP = 1 the o_proj too; tests turn them off to compare against the separate launches
 FUSE_QKV_ATTN = True
+FUSE_OPROJ = True
 _QA_SYNC: dict = {}
+_STEP_TAG: dict = {}
+
+
+def step_tag(device) -> torch.Tensor:
+    """The per-device step tag word (bumped by every step's embedding launch; the attention -> o_proj
+    granules of the fused launch carry it)."""
+    key = _dev_key(device)
+    t = _STEP_TAG.get(key)
+    if t is None:
+        t = _STEP_TAG[key] = torch.zeros(16, dtype=torch.int32, device=device)
+    return t
 
 
 def qa_sync(device) -> torch.Tensor:
     """Zeroed granule buffer of the fused QKV + attention launch (QaSync: 16 rows x N/2 x 8 B, N <= 32768;
     the consumers clear what they read)."""
-    key = str(device)
+    key = _dev_key(device)
     t = _QA_SYNC.get(key)
     if t is None:
         t = _QA_SYNC[key] = torch.zeros(1 << 20, dtype=torch.int32, device=device)
@@ -424,7 +454,7 @@ _AWQ_SCRATCH: dict = {}
 
 def reserve_awq_scratch(device, numel: int) -> torch.Tensor:
     """The per-device bf16 scratch one dequantised AWQ matrix lives in during a long step."""
-    key = str(device)
+    key = _dev_key(device)
     t = _AWQ_SCRATCH.get(key)
     if t is None or t.numel() < numel:
         t = _AWQ_SCRATCH[key] = torch.empty(numel, dtype=torch.bfloat16, device=device)
@@ -476,7 +506,7 @@ def fault_word(device) -> torch.Tensor:
     up, 4: a stream-K partial poll, 8: a split-K granule poll, 16: a sampler row meeting; bit 0 is
     reserved). Kernels only OR bits in; the step graph's last node
     copies it to the host ring (ModelRunner.kernel_fault), and a non-zero word fails the engine."""
-    key = str(device)
+    key = _dev_key(device)
     t = _FAULT.get(key)
     if t is None:
         t = _FAULT[key] = torch.zeros(4, dtype=torch.int32, device=device)
@@ -488,7 +518,7 @@ _TICKETS: dict = {}
 
 def attn_tickets(device) -> torch.Tensor:
     """Self-resetting decode-partition tickets (allocated once per device, before any capture)."""
-    key = str(device)
+    key = _dev_key(device)
     t = _TICKETS.get(key)
     if t is None:
         t = torch.zeros(1 << 16, dtype=torch.int32, device=device)
@@ -512,7 +542,7 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor
 
 
 def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None, vstart: int = 0,
-              prev: torch.Tensor | None = None):
+              prev: torch.Tensor | None = None, bump_step: bool = False):
     """Row gather with vocab-shard masking (rows outside this TP rank's shard are zero).
     ids < 0 name a token the previous step sampled on the device: id = prev[-id - 1]."""
     if out is None:
@@ -522,7 +552,7 @@ def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None =
             ids = torch.where(ids < 0, prev.to(ids.device)[(-ids - 1).clamp(min=0).long()], ids)
         out.copy_(ref.embedding_ref(ids, table, vstart))
         return out
-    native().embedding(ids, table, out, vstart, prev)
+    native().embedding(ids, table, out, vstart, prev, step_tag(table.device) if bump_step else None)
     return out
 
 
@@ -870,7 +900,7 @@ _SWS: dict = {}
 def sample_workspace(device) -> torch.Tensor:
     """Per-row epochs + fixed per-row granule regions of the segmented sampler (zeroed once, per
     device; launchers.h SAMPLE_WS_*)."""
-    key = str(device)
+    key = _dev_key(device)
     ws = _SWS.get(key)
     if ws is None:
         ws = torch.zeros(int(native().SAMPLE_WS_WORDS), dtype=torch.int32, device=device)
@@ -888,7 +918,7 @@ _SKWS: dict = {}
 def sk_workspace(device) -> torch.Tensor:
     """Zeroed publisher slots of the stream-K decode kernel (the owner clears what it reads, so it
     stays zero between launches): 64 MiB covers ntiles x (contributors - 1) x 3 KiB of any model."""
-    key = str(device)
+    key = _dev_key(device)
     t = _SKWS.get(key)
     if t is None:
         t = _SKWS[key] = torch.zeros(16 * 2**20, dtype=torch.int32, device=device)
