@@ -31,7 +31,6 @@ def main():
     ap.add_argument("--hq", type=int, default=12)
     ap.add_argument("--hkv", type=int, default=2)
     ap.add_argument("--hidden", type=int, default=1536)
-    ap.add_argument("--oproj", action="store_true", help="the o_proj as the launch's third role")
     a = ap.parse_args()
     C = ops.native()
     dev = torch.device("cuda")
@@ -63,23 +62,16 @@ def main():
     q = torch.empty(S, hq * D, dtype=torch.bfloat16, device=dev)
     o = torch.empty(S, hq * D, dtype=torch.bfloat16, device=dev)
     dbg = torch.zeros(16, dtype=torch.int64, device=dev)
-    lo = ops.Linear((torch.randn(H, hq * D, device=dev) / math.sqrt(hq * D)).bfloat16())
-    resid = torch.randn(S, H, device=dev).bfloat16()
-    ssp = torch.zeros(S, H // 16, dtype=torch.float32, device=dev)
     buf = torch.zeros(1 << 16, dtype=torch.int64, device=dev)
     rows = []
     for it in range(48):
         dbg.zero_()
         buf.zero_()
-        ops.step_tag(dev).add_(1)
-        fa = dict(block_tables=bt, context_lens=cl, query_start=qs, out=o, part_o=po, part_ml=pml,
-                  part_size=part, scale=D ** -0.5, dbg_ts=dbg)
-        if a.oproj:
-            fa.update(oproj=dict(lin=lo, out=resid, residual=resid, ssp_out=ssp), layer=1)
         C.timeline_start(buf)
         ops.linear(x, lins[it % copies], out=q, norm=(gamma, 1e-6),
                    qkv=dict(positions=pos, slots=slots, cos_sin=cs, k_cache=kc, v_cache=vc, hq=hq, hkv=hkv),
-                   attn=fa)
+                   attn=dict(block_tables=bt, context_lens=cl, query_start=qs, out=o, part_o=po, part_ml=pml,
+                             part_size=part, scale=D ** -0.5, dbg_ts=dbg))
         torch.cuda.synchronize()
         C.timeline_stop()
         ents = C.timeline_entries()
@@ -89,24 +81,16 @@ def main():
         st = buf[off: off + 2 * nb].view(nb, 2).cpu()
         t0 = int(st[:, 0].min())
         ncons = S * P * hkv
-        no = H // 16 if fa.get("fused", 0) & 2 else 0
-        nprod = nb - ncons - no
-        ost = st[nprod + ncons:]
-        o_start = (ost[:, 0] - t0).float() / 100.0 if no else torch.zeros(1)
-        o_end = (ost[:, 1] - t0).float() / 100.0 if no else torch.zeros(1)
+        nprod = nb - ncons
         prod_end = (st[:nprod, 1] - t0).float() / 100.0
-        cons = st[nprod: nprod + ncons]
+        cons = st[nprod:]
         work = [i for i in range(ncons) if (i % S) < S and (i // S) % P == 0]  # partition 0 blocks do the work
         cons_end = (cons[work, 1] - t0).float() / 100.0
         d = dbg.cpu().tolist()
         rows.append({"kernel": name, "gemm_end_med": float(prod_end.median()), "gemm_end_max": float(prod_end.max()),
                      "attn_end_med": float(cons_end.median()), "attn_end_max": float(cons_end.max()),
                      "b0_start": (d[0] - t0) / 100.0, "b0_meta": (d[1] - t0) / 100.0, "b0_q_seen": (d[6] - t0) / 100.0,
-                     "b0_chunk_done": (d[2] - t0) / 100.0, "b0_lds": (d[5] - t0) / 100.0, "b0_stored": (d[3] - t0) / 100.0,
-                     "o0_poll_start": (d[8] - t0) / 100.0, "o0_cheap_ok": (d[9] - t0) / 100.0,
-                     "o0_x_loaded": (d[10] - t0) / 100.0, "o0_done": (d[11] - t0) / 100.0,
-                     "o_start_med": float(o_start.median()), "o_start_max": float(o_start.max()),
-                     "o_end_med": float(o_end.median()), "o_end_max": float(o_end.max())})
+                     "b0_chunk_done": (d[2] - t0) / 100.0, "b0_lds": (d[5] - t0) / 100.0, "b0_stored": (d[3] - t0) / 100.0})
     out = {"ctx": a.ctx, "batch": S, "hq": hq, "hkv": hkv, "kernel": rows[0]["kernel"] if rows else None}
     for k in rows[0]:
         if k != "kernel":

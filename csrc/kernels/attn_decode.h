@@ -262,10 +262,6 @@ __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, in
   // the prefetched chunk (with_new) — until every tag is this step's; bounded (fault bit 32)
   const uint32_t tag = (uint32_t)ctx;  // position + 1 of the new token
   const uint32_t row0 = FUSED ? (uint32_t)qbeg * (uint32_t)qs->n2 : 0u;
-  // third role: the output also goes out as granules for the in-launch o_proj blocks
-  const bool out_gran = FUSED && qs->on2 > 0;
-  const uint32_t otag = out_gran ? ((*qs->step_tag) << 8) | (uint32_t)qs->layer : 0u;
-  const uint32_t orow = out_gran ? (uint32_t)qs->obase + (uint32_t)qbeg * (uint32_t)qs->on2 : 0u;
   auto poll = [&](bool with_q, bool with_new, uint4 (&kf)[8], uint4 (&vr)[8]) {
     const uint32_t qp = row0 + (uint32_t)(((h * G + (cok ? col : 0)) * D_ + 8 * (lane >> 4)) >> 1);
     const uint32_t kp = row0 + (uint32_t)(((a.Hq + h) * D_ + 8 * (lane >> 4)) >> 1);
@@ -487,12 +483,6 @@ __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, in
       pk.z = pack_bf2(acc[4] * inv, acc[5] * inv);
       pk.w = pack_bf2(acc[6] * inv, acc[7] * inv);
       out_store16<SC1>(a.out, (size_t)qbeg * a.out_stride + (size_t)hq * D_ + d0, pk);
-      if (out_gran) {
-        const uint32_t pr = orow + (uint32_t)((hq * D_ + d0) >> 1);
-        float* gb = reinterpret_cast<float*>(qs->gran);
-        st_sc1_x4(gb, pr * 8u, __builtin_bit_cast(f32x4, make_uint4(pk.x, otag, pk.y, otag)));
-        st_sc1_x4(gb, pr * 8u + 16u, __builtin_bit_cast(f32x4, make_uint4(pk.z, otag, pk.w, otag)));
-      }
     }
     ATTN_STAMP(3);
     return;
@@ -545,91 +535,14 @@ __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, in
     pk.x = pack_bf2(r[0] * iv, r[1] * iv);
     pk.y = pack_bf2(r[2] * iv, r[3] * iv);
     out_store8<SC1>(a.out, (size_t)qbeg * a.out_stride + (size_t)hh * D_ + dd, pk);
-    if (out_gran)
-      st_sc1_x4(reinterpret_cast<float*>(qs->gran), (orow + (uint32_t)((hh * D_ + dd) >> 1)) * 8u,
-                __builtin_bit_cast(f32x4, make_uint4(pk.x, otag, pk.y, otag)));
   }
-}
-
-// Third role of the fused launch (TP = 1 decode): the layer's o_proj, one 16-column tile per block
-// (blk_x: ids from vbase), nw waves splitting K (<= 8 k-steps each). Every weight fragment and the
-// epilogue operands are requested at launch; then the attention output (x) is polled as granules —
-// rows without a new token (slot < 0) have none and are not waited for (their output rows are
-// never read) — and the block finishes as the decode tile kernel does (gemm_finish: residual, RMSNorm
-// hand-off producer).
-__device__ __forceinline__ void oproj_block(const GemmParams& p, const QaSync& q, char* smem) {
-  TLScope tl_scope(p.dbg_ts);
-  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nt0 = blk_x(p), KT = p.K >> 5, r16 = lane & 15;
-  const int kbeg = (KT * wid) / nw, kend = (KT * (wid + 1)) / nw;  // <= 8 k-steps (host)
-  const uint4* wb = p.wp + (size_t)nt0 * KT * 64 + lane;
-  uint4 b[8], x[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) b[u] = ld_nt16(wb + (size_t)min(kbeg + u, kend - 1) * 64);
-  EpiPre<1> pre;
-  if (wid == 0) epi_pre_a<1, EPI_BF16>(p, pre, r16, nt0, 4 * (lane >> 4));
-  const int m = r16 < p.M ? r16 : p.M - 1;
-  const bool live = p.slots[m] >= 0;
-  const uint32_t tag = ((*q.step_tag) << 8) | (uint32_t)q.layer;
-  const uint32_t rowp = (uint32_t)q.obase + (uint32_t)m * (uint32_t)q.on2 + 4u * (uint32_t)(lane >> 4);
-  // a cheap poll first — the first and last granule group of the wave's k-range, 4 loads per lane
-  // (96 blocks re-reading their whole x slice every round trip took ~12 MB per poll round from the
-  // fabric the attention blocks need: the fused o_proj gained nothing) — then the whole slice,
-  // re-polled only if some tag is still old
-#define QA_OSTAMP(i)                                                      \
-  do {                                                                    \
-    if (q.dbg != nullptr && nt0 == 0 && threadIdx.x == 0) q.dbg[i] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-  QA_OSTAMP(8);
-  int spins = 0;
-  const uint32_t pa = rowp + 16u * (uint32_t)kbeg, pz = rowp + 16u * (uint32_t)(kend - 1);
-  while (true) {
-    uint4 t0, t1;
-    const bool ok = qa_get8(q, pa, tag, t0) && qa_get8(q, pz, tag, t1);
-    if (__all(ok || !live) || ++spins > (1 << 20)) break;
-    __builtin_amdgcn_s_sleep(2);
-  }
-  QA_OSTAMP(9);
-  while (true) {
-    bool ok = true;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) ok = qa_get8(q, rowp + 16u * (uint32_t)min(kbeg + u, kend - 1), tag, x[u]) && ok;
-    const bool all = __all(ok || !live);
-    if (all || ++spins > (1 << 20)) {  // bounded: the step fails loudly (fault word), never hangs
-      if (!all && lane == 0 && q.fault != nullptr) atomicOr(q.fault, 32u);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  QA_OSTAMP(10);
-  f32x4 acc[1][1] = {{f32x4{0.f, 0.f, 0.f, 0.f}}};
-#pragma unroll
-  for (int u = 0; u < 8; ++u)
-    if (kbeg + u < kend) acc[0][0] = mfma16(as_bf16x8(b[u]), as_bf16x8(x[u]), acc[0][0]);
-  const float ssr[1] = {0.f};
-  gemm_finish<1, 1, EPI_BF16, 0, true>(p, acc, ssr, smem, 0, nt0, pre);
-  QA_OSTAMP(11);
-#undef QA_OSTAMP
 }
 
 // Host side of the fused QKV projection + decode attention launch (qkv_attn.hip, gemm_kx.h): the
 // attention blocks' arguments and the launch's LDS for gx x slices GEMM blocks of `waves` waves;
 // false when the step or shape is not one it takes (the caller launches the two kernels).
-// the o_proj role's launch parameters (bf16 residual GEMM: operands, epilogue, hand-off producer)
-static inline GemmParams qa_oproj_params(const GemmArgs& g) {
-  GemmParams p{};
-  p.x = reinterpret_cast<const bf16_t*>(g.x); p.lda = g.lda; p.M = g.M;
-  p.wp = reinterpret_cast<const uint4*>(g.wp); p.N = g.N; p.K = g.K;
-  p.bias = reinterpret_cast<const bf16_t*>(g.bias); p.res = reinterpret_cast<const bf16_t*>(g.res); p.ldr = g.ldr;
-  p.out = g.out; p.ldo = g.ldo;
-  p.splitk = 1; p.fault = g.fault; p.eps = g.eps;
-  p.ssp_out = g.ssp_out;
-  return p;
-}
-
 static inline bool qa_setup(GemmParams& p, const GemmArgs& g, int gx, int slices, int waves, size_t lds_gemm,
-                            AttnArgs& a, QaSync& q, size_t& lds, GemmParams& po) {
+                            AttnArgs& a, QaSync& q, size_t& lds) {
   if (g.fa == nullptr || g.fa_gran == nullptr || g.fa_done == nullptr) return false;
   if ((size_t)g.M * (size_t)(g.N / 2) * 8 > g.fa_gran_bytes) return false;
   a = *g.fa;
@@ -639,45 +552,22 @@ static inline bool qa_setup(GemmParams& p, const GemmArgs& g, int gx, int slices
   if (a.S * a.num_parts * a.Hkv <= 0) return false;
   lds = std::max(lds_gemm, (size_t)attn_lds_bytes(waves));
   if (lds > 160 * 1024) return false;
-  q = QaSync{g.fa_gran, g.N / 2, gx * slices, g.fault, 0, 0, nullptr, 0, 0, a.dbg_ts};
+  q = QaSync{g.fa_gran, g.N / 2, gx * slices, g.fault};
   p.qa_gran = reinterpret_cast<uint4*>(g.fa_gran);
   p.vgx = gx;
   a.tl = nullptr;
-  // the o_proj role: bf16, decode rows, no norm mode, no all-reduce, K = the attention width, <= 8
-  // k-steps per wave, and its granules after the q / K / V region
-  po = GemmParams{};
-  const GemmArgs* fo = g.fo;
-  if (fo != nullptr && g.fo_done != nullptr && g.step_tag != nullptr && fo->M == g.M && fo->K == a.Hq * 128 &&
-      fo->N % 16 == 0 && fo->norm_w == nullptr && !fo->rownorm && fo->ssp_in == nullptr && fo->row_idx == nullptr &&
-      fo->ar_world == 0 && fo->epi == 0 && fo->K / 32 <= 8 * waves && fo->hg == nullptr && g.slots != nullptr) {
-    const size_t obase = (size_t)16 * (g.N / 2);
-    if ((obase + (size_t)g.M * (fo->K / 2)) * 8 <= g.fa_gran_bytes) {
-      po = qa_oproj_params(*fo);
-      po.splitk = 1;
-      po.slots = g.slots;  // liveness of the rows (a new token <=> slot >= 0)
-      po.vgx = fo->N / 16;
-      q.obase = (int)obase;
-      q.on2 = fo->K / 2;
-      q.step_tag = g.step_tag;
-      q.layer = g.layer % 255 + 1;  // (never 0: a tag of 0 would match the zeroed buffer)
-      q.ocons0 = q.nprod + a.S * a.num_parts * a.Hkv;
-      po.vbase = q.ocons0;
-      lds = std::max(lds, (size_t)red_bytes<1, 1>(waves) + ssq_bytes<1>(waves) + 16);
-    }
-  }
   return true;
 }
 
 template <typename K>
-static void qa_launch(K kern, const GemmParams& p, const AttnArgs& a, const QaSync& q, const GemmParams& po,
-                      int waves, size_t lds, hipStream_t st) {
+static void qa_launch(K kern, const GemmParams& p, const AttnArgs& a, const QaSync& q, int waves, size_t lds,
+                      hipStream_t st) {
   if (lds > 64 * 1024) {
     static bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
     (void)attr;
   }
-  const int nblk = q.nprod + a.S * a.num_parts * a.Hkv + (q.on2 > 0 ? po.vgx : 0);
-  hipLaunchKernelGGL(kern, dim3(nblk), dim3(64 * waves), lds, st, p, a, q, po);
+  hipLaunchKernelGGL(kern, dim3(q.nprod + a.S * a.num_parts * a.Hkv), dim3(64 * waves), lds, st, p, a, q);
 }
 
 }  // namespace vgate

@@ -85,13 +85,9 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int32_t* __restric
                                                          const int32_t* __restrict__ prev,
                                                          const bf16_t* __restrict__ table,
                                                          bf16_t* __restrict__ out, int H,
-                                                         int vstart, int vrows, unsigned long long* tl,
-                                                         uint32_t* step_tag) {
+                                                         int vstart, int vrows, unsigned long long* tl) {
   TLScope tl_scope(tl);
   const int t = blockIdx.x;
-  // the step's first kernel bumps the step tag (the in-launch attention -> o_proj hand-off's granule tag)
-  if (step_tag != nullptr && t == 0 && threadIdx.x == 0)
-    __hip_atomic_fetch_add(step_tag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   int tok = ids[t];
   if (tok < 0 && prev != nullptr) tok = prev[-tok - 1];
   const int id = tok - vstart;
@@ -102,10 +98,10 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int32_t* __restric
 }
 
 void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int T, int H,
-                      int vstart, int vrows, hipStream_t st, const int32_t* prev, uint32_t* step_tag) {
+                      int vstart, int vrows, hipStream_t st, const int32_t* prev) {
   if (T <= 0) return;
   hipLaunchKernelGGL(embedding_kernel, dim3(T), dim3(256), 0, st, ids, prev, table, out, H, vstart, vrows,
-                     tl_take("embedding", T), step_tag);
+                     tl_take("embedding", T));
 }
 
 // One workgroup per token. Work items:

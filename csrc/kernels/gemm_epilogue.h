@@ -47,7 +47,6 @@ struct GemmParams {
   ArFused ar;                  // world 0: no fused all-reduce
   uint4* qa_gran;              // EPI_QKV: also write q / K / V as tagged granules (qkv_attn.hip), or null
   int vgx;                     // > 0: a 1-D launch carries the (vgx, 1, slices) grid z-major (qkv_attn.hip)
-  int vbase;                   // ... from block id vbase on
 };
 
 // (column-tile block, K slice, slices) of this block: the grid decomposition of gemm_finish's hand-off
@@ -56,10 +55,10 @@ struct SplitPos {
 };
 __device__ __forceinline__ int grid_x(const GemmParams& p) { return p.vgx > 0 ? p.vgx : (int)gridDim.x; }
 __device__ __forceinline__ int blk_x(const GemmParams& p) {
-  return p.vgx > 0 ? ((int)blockIdx.x - p.vbase) % p.vgx : (int)blockIdx.x;
+  return p.vgx > 0 ? (int)blockIdx.x % p.vgx : (int)blockIdx.x;
 }
 __device__ __forceinline__ int blk_z(const GemmParams& p) {
-  return p.vgx > 0 ? ((int)blockIdx.x - p.vbase) / p.vgx : (int)blockIdx.z;
+  return p.vgx > 0 ? (int)blockIdx.x / p.vgx : (int)blockIdx.z;
 }
 __device__ __forceinline__ SplitPos split_pos(const GemmParams& p) {
   return SplitPos{(int)blockIdx.y * grid_x(p) + blk_x(p), blk_z(p), p.splitk};

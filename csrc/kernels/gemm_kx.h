@@ -306,14 +306,10 @@ __global__ __launch_bounds__((kx_max_threads<Q4, XP, KQW, TMAX, NORM>())) void k
 // The fused QKV projection + decode attention launch on this kernel (design: qkv_attn.hip): GROUP
 // one-tile blocks of <= 8 waves (z-major in the 1-D grid), then the attention blocks
 template <bool Q4, int XP, int KQW, int NORM>
-__global__ __launch_bounds__(512) void kx_qa_kernel(GemmParams p, AttnArgs a, QaSync q, GemmParams po) {
+__global__ __launch_bounds__(512) void kx_qa_kernel(GemmParams p, AttnArgs a, QaSync q) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if ((int)blockIdx.x < q.nprod) {
     kx_block<Q4, XP, KQW, 1, EPI_QKV, NORM, false>(p);
-    return;
-  }
-  if (q.on2 > 0 && (int)blockIdx.x >= q.ocons0) {
-    oproj_block(po, q, smem);
     return;
   }
   TLScope tl_scope(p.dbg_ts);
@@ -332,15 +328,11 @@ static bool kx_qa(GemmParams p, const GemmArgs& g, int groups, int S, int kqs, h
     AttnArgs a;
     QaSync q;
     size_t lds;
-    GemmParams po;
-    if (!qa_setup(p, g, groups, S, nw, red_bytes<1, 1>(nw) + ssq_bytes<1>(nw) + 16, a, q, lds, po)) return false;
-    const int nblk = q.nprod + a.S * a.num_parts * a.Hkv + (q.on2 > 0 ? po.vgx : 0);
-    if (p.dbg_ts == nullptr) p.dbg_ts = tl_take(Q4 ? "awq_kx_qa" : (q.on2 > 0 ? "kx_qa_o" : "kx_qa"), nblk);
-    po.dbg_ts = p.dbg_ts;
-    if (q.on2 > 0) *g.fo_done = true;
-    if (kqw == 1) qa_launch(kx_qa_kernel<Q4, XP, 1, NORM>, p, a, q, po, nw, lds, st);
-    else if (kqw == 2) qa_launch(kx_qa_kernel<Q4, XP, 2, NORM>, p, a, q, po, nw, lds, st);
-    else qa_launch(kx_qa_kernel<Q4, XP, 3, NORM>, p, a, q, po, nw, lds, st);
+    if (!qa_setup(p, g, groups, S, nw, red_bytes<1, 1>(nw) + ssq_bytes<1>(nw) + 16, a, q, lds)) return false;
+    if (p.dbg_ts == nullptr) p.dbg_ts = tl_take(Q4 ? "awq_kx_qa" : "kx_qa", q.nprod + a.S * a.num_parts * a.Hkv);
+    if (kqw == 1) qa_launch(kx_qa_kernel<Q4, XP, 1, NORM>, p, a, q, nw, lds, st);
+    else if (kqw == 2) qa_launch(kx_qa_kernel<Q4, XP, 2, NORM>, p, a, q, nw, lds, st);
+    else qa_launch(kx_qa_kernel<Q4, XP, 3, NORM>, p, a, q, nw, lds, st);
     *g.fa_done = true;
     return true;
   }

@@ -76,12 +76,6 @@ struct GemmArgs {
   void* fa_gran = nullptr;      // zeroed granule buffer (QaSync::gran), fa_gran_bytes long
   size_t fa_gran_bytes = 0;
   bool* fa_done = nullptr;
-  // with fa: the o_proj GEMM of the same layer as a third role of the launch (its x = the attention
-  // output; bf16, residual / hand-off producer epilogue); fo_done set when it ran there
-  const GemmArgs* fo = nullptr;
-  bool* fo_done = nullptr;
-  const uint32_t* step_tag = nullptr;
-  int layer = 0;
 };
 void launch_gemm(const GemmArgs& g, hipStream_t st);
 // stream-K decode GEMM (gemm_streamk.hip): M <= 16 dense rows, one equal share of the packed weight
@@ -144,8 +138,7 @@ void launch_rmsnorm(const uint16_t* x, int ldx, uint16_t* res, int ldres, const 
 
 // Embedding gather with vocab-shard masking (TP): rows outside [vstart, vstart+vrows) -> 0.
 void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int T, int H,
-                      int vstart, int vrows, hipStream_t st, const int32_t* prev = nullptr,
-                      uint32_t* step_tag = nullptr);
+                      int vstart, int vrows, hipStream_t st, const int32_t* prev = nullptr);
 
 // Default-policy read sweep of [p, p + bytes) over `blocks` workgroups (MALL warm-up).
 void launch_prefetch(const void* p, size_t bytes, int blocks, hipStream_t st);
@@ -220,15 +213,6 @@ struct QaSync {
   int n2;
   int nprod;
   uint32_t* fault;
-  // third role (attention -> o_proj, TP = 1): the attention blocks also write their output as granules
-  // {bf16 pair, tag} at pair offset obase (on2 pairs per row; on2 = 0: no o_proj role) with tag =
-  // step tag << 8 | (layer % 255 + 1) (step_tag: bumped by each step's embedding launch), and
-  // the o_proj blocks — ids from ocons0 — poll them
-  int obase, on2;
-  const uint32_t* step_tag;
-  int layer;
-  int ocons0;
-  unsigned long long* dbg;  // profiling: o_proj block 0 phase stamps [8, 12) (qa_phases.py), or null
 };
 void launch_attn_decode(const AttnArgs& a, hipStream_t st);
 void launch_attn_prefill(const AttnArgs& a, hipStream_t st);

@@ -27,14 +27,10 @@
 namespace vgate {
 
 template <int U, int XP, int NORM>
-__global__ __launch_bounds__(512) void qkv_attn_kernel(GemmParams p, AttnArgs a, QaSync q, GemmParams po) {
+__global__ __launch_bounds__(512) void qkv_attn_kernel(GemmParams p, AttnArgs a, QaSync q) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if ((int)blockIdx.x < q.nprod) {
     gemm_block<1, 1, U, EPI_QKV, NORM, true, XP>(p);
-    return;
-  }
-  if (q.on2 > 0 && (int)blockIdx.x >= q.ocons0) {
-    oproj_block(po, q, smem);
     return;
   }
   TLScope tl_scope(p.dbg_ts);
@@ -45,13 +41,13 @@ __global__ __launch_bounds__(512) void qkv_attn_kernel(GemmParams p, AttnArgs a,
 }
 
 template <int NORM>
-static bool qa_dispatch(int u, int xp, const GemmParams& p, const AttnArgs& a, const QaSync& q,
-                        const GemmParams& po, int waves, size_t lds, hipStream_t st) {
-  if (xp == 4 && u == 8) { qa_launch(qkv_attn_kernel<8, 4, NORM>, p, a, q, po, waves, lds, st); return true; }
-  if (xp == 2 && u == 6) { qa_launch(qkv_attn_kernel<6, 2, NORM>, p, a, q, po, waves, lds, st); return true; }
-  if (xp == 2 && u == 8) { qa_launch(qkv_attn_kernel<8, 2, NORM>, p, a, q, po, waves, lds, st); return true; }
-  if (xp == 1 && u == 6) { qa_launch(qkv_attn_kernel<6, 1, NORM>, p, a, q, po, waves, lds, st); return true; }
-  if (xp == 1 && u == 8) { qa_launch(qkv_attn_kernel<8, 1, NORM>, p, a, q, po, waves, lds, st); return true; }
+static bool qa_dispatch(int u, int xp, const GemmParams& p, const AttnArgs& a, const QaSync& q, int waves,
+                        size_t lds, hipStream_t st) {
+  if (xp == 4 && u == 8) { qa_launch(qkv_attn_kernel<8, 4, NORM>, p, a, q, waves, lds, st); return true; }
+  if (xp == 2 && u == 6) { qa_launch(qkv_attn_kernel<6, 2, NORM>, p, a, q, waves, lds, st); return true; }
+  if (xp == 2 && u == 8) { qa_launch(qkv_attn_kernel<8, 2, NORM>, p, a, q, waves, lds, st); return true; }
+  if (xp == 1 && u == 6) { qa_launch(qkv_attn_kernel<6, 1, NORM>, p, a, q, waves, lds, st); return true; }
+  if (xp == 1 && u == 8) { qa_launch(qkv_attn_kernel<8, 1, NORM>, p, a, q, waves, lds, st); return true; }
   return false;
 }
 
@@ -65,14 +61,10 @@ bool launch_qkv_attn(int u, int xp, int norm, GemmParams p, int gx, int slices, 
   AttnArgs a;
   QaSync q;
   size_t lds;
-  GemmParams po;
-  if (!qa_setup(p, g, gx, slices, waves, lds_gemm, a, q, lds, po)) return false;
-  const int nblk = q.nprod + a.S * a.num_parts * a.Hkv + (q.on2 > 0 ? po.vgx : 0);
-  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take(q.on2 > 0 ? "qkv_attn_o" : "qkv_attn", nblk);
-  po.dbg_ts = p.dbg_ts;
-  if (q.on2 > 0) *g.fo_done = true;
-  if (norm == 2) return qa_dispatch<2>(u, xp, p, a, q, po, waves, lds, st);
-  return qa_dispatch<3>(u, xp, p, a, q, po, waves, lds, st);
+  if (!qa_setup(p, g, gx, slices, waves, lds_gemm, a, q, lds)) return false;
+  if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("qkv_attn", q.nprod + a.S * a.num_parts * a.Hkv);
+  if (norm == 2) return qa_dispatch<2>(u, xp, p, a, q, waves, lds, st);
+  return qa_dispatch<3>(u, xp, p, a, q, waves, lds, st);
 }
 
 }  // namespace vgate

@@ -51,7 +51,7 @@ vgate::AttnArgs attn_common(const Tensor& q, int64_t q_stride, const Tensor& k_c
 // out = epilogue(prologue(x) @ W^T); W fragment-packed [N/16, K/32, 64, 8] bf16, or AWQ
 // int4 [N/16, K/128, 64, 4] int32 with scales/zeros. ws = int32 workspace: [0, 65536)
 // split-K tickets (zeroed once, self-resetting), the rest fp32 slabs.
-int64_t gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, int64_t epi,
+void gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& out, int64_t epi,
           const c10::optional<Tensor>& bias, const c10::optional<Tensor>& res,
           const c10::optional<Tensor>& norm_w, double eps, const c10::optional<Tensor>& row_idx,
           const c10::optional<Tensor>& ws, int64_t waves, int64_t splitk,
@@ -69,10 +69,7 @@ int64_t gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& ou
           const c10::optional<Tensor>& fa_out, const c10::optional<Tensor>& fa_part_o,
           const c10::optional<Tensor>& fa_part_ml, const c10::optional<Tensor>& fa_tickets,
           const c10::optional<Tensor>& fa_sync, int64_t fa_part_size, double fa_scale,
-          const c10::optional<Tensor>& fa_dbg_ts, const c10::optional<Tensor>& o_wp, int64_t o_N,
-          const c10::optional<Tensor>& o_out, const c10::optional<Tensor>& o_res,
-          const c10::optional<Tensor>& o_bias, const c10::optional<Tensor>& o_ssp_out,
-          const c10::optional<Tensor>& step_tag, int64_t layer) {
+          const c10::optional<Tensor>& fa_dbg_ts) {
   CHECK_DEV(x); CHECK_DEV(wp); CHECK_DEV(out);
   CHECK_DT(x, torch::kBFloat16);
   CHECK_LASTDIM(x); CHECK_LASTDIM(out);
@@ -224,42 +221,10 @@ int64_t gemm(const Tensor& x, const Tensor& wp, int64_t N, int64_t K, Tensor& ou
     g.fa_gran_bytes = (size_t)fa_sync->numel() * 4;
     g.fa_done = &fa_done;
   }
-  // with it (TP = 1 decode): the layer's o_proj on the attention output as the launch's third role
-  vgate::GemmArgs fo{};
-  bool fo_done = false;
-  if (fused_attn && o_wp.has_value() && o_wp->defined()) {
-    CHECK_DEV(*o_wp); CHECK_DT(*o_wp, torch::kBFloat16);
-    const int64_t oK = fa_out->size(1);
-    TORCH_CHECK(o_N % 16 == 0 && o_wp->numel() == o_N * oK, "fused o_proj: packed weight [N, Hq * 128]");
-    TORCH_CHECK(o_out.has_value() && o_out->defined() && step_tag.has_value() && step_tag->defined(),
-                "fused o_proj: out and step_tag");
-    CHECK_DEV(*o_out); CHECK_DT(*o_out, torch::kBFloat16); CHECK_LASTDIM(*o_out);
-    TORCH_CHECK(o_out->size(0) >= M && o_out->size(1) >= o_N, "fused o_proj: out shape");
-    CHECK_DEV(*step_tag); CHECK_DT(*step_tag, torch::kInt32);
-    fo.x = bf16p(*fa_out); fo.lda = (int)fa_out->stride(0); fo.M = (int)M;
-    fo.wp = o_wp->data_ptr(); fo.N = (int)o_N; fo.K = (int)oK;
-    fo.bias = opt_bf16(o_bias);
-    fo.res = opt_bf16(o_res);
-    fo.ldr = fo.res ? (int)o_res->stride(0) : 0;
-    if (fo.res) TORCH_CHECK(o_res->size(0) >= M && o_res->size(1) >= o_N, "fused o_proj: residual shape");
-    fo.out = o_out->data_ptr(); fo.ldo = (int)o_out->stride(0);
-    fo.epi = 0; fo.fault = g.fault;
-    if (o_ssp_out.has_value() && o_ssp_out->defined()) {
-      CHECK_DEV(*o_ssp_out); CHECK_DT(*o_ssp_out, torch::kFloat32);
-      TORCH_CHECK(o_ssp_out->numel() >= M * (o_N / 16), "fused o_proj: ssp_out [M][N/16]");
-      fo.ssp_out = reinterpret_cast<float*>(o_ssp_out->data_ptr());
-    }
-    g.fo = &fo;
-    g.fo_done = &fo_done;
-    g.step_tag = reinterpret_cast<const uint32_t*>(step_tag->data_ptr());
-    g.layer = (int)layer;
-  }
   c10::DeviceGuard guard(x.device());
   if (awq) vgate::launch_awq_gemm(g, cur_stream());
   else vgate::launch_gemm(g, cur_stream());
   if (fused_attn && !fa_done) vgate::launch_attention(fa, fa.S, cur_stream());
-  // 1: the attention ran in this launch, 2: the o_proj too (else the caller launches it)
-  return (fa_done ? 1 : 0) | (fa_done && fo_done ? 2 : 0);
 }
 
 // AWQ int4 packed weight -> bf16 packed weight (same fragment order / row permutation)
@@ -299,7 +264,7 @@ void rmsnorm(const Tensor& x, const c10::optional<Tensor>& res, const Tensor& w,
 }
 
 void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart,
-               const c10::optional<Tensor>& prev, const c10::optional<Tensor>& step_tag) {
+               const c10::optional<Tensor>& prev) {
   CHECK_DEV(ids); CHECK_DEV(table); CHECK_DEV(out);
   CHECK_DT(ids, torch::kInt32); CHECK_DT(table, torch::kBFloat16); CHECK_DT(out, torch::kBFloat16);
   TORCH_CHECK(table.is_contiguous() && out.is_contiguous(), "embedding: contiguous");
@@ -308,8 +273,7 @@ void embedding(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vsta
   c10::DeviceGuard guard(ids.device());
   vgate::launch_embedding(reinterpret_cast<const int32_t*>(ids.data_ptr()), bf16p(table),
                           bf16p_mut(out), (int)T, (int)H, (int)vstart, (int)table.size(0),
-                          cur_stream(), opt_ptr<const int32_t>(prev, torch::kInt32, "prev"),
-                          reinterpret_cast<uint32_t*>(opt_ptr<int32_t>(step_tag, torch::kInt32, "step_tag")));
+                          cur_stream(), opt_ptr<const int32_t>(prev, torch::kInt32, "prev"));
 }
 
 void rope_kv(Tensor& qkv, const Tensor& positions, const c10::optional<Tensor>& slots,
@@ -670,10 +634,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("ar_fused_off") = 0, py::arg("fa_block_tables") = py::none(), py::arg("fa_context_lens") = py::none(),
         py::arg("fa_query_start") = py::none(), py::arg("fa_out") = py::none(), py::arg("fa_part_o") = py::none(),
         py::arg("fa_part_ml") = py::none(), py::arg("fa_tickets") = py::none(), py::arg("fa_sync") = py::none(),
-        py::arg("fa_part_size") = 512, py::arg("fa_scale") = 1.0, py::arg("fa_dbg_ts") = py::none(),
-        py::arg("o_wp") = py::none(), py::arg("o_N") = 0, py::arg("o_out") = py::none(), py::arg("o_res") = py::none(),
-        py::arg("o_bias") = py::none(), py::arg("o_ssp_out") = py::none(), py::arg("step_tag") = py::none(),
-        py::arg("layer") = 0);
+        py::arg("fa_part_size") = 512, py::arg("fa_scale") = 1.0, py::arg("fa_dbg_ts") = py::none());
   m.def("attention", &attention, "unified paged attention: decode (partitions merged in-launch) + varlen prefill tiles",
         py::arg("q"), py::arg("q_stride"), py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"),
         py::arg("context_lens"), py::arg("query_start"), py::arg("tile_seq"), py::arg("tile_q0"), py::arg("out"),
@@ -681,8 +642,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("out_stride") = 0, py::arg("tickets") = py::none(), py::arg("dbg_ts") = py::none(),
         py::arg("flash_ws") = py::none(), py::arg("fault") = py::none());
   m.def("embedding", &embedding, "vocab-sharded embedding gather (negative ids: previous step's samples)",
-        py::arg("ids"), py::arg("table"), py::arg("out"), py::arg("vstart") = 0, py::arg("prev") = py::none(),
-        py::arg("step_tag") = py::none());
+        py::arg("ids"), py::arg("table"), py::arg("out"), py::arg("vstart") = 0, py::arg("prev") = py::none());
   m.def("rmsnorm", &rmsnorm, "RMSNorm with optional fused residual add");
   m.def("rope_kv", &rope_kv, "NeoX RoPE + paged KV-cache write (rotated q in place or into q_out)",
         py::arg("qkv"), py::arg("positions"), py::arg("slots"), py::arg("cos_sin"), py::arg("k_cache"),

@@ -202,7 +202,7 @@ class DecoderModel:
         dev = self.device
         # RMSNorms are folded into the consuming GEMMs (deferred row scale), so a layer is
         # qkv GEMM -> attention -> o GEMM (+residual) -> gate_up GEMM -> down GEMM (+residual).
-        resid = ops.embedding(sv.ids, self.embed, vstart=sh.vocab0, prev=sv.prev_tokens, bump_step=True)
+        resid = ops.embedding(sv.ids, self.embed, vstart=sh.vocab0, prev=sv.prev_tokens)
         if tp.size > 1:
             tp.all_reduce(resid)
         q = torch.empty(T, sh.hq * D, dtype=torch.bfloat16, device=dev)
@@ -241,10 +241,6 @@ class DecoderModel:
             fa = dict(block_tables=sv.block_tables, context_lens=sv.context_lens, query_start=sv.query_start,
                       out=attn, part_o=part_o, part_ml=part_ml, part_size=part_size,
                       scale=self.scale) if fuse_attn else None
-            gu = takes(L.gate_up)
-            if fa is not None and tp.size == 1 and L.o.kind == "dense":
-                # ... and the o_proj as the launch's third role (resid += attn @ Wo^T, hand-off sums)
-                fa.update(oproj=dict(lin=L.o, out=resid, residual=resid, ssp_out=ssp if gu else None), layer=li)
             if li > 0 and takes(L.qkv):
                 ops.linear(hg if awq else resid, L.qkv, out=q, prenorm=(ssp, eps), qkv=qkv_args, attn=fa)
             else:
@@ -252,8 +248,8 @@ class DecoderModel:
             if fa is None:
                 ops.attention(q, sh.hq * D, kc, vc, sv.block_tables, sv.context_lens, sv.query_start, sv.tile_seq,
                               sv.tile_q0, attn, part_o, part_ml, sh.hq, sh.hkv, part_size, self.scale)
-            if fa is None or not fa.get("fused", 0) & 2:
-                self._row_parallel(attn, L.o, resid, first, norm_out=(hg, ssp, L.post_norm) if gu else None)
+            gu = takes(L.gate_up)
+            self._row_parallel(attn, L.o, resid, first, norm_out=(hg, ssp, L.post_norm) if gu else None)
             if gu:
                 ops.linear(hg if awq else resid, L.gate_up, out=mlp, prenorm=(ssp, eps))
             else:

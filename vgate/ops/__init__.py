@@ -291,9 +291,7 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
     attn (with qkv, decode-only steps): dict(block_tables, context_lens, query_start, out, part_o,
     part_ml, part_size, scale) — the step's decode attention over q = this projection's output, run
     in the projection's launch when the decode kernel takes it (csrc/kernels/qkv_attn.hip), else
-    launched right after it; returns q as without it. With attn["oproj"] = dict(lin, out, residual,
-    ssp_out) and attn["layer"] (TP = 1, bf16) the layer's o_proj joins the launch as a third role
-    when it can; attn["fused"] tells the caller what ran (1: attention, 2: o_proj too).
+    launched right after it; returns q as without it.
 
     ar (GPU, <= 16 rows, bf16 epilogue): a :class:`vgate.parallel.custom_allreduce.CustomAllReduce`;
     the TP row-parallel GEMM then all-reduces in its epilogue: out = bf16(sum over ranks of
@@ -385,7 +383,6 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
     if attn is not None:
         if qkv is None or M > 16:
             raise ValueError("fused attention: the decode QKV projection (qkv epilogue, <= 16 rows)")
-        attn["fused"] = 0
         if not FUSE_QKV_ATTN:
             C.gemm(x, lin.wp, lin.N, lin.K, out, epi, **kw)
             _attn_after(out, qkv, attn)
@@ -394,33 +391,15 @@ def linear(x: torch.Tensor, lin: Linear, out: torch.Tensor | None = None,
                   fa_query_start=attn["query_start"], fa_out=attn["out"], fa_part_o=attn["part_o"],
                   fa_part_ml=attn["part_ml"], fa_tickets=attn_tickets(x.device), fa_sync=qa_sync(x.device),
                   fa_part_size=int(attn["part_size"]), fa_scale=float(attn["scale"]), fa_dbg_ts=attn.get("dbg_ts"))
-        op = attn.get("oproj")
-        if op is not None and FUSE_OPROJ and op["lin"].kind == "dense":
-            ol = op["lin"]
-            kw.update(o_wp=ol.wp, o_N=ol.N, o_out=op["out"], o_res=op.get("residual"), o_bias=ol.bias,
-                      o_ssp_out=op.get("ssp_out"), step_tag=step_tag(x.device), layer=int(attn.get("layer", 0)))
-        attn["fused"] = int(C.gemm(x, lin.wp, lin.N, lin.K, out, epi, **kw))
-        return out
     C.gemm(x, lin.wp, lin.N, lin.K, out, epi, **kw)
     return out
 
 
-# decode-only steps: the decode attention rides in the QKV projection's launch (qkv_attn.hip), and at
-# TP = 1 the o_proj too; tests turn them off to compare against the separate launches
+# decode-only steps: the decode attention rides in the QKV projection's launch (qkv_attn.hip); tests
+# turn it off to compare against the two-launch path (the o_proj as a third role measured no faster:
+# profiles/r5_qa_oproj_negative.log)
 FUSE_QKV_ATTN = True
-FUSE_OPROJ = True
 _QA_SYNC: dict = {}
-_STEP_TAG: dict = {}
-
-
-def step_tag(device) -> torch.Tensor:
-    """The per-device step tag word (bumped by every step's embedding launch; the attention -> o_proj
-    granules of the fused launch carry it)."""
-    key = _dev_key(device)
-    t = _STEP_TAG.get(key)
-    if t is None:
-        t = _STEP_TAG[key] = torch.zeros(16, dtype=torch.int32, device=device)
-    return t
 
 
 def qa_sync(device) -> torch.Tensor:
@@ -542,7 +521,7 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor
 
 
 def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None, vstart: int = 0,
-              prev: torch.Tensor | None = None, bump_step: bool = False):
+              prev: torch.Tensor | None = None):
     """Row gather with vocab-shard masking (rows outside this TP rank's shard are zero).
     ids < 0 name a token the previous step sampled on the device: id = prev[-id - 1]."""
     if out is None:
@@ -552,7 +531,7 @@ def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None =
             ids = torch.where(ids < 0, prev.to(ids.device)[(-ids - 1).clamp(min=0).long()], ids)
         out.copy_(ref.embedding_ref(ids, table, vstart))
         return out
-    native().embedding(ids, table, out, vstart, prev, step_tag(table.device) if bump_step else None)
+    native().embedding(ids, table, out, vstart, prev)
     return out
 
 
