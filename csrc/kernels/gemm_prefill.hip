@@ -183,10 +183,10 @@ __global__ __launch_bounds__(256, 2) void gemm_prefill_kernel(GemmParams p) {
 // SCHED (k-loop schedule): 0 = the stage's DMA issued before its reads + MFMAs; 1 = + MFMAs at raised
 // wave priority (s_setprio 1: the MFMA-issuing wave wins the SIMD's arbitration over the other wave's
 // LDS reads / DMA issue); 2 = 1 + the stage's DMA issue split in two, half in front of each k-step
-template <int BM, int BN, int WM, int WN, int NS, int EPI, int NORM, int NTB, int SCHED = 0>
+template <int BM, int BN, int WM, int WN, int NS, int EPI, int NORM, int NTB, int SCHED = 0, int KS = 2>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_prefill2_kernel(GemmParams p) {
   constexpr int NW = WM * WN;
-  constexpr int KS = 2;                        // 32-deep k-steps per stage (BK = 64)
+  // KS: 32-deep k-steps per stage (BK = 32 KS)
   constexpr int WTN = BN / 16, XTM = BM / 16;  // 16-wide tiles per block
   constexpr int NT = WTN / WN, MT = XTM / WM;  // per wave
   constexpr int PIECES = (WTN + XTM) * KS;     // 1 KiB pieces per stage
@@ -200,7 +200,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_prefill2_kernel(GemmPara
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int KT = p.K >> 5;
-  const int nk_all = p.K >> 6;
+  const int nk_all = KT / KS;
   const int z = blockIdx.y, nz = gridDim.y;
   const int kst0 = (nk_all * z) / nz, nk = (nk_all * (z + 1)) / nz - kst0;
   const int mblocks = (p.M + BM - 1) / BM;
@@ -215,15 +215,15 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_prefill2_kernel(GemmPara
     const int f = wid * PPW + i;
     if (f < WTN * KS) {
       const int nt = nt_blk + f / KS, ks = f % KS;
-      src[i] = reinterpret_cast<const char*>(p.wp) + (((size_t)nt * KT + 2 * kst0 + ks) * 64 + lane) * 16;
+      src[i] = reinterpret_cast<const char*>(p.wp) + (((size_t)nt * KT + KS * kst0 + ks) * 64 + lane) * 16;
       step[i] = KS * 1024;
     } else {
       const int g = f - WTN * KS;
       const int mt = g / KS, ks = g % KS;
       int row = m0 + mt * 16 + (lane & 15);
       row = row < p.M ? row : p.M - 1;
-      src[i] = reinterpret_cast<const char*>(p.x + (size_t)row * p.lda + kst0 * 64 + ks * 32 + 8 * (lane >> 4));
-      step[i] = 64 * 2;
+      src[i] = reinterpret_cast<const char*>(p.x + (size_t)row * p.lda + kst0 * 32 * KS + ks * 32 + 8 * (lane >> 4));
+      step[i] = 32 * KS * 2;
     }
   }
   const uint32_t lds0 = lds_addr_of(smem);
@@ -605,13 +605,14 @@ VG_RED_INST(EPI_SILU)
 VG_RED_INST(EPI_QKV)
 #undef VG_RED_INST
 
-template <int EPI, int NORM, int NTB, int BM = 256, int BN = 128, int WM = 4, int WN = 2, int NS = 3, int SCHED = 0>
+template <int EPI, int NORM, int NTB, int BM = 256, int BN = 128, int WM = 4, int WN = 2, int NS = 3, int SCHED = 0,
+          int KS = 2>
 static void launch_prefill2_one(const GemmParams& p, int nz, hipStream_t st) {
-  constexpr int STAGE = (BN / 16 + BM / 16) * 2 * 1024;
+  constexpr int STAGE = (BN / 16 + BM / 16) * KS * 1024;
   const int blocks = ((p.M + BM - 1) / BM) * (p.N / BN);
   GemmParams q = p;
   if (q.dbg_ts == nullptr) q.dbg_ts = tl_take("gemm_prefill2", blocks * nz);
-  auto kern = gemm_prefill2_kernel<BM, BN, WM, WN, NS, EPI, NORM, NTB, SCHED>;
+  auto kern = gemm_prefill2_kernel<BM, BN, WM, WN, NS, EPI, NORM, NTB, SCHED, KS>;
   static bool attr = [&] {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                NS * STAGE) == hipSuccess;
@@ -626,11 +627,11 @@ static void launch_prefill2_one(const GemmParams& p, int nz, hipStream_t st) {
   }
 }
 
-template <int EPI, int NORM, int NTB, int BM = 256, int BN = 128, int WM = 4, int WN = 2, int NS = 3>
+template <int EPI, int NORM, int NTB, int BM = 256, int BN = 128, int WM = 4, int WN = 2, int NS = 3, int KS = 2>
 static void launch_prefill2_cfg(const GemmParams& p, int nz, hipStream_t st) {
   // MFMAs at raised priority (schedule 1): +5-7 % on the 256 x 256 tile, neutral on 256 x 128; the
   // split DMA issue was neutral to negative (profiles/r2_prefill_gemm_sched.log)
-  launch_prefill2_one<EPI, NORM, NTB, BM, BN, WM, WN, NS, 1>(p, nz, st);
+  launch_prefill2_one<EPI, NORM, NTB, BM, BN, WM, WN, NS, 1, KS>(p, nz, st);
 }
 
 template <int EPI, int NORM, int NTB, int BN = 256>
@@ -741,6 +742,21 @@ static bool launch_prefill_epi(const GemmParams& p, int force_bn, int force_sk, 
     else launch_prefill2_cfg<EPI, NORM, NTB, 128, 128, 2, 4, 4>(p, nz, st);
     return true;
   }
+  // wide-N mid-M tiles that fill the chip where the 256- / 128-row tiles leave CUs idle or waste rows
+  // (gate_up at 448 rows: 256 x 256 covers 140 of 256 CUs, 128-row tiles make 280 blocks): 64 x 512
+  // over 8 waves (448 rows: 7 x 35 = 245 blocks, no padded rows) and 128 x 320 over 8 waves (224)
+  if (force_bn == 2560) {
+    if (p.N % 512 != 0) return false;
+    launch_prefill2_cfg<EPI, NORM, NTB, 64, 512, 1, 8, 2>(p, nz, st);
+    return true;
+  }
+  if (force_bn == 2561) {
+    if (p.N % 320 != 0) return false;
+    launch_prefill2_cfg<EPI, NORM, NTB, 128, 320, 2, 4, 2>(p, nz, st);
+    return true;
+  }
+  // (the same tiles with 32-deep stages on 4-deep rings measured 15-30 % slower warm and cold:
+  // profiles/r5_prefill_wide_tiles_sweep.log)
   if (force_bn == 640 || force_bn == 641) {
     if (force_bn == 640) launch_prefill2_cfg<EPI, NORM, NTB, 128, 64, 2, 2, 4>(p, nz, st);
     else launch_prefill2_cfg<EPI, NORM, NTB, 128, 64, 4, 2, 4>(p, nz, st);

@@ -1130,6 +1130,31 @@ def test_prefill_lds_gemm_all_epilogues(M, bn, sk):
     assert _rel_err(kc, kc2) < 2e-2 and _rel_err(vc, vc2) < 2e-2
 
 
+@pytest.mark.parametrize("M", [200, 448, 640])
+@pytest.mark.parametrize("bn,sk", [(2560, 0), (2561, 0), (2560, 2), (2561, 3)])
+def test_prefill_wide_tiles(M, bn, sk):
+    """The wide-N mid-M prefill tiles (gemm_prefill.hip: 64 x 512 and 128 x 320) against
+    the fp32 references: plain + in-place residual and folded-norm SiLU*mul, N = 2560 (both tiles
+    divide it), rows past M masked, K split + reduce."""
+    torch.manual_seed(90 + M + bn + sk)
+    H, N = 1536, 2560
+    x = (torch.randn(M, H, device=DEV) * 1.5).bfloat16()
+    w = (torch.randn(N, H, device=DEV) / math.sqrt(H)).bfloat16()
+    res = torch.randn(M, N, device=DEV).bfloat16()
+    out = res.clone()
+    ops.native().gemm(x, ops.Linear(w).wp, N, H, out, 0, res=out, ws=ops.workspace(DEV), path=1, ntb=bn, splitk=sk)
+    assert _rel_err(out, ref.linear_ref(x, w, None, res)) < 1e-2
+    nw = (torch.rand(H, device=DEV) + 0.5).bfloat16()
+    wg = (torch.randn(N // 2, H, device=DEV) / math.sqrt(H)).bfloat16()
+    wu = (torch.randn(N // 2, H, device=DEV) / math.sqrt(H)).bfloat16()
+    gu = ops.Linear(torch.cat([wg, wu]), layout="silu")
+    assert gu.fold_norm(nw)
+    h = torch.empty(M, N // 2, dtype=torch.bfloat16, device=DEV)
+    ops.native().gemm(x, gu.wp, N, H, h, 2, ws=ops.workspace(DEV), rownorm=True, eps=1e-6, path=1, ntb=bn, splitk=sk)
+    xn, _ = ref.rmsnorm_ref(x, nw, 1e-6)
+    assert _rel_err(h, ref.silu_mul_linear_ref(xn, wg, wu)) < 2e-2
+
+
 @pytest.mark.parametrize("M", [17, 24, 40, 48, 64])
 @pytest.mark.parametrize("w,s_long,s_short", [(0, 0, 0), (4, 6, 2), (4, 8, 3), (2, 12, 4), (1, 16, 6), (4, 7, 16),
                                               (8, 0, 0)])

@@ -643,7 +643,9 @@ PREFILL_CANDIDATES = [(0, 0), (64, 0), (128, 0), (128, 2), (128, 4), (256, 0), (
                       (1024, 6)]
 # 128-row tiles on a 4-deep ring, one block per CU (128 x 128 / 128 x 64, 4 or 8 waves): timed for
 # 64 < M <= 1024 only, where the grid of the 2-deep-ring tile is one or two partial rounds
-PREFILL_RING_CANDIDATES = [(t, s) for t in (1280, 1281, 640, 641) for s in (0, 2, 3)]
+# + the wide-N tiles 64 x 512 / 128 x 320 (gate_up at 320 / 448 rows: 245 / 224 blocks, 35 vs 44-64 us)
+PREFILL_RING_CANDIDATES = ([(t, s) for t in (1280, 1281, 640, 641) for s in (0, 2, 3)]
+                           + [(2560, 0), (2561, 0)])
 # medium-M kernel (csrc/kernels/gemm_mid.hip, 16 < M <= 64) candidates, encoded as tile code
 # MID_BASE - W (W tiles = waves per block) and K slices (0 = its heuristic)
 MID_BASE = -10
