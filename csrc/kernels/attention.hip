@@ -200,6 +200,9 @@ __global__ __launch_bounds__(64 * NW) void attn_flash_kernel(AttnArgs a, int laz
   if (q0 % QPB) return;  // block-uniform: not a group leader
   const int qs = a.query_start[s];
   const int qlen = a.query_start[s + 1] - qs;
+  // a single-query sequence is a decode row, computed by this launch's decode blocks: a tile of it
+  // (a tile list that names every sequence) must not write the same output row concurrently
+  if (qlen == 1 && dec_seqs > 0) return;  // block-uniform
   const int ctx = a.context_lens[s];
   const int hq = h * G + wid % G;
   const int qw0 = q0 + 16 * CT * (wid / G);  // this wave's first query
@@ -596,6 +599,9 @@ __global__ __launch_bounds__(MAXT) void attn_kernel(AttnArgs a, int dec_seqs, in
   if (bx < dec_blocks) {
     decode_block(a, bx % dec_seqs, blockIdx.y, bx / dec_seqs, smem);  // block = (sequence, partition)
   } else {
+    // (a tile of a single-query sequence: that row is a decode block's, see attn_flash_kernel)
+    const int s = a.tile_seq[bx - dec_blocks];
+    if (dec_seqs > 0 && s >= 0 && a.query_start[s + 1] - a.query_start[s] == 1) return;
     prefill_body(a, bx - dec_blocks, blockIdx.y, smem);
   }
 }

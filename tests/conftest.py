@@ -115,3 +115,35 @@ def gpu_available() -> bool:
         return torch.cuda.is_available()
     except Exception:  # noqa: BLE001
         return False
+
+
+# ---- GPU tests: the in-launch hand-off words are "zeroed once, self-resetting" — every launch leaves
+# them zero. A test that leaves one set would poison the next kernel that shares the buffer (the GEMM
+# split-K tickets and the flash K-split tickets live in the same workspace), so check after each GPU
+# test and name the test that did it.
+@pytest.fixture(autouse=True)
+def _gpu_handoff_words_clean(request):
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    try:
+        import torch
+
+        from vgate import ops
+    except Exception:  # noqa: BLE001
+        return
+    if not torch.cuda.is_available():
+        return
+    torch.cuda.synchronize()
+    dirty = []
+    for name, store, n in (("workspace tickets", getattr(ops, "_WS", {}), 65536),
+                           ("attention tickets", getattr(ops, "_TICKETS", {}), None)):
+        for key, t in list(store.items()):
+            v = t[:n] if n else t
+            if v.dtype != torch.int32:
+                v = v.view(torch.int32)[:n] if n else v.view(torch.int32)
+            nz = int(torch.count_nonzero(v))
+            if nz:
+                dirty.append(f"{name} [{key}]: {nz} non-zero words")
+                v.zero_()  # the next test starts clean
+    assert not dirty, "in-launch hand-off words left set: " + "; ".join(dirty)
