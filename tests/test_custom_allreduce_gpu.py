@@ -30,7 +30,7 @@ def _expect(xs):
     return acc.bfloat16()
 
 
-def _worker(rank, port, q, WORLD=2, two_shot=0):
+def _worker(rank, port, q, WORLD=2, modes=(0,)):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
         import torch.distributed as dist
@@ -40,40 +40,8 @@ def _worker(rank, port, q, WORLD=2, two_shot=0):
         torch.cuda.set_device(dev)
         ar = CustomAllReduce(dist.group.WORLD, rank, WORLD, dev, max_bytes=4 << 20)
         it = 0
-        for n in [8, 64, 4096, 8 * 1536, 64 * 8192, 2 << 20]:
-            for rep in range(3):
-                it += 1
-                xs = _inputs(n, it, WORLD)
-                t = xs[rank].to(dev)
-                if rep == 1:
-                    out = torch.empty_like(t)
-                    ar.all_reduce(t, out, two_shot=two_shot)
-                else:
-                    out = ar.all_reduce(t, two_shot=two_shot)
-                torch.cuda.synchronize()
-                ar.check()
-                assert torch.equal(out.cpu(), _expect(xs)), (rank, n, rep)
-        # captured into a hipGraph: replays read the static input, epochs advance on device
-        n = 8 * 4096
-        static = torch.zeros(n, dtype=torch.bfloat16, device=dev)
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            ar.all_reduce(static.clone(), two_shot=two_shot)  # warm-up outside capture
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        dist.barrier()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            res = ar.all_reduce(static, two_shot=two_shot)
-        for rep in range(4):
-            it += 1
-            xs = _inputs(n, it, WORLD)
-            static.copy_(xs[rank].to(dev))
-            g.replay()
-            torch.cuda.synchronize()
-            ar.check()
-            assert torch.equal(res.cpu(), _expect(xs)), (rank, "graph", rep)
+        for two_shot in modes:  # (one process group for every form: a spawn per form cost ~3 s of tier time)
+            it = _one_mode(ar, dist, dev, rank, WORLD, two_shot, it)
         dist.barrier()
         ar.close()
         dist.destroy_process_group()
@@ -83,6 +51,45 @@ def _worker(rank, port, q, WORLD=2, two_shot=0):
         q.put((rank, f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
 
 
+def _one_mode(ar, dist, dev, rank, WORLD, two_shot, it):
+    for n in [8, 64, 4096, 8 * 1536, 64 * 8192, 2 << 20]:
+        for rep in range(3):
+            it += 1
+            xs = _inputs(n, it, WORLD)
+            t = xs[rank].to(dev)
+            if rep == 1:
+                out = torch.empty_like(t)
+                ar.all_reduce(t, out, two_shot=two_shot)
+            else:
+                out = ar.all_reduce(t, two_shot=two_shot)
+            torch.cuda.synchronize()
+            ar.check()
+            assert torch.equal(out.cpu(), _expect(xs)), (rank, n, rep)
+    # captured into a hipGraph: replays read the static input, epochs advance on device
+    n = 8 * 4096
+    static = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ar.all_reduce(static.clone(), two_shot=two_shot)  # warm-up outside capture
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    dist.barrier()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        res = ar.all_reduce(static, two_shot=two_shot)
+    for rep in range(4):
+        it += 1
+        xs = _inputs(n, it, WORLD)
+        static.copy_(xs[rank].to(dev))
+        g.replay()
+        torch.cuda.synchronize()
+        ar.check()
+        assert torch.equal(res.cpu(), _expect(xs)), (rank, "graph", two_shot, rep)
+    dist.barrier()
+    return it
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -90,14 +97,14 @@ def _free_port():
 
 
 @pytest.mark.timeout(240)
-@pytest.mark.parametrize("world,two_shot", [(2, 0), (2, 1), (3, -1), (3, 1)])
-def test_custom_allreduce_processes_one_gpu(world, two_shot):
+@pytest.mark.parametrize("world,modes", [(2, (0, 1)), (3, (-1, 1))])
+def test_custom_allreduce_processes_one_gpu(world, modes):
     """One-shot (-1 / auto at 2 ranks) and two-shot (reduce-scatter + all-gather, 1) forms, 2 and
     3 ranks sharing the GPU: bit-exact vs the fp32 rank-order sum, eager and graph-replayed."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, q, world, two_shot)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, port, q, world, modes)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}

@@ -63,7 +63,40 @@ def _generate(eng, prompts=None):
 LONG = {"long600": [7 + (j * 13) % 450 for j in range(600)], "short": [9, 8, 7, 6, 5]}
 
 
-def _worker(rank, world, port, path, q, eager=False, env=None, tokens=320, prompts=None, opts=None, inject=False):
+def _worker(rank, world, port, path, q, eager=False, env=None, tokens=320, prompts=None, opts=None, inject=False,
+            runs=None):
+    """One TP rank. ``runs``: [(eager, opts), ...] engines built one after another in this process group
+    (one spawn for several configurations: a spawn costs ~3 s of the GPU tier); rank 0 reports
+    [(tokens, used_ar, graphs), ...]."""
+    if runs is not None:
+        try:
+            os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                              MASTER_PORT=str(port), **(env or {}))
+            import torch.distributed as dist
+
+            from vgate.runtime.engine import LLMEngine
+
+            torch.cuda.set_device(0)
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            res = []
+            for ea, op in runs:
+                eng = LLMEngine(_cfg(path, world, ea, tokens, **(op or {})))
+                eng.runner.defer_capture = False
+                assert eng.tp_self_check == "passed", eng.tp_self_check
+                if rank == 0:
+                    out = _generate(eng, prompts)
+                    res.append((out, eng.tp.custom_ar is not None and eng.tp.custom_ar.calls > 0,
+                                len(eng.runner.graphs)))
+                    eng.shutdown_followers()
+                else:
+                    eng.follower_loop()
+                del eng
+                torch.cuda.synchronize()
+                dist.barrier()
+            q.put(("ok", res if rank == 0 else None))
+        except Exception:  # noqa: BLE001
+            q.put(("err", traceback.format_exc()))
+        return
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                           MASTER_PORT=str(port), **(env or {}))
@@ -98,8 +131,7 @@ def _worker(rank, world, port, path, q, eager=False, env=None, tokens=320, promp
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("eager,fused", [(False, True), (True, True), (False, False)])
-def test_tp2_on_gpu_matches_tp1(tmp_path, eager, fused):
+def test_tp2_on_gpu_matches_tp1(tmp_path):
     """graph == eager == TP=1: with every decode collective on the IPC kernels (all-reduce and the
     logits all-gather) a gloo TP group replays captured hipGraphs for the buckets they cover.
     fused (default): the decode o_proj / down_proj all-reduce inside their GEMM epilogue
@@ -120,9 +152,9 @@ def test_tp2_on_gpu_matches_tp1(tmp_path, eager, fused):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, path, q, eager, None, 320, None,
-                                                           {"tp_fused_allreduce": fused}))
-             for r in range(2)]
+    cfgs = [(False, True), (True, True), (False, False)]  # (eager, fused)
+    runs = [(e, {"tp_fused_allreduce": f}) for e, f in cfgs]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, path, q), kwargs={"runs": runs}) for r in range(2)]
     for p in procs:
         p.start()
     try:
@@ -134,10 +166,12 @@ def test_tp2_on_gpu_matches_tp1(tmp_path, eager, fused):
                 p.kill()
     errs = [r[1] for r in results if r[0] == "err"]
     assert not errs, errs[0]
-    tp_out, used_ar, graphs = next(r[1] for r in results if r[1] is not None)
-    assert used_ar, "the custom all-reduce was not used between the two ranks"
-    assert tp_out == ref
-    assert (graphs > 0) == (not eager), graphs
+    per_run = next(r[1] for r in results if r[1] is not None)
+    assert len(per_run) == len(cfgs)
+    for (eager, fused), (tp_out, used_ar, graphs) in zip(cfgs, per_run):
+        assert used_ar, ("the custom all-reduce was not used between the two ranks", eager, fused)
+        assert tp_out == ref, (eager, fused)
+        assert (graphs > 0) == (not eager), (graphs, eager, fused)
 
 
 @pytest.mark.timeout(300)
