@@ -482,8 +482,8 @@ _FAULT: dict = {}
 
 def fault_word(device) -> torch.Tensor:
     """Per-device sticky fault word of the in-launch hand-offs (bit 1: a flash K-split waiter gave
-    up, 4: a stream-K partial poll, 8: a split-K granule poll, 16: a sampler row meeting; bit 0 is
-    reserved). Kernels only OR bits in; the step graph's last node
+    up, 4: a stream-K partial poll, 8: a split-K granule poll, 16: a sampler row meeting, 32: a fused
+    QKV + attention granule poll; bit 0 is reserved). Kernels only OR bits in; the step graph's last node
     copies it to the host ring (ModelRunner.kernel_fault), and a non-zero word fails the engine."""
     key = _dev_key(device)
     t = _FAULT.get(key)
