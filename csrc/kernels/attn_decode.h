@@ -217,10 +217,9 @@ __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, in
   const int G = a.Hq / a.Hkv;
   const int col = lane & 15;
   const bool cok = col < G;
-  uint4 qf[4];
-  const size_t qoff = (size_t)qbeg * a.q_stride + (size_t)(h * G + (cok ? col : 0)) * D_ + 8 * (lane >> 4);
+  uint4 qf[4];  // (FUSED: from the producer's granules, after the wait)
   if constexpr (!FUSED) {
-    const bf16_t* qp = a.q + qoff;
+    const bf16_t* qp = a.q + (size_t)qbeg * a.q_stride + (size_t)(h * G + (cok ? col : 0)) * D_ + 8 * (lane >> 4);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) qf[kk] = cok ? *reinterpret_cast<const uint4*>(qp + 32 * kk) : make_uint4(0, 0, 0, 0);
   }
