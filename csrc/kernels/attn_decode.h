@@ -3,6 +3,8 @@
 // online-softmax step, the V^T . P^T update and the per-(sequence, KV head, partition) decode block.
 // Layout and MFMA orientation: attention.hip (file comment).
 #pragma once
+#include <type_traits>
+
 #include "gemm_epilogue.h"
 
 namespace vgate {
@@ -435,34 +437,39 @@ __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, in
   const int icol = it >> 4, d0 = (it & 15) * 8;
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-  if (it < items) {
-    float mw[16];
+  // only the waves that had chunks carry partials (the others: l = 0, weight 0): a context of <= 4
+  // chunks merges 4 slots, not the block's 8 — the same sum, half the LDS reads and exponentials
+  const int nwa = min(nw, nch);
+  auto merge = [&](auto wc) {
+    constexpr int WP = decltype(wc)::value;  // slots per pass (<= 8), mw slots = 16 / (8 / WP)
+    constexpr int MWN = WP == 8 ? 16 : WP;
+    float mw[MWN];
 #pragma unroll
-    for (int w = 0; w < 16; ++w) mw[w] = mlp[((w < nw ? w : 0) * 16 + icol) * 2];
+    for (int w = 0; w < MWN; ++w) mw[w] = mlp[((w < nwa ? w : 0) * 16 + icol) * 2];
 #pragma unroll
-    for (int w = 0; w < 16; ++w)
-      if (w < nw) M = fmaxf(M, mw[w]);
+    for (int w = 0; w < MWN; ++w)
+      if (w < nwa) M = fmaxf(M, mw[w]);
     const float Mref = M == -INFINITY ? 0.f : M;
-    for (int base = 0; base < nw; base += 8) {  // <= 2 passes (G <= 16)
-      float lw[8];
-      f32x4 v0[8], v1[8];
+    for (int base = 0; base < nwa; base += WP) {  // <= 2 passes (G <= 16)
+      float lw[WP];
+      f32x4 v0[WP], v1[WP];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int ww = base + i < nw ? base + i : base;  // clamped: surplus slots weighted 0 below
+      for (int i = 0; i < WP; ++i) {
+        const int ww = base + i < nwa ? base + i : base;  // clamped: surplus slots weighted 0 below
         lw[i] = mlp[(ww * 16 + icol) * 2 + 1];
         const float* row = opart + ww * (16 * D_) + icol * D_;
         v0[i] = *reinterpret_cast<const f32x4*>(row + 4 * ((d0 >> 2) ^ icol));
         v1[i] = *reinterpret_cast<const f32x4*>(row + 4 * (((d0 >> 2) + 1) ^ icol));
       }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < WP; ++i) {
         const int w = base + i;
         // a wave without tokens has l = 0 and m = -inf: weight exactly 0 (no 0 * inf)
         float mv = mw[0];
 #pragma unroll
-        for (int k = 1; k < 16; ++k)
+        for (int k = 1; k < MWN; ++k)
           if (k == w) mv = mw[k];
-        const float e = (w < nw && lw[i] > 0.f) ? __builtin_amdgcn_exp2f(mv - Mref) : 0.f;
+        const float e = (w < nwa && lw[i] > 0.f) ? __builtin_amdgcn_exp2f(mv - Mref) : 0.f;
         L += lw[i] * e;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -471,6 +478,10 @@ __device__ __forceinline__ void decode_block(const AttnArgs& a, int s, int h, in
         }
       }
     }
+  };
+  if (it < items) {
+    if (nwa <= 4) merge(std::integral_constant<int, 4>{});
+    else merge(std::integral_constant<int, 8>{});
   }
   const float inv = L > 0.f ? 1.f / L : 0.f;
   const int hq = h * G + icol;
