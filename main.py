@@ -29,10 +29,13 @@ def main() -> None:
     if config.server.http == "uvicorn":
         import uvicorn
         uvicorn.run(app, host=config.server.host, port=config.server.port, log_level="warning",
-                    access_log=False)
+                    access_log=False, timeout_keep_alive=config.server.timeout_keep_alive,
+                    limit_concurrency=config.server.max_connections or None)
         return
     from vgate.api.server import run
-    run(app, host=config.server.host, port=config.server.port)
+    sc = config.server
+    run(app, host=sc.host, port=sc.port, timeout_keep_alive=sc.timeout_keep_alive,
+        timeout_request=sc.timeout_request, max_connections=sc.max_connections)
 
 
 if __name__ == "__main__":

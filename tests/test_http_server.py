@@ -259,3 +259,262 @@ async def test_fast_lane_is_used():
     finally:
         fdu.solve_dependencies = orig
         fr.solve_dependencies = orig
+
+
+# ---------------------------------------------------------------------------------------------
+# front-end hardening: timeouts, connection cap, strict framing, HTTP/1.0, 100-continue
+# (what the reference's deployment, uvicorn + h11, gives; VERDICT r5 missing #1 / ADVICE r5)
+
+async def _raw_app(scope, receive, send):
+    """Tiny ASGI app for protocol tests: /slow sleeps, /echo returns the body length, /stream
+    sends two body parts without a content-length."""
+    if scope["type"] == "lifespan":
+        while True:
+            m = await receive()
+            if m["type"] == "lifespan.startup":
+                await send({"type": "lifespan.startup.complete"})
+            elif m["type"] == "lifespan.shutdown":
+                await send({"type": "lifespan.shutdown.complete"})
+                return
+    path = scope["path"]
+    body = (await receive())["body"]
+    if path == "/slow":
+        await asyncio.sleep(0.3)
+    if path == "/stream":
+        await send({"type": "http.response.start", "status": 200, "headers": [(b"content-type", b"text/plain")]})
+        await send({"type": "http.response.body", "body": b"part1 ", "more_body": True})
+        await send({"type": "http.response.body", "body": b"part2", "more_body": False})
+        return
+    out = b"%d" % len(body)
+    await send({"type": "http.response.start", "status": 200,
+                "headers": [(b"content-type", b"text/plain"), (b"content-length", b"%d" % len(out))]})
+    await send({"type": "http.response.body", "body": out})
+
+
+async def _serve_raw(fn, app=_raw_app, **kw):
+    srv = Server(app, "127.0.0.1", _free_port(), **kw)
+    task = asyncio.create_task(srv.serve())
+    while not srv.started:
+        assert not task.done(), task
+        await asyncio.sleep(0.01)
+    try:
+        return await fn(srv.port, srv)
+    finally:
+        srv.should_exit = True
+        await asyncio.wait_for(task, 10)
+
+
+async def _exchange(port, data: bytes, timeout=5.0, eof=False) -> bytes:
+    r, w = await asyncio.open_connection("127.0.0.1", port)
+    w.write(data)
+    if eof:
+        w.write_eof()
+    try:
+        return await asyncio.wait_for(r.read(), timeout)
+    finally:
+        w.close()
+
+
+async def test_idle_keepalive_connection_closed_and_client_redials():
+    async def go(port, srv):
+        r, w = await asyncio.open_connection("127.0.0.1", port)
+        w.write(b"GET /echo HTTP/1.1\r\nhost: x\r\n\r\n")
+        head = await asyncio.wait_for(r.readuntil(b"\r\n\r\n"), 5)
+        assert head.startswith(b"HTTP/1.1 200") and b"connection: close" not in head
+        assert await asyncio.wait_for(r.read(1), 5) == b"0"
+        t0 = asyncio.get_running_loop().time()
+        assert await asyncio.wait_for(r.read(), 5) == b""  # closed by the server, silently
+        assert 0.25 < asyncio.get_running_loop().time() - t0 < 2.0
+        w.close()
+        # the keep-alive client notices the stale pooled connection and redials
+        pool = Http1Pool("127.0.0.1", port)
+        assert (await pool.request("POST", "/echo", b"abc"))[2] == b"3"
+        await asyncio.sleep(0.7)
+        assert (await pool.request("POST", "/echo", b"abcd"))[2] == b"4"
+        await pool.close()
+    await _serve_raw(go, timeout_keep_alive=0.3)
+
+
+async def test_request_timeout_slow_head_and_body():
+    async def go(port, srv):
+        loop = asyncio.get_running_loop()
+        # partial head
+        t0 = loop.time()
+        data = await _exchange(port, b"GET /echo HTTP/1.1\r\nhost:")
+        assert data.startswith(b"HTTP/1.1 408") and b"connection: close" in data
+        assert loop.time() - t0 < 2.0
+        # slowloris: a byte every 50 ms does not extend the deadline
+        r, w = await asyncio.open_connection("127.0.0.1", port)
+        t0 = loop.time()
+        got = bytearray()
+
+        async def collect():
+            try:
+                while True:
+                    b = await r.read(4096)
+                    if not b:
+                        return
+                    got.extend(b)
+            except ConnectionError:
+                return
+        reader = asyncio.create_task(collect())
+        for ch in b"GET /echo HTTP/1.1\r\nx-a: " + b"a" * 200:
+            if reader.done() or got or loop.time() - t0 > 3:
+                break
+            w.write(bytes([ch]))
+            await asyncio.sleep(0.05)
+        await asyncio.wait_for(reader, 5)
+        w.close()
+        assert bytes(got).startswith(b"HTTP/1.1 408") and loop.time() - t0 < 2.5
+        # partial body
+        data = await _exchange(port, b"POST /echo HTTP/1.1\r\nhost: x\r\ncontent-length: 100\r\n\r\n0123456789")
+        assert data.startswith(b"HTTP/1.1 408")
+        # a complete request still works on the same server
+        data = await _exchange(port, b"POST /echo HTTP/1.1\r\nconnection: close\r\ncontent-length: 3\r\n\r\nabc")
+        assert data.startswith(b"HTTP/1.1 200") and data.endswith(b"\r\n\r\n3")
+    await _serve_raw(go, timeout_request=0.4, timeout_keep_alive=5)
+
+
+async def test_half_closed_partial_request_is_closed():
+    async def go(port, srv):
+        t0 = asyncio.get_running_loop().time()
+        data = await _exchange(port, b"POST /echo HTTP/1.1\r\ncontent-length: 50\r\n\r\nabc", eof=True)
+        assert data == b"" and asyncio.get_running_loop().time() - t0 < 1.0
+        # a complete request followed by EOF is answered, then closed
+        data = await _exchange(port, b"POST /echo HTTP/1.1\r\ncontent-length: 2\r\n\r\nab", eof=True)
+        assert data.startswith(b"HTTP/1.1 200") and data.endswith(b"2")
+        for _ in range(50):
+            if not srv.connections:
+                break
+            await asyncio.sleep(0.02)
+        assert not srv.connections
+    await _serve_raw(go, timeout_request=30, timeout_keep_alive=30)
+
+
+async def test_size_limits_413_431():
+    async def go(port, srv):
+        data = await _exchange(port, b"POST /echo HTTP/1.1\r\ncontent-length: 5000\r\n\r\n")
+        assert data.startswith(b"HTTP/1.1 413")
+        chunk = b"%x\r\n%s\r\n" % (3000, b"z" * 3000)
+        data = await _exchange(port, b"POST /echo HTTP/1.1\r\ntransfer-encoding: chunked\r\n\r\n" + chunk)
+        assert data.startswith(b"HTTP/1.1 413")
+        big = b"GET /echo HTTP/1.1\r\n" + b"".join(b"x-h%d: %s\r\n" % (i, b"v" * 100) for i in range(700))
+        data = await _exchange(port, big)  # > 64 KiB and no end of head
+        assert data.startswith(b"HTTP/1.1 431")
+        data = await _exchange(port, b"POST /echo HTTP/1.1\r\nconnection: close\r\ncontent-length: 1000\r\n\r\n" + b"q" * 1000)
+        assert data.startswith(b"HTTP/1.1 200") and data.endswith(b"1000")
+    await _serve_raw(go, max_body=1000)
+
+
+@pytest.mark.parametrize("head,code", [
+    (b"POST /echo HTTP/1.1\r\ncontent-length: 3\r\ncontent-length: 3\r\n\r\nabc", 400),
+    (b"POST /echo HTTP/1.1\r\ncontent-length: 3\r\ncontent-length: 5\r\n\r\nabcde", 400),
+    (b"POST /echo HTTP/1.1\r\ncontent-length: 3\r\ntransfer-encoding: chunked\r\n\r\n3\r\nabc\r\n0\r\n\r\n", 400),
+    (b"POST /echo HTTP/1.1\r\ntransfer-encoding: chunked\r\ncontent-length: 3\r\n\r\n3\r\nabc\r\n0\r\n\r\n", 400),
+    (b"POST /echo HTTP/1.1\r\ncontent-length: +3\r\n\r\nabc", 400),
+    (b"POST /echo HTTP/1.1\r\ncontent-length: 1_0\r\n\r\n0123456789", 400),
+    (b"POST /echo HTTP/1.1\r\ncontent-length : 3\r\n\r\nabc", 400),
+    (b"POST /echo HTTP/1.1\r\nx-a: 1\r\n folded\r\ncontent-length: 3\r\n\r\nabc", 400),
+    (b"POST /echo HTTP/1.1\r\ntransfer-encoding: gzip, chunked\r\n\r\n3\r\nabc\r\n0\r\n\r\n", 501),
+    (b"POST /echo HTTP/1.1\r\ntransfer-encoding: chunked\r\ntransfer-encoding: chunked\r\n\r\n0\r\n\r\n", 501),
+])
+async def test_strict_framing_rejects_ambiguous_requests(head, code):
+    async def go(port, srv):
+        data = await _exchange(port, head)
+        assert data.startswith(b"HTTP/1.1 %d" % code), data[:80]
+        assert b"connection: close" in data
+    await _serve_raw(go)
+
+
+async def test_connection_cap_503_retry_after():
+    async def go(port, srv):
+        held = []
+        for _ in range(4):
+            r, w = await asyncio.open_connection("127.0.0.1", port)
+            w.write(b"GET /echo HTTP/1.1\r\n\r\n")
+            await asyncio.wait_for(r.readuntil(b"\r\n\r\n0"), 5)
+            held.append((r, w))
+        data = await _exchange(port, b"GET /echo HTTP/1.1\r\n\r\n")
+        assert data.startswith(b"HTTP/1.1 503") and b"retry-after: 1\r\n" in data
+        held.pop()[1].close()
+        for _ in range(50):
+            if len(srv.connections) < 4:
+                break
+            await asyncio.sleep(0.02)
+        data = await _exchange(port, b"GET /echo HTTP/1.1\r\nconnection: close\r\n\r\n")
+        assert data.startswith(b"HTTP/1.1 200")
+        for _, w in held:
+            w.close()
+    await _serve_raw(go, max_connections=4)
+
+
+async def test_500_idle_connections_served_then_reaped():
+    async def go(port, srv):
+        conns = []
+        for _ in range(500):
+            conns.append(await asyncio.open_connection("127.0.0.1", port))
+        for r, w in conns:
+            w.write(b"GET /echo HTTP/1.1\r\n\r\n")
+        got = await asyncio.gather(*(asyncio.wait_for(r.readuntil(b"\r\n\r\n0"), 10) for r, _ in conns))
+        assert all(g.startswith(b"HTTP/1.1 200") for g in got)
+        assert len(srv.connections) >= 500
+        # a new client is served promptly while 500 sit idle
+        t0 = asyncio.get_running_loop().time()
+        data = await _exchange(port, b"POST /echo HTTP/1.1\r\nconnection: close\r\ncontent-length: 1\r\n\r\nx")
+        assert data.endswith(b"1") and asyncio.get_running_loop().time() - t0 < 1.0
+        # every idle one is closed by the server after the keep-alive timeout
+        ends = await asyncio.gather(*(asyncio.wait_for(r.read(), 10) for r, _ in conns))
+        assert all(e == b"" for e in ends)
+        for _, w in conns:
+            w.close()
+        for _ in range(100):
+            if not srv.connections:
+                break
+            await asyncio.sleep(0.02)
+        assert not srv.connections
+    await _serve_raw(go, timeout_keep_alive=1.0)
+
+
+async def test_pipelined_large_body_behind_slow_request():
+    """a >1 MiB body pipelined behind a slow request must not stall with reading paused."""
+    async def go(port, srv):
+        r, w = await asyncio.open_connection("127.0.0.1", port)
+        n = 3 * 2**20
+        w.write(b"GET /slow HTTP/1.1\r\n\r\nPOST /echo HTTP/1.1\r\nconnection: close\r\ncontent-length: %d\r\n\r\n" % n)
+        for i in range(0, n, 2**16):
+            w.write(b"b" * min(2**16, n - i))
+            await w.drain()
+        data = await asyncio.wait_for(r.read(), 10)
+        w.close()
+        assert data.count(b"HTTP/1.1 200") == 2 and data.endswith(b"%d" % n)
+    await _serve_raw(go)
+
+
+async def test_http10_keepalive_echo_and_unframed_stream():
+    async def go(port, srv):
+        r, w = await asyncio.open_connection("127.0.0.1", port)
+        w.write(b"GET /echo HTTP/1.0\r\nconnection: keep-alive\r\n\r\n")
+        head = await asyncio.wait_for(r.readuntil(b"\r\n\r\n"), 5)
+        assert b"connection: keep-alive" in head
+        assert await r.readexactly(1) == b"0"
+        w.write(b"GET /stream HTTP/1.0\r\nconnection: keep-alive\r\n\r\n")
+        data = await asyncio.wait_for(r.read(), 5)  # no chunked coding for 1.0: the close ends the body
+        w.close()
+        assert b"transfer-encoding" not in data and b"connection: close" in data
+        assert data.endswith(b"\r\n\r\npart1 part2")
+        data = await _exchange(port, b"GET /stream HTTP/1.1\r\nconnection: close\r\n\r\n")
+        assert b"transfer-encoding: chunked" in data
+    await _serve_raw(go)
+
+
+async def test_expect_100_continue_chunked():
+    async def go(port, srv):
+        r, w = await asyncio.open_connection("127.0.0.1", port)
+        w.write(b"POST /echo HTTP/1.1\r\nexpect: 100-continue\r\ntransfer-encoding: chunked\r\nconnection: close\r\n\r\n")
+        interim = await asyncio.wait_for(r.readuntil(b"\r\n\r\n"), 5)
+        assert interim == b"HTTP/1.1 100 Continue\r\n\r\n"
+        w.write(b"4\r\nabcd\r\n0\r\n\r\n")
+        data = await asyncio.wait_for(r.read(), 5)
+        w.close()
+        assert data.startswith(b"HTTP/1.1 200") and data.endswith(b"4")
+    await _serve_raw(go)

@@ -12,10 +12,22 @@ This is an ``asyncio.Protocol`` per connection:
 * request head parsed with ``bytes.find``/``split`` (request line + ``name: value`` lines,
   names lower-cased as ASGI wants), bodies by ``Content-Length`` or ``chunked``,
   ``Expect: 100-continue`` answered, head/body size limits (431 / 413), 400 on garbage;
+* strict framing (request smuggling): duplicate ``Content-Length``, a non-digit length,
+  ``Content-Length`` together with ``Transfer-Encoding``, whitespace before a header colon and
+  obsolete line folding are 400; a transfer coding other than ``chunked`` is 501;
 * keep-alive and pipelining (requests of one connection run one after another),
-  ``Connection: close`` honoured both ways, HTTP/1.0 closes after the response;
+  ``Connection: close`` honoured both ways, HTTP/1.0 closes after the response unless it asked
+  for keep-alive (echoed back);
+* timeouts and limits (what ``uvicorn main:app``, the reference's deployment, gives): an idle
+  keep-alive connection is closed after ``timeout_keep_alive`` seconds (5); a request whose head
+  and body are not complete ``timeout_request`` seconds after its first byte gets 408 and the
+  connection closes (slow / partial heads and bodies, half-closed clients); above
+  ``max_connections`` open connections a new connection's first request gets 503 +
+  ``Retry-After`` and is closed. One server-wide sweeper task checks the deadlines, so the
+  per-request cost is a timestamp;
 * responses: the app's headers are written as given; without ``content-length`` the body is
-  sent ``Transfer-Encoding: chunked`` (SSE streams), HEAD sends no body;
+  sent ``Transfer-Encoding: chunked`` (SSE streams) to HTTP/1.1 clients, unframed + close to
+  HTTP/1.0 clients; HEAD sends no body;
 * ``receive()`` returns the whole body once, then blocks until the client disconnects or the
   response is complete (``http.disconnect``) — what Starlette's streaming responses listen
   for; writes pause on transport back-pressure;
@@ -56,9 +68,12 @@ def _status_line(code: int) -> bytes:
     return line
 
 
-def _plain(code: int, text: bytes, close: bool = True) -> bytes:
-    return (_status_line(code) + b"content-type: text/plain; charset=utf-8\r\ncontent-length: %d\r\n%s\r\n"
-            % (len(text), b"connection: close\r\n" if close else b"") + text)
+def _plain(code: int, text: bytes, close: bool = True, extra: bytes = b"") -> bytes:
+    return (_status_line(code) + b"content-type: text/plain; charset=utf-8\r\ncontent-length: %d\r\n%s%s\r\n"
+            % (len(text), extra, b"connection: close\r\n" if close else b"") + text)
+
+
+_WS = b" \t"
 
 
 class _BadRequest(Exception):
@@ -71,7 +86,7 @@ class _Cycle:
     """One request/response exchange on a connection."""
 
     __slots__ = ("proto", "scope", "body", "body_sent", "started", "complete", "chunked", "head",
-                 "keep_alive", "disconnect_waiter")
+                 "keep_alive", "disconnect_waiter", "http10")
 
     def __init__(self, proto: "HttpProtocol", scope: dict, body: bytes, keep_alive: bool):
         self.proto = proto
@@ -84,6 +99,7 @@ class _Cycle:
         self.head = scope["method"] == "HEAD"
         self.keep_alive = keep_alive
         self.disconnect_waiter: Optional[asyncio.Future] = None
+        self.http10 = scope["http_version"] == "1.0"
 
     async def receive(self) -> dict:
         if not self.body_sent:
@@ -116,10 +132,15 @@ class _Cycle:
                     continue  # the framing is ours
                 parts.append(name + b": " + value + b"\r\n")
             if not has_len and not self.head and status >= 200 and status not in (204, 304):
-                self.chunked = True
-                parts.append(b"transfer-encoding: chunked\r\n")
+                if self.http10:
+                    self.keep_alive = False  # no chunked coding for 1.0: the close ends the body
+                else:
+                    self.chunked = True
+                    parts.append(b"transfer-encoding: chunked\r\n")
             if not self.keep_alive:
                 parts.append(b"connection: close\r\n")
+            elif self.http10:
+                parts.append(b"connection: keep-alive\r\n")
             parts.append(b"\r\n")
             if proto.closed:
                 return
@@ -172,11 +193,19 @@ class HttpProtocol(asyncio.Protocol):
         self.sockname = None
         self._continued = False
         self.eof = False
+        self.read_paused = False
+        self.reject = False
+        self.since = 0.0  # when the connection last became idle, or its pending request began
 
     # ------------------------------------------------------------------ transport events
     def connection_made(self, transport):
         self.transport = transport
-        self.server.connections.add(self)
+        srv = self.server
+        srv.connections.add(self)
+        self.since = self.loop.time()
+        if srv.max_connections and len(srv.connections) > srv.max_connections:
+            self.reject = True  # answered 503 once its first head is in (a reply before the
+            # request risks a reset that discards it at the client)
         sock = transport.get_extra_info("socket")
         if sock is not None:
             try:
@@ -216,16 +245,22 @@ class HttpProtocol(asyncio.Protocol):
             await w
 
     def data_received(self, data: bytes):
-        self.buf += data
         if self.task is None:
+            if not self.buf:
+                self.since = self.loop.time()  # a new request's first bytes: its read deadline
+            self.buf += data
             self._next()
-        elif len(self.buf) > self.server.max_pending:
-            self.transport.pause_reading()  # a pipelining client ran far ahead: wait for the app
+        else:
+            self.buf += data
+            if len(self.buf) > self.server.max_pending and not self.read_paused:
+                self.read_paused = True  # a pipelining client ran far ahead: wait for the app
+                self.transport.pause_reading()
 
     def eof_received(self):
-        # the client half-closed: answer what is in flight, then close
+        # the client half-closed: answer what is in flight, then close. A partial request with
+        # no task can never complete now: close at once
         self.eof = True
-        if self.task is None and not self.buf:
+        if self.task is None:
             return False
         return True
 
@@ -245,10 +280,18 @@ class HttpProtocol(asyncio.Protocol):
         except _BadRequest as e:
             self._fail(e.code, e.text)
             return
+        if self.reject:
+            self.transport.write(_plain(503, b"Too many connections", extra=b"retry-after: 1\r\n"))
+            self.transport.close()
+            self.closed = True
+            return
         start = end + 4
         if chunked:
             got = self._dechunk(start)
             if got is None:
+                if expect and not self._continued and not self.closed:
+                    self._continued = True
+                    self.transport.write(b"HTTP/1.1 100 Continue\r\n\r\n")
                 return
             body, consumed = got
         else:
@@ -313,25 +356,28 @@ class HttpProtocol(asyncio.Protocol):
         else:
             raise _BadRequest(400, b"Unsupported HTTP version")
         headers = []
-        length = 0
+        length = -1
         chunked = False
         expect = False
         for line in lines[1:]:
             i = line.find(b":")
-            if i <= 0:
+            if i <= 0 or line[0] in _WS or line[i - 1] in _WS:
+                # no name, obsolete line folding, or whitespace before the colon (RFC 9112 5.1:
+                # a proxy in front may read such a line differently -> request smuggling)
                 raise _BadRequest(400, b"Invalid header line")
-            name = line[:i].strip().lower()
+            name = line[:i].lower()
             value = line[i + 1:].strip()
             headers.append((name, value))
             if name == b"content-length":
-                try:
-                    length = int(value)
-                except ValueError:
-                    raise _BadRequest(400, b"Invalid Content-Length") from None
-                if length < 0:
+                if length >= 0:
+                    raise _BadRequest(400, b"Duplicate Content-Length")
+                if not value.isdigit():
                     raise _BadRequest(400, b"Invalid Content-Length")
+                length = int(value)
             elif name == b"transfer-encoding":
-                chunked = b"chunked" in value.lower()
+                if chunked or value.lower() != b"chunked":
+                    raise _BadRequest(501, b"Unsupported Transfer-Encoding")
+                chunked = True
             elif name == b"connection":
                 v = value.lower()
                 if b"close" in v:
@@ -352,7 +398,9 @@ class HttpProtocol(asyncio.Protocol):
                  "client": self.client, "scheme": "http", "method": method.decode("latin-1"), "root_path": "",
                  "path": path, "raw_path": raw_path, "query_string": query, "headers": headers,
                  "state": self.server.state.copy()}
-        return scope, length, chunked, keep_alive, expect
+        if chunked and length >= 0:
+            raise _BadRequest(400, b"Content-Length with Transfer-Encoding")
+        return scope, max(length, 0), chunked, keep_alive, expect
 
     def _fail(self, code: int, text: bytes) -> None:
         if not self.closed:
@@ -392,10 +440,33 @@ class HttpProtocol(asyncio.Protocol):
             self.transport.close()
             self.closed = True
             return
-        if len(self.buf) <= self.server.max_pending:
+        self.since = self.loop.time()
+        if self.read_paused:
+            # always resume: a request bigger than max_pending may be half-read in the buffer,
+            # and _next can only start it once the rest arrives (re-paused below if another
+            # request starts while the buffer is still over the bound)
+            self.read_paused = False
             self.transport.resume_reading()
         if self.buf:
             self._next()
+            if self.task is not None and len(self.buf) > self.server.max_pending:
+                self.read_paused = True
+                self.transport.pause_reading()
+        if self.eof and self.task is None and not self.closed:
+            self.transport.close()  # half-closed: a partial request can never complete
+            self.closed = True
+
+    def check_deadline(self, now: float, keep_alive: float, request: float) -> None:
+        """Called by the server's sweeper: close an idle keep-alive connection, or answer 408 to
+        a request that has not arrived in full ``request`` seconds after its first byte."""
+        if self.task is not None or self.closed:
+            return
+        if not self.buf:
+            if keep_alive and now - self.since > keep_alive:
+                self.transport.close()
+                self.closed = True
+        elif request and now - self.since > request:
+            self._fail(408, b"Request Timeout")
 
     def shutdown_idle(self) -> None:
         if self.task is None and not self.closed:
@@ -411,8 +482,13 @@ class Server:
 
     def __init__(self, app: Callable, host: str = "127.0.0.1", port: int = 8000, lifespan: str = "on",
                  install_signal_handlers: bool = False, timeout_graceful_shutdown: float = 30.0,
-                 backlog: int = 2048, max_body: int = 64 * 2**20):
+                 backlog: int = 2048, max_body: int = 64 * 2**20, timeout_keep_alive: float = 5.0,
+                 timeout_request: float = 30.0, max_connections: int = 4096):
         self.app = app
+        self.timeout_keep_alive = timeout_keep_alive
+        self.timeout_request = timeout_request
+        self.max_connections = max_connections
+        self._sweeper: Optional[asyncio.Task] = None
         self.host = host
         self.port = port
         self.lifespan = lifespan
@@ -487,7 +563,19 @@ class Server:
         self.sockets = list(self._server.sockets or [])
         if self.port == 0 and self.sockets:
             self.port = self.sockets[0].getsockname()[1]
+        if self.timeout_keep_alive or self.timeout_request:
+            self._sweeper = self.loop.create_task(self._sweep())
         self.started = True
+
+    async def _sweep(self) -> None:
+        ts = [t for t in (self.timeout_keep_alive, self.timeout_request) if t]
+        period = min(1.0, max(0.02, min(ts) / 4))
+        ka, rq = self.timeout_keep_alive, self.timeout_request
+        while True:
+            await asyncio.sleep(period)
+            now = self.loop.time()
+            for c in list(self.connections):
+                c.check_deadline(now, ka, rq)
 
     async def serve(self) -> None:
         restore = self._install_signals()
@@ -504,6 +592,8 @@ class Server:
             restore()
 
     async def shutdown(self) -> None:
+        if self._sweeper is not None:
+            self._sweeper.cancel()
         if self._server is not None:
             self._server.close()
         for c in list(self.connections):

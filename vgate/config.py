@@ -37,6 +37,13 @@ class ServerConfig(_Section):
     # HTTP front end of ``python main.py``: "vgate" (vgate.api.server, lean HTTP/1.1) or
     # "uvicorn" (h11). ``uvicorn main:app`` works either way: the app is plain ASGI.
     http: str = "vgate"
+    # front-end limits (both servers): idle keep-alive connections close after this many seconds
+    # (uvicorn's default, what the reference deploys); a request whose head + body are not in
+    # ``timeout_request`` s after its first byte gets 408; above ``max_connections`` open
+    # connections a request gets 503 + Retry-After (uvicorn: limit_concurrency). 0 = off.
+    timeout_keep_alive: float = 5.0
+    timeout_request: float = 30.0
+    max_connections: int = 4096
 
 
 class WorkerDiscoveryConfig(_Section):

@@ -154,27 +154,38 @@ class Http1Pool:
 
     async def request(self, method: str, path: str, body: bytes = b"",
                       content_type: str = "application/json") -> tuple[int, dict, bytes]:
-        conn = None
-        while self._idle:
-            c = self._idle.pop()
-            if not c.closed:
-                conn = c
-                break
-        if conn is None:
-            conn = await self._dial()
         head = b"%s %s HTTP/1.1\r\n%scontent-type: %s\r\ncontent-length: %d\r\n\r\n" % (
             method.encode(), path.encode(), self._fixed, content_type.encode(), len(body))
-        fut = conn.start(head + body, head_only=method == "HEAD")
-        timer = conn.loop.call_later(self.timeout, _expire, fut) if self.timeout else None
-        try:
-            status, headers, data = await fut
-        except BaseException:
-            conn.transport.close()
-            self._all.discard(conn)
-            raise
-        finally:
-            if timer is not None:
-                timer.cancel()
+        while True:
+            conn = None
+            while self._idle:
+                c = self._idle.pop()
+                if not c.closed:
+                    conn = c
+                    break
+            reused = conn is not None
+            if conn is None:
+                conn = await self._dial()
+            fut = conn.start(head + body, head_only=method == "HEAD")
+            timer = conn.loop.call_later(self.timeout, _expire, fut) if self.timeout else None
+            try:
+                status, headers, data = await fut
+            except HttpError:
+                conn.transport.close()
+                self._all.discard(conn)
+                if reused and conn.closed and not conn.buf:
+                    # the server closed this idle keep-alive connection (its idle timeout) as the
+                    # request went out: nothing was answered, so nothing ran. Retry on a new one
+                    continue
+                raise
+            except BaseException:
+                conn.transport.close()
+                self._all.discard(conn)
+                raise
+            finally:
+                if timer is not None:
+                    timer.cancel()
+            break
         if conn.keep_alive and not conn.closed:
             self._idle.append(conn)
         else:
