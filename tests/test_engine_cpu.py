@@ -248,3 +248,56 @@ def test_idle_admission_window_only_waits_for_an_expected_wave():
     finally:
         eng._running = False
     eng.run_until_idle()
+
+
+def test_kernel_fault_is_recovered_then_bounded():
+    """A kernel hand-off fault (sticky fault word) fails the step's requests, resets the hand-off
+    buffers and the prefix cache, and the engine keeps serving; more than fault_recoveries_max
+    faults inside fault_window_s leave it unhealthy (VERDICT r5 weak #9)."""
+    import threading
+
+    from vgate import ops
+    from vgate.runtime.engine import KernelHandoffFault
+    eng = make_engine(enable_prefix_caching=True)
+    real_check = eng._check_collectives
+    inject = {"n": 0}
+
+    def check():
+        if inject["n"]:
+            inject["n"] -= 1
+            raise KernelHandoffFault("injected fault word 0x20")
+        real_check()
+    eng._check_collectives = check
+    done, ev = {}, threading.Event()
+
+    def cb(kind, seq, payload):
+        if kind in ("finish", "error"):
+            done[seq.request_id] = (kind, list(seq.output_ids))
+            ev.set()
+    sp = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
+    prompt = list(range(3, 40))
+    want = greedy_reference(eng.model, prompt, 6)
+    qa = ops.qa_sync(eng.device)
+    eng.start()
+    try:
+        for i in range(eng.fault_recoveries_max):
+            qa[:8] = 7  # a stale granule a give-up can leave behind
+            inject["n"] = 1
+            ev.clear()
+            eng.add_request(f"bad{i}", params=sp, callback=cb, prompt_ids=prompt)
+            assert ev.wait(30)
+            assert done[f"bad{i}"][0] == "error" and eng.healthy
+            assert int(qa[:8].abs().sum()) == 0
+            ev.clear()
+            eng.add_request(f"ok{i}", params=sp, callback=cb, prompt_ids=prompt)
+            assert ev.wait(30)
+            assert done[f"ok{i}"] == ("finish", want)
+        assert eng.stats.fault_recoveries == eng.fault_recoveries_max
+        assert eng.snapshot()["fault_recoveries"] == eng.fault_recoveries_max
+        inject["n"] = 1  # one more inside the window: unhealthy
+        ev.clear()
+        eng.add_request("last", params=sp, callback=cb, prompt_ids=prompt)
+        assert ev.wait(30)
+        assert done["last"][0] == "error" and not eng.healthy
+    finally:
+        eng.stop()

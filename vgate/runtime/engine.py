@@ -40,6 +40,11 @@ from vgate.utils.profiling import range_
 log = logging.getLogger("vgate.engine")
 
 
+class KernelHandoffFault(RuntimeError):
+    """An in-launch hand-off of a step gave up waiting (ops.fault_word): that step's results are
+    invalid, but the engine can reset the hand-off state and go on (LLMEngine._recover_fault)."""
+
+
 @dataclass
 class EngineConfig:
     model: str = "Qwen/Qwen2.5-1.5B-Instruct"
@@ -122,6 +127,7 @@ class EngineStats:
     max_cycle_ms: float = 0.0  # slowest schedule -> launch -> collect cycle and its (T, S) bucket
     max_cycle_bucket: tuple = (0, 0)
     batch_sizes: collections.Counter = field(default_factory=collections.Counter)
+    fault_recoveries: int = 0  # kernel hand-off faults the engine recovered from (LLMEngine._recover_fault)
     idle_s: float = 0.0        # engine thread waiting for work (no step in flight, nothing queued)
     prefill_steps: int = 0     # steps that carried prompt tokens (mixed or prefill-only)
     # idle -> busy transitions (engine._wave_account): sums of the three boundary phases
@@ -219,6 +225,9 @@ class LLMEngine:
         self._finish_times: collections.deque = collections.deque(maxlen=64)  # idle admission window
         self._calls: collections.deque = collections.deque()  # (fn, future) run on the engine thread
         self.last_error: str | None = None
+        self._fault_times: collections.deque = collections.deque()
+        self.fault_recoveries_max = 3
+        self.fault_window_s = 300.0
         self.last_step_wall = time.monotonic()
         log.info("engine ready: model=%s params=%.2fB weights=%.2f GB load=%.1fs kv_blocks=%d (%.1fk tokens) device=%s tp=%d",
                  self.arch.name, self.arch.num_params() / 1e9, self.model.weight_bytes() / 1e9, self.load_seconds,
@@ -427,10 +436,14 @@ class LLMEngine:
             except Exception as e:  # noqa: BLE001 - engine faults fail every in-flight request
                 log.exception("engine step failed")
                 self._inflight = None
-                self.healthy = False
                 self.last_error = f"{type(e).__name__}: {e}"
-                for seq in list(self.scheduler.running) + list(self.scheduler.waiting):
+                failed = list(self.scheduler.running) + list(self.scheduler.waiting)
+                for seq in failed:
                     self.scheduler.remove(seq)
+                # recover (or go unhealthy) before any client hears of the failure
+                if not (isinstance(e, KernelHandoffFault) and self._recover_fault()):
+                    self.healthy = False
+                for seq in failed:
                     self._finish(seq, "error", notify_sched=False, error=self.last_error)
         self.shutdown_followers()
 
@@ -687,8 +700,8 @@ class LLMEngine:
         blocking hipMemcpy of ``ar.check()`` serialised rank 0 with its in-flight step)."""
         fault = self.runner.kernel_fault() if self.runner.gpu else 0
         if fault:
-            raise RuntimeError(f"an in-launch kernel hand-off gave up waiting (fault word {fault:#x}); "
-                               "the step's results are invalid")
+            raise KernelHandoffFault(f"an in-launch kernel hand-off gave up waiting (fault word {fault:#x}); "
+                                     "the step's results are invalid")
         ar = self.tp.custom_ar
         if ar is None:
             return
@@ -705,6 +718,35 @@ class LLMEngine:
         if self._steps_since_check >= self._ar_check_every:
             self._steps_since_check = 0
             ar.check()
+
+    def _recover_fault(self) -> bool:
+        """A kernel hand-off gave up (sticky fault word): the step's requests were failed; reset the
+        hand-off state and keep serving instead of going unhealthy for good. One process, one GPU
+        only (a TP group is one failure domain: its ranks' streams cannot be reset in lock-step).
+        The prefix cache is dropped too: a faulted step may have written wrong K / V into blocks
+        it published. More than ``fault_recoveries_max`` faults inside ``fault_window_s``: the
+        engine goes unhealthy (something persistent is wrong; an external restart is the fix)."""
+        if self.tp.size > 1:
+            return False
+        now = time.monotonic()
+        hist = self._fault_times
+        while hist and now - hist[0] > self.fault_window_s:
+            hist.popleft()
+        if len(hist) >= self.fault_recoveries_max:
+            log.error("%d kernel faults within %.0f s: engine marked unhealthy", len(hist) + 1, self.fault_window_s)
+            return False
+        hist.append(now)
+        try:
+            ops.reset_handoffs(self.device)
+            self.runner.reset_fault_ring()
+            self.kvm.alloc.reset_prefix_cache()
+        except Exception:  # noqa: BLE001
+            log.exception("kernel fault recovery failed")
+            return False
+        self.stats.fault_recoveries += 1
+        log.warning("kernel hand-off fault recovered (%d in the last %.0f s): hand-off buffers reset, "
+                    "prefix cache dropped, in-flight requests failed", len(hist), self.fault_window_s)
+        return True
 
     def follower_loop(self) -> None:
         """TP ranks > 0: execute whatever rank 0 publishes on the step ring, until it stops."""
@@ -786,7 +828,7 @@ class LLMEngine:
             "max_cycle_ms": round(st.max_cycle_ms, 3),
             "max_cycle_tokens_seqs": list(st.max_cycle_bucket),
             "preemptions": self.scheduler.num_preemptions, "prefix_cache_hits": int(getattr(self.kvm.alloc, "hits", 0)),
-            "healthy": self.healthy,
+            "healthy": self.healthy, "fault_recoveries": st.fault_recoveries,
             "tp_custom_collectives": int(self.tp.custom_ar is not None), "tp_self_check": self.tp_self_check,
             "waves": st.waves, "wave_sum_ms": [round(1e3 * st.wave_first_s, 3), round(1e3 * st.wave_spread_s, 3),
                                                 round(1e3 * st.wave_tail_s, 3)], "wave_requests": st.wave_size,

@@ -353,6 +353,12 @@ class ModelRunner:
             k = self._last_collected if self._last_collected is not None else self._k ^ 1
         return int(self.out_ring[k][-1])
 
+    def reset_fault_ring(self) -> None:
+        """After the engine's fault recovery (ops.reset_handoffs, device idle): clear the fault
+        word copies in both ring slots, so the next check reads the new steps' words."""
+        if self.gpu:
+            self.out_ring[:, -1].zero_()
+
     def collective_words(self, k: int | None = None) -> tuple[int, float, int]:
         """(error, seconds, calls) of the custom all-reduce since the previous call, from the words
         the step graph's last node copied into ring slot ``k`` (default: the last launched one).
