@@ -115,7 +115,8 @@ def engine_model_cfg(args, rank: int, local: int) -> dict:
             "device": f"cuda:{local}" if torch.cuda.device_count() > 0 else "cpu",
             # every rank of a TP group uses the same seed (one replica); replicas differ
             "seed": 1234 + rank // args.tp, "tensor_parallel_size": args.tp,
-            "engine_process": bool(args.engine_process) and args.tp == 1}
+            "engine_process": bool(args.engine_process) and args.tp == 1,
+            **({"idle_batch_window_ms": args.idle_window_ms} if args.idle_window_ms is not None else {})}
 
 
 async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=None, group=None):
@@ -194,7 +195,6 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
     inner = getattr(eng.backend, "engine", None)
     if hasattr(inner, "reset_peaks"):
         inner.reset_peaks()
-    snap0 = eng.backend.stats() if hasattr(eng.backend, "stats") else {}
     barrier()
     # server event-loop lag during the timed region (a stalled loop delays every response)
     lag = {"max_ms": 0.0, "at_s": 0.0}
@@ -221,6 +221,7 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
         import cProfile
         prof = cProfile.Profile()
         prof.enable()
+    snap0 = eng.backend.stats() if hasattr(eng.backend, "stats") else {}
     t0 = time.perf_counter()
     mon = asyncio.create_task(lag_monitor(t0))
     lat, fails, tokens, _, starts = await load(per_step * args.steps, 0)
@@ -236,9 +237,17 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
     # timed-region forensics (p99): eager (graph-miss) steps and captures INSIDE the timed region
     snap = dict(snap)
     for k in ("graph_misses_eager", "graph_captures", "steps", "graph_hits", "idle_ms", "prefill_steps", "waves",
-              "wave_requests"):
+              "wave_requests", "coalesce_ms", "busy_ms", "collect_wait_ms", "sum_step_ms", "sum_cycle_ms",
+              "sum_gpu_ms", "gpu_steps"):
         if k in snap and k in snap0:
             snap[f"timed_{k}"] = snap[k] - snap0[k]
+    # per-step averages over the timed region only (the snapshot's avg_* are since boot, warm-up
+    # and captures included): the engine's busy time per step, the device time of the timed steps
+    ts = snap.get("timed_steps") or 0
+    if ts and "timed_busy_ms" in snap:
+        snap["timed_avg_step_ms"] = round(snap["timed_busy_ms"] / ts, 3)
+        snap["timed_avg_cycle_ms"] = round(snap["timed_sum_cycle_ms"] / ts, 3)
+        snap["timed_avg_gpu_ms"] = round(snap["timed_sum_gpu_ms"] / max(1, snap["timed_gpu_steps"]), 3)
     if "wave_sum_ms" in snap and "wave_sum_ms" in snap0:
         nw = max(1, snap.get("timed_waves", 0))
         snap["wave_breakdown_ms"] = [round((a - b) / nw, 3) for a, b in zip(snap["wave_sum_ms"], snap0["wave_sum_ms"])]
@@ -287,6 +296,8 @@ def main():
     ap.add_argument("--quantization", default=None)
     ap.add_argument("--kv-blocks", type=int, default=4096)
     ap.add_argument("--eager", action="store_true")
+    ap.add_argument("--idle-window-ms", type=float, default=None,
+                    help="model.idle_batch_window_ms (0 = no idle admission window; default: config.yaml's)")
     ap.add_argument("--port", type=int, default=18100)
     ap.add_argument("--security", action="store_true", help="bearer auth + rate limiter on the request path")
     ap.add_argument("--engine-process", action="store_true",
@@ -382,9 +393,12 @@ def main():
             "mean_s": round(sum(lat) / max(1, len(lat)), 4),
             "generated_tokens_per_s": round(toks / wall, 1),
             "failures": sum(r["fails"] for r in allr),
-            "engine_avg_step_ms": allr[0]["engine"].get("avg_step_ms"),
-            "engine_avg_cycle_ms": allr[0]["engine"].get("avg_cycle_ms"),
-            "engine_avg_gpu_ms": allr[0]["engine"].get("avg_gpu_ms"),
+            # timed region only: engine busy time per step (schedule + launch + wait + process; with
+            # asynchronous scheduling the cycles of consecutive steps overlap, so avg_cycle can exceed
+            # it), the mean schedule -> processed cycle, the device time of the timed steps
+            "engine_avg_step_ms": allr[0]["engine"].get("timed_avg_step_ms"),
+            "engine_avg_cycle_ms": allr[0]["engine"].get("timed_avg_cycle_ms"),
+            "engine_avg_gpu_ms": allr[0]["engine"].get("timed_avg_gpu_ms"),
             "boot_s": round(max(r["boot_s"] for r in allr), 1),
             "max_s": round(max(lat), 4) if lat else 0.0,
             "timed_engine_steps": allr[0]["engine"].get("timed_steps"),
@@ -392,6 +406,15 @@ def main():
             # prompt tokens, over the timed region: at concurrency c the requests run in waves of c
             # that start together, so every wave boundary waits for the next c requests' HTTP path
             "timed_engine_idle_ms": allr[0]["engine"].get("timed_idle_ms"),
+            # the engine thread's timed wall time, split: idle (nothing to do) + coalesce (the idle
+            # admission window waiting for the rest of a wave) + busy (steps); accounted / wall
+            "timed_engine_coalesce_ms": allr[0]["engine"].get("timed_coalesce_ms"),
+            "timed_engine_busy_ms": allr[0]["engine"].get("timed_busy_ms"),
+            "timed_engine_collect_wait_ms": allr[0]["engine"].get("timed_collect_wait_ms"),
+            "timed_wall_ms": round(1e3 * allr[0]["wall"], 3),
+            "timed_wall_ms_accounted": (round(sum(allr[0]["engine"].get(k, 0.0) for k in
+                                                  ("timed_idle_ms", "timed_coalesce_ms", "timed_busy_ms")), 3)
+                                        if "timed_busy_ms" in allr[0]["engine"] else None),
             "timed_prefill_steps": allr[0]["engine"].get("timed_prefill_steps"),
             # per idle -> busy transition: [idle start -> first arrival, first -> last arrival of the
             # wave, last arrival -> step start] in ms, and the requests per transition

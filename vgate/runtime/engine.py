@@ -129,6 +129,11 @@ class EngineStats:
     batch_sizes: collections.Counter = field(default_factory=collections.Counter)
     fault_recoveries: int = 0  # kernel hand-off faults the engine recovered from (LLMEngine._recover_fault)
     idle_s: float = 0.0        # engine thread waiting for work (no step in flight, nothing queued)
+    # the engine thread's wall time splits into idle_s + coalesce_s + busy_s (+ captures / loop
+    # overhead): coalesce_s = the idle admission window waiting for the rest of a wave
+    # (_coalesce_arrivals), busy_s = inside step() / side calls (schedule, launch, collect, process)
+    coalesce_s: float = 0.0
+    busy_s: float = 0.0
     prefill_steps: int = 0     # steps that carried prompt tokens (mixed or prefill-only)
     # idle -> busy transitions (engine._wave_account): sums of the three boundary phases
     waves: int = 0
@@ -226,6 +231,7 @@ class LLMEngine:
         self._calls: collections.deque = collections.deque()  # (fn, future) run on the engine thread
         self.last_error: str | None = None
         self._fault_times: collections.deque = collections.deque()
+        self._idle_t: float | None = None  # start of the engine thread's current idle wait
         self.fault_recoveries_max = 3
         self.fault_window_s = 300.0
         self.last_step_wall = time.monotonic()
@@ -372,7 +378,7 @@ class LLMEngine:
             if len(self._inbox) == n:
                 break  # nobody arrived within the gap
             n = len(self._inbox)
-        self.stats.idle_s += time.perf_counter() - t0
+        self.stats.coalesce_s += time.perf_counter() - t0
 
     def _wave_account(self, t_idle0: float) -> None:
         """Break an idle -> busy transition into (idle start -> first arrival), (first -> last
@@ -416,10 +422,11 @@ class LLMEngine:
                 while self._running and self._idle() and not self.runner.pending_captures:
                     if self.ring is not None:  # an idle TP group must not look dead to its followers
                         self.ring.heartbeat()
-                    t_idle = time.perf_counter()
+                    t_idle = self._idle_t = time.perf_counter()
                     if t_idle0 is None:
                         t_idle0 = t_idle
                     self._cv.wait(timeout=0.5)
+                    self._idle_t = None
                     self.stats.idle_s += time.perf_counter() - t_idle
                 if self._idle():
                     continue  # idle with captures pending: back to the capture check
@@ -429,10 +436,12 @@ class LLMEngine:
                 if t_idle0 is not None and self._inbox:
                     self._wave_account(t_idle0)
                 self._drain_inbox()
+            t_busy = time.perf_counter()
             if self._calls:
                 self._run_calls()
             try:
                 self.step()
+                self.stats.busy_s += time.perf_counter() - t_busy
             except Exception as e:  # noqa: BLE001 - engine faults fail every in-flight request
                 log.exception("engine step failed")
                 self._inflight = None
@@ -806,6 +815,7 @@ class LLMEngine:
 
     def snapshot(self) -> dict:
         st = self.stats
+        t_idle = self._idle_t  # an idle wait in progress counts up to now
         return {
             "model": self.arch.name, "device": str(self.device), "tp": self.tp.size,
             "running": len(self.scheduler.running), "waiting": len(self.scheduler.waiting),
@@ -816,7 +826,15 @@ class LLMEngine:
             "avg_cycle_ms": round(1e3 * st.cycle_time_s / max(1, st.steps), 3),
             "avg_gpu_ms": round(self.runner.gpu_ms / max(1, self.runner.gpu_steps), 3),
             "avg_host_ms": round(self.runner.host_ms / max(1, st.steps), 3),
-            "idle_ms": round(1e3 * st.idle_s, 3), "prefill_steps": st.prefill_steps,
+            "idle_ms": round(1e3 * (st.idle_s + (time.perf_counter() - t_idle if t_idle is not None else 0.0)), 3),
+            "prefill_steps": st.prefill_steps,
+            # raw cumulative sums (bench.py differences them over its timed region): the engine
+            # thread's wall = idle + coalesce + busy (+ deferred captures); collect_wait = busy time
+            # blocked on the device; gpu = device time of the timed steps (every 8th)
+            "coalesce_ms": round(1e3 * st.coalesce_s, 3), "busy_ms": round(1e3 * st.busy_s, 3),
+            "collect_wait_ms": round(self.runner.collect_wait_ms, 3),
+            "sum_step_ms": round(1e3 * st.step_time_s, 3), "sum_cycle_ms": round(1e3 * st.cycle_time_s, 3),
+            "sum_gpu_ms": round(self.runner.gpu_ms, 3), "gpu_steps": self.runner.gpu_steps,
             "graphs_captured": len(self.runner.graphs), "graph_hits": self.runner.graph_hits,
             "graph_misses_eager": self.runner.graph_misses,
             "pending_captures": len(self.runner.pending_captures),

@@ -114,6 +114,7 @@ class ModelRunner:
         self.gpu_ms = 0.0  # device time of every 8th step (upload -> sampled ids on host)
         self.host_ms = 0.0  # host time of execute() outside the device wait
         self.gpu_steps = 0
+        self.collect_wait_ms = 0.0  # host time blocked in collect() waiting for a step's device work
         self.captures = 0  # hipGraph captures so far (start-up warm-up + deferred + on-miss)
         self.max_gpu_ms = 0.0  # slowest step's device time and its bucket (p99 forensics)
         self.max_gpu_bucket = (0, 0)
@@ -330,7 +331,9 @@ class ModelRunner:
         """Wait for a launched step and return its sampled ids (one per batch item)."""
         if h.toks is not None:
             return h.toks
+        t_wait = time.perf_counter()
         self.dones[h.k].synchronize()
+        self.collect_wait_ms += 1e3 * (time.perf_counter() - t_wait)
         if h.timed:
             ms = self.started[h.k].elapsed_time(self.dones[h.k])
             self.gpu_ms += ms
