@@ -34,7 +34,7 @@ PLANS: dict[tuple[int, int, str, str], tuple] = {
     (4096, 14336, "plain", "dense"): (4, 1, 1),
     # Qwen2.5-1.5B bf16 gate_up on the register-stationary kernel (one block per CU owning 4-5 whole
     # tiles, every weight fragment requested at once; csrc/kernels/gemm_kx.h): 10.5 vs 11.9 us per
-    # launch as the hand-off consumer, cold weights (benchmarks/dense_kx_sweep.py,
+    # launch as the hand-off consumer, cold weights (benchmarks/probes/dense_kx_sweep.py,
     # profiles/r5_dense_kx_sweep.log). qkv / o_proj / down_proj stay on the tile kernels there.
     (17920, 1536, "silu", "dense"): ("kx", 0, 0, 0),
     # Qwen2.5-1.5B AWQ int4: no entries — every int4 decode GEMM runs the register-stationary kernel
