@@ -25,10 +25,10 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _cfg(path, tp, timeout=120.0):
+def _cfg(path, tp, timeout=120.0, **kw):
     return EngineConfig(model=path, device="cpu", tensor_parallel_size=tp, max_model_len=256, max_num_seqs=8,
                         max_num_batched_tokens=64, num_kv_blocks=128, warmup=False, seed=0,
-                        tp_timeout_seconds=timeout)
+                        tp_timeout_seconds=timeout, **kw)
 
 
 def _generate(eng):
@@ -45,17 +45,33 @@ def _generate(eng):
     return done
 
 
-def _worker(rank, world, port, path, q, overlap_min=None, embed_ids=None):
+def _worker(rank, world, port, path, q, overlap_min=None, embed_ids=None, interval=None, inject=0.0):
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                           MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         if overlap_min is not None:  # row-chunked row-parallel GEMMs + per-chunk all-reduce
             from vgate.models import transformer
             transformer.TP_OVERLAP_MIN_TOKENS, transformer.TP_OVERLAP_CHUNKS = overlap_min, 3
+        if inject:  # the last rank's all-reduce results are perturbed (run-time divergence guard)
+            from vgate.parallel import comm
+            comm._INJECT_DIVERGENCE = inject
         torch.set_num_threads(1)
-        eng = LLMEngine(_cfg(path, world))
+        eng = LLMEngine(_cfg(path, world, **({"tp_consistency_interval": interval} if interval else {})))
         assert eng.tp.size == world and eng.tp.rank == rank
         assert eng.model.num_heads_local * world == eng.arch.num_heads
+        if interval:
+            if rank == 0:
+                try:
+                    out = {"gen": _generate(eng), "error": None}
+                except Exception as e:  # noqa: BLE001 - the guard fails the step
+                    out = {"gen": None, "error": f"{type(e).__name__}: {e}"}
+                out.update(healthy=eng.healthy, state=eng.tp_consistency, checks=eng.tp_consistency_checks)
+                eng.shutdown_followers()
+                q.put(("ok", out))
+            else:
+                eng.follower_loop()
+                q.put(("ok", None) if eng.tp_consistency_checks > 0 else ("err", "follower ran no check"))
+            return
         if rank == 0:
             out = _generate(eng)
             if embed_ids is not None:  # the followers run the same hidden-states forward
@@ -294,3 +310,23 @@ def test_decode_plan_table_applies_to_matching_shapes():
     assert decode_plans.apply(m) == 5
     assert (L.gate_up.dec_waves, L.gate_up.dec_splitk) == (4, 1) and L.qkv.dec_splitk == 3
     assert all(getattr(other, k).dec_waves == 0 for k in ("qkv", "o", "gate_up", "down"))
+
+
+@pytest.mark.timeout(300)
+def test_tp_runtime_consistency_guard(tmp_path):
+    """Run-time divergence guard: every 2nd step the ranks compare checksums of
+    their replicated logits. Clean: tokens == TP = 1 and the checks ran on every rank. With the
+    last rank's all-reduce results perturbed (as if it read a peer's partial stale): the first
+    check fails the step, marks rank 0 unhealthy with the reason, on every rank."""
+    ref_eng = LLMEngine(EngineConfig(model="tiny", device="cpu", max_model_len=256, max_num_seqs=8,
+                                     max_num_batched_tokens=64, num_kv_blocks=128, warmup=False, seed=0))
+    path = str(tmp_path / "ckpt")
+    save_checkpoint(ref_eng.model, path)
+    ref = _generate(LLMEngine(_cfg(path, 1)))
+    clean = _run_group(2, path, interval=2)
+    assert clean["error"] is None and clean["gen"] == ref
+    assert clean["healthy"] and clean["state"] == "ok" and clean["checks"] >= 3
+    bad = _run_group(2, path, interval=2, inject=0.25)
+    assert bad["error"] is not None and bad["error"].startswith("TPDivergence"), bad
+    assert not bad["healthy"] and "diverged" in bad["state"] and "ranks [1]" in bad["state"]
+    assert bad["checks"] == 1

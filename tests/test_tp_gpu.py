@@ -338,3 +338,73 @@ def test_tp2_peer_stops_custom_allreduce_times_out_and_engine_fails(tmp_path):
             p.join(timeout=60)
             if p.is_alive():
                 p.kill()
+
+
+def _guard_worker(rank, port, path, q, runs):
+    """TP = 2 on the one GPU; per run (fused, inject): a consistency-checked generation. Rank 0
+    reports (tokens or None, error, healthy, state, checks, custom collectives left on)."""
+    try:
+        os.environ.update(RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(port))
+        import torch.distributed as dist
+
+        from vgate.parallel import comm
+        from vgate.runtime.engine import LLMEngine
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=2)
+        res = []
+        for fused, inject in runs:
+            comm._INJECT_DIVERGENCE = inject
+            eng = LLMEngine(_cfg(path, 2, tp_fused_allreduce=fused, tp_consistency_interval=2))
+            eng.runner.defer_capture = False
+            if rank == 0:
+                try:
+                    out, err = _generate(eng), None
+                except Exception as e:  # noqa: BLE001 - the guard fails the step
+                    out, err = None, f"{type(e).__name__}: {e}"
+                res.append((out, err, eng.healthy, eng.tp_consistency, eng.tp_consistency_checks,
+                            eng.tp.custom_ar is not None))
+                eng.shutdown_followers()
+            else:
+                eng.follower_loop()
+                assert eng.tp_consistency_checks > 0
+                assert (eng.tp.custom_ar is None) == bool(inject), "the fallback must be group-wide"
+            del eng
+            torch.cuda.synchronize()
+            dist.barrier()
+        q.put(("ok", res if rank == 0 else None))
+    except Exception:  # noqa: BLE001
+        q.put(("err", traceback.format_exc()))
+
+
+@pytest.mark.timeout(300)
+def test_tp2_runtime_consistency_guard(tmp_path):
+    """Run-time TP divergence guard on the GPU (graph replay, custom IPC collectives): every 2nd
+    step the two ranks compare checksums of the post-all-reduce residual, the logits and the
+    sampled ids. Clean (fused epilogue all-reduce): tokens == TP = 1 and no false alarm. With rank
+    1's all-reduce results perturbed inside the captured step (the unfused path, as a peer partial
+    read stale): the first check fails the step, rank 0 goes unhealthy with the reason, and BOTH
+    ranks drop the custom collectives."""
+    path = _ckpt(tmp_path)
+    ref_eng = __import__("vgate.runtime.engine", fromlist=["LLMEngine"]).LLMEngine(_cfg(path, 1, True))
+    ref = _generate(ref_eng)
+    del ref_eng
+    torch.cuda.synchronize()
+    port = _free_port()
+    runs = [(True, 0.0), (False, 0.25)]
+    _, q, procs = _spawn(2, _guard_worker, lambda r, q: (r, port, path, q, runs))
+    try:
+        results = [q.get(timeout=240) for _ in procs]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    errs = [r[1] for r in results if r[0] == "err"]
+    assert not errs, errs[0]
+    (out, err, healthy, state, checks, car_on), bad = next(r[1] for r in results if r[1] is not None)
+    assert err is None and out == ref and healthy and state == "ok" and checks >= 3 and car_on
+    out, err, healthy, state, checks, car_on = bad
+    assert out is None and err.startswith("TPDivergence") and not healthy and not car_on, bad
+    assert "residual" in state and checks == 1, state

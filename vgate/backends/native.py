@@ -48,7 +48,8 @@ def engine_config_from(model_config: ModelConfig):
         idle_batch_recent_ms=model_config.idle_batch_recent_ms, prefill_autotune=model_config.prefill_autotune,
         plan_cache=model_config.plan_cache or "", tp_timeout_seconds=model_config.tp_timeout_seconds,
         tp_custom_allreduce=model_config.tp_custom_allreduce, tp_fused_allreduce=model_config.tp_fused_allreduce,
-        tp_collective_self_check=model_config.tp_collective_self_check)
+        tp_collective_self_check=model_config.tp_collective_self_check,
+        tp_consistency_interval=model_config.tp_consistency_interval)
 
 
 def freeze_heap() -> None:

@@ -143,6 +143,11 @@ class ModelConfig(_Section):
     tp_custom_allreduce: bool = True
     tp_fused_allreduce: bool = True
     tp_collective_self_check: bool = True
+    # run-time TP divergence guard: every N-th step every rank checksums its logits and sampled ids
+    # (replicated after the collectives, bit-identical by the fixed-rank-order reductions) and the
+    # group compares them; a mismatch turns the custom collectives off group-wide and marks the
+    # engine unhealthy. 0 = off
+    tp_consistency_interval: int = 256
 
     @field_validator("engine_type")
     @classmethod

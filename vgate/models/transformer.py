@@ -256,6 +256,7 @@ class DecoderModel:
                 ops.linear(resid, L.gate_up, out=mlp, norm=(L.post_norm, eps))
             nq = li + 1 < nl and takes(self.layers[li + 1].qkv)
             self._row_parallel(mlp, L.down, resid, first, norm_out=(hg, ssp, self.layers[li + 1].in_norm) if nq else None)
+        self.last_resid = resid  # the post-all-reduce residual (replicated over TP): consistency guard
         if return_hidden:
             return resid
         logits = ops.linear(resid, self.lm_head, out_f32=True, norm=(self.final_norm, eps), row_idx=sv.sample_idx)
@@ -289,6 +290,7 @@ class DecoderModel:
             ops.rmsnorm(resid, L.post_norm, a.rms_eps, out=x)
             ops.linear(x, L.gate_up, out=mlp)
             self._row_parallel(mlp, L.down, resid, first)
+        self.last_resid = resid
         if return_hidden:
             return resid
         xs = resid.index_select(0, sv.sample_idx.long())

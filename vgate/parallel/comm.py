@@ -21,6 +21,27 @@ import torch
 import torch.distributed as dist
 
 
+# tests: the last rank adds this to the first element of every all-reduce result it gets, as if it
+# had read a peer's partial stale (a torch op after the collective: captured into the step graphs
+# with it). 0 = off. tests/test_tp_cpu.py, tests/test_tp_gpu.py (the run-time divergence guard).
+_INJECT_DIVERGENCE = 0.0
+
+
+def checksum64(t: torch.Tensor) -> torch.Tensor:
+    """Order- and position-sensitive 64-bit checksum of ``t``'s bits (int64 scalar on t's device):
+    sum_i bits_i * (i * 2654435761 + 1) in wrapping int64 arithmetic — exact integer adds, so the
+    same bits give the same value whatever the reduction order."""
+    flat = t.contiguous().reshape(-1)
+    if flat.element_size() == 4:
+        bits = flat.view(torch.int32).to(torch.int64)
+    elif flat.element_size() == 2:
+        bits = flat.view(torch.int16).to(torch.int64)
+    else:
+        bits = flat.view(torch.int64) if flat.element_size() == 8 else flat.to(torch.int64)
+    w = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) * 2654435761 + 1
+    return (bits * w).sum()
+
+
 @dataclass
 class TPGroup:
     rank: int = 0
@@ -42,14 +63,29 @@ class TPGroup:
         if self.size == 1 or self.simulated:
             return t
         if self.custom_ar is not None and self.custom_ar.should_use(t):
-            return self.custom_ar.all_reduce(t)
-        if self.backend == "gloo" and t.dtype in (torch.bfloat16, torch.float16):
+            t = self.custom_ar.all_reduce(t)
+        elif self.backend == "gloo" and t.dtype in (torch.bfloat16, torch.float16):
             f = t.float()
             dist.all_reduce(f, group=self.group)
             t.copy_(f)
-            return t
-        dist.all_reduce(t, group=self.group)
+        else:
+            dist.all_reduce(t, group=self.group)
+        if _INJECT_DIVERGENCE and self.rank == self.size - 1:
+            t.view(-1)[:1] += _INJECT_DIVERGENCE
         return t
+
+    def exchange_words(self, words: torch.Tensor) -> torch.Tensor:
+        """All-gather a small int64 vector over the group -> [size, n] (host tensor); RCCL takes the
+        device tensor, gloo a host copy. The run-time consistency guard's exchange (engine)."""
+        if self.size == 1 or self.simulated:
+            return words.reshape(1, -1).cpu()
+        src = words if self.backend == "nccl" else words.cpu()
+        out = torch.empty((self.size, src.numel()), dtype=src.dtype, device=src.device)
+        if self.backend == "gloo":
+            dist.all_gather(list(out.unbind(0)), src, group=self.group)
+        else:
+            dist.all_gather_into_tensor(out, src, group=self.group)
+        return out.cpu()
 
     def all_gather_lastdim(self, t: torch.Tensor) -> torch.Tensor:
         """[..., n] per rank -> [..., n * size] concatenated in rank order."""

@@ -40,6 +40,10 @@ from vgate.utils.profiling import range_
 log = logging.getLogger("vgate.engine")
 
 
+class TPDivergence(RuntimeError):
+    """The TP run-time consistency guard saw ranks disagree on replicated step outputs."""
+
+
 class KernelHandoffFault(RuntimeError):
     """An in-launch hand-off of a step gave up waiting (ops.fault_word): that step's results are
     invalid, but the engine can reset the hand-off state and go on (LLMEngine._recover_fault)."""
@@ -99,6 +103,7 @@ class EngineConfig:
     tp_custom_allreduce: bool = True
     tp_fused_allreduce: bool = True
     tp_collective_self_check: bool = True
+    tp_consistency_interval: int = 256  # run-time divergence guard: every N-th step (0 = off)
     arch_overrides: dict | None = None
 
     def resolve_device(self) -> torch.device:
@@ -232,6 +237,10 @@ class LLMEngine:
         self.last_error: str | None = None
         self._fault_times: collections.deque = collections.deque()
         self._idle_t: float | None = None  # start of the engine thread's current idle wait
+        self._launch_no = 0                # rank 0 launches (the consistency guard's step clock)
+        self.tp_consistent = True
+        self.tp_consistency = "ok"
+        self.tp_consistency_checks = 0
         self.fault_recoveries_max = 3
         self.fault_window_s = 300.0
         self.last_step_wall = time.monotonic()
@@ -530,7 +539,10 @@ class LLMEngine:
         if batch.empty:
             return 0
         t0 = time.perf_counter()
-        toks, samples = self.runner.execute(batch)
+        check = self._consistency_due()
+        toks, samples = self.runner.execute(batch, check=check)
+        if check:
+            self._consistency_exchange(batch.num_tokens, len(batch.items))
         self._check_collectives()
         for seq, n in batch.items:
             seq.num_computed += n
@@ -548,8 +560,13 @@ class LLMEngine:
             self._drain_inflight()
             return 0
         pend = {seq.seq_id: seq.pending_slot for seq, _ in batch.items if seq.pending}
+        check = self._consistency_due()
         with range_("vgate.launch"):
-            h = self.runner.launch(batch, pend)
+            h = self.runner.launch(batch, pend, check=check)
+        if check:
+            # synchronous: every rank must take (or not take) the group-wide fallback before its
+            # next launch, so the exchange is read right here, once per interval
+            self._consistency_exchange(batch.num_tokens, h.ns)
         for i, ((seq, n), smp) in enumerate(zip(batch.items, h.samples)):
             seq.num_computed += n
             if smp:
@@ -671,7 +688,7 @@ class LLMEngine:
             seq.callback("error" if error else "finish", seq, error)
 
     # ----------------------------------------------------------- tensor parallel
-    RING_PLAN, RING_EMBED, RING_CAPTURE, RING_STOP = 0, 1, 2, 3
+    RING_PLAN, RING_EMBED, RING_CAPTURE, RING_STOP, RING_PLAN_CHECK = 0, 1, 2, 3, 4
 
     def _init_ring(self) -> None:
         """Create (rank 0) / attach (followers) the group's shared-memory step ring. Rank 0 picks
@@ -757,6 +774,48 @@ class LLMEngine:
                     "prefix cache dropped, in-flight requests failed", len(hist), self.fault_window_s)
         return True
 
+    def _consistency_due(self) -> bool:
+        """Rank 0: is this launch one whose result the TP group cross-checks (every
+        ``tp_consistency_interval``-th launch; followers learn it from ring mode 4)?"""
+        n = self.cfg.tp_consistency_interval
+        if n <= 0 or self.tp.size == 1 or self.tp.simulated or not self.tp_consistent:
+            return False
+        self._launch_no += 1
+        return self._launch_no % n == 0
+
+    def _consistency_exchange(self, nt: int, S: int) -> None:
+        """Every rank, after the same step: all-gather [checksum(logits), checksum(sampled ids)]
+        and compare. They are replicated by construction (custom one-shot / fused all-reduce and
+        all-gather sum and concatenate in fixed rank order), so a difference means a rank computed
+        on different data, e.g. a peer partial read stale on the link — silently wrong tokens
+        otherwise. On a mismatch every rank sees it: the custom IPC collectives go off group-wide
+        (graphs dropped; RCCL for every collective from the next step on, buckets re-captured in
+        lock-step), and rank 0 fails the step and marks the engine unhealthy with the reason."""
+        words = self.tp.exchange_words(self.runner.consistency_words(nt, S))
+        self.tp_consistency_checks += 1
+        if bool((words == words[0:1]).all()):
+            return
+        bad = [r for r in range(words.shape[0]) if not bool((words[r] == words[0]).all())]
+        what = [n for i, n in enumerate(("residual", "logits", "sampled ids"))
+                if any(bool(words[r][i] != words[0][i]) for r in bad)]
+        reason = (f"TP ranks diverged at consistency check {self.tp_consistency_checks} "
+                  f"(step {self.stats.steps}): ranks {bad} differ from rank 0 in {', '.join(what)}")
+        self.tp_consistent = False
+        self.tp_consistency = reason
+        log.error("%s; custom collectives disabled group-wide", reason)
+        car = self.tp.custom_ar
+        if car is not None:
+            if self.runner.gpu:
+                torch.cuda.synchronize(self.device)
+            self.runner.graphs.clear()
+            self.runner.graph_logits.clear()
+            self.runner.ar_base = 0
+            self.tp.custom_ar = None
+            car.close()
+        if self.tp.is_first:
+            self.healthy = False
+            raise TPDivergence(reason)
+
     def follower_loop(self) -> None:
         """TP ranks > 0: execute whatever rank 0 publishes on the step ring, until it stops."""
         torch.set_grad_enabled(False)
@@ -783,11 +842,13 @@ class LLMEngine:
                 raise RuntimeError(f"TP step ring: no heartbeat from rank 0 for {timeout:.0f}s")
             if mode in (-1, self.RING_STOP):
                 return
-            r.follow_step(T, S, ns, nt, mode)
+            r.follow_step(T, S, ns, nt, self.RING_PLAN if mode == self.RING_PLAN_CHECK else mode)
             self.last_step_wall = time.monotonic()
-            if mode == self.RING_PLAN:
+            if mode in (self.RING_PLAN, self.RING_PLAN_CHECK):
                 self.stats.steps += 1
                 self._check_collectives()
+            if mode == self.RING_PLAN_CHECK:
+                self._consistency_exchange(nt, ns)
 
     def shutdown_followers(self) -> None:
         if self.tp.size > 1 and self.tp.is_first and self.ring is not None and not self._ring_closed:
@@ -848,6 +909,7 @@ class LLMEngine:
             "preemptions": self.scheduler.num_preemptions, "prefix_cache_hits": int(getattr(self.kvm.alloc, "hits", 0)),
             "healthy": self.healthy, "fault_recoveries": st.fault_recoveries,
             "tp_custom_collectives": int(self.tp.custom_ar is not None), "tp_self_check": self.tp_self_check,
+            "tp_consistency": self.tp_consistency, "tp_consistency_checks": self.tp_consistency_checks,
             "waves": st.waves, "wave_sum_ms": [round(1e3 * st.wave_first_s, 3), round(1e3 * st.wave_spread_s, 3),
                                                 round(1e3 * st.wave_tail_s, 3)], "wave_requests": st.wave_size,
         }

@@ -115,6 +115,8 @@ class ModelRunner:
         self.host_ms = 0.0  # host time of execute() outside the device wait
         self.gpu_steps = 0
         self.collect_wait_ms = 0.0  # host time blocked in collect() waiting for a step's device work
+        self.graph_logits: dict = {}  # (T, S) -> the captured graph's static logits tensor
+        self.last_out = None          # (residual, logits) of the last launched / followed step (consistency guard)
         self.captures = 0  # hipGraph captures so far (start-up warm-up + deferred + on-miss)
         self.max_gpu_ms = 0.0  # slowest step's device time and its bucket (p99 forensics)
         self.max_gpu_bucket = (0, 0)
@@ -257,7 +259,9 @@ class ModelRunner:
             self.pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=self.pool, stream=s):
-            self._forward_sample(view)
+            logits = self._forward_sample(view)
+        # the graph's static residual + logits tensors (the TP consistency guard reads them)
+        self.graph_logits[(T, S)] = (self.model.last_resid, logits)
         torch.cuda.synchronize()
         self.captures += 1
         self.capture_seconds += time.perf_counter() - t0
@@ -265,17 +269,18 @@ class ModelRunner:
         return g
 
     @torch.inference_mode()
-    def execute(self, batch: ScheduledBatch) -> tuple[list[int], list[bool]]:
+    def execute(self, batch: ScheduledBatch, check: bool = False) -> tuple[list[int], list[bool]]:
         """Run one step synchronously; returns (sampled token per item, whether consumed)."""
-        h = self.launch(batch)
+        h = self.launch(batch, check=check)
         return self.collect(h), h.samples
 
     @torch.inference_mode()
-    def launch(self, batch: ScheduledBatch, pending_slots: dict | None = None) -> "StepHandle":
+    def launch(self, batch: ScheduledBatch, pending_slots: dict | None = None, check: bool = False) -> "StepHandle":
         """Enqueue one step (GPU: returns before it runs). ``pending_slots`` maps a
-        sequence id to the previous step's sample slot of its unresolved last token."""
+        sequence id to the previous step's sample slot of its unresolved last token. ``check``:
+        TP followers are told to join the consistency exchange after this step (ring mode 4)."""
         if not self.gpu:
-            toks, samples = self._execute_cpu(batch)
+            toks, samples = self._execute_cpu(batch, check)
             return StepHandle(0, len(batch.items), samples, toks, time.perf_counter())
         ns = len(batch.items)
         nt = batch.num_tokens
@@ -292,7 +297,7 @@ class ModelRunner:
         samples = self._fill(batch, T, S, pending_slots)
         self.meta.h["ring_slot"][0] = k
         if self.on_plan is not None:
-            self.on_plan(T, S, ns, nt, 0)
+            self.on_plan(T, S, ns, nt, 4 if check else 0)
         # device time of every 8th step (an event record is a marker packet in the queue)
         timed = self._launches % 8 == 0
         self._launches += 1
@@ -312,6 +317,7 @@ class ModelRunner:
         if g is not None:
             self.graph_hits += 1
             g.replay()
+            self.last_out = self.graph_logits.get((T, S))
         else:
             if graphs and not self.defer_capture_failed:
                 # first sight of this bucket under load: run it eagerly (a few ms of launch
@@ -322,7 +328,8 @@ class ModelRunner:
                 self.pending_captures[(T, S)] = self.pending_captures.get((T, S), 0) + 1
             view = self.meta.view(T, S)
             view.num_tokens, view.num_seqs = nt, ns
-            self._forward_sample(view)
+            lg = self._forward_sample(view)
+            self.last_out = (self.model.last_resid, lg)
         self.dones[k].record()
         self.host_ms += 1e3 * (time.perf_counter() - t_host)
         return StepHandle(k, ns, samples, None, t_host, (T, S), eager, timed)
@@ -355,6 +362,22 @@ class ModelRunner:
         if k is None:
             k = self._last_collected if self._last_collected is not None else self._k ^ 1
         return int(self.out_ring[k][-1])
+
+    def consistency_words(self, nt: int, S: int) -> torch.Tensor:
+        """[checksum of the last step's post-all-reduce residual rows, of its logits rows, of its
+        sampled ids] (int64, device). All three are replicated over a TP group: every rank's
+        all-reduce sums the same partials in rank order, the logits all-gather concatenates in rank
+        order, the sampler draws with the same seeds. The residual is the one that catches a
+        collective read stale on one rank (the logits would hide it: the next all-reduce adds only
+        rank 0's residual). CPU followers take argmax instead of sampling: ids count on the GPU only,
+        where followers' sampled ids resolve their next step's inputs."""
+        from vgate.parallel.comm import checksum64
+        zero = torch.zeros((), dtype=torch.int64, device=self.device)
+        resid, lg = self.last_out if self.last_out is not None else (None, None)
+        a = checksum64(resid[:nt]) if resid is not None else zero
+        b = checksum64(lg[:S]) if lg is not None else zero
+        c = checksum64(self.out_tokens[:S]) if self.gpu else zero
+        return torch.stack([a, b.to(a.device), c.to(a.device)])
 
     def reset_fault_ring(self) -> None:
         """After the engine's fault recovery (ops.reset_handoffs, device idle): clear the fault
@@ -399,12 +422,12 @@ class ModelRunner:
         h = self.model.forward(view, self.kv, self.part_size, return_hidden=True)
         return h[:nt]
 
-    def _execute_cpu(self, batch):
+    def _execute_cpu(self, batch, check: bool = False):
         ns, nt = len(batch.items), batch.num_tokens
         self.meta.select(0)
         samples = self._fill(batch, nt, ns)
         if self.on_plan is not None:
-            self.on_plan(nt, ns, ns, nt, 0)
+            self.on_plan(nt, ns, ns, nt, 4 if check else 0)
         self.meta.upload(ns)
         view = self.meta.view(nt, ns)
         view.num_tokens, view.num_seqs = nt, ns
@@ -413,6 +436,7 @@ class ModelRunner:
 
     def _cpu_sample(self, view, batch):
         logits = self.model.forward(view, self.kv, self.part_size)
+        self.last_out = (self.model.last_resid, logits)
         gens = []
         for seq, _ in batch.items:
             g = torch.Generator()
@@ -464,6 +488,7 @@ class ModelRunner:
                 self.model.forward(view, self.kv, self.part_size, return_hidden=True)
             elif mode == 0:
                 logits = self.model.forward(view, self.kv, self.part_size)
+                self.last_out = (self.model.last_resid, logits)
                 self.out_tokens[:S] = logits.argmax(-1).int()
             return
         k = self._k
@@ -491,8 +516,10 @@ class ModelRunner:
         if g is not None:
             self.graph_hits += 1
             g.replay()
+            self.last_out = self.graph_logits.get((T, S))
         else:
-            self._forward_sample(view)
+            lg = self._forward_sample(view)
+            self.last_out = (self.model.last_resid, lg)
 
     def capture_pending(self, max_graphs: int = 64) -> int:
         """Capture the buckets that ran eagerly since the last call (most frequent first).
