@@ -30,6 +30,7 @@ os.environ.setdefault("VGATE_LOGGING__LEVEL", "WARNING")
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 BASELINE_REQ_S = 6.47
+LAST_T_RUN = 0.0  # perf_counter origin of the last run_load's ``starts``
 BENCH_KEY = "vgate-bench-key"
 METRIC = "req/s + p50/p99 end-to-end latency, {model} /v1/chat/completions at fixed concurrency"
 
@@ -96,8 +97,9 @@ async def run_load(port: int, n: int, concurrency: int, max_tokens: int, rank: i
             lat.append(time.perf_counter() - t0)
             starts.append(t0 - t_run)
 
+    global LAST_T_RUN
     try:
-        t_run = t0 = time.perf_counter()
+        t_run = t0 = LAST_T_RUN = time.perf_counter()
         await asyncio.gather(*(one(i) for i in range(n)))
         wall = time.perf_counter() - t0
     finally:
@@ -251,6 +253,31 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
     if "wave_sum_ms" in snap and "wave_sum_ms" in snap0:
         nw = max(1, snap.get("timed_waves", 0))
         snap["wave_breakdown_ms"] = [round((a - b) / nw, 3) for a, b in zip(snap["wave_sum_ms"], snap0["wave_sum_ms"])]
+    # wave-boundary trace (in-process engine, lean client: one clock): per timed wave, last finish
+    # in the engine -> idle start, -> first response received by the client, -> the client's first
+    # new request sent, -> that request reaching the engine, -> the last of the wave arriving
+    trace = None
+    wl = list(getattr(inner, "wave_log", []))
+    if wl and starts and client is None:
+        t_run_abs = LAST_T_RUN
+        sends = sorted(t_run_abs + s for s in starts)
+        recvs = sorted(t_run_abs + s + la for s, la in zip(starts, lat))
+        import bisect as _bs
+        parts = {k: [] for k in ("finish_to_idle", "finish_to_first_recv", "first_recv_to_first_send",
+                                 "first_send_to_first_arrival", "first_to_last_arrival")}
+        for fin, idle0, a0, a1, _ in wl:
+            if fin < t0:
+                continue
+            i = _bs.bisect_left(recvs, fin)
+            j = _bs.bisect_left(sends, fin)
+            if i >= len(recvs) or j >= len(sends):
+                continue
+            parts["finish_to_idle"].append(idle0 - fin)
+            parts["finish_to_first_recv"].append(recvs[i] - fin)
+            parts["first_recv_to_first_send"].append(sends[j] - recvs[i])
+            parts["first_send_to_first_arrival"].append(a0 - sends[j])
+            parts["first_to_last_arrival"].append(a1 - a0)
+        trace = {k: round(1e3 * sorted(v)[len(v) // 2], 3) for k, v in parts.items() if v}
     server.should_exit = True
     await srv_task
     slow = sorted(zip(lat, starts), reverse=True)[:8]
@@ -258,7 +285,7 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
             "slowest": [[round(st, 3), round(la, 4)] for la, st in slow],
             "loop_lag_max_ms": round(lag["max_ms"], 2), "loop_lag_at_s": round(lag["at_s"], 3),
             "gc_gen2_collections": gcs["n2"], "gc_max_pause_ms": round(gcs["max_ms"], 2),
-            "n": per_step * args.steps, "engine": snap}
+            "n": per_step * args.steps, "engine": snap, "wave_trace_ms": trace}
 
 
 def run_follower(args, rank: int) -> None:
@@ -419,6 +446,8 @@ def main():
             # per idle -> busy transition: [idle start -> first arrival, first -> last arrival of the
             # wave, last arrival -> step start] in ms, and the requests per transition
             "wave_breakdown_ms": allr[0]["engine"].get("wave_breakdown_ms"),
+            # medians over the timed waves (rank 0, in-process client): where a wave boundary's idle goes
+            "wave_trace_ms": allr[0].get("wave_trace_ms"),
             "timed_waves": allr[0]["engine"].get("timed_waves"),
             "timed_wave_requests": allr[0]["engine"].get("timed_wave_requests"),
             "timed_eager_steps": allr[0]["engine"].get("timed_graph_misses_eager"),

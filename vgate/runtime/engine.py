@@ -238,6 +238,9 @@ class LLMEngine:
         self._fault_times: collections.deque = collections.deque()
         self._idle_t: float | None = None  # start of the engine thread's current idle wait
         self._launch_no = 0                # rank 0 launches (the consistency guard's step clock)
+        # per idle -> busy transition: (last finish before it, idle start, first / last arrival, step
+        # start), perf_counter clock (bench.py joins it with its client's send / receive times)
+        self.wave_log: collections.deque = collections.deque(maxlen=4096)
         self.tp_consistent = True
         self.tp_consistency = "ok"
         self.tp_consistency_checks = 0
@@ -395,6 +398,8 @@ class LLMEngine:
         bench.py (``wave_breakdown_ms``)."""
         arr = [s.arrival for s in self._inbox]
         now = time.perf_counter()
+        fin = self._finish_times[-1] if self._finish_times else t_idle0
+        self.wave_log.append((fin, t_idle0, min(arr), max(arr), now))
         st = self.stats
         st.waves += 1
         st.wave_first_s += max(0.0, min(arr) - t_idle0)
