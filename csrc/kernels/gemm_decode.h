@@ -4,6 +4,7 @@
 #pragma once
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "gemm_epilogue.h"
 
@@ -328,6 +329,42 @@ constexpr int TG_MB = 4;      // 16-row m-tiles per block (64 rows)
 constexpr int TG_KS = 8;      // k-steps per LDS stage
 constexpr int TG_STAGE_BYTES = TG_KS * TG_MB * 64 * 16;  // 32 KiB
 
+// Epilogue of the tile kernels (this wave: rows m_base.. x its NTW column tiles, 4 m-tiles). The
+// epilogue operands of all 4 m-tiles (QKV: position, slot, bias, then cos / sin by position;
+// residual GEMMs: residual + bias words) are requested together first: per m-tile inside the store
+// loop they were 4 serial chains of dependent loads (the compiler cannot hoist a load above an earlier
+// m-tile's stores it might alias) — ~4.5 us of the 448-row QKV projection's 21 us.
+template <int NTW, int EPI, int NORM>
+__device__ __forceinline__ void tile_epilogue(const GemmParams& p, f32x4 (&acc)[TG_MB][NTW], const float (&ssr)[TG_MB],
+                                              int m_base, int nt0, int lane) {
+  constexpr bool PREF = NTW <= 2;  // EpiPre carries two tiles' words
+  const int nsub = 4 * (lane >> 4);
+  EpiPre<NTW> pre[TG_MB];
+  if constexpr (PREF) {
+#pragma unroll
+    for (int mb = 0; mb < TG_MB; ++mb) epi_pre_a<NTW, EPI>(p, pre[mb], m_base + mb * 16 + (lane & 15), nt0, nsub);
+#pragma unroll
+    for (int mb = 0; mb < TG_MB; ++mb) epi_pre_b<NTW, EPI>(p, pre[mb], nt0, nsub);
+  }
+#pragma unroll
+  for (int mb = 0; mb < TG_MB; ++mb) {
+    const int m = m_base + mb * 16 + (lane & 15);
+    f32x4 v[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) v[j] = acc[mb][j];
+    if constexpr (NORM) {
+      float ss = ssr[mb];
+      ss += xor16(ss);
+      ss += xor32(ss);
+      const float sc = rsqrtf(ss / (float)p.K + p.eps);
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) v[j] *= sc;
+    }
+    if constexpr (PREF) epilogue<NTW, EPI, true>(p, v, m, nt0, nsub, pre[mb], m < p.M);
+    else epilogue<NTW, EPI, false>(p, v, m, nt0, nsub, EpiPre<NTW>{}, m < p.M);
+  }
+}
+
 template <int NTW, int EPI, int NORM>
 __global__ __launch_bounds__(256) void gemm_tile_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -433,22 +470,126 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(GemmParams p) {
     }
   }
   // epilogue straight from registers: this wave owns rows m_base.. x its NTW tiles
+  tile_epilogue<NTW, EPI, NORM>(p, acc, ssr, m_base, nt0, lane);
+}
+
+// Same tile, grid, x layout and epilogue as gemm_tile_kernel, with the stage pipeline two stages
+// deep instead of one. gemm_tile_kernel issues stage s+1 (x to registers, weights to registers)
+// while it computes stage s, then stores x(s+1) into LDS — so every stage waits out a whole load
+// round trip behind a compute phase of ~32 MFMAs per wave: at M = 448 the Qwen2.5-1.5B qkv / o
+// projections took 23 / 15 us cold in the prefill step for 2.8 / 2.1 GFLOP (18 GB/s of L2 / HBM
+// traffic per CU, profiles/r6_base_prefill_timeline.log). Here iteration s issues stage s+2 and
+// stores x(s+1), loaded one iteration earlier, after computing s: each load has two iterations to
+// land, 128 KB per block in flight instead of 64. Registers: 3 weight groups + 2 x groups
+// (~190 VGPRs at NTW = 1; one 4-wave block per CU as before). Loads past the last stage re-read it
+// (clamped, unconditional: a guarded load would put a vmcnt(0) where the branch joins).
+template <int NTW, int EPI, int NORM>
+__global__ __launch_bounds__(256) void gemm_tile3_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  TLScope tl_scope(p.dbg_ts);
+  uint4* xs = reinterpret_cast<uint4*>(smem);  // [2][KS][MB][64] fragments
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int KT = p.K >> 5;
+  const int mchunks = (p.M + 16 * TG_MB - 1) / (16 * TG_MB);
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int nt0 = ((wgid / mchunks) * TG_WAVES + wid) * NTW;
+  const int m_base = (wgid % mchunks) * 16 * TG_MB;
+  const bf16_t* nw_ptr = p.norm_w ? p.norm_w + 8 * (lane >> 4) : nullptr;
+  f32x4 acc[TG_MB][NTW];
 #pragma unroll
-  for (int mb = 0; mb < TG_MB; ++mb) {
-    const int m = m_base + mb * 16 + (lane & 15);
-    f32x4 v[NTW];
+  for (int a = 0; a < TG_MB; ++a)
 #pragma unroll
-    for (int j = 0; j < NTW; ++j) v[j] = acc[mb][j];
-    if constexpr (NORM) {
-      float ss = ssr[mb];
-      ss += xor16(ss);
-      ss += xor32(ss);
-      const float sc = rsqrtf(ss / (float)p.K + p.eps);
+    for (int b = 0; b < NTW; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ssr[TG_MB];
 #pragma unroll
-      for (int j = 0; j < NTW; ++j) v[j] *= sc;
+  for (int mb = 0; mb < TG_MB; ++mb) ssr[mb] = 0.f;
+  constexpr int STAGE_FRAGS = TG_KS * TG_MB * 64;
+  constexpr int NX = STAGE_FRAGS / 256;
+  static_assert(NX == TG_KS && TG_MB == TG_WAVES, "stage mapping");
+  // buffer loads: one per-lane byte offset VGPR per operand, the k-step in the scalar offset — no
+  // 64-bit address temporaries (with flat addresses the register allocator gave the last weight
+  // load's destination to the next iteration's address temp: a vmcnt(0) at the loop head)
+  const uint32_t xoff = (uint32_t)(((size_t)row_of(p, min(m_base + wid * 16 + (lane & 15), p.M - 1)) * p.lda +
+                                    8 * (lane >> 4)) * 2);
+  const __amdgpu_buffer_rsrc_t xr = rsrc_of(p.x), wr = rsrc_of(p.wp);
+  uint32_t woff[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) woff[j] = (uint32_t)((((size_t)(nt0 + j) * KT) * 64 + lane) * 16);
+  const int nstage = (KT + TG_KS - 1) / TG_KS;
+  uint4 W[3][TG_KS][NTW];
+  uint4 X[2][NX];
+  auto as_u4 = [](u32x4 v) __attribute__((always_inline)) { return make_uint4(v[0], v[1], v[2], v[3]); };
+  auto load_x = [&](uint4 (&rr)[NX], int st) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NX; ++i)
+      rr[i] = as_u4(__builtin_amdgcn_raw_buffer_load_b128(xr, xoff, min(st * TG_KS + i, KT - 1) * 64, 0));
+  };
+  auto store_x = [&](const uint4 (&rr)[NX], int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NX; ++i) xs[buf * STAGE_FRAGS + i * 256 + threadIdx.x] = rr[i];
+  };
+  auto issue_w = [&](uint4 (&w)[TG_KS][NTW], int st) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < TG_KS; ++u) {
+      const int kt = min(st * TG_KS + u, KT - 1);
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+        w[u][j] = as_u4(__builtin_amdgcn_raw_buffer_load_b128(wr, woff[j], kt * 1024, 2 /* nt */));
     }
-    epilogue<NTW, EPI, false>(p, v, m, nt0, 4 * (lane >> 4), EpiPre<NTW>{}, m < p.M);
+  };
+  // whole stages only (host: K % (32 * TG_KS) == 0): no per-k-step guard, so the stage's MFMAs are
+  // one branch-free block and the compiler keeps exact partial vmcnt waits across it
+  auto compute = [&](const uint4 (&w)[TG_KS][NTW], int st) __attribute__((always_inline)) {
+    const int buf = st & 1;
+    const int kt0 = st * TG_KS;
+#pragma unroll
+    for (int ks = 0; ks < TG_KS; ++ks) {
+      uint4 xa[TG_MB];
+#pragma unroll
+      for (int mb = 0; mb < TG_MB; ++mb) {
+        xa[mb] = xs[buf * STAGE_FRAGS + (ks * TG_MB + mb) * 64 + lane];
+        if constexpr (NORM) xa[mb] = norm_frag<NORM>(xa[mb], nw_ptr, (kt0 + ks) * 32, ssr[mb]);
+      }
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int mb = 0; mb < TG_MB; ++mb) acc[mb][j] = mfma16(as_bf16x8(w[ks][j]), as_bf16x8(xa[mb]), acc[mb][j]);
+    }
+  };
+  // iteration s (A = s % 3, B = s % 2): issue stage s+2 into the registers stage s-1 / s left,
+  // compute s, store x(s+1) into the LDS buffer stage s-1 was read from, barrier
+  auto iter = [&](auto A, auto B, int s) __attribute__((always_inline)) {
+    constexpr int a = decltype(A)::value, b = decltype(B)::value;
+    load_x(X[b], s + 2);
+    issue_w(W[(a + 2) % 3], s + 2);
+    compute(W[a], s);
+    store_x(X[1 - b], 1 - b);
+    lds_barrier();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  load_x(X[0], 0);
+  issue_w(W[0], 0);
+  load_x(X[1], 1);
+  issue_w(W[1], 1);
+  store_x(X[0], 0);
+  lds_barrier();
+  for (int s = 0; s < nstage; s += 6) {
+    iter(I0{}, I0{}, s);
+    if (s + 1 >= nstage) break;
+    iter(I1{}, I1{}, s + 1);
+    if (s + 2 >= nstage) break;
+    iter(I2{}, I0{}, s + 2);
+    if (s + 3 >= nstage) break;
+    iter(I0{}, I1{}, s + 3);
+    if (s + 4 >= nstage) break;
+    iter(I1{}, I0{}, s + 4);
+    if (s + 5 >= nstage) break;
+    iter(I2{}, I1{}, s + 5);
   }
+  tile_epilogue<NTW, EPI, NORM>(p, acc, ssr, m_base, nt0, lane);
 }
 
 // ------------------------------------------------------------------ host side
@@ -619,7 +760,18 @@ static void launch_m(GemmParams p, const GemmArgs& g, hipStream_t st) {
     const bool tile_wins = tblocks >= 128 || g.M >= 128;
     if (g.M > 16 && g.splitk <= 0 && tblocks > 0 && (g.waves < 0 || (g.waves == 0 && tile_wins))) {
       dim3 grid(tblocks), block(64 * TG_WAVES);
-      if (p.dbg_ts == nullptr) p.dbg_ts = tl_take("gemm_tile", tblocks);
+      // two-deep stage pipeline (gemm_tile3_kernel) once K has >= 3 stages; waves -1 / -2 force
+      // the one-deep / two-deep form (sweeps, tests)
+      // (one column tile per wave only: with 2 / 4 the three weight groups spill to scratch)
+      const bool deep = NTW == 1 && g.K % (32 * TG_KS) == 0 &&
+                        (g.waves == -2 || (g.waves != -1 && (g.K / 32) >= 3 * TG_KS));
+      if (p.dbg_ts == nullptr) p.dbg_ts = tl_take(deep ? "gemm_tile3" : "gemm_tile", tblocks);
+      if constexpr (NTW == 1) {
+        if (deep) {
+          hipLaunchKernelGGL((gemm_tile3_kernel<NTW, EPI, NORM>), grid, block, 2 * TG_STAGE_BYTES, st, p);
+          return;
+        }
+      }
       hipLaunchKernelGGL((gemm_tile_kernel<NTW, EPI, NORM>), grid, block, 2 * TG_STAGE_BYTES, st, p);
       return;
     }

@@ -1032,6 +1032,59 @@ def test_gemm_tile_kernel_prefill_shapes(M):
     assert _rel_err(lf.cpu(), ref.linear_ref(xh[idx.long()].cpu(), wl.cpu(), out_f32=True)) < 1e-2
 
 
+@pytest.mark.parametrize("M,K", [(17, 1536), (100, 2048), (448, 1536), (448, 8960), (640, 2304)])
+def test_gemm_tile3_two_deep_pipeline(M, K):
+    """waves=-2 forces the two-deep-pipeline tile kernel (gemm_tile3_kernel; K % 256 == 0, any number
+    of stages incl. the loop's early exits): residual, folded-norm SiLU and f32 + row gather against
+    the fp32 references, and bit-identical to the one-deep tile kernel (same k order per block)."""
+    torch.manual_seed(70 + M + K)
+    N = 1536
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    lin = ops.Linear(w)
+    out3, out1 = r.clone(), r.clone()
+    ops.linear(x, lin, out=out3, residual=out3, waves=-2)
+    ops.linear(x, lin, out=out1, residual=out1, waves=-1)
+    assert _rel_err(out3.float().cpu(), ref.linear_ref(x.cpu(), w.cpu(), None, r.cpu()).float()) < 1e-2
+    assert torch.equal(out3, out1)
+    I = 1024
+    g = (torch.rand(K, device=DEV) + 0.5).bfloat16()
+    wg = (torch.randn(2 * I, K, device=DEV) / math.sqrt(K)).bfloat16()
+    ls = ops.Linear(wg, kind="silu")
+    ls.fold_norm(g)
+    y = ops.linear(x, ls, norm=(g, 1e-6), waves=-2)
+    xn, _ = ref.rmsnorm_ref(x.cpu(), g.cpu(), 1e-6)
+    assert _rel_err(y.float().cpu(), ref.silu_mul_linear_ref(xn, wg[:I].cpu(), wg[I:].cpu()).float()) < 1e-2
+    idx = torch.randperm(M, device=DEV)[: max(17, M // 2)].int()
+    lf = ops.linear(x, lin, out_f32=True, row_idx=idx, waves=-2)
+    assert _rel_err(lf.cpu(), ref.linear_ref(x[idx.long()].cpu(), w.cpu(), out_f32=True)) < 1e-2
+    # QKV epilogue (bias + folded-norm row scale + RoPE + paged KV write), the prefill step's qkv form
+    hq, hkv, D, BS = 12, 2, 128, 16
+    Nq = (hq + 2 * hkv) * D
+    wq = (torch.randn(Nq, K, device=DEV) / math.sqrt(K)).bfloat16()
+    bq = (torch.randn(Nq, device=DEV) * 0.1).bfloat16()
+    lq = ops.Linear(wq, bias=bq, layout="qkv")
+    lq.fold_norm(g)
+    pos = torch.randint(0, 1000, (M,), dtype=torch.int32, device=DEV)
+    slots = torch.randperm(64 * BS, device=DEV)[:M].int()
+    cs = ref.rope_cos_sin(1024, D, 1e6, device=DEV)
+    outs = []
+    for wv in (-2, -1):
+        kc = torch.zeros(64, hkv, BS, D, device=DEV).bfloat16()
+        vc = torch.zeros_like(kc)
+        q = ops.linear(x, lq, norm=(g, 1e-6), waves=wv, qkv=dict(positions=pos, slots=slots, cos_sin=cs,
+                                                                 k_cache=kc, v_cache=vc, hq=hq, hkv=hkv))
+        outs.append((q, kc, vc))
+    xq = ref.linear_ref(xn, wq.cpu(), bq.cpu())
+    kc2, vc2 = torch.zeros(64, hkv, BS, D).bfloat16(), torch.zeros(64, hkv, BS, D).bfloat16()
+    ref.rope_kv_ref(xq, pos.cpu(), slots.cpu(), cs.cpu(), kc2, vc2, hq, hkv, D)
+    (q3, k3, v3), (q1, k1, v1) = outs
+    assert _rel_err(q3.float().cpu(), xq[:, : hq * D].float()) < 1e-2
+    assert _rel_err(k3.float().cpu(), kc2.float()) < 1e-2 and _rel_err(v3.float().cpu(), vc2.float()) < 1e-2
+    assert torch.equal(q3, q1) and torch.equal(k3, k1) and torch.equal(v3, v1)
+
+
 @pytest.mark.parametrize("layout", ["plain", "silu", "qkv"])
 def test_awq_long_step_dequant_path(layout):
     """AWQ linear at M > 64 (a prefill step): int4 -> bf16 scratch (awq_dequant, RMSNorm gamma folded
