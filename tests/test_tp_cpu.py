@@ -330,3 +330,31 @@ def test_tp_runtime_consistency_guard(tmp_path):
     assert bad["error"] is not None and bad["error"].startswith("TPDivergence"), bad
     assert not bad["healthy"] and "diverged" in bad["state"] and "ranks [1]" in bad["state"]
     assert bad["checks"] == 1
+
+
+def test_checksum64_is_exact_and_position_sensitive():
+    """The consistency guard's checksum: same bits -> same value whatever the reduction order (exact
+    wrapping int64 adds), any single-bit or position change -> a different value, all dtypes."""
+    from vgate.parallel.comm import checksum64
+    torch.manual_seed(3)
+    for dt in (torch.float32, torch.bfloat16, torch.int32, torch.int64):
+        t = (torch.randn(37, 129) * 100).to(dt)
+        a = int(checksum64(t))
+        assert a == int(checksum64(t.clone().contiguous()))
+        assert a == int(checksum64(t.t().contiguous().t()))  # non-contiguous view of the same values
+        u = t.clone()
+        flat = u.view(-1)
+        flat[1000] = flat[1001] if flat[1000] != flat[1001] else flat[1000] + 1
+        assert int(checksum64(u)) != a
+        sw = t.clone().view(-1)
+        i, j = 5, 4000
+        if sw[i] != sw[j]:
+            sw[i], sw[j] = sw[j].clone(), sw[i].clone()
+            assert int(checksum64(sw)) != a  # a permutation changes it
+
+
+def test_exchange_words_single_rank():
+    from vgate.parallel.comm import TPGroup
+    w = torch.tensor([1, -2, 3], dtype=torch.int64)
+    out = TPGroup().exchange_words(w)
+    assert out.shape == (1, 3) and torch.equal(out[0], w)
