@@ -796,7 +796,7 @@ class LLMEngine:
         otherwise. On a mismatch every rank sees it: the custom IPC collectives go off group-wide
         (graphs dropped; RCCL for every collective from the next step on, buckets re-captured in
         lock-step), and rank 0 fails the step and marks the engine unhealthy with the reason."""
-        words = self.tp.exchange_words(self.runner.consistency_words(nt, S))
+        words = self.tp.exchange_words(self.runner.check_words)
         self.tp_consistency_checks += 1
         if bool((words == words[0:1]).all()):
             return
@@ -813,7 +813,6 @@ class LLMEngine:
             if self.runner.gpu:
                 torch.cuda.synchronize(self.device)
             self.runner.graphs.clear()
-            self.runner.graph_logits.clear()
             self.runner.ar_base = 0
             self.tp.custom_ar = None
             car.close()
@@ -847,7 +846,8 @@ class LLMEngine:
                 raise RuntimeError(f"TP step ring: no heartbeat from rank 0 for {timeout:.0f}s")
             if mode in (-1, self.RING_STOP):
                 return
-            r.follow_step(T, S, ns, nt, self.RING_PLAN if mode == self.RING_PLAN_CHECK else mode)
+            r.follow_step(T, S, ns, nt, self.RING_PLAN if mode == self.RING_PLAN_CHECK else mode,
+                          check=mode == self.RING_PLAN_CHECK)
             self.last_step_wall = time.monotonic()
             if mode in (self.RING_PLAN, self.RING_PLAN_CHECK):
                 self.stats.steps += 1

@@ -115,8 +115,7 @@ class ModelRunner:
         self.host_ms = 0.0  # host time of execute() outside the device wait
         self.gpu_steps = 0
         self.collect_wait_ms = 0.0  # host time blocked in collect() waiting for a step's device work
-        self.graph_logits: dict = {}  # (T, S) -> the captured graph's static logits tensor
-        self.last_out = None          # (residual, logits) of the last launched / followed step (consistency guard)
+        self.check_words = None  # consistency-guard words of the last step launched with check=True
         self.captures = 0  # hipGraph captures so far (start-up warm-up + deferred + on-miss)
         self.max_gpu_ms = 0.0  # slowest step's device time and its bucket (p99 forensics)
         self.max_gpu_bucket = (0, 0)
@@ -260,8 +259,10 @@ class ModelRunner:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=self.pool, stream=s):
             logits = self._forward_sample(view)
-        # the graph's static residual + logits tensors (the TP consistency guard reads them)
-        self.graph_logits[(T, S)] = (self.model.last_resid, logits)
+        # the graph's static residual + logits tensors (the TP consistency guard reads them), owned by
+        # the graph object: dropping a graph drops them with it (references kept beside a deleted
+        # graph would pin blocks of its private pool, which the next capture into that pool asserts on)
+        g.vg_out = (self.model.last_resid, logits)
         torch.cuda.synchronize()
         self.captures += 1
         self.capture_seconds += time.perf_counter() - t0
@@ -317,7 +318,8 @@ class ModelRunner:
         if g is not None:
             self.graph_hits += 1
             g.replay()
-            self.last_out = self.graph_logits.get((T, S))
+            if check:
+                self.check_words = self._words(*g.vg_out, nt, ns)
         else:
             if graphs and not self.defer_capture_failed:
                 # first sight of this bucket under load: run it eagerly (a few ms of launch
@@ -329,7 +331,8 @@ class ModelRunner:
             view = self.meta.view(T, S)
             view.num_tokens, view.num_seqs = nt, ns
             lg = self._forward_sample(view)
-            self.last_out = (self.model.last_resid, lg)
+            if check:
+                self.check_words = self._words(self.model.last_resid, lg, nt, ns)
         self.dones[k].record()
         self.host_ms += 1e3 * (time.perf_counter() - t_host)
         return StepHandle(k, ns, samples, None, t_host, (T, S), eager, timed)
@@ -363,9 +366,9 @@ class ModelRunner:
             k = self._last_collected if self._last_collected is not None else self._k ^ 1
         return int(self.out_ring[k][-1])
 
-    def consistency_words(self, nt: int, S: int) -> torch.Tensor:
-        """[checksum of the last step's post-all-reduce residual rows, of its logits rows, of its
-        sampled ids] (int64, device). All three are replicated over a TP group: every rank's
+    def _words(self, resid, lg, nt: int, S: int) -> torch.Tensor:
+        """[checksum of a step's post-all-reduce residual rows, of its logits rows, of its sampled
+        ids] (int64, device; enqueued right behind the step). All three are replicated over a TP group: every rank's
         all-reduce sums the same partials in rank order, the logits all-gather concatenates in rank
         order, the sampler draws with the same seeds. The residual is the one that catches a
         collective read stale on one rank (the logits would hide it: the next all-reduce adds only
@@ -373,7 +376,6 @@ class ModelRunner:
         where followers' sampled ids resolve their next step's inputs."""
         from vgate.parallel.comm import checksum64
         zero = torch.zeros((), dtype=torch.int64, device=self.device)
-        resid, lg = self.last_out if self.last_out is not None else (None, None)
         a = checksum64(resid[:nt]) if resid is not None else zero
         b = checksum64(lg[:S]) if lg is not None else zero
         c = checksum64(self.out_tokens[:S]) if self.gpu else zero
@@ -431,18 +433,20 @@ class ModelRunner:
         self.meta.upload(ns)
         view = self.meta.view(nt, ns)
         view.num_tokens, view.num_seqs = nt, ns
-        self._cpu_sample(view, batch)
+        logits = self._cpu_sample(view, batch)
+        if check:
+            self.check_words = self._words(self.model.last_resid, logits, nt, ns)
         return self.out_tokens[:ns].tolist(), samples
 
     def _cpu_sample(self, view, batch):
         logits = self.model.forward(view, self.kv, self.part_size)
-        self.last_out = (self.model.last_resid, logits)
         gens = []
         for seq, _ in batch.items:
             g = torch.Generator()
             g.manual_seed((seq.seed * 1000003 + len(seq.output_ids)) & 0x7FFFFFFFFFFFFFFF)
             gens.append(g)
         self.out_tokens[: view.S] = ops.ref.sample_ref(logits, view.temperature, view.top_p, view.top_k, gens)
+        return logits
 
     def warmup(self, token_buckets: list[int] | None = None, seq_buckets: list[int] | None = None) -> float:
         """Pre-capture graphs for the given buckets (all-padding metadata)."""
@@ -474,7 +478,7 @@ class ModelRunner:
         return self.meta.host
 
     @torch.inference_mode()
-    def follow_step(self, T: int, S: int, ns: int, nt: int, mode: int):
+    def follow_step(self, T: int, S: int, ns: int, nt: int, mode: int, check: bool = False):
         """Run rank 0's step from the metadata just copied into follower_host_buffer():
         mode 0 = a step (graph replay, captured on first sight exactly as rank 0 does), 1 = the
         hidden-states forward of an embedding request, 2 = capture bucket (T, S) (start-up
@@ -488,8 +492,9 @@ class ModelRunner:
                 self.model.forward(view, self.kv, self.part_size, return_hidden=True)
             elif mode == 0:
                 logits = self.model.forward(view, self.kv, self.part_size)
-                self.last_out = (self.model.last_resid, logits)
                 self.out_tokens[:S] = logits.argmax(-1).int()
+                if check:
+                    self.check_words = self._words(self.model.last_resid, logits, nt, S)
             return
         k = self._k
         if mode == 2:
@@ -516,10 +521,12 @@ class ModelRunner:
         if g is not None:
             self.graph_hits += 1
             g.replay()
-            self.last_out = self.graph_logits.get((T, S))
+            if check:
+                self.check_words = self._words(*g.vg_out, nt, S)
         else:
             lg = self._forward_sample(view)
-            self.last_out = (self.model.last_resid, lg)
+            if check:
+                self.check_words = self._words(self.model.last_resid, lg, nt, S)
 
     def capture_pending(self, max_graphs: int = 64) -> int:
         """Capture the buckets that ran eagerly since the last call (most frequent first).
