@@ -108,6 +108,33 @@ __device__ __forceinline__ RowParams row_params(const SampleArgs& a, int row) {
   return r;
 }
 
+// One element's contribution to a pass (shared by the memory sweep and the register-resident
+// rounds below, so both produce the same bits): mode 0 (max / Z / argmax + Gumbel key), mode 1
+// (count and mass above xj + the key restricted to x > xj). L = logf(fmaxf(-logf(u), 1e-30f)) of
+// this element's uniform for the pass's round (key = v / T - L: a Gumbel draw).
+__device__ __forceinline__ void accum_elem(int mode, float v, int i, float L, float xj, float rmx, const RowParams& rp,
+                                           Acc& acc) {
+  if (mode == 0) {
+    if (v > acc.mx) {
+      acc.z = (acc.mx == -INFINITY ? 0.f : acc.z * exp2f((acc.mx - v) * rp.c)) + 1.f;
+      acc.mx = v;
+      acc.amx = i;
+    } else if (v > -INFINITY) {
+      acc.z += exp2f((v - acc.mx) * rp.c);
+    }
+  } else if (v > xj) {
+    acc.cnt += 1.f;
+    acc.q += exp2f((v - rmx) * rp.c);
+  }
+  if (!rp.greedy && (mode == 0 || v > xj) && v > -INFINITY) {
+    const float g = v * rp.cn - L;
+    if (g > acc.gk) { acc.gk = g; acc.gi = i; }
+  }
+}
+
+// accurate logs: a fast log rounding -log(u) to 0 near u = 1 would make an infinite key
+__device__ __forceinline__ float gumbel_log(float u) { return logf(fmaxf(-logf(u), 1e-30f)); }
+
 // One sweep of float4 range [v_lo, v_hi) of a row by this block (8 float4 loads in flight per
 // thread). mode 0: max / Z / argmax + Gumbel keys; mode 1: acceptance statistics of candidate
 // value xj (count and mass of x > xj, mass relative to the row max rmx) + Gumbel keys restricted
@@ -134,24 +161,8 @@ __device__ __forceinline__ void sweep_range(const float4* x4, int v_lo, int v_hi
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float v = e[j];
-        const int i = 4 * vi + j;
-        if (mode == 0) {
-          if (v > acc.mx) {
-            acc.z = (acc.mx == -INFINITY ? 0.f : acc.z * exp2f((acc.mx - v) * rp.c)) + 1.f;
-            acc.mx = v;
-            acc.amx = i;
-          } else if (v > -INFINITY) {
-            acc.z += exp2f((v - acc.mx) * rp.c);
-          }
-        } else if (v > xj) {
-          acc.cnt += 1.f;
-          acc.q += exp2f((v - rmx) * rp.c);
-        }
-        if (!rp.greedy && (mode == 0 || v > xj) && v > -INFINITY) {
-          // accurate logs: a fast log rounding -log(u) to 0 near u = 1 would make an infinite key
-          const float g = v * rp.cn - logf(fmaxf(-logf(uu[j]), 1e-30f));
-          if (g > acc.gk) { acc.gk = g; acc.gi = i; }
-        }
+        const float L = (!rp.greedy && (mode == 0 || v > xj) && v > -INFINITY) ? gumbel_log(uu[j]) : 0.f;
+        accum_elem(mode, v, 4 * vi + j, L, xj, rmx, rp, acc);
       }
     }
   }
@@ -266,6 +277,70 @@ __device__ __forceinline__ bool gran_gather(const uint4* gbase, int nseg, int mo
   return all_ok;
 }
 
+// Register-resident rounds (sample_gran_kernel): when a block's segment is at most RF4 float4 per
+// thread (every batch up to 8 rows at Qwen / Llama vocabularies: 32-64 segments), pass 0 keeps its
+// logits in registers and also draws the uniforms of the first RROUNDS rejection rounds (their
+// Philox + two logs per element need no logit, so they overlap the loads); those rounds then run
+// from registers — no reload of the segment, no noise work — and only the block merge and the row
+// meeting remain. Same elements, order and formulas as the memory sweep: identical bits. Rounds
+// past RROUNDS (rare) sweep memory as before. With near-uniform logits at top-p 0.9 a row is
+// accepted in round 1 with p ~ 0.9, so a batch of 8 needs round 2+ on most steps: ~10 us each from
+// memory (timeline sample_gran: median block 24.7 us, p90 44.6 us, profiles/r6_base_decode_timeline.log).
+constexpr int RF4 = 8;
+constexpr int RROUNDS = 3;
+
+struct RegSeg {
+  float x[RF4][4];
+  float L[RROUNDS][RF4][4];
+};
+
+__device__ __forceinline__ void regs_pass0(const float4* x4, int v_lo, int v_hi, const RowParams& rp, RegSeg& rs,
+                                           Acc& acc) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+#pragma unroll
+  for (int u = 0; u < RF4; ++u) {
+    const int vi = v_lo + tid + u * nt;
+    const float4 q = vi < v_hi ? x4[vi] : make_float4(0.f, 0.f, 0.f, 0.f);
+    rs.x[u][0] = q.x; rs.x[u][1] = q.y; rs.x[u][2] = q.z; rs.x[u][3] = q.w;
+  }
+  float L0[RF4][4];
+#pragma unroll
+  for (int u = 0; u < RF4; ++u) {
+    const int vi = v_lo + tid + u * nt;
+#pragma unroll
+    for (int r = 0; r <= RROUNDS; ++r) {
+      float uu[4] = {0.5f, 0.5f, 0.5f, 0.5f};
+      if (!rp.greedy && vi < v_hi) philox4(rp.seed, rp.off, (uint32_t)vi, (uint32_t)r, uu);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float L = rp.greedy ? 0.f : gumbel_log(uu[j]);
+        if (r == 0) L0[u][j] = L;
+        else rs.L[r - 1][u][j] = L;
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < RF4; ++u) {
+    const int vi = v_lo + tid + u * nt;
+    if (vi >= v_hi) break;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) accum_elem(0, rs.x[u][j], 4 * vi + j, L0[u][j], 0.f, 0.f, rp, acc);
+  }
+}
+
+template <int R>
+__device__ __forceinline__ void regs_round(int v_lo, int v_hi, float xj, float rmx, const RowParams& rp,
+                                           const RegSeg& rs, Acc& acc) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+#pragma unroll
+  for (int u = 0; u < RF4; ++u) {
+    const int vi = v_lo + tid + u * nt;
+    if (vi >= v_hi) break;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) accum_elem(1, rs.x[u][j], 4 * vi + j, rs.L[R - 1][u][j], xj, rmx, rp, acc);
+  }
+}
+
 template <int NT>
 __global__ __launch_bounds__(NT) void sample_gran_kernel(SampleArgs a) {
   TLScope tl_scope(a.tl);
@@ -281,10 +356,17 @@ __global__ __launch_bounds__(NT) void sample_gran_kernel(SampleArgs a) {
   const float c = rp.c;
   const uint32_t ep = __builtin_amdgcn_readfirstlane(__float_as_uint(ld_sc1(reinterpret_cast<const float*>(a.epoch + row))));
   uint4* rowg = reinterpret_cast<uint4*>(a.gran) + (size_t)row * SAMPLE_GRAN_ROW;  // [parity][SEGS][2]
-  // one pass: sweep, block merge, publish, gather every segment's granules, share the row merge
+  // one pass: sweep (or the register-resident segment), block merge, publish, gather every
+  // segment's granules, share the row merge
+  const bool regs = v_hi - v_lo <= RF4 * NT;  // block-uniform
+  RegSeg rs;
   auto pass = [&](int mode, float xj, float rmx, uint32_t round, uint32_t gen) -> bool {
     Acc acc = acc_init();
-    sweep_range(x4, v_lo, v_hi, mode, xj, rmx, round, rp, acc);
+    if (regs && mode == 0) regs_pass0(x4, v_lo, v_hi, rp, rs, acc);
+    else if (regs && round == 1) regs_round<1>(v_lo, v_hi, xj, rmx, rp, rs, acc);
+    else if (regs && round == 2) regs_round<2>(v_lo, v_hi, xj, rmx, rp, rs, acc);
+    else if (regs && round == 3) regs_round<3>(v_lo, v_hi, xj, rmx, rp, rs, acc);
+    else sweep_range(x4, v_lo, v_hi, mode, xj, rmx, round, rp, acc);
     block_reduce_acc(acc, c, red);
     const uint32_t tag = (ep << 6) | gen;
     uint4* pg = rowg + (size_t)(gen & 1) * SAMPLE_GRAN_SEGS * 2;

@@ -494,7 +494,7 @@ class ModelRunner:
                 logits = self.model.forward(view, self.kv, self.part_size)
                 self.out_tokens[:S] = logits.argmax(-1).int()
                 if check:
-                    self.check_words = self._words(self.model.last_resid, logits, nt, S)
+                    self.check_words = self._words(self.model.last_resid, logits, nt, ns)
             return
         k = self._k
         if mode == 2:
@@ -522,11 +522,11 @@ class ModelRunner:
             self.graph_hits += 1
             g.replay()
             if check:
-                self.check_words = self._words(*g.vg_out, nt, S)
+                self.check_words = self._words(*g.vg_out, nt, ns)
         else:
             lg = self._forward_sample(view)
             if check:
-                self.check_words = self._words(self.model.last_resid, lg, nt, S)
+                self.check_words = self._words(self.model.last_resid, lg, nt, ns)
 
     def capture_pending(self, max_graphs: int = 64) -> int:
         """Capture the buckets that ran eagerly since the last call (most frequent first).
