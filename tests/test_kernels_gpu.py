@@ -376,10 +376,14 @@ def test_sample_segmented_matches_row_kernel_across_batch_sizes():
             kw = dict(top_p=tp[:B], top_k=tk[:B], seeds=seeds[:B], offsets=offs)
             assert C.sample_segments(B, V) > 1
             a = ops.sample(*args, **kw).clone()
+            C.set_sample_regs(False)  # the segmented kernel's memory-sweep rounds
+            m = ops.sample(*args, **kw).clone()
+            C.set_sample_regs(True)
             C.set_sample_nseg(1)
             b = ops.sample(*args, **kw)
             C.set_sample_nseg(64)
             assert torch.equal(a, b), (off, B, a, b)
+            assert torch.equal(a, m), (off, B, a, m)
         B = 8
         offs = torch.full((B,), 7, dtype=torch.int64, device=DEV)
         out = torch.empty(B, dtype=torch.int32, device=DEV)
@@ -402,6 +406,7 @@ def test_sample_segmented_matches_row_kernel_across_batch_sizes():
         assert int(ops.fault_word(DEV)[0].item()) & 16 == 0, "a sampler row wait gave up"
     finally:
         C.set_sample_nseg(64)
+        C.set_sample_regs(True)
 
 
 def test_sample_logprob():
