@@ -4,6 +4,8 @@ epilogue): block spans in a hipGraph, weights cycling through > 600 MB of copies
 launch behind a gate_up-sized stream as in a step.
 
     python benchmarks/probes/half_tile_probe.py
+
+(Measured negative and removed: profiles/r6_half_tile_negative.log. path=5 now runs the default plan.)
 """
 from __future__ import annotations
 
