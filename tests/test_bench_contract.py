@@ -53,3 +53,20 @@ def test_bench_tensor_parallel_two_ranks_cpu(tmp_path):
     assert REQUIRED <= set(r)
     assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp1xtp2" and r["config"]["global_batch"] == 8
     assert r["value"] > 0 and r["failures"] == 0
+
+
+@pytest.mark.timeout(600)
+def test_bench_forensics_account_for_the_timed_wall(tmp_path):
+    """One rank on CPU: the engine thread's timed wall splits into idle + coalesce + busy and that sum
+    matches the timed wall; per-step averages and the wave trace are timed-region
+    fields."""
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="2", VGATE_DRY_RUN="false")
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "1", "--steps", "2", "--warmup", "1", "--model", "tiny",
+           "--max-tokens", "8", "--requests-per-step", "16", "--kv-blocks", "512", "--port", "18340"]
+    p = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=540)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    wall, acc = r["timed_wall_ms"], r["timed_wall_ms_accounted"]
+    assert wall > 0 and abs(acc - wall) / wall < 0.05, (acc, wall)
+    assert r["timed_engine_busy_ms"] > 0 and r["timed_engine_coalesce_ms"] >= 0
+    assert r["engine_avg_step_ms"] is not None and r["engine_avg_step_ms"] > 0
