@@ -142,7 +142,10 @@ __device__ __forceinline__ void epi_pre_a(const GemmParams& p, EpiPre<NTB>& e, i
     e.slot = p.slots[m];
     e.b0 = *reinterpret_cast<const uint2*>(bias + qkv_col(nt0, nsub));
   } else if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_AR || EPI == EPI_F32) {
-    const bf16_t* res = p.res ? p.res + (size_t)m * p.ldr : safe + (size_t)m * p.N;
+    // (no residual: row 0 of the packed weights — in bounds for any m; m * N is not once the tile
+    // kernels prefetch with M up to the prefill bucket: a TP follower's row-parallel GEMMs carry no
+    // residual, and their 448-row steps read past the matrix)
+    const bf16_t* res = p.res ? p.res + (size_t)m * p.ldr : safe;
 #pragma unroll
     for (int j = 0; j < NTB; ++j) {
       const int n = (nt0 + j) * 16 + nsub;

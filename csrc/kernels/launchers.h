@@ -240,7 +240,6 @@ struct SampleArgs {
   void* gran = nullptr;
   uint32_t* epoch = nullptr;
   uint32_t* fault = nullptr;
-  int regs = 1;  // register-resident rejection rounds (set by the launcher from set_sample_regs)
 };
 // sampler workspace (int32 words): [0, SAMPLE_WS_GRAN) per-row epochs, then the granule regions
 constexpr int SAMPLE_GRAN_SEGS = 64;                        // max segments per row
@@ -250,7 +249,6 @@ constexpr int SAMPLE_WS_GRAN = 256;                         // int32 offset of t
 constexpr int SAMPLE_WS_WORDS = SAMPLE_WS_GRAN + SAMPLE_GRAN_ROWS * SAMPLE_GRAN_ROW * 4;
 void launch_sample(const SampleArgs& s, hipStream_t st);
 int sample_segments(int B, int V);
-void set_sample_regs(bool on);  // register-resident rejection rounds on / off (A/B, exactness tests)
 void set_sample_nseg(int n);  // cap on segments per row, 1..SAMPLE_GRAN_SEGS (1 = one block per row)
 
 // Custom one-shot all-reduce over IPC-mapped peer buffers (xGMI).

@@ -277,59 +277,6 @@ __device__ __forceinline__ bool gran_gather(const uint4* gbase, int nseg, int mo
   return all_ok;
 }
 
-// Register-resident rounds (sample_gran_kernel): when a block's segment is at most RF4 float4 per
-// thread (every batch up to 8 rows at Qwen / Llama vocabularies: 32-64 segments), pass 0 keeps its
-// logits in registers, and every pass computes the NEXT round's Gumbel noise (Philox + two logs per
-// element: no logit needed) between publishing its partial and gathering the row's — the wait for
-// the other segments' granules hides it. A rejection round then runs from registers: no reload of
-// the segment, no noise work on the critical path, only the block merge and the row meeting. Same
-// elements, order and formulas as the memory sweep: identical bits. (Precomputing three rounds'
-// noise inside pass 0 instead made pass 0 ~9 us longer than the rounds it saved:
-// profiles/r6_sampler_regs.log.) With near-uniform logits at top-p 0.9 a row is accepted in round 1
-// with p ~ 0.9, so a batch of 8 needs round 2+ on most steps: ~10 us each from memory.
-constexpr int RF4 = 8;
-
-struct RegSeg {
-  float x[RF4][4];
-  float L[RF4][4];  // L of the round the next pass runs
-};
-
-// Gumbel logs of round `round` for this thread's elements (skipped for greedy rows: keys unused)
-__device__ __forceinline__ void regs_noise(int v_lo, int v_hi, const RowParams& rp, uint32_t round, RegSeg& rs) {
-  if (rp.greedy) return;
-  const int tid = threadIdx.x, nt = blockDim.x;
-#pragma unroll
-  for (int u = 0; u < RF4; ++u) {
-    const int vi = v_lo + tid + u * nt;
-    float uu[4] = {0.5f, 0.5f, 0.5f, 0.5f};
-    if (vi < v_hi) philox4(rp.seed, rp.off, (uint32_t)vi, round, uu);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) rs.L[u][j] = gumbel_log(uu[j]);
-  }
-}
-
-__device__ __forceinline__ void regs_load(const float4* x4, int v_lo, int v_hi, RegSeg& rs) {
-  const int tid = threadIdx.x, nt = blockDim.x;
-#pragma unroll
-  for (int u = 0; u < RF4; ++u) {
-    const int vi = v_lo + tid + u * nt;
-    const float4 q = vi < v_hi ? x4[vi] : make_float4(0.f, 0.f, 0.f, 0.f);
-    rs.x[u][0] = q.x; rs.x[u][1] = q.y; rs.x[u][2] = q.z; rs.x[u][3] = q.w;
-  }
-}
-
-__device__ __forceinline__ void regs_pass(int mode, int v_lo, int v_hi, float xj, float rmx, const RowParams& rp,
-                                          const RegSeg& rs, Acc& acc) {
-  const int tid = threadIdx.x, nt = blockDim.x;
-#pragma unroll
-  for (int u = 0; u < RF4; ++u) {
-    const int vi = v_lo + tid + u * nt;
-    if (vi >= v_hi) break;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) accum_elem(mode, rs.x[u][j], 4 * vi + j, rs.L[u][j], xj, rmx, rp, acc);
-  }
-}
-
 template <int NT>
 __global__ __launch_bounds__(NT) void sample_gran_kernel(SampleArgs a) {
   TLScope tl_scope(a.tl);
@@ -345,26 +292,16 @@ __global__ __launch_bounds__(NT) void sample_gran_kernel(SampleArgs a) {
   const float c = rp.c;
   const uint32_t ep = __builtin_amdgcn_readfirstlane(__float_as_uint(ld_sc1(reinterpret_cast<const float*>(a.epoch + row))));
   uint4* rowg = reinterpret_cast<uint4*>(a.gran) + (size_t)row * SAMPLE_GRAN_ROW;  // [parity][SEGS][2]
-  // one pass: sweep (or the register-resident segment), block merge, publish, gather every
-  // segment's granules, share the row merge
-  const bool regs = a.regs && v_hi - v_lo <= RF4 * NT;  // block-uniform
-  RegSeg rs;
-  if (regs) {
-    regs_load(x4, v_lo, v_hi, rs);
-    regs_noise(v_lo, v_hi, rp, 0u, rs);
-  }
+  // one pass: sweep, block merge, publish, gather every segment's granules, share the row merge
   auto pass = [&](int mode, float xj, float rmx, uint32_t round, uint32_t gen) -> bool {
     Acc acc = acc_init();
-    if (regs) regs_pass(mode, v_lo, v_hi, xj, rmx, rp, rs, acc);
-    else sweep_range(x4, v_lo, v_hi, mode, xj, rmx, round, rp, acc);
+    sweep_range(x4, v_lo, v_hi, mode, xj, rmx, round, rp, acc);
     block_reduce_acc(acc, c, red);
     const uint32_t tag = (ep << 6) | gen;
     uint4* pg = rowg + (size_t)(gen & 1) * SAMPLE_GRAN_SEGS * 2;
     if (tid == 0) {
       gran_publish(pg + 2 * seg, acc, mode, tag);
     }
-    // the next round's noise while the row's other segments publish (rows with top-k / top-p only)
-    if (regs && (rp.use_k || rp.use_p)) regs_noise(v_lo, v_hi, rp, round + 1, rs);
     if (tid < 64) {
       Acc r;
       const bool ok = gran_gather(pg, nseg, mode, tag, c, r, a.fault);
@@ -405,8 +342,6 @@ __global__ __launch_bounds__(NT) void sample_gran_kernel(SampleArgs a) {
 
 int g_sample_nseg = SAMPLE_GRAN_SEGS;  // segments per row cap (set_sample_nseg; benchmarks/sampler_stress.py)
 void set_sample_nseg(int n) { g_sample_nseg = n < 1 ? 1 : (n > SAMPLE_GRAN_SEGS ? SAMPLE_GRAN_SEGS : n); }
-bool g_sample_regs = true;  // register-resident rounds (set_sample_regs: A/B and exactness tests)
-void set_sample_regs(bool on) { g_sample_regs = on; }
 
 int sample_segments(int B, int V) {
   const int V4 = V >> 2;
@@ -421,7 +356,6 @@ void launch_sample(const SampleArgs& s, hipStream_t st) {
   if (s.B <= 0) return;
   const int nseg = sample_segments(s.B, s.V);
   SampleArgs a = s;
-  a.regs = g_sample_regs ? 1 : 0;
   if (nseg > 1 && s.gran != nullptr && s.epoch != nullptr && s.B <= SAMPLE_GRAN_ROWS) {
     a.tl = tl_take("sample_gran", nseg * s.B);
     // 256 threads per block: 512 / 1024 measured no faster / slower (profiles/r4_sampler_single_launch.log)

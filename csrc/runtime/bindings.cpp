@@ -663,7 +663,6 @@ PYBIND11_MODULE(_C, m) {
         py::arg("fault") = py::none());
   m.def("sample_segments", &vgate::sample_segments, "blocks per row the sampler uses for (B, V)");
   m.def("set_sample_nseg", &vgate::set_sample_nseg, "cap the sampler's segments per row (1 = one block per row)");
-  m.def("set_sample_regs", &vgate::set_sample_regs, "sampler: register-resident rejection rounds on / off");
   m.attr("SAMPLE_WS_WORDS") = vgate::SAMPLE_WS_WORDS;
   m.def("kernel_copy", &kernel_copy, "pinned host <-> device copy by a kernel on the current stream (no SDMA)",
         py::arg("dst"), py::arg("src"), py::arg("nbytes"));

@@ -376,14 +376,10 @@ def test_sample_segmented_matches_row_kernel_across_batch_sizes():
             kw = dict(top_p=tp[:B], top_k=tk[:B], seeds=seeds[:B], offsets=offs)
             assert C.sample_segments(B, V) > 1
             a = ops.sample(*args, **kw).clone()
-            C.set_sample_regs(False)  # the segmented kernel's memory-sweep rounds
-            m = ops.sample(*args, **kw).clone()
-            C.set_sample_regs(True)
             C.set_sample_nseg(1)
             b = ops.sample(*args, **kw)
             C.set_sample_nseg(64)
             assert torch.equal(a, b), (off, B, a, b)
-            assert torch.equal(a, m), (off, B, a, m)
         B = 8
         offs = torch.full((B,), 7, dtype=torch.int64, device=DEV)
         out = torch.empty(B, dtype=torch.int32, device=DEV)
@@ -406,7 +402,6 @@ def test_sample_segmented_matches_row_kernel_across_batch_sizes():
         assert int(ops.fault_word(DEV)[0].item()) & 16 == 0, "a sampler row wait gave up"
     finally:
         C.set_sample_nseg(64)
-        C.set_sample_regs(True)
 
 
 def test_sample_logprob():
@@ -1088,6 +1083,19 @@ def test_gemm_tile3_two_deep_pipeline(M, K):
     assert _rel_err(q3.float().cpu(), xq[:, : hq * D].float()) < 1e-2
     assert _rel_err(k3.float().cpu(), kc2.float()) < 1e-2 and _rel_err(v3.float().cpu(), vc2.float()) < 1e-2
     assert torch.equal(q3, q1) and torch.equal(k3, k1) and torch.equal(v3, v1)
+
+
+def test_tile_kernel_no_residual_small_k_large_m():
+    """The tile kernels prefetch every m-tile's epilogue words; without a residual (a TP follower's
+    row-parallel GEMM) those reads must stay inside the packed weights at any M (round 6: M x N past
+    a 256 x 256 matrix faulted the TP = 2 tests)."""
+    torch.manual_seed(77)
+    M, N, K = 640, 256, 256
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    y = ops.linear(x, ops.Linear(w), waves=-1)
+    torch.cuda.synchronize()
+    assert _rel_err(y.float().cpu(), ref.linear_ref(x.cpu(), w.cpu()).float()) < 1e-2
 
 
 @pytest.mark.parametrize("layout", ["plain", "silu", "qkv"])
