@@ -5,7 +5,7 @@ back-to-back launches (weights warm in the Infinity Cache / L2). Inside a prefil
 reads its weights cold. This times every candidate both ways, plus hipBLASLt (torch.mm, oracle)
 cold, and prints the best of each per (shape, M).
 
-    python benchmarks/probes/prefill_cold_sweep.py [--ms 320,448,640]
+    python benchmarks/probes/prefill_cold_sweep.py [--ms 320,448,640] [--model llama8b] [--only 1024,1025]
 """
 from __future__ import annotations
 
@@ -21,13 +21,17 @@ import torch  # noqa: E402
 
 from vgate import ops  # noqa: E402
 
-SHAPES = [("qkv", 2048, 1536), ("o", 1536, 1536), ("gate_up", 17920, 1536), ("down", 1536, 8960)]
+SHAPES = {"qwen": [("qkv", 2048, 1536), ("o", 1536, 1536), ("gate_up", 17920, 1536), ("down", 1536, 8960)],
+          "llama8b": [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096), ("down", 4096, 14336)]}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ms", default="320,448,640")
     ap.add_argument("--iters", type=int, default=4)
+    ap.add_argument("--model", default="qwen", choices=sorted(SHAPES))
+    ap.add_argument("--only", default="", help="comma list of tile codes to time (default: every candidate)")
+    ap.add_argument("--norm", action="store_true", help="with the folded RMSNorm row scale (qkv / gate_up in a step)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     C = ops.native()
@@ -57,7 +61,9 @@ def main():
         return 1e3 * s0.elapsed_time(s1) / a.iters
 
     cands = ops.PREFILL_CANDIDATES + ops.PREFILL_RING_CANDIDATES
-    for name, N, K in SHAPES:
+    cands += [(t, s) for t in (1025, 769, 1026, 770) for s in (0, 1, 2, 4, 8) if (t, s) not in cands]  # persistent: tail slices
+    only = {int(c) for c in a.only.split(",") if c}
+    for name, N, K in SHAPES[a.model]:
         w = (torch.randn(N, K, device=dev) / math.sqrt(K)).bfloat16()
         wp = ops.pack_weight(w)
         for M in [int(m) for m in a.ms.split(",")]:
@@ -65,7 +71,12 @@ def main():
             out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             rows = {}
             for bn, sk in cands + [("tile", 0), ("tile3", 0)]:
+                if only and (not isinstance(bn, int) or bn not in only):
+                    continue
                 kw = dict(waves=-1) if bn == "tile" else dict(waves=-2) if bn == "tile3" else ops._plan_kw((bn, sk), M)
+
+                if a.norm:
+                    kw = dict(kw, rownorm=True, eps=1e-6)
 
                 def run(kw=kw):
                     C.gemm(x, wp, N, K, out, 0, ws=ws, **kw)

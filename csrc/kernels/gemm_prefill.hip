@@ -350,30 +350,37 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_prefill2_kernel(GemmPara
 // Group sizes per wave: 4 / 2 / 2 pieces -> the waits of phases 0 / 1 / 2: vmcnt(4) / (6) / (6).
 // BN = 128: the same schedule on a 256 x 128 tile (wave 64 n x 64 m, 8 MFMAs per phase, 96 KiB;
 // groups 3 / 2 / 1 pieces per wave -> vmcnt(3) / (4) / (5)).
-template <int BN, int EPI, int NORM, int NTB>
-__global__ __launch_bounds__(512, 1) void gemm_prefill4_kernel(GemmParams p) {
-  constexpr int BM = 256, KS = 2;
-  constexpr int WTN = BN / 16, XTM = BM / 16;  // W + x tiles per block (16 / 8 + 16)
-  constexpr int NWN = WTN / 2, NH = NWN / 2;   // n-tiles per wave, per n-half
-  constexpr int STAGE = (WTN + XTM) * KS * 1024;
-  constexpr int G0 = 4 * NH + 16, G1 = 16, G2 = 4 * NH;  // pieces per group (block)
-  constexpr int P0 = G0 / 8, P1 = G1 / 8, P2 = G2 / 8;  // per wave
-  constexpr int PPW = P0 + P1 + P2;
+typedef __bf16 p4_bf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float sumsq8(uint4 v, float acc) {
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(p4_bf2, v.x), __builtin_bit_cast(p4_bf2, v.x), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(p4_bf2, v.y), __builtin_bit_cast(p4_bf2, v.y), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(p4_bf2, v.z), __builtin_bit_cast(p4_bf2, v.z), acc, false);
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(p4_bf2, v.w), __builtin_bit_cast(p4_bf2, v.w), acc, false);
+}
+
+template <int BN>
+struct P4 {  // geometry of the 4-phase 256 x BN kernel
+  static constexpr int BM = 256, KS = 2;
+  static constexpr int WTN = BN / 16, XTM = BM / 16;  // W + x tiles per block (16 / 8 + 16)
+  static constexpr int NWN = WTN / 2, NH = NWN / 2;   // n-tiles per wave, per n-half
+  static constexpr int STAGE = (WTN + XTM) * KS * 1024;
+  static constexpr int G0 = 4 * NH + 16, G1 = 16, G2 = 4 * NH;  // pieces per group (block)
+  static constexpr int P0 = G0 / 8, P1 = G1 / 8, P2 = G2 / 8;  // per wave
+  static constexpr int PPW = P0 + P1 + P2;
   static_assert(G0 % 8 == 0 && G2 % 8 == 0 && (BN == 256 || BN == 128), "pieces split over 8 waves");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  TLScope tl_scope(p.dbg_ts);
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+};
+
+// The K loop of the 4-phase kernel over K-tiles [kst0, kst0 + nk) of the block tile (m0, nt_blk),
+// accumulated into acc / ss (zeroed by the caller). Ends with every DMA of this wave landed (the
+// trailing clamped duplicates included); a caller that runs it again on the same LDS barriers first.
+template <int BN, int NORM>
+__device__ __forceinline__ void p4_kloop(const GemmParams& p, char* smem, int wid, int lane, int m0, int nt_blk,
+                                         int kst0, int nk, f32x4 (&acc)[BN / 32][4], float (&ss)[4]) {
+  using G = P4<BN>;
+  constexpr int KS = G::KS, WTN = G::WTN, NWN = G::NWN, NH = G::NH, STAGE = G::STAGE;
+  constexpr int P0 = G::P0, P1 = G::P1, P2 = G::P2, PPW = G::PPW;
   const int wr = wid >> 2, wc = wid & 3;
   const int KT = p.K >> 5;
-  const int nk_all = p.K >> 6;
-  const int z = blockIdx.y, nz = gridDim.y;
-  const int kst0 = (nk_all * z) / nz, nk = (nk_all * (z + 1)) / nz - kst0;
-  const int mblocks = (p.M + BM - 1) / BM;
-  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-  const int m0 = (wgid % mblocks) * BM;
-  const int nt_blk = (wgid / mblocks) * WTN;
   // this wave's pieces: entries of the group lists (block-local tile, k-step; W or x)
   //   group 0: the n0 W tiles of both wave rows, then x tiles {4c, 4c + 1}, x 2 k-steps
   //   group 1: x tiles {4c + 2, 4c + 3} x 2
@@ -429,12 +436,6 @@ __global__ __launch_bounds__(512, 1) void gemm_prefill4_kernel(GemmParams p) {
       glds16(src[i] + (size_t)st * step[i], __builtin_amdgcn_readfirstlane(lds0 + buf * STAGE + dst[i]));
     }
   };
-  f32x4 acc[NWN][4];
-#pragma unroll
-  for (int a = 0; a < NWN; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float ss[4] = {0.f, 0.f, 0.f, 0.f};
   uint4 wf[KS][NH], x0[KS][2], x1[KS][2];
   auto read_w = [&](const char* sb, int half) {
 #pragma unroll
@@ -449,16 +450,18 @@ __global__ __launch_bounds__(512, 1) void gemm_prefill4_kernel(GemmParams p) {
 #pragma unroll
       for (int b = 0; b < 2; ++b)
         xf[ks][b] = *reinterpret_cast<const uint4*>(sb + (WTN * KS + (wc * 4 + half * 2 + b) * KS + ks) * 1024 + lane * 16);
+    // folded RMSNorm: x^2 of the rows in packed bf16 dot products (v_dot2_f32_bf16: one op per 2
+    // elements, no unpack), and only in wave row 0 — wave row 1 reads the same x tiles; the row
+    // sums reach it through LDS in p4_finish. (The unpack + FMA form in both wave rows cost the
+    // folded-norm GEMMs ~20 % against the same tile without the norm: Llama-3-8B gate_up at
+    // 2048 rows 472 vs 399 us.)
     if constexpr (NORM == 2) {
+      if (wr == 0) {
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
+        for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          float f[8];
-          unpack8(xf[ks][b], f);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) ss[half * 2 + b] += f[j] * f[j];
-        }
+          for (int b = 0; b < 2; ++b) ss[half * 2 + b] = sumsq8(xf[ks][b], ss[half * 2 + b]);
+      }
     }
   };
   auto quadrant = [&](int nh, int mh, const uint4 (&xf)[KS][2]) {
@@ -498,6 +501,75 @@ __global__ __launch_bounds__(512, 1) void gemm_prefill4_kernel(GemmParams p) {
     quadrant(1, 0, x0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing duplicate DMAs
+}
+
+// the epilogue of a finished 256 x BN block tile straight from the accumulators (deferred row scale)
+// (NORM == 2: the row sums of squares are in wave row 0's ss; wave row 1 gets them through the 1 KiB
+// LDS area P4_ROWSS past the ring — block-uniform call, one barrier)
+constexpr int P4_ROWSS = 16;  // byte offset past the 2-stage ring (the queue item word sits at +0)
+template <int BN, int EPI, int NORM, int NTB>
+__device__ __forceinline__ void p4_finish(const GemmParams& p, char* smem, int wid, int lane, int m0, int nt_blk,
+                                          f32x4 (&acc)[BN / 32][4], const float (&ss)[4]) {
+  constexpr int NWN = P4<BN>::NWN;
+  const int wr = wid >> 2, wc = wid & 3;
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (NORM == 2) {
+    float* rows = reinterpret_cast<float*>(smem + 2 * P4<BN>::STAGE + P4_ROWSS);
+    if (wr == 0) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        float s2 = ss[b];
+        s2 += xor16(s2);
+        s2 += xor32(s2);
+        rs[b] = s2;
+        if (lane < 16) rows[wc * 64 + b * 16 + lane] = s2;
+      }
+    }
+    lds_barrier();
+    if (wr != 0) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) rs[b] = rows[wc * 64 + b * 16 + (lane & 15)];
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int m = m0 + wc * 64 + b * 16 + (lane & 15);
+    float sc = 1.f;
+    if constexpr (NORM == 2) sc = rsqrtf(rs[b] / (float)p.K + p.eps);
+#pragma unroll
+    for (int a = 0; a < NWN; a += NTB) {
+      f32x4 v[NTB];
+#pragma unroll
+      for (int j = 0; j < NTB; ++j) v[j] = acc[a + j][b] * sc;
+      epilogue<NTB, EPI, false>(p, v, m, nt_blk + wr * NWN + a, 4 * (lane >> 4), EpiPre<NTB>{}, m < p.M);
+    }
+  }
+}
+
+template <int BN, int EPI, int NORM, int NTB>
+__global__ __launch_bounds__(512, 1) void gemm_prefill4_kernel(GemmParams p) {
+  using G = P4<BN>;
+  constexpr int BM = G::BM, WTN = G::WTN, NWN = G::NWN;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  TLScope tl_scope(p.dbg_ts);
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int nk_all = p.K >> 6;
+  const int z = blockIdx.y, nz = gridDim.y;
+  const int kst0 = (nk_all * z) / nz, nk = (nk_all * (z + 1)) / nz - kst0;
+  const int mblocks = (p.M + BM - 1) / BM;
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int m0 = (wgid % mblocks) * BM;
+  const int nt_blk = (wgid / mblocks) * WTN;
+  f32x4 acc[NWN][4];
+#pragma unroll
+  for (int a = 0; a < NWN; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ss[4] = {0.f, 0.f, 0.f, 0.f};
+  p4_kloop<BN, NORM>(p, smem, wid, lane, m0, nt_blk, kst0, nk, acc, ss);
   if (nz > 1) {
     float* part = p.slabs + (size_t)z * p.M * p.N;
     float* ssq = p.slabs + (size_t)nz * p.M * p.N + (size_t)z * p.M;
@@ -520,22 +592,167 @@ __global__ __launch_bounds__(512, 1) void gemm_prefill4_kernel(GemmParams p) {
     }
     return;
   }
-#pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    const int m = m0 + wc * 64 + b * 16 + (lane & 15);
-    float sc = 1.f;
-    if constexpr (NORM == 2) {
-      float s2 = ss[b];
-      s2 += xor16(s2);
-      s2 += xor32(s2);
-      sc = rsqrtf(s2 / (float)p.K + p.eps);
+  p4_finish<BN, EPI, NORM, NTB>(p, smem, wid, lane, m0, nt_blk, acc, ss);
+}
+
+// ---- persistent form of the 4-phase kernel: whole rounds + a K-split last round, one launch ----
+// A tile grid of T tiles on G CUs takes ceil(T / G) rounds and the last one runs R = T mod G tiles
+// on a fraction of the chip (Llama-3-8B gate_up at 2048 rows: 896 tiles = 3 rounds + 128 tiles; o /
+// down: 128 tiles = half the chip). Here G = #CU resident blocks (one per CU: the LDS ring) run the
+// T - R tiles of the whole rounds in order — block g takes tile r * G + g in round r, so each XCD
+// keeps working on 4 weight panels x all m-blocks at the same K position, as the tile grid does
+// (the L2 reuse a free (tile, K-tile) stream-K split loses: its blocks sit at unrelated K offsets
+// and it measured 1.3x SLOWER than the tile grid, profiles/r6_prefill_stream_k.log) — and then
+// the R tail tiles as S K slices each (S = G / R, >= 4 K-tiles per slice): unit g = c * R + j is
+// slice c of tail tile j, so the blocks of one XCD again share panels and K positions. Slices
+// c > 0 publish their fp32 partial (+ the x sums of squares of the folded RMSNorm) to their own
+// slot with device-coherent stores and count in on the tile's ticket; slice 0 (the owner) waits
+// for the S - 1 tickets, adds the partials in slice order (bit-reproducible), runs the epilogue and
+// clears the ticket. Nothing waits on a block that waits: the owners are the only waiters, and the
+// poll is bounded all the same (give-up: bit 64 of the fault word, garbage, never a hang).
+constexpr int P4SK_SPIN = 1 << 20;
+
+template <int BN>
+__host__ __device__ constexpr int p4sk_slot_floats() {
+  return (P4<BN>::NWN * 4 + 1) * 512 * 4;  // 512 threads x (NWN x 4 accumulators + the row sums) f32x4
+}
+
+// slot traffic: lane part in ONE VGPR (tid * 16), the accumulator index in the scalar offset (a
+// per-index VGPR offset is loop-invariant, gets hoisted over the K loop and spills the 256-wide tile)
+__device__ __forceinline__ void p4sk_st(float* slot, int tid, int j, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, rsrc_of(slot), (uint32_t)tid * 16, j * 8192, 16 /* sc1 */);
+}
+__device__ __forceinline__ f32x4 p4sk_ld(const float* slot, int tid, int j) {
+  return __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(slot), (uint32_t)tid * 16, j * 8192, 16 /* sc1 */);
+}
+
+// DYN: the work items are taken from per-XCD queues instead of a fixed list per block: an XCD's
+// items are the same as in the static form (its tile panels, then its tail units, the K slices
+// c > 0 ahead of the owners so an owner only ever waits for items already taken), and whichever
+// of its CUs frees up first takes the next one, as the hardware's dispatch of a tile grid does.
+// Queue heads at counters[qbase .. qbase + 7], a block count at qbase + 8: the last block out
+// resets all nine.
+template <int BN, int EPI, int NORM, int NTB, bool DYN>
+__global__ __launch_bounds__(512, 1) void gemm_prefill4sk_kernel(GemmParams p0, int tiles, int S, int qbase) {
+  using G = P4<BN>;
+  constexpr int BM = G::BM, WTN = G::WTN, NWN = G::NWN, NACC = NWN * 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  TLScope tl_scope(p0.dbg_ts);
+  const int KT = p0.K >> 6;
+  const int mblocks = (p0.M + BM - 1) / BM;
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  // XCD-aware: consecutive g (tiles of one weight column panel, m-blocks fastest) on one XCD
+  const int gx0 = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q, nx = q + (xcd < r ? 1 : 0);
+  const int g = gx0 + (orig >> 3);
+  const int full = tiles / nwg, R = tiles - full * nwg;
+  // this XCD's tail units g' in [gx0, gx0 + nx) with g' < R * S: K slices c > 0 (g' >= R) first
+  const int t1 = min(gx0 + nx, R * S), ncon = max(0, t1 - max(gx0, R)), ntail = max(0, t1 - gx0);
+  const int nseg = DYN ? full * nx + ntail : full + (g < R * S ? 1 : 0);
+  uint32_t* qhead = p0.counters + qbase + xcd;
+  int* lds_item = reinterpret_cast<int*>(smem + 2 * G::STAGE);
+  int nxt = 0;
+  if (DYN && threadIdx.x == 0) nxt = (int)__hip_atomic_fetch_add(qhead, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const auto kp0 = (const GemmParams __attribute__((address_space(4)))*)(__builtin_amdgcn_kernarg_segment_ptr());
+  for (int i = 0;; ++i) {  // block-uniform
+    int item = i;
+    if constexpr (DYN) {
+      if (threadIdx.x == 0) *lds_item = nxt;
+      __syncthreads();  // also: the previous item's LDS reads + DMAs are done
+      item = __builtin_amdgcn_readfirstlane(*lds_item);
+      if (item >= nseg) break;
+      if (threadIdx.x == 0)  // the next grab's latency hides under this item
+        nxt = (int)__hip_atomic_fetch_add(qhead, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (i >= nseg) break;
+      if (i > 0) __builtin_amdgcn_s_barrier();  // the previous tile's LDS reads + DMAs are done
     }
+    // the parameters re-read from the kernel-argument segment per tile: hoisted out of this loop,
+    // the epilogue's pointers would sit in SGPRs across the K loop (SGPR spills into VGPR lanes);
+    // thread ids laundered likewise (no lane-derived epilogue / slot address stays live across it)
+    auto kp = kp0;
+    asm volatile("" : "+s"(kp));
+    const GemmParams& p = *(const GemmParams*)kp;
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int tile, k0 = 0, k1 = KT, c = -1, j = 0;
+    bool tail;
+    int gu;  // the tail unit
+    if constexpr (DYN) {
+      tail = item >= full * nx;
+      tile = (item / max(nx, 1)) * nwg + gx0 + item % max(nx, 1);
+      const int e = item - full * nx;
+      gu = e < ncon ? max(gx0, R) + e : gx0 + (e - ncon);
+    } else {
+      tail = item == full;
+      tile = item * nwg + g;
+      gu = g;
+    }
+    if (tail) {  // slice c of tail tile j
+      j = gu % R;
+      c = gu / R;
+      tile = full * nwg + j;
+      k0 = (KT * c) / S;
+      k1 = (KT * (c + 1)) / S;
+    }
+    const int m0 = (tile % mblocks) * BM, nt_blk = (tile / mblocks) * WTN;
+    f32x4 acc[NWN][4];
 #pragma unroll
-    for (int a = 0; a < NWN; a += NTB) {
-      f32x4 v[NTB];
+    for (int a = 0; a < NWN; ++a)
 #pragma unroll
-      for (int j = 0; j < NTB; ++j) v[j] = acc[a + j][b] * sc;
-      epilogue<NTB, EPI, false>(p, v, m, nt_blk + wr * NWN + a, 4 * (lane >> 4), EpiPre<NTB>{}, m < p.M);
+      for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float ss[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c > 0) {  // a later K slice of a tail tile: publish, count in (its own copy of the K loop: with
+                  // one copy shared by this path and the owner's the allocator spills the accumulators)
+      p4_kloop<BN, NORM>(p, smem, wid, lane, m0, nt_blk, k0, k1 - k0, acc, ss);
+      float* slot = p.slabs + (size_t)gu * p4sk_slot_floats<BN>();
+#pragma unroll
+      for (int e = 0; e < NACC; ++e) p4sk_st(slot, tid, e, acc[e >> 2][e & 3]);
+      if constexpr (NORM == 2) p4sk_st(slot, tid, NACC, f32x4{ss[0], ss[1], ss[2], ss[3]});
+      drain_stores();
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(p.counters + j, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      continue;
+    }
+    p4_kloop<BN, NORM>(p, smem, wid, lane, m0, nt_blk, k0, k1 - k0, acc, ss);
+    if (c == 0 && S > 1) {  // the owner of a split tail tile: wait for slices 1 .. S - 1, add in order
+      if (tid == 0) {
+        int spins = 0;
+        while (__hip_atomic_load(p.counters + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)(S - 1)) {
+          if (++spins > P4SK_SPIN) {
+            if (p.fault != nullptr) atomicOr(p.fault, 64u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+      for (int cc = 1; cc < S; ++cc) {
+        const float* slot = p.slabs + (size_t)(cc * R + j) * p4sk_slot_floats<BN>();
+        // a quarter of the accumulators per round trip (the loads' registers: 32 / 16 per lane)
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          f32x4 v[NACC / 4];
+#pragma unroll
+          for (int e = 0; e < NACC / 4; ++e) v[e] = p4sk_ld(slot, tid, h * NACC / 4 + e);
+#pragma unroll
+          for (int e = 0; e < NACC / 4; ++e) acc[(h * NACC / 4 + e) >> 2][(h * NACC / 4 + e) & 3] += v[e];
+          asm volatile("" ::: "memory");
+        }
+        if constexpr (NORM == 2) {
+          const f32x4 s4 = p4sk_ld(slot, tid, NACC);
+          ss[0] += s4[0]; ss[1] += s4[1]; ss[2] += s4[2]; ss[3] += s4[3];
+        }
+      }
+      if (tid == 0) __hip_atomic_store(p.counters + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    p4_finish<BN, EPI, NORM, NTB>(p, smem, wid, lane, m0, nt_blk, acc, ss);
+  }
+  if (DYN && threadIdx.x == 0) {  // every grab of this block is done: the last block out resets the queues
+    uint32_t* done = p0.counters + qbase + 8;
+    if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(nwg - 1)) {
+      for (int x = 0; x < 9; ++x) __hip_atomic_store(p0.counters + qbase + x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -641,18 +858,60 @@ static void launch_prefill4_cfg(const GemmParams& p, int nz, hipStream_t st) {
   GemmParams q = p;
   if (q.dbg_ts == nullptr) q.dbg_ts = tl_take("gemm_prefill4", blocks * nz);
   auto kern = gemm_prefill4_kernel<BN, EPI, NORM, NTB>;
+  constexpr int LDS = 2 * STAGE + P4_ROWSS + 1024;  // ring + the folded norm's row sums
   static bool attr = [&] {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               2 * STAGE) == hipSuccess;
+                               LDS) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL(kern, dim3(blocks, nz), dim3(512), 2 * STAGE, st, q);
+  hipLaunchKernelGGL(kern, dim3(blocks, nz), dim3(512), LDS, st, q);
   if (nz > 1) {
     const int groups = ((p.M + 15) / 16) * (p.N / (16 * NTB));
     GemmParams r = p;
     r.dbg_ts = tl_take("prefill_reduce", (groups + 3) / 4);
     hipLaunchKernelGGL((prefill_reduce_kernel<EPI, NORM, NTB>), dim3((groups + 3) / 4), dim3(256), 0, st, r, nz);
   }
+}
+
+static int cu_count() {
+  static const int n = [] {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      c = 0;
+    return c;
+  }();
+  return n;
+}
+
+// persistent 4-phase kernel (whole rounds + the K-split tail), one block per CU; slices = the tail's K
+// slices (0: G / R, at least 4 K-tiles each, at most 8). false = not taken (no tail to split, no
+// tickets / slot room)
+template <int EPI, int NORM, int NTB, int BN, bool DYN = false>
+static bool launch_prefill4sk_cfg(const GemmParams& p, int slices, int max_counters, size_t slab_bytes,
+                                  hipStream_t st) {
+  constexpr int STAGE = (BN / 16 + 16) * 2 * 1024;
+  const int tiles = ((p.M + 255) / 256) * (p.N / BN);
+  const int G = cu_count();
+  if (G <= 0 || p.counters == nullptr || p.slabs == nullptr) return false;
+  const int R = tiles % G, KT = p.K / 64;
+  if (R == 0) return false;  // whole rounds: the tile grid is the same schedule
+  int S = slices > 0 ? slices : G / R;
+  S = S > G / R ? G / R : S;
+  S = S > 8 && slices <= 0 ? 8 : S;
+  while (S > 1 && KT / S < 4) --S;
+  const int qbase = max_counters - 9;  // DYN: the queue heads + block count, above the tail tickets
+  if (S < 1 || R > qbase || (size_t)G * p4sk_slot_floats<BN>() * 4 > slab_bytes) return false;
+  GemmParams q = p;
+  if (q.dbg_ts == nullptr) q.dbg_ts = tl_take("gemm_prefill4sk", G);
+  auto kern = gemm_prefill4sk_kernel<BN, EPI, NORM, NTB, DYN>;
+  constexpr int LDS = 2 * STAGE + P4_ROWSS + 1024;  // ring + the queue item word + the row sums
+  static bool attr = [&] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               LDS) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL(kern, dim3(G), dim3(512), LDS, st, q, tiles, S, qbase);
+  return true;
 }
 
 template <int BM, int BN, int EPI, int NORM, int NTB>
@@ -678,7 +937,8 @@ static void launch_prefill_cfg(const GemmParams& p, int nz, hipStream_t st) {
 // Returns false for shapes the kernel does not take (the caller keeps the N-split tile
 // kernel): K % 64, N % 64, a row gather, the gamma-in-registers RMSNorm mode.
 template <int EPI, int NORM>
-static bool launch_prefill_epi(const GemmParams& p, int force_bn, int force_sk, size_t slab_bytes, hipStream_t st) {
+static bool launch_prefill_epi(const GemmParams& p, int force_bn, int force_sk, size_t slab_bytes, int max_counters,
+                               hipStream_t st) {
   constexpr int NTB = 1;  // every epilogue works on self-contained 16-column tiles
   if (p.K % 64 != 0 || p.N % 64 != 0 || p.row_idx != nullptr) return false;
   const int mb = (p.M + 127) / 128;
@@ -727,6 +987,32 @@ static bool launch_prefill_epi(const GemmParams& p, int force_bn, int force_sk, 
   if (force_bn == 1024) {  // v4: the 4-phase 256 x 256 kernel (sweeps / tests)
     if (p.N % 256 != 0) return false;
     launch_prefill4_cfg<EPI, NORM, NTB>(p, nz, st);
+    return true;
+  }
+  // persistent forms of the 4-phase kernel, K-split tail (start-up tuner candidates; force_sk = the
+  // tail's K slices); declined -> the tile grid
+  if (force_bn == 1025) {
+    if (p.N % 256 != 0) return false;
+    if (!launch_prefill4sk_cfg<EPI, NORM, NTB, 256>(p, force_sk, max_counters, slab_bytes, st))
+      launch_prefill4_cfg<EPI, NORM, NTB>(p, 1, st);
+    return true;
+  }
+  if (force_bn == 769) {
+    if (p.N % 128 != 0) return false;
+    if (!launch_prefill4sk_cfg<EPI, NORM, NTB, 128>(p, force_sk, max_counters, slab_bytes, st))
+      launch_prefill4_cfg<EPI, NORM, NTB, 128>(p, 1, st);
+    return true;
+  }
+  if (force_bn == 1026) {  // the same, items from per-XCD queues
+    if (p.N % 256 != 0) return false;
+    if (!launch_prefill4sk_cfg<EPI, NORM, NTB, 256, true>(p, force_sk, max_counters, slab_bytes, st))
+      launch_prefill4_cfg<EPI, NORM, NTB>(p, 1, st);
+    return true;
+  }
+  if (force_bn == 770) {
+    if (p.N % 128 != 0) return false;
+    if (!launch_prefill4sk_cfg<EPI, NORM, NTB, 128, true>(p, force_sk, max_counters, slab_bytes, st))
+      launch_prefill4_cfg<EPI, NORM, NTB, 128>(p, 1, st);
     return true;
   }
   if (force_bn == 768) {  // v4 on a 256 x 128 tile (sweeps / tests)
@@ -779,14 +1065,15 @@ bool launch_gemm_prefill(const GemmArgs& g, hipStream_t st) {
   p.out = g.out; p.ldo = g.ldo;
   p.splitk = 1;
   p.slabs = g.slabs;
+  p.counters = g.counters; p.fault = g.fault;
   p.positions = g.positions; p.slots = g.slots; p.cos_sin = g.cos_sin;
   p.k_cache = g.k_cache; p.v_cache = g.v_cache; p.hq = g.hq; p.hkv = g.hkv; p.bs = g.bs;
   p.dbg_ts = g.dbg_ts;
   const int fb = g.ntb;      // reused as the forced tile width (0 = heuristic, 64 / 128)
   const int fs = g.splitk;   // forced K slices (0 = heuristic)
 #define VG_PF(E)                                                                                         \
-  return norm == 2 ? launch_prefill_epi<E, 2>(p, fb, fs, g.slab_bytes, st)                               \
-                   : launch_prefill_epi<E, 0>(p, fb, fs, g.slab_bytes, st)
+  return norm == 2 ? launch_prefill_epi<E, 2>(p, fb, fs, g.slab_bytes, g.max_counters, st)               \
+                   : launch_prefill_epi<E, 0>(p, fb, fs, g.slab_bytes, g.max_counters, st)
   switch (g.epi) {
     case EPI_SILU: VG_PF(EPI_SILU);
     case EPI_QKV: VG_PF(EPI_QKV);
