@@ -26,6 +26,16 @@
 
 namespace vgate {
 
+// x^2 of 8 bf16 (one B fragment) into acc: 4 packed dot products (v_dot2_f32_bf16), no unpack — the
+// folded RMSNorm's row sums ride along the MFMA loop at a quarter of the unpack + FMA VALU cost
+typedef __bf16 p4_bf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float sumsq8(uint4 v, float acc) {
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(p4_bf2, v.x), __builtin_bit_cast(p4_bf2, v.x), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(p4_bf2, v.y), __builtin_bit_cast(p4_bf2, v.y), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(p4_bf2, v.z), __builtin_bit_cast(p4_bf2, v.z), acc, false);
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(p4_bf2, v.w), __builtin_bit_cast(p4_bf2, v.w), acc, false);
+}
+
 template <int BM, int BN, int EPI, int NORM, int NTB>
 __global__ __launch_bounds__(256, 2) void gemm_prefill_kernel(GemmParams p) {
   static_assert(BM % 32 == 0 && BN % 32 == 0, "2 x 2 waves of 16-multiple tiles");
@@ -109,10 +119,7 @@ __global__ __launch_bounds__(256, 2) void gemm_prefill_kernel(GemmParams p) {
       if constexpr (NORM == 2) {
 #pragma unroll
         for (int b = 0; b < MT; ++b) {
-          float f[8];
-          unpack8(xb[b], f);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) ss[b] += f[j] * f[j];
+          ss[b] = sumsq8(xb[b], ss[b]);
         }
       }
 #pragma unroll
@@ -276,10 +283,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_prefill2_kernel(GemmPara
       if constexpr (NORM == 2) {
 #pragma unroll
         for (int b = 0; b < MT; ++b) {
-          float f[8];
-          unpack8(xb[b], f);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) ss[b] += f[j] * f[j];
+          ss[b] = sumsq8(xb[b], ss[b]);
         }
       }
       if constexpr (SCHED == 2)
@@ -350,14 +354,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_prefill2_kernel(GemmPara
 // Group sizes per wave: 4 / 2 / 2 pieces -> the waits of phases 0 / 1 / 2: vmcnt(4) / (6) / (6).
 // BN = 128: the same schedule on a 256 x 128 tile (wave 64 n x 64 m, 8 MFMAs per phase, 96 KiB;
 // groups 3 / 2 / 1 pieces per wave -> vmcnt(3) / (4) / (5)).
-typedef __bf16 p4_bf2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ float sumsq8(uint4 v, float acc) {
-  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(p4_bf2, v.x), __builtin_bit_cast(p4_bf2, v.x), acc, false);
-  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(p4_bf2, v.y), __builtin_bit_cast(p4_bf2, v.y), acc, false);
-  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(p4_bf2, v.z), __builtin_bit_cast(p4_bf2, v.z), acc, false);
-  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(p4_bf2, v.w), __builtin_bit_cast(p4_bf2, v.w), acc, false);
-}
-
 template <int BN>
 struct P4 {  // geometry of the 4-phase 256 x BN kernel
   static constexpr int BM = 256, KS = 2;
