@@ -502,7 +502,7 @@ __device__ __forceinline__ void p4_kloop(const GemmParams& p, char* smem, int wi
 // the epilogue of a finished 256 x BN block tile straight from the accumulators (deferred row scale)
 // (NORM == 2: the row sums of squares are in wave row 0's ss; wave row 1 gets them through the 1 KiB
 // LDS area P4_ROWSS past the ring — block-uniform call, one barrier)
-constexpr int P4_ROWSS = 16;  // byte offset past the 2-stage ring (the queue item word sits at +0)
+constexpr int P4_ROWSS = 16;  // byte offset past the 2-stage ring
 template <int BN, int EPI, int NORM, int NTB>
 __device__ __forceinline__ void p4_finish(const GemmParams& p, char* smem, int wid, int lane, int m0, int nt_blk,
                                           f32x4 (&acc)[BN / 32][4], const float (&ss)[4]) {
@@ -622,14 +622,8 @@ __device__ __forceinline__ f32x4 p4sk_ld(const float* slot, int tid, int j) {
   return __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(slot), (uint32_t)tid * 16, j * 8192, 16 /* sc1 */);
 }
 
-// DYN: the work items are taken from per-XCD queues instead of a fixed list per block: an XCD's
-// items are the same as in the static form (its tile panels, then its tail units, the K slices
-// c > 0 ahead of the owners so an owner only ever waits for items already taken), and whichever
-// of its CUs frees up first takes the next one, as the hardware's dispatch of a tile grid does.
-// Queue heads at counters[qbase .. qbase + 7], a block count at qbase + 8: the last block out
-// resets all nine.
-template <int BN, int EPI, int NORM, int NTB, bool DYN>
-__global__ __launch_bounds__(512, 1) void gemm_prefill4sk_kernel(GemmParams p0, int tiles, int S, int qbase) {
+template <int BN, int EPI, int NORM, int NTB>
+__global__ __launch_bounds__(512, 1) void gemm_prefill4sk_kernel(GemmParams p0, int tiles, int S) {
   using G = P4<BN>;
   constexpr int BM = G::BM, WTN = G::WTN, NWN = G::NWN, NACC = NWN * 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -641,27 +635,10 @@ __global__ __launch_bounds__(512, 1) void gemm_prefill4sk_kernel(GemmParams p0, 
   const int gx0 = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q, nx = q + (xcd < r ? 1 : 0);
   const int g = gx0 + (orig >> 3);
   const int full = tiles / nwg, R = tiles - full * nwg;
-  // this XCD's tail units g' in [gx0, gx0 + nx) with g' < R * S: K slices c > 0 (g' >= R) first
-  const int t1 = min(gx0 + nx, R * S), ncon = max(0, t1 - max(gx0, R)), ntail = max(0, t1 - gx0);
-  const int nseg = DYN ? full * nx + ntail : full + (g < R * S ? 1 : 0);
-  uint32_t* qhead = p0.counters + qbase + xcd;
-  int* lds_item = reinterpret_cast<int*>(smem + 2 * G::STAGE);
-  int nxt = 0;
-  if (DYN && threadIdx.x == 0) nxt = (int)__hip_atomic_fetch_add(qhead, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int nseg = full + (g < R * S ? 1 : 0);
   const auto kp0 = (const GemmParams __attribute__((address_space(4)))*)(__builtin_amdgcn_kernarg_segment_ptr());
-  for (int i = 0;; ++i) {  // block-uniform
-    int item = i;
-    if constexpr (DYN) {
-      if (threadIdx.x == 0) *lds_item = nxt;
-      __syncthreads();  // also: the previous item's LDS reads + DMAs are done
-      item = __builtin_amdgcn_readfirstlane(*lds_item);
-      if (item >= nseg) break;
-      if (threadIdx.x == 0)  // the next grab's latency hides under this item
-        nxt = (int)__hip_atomic_fetch_add(qhead, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      if (i >= nseg) break;
-      if (i > 0) __builtin_amdgcn_s_barrier();  // the previous tile's LDS reads + DMAs are done
-    }
+  for (int i = 0; i < nseg; ++i) {  // block-uniform
+    if (i > 0) __builtin_amdgcn_s_barrier();  // the previous tile's LDS reads + DMAs are done
     // the parameters re-read from the kernel-argument segment per tile: hoisted out of this loop,
     // the epilogue's pointers would sit in SGPRs across the K loop (SGPR spills into VGPR lanes);
     // thread ids laundered likewise (no lane-derived epilogue / slot address stays live across it)
@@ -672,22 +649,10 @@ __global__ __launch_bounds__(512, 1) void gemm_prefill4sk_kernel(GemmParams p0, 
     asm volatile("" : "+v"(tid));
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    int tile, k0 = 0, k1 = KT, c = -1, j = 0;
-    bool tail;
-    int gu;  // the tail unit
-    if constexpr (DYN) {
-      tail = item >= full * nx;
-      tile = (item / max(nx, 1)) * nwg + gx0 + item % max(nx, 1);
-      const int e = item - full * nx;
-      gu = e < ncon ? max(gx0, R) + e : gx0 + (e - ncon);
-    } else {
-      tail = item == full;
-      tile = item * nwg + g;
-      gu = g;
-    }
-    if (tail) {  // slice c of tail tile j
-      j = gu % R;
-      c = gu / R;
+    int tile = i * nwg + g, k0 = 0, k1 = KT, c = -1, j = 0;
+    if (i == full) {  // the tail: slice c of tail tile j
+      j = g % R;
+      c = g / R;
       tile = full * nwg + j;
       k0 = (KT * c) / S;
       k1 = (KT * (c + 1)) / S;
@@ -702,7 +667,7 @@ __global__ __launch_bounds__(512, 1) void gemm_prefill4sk_kernel(GemmParams p0, 
     if (c > 0) {  // a later K slice of a tail tile: publish, count in (its own copy of the K loop: with
                   // one copy shared by this path and the owner's the allocator spills the accumulators)
       p4_kloop<BN, NORM>(p, smem, wid, lane, m0, nt_blk, k0, k1 - k0, acc, ss);
-      float* slot = p.slabs + (size_t)gu * p4sk_slot_floats<BN>();
+      float* slot = p.slabs + (size_t)g * p4sk_slot_floats<BN>();
 #pragma unroll
       for (int e = 0; e < NACC; ++e) p4sk_st(slot, tid, e, acc[e >> 2][e & 3]);
       if constexpr (NORM == 2) p4sk_st(slot, tid, NACC, f32x4{ss[0], ss[1], ss[2], ss[3]});
@@ -744,12 +709,6 @@ __global__ __launch_bounds__(512, 1) void gemm_prefill4sk_kernel(GemmParams p0, 
       if (tid == 0) __hip_atomic_store(p.counters + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     p4_finish<BN, EPI, NORM, NTB>(p, smem, wid, lane, m0, nt_blk, acc, ss);
-  }
-  if (DYN && threadIdx.x == 0) {  // every grab of this block is done: the last block out resets the queues
-    uint32_t* done = p0.counters + qbase + 8;
-    if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(nwg - 1)) {
-      for (int x = 0; x < 9; ++x) __hip_atomic_store(p0.counters + qbase + x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
 }
 
@@ -882,7 +841,7 @@ static int cu_count() {
 // persistent 4-phase kernel (whole rounds + the K-split tail), one block per CU; slices = the tail's K
 // slices (0: G / R, at least 4 K-tiles each, at most 8). false = not taken (no tail to split, no
 // tickets / slot room)
-template <int EPI, int NORM, int NTB, int BN, bool DYN = false>
+template <int EPI, int NORM, int NTB, int BN>
 static bool launch_prefill4sk_cfg(const GemmParams& p, int slices, int max_counters, size_t slab_bytes,
                                   hipStream_t st) {
   constexpr int STAGE = (BN / 16 + 16) * 2 * 1024;
@@ -895,18 +854,17 @@ static bool launch_prefill4sk_cfg(const GemmParams& p, int slices, int max_count
   S = S > G / R ? G / R : S;
   S = S > 8 && slices <= 0 ? 8 : S;
   while (S > 1 && KT / S < 4) --S;
-  const int qbase = max_counters - 9;  // DYN: the queue heads + block count, above the tail tickets
-  if (S < 1 || R > qbase || (size_t)G * p4sk_slot_floats<BN>() * 4 > slab_bytes) return false;
+  if (S < 1 || R > max_counters || (size_t)G * p4sk_slot_floats<BN>() * 4 > slab_bytes) return false;
   GemmParams q = p;
   if (q.dbg_ts == nullptr) q.dbg_ts = tl_take("gemm_prefill4sk", G);
-  auto kern = gemm_prefill4sk_kernel<BN, EPI, NORM, NTB, DYN>;
-  constexpr int LDS = 2 * STAGE + P4_ROWSS + 1024;  // ring + the queue item word + the row sums
+  auto kern = gemm_prefill4sk_kernel<BN, EPI, NORM, NTB>;
+  constexpr int LDS = 2 * STAGE + P4_ROWSS + 1024;  // ring + the folded norm's row sums
   static bool attr = [&] {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                LDS) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL(kern, dim3(G), dim3(512), LDS, st, q, tiles, S, qbase);
+  hipLaunchKernelGGL(kern, dim3(G), dim3(512), LDS, st, q, tiles, S);
   return true;
 }
 
@@ -996,18 +954,6 @@ static bool launch_prefill_epi(const GemmParams& p, int force_bn, int force_sk, 
   if (force_bn == 769) {
     if (p.N % 128 != 0) return false;
     if (!launch_prefill4sk_cfg<EPI, NORM, NTB, 128>(p, force_sk, max_counters, slab_bytes, st))
-      launch_prefill4_cfg<EPI, NORM, NTB, 128>(p, 1, st);
-    return true;
-  }
-  if (force_bn == 1026) {  // the same, items from per-XCD queues
-    if (p.N % 256 != 0) return false;
-    if (!launch_prefill4sk_cfg<EPI, NORM, NTB, 256, true>(p, force_sk, max_counters, slab_bytes, st))
-      launch_prefill4_cfg<EPI, NORM, NTB>(p, 1, st);
-    return true;
-  }
-  if (force_bn == 770) {
-    if (p.N % 128 != 0) return false;
-    if (!launch_prefill4sk_cfg<EPI, NORM, NTB, 128, true>(p, force_sk, max_counters, slab_bytes, st))
       launch_prefill4_cfg<EPI, NORM, NTB, 128>(p, 1, st);
     return true;
   }

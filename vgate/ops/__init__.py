@@ -662,10 +662,10 @@ def _plan_bucket(plan: dict, M: int):
 # 256 = 256 x 128 3-deep ring, 768 / 1024 = the 4-phase 256 x 128 / 256 x 256 kernels
 PREFILL_CANDIDATES = [(0, 0), (64, 0), (128, 0), (128, 2), (128, 4), (256, 0), (256, 4), (256, 6), (768, 0),
                       (768, 2), (768, 3), (768, 4), (768, 6), (1024, 0), (1024, 2), (1024, 3), (1024, 4),
-                      (1024, 6), (1025, 0), (769, 0), (1026, 0), (770, 0)]
+                      (1024, 6), (1025, 0), (769, 0)]
 # (1025 / 769: the persistent forms of the 4-phase 256 x 256 / 256 x 128 kernel — one block per CU,
-# whole rounds of tiles + the last round K-split and met in-launch; 1026 / 770: the same with the
-# items taken from per-XCD queues; gemm_prefill.hip gemm_prefill4sk_kernel)
+# whole rounds of tiles + the last round K-split and met in-launch; gemm_prefill.hip
+# gemm_prefill4sk_kernel)
 # 128-row tiles on a 4-deep ring, one block per CU (128 x 128 / 128 x 64, 4 or 8 waves): timed for
 # 64 < M <= 1024 only, where the grid of the 2-deep-ring tile is one or two partial rounds
 # + the wide-N tiles 64 x 512 / 128 x 320 (gate_up at 320 / 448 rows: 245 / 224 blocks, 35 vs 44-64 us)
