@@ -49,7 +49,8 @@ def main():
     ap.add_argument("--bn", type=int, default=0)
     ap.add_argument("--tuned", action="store_true",
                     help="report the decomposition the engine's start-up tuner (ops.tune_prefill) would pick: "
-                         "the fastest of ops.PREFILL_CANDIDATES unless within 5%% of the heuristic")
+                         "the fastest of ops.PREFILL_CANDIDATES (+ the ring candidates at 64 < M <= 1024) unless "
+                         "within 5%% of the heuristic")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     C = ops.native()
@@ -67,7 +68,8 @@ def main():
                 pick = (a.bn, 0)
                 if a.tuned:
                     t = {}
-                    for bn, sk in ops.PREFILL_CANDIDATES:
+                    extra = ops.PREFILL_RING_CANDIDATES if 64 < M <= 1024 else []  # as ops.tune_prefill
+                    for bn, sk in ops.PREFILL_CANDIDATES + extra:
                         try:
                             t[(bn, sk)] = timeit(lambda: C.gemm(x, wp, N, K, out, 0, ws=ws, path=1, ntb=bn, splitk=sk),
                                                  a.iters)
