@@ -61,7 +61,7 @@ def main():
         return 1e3 * s0.elapsed_time(s1) / a.iters
 
     cands = ops.PREFILL_CANDIDATES + ops.PREFILL_RING_CANDIDATES
-    cands += [(t, s) for t in (1025, 769) for s in (0, 1, 2, 4, 8) if (t, s) not in cands]  # persistent: tail slices
+    cands += [(t, s) for t in (1025, 769) for s in range(9) if (t, s) not in cands]  # persistent: tail slices
     only = {int(c) for c in a.only.split(",") if c}
     for name, N, K in SHAPES[a.model]:
         w = (torch.randn(N, K, device=dev) / math.sqrt(K)).bfloat16()

@@ -599,13 +599,17 @@ __global__ __launch_bounds__(512, 1) void gemm_prefill4_kernel(GemmParams p) {
 // keeps working on 4 weight panels x all m-blocks at the same K position, as the tile grid does
 // (the L2 reuse a free (tile, K-tile) stream-K split loses: its blocks sit at unrelated K offsets
 // and it measured 1.3x SLOWER than the tile grid, profiles/r6_prefill_stream_k.log) — and then
-// the R tail tiles as S K slices each (S = G / R, >= 4 K-tiles per slice): unit g = c * R + j is
-// slice c of tail tile j, so the blocks of one XCD again share panels and K positions. Slices
-// c > 0 publish their fp32 partial (+ the x sums of squares of the folded RMSNorm) to their own
-// slot with device-coherent stores and count in on the tile's ticket; slice 0 (the owner) waits
-// for the S - 1 tickets, adds the partials in slice order (bit-reproducible), runs the epilogue and
-// clears the ticket. Nothing waits on a block that waits: the owners are the only waiters, and the
-// poll is bounded all the same (give-up: bit 64 of the fault word, garbage, never a hang).
+// the R tail tiles as S K slices each: unit u = (S - 1 - c) * R + j is slice c of tail tile j, block
+// g takes units g, g + G, ... (one round when R S <= G: Llama-3-8B gate_up / down / o_proj at 2048
+// rows, S = 2; three for its qkv_proj's 192 tiles, S = 4: each CU computes 3/4 of a tile instead of a
+// whole one on 3/4 of the chip), so the blocks of one XCD again share panels and K positions.
+// Slices c > 0 publish their fp32 partial (+ the x sums of squares of the folded RMSNorm) to the
+// unit's slot with device-coherent stores and count in on the tile's ticket; slice 0 (the owner)
+// waits for the S - 1 tickets, adds the partials in slice order (bit-reproducible), runs the epilogue
+// and clears the ticket. Every block takes its units in order and all of the later slices come
+// before the owners, so a slice never waits: an owner's partials are either done or being computed
+// by a resident block that needs nothing from anyone; the poll is bounded all the same (give-up:
+// bit 64 of the fault word, garbage, never a hang).
 constexpr int P4SK_SPIN = 1 << 20;
 
 template <int BN>
@@ -635,7 +639,7 @@ __global__ __launch_bounds__(512, 1) void gemm_prefill4sk_kernel(GemmParams p0, 
   const int gx0 = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q, nx = q + (xcd < r ? 1 : 0);
   const int g = gx0 + (orig >> 3);
   const int full = tiles / nwg, R = tiles - full * nwg;
-  const int nseg = full + (g < R * S ? 1 : 0);
+  const int RS = R * S, nseg = full + (g < RS ? (RS - g + nwg - 1) / nwg : 0);
   const auto kp0 = (const GemmParams __attribute__((address_space(4)))*)(__builtin_amdgcn_kernarg_segment_ptr());
   for (int i = 0; i < nseg; ++i) {  // block-uniform
     if (i > 0) __builtin_amdgcn_s_barrier();  // the previous tile's LDS reads + DMAs are done
@@ -649,10 +653,11 @@ __global__ __launch_bounds__(512, 1) void gemm_prefill4sk_kernel(GemmParams p0, 
     asm volatile("" : "+v"(tid));
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    int tile = i * nwg + g, k0 = 0, k1 = KT, c = -1, j = 0;
-    if (i == full) {  // the tail: slice c of tail tile j
-      j = g % R;
-      c = g / R;
+    int tile = i * nwg + g, k0 = 0, k1 = KT, c = -1, j = 0, u = 0;
+    if (i >= full) {  // tail unit u: slice c of tail tile j, the later slices first (the owners last)
+      u = g + (i - full) * nwg;
+      j = u % R;
+      c = S - 1 - u / R;
       tile = full * nwg + j;
       k0 = (KT * c) / S;
       k1 = (KT * (c + 1)) / S;
@@ -667,7 +672,7 @@ __global__ __launch_bounds__(512, 1) void gemm_prefill4sk_kernel(GemmParams p0, 
     if (c > 0) {  // a later K slice of a tail tile: publish, count in (its own copy of the K loop: with
                   // one copy shared by this path and the owner's the allocator spills the accumulators)
       p4_kloop<BN, NORM>(p, smem, wid, lane, m0, nt_blk, k0, k1 - k0, acc, ss);
-      float* slot = p.slabs + (size_t)g * p4sk_slot_floats<BN>();
+      float* slot = p.slabs + (size_t)u * p4sk_slot_floats<BN>();  // u < R (S - 1): one slot per unit
 #pragma unroll
       for (int e = 0; e < NACC; ++e) p4sk_st(slot, tid, e, acc[e >> 2][e & 3]);
       if constexpr (NORM == 2) p4sk_st(slot, tid, NACC, f32x4{ss[0], ss[1], ss[2], ss[3]});
@@ -690,7 +695,7 @@ __global__ __launch_bounds__(512, 1) void gemm_prefill4sk_kernel(GemmParams p0, 
       }
       __syncthreads();
       for (int cc = 1; cc < S; ++cc) {
-        const float* slot = p.slabs + (size_t)(cc * R + j) * p4sk_slot_floats<BN>();
+        const float* slot = p.slabs + (size_t)((S - 1 - cc) * R + j) * p4sk_slot_floats<BN>();
         // a quarter of the accumulators per round trip (the loads' registers: 32 / 16 per lane)
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
@@ -850,11 +855,13 @@ static bool launch_prefill4sk_cfg(const GemmParams& p, int slices, int max_count
   if (G <= 0 || p.counters == nullptr || p.slabs == nullptr) return false;
   const int R = tiles % G, KT = p.K / 64;
   if (R == 0) return false;  // whole rounds: the tile grid is the same schedule
-  int S = slices > 0 ? slices : G / R;
-  S = S > G / R ? G / R : S;
-  S = S > 8 && slices <= 0 ? 8 : S;
+  // S (0: the launcher's choice): the tail in ONE round, S = G / R slices (<= 8). More slices than fit
+  // one round (forced, or a tuner candidate) run in several: measured slower at every shape tried but
+  // Llama-3-8B qkv_proj (192 tiles x 8 slices: 115 vs 123 us, where the split-K 6 grid + reduce is 108),
+  // every contributor pays the drain of its 270 KB partial (r6_prefill_persistent_tail.log)
+  int S = slices > 0 ? slices : (G / R > 8 ? 8 : G / R);
   while (S > 1 && KT / S < 4) --S;
-  if (S < 1 || R > max_counters || (size_t)G * p4sk_slot_floats<BN>() * 4 > slab_bytes) return false;
+  if (S < 1 || R > max_counters || (size_t)R * (S - 1) * p4sk_slot_floats<BN>() * 4 > slab_bytes) return false;
   GemmParams q = p;
   if (q.dbg_ts == nullptr) q.dbg_ts = tl_take("gemm_prefill4sk", G);
   auto kern = gemm_prefill4sk_kernel<BN, EPI, NORM, NTB>;

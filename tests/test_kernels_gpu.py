@@ -1221,13 +1221,15 @@ def test_prefill_wide_tiles(M, bn, sk):
     assert _rel_err(h, ref.silu_mul_linear_ref(xn, wg, wu)) < 2e-2
 
 
-@pytest.mark.parametrize("M,N,K", [(448, 2560, 1536), (1024, 7168, 1024), (2048, 3584, 2048), (640, 5120, 4096),
-                                   (2048, 9216, 1024)])
+@pytest.mark.parametrize("M,N,K,slices", [(448, 2560, 1536, 0), (1024, 7168, 1024, 0), (2048, 3584, 2048, 0),
+                                          (640, 5120, 4096, 0), (2048, 9216, 1024, 0), (2048, 6144, 4096, 0),
+                                          (640, 5120, 4096, 7), (448, 2560, 1536, 3)])
 @pytest.mark.parametrize("bn", [1025, 769])
-def test_prefill_persistent_k_split_tail(M, N, K, bn):
+def test_prefill_persistent_k_split_tail(M, N, K, slices, bn):
     """The persistent 4-phase prefill kernel (gemm_prefill4sk_kernel): whole rounds of tiles, then the
     last round's tiles as 2-6 K slices met in-launch (the owner adds the published partials in
-    slice order), or unsplit where the tail already fills the chip. Against the fp32 references
+    slice order), or unsplit where the tail already fills the chip; tails of several rounds (Llama-3-8B
+    qkv_proj at 2048 rows: 192 tiles x 4 slices; forced 7 slices of 60 tiles). Against the fp32 references
     (plain + residual, folded-norm SiLU*mul with the partial sums of squares), bit-identical on a
     repeat (fixed add order, tickets reset by the owner), and the fault word clear (no ticket poll
     gave up)."""
@@ -1241,7 +1243,8 @@ def test_prefill_persistent_k_split_tail(M, N, K, bn):
     outs = []
     for _ in range(2):
         out = res.clone()
-        ops.native().gemm(x, lin.wp, N, K, out, 0, res=out, ws=ops.workspace(DEV), path=1, ntb=bn, fault=fw)
+        ops.native().gemm(x, lin.wp, N, K, out, 0, res=out, ws=ops.workspace(DEV), path=1, ntb=bn, splitk=slices,
+                          fault=fw)
         outs.append(out)
     assert _rel_err(outs[0], ref.linear_ref(x, w, None, res)) < 1e-2
     assert torch.equal(outs[0], outs[1])
@@ -1254,7 +1257,7 @@ def test_prefill_persistent_k_split_tail(M, N, K, bn):
     for _ in range(2):
         h = torch.empty(M, N // 2, dtype=torch.bfloat16, device=DEV)
         ops.native().gemm(x, gu.wp, N, K, h, 2, ws=ops.workspace(DEV), rownorm=True, eps=1e-6, path=1, ntb=bn,
-                          fault=fw)
+                          splitk=slices, fault=fw)
         hs.append(h)
     xn, _ = ref.rmsnorm_ref(x, nw, 1e-6)
     assert _rel_err(hs[0], ref.silu_mul_linear_ref(xn, wg, wu)) < 2e-2
