@@ -1,10 +1,15 @@
-# ad-hoc GPU batch (the current experiment); see run.sh for the standing tasks
+# ad-hoc GPU batch: same-box A/B of the long-chunk tuner margin (A = 0.05 as before, B = 0.02)
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -m gpu \
-  -k "prefill or persistent_k_split" > gpurun_out/sk9_tests.log 2>&1 || { tail -30 gpurun_out/sk9_tests.log; exit 1; }
-tail -1 gpurun_out/sk9_tests.log
-timeout -k 10 400 python -u benchmarks/ttft_probe.py --model meta-llama/Meta-Llama-3-8B-Instruct --lens 512 2048 4096 > gpurun_out/sk9_ttft.log 2>&1 || { tail -30 gpurun_out/sk9_ttft.log; exit 1; }
-grep '^{' gpurun_out/sk9_ttft.log | tail -3
-timeout -k 10 400 python -u benchmarks/ttft_probe.py --lens 512 2048 4096 > gpurun_out/sk9_ttft_qwen.log 2>&1 || { tail -30 gpurun_out/sk9_ttft_qwen.log; exit 1; }
-grep '^{' gpurun_out/sk9_ttft_qwen.log | tail -3
+for i in 1 2; do
+for arm in 0.05 0.02; do
+timeout -k 10 400 python -u -c "
+import runpy, sys
+import vgate.ops as o
+o.LONG_MARGIN = $arm
+sys.argv = ['ttft_probe.py', '--model', 'meta-llama/Meta-Llama-3-8B-Instruct', '--lens', '2048']
+runpy.run_path('benchmarks/ttft_probe.py', run_name='__main__')
+" > gpurun_out/sk11_ttft_${arm}_$i.log 2>&1 || { tail -30 gpurun_out/sk11_ttft_${arm}_$i.log; exit 1; }
+echo "margin $arm run $i: $(grep '^{' gpurun_out/sk11_ttft_${arm}_$i.log | tail -1)"
+done
+done
