@@ -408,3 +408,54 @@ def test_tp2_runtime_consistency_guard(tmp_path):
     out, err, healthy, state, checks, car_on = bad
     assert out is None and err.startswith("TPDivergence") and not healthy and not car_on, bad
     assert "residual" in state and checks == 1, state
+
+
+_RCCL_GRAPH_SCRIPT = r"""
+import torch, torch.distributed as dist
+from vgate.parallel.comm import TPGroup
+dist.init_process_group("nccl")
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+tp = TPGroup(rank=0, size=1, group=dist.group.WORLD, backend="nccl")
+x = (torch.arange(4 << 20, device=dev, dtype=torch.float32) % 977).bfloat16()  # 8 MiB: the RCCL size class
+ref = x.clone()
+out = torch.empty((1,) + tuple(x.shape), dtype=x.dtype, device=dev)
+m = torch.tensor([7, 3], dtype=torch.int64, device=dev)
+s = torch.cuda.Stream()
+s.wait_stream(torch.cuda.current_stream())
+with torch.cuda.stream(s):  # RCCL's first calls (communicator set-up) outside the capture
+    dist.all_reduce(x)
+    dist.all_gather_into_tensor(out, x)
+    dist.all_reduce(m, op=dist.ReduceOp.MIN)
+torch.cuda.current_stream().wait_stream(s)
+torch.cuda.synchronize()
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g):
+    dist.all_reduce(x)
+    dist.all_gather_into_tensor(out, x)
+    dist.all_reduce(m, op=dist.ReduceOp.MIN)
+for _ in range(3):
+    g.replay()
+torch.cuda.synchronize()
+assert torch.equal(x, ref) and torch.equal(out[0], ref) and m.tolist() == [7, 3]
+w = tp.exchange_words(torch.tensor([11, 22], dtype=torch.int64, device=dev))
+assert w.tolist() == [[11, 22]]
+dist.destroy_process_group()
+print("rccl-graph-ok")
+"""
+
+
+def test_rccl_collectives_inside_a_captured_graph_single_rank(tmp_path):
+    """RCCL (the `nccl` backend) on this stack, one rank on the box's one GPU: an 8 MiB bf16
+    all-reduce (the size class the TP path hands to RCCL above the IPC kernels), the logits-style
+    all-gather and the int64 MIN-reduce the engine's KV sizing uses, captured in a hipGraph and
+    replayed, plus the consistency guard's word exchange. One rank only (RCCL refuses two on one
+    device): this executes the RCCL calls and their graph capture, not a cross-device transfer."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "-c", _RCCL_GRAPH_SCRIPT], env=env, capture_output=True, text=True,
+                       timeout=180, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0 and "rccl-graph-ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
