@@ -600,9 +600,9 @@ __global__ __launch_bounds__(512, 1) void gemm_prefill4_kernel(GemmParams p) {
 // (the L2 reuse a free (tile, K-tile) stream-K split loses: its blocks sit at unrelated K offsets
 // and it measured 1.3x SLOWER than the tile grid, profiles/r6_prefill_stream_k.log) — and then
 // the R tail tiles as S K slices each: unit u = (S - 1 - c) * R + j is slice c of tail tile j, block
-// g takes units g, g + G, ... (one round when R S <= G: Llama-3-8B gate_up / down / o_proj at 2048
-// rows, S = 2; three for its qkv_proj's 192 tiles, S = 4: each CU computes 3/4 of a tile instead of a
-// whole one on 3/4 of the chip), so the blocks of one XCD again share panels and K positions.
+// g takes units g, g + G, ... (the launcher's S keeps R S <= G, one round: Llama-3-8B gate_up / down /
+// o_proj at 2048 rows, S = 2; a forced larger S runs several rounds), so the blocks of one XCD
+// again share panels and K positions.
 // Slices c > 0 publish their fp32 partial (+ the x sums of squares of the folded RMSNorm) to the
 // unit's slot with device-coherent stores and count in on the tile's ticket; slice 0 (the owner)
 // waits for the S - 1 tickets, adds the partials in slice order (bit-reproducible), runs the epilogue
@@ -636,8 +636,7 @@ __global__ __launch_bounds__(512, 1) void gemm_prefill4sk_kernel(GemmParams p0, 
   const int mblocks = (p0.M + BM - 1) / BM;
   const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
   // XCD-aware: consecutive g (tiles of one weight column panel, m-blocks fastest) on one XCD
-  const int gx0 = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q, nx = q + (xcd < r ? 1 : 0);
-  const int g = gx0 + (orig >> 3);
+  const int g = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
   const int full = tiles / nwg, R = tiles - full * nwg;
   const int RS = R * S, nseg = full + (g < RS ? (RS - g + nwg - 1) / nwg : 0);
   const auto kp0 = (const GemmParams __attribute__((address_space(4)))*)(__builtin_amdgcn_kernarg_segment_ptr());
