@@ -721,7 +721,7 @@ MEDIUM_DEFAULT = (-1, -1)  # medium-M plan entry: keep the default (decode / til
 
 # bump whenever the MEANING of a stored plan changes on the Python side (the _plan_kw encoding of a
 # (tile, K slices) code, MID_BASE, the tuner margin): a cached plan set is keyed on this too
-PLAN_FORMAT = 2
+PLAN_FORMAT = 3  # 3: candidates timed with the layer's folded-norm row scale
 TUNE_MARGIN = 0.05
 LONG_M, LONG_MARGIN = 1024, 0.02  # the margin for M >= LONG_M buckets
 
@@ -763,6 +763,11 @@ def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = TUNE
         # shape (_linear_awq_dequant): time a random bf16 matrix in that layout
         wp = lin.wp if lin.kind == "dense" else pack_weight(
             (torch.rand(lin.N, lin.K, device=dev, generator=g) * 2 - 1).bfloat16())
+        # the folded RMSNorm's row scale as in the step (qkv / gate_up: the x^2 sums ride in the K loop
+        # and cost some kernels up to ~30 % more than others — 128 x 320 tiles with four wave columns:
+        # Qwen2.5-1.5B qkv at 448 rows 17.7 -> 22.9 us, profiles/r6_tuner_norm_timing.log)
+        nkw = dict(rownorm=True, eps=1e-6) if (lin.norm_gamma is not None
+                                                or getattr(lin, "layout", "plain") in ("qkv", "silu")) else {}
         for M in ms:
             x = torch.rand(M, lin.K, device=dev, generator=g).bfloat16()
             out = torch.empty(M, lin.N, dtype=torch.bfloat16, device=dev)
@@ -773,7 +778,7 @@ def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = TUNE
             extra = MID_CANDIDATES if 16 < M <= 64 else PREFILL_RING_CANDIDATES if 64 < M <= 1024 else []
             for bn, sk in PREFILL_CANDIDATES + extra:
                 def run():
-                    C.gemm(x, wp, lin.N, lin.K, out, 0, ws=ws, **_plan_kw((bn, sk), M))
+                    C.gemm(x, wp, lin.N, lin.K, out, 0, ws=ws, **_plan_kw((bn, sk), M), **nkw)
                 try:
                     run()
                 except RuntimeError:
@@ -794,7 +799,7 @@ def tune_prefill(lins: list, ms: list[int], iters: int = 5, margin: float = TUNE
             if M < 128:
                 # medium bucket: against the default path (M > 16 rows -> decode / tile kernels)
                 def run_default():
-                    C.gemm(x, wp, lin.N, lin.K, out, 0, ws=ws)
+                    C.gemm(x, wp, lin.N, lin.K, out, 0, ws=ws, **nkw)
                 run_default()
                 t_def = cold(run_default, iters)
                 plan[M] = best if times[best] < (1.0 - margin) * t_def else MEDIUM_DEFAULT
