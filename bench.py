@@ -224,6 +224,8 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
         prof = cProfile.Profile()
         prof.enable()
     snap0 = eng.backend.stats() if hasattr(eng.backend, "stats") else {}
+    rcache = getattr(getattr(app.state.vgate, "batcher", None), "cache", None)
+    rc0 = rcache.hits if rcache is not None else None
     t0 = time.perf_counter()
     mon = asyncio.create_task(lag_monitor(t0))
     lat, fails, tokens, _, starts = await load(per_step * args.steps, 0)
@@ -238,9 +240,11 @@ async def serve_and_bench(args, rank: int, world: int, dist_ok: bool, client=Non
     snap = eng.backend.stats() if hasattr(eng.backend, "stats") else {}
     # timed-region forensics (p99): eager (graph-miss) steps and captures INSIDE the timed region
     snap = dict(snap)
+    if rc0 is not None:  # gateway result-cache hits in the timed region (unique prompts: 0)
+        snap["timed_result_cache_hits"] = rcache.hits - rc0
     for k in ("graph_misses_eager", "graph_captures", "steps", "graph_hits", "idle_ms", "prefill_steps", "waves",
               "wave_requests", "coalesce_ms", "busy_ms", "collect_wait_ms", "sum_step_ms", "sum_cycle_ms",
-              "sum_gpu_ms", "gpu_steps"):
+              "sum_gpu_ms", "gpu_steps", "prefix_cache_hits"):
         if k in snap and k in snap0:
             snap[f"timed_{k}"] = snap[k] - snap0[k]
     # per-step averages over the timed region only (the snapshot's avg_* are since boot, warm-up
@@ -452,6 +456,10 @@ def main():
                                                   ("timed_idle_ms", "timed_coalesce_ms", "timed_busy_ms")), 3)
                                         if "timed_busy_ms" in allr[0]["engine"] else None),
             "timed_prefill_steps": allr[0]["engine"].get("timed_prefill_steps"),
+            # reuse in the timed region: KV blocks served by the prefix cache (the chat template's
+            # shared head; every prompt is unique) and gateway result-cache hits (must be 0)
+            "timed_prefix_cache_hit_blocks": allr[0]["engine"].get("timed_prefix_cache_hits"),
+            "timed_result_cache_hits": allr[0]["engine"].get("timed_result_cache_hits"),
             # per idle -> busy transition: [idle start -> first arrival, first -> last arrival of the
             # wave, last arrival -> step start] in ms, and the requests per transition
             "wave_breakdown_ms": ((allr[0].get("wave_trace_ms") or {}).get("wave_breakdown_median_ms")
